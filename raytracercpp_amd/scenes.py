@@ -1,0 +1,315 @@
+"""Deterministic workload scenes for BASELINE.json's configs.
+
+* C1 ``sphere256``  : analytic Sphere(Point(0,0,-3), 1) + Renderer::DEFAULT_MATERIAL, 256x256
+* C2 ``cube1080``   : tp2/data/cube.obj (12 tris), T(0,0,-5)*Ry30*Rx20, 1920x1080
+* ``robot1080``     : tp2/data/Robot/robot.obj (3,238 tris), T(0,0,-4)*Ry30*Rx20
+* C3 ``bumpy70k``   : bumpy UV sphere nu=264 nv=133 (70,224 tris), T(0,0,-3)*Ry30*Rx20*S1.2
+* C4 ``sphere1m``   : UV sphere nu=1000 nv=500 (1,000,000 tris, texcoords), T(0,0,-3)*Ry30*Rx20*S1.5,
+                      1920x1080 with 2x2 SSAA (ssaa_factor 2)
+* C5 ``sphere1m_refl``: C4 + reflection 0.5 / roughness 0.3 / 16 samples + normal & parallax maps
+
+All camera placements follow the survey probe: camera at the origin, fov 80,
+light (3,3,2), shadows on, BVH depth 12 / leaf 40.
+
+Geometry is generated in float64 with a polynomial sin/cos built from IEEE
++,-,*,/ only (no libm), then rounded to float32 and transformed with the
+reference's own Point-transform operation order (mat.cpp:83-100) in float32,
+so the triangle arrays are bit-identical on every host.  Matrices come from a
+``transforms`` provider: the product library (default) or, when generating
+golden fixtures, the reference harness.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import numpy as np
+
+from .scene import (RenderSettings, SceneData, empty_shapes, material, SHAPE_SPHERE, TEX_NORMAL,
+                    TEX_DISPLACEMENT)
+
+_PIO2_HI = 1.5707963267948966
+_PIO2_LO = 6.123233995736766e-17
+
+
+def det_sincos(x):
+    """sin/cos in float64 from +,-,*,/ only (bit-reproducible across hosts)."""
+    x = np.asarray(x, dtype=np.float64)
+    k = np.rint(x / _PIO2_HI)
+    r = (x - k * _PIO2_HI) - k * _PIO2_LO
+    r2 = r * r
+    s = r2 * (1.0 / 1307674368000.0 * -1.0 + r2 * (1.0 / 355687428096000.0))
+    s = r2 * (1.0 / 6227020800.0 + s)
+    s = r2 * (-1.0 / 39916800.0 + s)
+    s = r2 * (1.0 / 362880.0 + s)
+    s = r2 * (-1.0 / 5040.0 + s)
+    s = r2 * (1.0 / 120.0 + s)
+    s = r2 * (-1.0 / 6.0 + s)
+    s = r + r * s
+    c = r2 * (-1.0 / 87178291200.0 + r2 * (1.0 / 20922789888000.0))
+    c = r2 * (1.0 / 479001600.0 + c)
+    c = r2 * (-1.0 / 3628800.0 + c)
+    c = r2 * (1.0 / 40320.0 + c)
+    c = r2 * (-1.0 / 720.0 + c)
+    c = r2 * (1.0 / 24.0 + c)
+    c = r2 * (-0.5 + c)
+    c = 1.0 + c
+    q = np.mod(k, 4).astype(np.int64)
+    sin = np.where(q == 0, s, np.where(q == 1, c, np.where(q == 2, -s, -c)))
+    cos = np.where(q == 0, c, np.where(q == 1, -s, np.where(q == 2, -c, s)))
+    return sin, cos
+
+
+def transform_points_f32(m, pts):
+    """Transform::operator()(Point) (mat.cpp:83-100) in float32, reference operation order."""
+    m = np.asarray(m, np.float32).reshape(4, 4)
+    p = np.asarray(pts, np.float32).reshape(-1, 3)
+    x, y, z = p[:, 0], p[:, 1], p[:, 2]
+
+    def row(i):
+        return ((m[i, 0] * x + m[i, 1] * y) + m[i, 2] * z) + m[i, 3]
+
+    xt, yt, zt, wt = row(0), row(1), row(2), row(3)
+    one = np.float32(1.0)
+    w = one / wt
+    keep = wt == one
+    out = np.stack([np.where(keep, xt, xt * w), np.where(keep, yt, yt * w), np.where(keep, zt, zt * w)], axis=1)
+    return out.astype(np.float32)
+
+
+def uv_sphere_triangles(nu, nv, bump=0.0, bump_theta=7, bump_phi=5, texcoords=True):
+    """Object-space UV sphere: quad (i,j) -> tris (a,b,c), (a,c,d); a=(i,j) b=(i+1,j) c=(i+1,j+1) d=(i,j+1),
+    outward-facing under Triangle's backface culling (triangle.cpp:44-46).
+
+    theta = pi*j/nv (pole to pole), phi = 2*pi*i/nu.  Returns (tri9 float32, uv6 float32 or None).
+    """
+    i = np.arange(nu + 1, dtype=np.float64)
+    j = np.arange(nv + 1, dtype=np.float64)
+    theta = np.pi * j / nv
+    phi = 2.0 * np.pi * (np.arange(nu + 1) % nu) / nu
+    st, ct = det_sincos(theta)
+    sp, cp = det_sincos(phi)
+    TH, PH = np.meshgrid(np.arange(nv + 1), np.arange(nu + 1))   # [i][j]
+    r = np.ones((nu + 1, nv + 1), np.float64)
+    if bump != 0.0:
+        s7, _ = det_sincos(bump_theta * theta)
+        _, c5 = det_sincos(bump_phi * phi)
+        r = 1.0 + bump * s7[TH] * c5[PH]
+    px = r * st[TH] * cp[PH]
+    py = r * ct[TH]
+    pz = r * st[TH] * sp[PH]
+    P = np.stack([px, py, pz], axis=-1).astype(np.float32)      # (nu+1, nv+1, 3)
+    ii, jj = np.meshgrid(np.arange(nu), np.arange(nv), indexing="ij")
+    ii = ii.ravel()
+    jj = jj.ravel()
+    a = P[ii, jj]
+    b = P[ii + 1, jj]
+    c = P[ii + 1, jj + 1]
+    d = P[ii, jj + 1]
+    t1 = np.concatenate([a, b, c], axis=1)
+    t2 = np.concatenate([a, c, d], axis=1)
+    tri = np.stack([t1, t2], axis=1).reshape(-1, 9)
+    uv = None
+    if texcoords:
+        U = (i / nu).astype(np.float32)
+        Vv = (j / nv).astype(np.float32)
+        ua, va = U[ii], Vv[jj]
+        ub, vb = U[ii + 1], Vv[jj]
+        uc, vc = U[ii + 1], Vv[jj + 1]
+        ud, vd = U[ii], Vv[jj + 1]
+        uv1 = np.stack([ua, ub, uc, va, vb, vc], axis=1)
+        uv2 = np.stack([ua, uc, ud, va, vc, vd], axis=1)
+        uv = np.stack([uv1, uv2], axis=1).reshape(-1, 6).astype(np.float32)
+    return np.ascontiguousarray(tri, np.float32), uv
+
+
+def transform_triangles(m, tri9):
+    pts = transform_points_f32(m, tri9.reshape(-1, 3))
+    return pts.reshape(-1, 9)
+
+
+class _ProductTransforms:
+    """Matrices from the product library (restated mat.cpp in C++)."""
+
+    def camera_matrices(self, fov, aspect, znear=0.1, zfar=1000.0):
+        from . import _lib
+        return _lib.camera_matrices(fov, aspect, znear, zfar)
+
+    def transform(self, kind, x=0.0, y=0.0, z=0.0):
+        from . import _lib
+        return _lib.make_transform(kind, x, y, z)
+
+    def compose(self, a, b):
+        from . import _lib
+        return _lib.compose(a, b)
+
+
+def default_transforms():
+    return _ProductTransforms()
+
+
+def object_transform(T, tz, scale=None, ry=30.0, rx=20.0):
+    """Translation(0,0,tz) * RotationY(ry) * RotationX(rx) [* Scale(s)] via compose_transform (mat.cpp:363-371)."""
+    m = T.compose(T.transform("translation", 0.0, 0.0, tz), T.transform("ry", ry))
+    m = T.compose(m, T.transform("rx", rx))
+    if scale is not None:
+        m = T.compose(m, T.transform("scale", scale, scale, scale))
+    return m
+
+
+def specular_threshold(spec, ns):
+    """MainWindow::precompute_materials (mainwindow.cpp:240-249), evaluated with the host libm."""
+    s = np.asarray(spec, np.float32)
+    lum = np.float32(np.float64(np.float32(np.float32(0.2126) * s[0]) + np.float32(np.float32(0.7152) * s[1]))
+                     + 0.0722 * np.float64(s[2]))
+    import ctypes
+    libm = ctypes.CDLL("libm.so.6")
+    libm.powf.restype = ctypes.c_float
+    libm.powf.argtypes = [ctypes.c_float, ctypes.c_float]
+    return float(libm.powf(float(np.float32(1.0e-3) / lum), float(np.float32(1.0) / np.float32(ns))))
+
+
+def default_material():
+    """Renderer::DEFAULT_MATERIAL (renderer.cpp:21-30)."""
+    return dict(diffuse=(1.0, 0.0, 0.5), specular=(0.5, 0.5, 0.5), ns=5.0, reflection=0.0, roughness=0.0)
+
+
+def base_settings(w, h, **kw) -> RenderSettings:
+    st = RenderSettings(image_width=w, image_height=h, compute_shadows=True, enable_bvh=True,
+                        bvh_max_depth=12, bvh_leaf_object_count=40)
+    return st.copy(**kw)
+
+
+def _camera(T, st: RenderSettings):
+    rw, rh = st.render_size()
+    _, pinv = T.camera_matrices(80.0, np.float32(rw) / np.float32(rh))
+    ident = T.transform("identity")
+    return np.zeros(3, np.float32), pinv, ident
+
+
+def _finish(tri, mat_idx, uv, mats, cam, light=(3.0, 3.0, 2.0), shapes=None, textures=None):
+    cam_pos, pinv, c2w = cam
+    sk, sh, sm = shapes if shapes is not None else empty_shapes()
+    return SceneData(tri=np.ascontiguousarray(tri, np.float32).reshape(-1, 9),
+                     tri_mat=np.ascontiguousarray(mat_idx, np.int32),
+                     tri_uv=None if uv is None else np.ascontiguousarray(uv, np.float32),
+                     shape_kind=sk, shape=sh, shape_mat=sm,
+                     materials=np.ascontiguousarray(mats, np.float32).reshape(-1, 16),
+                     cam_pos=np.asarray(cam_pos, np.float32), proj_inv=np.asarray(pinv, np.float32),
+                     cam_to_world=np.asarray(c2w, np.float32), light=np.asarray(light, np.float32),
+                     textures=textures or {})
+
+
+def sphere256(T=None, width=256, height=256):
+    """C1: Sphere(Point(0,0,-3), 1.0, mat 0) with DEFAULT_MATERIAL, 256^2, shadows on, no triangles."""
+    T = T or default_transforms()
+    st = base_settings(width, height)
+    dm = default_material()
+    thr = specular_threshold(dm["specular"], dm["ns"])
+    mats = material(diffuse=dm["diffuse"], specular=dm["specular"], ns=dm["ns"], specular_threshold=thr)[None]
+    shapes = (np.array([SHAPE_SPHERE], np.int32), np.array([[0.0, 0.0, -3.0, 1.0, 0.0, 0.0]], np.float32),
+              np.array([0], np.int32))
+    sc = _finish(np.zeros((0, 9), np.float32), np.zeros(0, np.int32), None, mats, _camera(T, st), shapes=shapes)
+    return sc, st
+
+
+def uv_sphere_scene(nu, nv, scale, bump, width, height, T=None, texcoords=True, **kw):
+    T = T or default_transforms()
+    st = base_settings(width, height, **kw)
+    tri, uv = uv_sphere_triangles(nu, nv, bump=bump, texcoords=texcoords)
+    m = object_transform(T, -3.0, scale=scale)
+    tri = transform_triangles(m, tri)
+    thr = specular_threshold((0.5, 0.5, 0.5), 20.0)
+    mats = material(diffuse=(0.8, 0.3, 0.3), specular=(0.5, 0.5, 0.5), ns=20.0, specular_threshold=thr)[None]
+    sc = _finish(tri, np.zeros(tri.shape[0], np.int32), uv, mats, _camera(T, st))
+    return sc, st
+
+
+def bumpy70k(T=None, width=1920, height=1080, **kw):
+    """C3 stand-in (stanford_bunny.obj is missing from the reference snapshot)."""
+    return uv_sphere_scene(264, 133, 1.2, 0.08, width, height, T=T, texcoords=False, **kw)
+
+
+def sphere1m(T=None, width=1920, height=1080, ssaa=True, **kw):
+    """C4: 1,000,000-tri UV sphere, 1920x1080, 2x2 SSAA."""
+    return uv_sphere_scene(1000, 500, 1.5, 0.0, width, height, T=T, texcoords=True,
+                           enable_ssaa=ssaa, ssaa_factor=2, **kw)
+
+
+def procedural_maps(size=1024, seed=1234):
+    """Seeded normal + height maps for C5 (values are k/255 like an 8-bit texture read by read_image)."""
+    rng = np.random.default_rng(seed)
+    h = rng.integers(0, 256, size=(size // 16 + 1, size // 16 + 1)).astype(np.float64)
+    # smooth the height field by bilinear upsampling (integer arithmetic on the grid, then quantise)
+    ys = np.linspace(0, size // 16, size, endpoint=False)
+    y0 = np.floor(ys).astype(int)
+    fy = ys - y0
+    hh = (h[y0][:, y0] * ((1 - fy)[:, None] * (1 - fy)[None, :]) + h[y0 + 1][:, y0] * (fy[:, None] * (1 - fy)[None, :])
+          + h[y0][:, y0 + 1] * ((1 - fy)[:, None] * fy[None, :]) + h[y0 + 1][:, y0 + 1] * (fy[:, None] * fy[None, :]))
+    hq = np.clip(np.rint(hh), 0, 255).astype(np.uint8)
+    gx = np.gradient(hh, axis=1) / 64.0
+    gy = np.gradient(hh, axis=0) / 64.0
+    n = np.stack([-gx, -gy, np.ones_like(gx)], axis=-1)
+    n /= np.linalg.norm(n, axis=-1, keepdims=True)
+    nq = np.clip(np.rint((n * 0.5 + 0.5) * 255), 0, 255).astype(np.uint8)
+    inv255 = np.float32(1.0) / np.float32(255)   # read_image: Color(bytes) / 255 == bytes * (1/255) (color.cpp:88-92)
+    disp = np.zeros((size, size, 4), np.float32)
+    disp[..., 0] = hq.astype(np.float32) * inv255
+    disp[..., 1] = disp[..., 0]
+    disp[..., 2] = disp[..., 0]
+    disp[..., 3] = np.float32(255) * inv255
+    nm = np.zeros((size, size, 4), np.float32)
+    nm[..., :3] = nq.astype(np.float32) * inv255
+    nm[..., 3] = np.float32(255) * inv255
+    return nm, disp
+
+
+def sphere1m_refl(T=None, width=1920, height=1080, ssaa=True, samples=16, **kw):
+    """C5: C4 + rough reflections (reflection 0.5, roughness 0.3, 16 samples) + normal / parallax maps."""
+    sc, st = sphere1m(T=T, width=width, height=height, ssaa=ssaa, **kw)
+    sc.materials[0, 12] = 0.5   # reflection
+    sc.materials[0, 13] = 0.3   # roughness
+    nm, disp = procedural_maps()
+    sc.textures = {TEX_NORMAL: nm, TEX_DISPLACEMENT: disp}
+    st = st.copy(rough_reflections_sample_count=samples, max_recursion_depth=5, enable_normal_mapping=True,
+                 enable_displacement_mapping=True, displacement_mapping_strength=0.02, parallax_mapping_steps=32)
+    return sc, st
+
+
+def obj_scene(path, tz, width, height, T=None, loader=None, **kw):
+    """An OBJ through read_meshio_data + create_triangles(data, 0, T(0,0,tz)*Ry30*Rx20); thresholds per
+    precompute_materials.  ``loader(path, xform) -> (tri9, mat, uv, mats)``."""
+    T = T or default_transforms()
+    st = base_settings(width, height, **kw)
+    m = object_transform(T, tz)
+    if loader is None:
+        from . import _lib
+        loader = _lib.load_obj
+    tri, mat, uv, mats = loader(path, m)
+    mats = np.array(mats, np.float32).reshape(-1, 16)
+    for k in range(mats.shape[0]):
+        mats[k, 15] = specular_threshold(mats[k, 6:9], mats[k, 14])
+    return _finish(tri, mat, uv, mats, _camera(T, st)), st
+
+
+def data_path(name):
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    return os.path.join(here, "tests", "golden", "data", name)
+
+
+def cube1080(T=None, width=1920, height=1080, loader=None, **kw):
+    return obj_scene(data_path("cube.obj"), -5.0, width, height, T=T, loader=loader, **kw)
+
+
+def robot1080(T=None, width=1920, height=1080, loader=None, **kw):
+    return obj_scene(data_path(os.path.join("Robot", "robot.obj")), -4.0, width, height, T=T, loader=loader, **kw)
+
+
+CONFIGS = {
+    "sphere256": sphere256,
+    "cube1080": cube1080,
+    "robot1080": robot1080,
+    "bumpy70k": bumpy70k,
+    "sphere1m": sphere1m,
+    "sphere1m_refl": sphere1m_refl,
+}
