@@ -1,0 +1,212 @@
+/*
+ * rt_mi355x.h -- C ABI of the MI355X-native primary-ray + shadow-ray renderer
+ * (librt_mi355x.so).  Drop-in for the hot path of TomClabault/RayTracerCPP:
+ * each entry point replaces one member of the reference's Renderer class
+ * (tp2/projets/renderer/renderer.h:20-355) or one free function it depends on;
+ * the reference interface is cited next to each declaration.
+ *
+ * Conventions
+ *   - plain pointers + sizes, no C++ types; every function is synchronous;
+ *   - matrices are 16 floats, row-major (Transform::m[i][j] = m[4*i+j], tp2/src/mat.h:21-71);
+ *   - triangles are [n][9] floats (a.xyz b.xyz c.xyz, world space as left by
+ *     MeshIOUtils::create_triangles), material indices [n] int32, optional
+ *     texture coordinates [n][6] floats (u0 u1 u2 v0 v1 v2 == Triangle::_tex_coords_u/_v);
+ *   - materials are [n][16] floats: ambient_coeff rgb, diffuse rgb, specular rgb,
+ *     emission rgb, reflection, roughness, ns, specular_threshold (Material, tp2/src/materials.h:14-38);
+ *   - images are ARGB32 (0xAARRGGBB, QImage::Format_ARGB32), row-major, row 0 = NDC y = -1;
+ *   - every function returns RT_OK (0) or a negative RT_E* code; rt_last_error()
+ *     gives the message of the calling thread's last failure.  No exceptions
+ *     cross this boundary.  The reference has no error reporting (asserts / UB):
+ *     invalid material indices, absent textures and renders without geometry
+ *     are rejected here up front with RT_EINVAL.
+ *   - a handle belongs to one thread at a time (as Renderer does).
+ */
+#ifndef RT_MI355X_H
+#define RT_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_OK 0
+#define RT_EINVAL (-1)
+#define RT_EHIP (-2)
+#define RT_ENOMEM (-3)
+#define RT_ESTATE (-4)
+#define RT_EUNSUPPORTED (-5)
+#define RT_EIO (-6)
+
+/* RenderSettings::ShadingMethod (rendererSettings.h:8-25) */
+#define RT_SHADING_RT 0
+#define RT_SHADING_ABS_NORMALS 1
+#define RT_SHADING_PASTEL_NORMALS 2
+#define RT_SHADING_BARYCENTRIC 3
+#define RT_SHADING_VISUALIZE_AO 4
+
+/* texture slots: Renderer::set_{ao,diffuse,normal,displacement,roughness}_map, set_skysphere (renderer.h:77-84) */
+#define RT_TEX_AO 0
+#define RT_TEX_DIFFUSE 1
+#define RT_TEX_NORMAL 2
+#define RT_TEX_DISPLACEMENT 3
+#define RT_TEX_ROUGHNESS 4
+#define RT_TEX_SKYSPHERE 5
+
+/* RenderSettings, field for field (tp2/projets/renderer/rendererSettings.h:6-105);
+ * the raster / SSAO / clipping fields are accepted but those paths are out of scope. */
+typedef struct rt_settings {
+    int32_t image_width, image_height;
+    int32_t enable_ssaa, ssaa_factor;
+    int32_t enable_clipping;
+    int32_t hybrid_rasterization_tracing;   /* must be 0: raster path out of scope */
+    int32_t shading_method;
+    int32_t compute_shadows;
+    int32_t max_recursion_depth;
+    int32_t enable_bvh, bvh_max_depth, bvh_leaf_object_count;
+    int32_t enable_ssao;                    /* must be 0: SSAO out of scope (stubbed) */
+    int32_t ssao_sample_count;
+    float ssao_radius, ssao_amount;
+    int32_t enable_ambient, enable_diffuse, enable_specular, enable_emissive;
+    int32_t rough_reflections_sample_count;
+    int32_t enable_ao_mapping, enable_diffuse_mapping, enable_normal_mapping, enable_displacement_mapping;
+    float displacement_mapping_strength;
+    int32_t parallax_mapping_steps;
+    int32_t enable_roughness_mapping;
+    int32_t enable_skysphere, enable_skybox;
+    uint32_t rng_seed;                      /* counter-based rough-reflection RNG seed (no reference equivalent) */
+} rt_settings;
+
+/* Per-render statistics (no reference equivalent; Renderer prints timings only). */
+typedef struct rt_stats {
+    int64_t primary_rays;      /* render_w * render_h of the last ray_trace */
+    int64_t shadow_rays;       /* one per shaded hit with compute_shadows */
+    int64_t reflection_rays;
+    float kernel_ms;           /* GPU time of the last ray_trace kernel (HIP events) */
+    float post_ms;             /* GPU time of the last post_process */
+    float build_ms;            /* host octree build + flatten + upload */
+    int64_t octree_inner, octree_leaves, octree_empty_leaves, octree_max_leaf, octree_max_depth;
+    int64_t gpu_nodes, gpu_tris;
+    int32_t render_width, render_height;
+} rt_stats;
+
+typedef struct rt_renderer rt_renderer;
+
+/* RenderSettings() defaults (rendererSettings.h:27-102) */
+void rt_default_settings(rt_settings *s);
+
+/* Renderer::Renderer() (renderer.cpp:80): default Scene (Camera at origin, fov 45,
+ * near 0.1, far 1000; PointLight (3,3,2)), RenderSettings(), no geometry.
+ * device: HIP device ordinal.  Returns NULL on failure (see rt_last_error). */
+rt_renderer *rt_create(int device);
+void rt_destroy(rt_renderer *r);
+const char *rt_last_error(void);
+
+/* Renderer::render_settings() (renderer.h:46): read / replace the settings.
+ * Replacing them re-creates the image (init_buffers, renderer.cpp:122-135) when the
+ * render size changed and rebuilds the octree when the BVH parameters changed. */
+int rt_get_settings(rt_renderer *r, rt_settings *out);
+int rt_set_settings(rt_renderer *r, const rt_settings *s);
+
+/* Renderer::change_render_size (renderer.cpp:250-261) */
+int rt_change_render_size(rt_renderer *r, int32_t width, int32_t height);
+
+/* Renderer::set_triangles (renderer.cpp:137-144): copies, then builds the octree
+ * BVH(&_triangles, bvh_max_depth, bvh_leaf_object_count) on the host, flattens
+ * and uploads it.  uv6 may be NULL ((-1,-1,-1) texture coordinates). */
+int rt_set_triangles(rt_renderer *r, const float *tri9, const int32_t *mat, const float *uv6, int64_t n);
+
+/* Renderer::add_analytic_shape (renderer.cpp:146) with Sphere / Plane (analyticShape.h:20-53) */
+int rt_add_sphere(rt_renderer *r, float cx, float cy, float cz, float radius, int32_t mat);
+int rt_add_plane(rt_renderer *r, float px, float py, float pz, float nx, float ny, float nz, int32_t mat);
+
+/* Renderer::clear_geometry (renderer.cpp:182-186) */
+int rt_clear_geometry(rt_renderer *r);
+
+/* Renderer::set_materials / get_materials (renderer.cpp:148-150) */
+int rt_set_materials(rt_renderer *r, const float *mats16, int32_t n);
+int rt_get_material_count(rt_renderer *r, int32_t *n);
+
+/* Renderer::change_camera_fov / change_camera_aspect_ratio / set_light_position (renderer.cpp:188-190) */
+int rt_change_camera_fov(rt_renderer *r, float fov);
+int rt_change_camera_aspect_ratio(rt_renderer *r, float aspect);
+int rt_set_light_position(rt_renderer *r, float x, float y, float z);
+
+/* Renderer::set_camera_transform / apply_transformation_to_camera (renderer.cpp:226-241) */
+int rt_set_camera_transform(rt_renderer *r, const float m[16]);
+int rt_apply_transformation_to_camera(rt_renderer *r, const float m[16]);
+
+/* Direct camera state (Camera::_position, _perspective_proj_mat_inv, _camera_to_world_mat,
+ * scene/camera.h:19-30), for callers that computed the matrices themselves. */
+int rt_set_camera_matrices(rt_renderer *r, const float pos[3], const float proj_inv[16], const float cam_to_world[16]);
+int rt_get_camera_matrices(rt_renderer *r, float pos[3], float proj_inv[16], float cam_to_world[16]);
+
+/* Renderer::set_object_transform / reset_previous_transform (renderer.cpp:212-224) */
+int rt_set_object_transform(rt_renderer *r, const float m[16]);
+int rt_reset_previous_transform(rt_renderer *r);
+
+/* Renderer::set_*_map / set_skysphere and clear_*_map (renderer.cpp:192-205).
+ * rgba: w*h*4 floats (Image texels); NULL clears the slot. */
+int rt_set_texture(rt_renderer *r, int32_t slot, int32_t w, int32_t h, const float *rgba);
+
+/* Renderer::set_skybox(Skybox(faces)) (renderer.cpp:199, skybox.h:12-16): faces
+ * right, left, top, bottom, back, front. */
+int rt_set_skybox(rt_renderer *r, const int32_t w[6], const int32_t h[6], const float *const faces[6]);
+
+/* Renderer::reconstruct_bvh_new / destroy_bvh (renderer.cpp:243-248) */
+int rt_reconstruct_bvh_new(rt_renderer *r);
+int rt_destroy_bvh(rt_renderer *r);
+
+/* Renderer::ray_trace (renderer.cpp:1068-1116): renders the render_w x render_h
+ * internal image on the GPU (synchronous). */
+int rt_ray_trace(rt_renderer *r);
+
+/* Renderer::post_process (renderer.cpp:1118-1124): SSAA downscale when enabled
+ * (SSAO is out of scope and rejected in rt_set_settings). */
+int rt_post_process(rt_renderer *r);
+
+/* Renderer::get_image (renderer.cpp:106-109): copies the current image
+ * (image_width x image_height after post_process) to argb; w/h receive its size. */
+int rt_get_image(rt_renderer *r, uint32_t *argb, int32_t *w, int32_t *h);
+
+/* render(Renderer&) (utils/mainUtils.cpp:6-21): ray_trace + post_process;
+ * *ms receives the wall time in milliseconds (may be NULL). */
+int rt_render(rt_renderer *r, float *ms);
+
+/* Parity / debug buffers of the last ray_trace at internal resolution
+ * (render_w x render_h); any pointer may be NULL.  Requesting them before the
+ * render (rt_request_aux) makes the kernel write them. */
+int rt_request_aux(rt_renderer *r, int32_t want_rgba, int32_t want_hit, int32_t want_shadow);
+int rt_get_internal(rt_renderer *r, uint32_t *argb, float *rgba, int32_t *hit_id, float *hit_t, uint8_t *shadow);
+
+int rt_get_stats(rt_renderer *r, rt_stats *out);
+
+/* Image-strip rendering for multi-GPU (one process per GPU): renders the bands of
+ * band_rows OUTPUT rows with band % nranks == rank into the device buffer d_out
+ * (image_width x local_rows(...) ARGB32, final resolution, SSAA applied) on the
+ * given HIP stream (NULL = the handle's stream).  Does not synchronise. */
+int rt_local_rows(rt_renderer *r, int32_t band_rows, int32_t rank, int32_t nranks, int32_t *rows_out);
+int rt_render_bands_device(rt_renderer *r, int32_t band_rows, int32_t rank, int32_t nranks, uint32_t *d_out,
+                           void *hip_stream);
+
+/* ---- tp2/src/mat.cpp restated (host) ---- */
+/* kind: 0 Translation(x,y,z) 1 RotationX(x deg) 2 RotationY 3 RotationZ 4 Scale(x,y,z) 5 Identity */
+void rt_make_transform(int32_t kind, float x, float y, float z, float out[16]);
+void rt_compose(const float a[16], const float b[16], float out[16]);                      /* a(b), mat.cpp:363-371 */
+void rt_inverse(const float m[16], float out[16]);                                          /* mat.cpp:378-447 */
+void rt_perspective(float fov, float aspect, float znear, float zfar, float out[16]);       /* mat.cpp:307-319 */
+void rt_transform_points(const float m[16], const float *pts, int64_t n, float *out);       /* mat.cpp:83-100 */
+
+/* ---- OBJ / MTL loading: read_meshio_data (tp2/src/mesh_io.cpp:426-591) +
+ * MeshIOUtils::create_triangles(data, mat_offset, xform) (utils/meshIOUtils.cpp:4-30).
+ * Two-step: rt_obj_open parses, rt_obj_fetch copies out (arrays sized from the counts). */
+typedef struct rt_obj rt_obj;
+rt_obj *rt_obj_open(const char *path, const float xform[16], int32_t mat_offset);
+int rt_obj_counts(const rt_obj *o, int64_t *ntri, int32_t *nmat, int32_t *has_uv);
+int rt_obj_fetch(const rt_obj *o, float *tri9, int32_t *mat, float *uv6, float *mats16);
+void rt_obj_close(rt_obj *o);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,215 @@
+"""ctypes binding of librt_mi355x.so (include/rt_mi355x.h).
+
+The product path is this HIP library; there is no CPU fallback.  Loading fails
+loudly when the in-tree .so is missing (build it with ``__graft_entry__.build()``
+or ``make -C raytracercpp_amd/csrc``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librt_mi355x.so")
+
+RT_OK = 0
+ERRORS = {-1: "RT_EINVAL", -2: "RT_EHIP", -3: "RT_ENOMEM", -4: "RT_ESTATE", -5: "RT_EUNSUPPORTED", -6: "RT_EIO"}
+
+_f32p = C.POINTER(C.c_float)
+_i32p = C.POINTER(C.c_int32)
+_u32p = C.POINTER(C.c_uint32)
+_u8p = C.POINTER(C.c_uint8)
+_i64p = C.POINTER(C.c_int64)
+
+
+class RtSettings(C.Structure):
+    _fields_ = [
+        ("image_width", C.c_int32), ("image_height", C.c_int32),
+        ("enable_ssaa", C.c_int32), ("ssaa_factor", C.c_int32),
+        ("enable_clipping", C.c_int32), ("hybrid_rasterization_tracing", C.c_int32),
+        ("shading_method", C.c_int32), ("compute_shadows", C.c_int32), ("max_recursion_depth", C.c_int32),
+        ("enable_bvh", C.c_int32), ("bvh_max_depth", C.c_int32), ("bvh_leaf_object_count", C.c_int32),
+        ("enable_ssao", C.c_int32), ("ssao_sample_count", C.c_int32),
+        ("ssao_radius", C.c_float), ("ssao_amount", C.c_float),
+        ("enable_ambient", C.c_int32), ("enable_diffuse", C.c_int32), ("enable_specular", C.c_int32),
+        ("enable_emissive", C.c_int32), ("rough_reflections_sample_count", C.c_int32),
+        ("enable_ao_mapping", C.c_int32), ("enable_diffuse_mapping", C.c_int32),
+        ("enable_normal_mapping", C.c_int32), ("enable_displacement_mapping", C.c_int32),
+        ("displacement_mapping_strength", C.c_float), ("parallax_mapping_steps", C.c_int32),
+        ("enable_roughness_mapping", C.c_int32), ("enable_skysphere", C.c_int32), ("enable_skybox", C.c_int32),
+        ("rng_seed", C.c_uint32),
+    ]
+
+
+class RtStats(C.Structure):
+    _fields_ = [
+        ("primary_rays", C.c_int64), ("shadow_rays", C.c_int64), ("reflection_rays", C.c_int64),
+        ("kernel_ms", C.c_float), ("post_ms", C.c_float), ("build_ms", C.c_float),
+        ("octree_inner", C.c_int64), ("octree_leaves", C.c_int64), ("octree_empty_leaves", C.c_int64),
+        ("octree_max_leaf", C.c_int64), ("octree_max_depth", C.c_int64),
+        ("gpu_nodes", C.c_int64), ("gpu_tris", C.c_int64),
+        ("render_width", C.c_int32), ("render_height", C.c_int32),
+    ]
+
+    def as_dict(self):
+        return {n: (float(getattr(self, n)) if t is C.c_float else int(getattr(self, n))) for n, t in self._fields_}
+
+
+# every exported symbol and its ctypes signature (restype, argtypes); tests check
+# that the .so exports exactly what include/rt_mi355x.h declares.
+_H = C.c_void_p
+SIGNATURES = {
+    "rt_default_settings": (None, [C.POINTER(RtSettings)]),
+    "rt_create": (_H, [C.c_int]),
+    "rt_destroy": (None, [_H]),
+    "rt_last_error": (C.c_char_p, []),
+    "rt_get_settings": (C.c_int, [_H, C.POINTER(RtSettings)]),
+    "rt_set_settings": (C.c_int, [_H, C.POINTER(RtSettings)]),
+    "rt_change_render_size": (C.c_int, [_H, C.c_int32, C.c_int32]),
+    "rt_set_triangles": (C.c_int, [_H, _f32p, _i32p, _f32p, C.c_int64]),
+    "rt_add_sphere": (C.c_int, [_H, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int32]),
+    "rt_add_plane": (C.c_int, [_H] + [C.c_float] * 6 + [C.c_int32]),
+    "rt_clear_geometry": (C.c_int, [_H]),
+    "rt_set_materials": (C.c_int, [_H, _f32p, C.c_int32]),
+    "rt_get_material_count": (C.c_int, [_H, _i32p]),
+    "rt_change_camera_fov": (C.c_int, [_H, C.c_float]),
+    "rt_change_camera_aspect_ratio": (C.c_int, [_H, C.c_float]),
+    "rt_set_light_position": (C.c_int, [_H, C.c_float, C.c_float, C.c_float]),
+    "rt_set_camera_transform": (C.c_int, [_H, _f32p]),
+    "rt_apply_transformation_to_camera": (C.c_int, [_H, _f32p]),
+    "rt_set_camera_matrices": (C.c_int, [_H, _f32p, _f32p, _f32p]),
+    "rt_get_camera_matrices": (C.c_int, [_H, _f32p, _f32p, _f32p]),
+    "rt_set_object_transform": (C.c_int, [_H, _f32p]),
+    "rt_reset_previous_transform": (C.c_int, [_H]),
+    "rt_set_texture": (C.c_int, [_H, C.c_int32, C.c_int32, C.c_int32, _f32p]),
+    "rt_set_skybox": (C.c_int, [_H, _i32p, _i32p, C.POINTER(_f32p)]),
+    "rt_reconstruct_bvh_new": (C.c_int, [_H]),
+    "rt_destroy_bvh": (C.c_int, [_H]),
+    "rt_ray_trace": (C.c_int, [_H]),
+    "rt_post_process": (C.c_int, [_H]),
+    "rt_get_image": (C.c_int, [_H, _u32p, _i32p, _i32p]),
+    "rt_render": (C.c_int, [_H, _f32p]),
+    "rt_request_aux": (C.c_int, [_H, C.c_int32, C.c_int32, C.c_int32]),
+    "rt_get_internal": (C.c_int, [_H, _u32p, _f32p, _i32p, _f32p, _u8p]),
+    "rt_get_stats": (C.c_int, [_H, C.POINTER(RtStats)]),
+    "rt_local_rows": (C.c_int, [_H, C.c_int32, C.c_int32, C.c_int32, _i32p]),
+    "rt_render_bands_device": (C.c_int, [_H, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]),
+    "rt_make_transform": (None, [C.c_int32, C.c_float, C.c_float, C.c_float, _f32p]),
+    "rt_compose": (None, [_f32p, _f32p, _f32p]),
+    "rt_inverse": (None, [_f32p, _f32p]),
+    "rt_perspective": (None, [C.c_float, C.c_float, C.c_float, C.c_float, _f32p]),
+    "rt_transform_points": (None, [_f32p, _f32p, C.c_int64, _f32p]),
+    "rt_obj_open": (_H, [C.c_char_p, _f32p, C.c_int32]),
+    "rt_obj_counts": (C.c_int, [_H, _i64p, _i32p, _i32p]),
+    "rt_obj_fetch": (C.c_int, [_H, _f32p, _i32p, _f32p, _f32p]),
+    "rt_obj_close": (None, [_H]),
+}
+
+_lib = None
+
+
+def lib():
+    """The loaded librt_mi355x.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: the HIP library must be built "
+                               "(python -c 'import __graft_entry__ as g; g.build()')")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+class RtError(RuntimeError):
+    def __init__(self, code, where):
+        msg = lib().rt_last_error()
+        super().__init__(f"{where}: {ERRORS.get(code, code)}: {msg.decode() if msg else ''}")
+        self.code = code
+
+
+def check(rc, where):
+    if rc != RT_OK:
+        raise RtError(rc, where)
+    return rc
+
+
+def ptr(a, t):
+    if a is None:
+        return C.cast(None, t)
+    return a.ctypes.data_as(t)
+
+
+def f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+# ---- mat.cpp helpers -----------------------------------------------------------
+_KINDS = {"translation": 0, "rx": 1, "ry": 2, "rz": 3, "scale": 4, "identity": 5}
+
+
+def make_transform(kind, x=0.0, y=0.0, z=0.0):
+    out = np.zeros(16, np.float32)
+    lib().rt_make_transform(_KINDS[kind], x, y, z, ptr(out, _f32p))
+    return out
+
+
+def compose(a, b):
+    a, b = f32(a), f32(b)
+    out = np.zeros(16, np.float32)
+    lib().rt_compose(ptr(a, _f32p), ptr(b, _f32p), ptr(out, _f32p))
+    return out
+
+
+def inverse(m):
+    m = f32(m)
+    out = np.zeros(16, np.float32)
+    lib().rt_inverse(ptr(m, _f32p), ptr(out, _f32p))
+    return out
+
+
+def perspective(fov, aspect, znear=0.1, zfar=1000.0):
+    out = np.zeros(16, np.float32)
+    lib().rt_perspective(fov, aspect, znear, zfar, ptr(out, _f32p))
+    return out
+
+
+def camera_matrices(fov, aspect, znear=0.1, zfar=1000.0):
+    """Camera::set_aspect_ratio (camera.cpp:5-11): (Perspective, Perspective.inverse())."""
+    p = perspective(fov, aspect, znear, zfar)
+    return p, inverse(p)
+
+
+def transform_points(m, pts):
+    m = f32(m)
+    pts = f32(pts).reshape(-1, 3)
+    out = np.zeros_like(pts)
+    lib().rt_transform_points(ptr(m, _f32p), ptr(pts, _f32p), pts.shape[0], ptr(out, _f32p))
+    return out
+
+
+def load_obj(path, xform, mat_offset=0):
+    """read_meshio_data + create_triangles -> (tri9, mat, uv6 or None, mats16)."""
+    xform = f32(xform)
+    L = lib()
+    h = L.rt_obj_open(path.encode(), ptr(xform, _f32p), mat_offset)
+    if not h:
+        raise RuntimeError(f"rt_obj_open({path}): {L.rt_last_error().decode()}")
+    try:
+        n = C.c_int64()
+        nm = C.c_int32()
+        has_uv = C.c_int32()
+        check(L.rt_obj_counts(h, C.byref(n), C.byref(nm), C.byref(has_uv)), "rt_obj_counts")
+        tri = np.zeros((n.value, 9), np.float32)
+        mat = np.zeros(n.value, np.int32)
+        uv = np.zeros((n.value, 6), np.float32) if has_uv.value else None
+        mats = np.zeros((nm.value, 16), np.float32)
+        check(L.rt_obj_fetch(h, ptr(tri, _f32p), ptr(mat, _i32p), ptr(uv, _f32p), ptr(mats, _f32p)), "rt_obj_fetch")
+        return tri, mat, uv, mats
+    finally:
+        L.rt_obj_close(h)

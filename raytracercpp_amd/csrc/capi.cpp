@@ -1,0 +1,333 @@
+// capi.cpp -- extern "C" boundary (include/rt_mi355x.h).  No exception crosses it.
+#include <chrono>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "../../include/rt_mi355x.h"
+#include "host_scene.hpp"
+#include "renderer.hpp"
+
+namespace {
+thread_local std::string g_err;
+
+int record(rt::Renderer* r, int rc)
+{
+    if (rc != RT_OK)
+        g_err = r->error();
+    return rc;
+}
+
+int bad(const char* msg)
+{
+    g_err = msg;
+    return RT_EINVAL;
+}
+
+template <class F>
+int guarded(rt::Renderer* r, F&& f)
+{
+    if (!r)
+        return bad("null renderer handle");
+    try {
+        return record(r, f());
+    } catch (const std::bad_alloc&) {
+        g_err = "out of host memory";
+        return RT_ENOMEM;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return RT_EINVAL;
+    }
+}
+
+rt::Renderer* R(rt_renderer* r) { return reinterpret_cast<rt::Renderer*>(r); }
+}  // namespace
+
+extern "C" {
+
+void rt_default_settings(rt_settings* s)
+{
+    std::memset(s, 0, sizeof(*s));
+    s->image_width = 1024;
+    s->image_height = 1024;
+    s->enable_ssaa = 0;
+    s->ssaa_factor = 2;
+    s->enable_clipping = 1;
+    s->hybrid_rasterization_tracing = 0;
+    s->shading_method = RT_SHADING_RT;
+    s->compute_shadows = 0;
+    s->max_recursion_depth = 5;
+    s->enable_bvh = 1;
+    s->bvh_max_depth = 12;
+    s->bvh_leaf_object_count = 40;
+    s->enable_ssao = 0;
+    s->ssao_sample_count = 64;
+    s->ssao_radius = 0.5f;
+    s->ssao_amount = 1.0f;
+    s->enable_ambient = 1;
+    s->enable_diffuse = 1;
+    s->enable_specular = 1;
+    s->enable_emissive = 1;
+    s->rough_reflections_sample_count = 3;
+    s->displacement_mapping_strength = 0.02f;
+    s->parallax_mapping_steps = 32;
+    s->rng_seed = 0x5EED1234u;
+}
+
+rt_renderer* rt_create(int device)
+{
+    try {
+        rt::Renderer* r = new rt::Renderer(device);
+        std::string err;
+        if (r->init(err) != RT_OK) {
+            g_err = err;
+            delete r;
+            return nullptr;
+        }
+        return reinterpret_cast<rt_renderer*>(r);
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return nullptr;
+    }
+}
+
+void rt_destroy(rt_renderer* r) { delete R(r); }
+
+const char* rt_last_error(void) { return g_err.c_str(); }
+
+int rt_get_settings(rt_renderer* r, rt_settings* out)
+{
+    return guarded(R(r), [&] {
+        *out = R(r)->render_settings();
+        return RT_OK;
+    });
+}
+int rt_set_settings(rt_renderer* r, const rt_settings* s)
+{
+    return guarded(R(r), [&] { return s ? R(r)->set_settings(*s) : RT_EINVAL; });
+}
+int rt_change_render_size(rt_renderer* r, int32_t w, int32_t h)
+{
+    return guarded(R(r), [&] { return R(r)->change_render_size(w, h); });
+}
+int rt_set_triangles(rt_renderer* r, const float* tri9, const int32_t* mat, const float* uv6, int64_t n)
+{
+    return guarded(R(r), [&] { return R(r)->set_triangles(tri9, mat, uv6, n); });
+}
+int rt_add_sphere(rt_renderer* r, float cx, float cy, float cz, float radius, int32_t mat)
+{
+    return guarded(R(r), [&] { return R(r)->add_sphere(cx, cy, cz, radius, mat); });
+}
+int rt_add_plane(rt_renderer* r, float px, float py, float pz, float nx, float ny, float nz, int32_t mat)
+{
+    return guarded(R(r), [&] { return R(r)->add_plane(px, py, pz, nx, ny, nz, mat); });
+}
+int rt_clear_geometry(rt_renderer* r)
+{
+    return guarded(R(r), [&] { return R(r)->clear_geometry(); });
+}
+int rt_set_materials(rt_renderer* r, const float* mats16, int32_t n)
+{
+    return guarded(R(r), [&] { return R(r)->set_materials(mats16, n); });
+}
+int rt_get_material_count(rt_renderer* r, int32_t* n)
+{
+    return guarded(R(r), [&] {
+        *n = R(r)->material_count();
+        return RT_OK;
+    });
+}
+int rt_change_camera_fov(rt_renderer* r, float fov)
+{
+    return guarded(R(r), [&] { return R(r)->change_camera_fov(fov); });
+}
+int rt_change_camera_aspect_ratio(rt_renderer* r, float aspect)
+{
+    return guarded(R(r), [&] { return R(r)->change_camera_aspect_ratio(aspect); });
+}
+int rt_set_light_position(rt_renderer* r, float x, float y, float z)
+{
+    return guarded(R(r), [&] { return R(r)->set_light_position(x, y, z); });
+}
+int rt_set_camera_transform(rt_renderer* r, const float m[16])
+{
+    return guarded(R(r), [&] { return m ? R(r)->set_camera_transform(m) : RT_EINVAL; });
+}
+int rt_apply_transformation_to_camera(rt_renderer* r, const float m[16])
+{
+    return guarded(R(r), [&] { return m ? R(r)->apply_transformation_to_camera(m) : RT_EINVAL; });
+}
+int rt_set_camera_matrices(rt_renderer* r, const float pos[3], const float proj_inv[16], const float c2w[16])
+{
+    return guarded(R(r), [&] { return (pos && proj_inv && c2w) ? R(r)->set_camera_matrices(pos, proj_inv, c2w) : RT_EINVAL; });
+}
+int rt_get_camera_matrices(rt_renderer* r, float pos[3], float proj_inv[16], float c2w[16])
+{
+    return guarded(R(r), [&] {
+        R(r)->get_camera_matrices(pos, proj_inv, c2w);
+        return RT_OK;
+    });
+}
+int rt_set_object_transform(rt_renderer* r, const float m[16])
+{
+    return guarded(R(r), [&] { return m ? R(r)->set_object_transform(m) : RT_EINVAL; });
+}
+int rt_reset_previous_transform(rt_renderer* r)
+{
+    return guarded(R(r), [&] { return R(r)->reset_previous_transform(); });
+}
+int rt_set_texture(rt_renderer* r, int32_t slot, int32_t w, int32_t h, const float* rgba)
+{
+    return guarded(R(r), [&] { return R(r)->set_texture(slot, w, h, rgba); });
+}
+int rt_set_skybox(rt_renderer* r, const int32_t w[6], const int32_t h[6], const float* const faces[6])
+{
+    return guarded(R(r), [&] { return R(r)->set_skybox(w, h, faces); });
+}
+int rt_reconstruct_bvh_new(rt_renderer* r)
+{
+    return guarded(R(r), [&] { return R(r)->reconstruct_bvh_new(); });
+}
+int rt_destroy_bvh(rt_renderer* r)
+{
+    return guarded(R(r), [&] { return R(r)->destroy_bvh(); });
+}
+int rt_ray_trace(rt_renderer* r)
+{
+    return guarded(R(r), [&] { return R(r)->ray_trace(); });
+}
+int rt_post_process(rt_renderer* r)
+{
+    return guarded(R(r), [&] { return R(r)->post_process(); });
+}
+int rt_get_image(rt_renderer* r, uint32_t* argb, int32_t* w, int32_t* h)
+{
+    return guarded(R(r), [&] { return R(r)->get_image(argb, w, h); });
+}
+int rt_render(rt_renderer* r, float* ms)
+{
+    return guarded(R(r), [&] {
+        auto t0 = std::chrono::steady_clock::now();
+        int rc = R(r)->ray_trace();
+        if (rc == RT_OK)
+            rc = R(r)->post_process();
+        if (ms)
+            *ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        return rc;
+    });
+}
+int rt_request_aux(rt_renderer* r, int32_t want_rgba, int32_t want_hit, int32_t want_shadow)
+{
+    return guarded(R(r), [&] { return R(r)->request_aux(want_rgba != 0, want_hit != 0, want_shadow != 0); });
+}
+int rt_get_internal(rt_renderer* r, uint32_t* argb, float* rgba, int32_t* hit_id, float* hit_t, uint8_t* shadow)
+{
+    return guarded(R(r), [&] { return R(r)->get_internal(argb, rgba, hit_id, hit_t, shadow); });
+}
+int rt_get_stats(rt_renderer* r, rt_stats* out)
+{
+    return guarded(R(r), [&] { return out ? R(r)->get_stats(out) : RT_EINVAL; });
+}
+int rt_local_rows(rt_renderer* r, int32_t band_rows, int32_t rank, int32_t nranks, int32_t* rows_out)
+{
+    return guarded(R(r), [&] {
+        int n = R(r)->local_rows(band_rows, rank, nranks);
+        if (n < 0)
+            return bad("bad band layout");
+        *rows_out = n;
+        return RT_OK;
+    });
+}
+int rt_render_bands_device(rt_renderer* r, int32_t band_rows, int32_t rank, int32_t nranks, uint32_t* d_out,
+                           void* hip_stream)
+{
+    return guarded(R(r), [&] {
+        return R(r)->render_bands_device(band_rows, rank, nranks, d_out, reinterpret_cast<hipStream_t>(hip_stream));
+    });
+}
+
+void rt_make_transform(int32_t kind, float x, float y, float z, float out[16])
+{
+    switch (kind) {
+    case 0: rt::mat::translation(x, y, z, out); break;
+    case 1: rt::mat::rotation_x(x, out); break;
+    case 2: rt::mat::rotation_y(x, out); break;
+    case 3: rt::mat::rotation_z(x, out); break;
+    case 4: rt::mat::scale(x, y, z, out); break;
+    default: rt::mat::identity(out); break;
+    }
+}
+void rt_compose(const float a[16], const float b[16], float out[16]) { rt::mat::compose(a, b, out); }
+void rt_inverse(const float m[16], float out[16]) { rt::mat::inverse(m, out); }
+void rt_perspective(float fov, float aspect, float znear, float zfar, float out[16])
+{
+    rt::mat::perspective(fov, aspect, znear, zfar, out);
+}
+void rt_transform_points(const float m[16], const float* pts, int64_t n, float* out)
+{
+    rt::mat::transform_points(m, pts, n, out);
+}
+
+struct rt_obj {
+    rt::ObjData data;
+};
+
+rt_obj* rt_obj_open(const char* path, const float xform[16], int32_t mat_offset)
+{
+    try {
+        float ident[16];
+        rt::mat::identity(ident);
+        rt_obj* o = new rt_obj;
+        std::string err;
+        if (!rt::load_obj(path, xform ? xform : ident, mat_offset, o->data, err)) {
+            g_err = err;
+            delete o;
+            return nullptr;
+        }
+        return o;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return nullptr;
+    }
+}
+
+int rt_obj_counts(const rt_obj* o, int64_t* ntri, int32_t* nmat, int32_t* has_uv)
+{
+    if (!o)
+        return bad("null obj");
+    if (ntri) *ntri = (int64_t)o->data.mat.size();
+    if (nmat) *nmat = (int32_t)o->data.materials.size();
+    if (has_uv) *has_uv = o->data.has_uv;
+    return RT_OK;
+}
+
+int rt_obj_fetch(const rt_obj* o, float* tri9, int32_t* mat, float* uv6, float* mats16)
+{
+    if (!o)
+        return bad("null obj");
+    const rt::ObjData& d = o->data;
+    if (tri9) std::memcpy(tri9, d.tri.data(), d.tri.size() * 4);
+    if (mat) std::memcpy(mat, d.mat.data(), d.mat.size() * 4);
+    if (uv6 && d.has_uv) std::memcpy(uv6, d.uv.data(), d.uv.size() * 4);
+    if (mats16) {
+        for (size_t i = 0; i < d.materials.size(); i++) {
+            const rt::ObjMaterial& m = d.materials[i];
+            float* f = mats16 + 16 * i;
+            for (int c = 0; c < 3; c++) {
+                f[0 + c] = m.ambient[c];
+                f[3 + c] = m.diffuse[c];
+                f[6 + c] = m.specular[c];
+                f[9 + c] = m.emission[c];
+            }
+            f[12] = m.reflection;
+            f[13] = m.roughness;
+            f[14] = m.ns;
+            f[15] = 0.0f;   // specular_threshold: set by the caller (MainWindow::precompute_materials)
+        }
+    }
+    return RT_OK;
+}
+
+void rt_obj_close(rt_obj* o) { delete o; }
+
+}  // extern "C"

@@ -1,0 +1,879 @@
+// kernels.hip -- gfx950 (CDNA4) kernels for the primary-ray + shadow-ray hot path.
+//
+// One 64-lane wavefront renders one 8x8 pixel tile (one lane per pixel).  Each
+// lane runs the reference's best-first octree traversal
+// (OctreeNode::intersect, tp2/projets/bvh.h:212-287) as an iterative state
+// machine whose visit order is exactly the reference's recursion:
+//   * children that pass BoundingVolume::intersect (bvh.h:79-105) are ordered
+//     as std::priority_queue<..., std::greater<>> pops them (bvh.h:250-256):
+//     ascending t_near; when two t_near compare equal the libstdc++ heap is
+//     emulated move for move, so ties pop in the same order;
+//   * after a child returns true, the remaining siblings are skipped as soon as
+//     the closest hit is nearer than the next t_near (bvh.h:264-276);
+//   * a leaf "returns" hit.t > 0 of the query-global hit record (bvh.h:235-248).
+// The per-depth pending-children queues live in LDS (one 8-byte entry per depth
+// per lane: first child index + packed 3-bit child ranks + count); the next
+// sibling's t_near is recomputed from its 64-byte node when needed instead of
+// being stored.  Node and triangle records are 64 B / 48 B and read with
+// 16-byte loads.  All arithmetic follows the reference expression trees with
+// no contraction (-ffp-contract=off) and IEEE division / sqrt, so results are
+// bit-identical to the reference compiled with -ffp-contract=off.
+#include "kparams.hpp"
+#include "rt_math.hpp"
+
+namespace rt {
+
+constexpr int WAVES_PER_BLOCK = 4;
+constexpr int BLOCK = 64 * WAVES_PER_BLOCK;
+
+struct TRay {
+    v3 o, d;
+    float den[NPLANES], num[NPLANES];
+    bool nan;
+};
+
+// HitInfo (hitInfo.h:8-24) reduced to what the kernels need.
+struct Rec {
+    int tri;      // caller triangle index (HitInfo::triangle), -1 == nullptr
+    float t, u, v;
+    int mat;
+    v3 normal, tangent;
+};
+
+__device__ __forceinline__ Rec rec_fresh()
+{
+    Rec r;
+    r.tri = -1; r.t = -1.0f; r.u = 1.0f; r.v = 0.0f; r.mat = -1;
+    r.normal = mk(0, 0, 0); r.tangent = mk(0, 0, 0);
+    return r;
+}
+
+// OctreeNode::intersect(ray, hit) prologue, bvh.h:216-223
+__device__ __forceinline__ TRay make_ray(const KParams& P, v3 o, v3 d)
+{
+    TRay R;
+    R.o = o;
+    R.d = d;
+    bool nan = false;
+#pragma unroll
+    for (int i = 0; i < NPLANES; i++) {
+        v3 n = mk(P.pn[i][0], P.pn[i][1], P.pn[i][2]);
+        R.den[i] = dot(n, d);
+        R.num[i] = dot(n, o);
+        nan |= (R.den[i] != R.den[i]) || (R.num[i] != R.num[i]);
+    }
+    R.nan = nan;
+    return R;
+}
+
+struct NodeBox {
+    float dn[NPLANES], df[NPLANES];
+    uint32_t a, b;
+};
+
+__device__ __forceinline__ NodeBox load_node(const GNode* nodes, uint32_t i)
+{
+    const float4* p = reinterpret_cast<const float4*>(nodes + i);
+    float4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+    NodeBox n;
+    n.dn[0] = q0.x; n.dn[1] = q0.y; n.dn[2] = q0.z; n.dn[3] = q0.w;
+    n.dn[4] = q1.x; n.dn[5] = q1.y; n.dn[6] = q1.z;
+    n.df[0] = q1.w;
+    n.df[1] = q2.x; n.df[2] = q2.y; n.df[3] = q2.z; n.df[4] = q2.w;
+    n.df[5] = q3.x; n.df[6] = q3.y;
+    n.a = __float_as_uint(q3.z);
+    n.b = __float_as_uint(q3.w);
+    return n;
+}
+
+__device__ __forceinline__ uint2 load_node_link(const GNode* nodes, uint32_t i)
+{
+    const uint4* p = reinterpret_cast<const uint4*>(nodes + i);
+    uint4 q3 = p[3];
+    return make_uint2(q3.z, q3.w);
+}
+
+// BoundingVolume::intersect, bvh.h:79-105.  t_near only ever grows and t_far
+// only shrinks (std::max / std::min never return a NaN second operand), so
+// testing t_far < t_near once after the loop equals the reference's early exit.
+__device__ __forceinline__ bool vol_test(const NodeBox& n, const TRay& R, float& t_near_out)
+{
+    float t_near = -INFINITY, t_far = INFINITY;
+#pragma unroll
+    for (int i = 0; i < NPLANES; i++) {
+        float denom = R.den[i];
+        if (denom != 0.0f) {
+            float d0 = (n.dn[i] - R.num[i]) / denom;
+            float d1 = (n.df[i] - R.num[i]) / denom;
+            float lo = denom < 0 ? d1 : d0;
+            float hi = denom < 0 ? d0 : d1;
+            t_near = smax(t_near, lo);
+            t_far = smin(t_far, hi);
+        }
+    }
+    t_near_out = t_near;
+    return !(t_far < t_near);
+}
+
+// Triangle::intersect (Moller-Trumbore, backface culling), triangle.cpp:25-91
+__device__ __forceinline__ bool tri_test(const GTri* tris, uint32_t k, const TRay& R, float& t_out, float& u_out,
+                                         float& v_out)
+{
+    const float4* p = reinterpret_cast<const float4*>(tris + k);
+    float4 q0 = p[0], q1 = p[1], q2 = p[2];
+    v3 a = mk(q0.x, q0.y, q0.z);
+    v3 ab = mk(q0.w, q1.x, q1.y);
+    v3 ac = mk(q1.z, q1.w, q2.x);
+    v3 n = mk(q2.y, q2.z, q2.w);
+    v3 OA = R.o - a;
+    v3 nd = -R.d;
+    v3 m = cross(nd, OA);
+    float Mdet = dot(n, nd);
+    if (Mdet <= 0)
+        return false;
+    Mdet = 1 / Mdet;
+    float u = dot(m, ac) * Mdet;
+    if (u < 0 || u > 1)
+        return false;
+    float v = dot(m, -ab) * Mdet;
+    if (v < 0 || u + v > 1)
+        return false;
+    float t = dot(n, OA) * Mdet;
+    if (t < 0)
+        return false;
+    t_out = t;
+    u_out = u;
+    v_out = v;
+    return true;
+}
+
+struct THit {
+    float t, u, v;
+    int k;   // GTri slot, -1 none
+};
+
+// ---- libstdc++ binary heap (push_heap / pop_heap with std::greater), only
+// used when two pending children have equal t_near. ----
+__device__ __noinline__ uint32_t heap_order(const float key[8], const bool valid[8], const uint32_t rank[8], int n)
+{
+    float hk[8];
+    uint32_t hr[8];
+    int len = 0;
+    for (int s = 0; s < 8; s++) {
+        if (!valid[s])
+            continue;
+        // push_back + __push_heap(first, len, 0, value)
+        float vk = key[s];
+        uint32_t vr = rank[s];
+        int hole = len, parent = (hole - 1) / 2;
+        while (hole > 0 && hk[parent] > vk) {
+            hk[hole] = hk[parent];
+            hr[hole] = hr[parent];
+            hole = parent;
+            parent = (hole - 1) / 2;
+        }
+        hk[hole] = vk;
+        hr[hole] = vr;
+        len++;
+    }
+    uint32_t order = 0;
+    for (int i = 0; i < n; i++) {
+        order |= hr[0] << (3 * i);
+        // pop_heap: value = last; last = first; __adjust_heap(first, 0, len - 1, value)
+        if (len > 1) {
+            int l = len - 1;
+            float vk = hk[l];
+            uint32_t vr = hr[l];
+            int hole = 0, second = 0;
+            while (second < (l - 1) / 2) {
+                second = 2 * (second + 1);
+                if (hk[second] > hk[second - 1])
+                    second--;
+                hk[hole] = hk[second];
+                hr[hole] = hr[second];
+                hole = second;
+            }
+            if ((l & 1) == 0 && second == (l - 2) / 2) {
+                second = 2 * (second + 1);
+                hk[hole] = hk[second - 1];
+                hr[hole] = hr[second - 1];
+                hole = second - 1;
+            }
+            int parent = (hole - 1) / 2;
+            while (hole > 0 && hk[parent] > vk) {
+                hk[hole] = hk[parent];
+                hr[hole] = hr[parent];
+                hole = parent;
+                parent = (hole - 1) / 2;
+            }
+            hk[hole] = vk;
+            hr[hole] = vr;
+        }
+        len--;
+    }
+    return order;
+}
+
+// BVH::intersect (bvh.cpp:68-71) -> OctreeNode::intersect, iteratively.
+// Returns the reference's boolean; h is the query-global HitInfo (t,u,v,slot).
+// lv: this lane's LDS level stack, entry d at lv[d * BLOCK].
+__device__ bool bvh_closest(const KParams& P, const TRay& R, THit& h, uint2* lv)
+{
+    h.t = -1.0f;
+    h.u = 1.0f;
+    h.v = 0.0f;
+    h.k = -1;
+    if (P.nnodes == 0)
+        return false;
+    if (R.nan) {
+        // every volume passes with t_near = -inf, every triangle "hits" with
+        // t = NaN and no leaf ever returns true: the query returns false with
+        // a NaN record (NaN rays).
+        h.t = __int_as_float(0x7fc00000);
+        return false;
+    }
+    float tn;
+    NodeBox nb = load_node(P.nodes, 0);
+    if (!vol_test(nb, R, tn))
+        return false;
+
+    uint32_t a = nb.a, b = nb.b;
+    int depth = 0;
+    uint32_t any_true = 0;
+    bool r = false;
+    for (;;) {
+        // ---- VISIT the node whose link word is (a, b) at 'depth' ----
+        bool ret;
+        if (b & LEAF_BIT) {
+            uint32_t cnt = b & ~LEAF_BIT;
+            for (uint32_t k = a; k < a + cnt; k++) {
+                float t, u, v;
+                if (tri_test(P.tris, k, R, t, u, v))
+                    if (t < h.t || h.t == -1) {
+                        h.t = t;
+                        h.u = u;
+                        h.v = v;
+                        h.k = (int)k;
+                    }
+            }
+            r = h.t > 0;
+            ret = true;
+        } else {
+            uint32_t mask = b & 0xffu;
+            float key[8];
+            bool valid[8];
+            uint32_t rank[8];
+            int n = 0;
+#pragma unroll
+            for (int s = 0; s < 8; s++) {
+                rank[s] = __popc(mask & ((1u << s) - 1u));
+                valid[s] = false;
+                key[s] = INFINITY;
+                if (mask & (1u << s)) {
+                    NodeBox c = load_node(P.nodes, a + rank[s]);
+                    float t;
+                    if (vol_test(c, R, t)) {
+                        valid[s] = true;
+                        key[s] = t;
+                        n++;
+                    }
+                }
+            }
+            if (n == 0) {
+                r = false;
+                ret = true;
+            } else {
+                uint32_t order = 0;
+                bool tie = false;
+#pragma unroll
+                for (int s = 0; s < 8; s++) {
+                    if (!valid[s])
+                        continue;
+                    uint32_t pos = 0;
+#pragma unroll
+                    for (int t2 = 0; t2 < 8; t2++) {
+                        if (t2 == s || !valid[t2])
+                            continue;
+                        if (key[t2] < key[s])
+                            pos++;
+                        else if (key[t2] == key[s]) {
+                            tie = true;
+                            if (t2 < s)
+                                pos++;
+                        }
+                    }
+                    order |= rank[s] << (3 * pos);
+                }
+                if (tie)
+                    order = heap_order(key, valid, rank, n);
+                depth++;
+                any_true &= ~(1u << depth);
+                uint32_t first = a + (order & 7u);
+                lv[depth * BLOCK] = make_uint2(a, (order >> 3) | ((uint32_t)(n - 1) << 24));
+                uint2 link = load_node_link(P.nodes, first);
+                a = link.x;
+                b = link.y;
+                ret = false;
+            }
+        }
+        if (!ret)
+            continue;
+        // ---- RETURN r from the node at 'depth' to its parent ----
+        for (;;) {
+            if (depth == 0)
+                return r;
+            uint2 e = lv[depth * BLOCK];
+            uint32_t cnt = e.y >> 24;
+            uint32_t ord = e.y & 0xffffffu;
+            if (r) {
+                any_true |= 1u << depth;
+                if (cnt == 0) {
+                    depth--;
+                    continue;   // queue empty: parent returns true
+                }
+                NodeBox nx = load_node(P.nodes, e.x + (ord & 7u));
+                float t_next;
+                vol_test(nx, R, t_next);
+                if (h.t < t_next) {
+                    depth--;    // closest hit nearer than the next child: parent returns true
+                    continue;
+                }
+                lv[depth * BLOCK] = make_uint2(e.x, (ord >> 3) | ((cnt - 1) << 24));
+                a = nx.a;
+                b = nx.b;
+                break;
+            } else {
+                if (cnt == 0) {
+                    r = (any_true >> depth) & 1u;   // closest_inter != INFINITY
+                    depth--;
+                    continue;
+                }
+                uint2 link = load_node_link(P.nodes, e.x + (ord & 7u));
+                lv[depth * BLOCK] = make_uint2(e.x, (ord >> 3) | ((cnt - 1) << 24));
+                a = link.x;
+                b = link.y;
+                break;
+            }
+        }
+    }
+}
+
+// HitInfo filled by Triangle::intersect for slot k (triangle.cpp:81-88)
+__device__ __forceinline__ Rec tri_record(const KParams& P, const THit& h)
+{
+    Rec r;
+    int id = P.tri_id[h.k];
+    const float4* p = reinterpret_cast<const float4*>(P.tris + h.k);
+    float4 q0 = p[0], q1 = p[1], q2 = p[2];
+    v3 ab = mk(q0.w, q1.x, q1.y);
+    v3 ac = mk(q1.z, q1.w, q2.x);
+    v3 n = mk(q2.y, q2.z, q2.w);
+    r.tri = id;
+    r.t = h.t;
+    r.u = h.u;
+    r.v = h.v;
+    r.mat = P.tri_mat[id];
+    r.normal = normalize(n);
+    // Triangle::get_tangent, triangle.cpp:134-153
+    float u1 = -1, v1 = -1, u2 = -1, v2 = -1, u3 = -1, v3_ = -1;
+    if (P.tri_uv) {
+        const float* uv = P.tri_uv + 6 * (size_t)id;
+        u1 = uv[0]; u2 = uv[1]; u3 = uv[2];
+        v1 = uv[3]; v2 = uv[4]; v3_ = uv[5];
+    }
+    float dU1 = u2 - u1, dV1 = v2 - v1, dU2 = u3 - u1, dV2 = v3_ - v1;
+    float f = 1.0f / (dU1 * dV2 - dU2 * dV1);
+    r.tangent.x = f * (dV2 * ab.x - dV1 * ac.x);
+    r.tangent.y = f * (dV2 * ab.y - dV1 * ac.y);
+    r.tangent.z = f * (dV2 * ab.z - dV1 * ac.z);
+    return r;
+}
+
+// Sphere::intersect, analyticShape.cpp:9-60 (compute_uv forced true; reads a stale hit.t when delta>0 and t1>=t2)
+__device__ __forceinline__ bool sphere_test(const float* s, int mat, v3 o, v3 d, Rec& h)
+{
+    v3 c = mk(s[0], s[1], s[2]);
+    float r2 = s[3] * s[3];
+    v3 L = o - c;
+    const float a = 1;
+    float b = 2 * dot(d, L);
+    float cc = dot(L, L) - r2;
+    float delta = b * b - 4 * a * cc;
+    if (delta < 0)
+        return false;
+    const float a2 = 2 * a;
+    if (delta == 0.0f)
+        h.t = -b / a2;
+    else {
+        float sq = sqrtf(delta);
+        float t1 = (-b - sq) / a2;
+        float t2 = (-b + sq) / a2;
+        if (t1 < t2) {
+            h.t = t1;
+            if (h.t < 0)
+                h.t = t2;
+        }
+    }
+    if (h.t < 0)
+        return false;
+    h.normal = normalize((o + d * h.t) - c);
+    h.u = 0.5f + atan2f(-h.normal.z, -h.normal.x) / (2.0f * (float)M_PI);
+    h.v = 0.5f + asinf(-h.normal.y) / (float)M_PI;
+    h.tangent = cross(mk(0, 1, 0), h.normal);
+    h.mat = mat;
+    return true;
+}
+
+// Plane::intersect, analyticShape.cpp:64-76
+__device__ __forceinline__ bool plane_test(const float* p, int mat, v3 o, v3 d, Rec& h)
+{
+    v3 n = mk(p[3], p[4], p[5]);
+    float t = dot(mk(p[0], p[1], p[2]) - o, n) / dot(d, n);
+    if (t < 0)
+        return false;
+    h.t = t;
+    h.mat = mat;
+    h.normal = n;
+    return true;
+}
+
+// Image::offset clamp + texel (image.h:122-134)
+__device__ __forceinline__ float4 texel(const KTex& T, int x, int y)
+{
+    int px = x;
+    if (px < 0) px = 0;
+    if (px > T.w - 1) px = T.w - 1;
+    int py = y;
+    if (py < 0) py = 0;
+    if (py > T.h - 1) py = T.h - 1;
+    return T.px[(unsigned)(py * T.w + px)];
+}
+
+// Image::texture_floor -> sample_floor, image.h:79-86, 94-97
+__device__ __forceinline__ c3 tex_floor(const KTex& T, float x, float y)
+{
+    float u = floorf(x * T.w);
+    float v = floorf(y * T.h);
+    float4 p = texel(T, f2i(u), f2i(v));
+    return col(p.x, p.y, p.z);
+}
+
+// Image::texture_bilinear -> sample_bilinear, image.h:66-77, 89-92
+__device__ __forceinline__ c3 tex_bilinear(const KTex& T, float xx, float yy)
+{
+    float x = xx * T.w, y = yy * T.h;
+    float u = x - floorf(x);
+    float v = y - floorf(y);
+    int ix = f2i(x), iy = f2i(y);
+    float4 p00 = texel(T, ix, iy), p10 = texel(T, ix + 1, iy), p01 = texel(T, ix, iy + 1), p11 = texel(T, ix + 1, iy + 1);
+    float w00 = (1 - u) * (1 - v), w10 = u * (1 - v), w01 = (1 - u) * v, w11 = u * v;
+    return col(p00.x * w00 + p10.x * w10 + p01.x * w01 + p11.x * w11,
+               p00.y * w00 + p10.y * w10 + p01.y * w01 + p11.y * w11,
+               p00.z * w00 + p10.z * w10 + p01.z * w01 + p11.z * w11);
+}
+
+// Skybox::sample, skybox.cpp:12-51
+__device__ c3 skybox_sample(const KParams& P, v3 dir)
+{
+    v3 d2 = mk(dir.x, dir.y, -dir.z);
+    v3 da = mk(fabsf(d2.x), fabsf(d2.y), fabsf(d2.z));
+    int face;
+    float nf, u, v;
+    if (da.z >= da.x && da.z >= da.y) {
+        face = d2.z < 0.0f ? 4 : 5;
+        nf = (float)(0.5 / (double)da.z);
+        u = d2.z < 0.0f ? -d2.x : d2.x;
+        v = -d2.y;
+    } else if (da.y >= da.x) {
+        face = d2.y < 0.0f ? 3 : 2;
+        nf = (float)(0.5 / (double)da.y);
+        u = d2.x;
+        v = d2.y < 0.0f ? -d2.z : d2.z;
+    } else {
+        face = d2.x < 0.0f ? 1 : 0;
+        nf = (float)(0.5 / (double)da.x);
+        u = d2.x < 0.0f ? d2.z : -d2.z;
+        v = -d2.y;
+    }
+    u = (float)((double)(u * nf) + 0.5);
+    v = (float)((double)(v * nf) + 0.5);
+    return tex_bilinear(P.sky[face], u, v);
+}
+
+__device__ __forceinline__ const float* mat_of(const KParams& P, int id) { return P.mats + (size_t)MAT_STRIDE * id; }
+__device__ __forceinline__ c3 mat_col(const float* m, int off) { return col(m[off], m[off + 1], m[off + 2]); }
+
+// Triangle::interpolate_texcoords (triangle.cpp:155-160) / get_tex_coords (renderer.cpp:436-445)
+__device__ __forceinline__ void get_tex_coords(const KParams& P, int tri, float u, float v, float& tu, float& tv)
+{
+    if (tri >= 0) {
+        float u0 = -1, u1 = -1, u2 = -1, v0 = -1, v1 = -1, v2 = -1;
+        if (P.tri_uv) {
+            const float* uv = P.tri_uv + 6 * (size_t)tri;
+            u0 = uv[0]; u1 = uv[1]; u2 = uv[2];
+            v0 = uv[3]; v1 = uv[4]; v2 = uv[5];
+        }
+        tu = (1 - u - v) * u0 + u * u1 + v * u2;
+        tv = (1 - u - v) * v0 + u * v1 + v * v2;
+    } else {
+        tu = u;
+        tv = v;
+    }
+}
+
+// renderer.cpp:464-478
+__device__ v3 normal_mapping(const KParams& P, const Rec& h, float u, float v)
+{
+    float tu, tv;
+    get_tex_coords(P, h.tri, u, v, tu, tv);
+    v3 T = h.tangent;
+    v3 B = cross(T, h.normal);
+    v3 N = h.normal;
+    c3 nc = tex_floor(P.tex[TEX_NORMAL], tu, tv);
+    v3 nm = mk(nc.r, nc.g, nc.b) * 2.0f - mk(1, 1, 1);
+    v3 q = normalize(nm);
+    v3 p = mk(T.x * q.x + B.x * q.y + N.x * q.z, T.y * q.x + B.y * q.y + N.y * q.z, T.z * q.x + B.z * q.y + N.z * q.z);
+    return normalize(p);
+}
+
+// renderer.cpp:518-554
+__device__ void parallax_occlusion_mapping(const KParams& P, int tri, float u, float v, v3 view, float& nu, float& nv)
+{
+    float tu, tv;
+    get_tex_coords(P, tri, u, v, tu, tv);
+    const KTex& D = P.tex[TEX_DISPLACEMENT];
+    int steps = P.parallax_mapping_steps;
+    float current_depth;
+    float depth_step = 1.0f / steps;
+    float sampled = tex_floor(D, tu, tv).r;
+    v3 search = -view * P.displacement_mapping_strength;
+    float du = search.x / steps;
+    float dv = search.y / steps;
+    current_depth = 0.0f;
+    float u2 = tu, v2 = tv;
+    while (current_depth < sampled) {
+        u2 += du;
+        v2 += dv;
+        sampled = tex_floor(D, u2, v2).r;
+        current_depth += depth_step;
+    }
+    float pu = u2 - du, pv = v2 - dv;
+    float after = sampled - current_depth;
+    float before = tex_floor(D, pu, pv).r - (current_depth - depth_step);
+    float w = after / (after - before);
+    nu = (1 - w) * u2 + w * pu;
+    nv = (1 - w) * v2 + w * pv;
+}
+
+// renderer.cpp:340-402
+__device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
+{
+    if (!P.compute_shadows)
+        return false;
+    v3 o = p + n * 1.0e-4f;
+    v3 d = normalize(lp - p);
+    TRay R = make_ray(P, o, d);
+    THit h;
+    bool r;
+    if (P.enable_bvh) {
+        r = bvh_closest(P, R, h, lv);
+        if (r) {
+            v3 q = o + d * h.t;
+            if (length2(p - q) < length2(p - lp))
+                return true;
+        }
+    } else {
+        h.t = -1.0f;
+        for (int k = 0; k < P.ntri_slots; k++) {
+            float t, u, v;
+            if (tri_test(P.tris, (uint32_t)k, R, t, u, v)) {
+                h.t = t;
+                v3 q = o + d * h.t;
+                if (length2(p - q) < length2(p - lp))
+                    return true;
+            }
+        }
+    }
+    if (P.nshape > 0) {
+        Rec hi = rec_fresh();
+        hi.t = h.t;
+        for (int k = 0; k < P.nshape; k++) {
+            bool hk = P.shape_kind[k] == 0 ? sphere_test(P.shape[k], P.shape_mat[k], o, d, hi)
+                                           : plane_test(P.shape[k], P.shape_mat[k], o, d, hi);
+            if (hk) {
+                v3 q = o + d * hi.t;
+                if (length2(p - q) < length2(p - lp))
+                    return true;
+            }
+        }
+    }
+    return false;
+}
+
+// BACKGROUND_COLOR, renderer.cpp:19
+__device__ __forceinline__ c3 background() { return col(135.0f / 255.0f, 206.0f / 255.0f, 235.0f / 255.0f); }
+
+// Closest hit over the BVH then the analytic shapes (renderer.cpp:1015-1037).
+// fin is the caller's HitInfo; returns the source (-1 none, >=0 triangle, -2-k shape k).
+__device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv)
+{
+    Rec local = rec_fresh();
+    TRay R = make_ray(P, o, d);
+    int src = -1;
+    if (P.enable_bvh) {
+        THit h;
+        bool r = bvh_closest(P, R, h, lv);
+        if (h.k >= 0)
+            local = tri_record(P, h);
+        else if (h.t != h.t)
+            local.t = h.t;   // NaN ray: stale NaN record
+        if (r && (local.t < fin.t || fin.t == -1)) {
+            fin = local;
+            src = local.tri;
+        }
+    } else {
+        // brute-force loop, renderer.cpp:1021-1027: fin takes every hit nearer
+        // than itself; local keeps the last triangle that was hit.
+        THit best, last;
+        best.k = -1;
+        last.k = -1;
+        float bt = fin.t;
+        for (int k = 0; k < P.ntri_slots; k++) {
+            float t, u, v;
+            if (tri_test(P.tris, (uint32_t)k, R, t, u, v)) {
+                last.t = t; last.u = u; last.v = v; last.k = k;
+                if (t < bt || bt == -1) {
+                    bt = t;
+                    best = last;
+                }
+            }
+        }
+        if (best.k >= 0) {
+            fin = tri_record(P, best);
+            src = fin.tri;
+        }
+        if (last.k >= 0)
+            local = tri_record(P, last);
+    }
+    for (int k = 0; k < P.nshape; k++) {
+        bool hk = P.shape_kind[k] == 0 ? sphere_test(P.shape[k], P.shape_mat[k], o, d, local)
+                                       : plane_test(P.shape[k], P.shape_mat[k], o, d, local);
+        if (hk && (local.t < fin.t || fin.t == -1)) {
+            fin = local;
+            src = -2 - k;
+        }
+    }
+    return src;
+}
+
+// shade_ray_inter_point (renderer.cpp:556-617) without the reflection term,
+// which the caller adds (reflection > 0 is handled by the recursive path).
+// Returns the colour before the final clamp; *partial receives the pieces the
+// reflection path needs.
+struct ShadeOut {
+    c3 color;      // clamped colour when no reflection is involved
+    c3 pre_refl;   // fc before "+ reflection", after emission
+    bool shadowed;
+    v3 ip;
+};
+
+__device__ ShadeOut shade(const KParams& P, v3 ro, v3 rd, Rec& h, uint2* lv)
+{
+    ShadeOut out;
+    out.shadowed = false;
+    c3 fc = col(0.0f, 0.0f, 0.0f);
+    out.ip = mk(0, 0, 0);
+    if (P.shading_method == RT_SHADING) {
+        float u = h.u, v = h.v;
+        v3 ip = ro + rd * h.t;
+        out.ip = ip;
+        v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+        v3 light = mk(P.light[0], P.light[1], P.light[2]);
+        if (P.enable_displacement_mapping)
+            parallax_occlusion_mapping(P, h.tri, h.u, h.v, normalize(cam - ip), u, v);
+        v3 dl = normalize(light - ip);
+        if (P.enable_normal_mapping)
+            h.normal = normal_mapping(P, h, u, v);
+        const float* m = mat_of(P, h.mat);
+        float ao = 1.0f;
+        if (P.enable_ao_mapping) {
+            float tu, tv;
+            get_tex_coords(P, h.tri, u, v, tu, tv);
+            ao = tex_floor(P.tex[TEX_AO], tu, tv).r;
+        }
+        c3 dc;
+        if (P.enable_diffuse_mapping) {
+            float tu, tv;
+            get_tex_coords(P, h.tri, u, v, tu, tv);
+            dc = tex_floor(P.tex[TEX_DIFFUSE], tu, tv);
+            float f = smax(0.5f, dot(h.normal, normalize(cam - ip)));
+            dc = dc * col(f, f, f);
+        } else {
+            float f = smax(0.0f, dot(h.normal, dl));   // compute_diffuse, :263-266
+            dc = mat_col(m, 3) * col(f, f, f);
+        }
+        fc = fc + (dc * ao) * (float)(P.enable_diffuse != 0);
+        c3 spec;   // compute_specular, :270-280
+        {
+            v3 hv = normalize(dl - rd);
+            float angle = dot(hv, h.normal);
+            if (angle <= m[15])
+                spec = col(0, 0, 0);
+            else {
+                float pw = powf(smax(0.0f, angle), m[14]);
+                spec = mat_col(m, 6) * col(pw, pw, pw);
+            }
+        }
+        fc = fc + spec * (float)(P.enable_specular != 0);
+        bool sh = is_shadowed(P, ip, h.normal, light, lv);
+        out.shadowed = sh;
+        if (sh)
+            fc = fc * col(0.5f, 0.5f, 0.5f);
+        fc = fc + mat_col(m, 9) * (float)(P.enable_emissive != 0);
+        out.pre_refl = fc;
+        float refl = m[12];
+        fc = fc + (col(0.1f, 0.1f, 0.1f) * mat_col(m, 0)) * (1 - refl) * (float)(P.enable_ambient != 0);
+    } else if (P.shading_method == ABS_NORMALS) {
+        fc = col(fabsf(h.normal.x), fabsf(h.normal.y), fabsf(h.normal.z));
+    } else if (P.shading_method == PASTEL_NORMALS) {
+        fc = (col(h.normal.x, h.normal.y, h.normal.z) + col(1.0f, 1.0f, 1.0f)) * 0.5f;
+    } else if (P.shading_method == BARYCENTRIC) {
+        fc = (col(1, 0, 0) * h.u + col(0, 1.0f, 0) * h.v) + col(0, 0, 1) * (1 - h.u - h.v);
+    } else if (P.shading_method == VISUALIZE_AO) {
+        c3 c = col(0.9f, 0.9f, 0.9f);
+        if (P.enable_ao_mapping) {
+            float tu, tv;
+            get_tex_coords(P, h.tri, h.u, h.v, tu, tv);
+            float a = tex_floor(P.tex[TEX_AO], tu, tv).r;
+            c = c * col(a, a, a);
+        }
+        fc = c;
+    }
+    out.color = col(clamp01(fc.r), clamp01(fc.g), clamp01(fc.b));
+    return out;
+}
+
+// trace_ray miss colour (renderer.cpp:1052-1065)
+__device__ c3 miss_color(const KParams& P, v3 d)
+{
+    if (P.enable_skysphere) {
+        float u = (float)(0.5 + (double)atan2f(-d.z, -d.x) / (2 * M_PI));
+        float v = (float)(0.5 + (double)asinf(-d.y) / M_PI);
+        return tex_floor(P.tex[TEX_SKYSPHERE], u, v);
+    } else if (P.enable_skybox)
+        return skybox_sample(P, d);
+    return background();
+}
+
+// Global internal row of a launch-local row (interleaved bands across ranks).
+__device__ __forceinline__ int global_row(const KParams& P, int lr)
+{
+    int band = lr / P.band_rows;
+    return (band * P.nranks + P.rank) * P.band_rows + (lr - band * P.band_rows);
+}
+
+// XCD-aware tile order: blocks b and b+8 share an XCD, so give every XCD a
+// contiguous run of tiles (neighbouring tiles share octree nodes in its L2).
+__device__ __forceinline__ int swizzled_block()
+{
+    int nb = gridDim.x;
+    int b = blockIdx.x;
+    if (nb % 8 != 0)
+        return b;
+    return (b % 8) * (nb / 8) + (b / 8);
+}
+
+// Renderer::ray_trace (renderer.cpp:1068-1116) for primary + shadow rays with
+// RT/debug shading, no reflections.
+__global__ __launch_bounds__(BLOCK) void ray_trace_kernel(KParams P)
+{
+    extern __shared__ uint2 lds_levels[];
+    uint2* lv = lds_levels + threadIdx.x;
+    int wave = threadIdx.x >> 6;
+    int lane = threadIdx.x & 63;
+    int tile = swizzled_block() * WAVES_PER_BLOCK + wave;
+    if (tile >= P.tiles_x * P.tiles_y)
+        return;
+    int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+    int px = tx * 8 + (lane & 7);
+    int lr = ty * 8 + (lane >> 3);
+    if (px >= P.rw || lr >= P.local_rows)
+        return;
+    int py = global_row(P, lr);
+    if (py >= P.rh)
+        return;
+
+    // ray generation, renderer.cpp:1086-1098
+    float y_world = ((float)py + 0.5f) / P.rh * 2 - 1;
+    float x_world = ((float)px + 0.5f) / P.rw * 2 - 1;
+    v3 vs = xform_point(P.proj_inv, mk(x_world, y_world, -1));
+    v3 ws = xform_point(P.cam_to_world, vs);
+    v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+    v3 rd = normalize(ws - cam);
+
+    Rec fin = rec_fresh();
+    int src = closest_hit(P, cam, rd, fin, lv);
+    c3 c;
+    bool found = false, shadowed = false;
+    float min_t = 0.1f;
+    if (fin.t > min_t) {
+        found = true;
+        ShadeOut s = shade(P, cam, rd, fin, lv);
+        shadowed = s.shadowed;
+        c = s.color;
+        if (P.counters && P.compute_shadows && P.shading_method == RT_SHADING)
+            atomicAdd(&P.counters[0], 1ull);
+    } else
+        c = miss_color(P, rd);
+
+    size_t o = (size_t)lr * P.rw + px;
+    if (P.argb) P.argb[o] = color_to_argb(c);
+    if (P.rgba) P.rgba[o] = make_float4(c.r, c.g, c.b, 1.0f);
+    if (P.hit_id) P.hit_id[o] = found ? src : -1;
+    if (P.hit_t) P.hit_t[o] = fin.t;
+    if (P.shadow) P.shadow[o] = (uint8_t)(found && shadowed);
+}
+
+// ImageUtils::downscale_image_qt_ARGB32 (imageUtils.h:98-147): integer box
+// filter of 8-bit channels, truncating division.
+__global__ __launch_bounds__(256) void downscale_kernel(const uint32_t* __restrict__ in, int w, int h_rows, int f,
+                                                        uint32_t* __restrict__ out)
+{
+    int dw = w / f, dh = h_rows / f;
+    int x = blockIdx.x * blockDim.x + threadIdx.x;
+    int y = blockIdx.y;
+    if (x >= dw || y >= dh)
+        return;
+    int ar = 0, ag = 0, ab = 0;
+    for (int i = 0; i < f; i++)
+        for (int j = 0; j < f; j++) {
+            uint32_t p = in[(size_t)(y * f + i) * w + (x * f + j)];
+            ar += (p >> 16) & 0xff;
+            ag += (p >> 8) & 0xff;
+            ab += p & 0xff;
+        }
+    out[(size_t)y * dw + x] = qrgb(ar / (f * f), ag / (f * f), ab / (f * f));
+}
+
+}  // namespace rt
+
+// ---- host-side launch wrappers (called from renderer.cpp) ----
+extern "C" hipError_t rt_launch_ray_trace(const rt::KParams* P, hipStream_t stream)
+{
+    int tiles = P->tiles_x * P->tiles_y;
+    int blocks = (tiles + rt::WAVES_PER_BLOCK - 1) / rt::WAVES_PER_BLOCK;
+    size_t lds = (size_t)(P->levels > 0 ? P->levels : 1) * rt::BLOCK * sizeof(uint2);
+    hipLaunchKernelGGL(rt::ray_trace_kernel, dim3(blocks), dim3(rt::BLOCK), lds, stream, *P);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rt_launch_downscale(const uint32_t* in, int w, int h_rows, int f, uint32_t* out,
+                                          hipStream_t stream)
+{
+    int dw = w / f, dh = h_rows / f;
+    if (dw <= 0 || dh <= 0)
+        return hipSuccess;
+    dim3 grid((dw + 255) / 256, dh);
+    hipLaunchKernelGGL(rt::downscale_kernel, grid, dim3(256), 0, stream, in, w, h_rows, f, out);
+    return hipGetLastError();
+}

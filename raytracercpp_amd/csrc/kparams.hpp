@@ -1,0 +1,80 @@
+// kparams.hpp -- plain-old-data launch parameters shared by the host library
+// and the kernels (passed by value as the kernel argument).
+#pragma once
+
+#include <stdint.h>
+
+#include "octree.hpp"
+
+namespace rt {
+
+constexpr int TEX_SLOTS = 6;   // ao, diffuse, normal, displacement, roughness, skysphere (renderer.h:77-84)
+constexpr int MAT_STRIDE = 16; // see include/rt_mi355x.h
+constexpr int MAX_SHAPES = 64;
+
+enum TexSlot { TEX_AO = 0, TEX_DIFFUSE = 1, TEX_NORMAL = 2, TEX_DISPLACEMENT = 3, TEX_ROUGHNESS = 4, TEX_SKYSPHERE = 5 };
+enum Shading { RT_SHADING = 0, ABS_NORMALS = 1, PASTEL_NORMALS = 2, BARYCENTRIC = 3, VISUALIZE_AO = 4 };
+
+struct KTex {
+    const float4* px;   // row-major texels (Image, tp2/src/image.h:20-135), nullptr when absent
+    int w, h;
+};
+
+struct KParams {
+    // geometry (flattened octree, octree.hpp)
+    const GNode* nodes;
+    const GTri* tris;
+    const int32_t* tri_id;    // GTri slot -> caller triangle index
+    const int32_t* tri_mat;   // caller index -> material
+    const float* tri_uv;      // caller index -> u0 u1 u2 v0 v1 v2 (nullptr: (-1,-1,-1))
+    int32_t nnodes;
+    int32_t ntri_slots;       // GTri count (brute-force loop bound when enable_bvh == 0)
+    int32_t levels;           // flattened tree depth + 1 (LDS level-stack entries per lane)
+    float pn[NPLANES][3];     // BVH::BoundingVolume::PLANE_NORMALS (bvh.cpp:8-16)
+
+    int32_t nshape;
+    int32_t shape_kind[MAX_SHAPES];
+    float shape[MAX_SHAPES][6];
+    int32_t shape_mat[MAX_SHAPES];
+
+    const float* mats;        // [nmat][16]
+    int32_t nmat;
+
+    float cam_pos[3];
+    float proj_inv[16];
+    float cam_to_world[16];
+    float light[3];
+
+    KTex tex[TEX_SLOTS];
+    KTex sky[6];
+
+    // RenderSettings (rendererSettings.h:6-105)
+    int32_t shading_method;
+    int32_t compute_shadows;
+    int32_t max_recursion_depth;
+    int32_t enable_bvh;
+    int32_t enable_ambient, enable_diffuse, enable_specular, enable_emissive;
+    int32_t rough_reflections_sample_count;
+    int32_t enable_ao_mapping, enable_diffuse_mapping, enable_normal_mapping, enable_displacement_mapping;
+    float displacement_mapping_strength;
+    int32_t parallax_mapping_steps;
+    int32_t enable_roughness_mapping, enable_skysphere, enable_skybox;
+    uint32_t rng_seed;
+
+    // image: render size (internal, after the SSAA factor) and this launch's rows
+    int32_t rw, rh;
+    int32_t band_rows;        // internal rows per band
+    int32_t nranks, rank;     // bands b with b % nranks == rank are rendered
+    int32_t local_rows;       // rows in this launch's (padded) local buffers
+    int32_t tiles_x, tiles_y; // 8x8 tiles over (rw, local_rows)
+
+    // outputs, indexed by local_row * rw + px (nullptr = not requested)
+    uint32_t* argb;
+    float4* rgba;
+    int32_t* hit_id;
+    float* hit_t;
+    uint8_t* shadow;
+    unsigned long long* counters;   // [0] shadow rays, [1] reflection rays
+};
+
+}  // namespace rt

@@ -1,0 +1,67 @@
+// octree.hpp -- host-side octree BVH build (the reference's algorithm, restated)
+// and its flattening into the gfx950 traversal layout.
+//
+// Build: BVH::BVH / build_bvh (tp2/projets/bvh.cpp:19-66), OctreeNode::insert /
+// insert_to_children / create_children / compute_volume (tp2/projets/bvh.h:141-210),
+// BoundingVolume (bvh.h:15-74), PLANE_NORMALS (bvh.cpp:8-16).
+//
+// Flattened layout (HBM):
+//   GNode[ ]  64 B each: 7 near + 7 far k-DOP slab distances, then
+//             a = first child (inner) or first triangle (leaf),
+//             b = LEAF_BIT | triangle count (leaf) or the 8-bit mask of
+//                 non-empty child octants (inner).
+//             The non-empty children of an inner node are contiguous, in octant
+//             order, so heap insertion order (bvh.h:251-256) is rank order.
+//             Empty leaves are dropped: their empty volume (+inf / -inf) can
+//             never pass BoundingVolume::intersect for a non-NaN ray.
+//   GTri[ ]   48 B each, leaf-contiguous: a, b - a, c - a, cross(b - a, c - a)
+//             (Triangle::_normal, triangle.cpp:11-12), plus tri_id[ ] mapping
+//             back to the caller's triangle index.
+#pragma once
+
+#include <stdint.h>
+
+#include <vector>
+
+#include "rt_math.hpp"
+
+namespace rt {
+
+constexpr int NPLANES = 7;
+constexpr uint32_t LEAF_BIT = 0x80000000u;
+
+struct alignas(16) GNode {
+    float dn[NPLANES];
+    float df[NPLANES];
+    uint32_t a;
+    uint32_t b;
+};
+static_assert(sizeof(GNode) == 64, "GNode must be 64 B");
+
+struct alignas(16) GTri {
+    float a[3];
+    float ab[3];
+    float ac[3];
+    float n[3];
+};
+static_assert(sizeof(GTri) == 48, "GTri must be 48 B");
+
+// PLANE_NORMALS (bvh.cpp:8-16), in float, with the reference's expressions.
+void plane_normals(v3 out[NPLANES]);
+
+struct OctreeStats {
+    int64_t inner = 0, leaves = 0, empty_leaves = 0, max_leaf = 0, max_depth = 0, nodes = 0;
+};
+
+struct FlatOctree {
+    std::vector<GNode> nodes;      // nodes[0] = root (empty when there are no triangles)
+    std::vector<GTri> tris;        // leaf-contiguous
+    std::vector<int32_t> tri_id;   // GTri slot -> caller triangle index
+    int levels = 0;                // max depth + 1 of the flattened tree
+    OctreeStats stats;             // of the unflattened (reference) tree
+};
+
+// Builds the reference octree over tri9 ([n][9] world-space vertices) and flattens it.
+void build_flat_octree(const float* tri9, int64_t n, int max_depth, int leaf_max_obj_count, FlatOctree& out);
+
+}  // namespace rt

@@ -1,0 +1,721 @@
+// renderer.cpp -- rt::Renderer (see renderer.hpp).
+#include "renderer.hpp"
+
+#include <chrono>
+#include <cmath>
+#include <cstring>
+
+#include "host_scene.hpp"
+
+extern "C" hipError_t rt_launch_ray_trace(const rt::KParams* P, hipStream_t stream);
+extern "C" hipError_t rt_launch_downscale(const uint32_t* in, int w, int h_rows, int f, uint32_t* out,
+                                          hipStream_t stream);
+
+namespace rt {
+
+DevBuf::~DevBuf() { release(); }
+
+void DevBuf::release()
+{
+    if (p) {
+        hipSetDevice(device);
+        (void)hipFree(p);
+    }
+    p = nullptr;
+    bytes = 0;
+}
+
+hipError_t DevBuf::reserve(size_t n)
+{
+    if (n <= bytes && p)
+        return hipSuccess;
+    release();
+    if (n == 0)
+        n = 16;
+    hipError_t e = hipMalloc(&p, n);
+    if (e != hipSuccess) {
+        p = nullptr;
+        return e;
+    }
+    bytes = n;
+    return hipSuccess;
+}
+
+Renderer::Renderer(int device) : device_(device)
+{
+    rt_default_settings(&s_);
+    mat::identity(c2w_);
+    mat::identity(w2c_);
+    mat::identity(prev_object_);
+    int rw, rh;
+    render_size(rw, rh);
+    img_w_ = rw;
+    img_h_ = rh;
+    aspect_ = (float)rw / rh;   // Renderer ctor: _camera.set_aspect_ratio(render_w / render_h), renderer.cpp:93
+    update_camera_projection();
+}
+
+int Renderer::init(std::string& err)
+{
+    hipError_t e = hipSetDevice(device_);
+    if (e == hipSuccess)
+        e = hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking);
+    for (int i = 0; i < 4 && e == hipSuccess; i++)
+        e = hipEventCreate(&ev_[i]);
+    if (e != hipSuccess) {
+        err = std::string("HIP init failed: ") + hipGetErrorString(e);
+        return RT_EHIP;
+    }
+    DevBuf* all[] = {&d_nodes_, &d_tris_, &d_tri_id_, &d_tri_mat_, &d_tri_uv_, &d_mats_, &d_internal_, &d_image_,
+                     &d_rgba_, &d_hit_id_, &d_hit_t_, &d_shadow_, &d_counters_, &d_band_tmp_};
+    for (DevBuf* b : all) b->device = device_;
+    for (auto& b : d_tex_) b.device = device_;
+    for (auto& b : d_sky_) b.device = device_;
+    return RT_OK;
+}
+
+Renderer::~Renderer()
+{
+    hipSetDevice(device_);
+    for (auto& e : ev_)
+        if (e) hipEventDestroy(e);
+    if (stream_) hipStreamDestroy(stream_);
+}
+
+int Renderer::fail(int code, const std::string& msg)
+{
+    err_ = msg;
+    return code;
+}
+
+int Renderer::hip_fail(hipError_t e, const char* what)
+{
+    err_ = std::string(what) + ": " + hipGetErrorString(e);
+    return RT_EHIP;
+}
+
+// Renderer::get_render_width_height, renderer.cpp:116-120
+void Renderer::render_size(int& w, int& h) const
+{
+    w = s_.enable_ssaa ? s_.image_width * s_.ssaa_factor : s_.image_width;
+    h = s_.enable_ssaa ? s_.image_height * s_.ssaa_factor : s_.image_height;
+}
+
+// Camera::set_aspect_ratio / set_fov (camera.cpp:5-19)
+void Renderer::update_camera_projection()
+{
+    mat::perspective(fov_, aspect_, near_, far_, proj_);
+    mat::inverse(proj_, proj_inv_);
+}
+
+int Renderer::set_settings(const rt_settings& s)
+{
+    if (s.hybrid_rasterization_tracing)
+        return fail(RT_EUNSUPPORTED, "hybrid_rasterization_tracing: the raster path is out of scope");
+    if (s.enable_ssao)
+        return fail(RT_EUNSUPPORTED, "enable_ssao: SSAO post-processing is out of scope (stubbed)");
+    if (s.image_width <= 0 || s.image_height <= 0 || (s.enable_ssaa && s.ssaa_factor <= 0))
+        return fail(RT_EINVAL, "invalid image size / ssaa_factor");
+    if (s.bvh_max_depth > 30)
+        return fail(RT_EUNSUPPORTED, "bvh_max_depth > 30");
+    bool bvh_changed = s.enable_bvh != s_.enable_bvh || s.bvh_max_depth != s_.bvh_max_depth ||
+                       s.bvh_leaf_object_count != s_.bvh_leaf_object_count;
+    s_ = s;
+    if (bvh_changed)
+        geom_dirty_ = true;
+    return RT_OK;
+}
+
+// renderer.cpp:250-261
+int Renderer::change_render_size(int w, int h)
+{
+    if (w <= 0 || h <= 0)
+        return fail(RT_EINVAL, "invalid render size");
+    s_.image_width = w;
+    s_.image_height = h;
+    int rw, rh;
+    render_size(rw, rh);
+    img_w_ = rw;
+    img_h_ = rh;
+    rendered_ = false;
+    aspect_ = (float)rw / rh;
+    update_camera_projection();
+    return RT_OK;
+}
+
+// renderer.cpp:137-144
+int Renderer::set_triangles(const float* tri9, const int32_t* mat, const float* uv6, int64_t n)
+{
+    if (n < 0 || (n > 0 && (!tri9 || !mat)))
+        return fail(RT_EINVAL, "set_triangles: null arrays");
+    if (n >= (int64_t)1 << 30)
+        return fail(RT_EUNSUPPORTED, "set_triangles: more than 2^30 triangles");
+    tri_.assign(tri9, tri9 + 9 * n);
+    tri_mat_.assign(mat, mat + n);
+    if (uv6)
+        tri_uv_.assign(uv6, uv6 + 6 * n);
+    else
+        tri_uv_.clear();
+    has_bvh_ = s_.enable_bvh;
+    geom_dirty_ = true;
+    return RT_OK;
+}
+
+int Renderer::add_sphere(float cx, float cy, float cz, float r, int mat)
+{
+    if ((int)shape_kind_.size() >= MAX_SHAPES)
+        return fail(RT_EUNSUPPORTED, "too many analytic shapes");
+    shape_kind_.push_back(0);
+    float p[6] = {cx, cy, cz, r, 0, 0};
+    shape_.insert(shape_.end(), p, p + 6);
+    shape_mat_.push_back(mat);
+    return RT_OK;
+}
+
+int Renderer::add_plane(float px, float py, float pz, float nx, float ny, float nz, int mat)
+{
+    if ((int)shape_kind_.size() >= MAX_SHAPES)
+        return fail(RT_EUNSUPPORTED, "too many analytic shapes");
+    shape_kind_.push_back(1);
+    float p[6] = {px, py, pz, nx, ny, nz};
+    shape_.insert(shape_.end(), p, p + 6);
+    shape_mat_.push_back(mat);
+    return RT_OK;
+}
+
+// renderer.cpp:182-186
+int Renderer::clear_geometry()
+{
+    tri_.clear();
+    tri_mat_.clear();
+    tri_uv_.clear();
+    shape_kind_.clear();
+    shape_.clear();
+    shape_mat_.clear();
+    geom_dirty_ = true;
+    return RT_OK;
+}
+
+int Renderer::set_materials(const float* mats16, int n)
+{
+    if (n < 0 || (n > 0 && !mats16))
+        return fail(RT_EINVAL, "set_materials: null array");
+    mats_.assign(mats16, mats16 + (size_t)MAT_STRIDE * n);
+    mats_dirty_ = true;
+    return RT_OK;
+}
+
+int Renderer::change_camera_fov(float fov)
+{
+    fov_ = fov;
+    update_camera_projection();
+    return RT_OK;
+}
+
+int Renderer::change_camera_aspect_ratio(float aspect)
+{
+    aspect_ = aspect;
+    update_camera_projection();
+    return RT_OK;
+}
+
+int Renderer::set_light_position(float x, float y, float z)
+{
+    light_[0] = x;
+    light_[1] = y;
+    light_[2] = z;
+    return RT_OK;
+}
+
+// renderer.cpp:226-233
+int Renderer::set_camera_transform(const float m[16])
+{
+    std::memcpy(c2w_, m, sizeof(c2w_));
+    mat::inverse(c2w_, w2c_);
+    v3 p = xform_point(c2w_, mk(0, 0, 0));
+    cam_pos_[0] = p.x;
+    cam_pos_[1] = p.y;
+    cam_pos_[2] = p.z;
+    return RT_OK;
+}
+
+// renderer.cpp:235-241
+int Renderer::apply_transformation_to_camera(const float m[16])
+{
+    mat::compose(m, c2w_, c2w_);
+    mat::inverse(c2w_, w2c_);
+    v3 p = xform_point(m, mk(cam_pos_[0], cam_pos_[1], cam_pos_[2]));
+    cam_pos_[0] = p.x;
+    cam_pos_[1] = p.y;
+    cam_pos_[2] = p.z;
+    return RT_OK;
+}
+
+int Renderer::set_camera_matrices(const float pos[3], const float proj_inv[16], const float c2w[16])
+{
+    std::memcpy(cam_pos_, pos, sizeof(cam_pos_));
+    std::memcpy(proj_inv_, proj_inv, sizeof(proj_inv_));
+    std::memcpy(c2w_, c2w, sizeof(c2w_));
+    mat::inverse(c2w_, w2c_);
+    return RT_OK;
+}
+
+void Renderer::get_camera_matrices(float pos[3], float proj_inv[16], float c2w[16]) const
+{
+    std::memcpy(pos, cam_pos_, sizeof(cam_pos_));
+    std::memcpy(proj_inv, proj_inv_, sizeof(proj_inv_));
+    std::memcpy(c2w, c2w_, sizeof(c2w_));
+}
+
+// renderer.cpp:214-224: every triangle goes through object_transform * previous^-1,
+// then the BVH is rebuilt.
+int Renderer::set_object_transform(const float m[16])
+{
+    float inv[16], t[16];
+    mat::inverse(prev_object_, inv);
+    std::memcpy(prev_object_, inv, sizeof(inv));
+    mat::compose(m, prev_object_, t);
+    size_t n = tri_.size() / 3;
+    std::vector<float> out(tri_.size());
+    mat::transform_points(t, tri_.data(), (int64_t)n, out.data());
+    tri_.swap(out);
+    has_bvh_ = true;
+    geom_dirty_ = true;
+    std::memcpy(prev_object_, m, sizeof(prev_object_));
+    return RT_OK;
+}
+
+int Renderer::reset_previous_transform()
+{
+    mat::identity(prev_object_);
+    return RT_OK;
+}
+
+int Renderer::set_texture(int slot, int w, int h, const float* rgba)
+{
+    if (slot < 0 || slot >= TEX_SLOTS)
+        return fail(RT_EINVAL, "set_texture: bad slot");
+    if (!rgba) {
+        tex_[slot] = HostTex();
+    } else {
+        if (w <= 0 || h <= 0)
+            return fail(RT_EINVAL, "set_texture: bad size");
+        tex_[slot].w = w;
+        tex_[slot].h = h;
+        tex_[slot].rgba.assign(rgba, rgba + (size_t)w * h * 4);
+    }
+    tex_dirty_ = true;
+    return RT_OK;
+}
+
+int Renderer::set_skybox(const int32_t w[6], const int32_t h[6], const float* const faces[6])
+{
+    for (int i = 0; i < 6; i++) {
+        if (!faces || !faces[i]) {
+            sky_[i] = HostTex();
+            continue;
+        }
+        if (w[i] <= 0 || h[i] <= 0)
+            return fail(RT_EINVAL, "set_skybox: bad face size");
+        sky_[i].w = w[i];
+        sky_[i].h = h[i];
+        sky_[i].rgba.assign(faces[i], faces[i] + (size_t)w[i] * h[i] * 4);
+    }
+    tex_dirty_ = true;
+    return RT_OK;
+}
+
+int Renderer::reconstruct_bvh_new()
+{
+    has_bvh_ = true;
+    geom_dirty_ = true;
+    return RT_OK;
+}
+
+int Renderer::destroy_bvh()
+{
+    has_bvh_ = false;
+    geom_dirty_ = true;
+    return RT_OK;
+}
+
+int Renderer::ensure_device_scene()
+{
+    hipError_t e = hipSetDevice(device_);
+    if (e != hipSuccess)
+        return hip_fail(e, "hipSetDevice");
+    if (geom_dirty_) {
+        auto t0 = std::chrono::steady_clock::now();
+        int64_t n = (int64_t)tri_mat_.size();
+        if (s_.enable_bvh) {
+            build_flat_octree(tri_.data(), n, s_.bvh_max_depth, s_.bvh_leaf_object_count, oct_);
+            if (oct_.levels > 31)
+                return fail(RT_EUNSUPPORTED, "octree deeper than 31 levels");
+        } else {
+            // brute-force mode (renderer.cpp:1021-1027): triangles in caller order, no nodes
+            oct_ = FlatOctree();
+            oct_.tris.resize((size_t)n);
+            oct_.tri_id.resize((size_t)n);
+            for (int64_t i = 0; i < n; i++) {
+                const float* p = tri_.data() + 9 * i;
+                v3 a = mk(p[0], p[1], p[2]), b = mk(p[3], p[4], p[5]), c = mk(p[6], p[7], p[8]);
+                v3 ab = b - a, ac = c - a, nn = cross(b - a, c - a);
+                GTri& g = oct_.tris[(size_t)i];
+                g.a[0] = a.x; g.a[1] = a.y; g.a[2] = a.z;
+                g.ab[0] = ab.x; g.ab[1] = ab.y; g.ab[2] = ab.z;
+                g.ac[0] = ac.x; g.ac[1] = ac.y; g.ac[2] = ac.z;
+                g.n[0] = nn.x; g.n[1] = nn.y; g.n[2] = nn.z;
+                oct_.tri_id[(size_t)i] = (int32_t)i;
+            }
+        }
+        size_t nb = oct_.nodes.size() * sizeof(GNode), tb = oct_.tris.size() * sizeof(GTri);
+        if ((e = d_nodes_.reserve(nb)) != hipSuccess || (e = d_tris_.reserve(tb)) != hipSuccess ||
+            (e = d_tri_id_.reserve(oct_.tri_id.size() * 4)) != hipSuccess ||
+            (e = d_tri_mat_.reserve(tri_mat_.size() * 4)) != hipSuccess ||
+            (e = d_tri_uv_.reserve(tri_uv_.size() * 4)) != hipSuccess)
+            return hip_fail(e, "hipMalloc (scene)");
+        if (nb) e = hipMemcpyAsync(d_nodes_.p, oct_.nodes.data(), nb, hipMemcpyHostToDevice, stream_);
+        if (e == hipSuccess && tb) e = hipMemcpyAsync(d_tris_.p, oct_.tris.data(), tb, hipMemcpyHostToDevice, stream_);
+        if (e == hipSuccess && !oct_.tri_id.empty())
+            e = hipMemcpyAsync(d_tri_id_.p, oct_.tri_id.data(), oct_.tri_id.size() * 4, hipMemcpyHostToDevice, stream_);
+        if (e == hipSuccess && !tri_mat_.empty())
+            e = hipMemcpyAsync(d_tri_mat_.p, tri_mat_.data(), tri_mat_.size() * 4, hipMemcpyHostToDevice, stream_);
+        if (e == hipSuccess && !tri_uv_.empty())
+            e = hipMemcpyAsync(d_tri_uv_.p, tri_uv_.data(), tri_uv_.size() * 4, hipMemcpyHostToDevice, stream_);
+        if (e == hipSuccess)
+            e = hipStreamSynchronize(stream_);
+        if (e != hipSuccess)
+            return hip_fail(e, "upload (scene)");
+        geom_dirty_ = false;
+        build_ms_ = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    if (mats_dirty_) {
+        if ((e = d_mats_.reserve(mats_.size() * 4)) != hipSuccess)
+            return hip_fail(e, "hipMalloc (materials)");
+        if (!mats_.empty() &&
+            (e = hipMemcpy(d_mats_.p, mats_.data(), mats_.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
+            return hip_fail(e, "upload (materials)");
+        mats_dirty_ = false;
+    }
+    if (tex_dirty_) {
+        for (int i = 0; i < TEX_SLOTS + 6; i++) {
+            HostTex& t = i < TEX_SLOTS ? tex_[i] : sky_[i - TEX_SLOTS];
+            DevBuf& d = i < TEX_SLOTS ? d_tex_[i] : d_sky_[i - TEX_SLOTS];
+            if (t.rgba.empty())
+                continue;
+            if ((e = d.reserve(t.rgba.size() * 4)) != hipSuccess)
+                return hip_fail(e, "hipMalloc (texture)");
+            if ((e = hipMemcpy(d.p, t.rgba.data(), t.rgba.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
+                return hip_fail(e, "upload (texture)");
+        }
+        tex_dirty_ = false;
+    }
+    return RT_OK;
+}
+
+int Renderer::validate() const
+{
+    int nmat = material_count();
+    if (s_.shading_method == RT_SHADING) {
+        for (int32_t m : tri_mat_)
+            if (m < 0 || m >= nmat)
+                return RT_EINVAL;
+        for (int32_t m : shape_mat_)
+            if (m < 0 || m >= nmat)
+                return RT_EINVAL;
+    }
+    if (s_.shading_method < 0 || s_.shading_method > 4)
+        return RT_EINVAL;
+    if ((s_.enable_ao_mapping || s_.shading_method == VISUALIZE_AO) && s_.enable_ao_mapping && tex_[TEX_AO].rgba.empty())
+        return RT_EINVAL;
+    if (s_.shading_method == RT_SHADING) {
+        if (s_.enable_diffuse_mapping && tex_[TEX_DIFFUSE].rgba.empty()) return RT_EINVAL;
+        if (s_.enable_normal_mapping && tex_[TEX_NORMAL].rgba.empty()) return RT_EINVAL;
+        if (s_.enable_displacement_mapping && (tex_[TEX_DISPLACEMENT].rgba.empty() || s_.parallax_mapping_steps <= 0))
+            return RT_EINVAL;
+        if (s_.enable_roughness_mapping && tex_[TEX_ROUGHNESS].rgba.empty()) return RT_EINVAL;
+    }
+    if (s_.enable_skysphere && tex_[TEX_SKYSPHERE].rgba.empty())
+        return RT_EINVAL;
+    if (!s_.enable_skysphere && s_.enable_skybox)
+        for (int i = 0; i < 6; i++)
+            if (sky_[i].rgba.empty())
+                return RT_EINVAL;
+    return RT_OK;
+}
+
+void Renderer::fill_params(KParams& P) const
+{
+    std::memset(&P, 0, sizeof(P));
+    P.nodes = d_nodes_.as<GNode>();
+    P.tris = d_tris_.as<GTri>();
+    P.tri_id = d_tri_id_.as<int32_t>();
+    P.tri_mat = d_tri_mat_.as<int32_t>();
+    P.tri_uv = tri_uv_.empty() ? nullptr : d_tri_uv_.as<float>();
+    P.nnodes = (int32_t)oct_.nodes.size();
+    P.ntri_slots = (int32_t)oct_.tris.size();
+    P.levels = oct_.levels > 0 ? oct_.levels : 1;
+    v3 pn[NPLANES];
+    plane_normals(pn);
+    for (int i = 0; i < NPLANES; i++) {
+        P.pn[i][0] = pn[i].x;
+        P.pn[i][1] = pn[i].y;
+        P.pn[i][2] = pn[i].z;
+    }
+    P.nshape = (int32_t)shape_kind_.size();
+    for (int k = 0; k < P.nshape; k++) {
+        P.shape_kind[k] = shape_kind_[k];
+        for (int j = 0; j < 6; j++) P.shape[k][j] = shape_[6 * k + j];
+        P.shape_mat[k] = shape_mat_[k];
+    }
+    P.mats = d_mats_.as<float>();
+    P.nmat = material_count();
+    std::memcpy(P.cam_pos, cam_pos_, sizeof(P.cam_pos));
+    std::memcpy(P.proj_inv, proj_inv_, sizeof(P.proj_inv));
+    std::memcpy(P.cam_to_world, c2w_, sizeof(P.cam_to_world));
+    std::memcpy(P.light, light_, sizeof(P.light));
+    for (int i = 0; i < TEX_SLOTS; i++) {
+        P.tex[i].px = tex_[i].rgba.empty() ? nullptr : d_tex_[i].as<float4>();
+        P.tex[i].w = tex_[i].w;
+        P.tex[i].h = tex_[i].h;
+    }
+    for (int i = 0; i < 6; i++) {
+        P.sky[i].px = sky_[i].rgba.empty() ? nullptr : d_sky_[i].as<float4>();
+        P.sky[i].w = sky_[i].w;
+        P.sky[i].h = sky_[i].h;
+    }
+    P.shading_method = s_.shading_method;
+    P.compute_shadows = s_.compute_shadows;
+    P.max_recursion_depth = s_.max_recursion_depth;
+    P.enable_bvh = s_.enable_bvh;
+    P.enable_ambient = s_.enable_ambient;
+    P.enable_diffuse = s_.enable_diffuse;
+    P.enable_specular = s_.enable_specular;
+    P.enable_emissive = s_.enable_emissive;
+    P.rough_reflections_sample_count = s_.rough_reflections_sample_count;
+    P.enable_ao_mapping = s_.enable_ao_mapping;
+    P.enable_diffuse_mapping = s_.enable_diffuse_mapping;
+    P.enable_normal_mapping = s_.enable_normal_mapping;
+    P.enable_displacement_mapping = s_.enable_displacement_mapping;
+    P.displacement_mapping_strength = s_.displacement_mapping_strength;
+    P.parallax_mapping_steps = s_.parallax_mapping_steps;
+    P.enable_roughness_mapping = s_.enable_roughness_mapping;
+    P.enable_skysphere = s_.enable_skysphere;
+    P.enable_skybox = s_.enable_skybox;
+    P.rng_seed = s_.rng_seed;
+    render_size(P.rw, P.rh);
+}
+
+static bool any_reflection(const std::vector<float>& mats)
+{
+    for (size_t i = 0; i + MAT_STRIDE <= mats.size(); i += MAT_STRIDE)
+        if (mats[i + 12] > 0.0f)
+            return true;
+    return false;
+}
+
+// Renderer::ray_trace, renderer.cpp:1068-1116
+int Renderer::ray_trace()
+{
+    if (validate() != RT_OK)
+        return fail(RT_EINVAL, "invalid scene: material index out of range or enabled texture map missing");
+    if (s_.shading_method == RT_SHADING && any_reflection(mats_))
+        return fail(RT_EUNSUPPORTED, "reflective materials: not implemented yet in this build");
+    int rc = ensure_device_scene();
+    if (rc != RT_OK)
+        return rc;
+    KParams P;
+    fill_params(P);
+    size_t npx = (size_t)P.rw * P.rh;
+    hipError_t e;
+    if ((e = d_internal_.reserve(npx * 4)) != hipSuccess || (e = d_counters_.reserve(64)) != hipSuccess)
+        return hip_fail(e, "hipMalloc (image)");
+    if (want_rgba_ && (e = d_rgba_.reserve(npx * 16)) != hipSuccess) return hip_fail(e, "hipMalloc (rgba)");
+    if (want_hit_ && ((e = d_hit_id_.reserve(npx * 4)) != hipSuccess || (e = d_hit_t_.reserve(npx * 4)) != hipSuccess))
+        return hip_fail(e, "hipMalloc (hit)");
+    if (want_shadow_ && (e = d_shadow_.reserve(npx)) != hipSuccess) return hip_fail(e, "hipMalloc (shadow)");
+    P.band_rows = P.rh;
+    P.nranks = 1;
+    P.rank = 0;
+    P.local_rows = P.rh;
+    P.tiles_x = (P.rw + 7) / 8;
+    P.tiles_y = (P.rh + 7) / 8;
+    P.argb = d_internal_.as<uint32_t>();
+    P.rgba = want_rgba_ ? d_rgba_.as<float4>() : nullptr;
+    P.hit_id = want_hit_ ? d_hit_id_.as<int32_t>() : nullptr;
+    P.hit_t = want_hit_ ? d_hit_t_.as<float>() : nullptr;
+    P.shadow = want_shadow_ ? d_shadow_.as<uint8_t>() : nullptr;
+    P.counters = d_counters_.as<unsigned long long>();
+    if ((e = hipMemsetAsync(d_counters_.p, 0, 64, stream_)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+    hipEventRecord(ev_[0], stream_);
+    if ((e = rt_launch_ray_trace(&P, stream_)) != hipSuccess) return hip_fail(e, "ray_trace_kernel launch");
+    hipEventRecord(ev_[1], stream_);
+    unsigned long long cnt[2] = {0, 0};
+    if ((e = hipMemcpyAsync(cnt, d_counters_.p, sizeof(cnt), hipMemcpyDeviceToHost, stream_)) != hipSuccess)
+        return hip_fail(e, "counters");
+    if ((e = hipStreamSynchronize(stream_)) != hipSuccess) return hip_fail(e, "ray_trace_kernel");
+    hipEventElapsedTime(&kernel_ms_, ev_[0], ev_[1]);
+    last_primary_ = (int64_t)npx;
+    last_shadow_ = (int64_t)cnt[0];
+    last_refl_ = (int64_t)cnt[1];
+    img_w_ = P.rw;
+    img_h_ = P.rh;
+    img_is_internal_ = true;
+    rendered_ = true;
+    aux_valid_ = true;
+    post_ms_ = 0;
+    return RT_OK;
+}
+
+// Renderer::post_process / apply_ssaa, renderer.cpp:1118-1135
+int Renderer::post_process()
+{
+    if (!rendered_)
+        return fail(RT_ESTATE, "post_process before ray_trace");
+    if (!s_.enable_ssaa || !img_is_internal_)
+        return RT_OK;
+    int f = s_.ssaa_factor;
+    if (img_w_ % f != 0 || img_h_ % f != 0)
+        return RT_OK;   // downscale_image_qt_ARGB32 prints and leaves the output untouched
+    hipError_t e = hipSetDevice(device_);
+    int dw = img_w_ / f, dh = img_h_ / f;
+    if (e == hipSuccess) e = d_image_.reserve((size_t)dw * dh * 4);
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc (ssaa)");
+    hipEventRecord(ev_[2], stream_);
+    if ((e = rt_launch_downscale(d_internal_.as<uint32_t>(), img_w_, img_h_, f, d_image_.as<uint32_t>(), stream_)) !=
+        hipSuccess)
+        return hip_fail(e, "downscale launch");
+    hipEventRecord(ev_[3], stream_);
+    if ((e = hipStreamSynchronize(stream_)) != hipSuccess) return hip_fail(e, "downscale");
+    hipEventElapsedTime(&post_ms_, ev_[2], ev_[3]);
+    img_w_ = dw;
+    img_h_ = dh;
+    img_is_internal_ = false;
+    return RT_OK;
+}
+
+int Renderer::get_image(uint32_t* argb, int32_t* w, int32_t* h)
+{
+    if (w) *w = img_w_;
+    if (h) *h = img_h_;
+    if (!argb)
+        return RT_OK;
+    if (!rendered_) {
+        // init_buffers / clear_image fill with BACKGROUND_COLOR (renderer.cpp:131-134)
+        uint32_t bg = color_to_argb(col(135.0f / 255.0f, 206.0f / 255.0f, 235.0f / 255.0f));
+        for (size_t i = 0; i < (size_t)img_w_ * img_h_; i++) argb[i] = bg;
+        return RT_OK;
+    }
+    hipSetDevice(device_);
+    const DevBuf& src = img_is_internal_ ? d_internal_ : d_image_;
+    hipError_t e = hipMemcpy(argb, src.p, (size_t)img_w_ * img_h_ * 4, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_fail(e, "get_image");
+    return RT_OK;
+}
+
+int Renderer::request_aux(bool rgba, bool hit, bool shadow)
+{
+    want_rgba_ = rgba;
+    want_hit_ = hit;
+    want_shadow_ = shadow;
+    aux_valid_ = false;
+    return RT_OK;
+}
+
+int Renderer::get_internal(uint32_t* argb, float* rgba, int32_t* hit_id, float* hit_t, uint8_t* shadow)
+{
+    if (!aux_valid_)
+        return fail(RT_ESTATE, "get_internal: no ray_trace since the last request_aux");
+    hipSetDevice(device_);
+    int rw, rh;
+    render_size(rw, rh);
+    size_t n = (size_t)rw * rh;
+    hipError_t e = hipSuccess;
+    if (argb) e = hipMemcpy(argb, d_internal_.p, n * 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && rgba) {
+        if (!want_rgba_) return fail(RT_ESTATE, "rgba not requested");
+        e = hipMemcpy(rgba, d_rgba_.p, n * 16, hipMemcpyDeviceToHost);
+    }
+    if (e == hipSuccess && (hit_id || hit_t)) {
+        if (!want_hit_) return fail(RT_ESTATE, "hit buffers not requested");
+        if (hit_id) e = hipMemcpy(hit_id, d_hit_id_.p, n * 4, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && hit_t) e = hipMemcpy(hit_t, d_hit_t_.p, n * 4, hipMemcpyDeviceToHost);
+    }
+    if (e == hipSuccess && shadow) {
+        if (!want_shadow_) return fail(RT_ESTATE, "shadow buffer not requested");
+        e = hipMemcpy(shadow, d_shadow_.p, n, hipMemcpyDeviceToHost);
+    }
+    if (e != hipSuccess) return hip_fail(e, "get_internal");
+    return RT_OK;
+}
+
+int Renderer::get_stats(rt_stats* out) const
+{
+    std::memset(out, 0, sizeof(*out));
+    out->primary_rays = last_primary_;
+    out->shadow_rays = last_shadow_;
+    out->reflection_rays = last_refl_;
+    out->kernel_ms = kernel_ms_;
+    out->post_ms = post_ms_;
+    out->build_ms = build_ms_;
+    out->octree_inner = oct_.stats.inner;
+    out->octree_leaves = oct_.stats.leaves;
+    out->octree_empty_leaves = oct_.stats.empty_leaves;
+    out->octree_max_leaf = oct_.stats.max_leaf;
+    out->octree_max_depth = oct_.stats.max_depth;
+    out->gpu_nodes = (int64_t)oct_.nodes.size();
+    out->gpu_tris = (int64_t)oct_.tris.size();
+    render_size(out->render_width, out->render_height);
+    return RT_OK;
+}
+
+int Renderer::local_rows(int band_rows, int rank, int nranks) const
+{
+    if (band_rows <= 0 || nranks <= 0 || rank < 0 || rank >= nranks)
+        return -1;
+    int nb = (s_.image_height + band_rows - 1) / band_rows;
+    int per = (nb + nranks - 1) / nranks;
+    return per * band_rows;
+}
+
+int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t* d_out, hipStream_t stream)
+{
+    int lrows = local_rows(band_rows, rank, nranks);
+    if (lrows < 0 || !d_out)
+        return fail(RT_EINVAL, "render_bands_device: bad band layout");
+    if (validate() != RT_OK)
+        return fail(RT_EINVAL, "invalid scene: material index out of range or enabled texture map missing");
+    if (s_.shading_method == RT_SHADING && any_reflection(mats_))
+        return fail(RT_EUNSUPPORTED, "reflective materials: not implemented yet in this build");
+    int rc = ensure_device_scene();
+    if (rc != RT_OK)
+        return rc;
+    if (!stream)
+        stream = stream_;
+    KParams P;
+    fill_params(P);
+    int f = s_.enable_ssaa ? s_.ssaa_factor : 1;
+    P.band_rows = band_rows * f;
+    P.nranks = nranks;
+    P.rank = rank;
+    P.local_rows = lrows * f;
+    P.tiles_x = (P.rw + 7) / 8;
+    P.tiles_y = (P.local_rows + 7) / 8;
+    hipError_t e;
+    if ((e = d_counters_.reserve(64)) != hipSuccess) return hip_fail(e, "hipMalloc (counters)");
+    uint32_t* target = d_out;
+    if (f > 1) {
+        if ((e = d_band_tmp_.reserve((size_t)P.rw * P.local_rows * 4)) != hipSuccess)
+            return hip_fail(e, "hipMalloc (band)");
+        target = d_band_tmp_.as<uint32_t>();
+    }
+    P.argb = target;
+    P.counters = d_counters_.as<unsigned long long>();
+    if ((e = hipMemsetAsync(d_counters_.p, 0, 64, stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+    if ((e = rt_launch_ray_trace(&P, stream)) != hipSuccess) return hip_fail(e, "ray_trace_kernel launch");
+    if (f > 1 && (e = rt_launch_downscale(target, P.rw, P.local_rows, f, d_out, stream)) != hipSuccess)
+        return hip_fail(e, "downscale launch");
+    return RT_OK;
+}
+
+}  // namespace rt

@@ -1,0 +1,127 @@
+// renderer.hpp -- rt::Renderer, the host-side mirror of the reference's
+// Renderer class (tp2/projets/renderer/renderer.h:20-355) for the ray-trace hot
+// path.  Scene state lives on the host (as in the reference); the octree is
+// built on the host and flattened, then nodes, triangles, materials and
+// textures are kept resident in HBM, and ray_trace() runs the gfx950 kernels.
+#pragma once
+
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/rt_mi355x.h"
+#include "kparams.hpp"
+#include "octree.hpp"
+
+namespace rt {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    int device = 0;
+    ~DevBuf();
+    hipError_t reserve(size_t n);   // grows (never shrinks); contents undefined after growth
+    void release();
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+struct HostTex {
+    int w = 0, h = 0;
+    std::vector<float> rgba;
+};
+
+class Renderer {
+public:
+    explicit Renderer(int device);
+    ~Renderer();
+    int init(std::string& err);
+
+    // ---- reference API (renderer.h) ----
+    const rt_settings& render_settings() const { return s_; }
+    int set_settings(const rt_settings& s);
+    int change_render_size(int w, int h);
+    int set_triangles(const float* tri9, const int32_t* mat, const float* uv6, int64_t n);
+    int add_sphere(float cx, float cy, float cz, float r, int mat);
+    int add_plane(float px, float py, float pz, float nx, float ny, float nz, int mat);
+    int clear_geometry();
+    int set_materials(const float* mats16, int n);
+    int material_count() const { return (int)(mats_.size() / MAT_STRIDE); }
+    int change_camera_fov(float fov);
+    int change_camera_aspect_ratio(float aspect);
+    int set_light_position(float x, float y, float z);
+    int set_camera_transform(const float m[16]);
+    int apply_transformation_to_camera(const float m[16]);
+    int set_camera_matrices(const float pos[3], const float proj_inv[16], const float c2w[16]);
+    void get_camera_matrices(float pos[3], float proj_inv[16], float c2w[16]) const;
+    int set_object_transform(const float m[16]);
+    int reset_previous_transform();
+    int set_texture(int slot, int w, int h, const float* rgba);
+    int set_skybox(const int32_t w[6], const int32_t h[6], const float* const faces[6]);
+    int reconstruct_bvh_new();
+    int destroy_bvh();
+    int ray_trace();
+    int post_process();
+    int get_image(uint32_t* argb, int32_t* w, int32_t* h);
+    int request_aux(bool rgba, bool hit, bool shadow);
+    int get_internal(uint32_t* argb, float* rgba, int32_t* hit_id, float* hit_t, uint8_t* shadow);
+    int get_stats(rt_stats* out) const;
+
+    // ---- multi-GPU strips ----
+    int local_rows(int band_rows, int rank, int nranks) const;
+    int render_bands_device(int band_rows, int rank, int nranks, uint32_t* d_out, hipStream_t stream);
+
+    const std::string& error() const { return err_; }
+
+private:
+    int fail(int code, const std::string& msg);
+    int hip_fail(hipError_t e, const char* what);
+    void render_size(int& w, int& h) const;
+    void update_camera_projection();
+    int ensure_device_scene();
+    int validate() const;
+    void fill_params(KParams& P) const;
+
+    int device_;
+    hipStream_t stream_ = nullptr;
+    hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};
+    std::string err_;
+
+    rt_settings s_;
+
+    // scene (host copies; the reference Renderer copies its inputs too)
+    std::vector<float> tri_;
+    std::vector<int32_t> tri_mat_;
+    std::vector<float> tri_uv_;
+    std::vector<int32_t> shape_kind_;
+    std::vector<float> shape_;
+    std::vector<int32_t> shape_mat_;
+    std::vector<float> mats_;
+    float cam_pos_[3] = {0, 0, 0};
+    float fov_ = 45.0f, near_ = 0.1f, far_ = 1000.0f, aspect_ = 1.0f;
+    float proj_[16], proj_inv_[16], c2w_[16], w2c_[16];
+    float light_[3] = {3, 3, 2};
+    float prev_object_[16];
+    HostTex tex_[TEX_SLOTS];
+    HostTex sky_[6];
+    bool has_bvh_ = false;   // Renderer::_bvh holds a built tree
+
+    // device state
+    FlatOctree oct_;
+    bool geom_dirty_ = true, mats_dirty_ = true, tex_dirty_ = true;
+    DevBuf d_nodes_, d_tris_, d_tri_id_, d_tri_mat_, d_tri_uv_, d_mats_;
+    DevBuf d_tex_[TEX_SLOTS], d_sky_[6];
+    DevBuf d_internal_, d_image_, d_rgba_, d_hit_id_, d_hit_t_, d_shadow_, d_counters_, d_band_tmp_;
+    bool want_rgba_ = false, want_hit_ = false, want_shadow_ = false;
+    bool aux_valid_ = false;
+    // current image (Renderer::_image): internal after ray_trace, downscaled after post_process
+    int img_w_ = 0, img_h_ = 0;
+    bool img_is_internal_ = false;
+    bool rendered_ = false;
+
+    // stats
+    int64_t last_primary_ = 0, last_shadow_ = 0, last_refl_ = 0;
+    float kernel_ms_ = 0, post_ms_ = 0, build_ms_ = 0;
+};
+
+}  // namespace rt
