@@ -1,0 +1,182 @@
+#!/usr/bin/env python
+"""Headline benchmark: Mrays/s (primary + shadow) at 1920x1080 on the 1M-triangle scene.
+
+Workload (BASELINE.json configs[3]): 1,000,000-triangle UV
+sphere, 1920x1080 with 2x2 SSAA (ssaa_factor 2 -> 3840x2160 internal rays), primary
+rays + one shadow ray per shaded hit, octree BVH depth 12 / leaf 40.  One "step"
+renders the whole frame: ray generation, octree traversal, Moller-Trumbore,
+shadow rays, RT shading, quantisation and the SSAA downscale, as image strips on
+N GPUs (one process per GPU) followed by the RCCL all-gather of the strips.
+
+Run: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
+torch.distributed.run (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* from the env).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md)
+NODE_BYTES = 56              # one k-DOP test reads 14 floats
+TRI_BYTES = 48               # one Moller-Trumbore test reads a, b-a, c-a, n
+PIXEL_BYTES = 4              # ARGB32 write per internal pixel
+COUNTS_FILE = os.path.join(ROOT, "profiles", "work_counts.json")
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="sphere1m")
+    ap.add_argument("--band-rows", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from raytracercpp_amd import scenes
+    from raytracercpp_amd.renderer import Renderer
+    from raytracercpp_amd.strips import assemble_torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    sc, st = scenes.CONFIGS[args.config]()
+    r = Renderer(local)
+    r.load_scene(sc, st)
+    W, H = st.image_width, st.image_height
+    rw, rh = st.render_size()
+    band = args.band_rows
+    nloc = r.local_rows(band, rank, world)
+    out = torch.empty((nloc, W), dtype=torch.int32, device=dev)
+    parts = [torch.empty_like(out) for _ in range(world)] if world > 1 else [out]
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        r.render_bands_device(band, rank, world, out.data_ptr(), stream.cuda_stream)
+        if world > 1:
+            dist.all_gather(parts, out)
+
+    t_build0 = time.perf_counter()
+    step()   # first call builds + uploads the octree
+    torch.cuda.synchronize()
+    t_first = time.perf_counter() - t_build0
+    shadow_local, _ = r.band_counters()
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ktimes = r.kernel_times(args.steps)
+    k_mean = float(np.mean(ktimes))
+
+    t = torch.tensor([elapsed, float(shadow_local), k_mean], dtype=torch.float64, device=dev)
+    if world > 1:
+        tm = t.clone()
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        ts = t.clone()
+        dist.all_reduce(ts, op=dist.ReduceOp.SUM)
+        elapsed_max = float(tm[0])
+        shadow_total = int(ts[1])
+        k_mean_max = float(tm[2])
+    else:
+        elapsed_max, shadow_total, k_mean_max = elapsed, int(shadow_local), k_mean
+    frame = assemble_torch(parts, H, band) if rank == 0 else None
+
+    if rank == 0:
+        primary = rw * rh
+        rays = primary + shadow_total
+        ms_per_step = 1e3 * elapsed_max / args.steps
+        value = rays * args.steps / elapsed_max / 1e6
+        img = frame.cpu().numpy().view(np.uint32)
+        res = {
+            "metric": "Mrays/sec (primary+shadow) at 1920x1080, 1M-tri scene; max |dpixel|",
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (deterministic 1M-tri UV sphere, SURVEY.md 8(d) C4)",
+            "config": {"workload": "C4 sphere1m: 1,000,000 tris, 1920x1080, ssaa_factor 2 (3840x2160 rays), "
+                                   "primary + shadow, octree 12/40", "image": [W, H], "render": [rw, rh],
+                       "rays_per_frame": rays, "primary_rays": primary, "shadow_rays": shadow_total,
+                       "band_rows": band, "parallelism": f"image strips x{world}"},
+            "kernel_ms": round(k_mean_max, 4),
+            "first_call_s": round(t_first, 3),
+        }
+        counts = None
+        if os.path.exists(COUNTS_FILE):
+            with open(COUNTS_FILE) as f:
+                counts = json.load(f).get(args.config)
+        if counts:
+            tests = counts["child_tests_primary"] + counts["child_tests_shadow"]
+            tris = counts["tri_tests_primary"] + counts["tri_tests_shadow"]
+            nbytes = NODE_BYTES * tests + TRI_BYTES * tris + PIXEL_BYTES * primary
+            share = 1.0 / world
+            achieved = nbytes * share / (k_mean_max * 1e-3) / 1e9
+            res["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                               "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": counts.get("pmc_traffic_bytes"),
+                               "algorithmic_bytes_per_frame": nbytes}
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"], res["max_abs_dpixel"] = cpu_baseline(sc, st, img, args.cpu_threads)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(sc, st, gpu_img, threads):
+    """The oracle's C restatement (OpenMP, oracle/liboracle.so) on the full frame: a bounded
+    sample of ~1-3 s on the box's host cores; also gives max |dpixel| of the GPU frame."""
+    from oracle.bindings import Oracle
+    threads = threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    o = Oracle(sc, st)
+    res = o.render_rows(nthreads=threads)
+    rw, rh = st.render_size()
+    ref = Oracle.downscale(res.argb, rw, rh, st.ssaa_factor) if st.enable_ssaa else res.argb
+    g = gpu_img.ravel()
+    d = 0
+    for sh in (16, 8, 0):
+        d = max(d, int(np.max(np.abs(((g >> sh) & 0xFF).astype(np.int32) - ((ref >> sh) & 0xFF).astype(np.int32)))))
+    rays = res.counters["primary_rays"] + res.counters["shadow_rays"]
+    base = {"value": round(rays / res.seconds / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"full C4 frame ({rw}x{rh} primary + {res.counters['shadow_rays']} shadow rays) "
+                      f"in {res.seconds:.2f} s, oracle.c OpenMP x{threads}"}
+    return base, d
+
+
+if __name__ == "__main__":
+    main()

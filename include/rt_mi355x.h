@@ -189,6 +189,12 @@ int rt_local_rows(rt_renderer *r, int32_t band_rows, int32_t rank, int32_t nrank
 int rt_render_bands_device(rt_renderer *r, int32_t band_rows, int32_t rank, int32_t nranks, uint32_t *d_out,
                            void *hip_stream);
 
+/* GPU durations (ms) of the ray-trace kernel of the last n rt_render_bands_device
+ * calls, from HIP events recorded around each launch on its stream (waits for them). */
+int rt_kernel_times(rt_renderer *r, float *ms, int32_t n);
+/* shadow / reflection ray counts of the last rt_render_bands_device (synchronises the device) */
+int rt_band_counters(rt_renderer *r, int64_t *shadow_rays, int64_t *reflection_rays);
+
 /* ---- tp2/src/mat.cpp restated (host) ---- */
 /* kind: 0 Translation(x,y,z) 1 RotationX(x deg) 2 RotationY 3 RotationZ 4 Scale(x,y,z) 5 Identity */
 void rt_make_transform(int32_t kind, float x, float y, float z, float out[16]);

@@ -246,6 +246,21 @@ int rt_render_bands_device(rt_renderer* r, int32_t band_rows, int32_t rank, int3
     });
 }
 
+int rt_kernel_times(rt_renderer* r, float* ms, int32_t n)
+{
+    return guarded(R(r), [&] { return ms ? R(r)->kernel_times(ms, n) : RT_EINVAL; });
+}
+int rt_band_counters(rt_renderer* r, int64_t* shadow_rays, int64_t* reflection_rays)
+{
+    return guarded(R(r), [&] {
+        unsigned long long c[2] = {0, 0};
+        int rc = R(r)->band_counters(c);
+        if (shadow_rays) *shadow_rays = (int64_t)c[0];
+        if (reflection_rays) *reflection_rays = (int64_t)c[1];
+        return rc;
+    });
+}
+
 void rt_make_transform(int32_t kind, float x, float y, float z, float out[16])
 {
     switch (kind) {

@@ -79,6 +79,8 @@ Renderer::~Renderer()
     hipSetDevice(device_);
     for (auto& e : ev_)
         if (e) hipEventDestroy(e);
+    for (auto& e : ring_)
+        if (e) hipEventDestroy(e);
     if (stream_) hipStreamDestroy(stream_);
 }
 
@@ -711,10 +713,42 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
     }
     P.argb = target;
     P.counters = d_counters_.as<unsigned long long>();
+    if (ring_.empty()) {
+        ring_.resize(2 * EV_RING, nullptr);
+        for (auto& ev : ring_)
+            if ((e = hipEventCreate(&ev)) != hipSuccess) return hip_fail(e, "hipEventCreate");
+    }
     if ((e = hipMemsetAsync(d_counters_.p, 0, 64, stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+    hipEventRecord(ring_[2 * ring_next_], stream);
     if ((e = rt_launch_ray_trace(&P, stream)) != hipSuccess) return hip_fail(e, "ray_trace_kernel launch");
+    hipEventRecord(ring_[2 * ring_next_ + 1], stream);
+    ring_next_ = (ring_next_ + 1) % EV_RING;
+    if (ring_count_ < EV_RING) ring_count_++;
     if (f > 1 && (e = rt_launch_downscale(target, P.rw, P.local_rows, f, d_out, stream)) != hipSuccess)
         return hip_fail(e, "downscale launch");
+    return RT_OK;
+}
+
+int Renderer::kernel_times(float* ms, int n)
+{
+    if (n > ring_count_)
+        return fail(RT_EINVAL, "kernel_times: fewer launches recorded");
+    hipSetDevice(device_);
+    for (int i = 0; i < n; i++) {
+        int slot = ((ring_next_ - n + i) % EV_RING + EV_RING) % EV_RING;
+        hipError_t e = hipEventSynchronize(ring_[2 * slot + 1]);
+        if (e == hipSuccess) e = hipEventElapsedTime(&ms[i], ring_[2 * slot], ring_[2 * slot + 1]);
+        if (e != hipSuccess) return hip_fail(e, "kernel_times");
+    }
+    return RT_OK;
+}
+
+int Renderer::band_counters(unsigned long long out[2])
+{
+    hipSetDevice(device_);
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(out, d_counters_.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_fail(e, "band_counters");
     return RT_OK;
 }
 

@@ -70,6 +70,10 @@ public:
     // ---- multi-GPU strips ----
     int local_rows(int band_rows, int rank, int nranks) const;
     int render_bands_device(int band_rows, int rank, int nranks, uint32_t* d_out, hipStream_t stream);
+    // durations (ms) of the last n ray_trace_kernel launches of render_bands_device,
+    // bracketed by HIP events on the launch stream (synchronises on them)
+    int kernel_times(float* ms, int n);
+    int band_counters(unsigned long long out[2]);
 
     const std::string& error() const { return err_; }
 
@@ -118,6 +122,11 @@ private:
     int img_w_ = 0, img_h_ = 0;
     bool img_is_internal_ = false;
     bool rendered_ = false;
+
+    // event ring for render_bands_device kernel timing
+    static constexpr int EV_RING = 256;
+    std::vector<hipEvent_t> ring_;
+    int ring_next_ = 0, ring_count_ = 0;
 
     // stats
     int64_t last_primary_ = 0, last_shadow_ = 0, last_refl_ = 0;

@@ -227,6 +227,16 @@ class Renderer:
         self._call("rt_render_bands_device", int(band_rows), int(rank), int(nranks), C.c_void_p(d_out_ptr),
                    C.c_void_p(stream_ptr))
 
+    def kernel_times(self, n):
+        ms = np.zeros(n, np.float32)
+        self._call("rt_kernel_times", ptr(ms, _f32p), int(n))
+        return ms
+
+    def band_counters(self):
+        a, b = C.c_int64(), C.c_int64()
+        self._call("rt_band_counters", C.byref(a), C.byref(b))
+        return a.value, b.value
+
     # -- convenience ----------------------------------------------------------------
     def load_scene(self, sc: SceneData, st: RenderSettings):
         """Settings, camera, light, materials, geometry and textures of a SceneData."""
