@@ -189,6 +189,14 @@ int rt_local_rows(rt_renderer *r, int32_t band_rows, int32_t rank, int32_t nrank
 int rt_render_bands_device(rt_renderer *r, int32_t band_rows, int32_t rank, int32_t nranks, uint32_t *d_out,
                            void *hip_stream);
 
+/* BVH::intersect (bvh.cpp:68-71; OctreeNode::intersect, bvh.h:212-287) for n arbitrary
+ * rays (origins / directions [n][3]): the closest-hit query trace_ray and is_shadowed
+ * issue, with the reference's visit order.  Outputs per ray: triangle index of the
+ * query's HitInfo (-1 none), its t / u / v, and the boolean BVH::intersect returned.
+ * Uses the brute-force loop when enable_bvh is 0. */
+int rt_trace_rays(rt_renderer *r, const float *orig, const float *dir, int64_t n, int32_t *tri_id, float *t,
+                  float *u, float *v, uint8_t *ret);
+
 /* GPU durations (ms) of the ray-trace kernel of the last n rt_render_bands_device
  * calls, from HIP events recorded around each launch on its stream (waits for them). */
 int rt_kernel_times(rt_renderer *r, float *ms, int32_t n);

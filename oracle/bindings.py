@@ -278,6 +278,7 @@ class RefHarness:
             L.ref_render_rows.argtypes = [C.POINTER(OrcScene), C.POINTER(OrcSettings), C.c_int, C.c_int,
                                           C.POINTER(OrcOutputs), C.POINTER(OrcCounters)]
             L.ref_downscale_argb.argtypes = [_u32p, C.c_int, C.c_int, C.c_int, _u32p]
+            L.ref_heap_order.argtypes = [_f32p, C.c_int, _i32p]
             cls._lib = L
         return cls._lib
 
@@ -371,6 +372,13 @@ class RefHarness:
             raise RuntimeError("ref_render_rows failed")
         res.counters = cnt.as_dict()
         return res
+
+    @classmethod
+    def heap_order(cls, keys):
+        k = np.ascontiguousarray(keys, np.float32)
+        out = np.zeros(len(k), np.int32)
+        cls.lib().ref_heap_order(_ptr(k, _f32p), len(k), _ptr(out, _i32p))
+        return out
 
     @classmethod
     def downscale(cls, argb, w, h, factor):

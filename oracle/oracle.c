@@ -611,16 +611,18 @@ static inline const float *img_at(const oimg *I, int x, int y)
 }
 
 /* Image::texture_floor -> sample_floor, image.h:79-86, 94-97 */
-static c3 tex_floor(const oimg *I, float x, float y)
+static c3 tex_floor_a(const oimg *I, float x, float y, float *alpha)
 {
     float u = floorf(x * I->w);
     float v = floorf(y * I->h);
     const float *p = img_at(I, f2i(u), f2i(v));
+    if (alpha) *alpha = p[3];
     return C(p[0], p[1], p[2]);
 }
+static c3 tex_floor(const oimg *I, float x, float y) { return tex_floor_a(I, x, y, NULL); }
 
 /* Image::texture_bilinear -> sample_bilinear, image.h:66-77, 89-92 */
-static c3 tex_bilinear(const oimg *I, float xx, float yy)
+static c3 tex_bilinear(const oimg *I, float xx, float yy, float *alpha)
 {
     float x = xx * I->w, y = yy * I->h;
     float u = x - floorf(x);
@@ -634,11 +636,12 @@ static c3 tex_bilinear(const oimg *I, float xx, float yy)
     r.r = p00[0] * w00 + p10[0] * w10 + p01[0] * w01 + p11[0] * w11;
     r.g = p00[1] * w00 + p10[1] * w10 + p01[1] * w01 + p11[1] * w11;
     r.b = p00[2] * w00 + p10[2] * w10 + p01[2] * w01 + p11[2] * w11;
+    if (alpha) *alpha = p00[3] * w00 + p10[3] * w10 + p01[3] * w01 + p11[3] * w11;
     return r;
 }
 
 /* Skybox::sample, skybox.cpp:12-51 */
-static c3 skybox_sample(const oimg *faces, v3 dir)
+static c3 skybox_sample(const oimg *faces, v3 dir, float *alpha)
 {
     v3 d2 = V(dir.x, dir.y, -dir.z);
     v3 da = V(fabsf(d2.x), fabsf(d2.y), fabsf(d2.z));
@@ -662,7 +665,7 @@ static c3 skybox_sample(const oimg *faces, v3 dir)
     }
     u = u * nf + 0.5;
     v = v * nf + 0.5;
-    return tex_bilinear(&faces[face], u, v);
+    return tex_bilinear(&faces[face], u, v, alpha);
 }
 
 /* ------------------------------------------------------------------------- */
@@ -684,6 +687,7 @@ typedef struct {
     uint32_t rng;
     orc_counters *cnt;
     int ray_kind;   /* 0 primary, 1 shadow, 2 reflection (for counters) */
+    float alpha;    /* Color::a of the last trace_ray result (sky textures carry theirs) */
 } otracer;
 
 static const float EPS_SHADOW = 1.0e-4f;       /* Renderer::EPSILON, renderer.h:23 */
@@ -965,8 +969,10 @@ static c3 trace_ray(otracer *T, v3 ro, v3 rd, ohit *fin, int depth, int *found, 
     const struct orc_ctx *X = T->X;
     const orc_settings *S = &X->s;
     ohit local = hit_fresh();
-    if (depth > S->max_recursion_depth)
+    if (depth > S->max_recursion_depth) {
+        T->alpha = 1.0f;
         return C(0.0f, 0.0f, 0.0f);
+    }
     int src = -1;
     T->ray_kind = depth == 0 ? 0 : 2;
     if (S->enable_bvh) {
@@ -1005,14 +1011,16 @@ static c3 trace_ray(otracer *T, v3 ro, v3 rd, ohit *fin, int depth, int *found, 
         c.r = sclamp01(c.r);
         c.g = sclamp01(c.g);
         c.b = sclamp01(c.b);
+        T->alpha = 1.0f;
         return c;
     }
     if (S->enable_skysphere) {
         float u = 0.5 + atan2f(-rd.z, -rd.x) / (2 * M_PI);
         float v = 0.5 + asinf(-rd.y) / M_PI;
-        return tex_floor(&X->tex[ORC_TEX_SKYSPHERE], u, v);
+        return tex_floor_a(&X->tex[ORC_TEX_SKYSPHERE], u, v, &T->alpha);
     } else if (S->enable_skybox)
-        return skybox_sample(X->sky, rd);
+        return skybox_sample(X->sky, rd, &T->alpha);
+    T->alpha = 1.0f;
     return background_color();
 }
 
@@ -1130,7 +1138,7 @@ ORC_API int orc_render_rows(const struct orc_ctx *X, int row_begin, int row_coun
                     out->rgba[4 * o] = c.r;
                     out->rgba[4 * o + 1] = c.g;
                     out->rgba[4 * o + 2] = c.b;
-                    out->rgba[4 * o + 3] = 1.0f;
+                    out->rgba[4 * o + 3] = T.alpha;
                 }
                 if (out->hit_id) out->hit_id[o] = found ? src : -1;
                 if (out->hit_t) out->hit_t[o] = hi.t;

@@ -692,6 +692,26 @@ int ref_render_rows(const orc_scene* sc, const orc_settings* st, int row_begin, 
     return 0;
 }
 
+/* Pop order of the reference's per-node queue type (bvh.h:110-123, 250):
+ * std::priority_queue<QueueElement, std::vector<QueueElement>, std::greater<QueueElement>>
+ * filled with n elements in index order. */
+void ref_heap_order(const float* keys, int n, int32_t* out_order)
+{
+    std::vector<BVH::OctreeNode> dummies;
+    dummies.reserve(n);
+    for (int i = 0; i < n; i++)
+        dummies.emplace_back(Point(0, 0, 0), Point(0, 0, 0));
+    std::priority_queue<BVH::OctreeNode::QueueElement, std::vector<BVH::OctreeNode::QueueElement>,
+                        std::greater<BVH::OctreeNode::QueueElement>>
+        q;
+    for (int i = 0; i < n; i++)
+        q.emplace(BVH::OctreeNode::QueueElement(&dummies[i], keys[i]));
+    for (int i = 0; i < n; i++) {
+        out_order[i] = (int32_t)(q.top()._node - dummies.data());
+        q.pop();
+    }
+}
+
 /* ImageUtils::downscale_image_qt_ARGB32 (imageUtils.h:98-147) */
 int ref_downscale_argb(const uint32_t* in, int w, int h, int factor, uint32_t* out)
 {

@@ -246,6 +246,11 @@ int rt_render_bands_device(rt_renderer* r, int32_t band_rows, int32_t rank, int3
     });
 }
 
+int rt_trace_rays(rt_renderer* r, const float* orig, const float* dir, int64_t n, int32_t* tri_id, float* t,
+                  float* u, float* v, uint8_t* ret)
+{
+    return guarded(R(r), [&] { return R(r)->trace_rays(orig, dir, n, tri_id, t, u, v, ret); });
+}
 int rt_kernel_times(rt_renderer* r, float* ms, int32_t n)
 {
     return guarded(R(r), [&] { return ms ? R(r)->kernel_times(ms, n) : RT_EINVAL; });

@@ -449,17 +449,18 @@ __device__ __forceinline__ float4 texel(const KTex& T, int x, int y)
     return T.px[(unsigned)(py * T.w + px)];
 }
 
-// Image::texture_floor -> sample_floor, image.h:79-86, 94-97
-__device__ __forceinline__ c3 tex_floor(const KTex& T, float x, float y)
+// Image::texture_floor -> sample_floor, image.h:79-86, 94-97 (alpha optional)
+__device__ __forceinline__ c3 tex_floor(const KTex& T, float x, float y, float* alpha = nullptr)
 {
     float u = floorf(x * T.w);
     float v = floorf(y * T.h);
     float4 p = texel(T, f2i(u), f2i(v));
+    if (alpha) *alpha = p.w;
     return col(p.x, p.y, p.z);
 }
 
 // Image::texture_bilinear -> sample_bilinear, image.h:66-77, 89-92
-__device__ __forceinline__ c3 tex_bilinear(const KTex& T, float xx, float yy)
+__device__ __forceinline__ c3 tex_bilinear(const KTex& T, float xx, float yy, float* alpha)
 {
     float x = xx * T.w, y = yy * T.h;
     float u = x - floorf(x);
@@ -467,13 +468,14 @@ __device__ __forceinline__ c3 tex_bilinear(const KTex& T, float xx, float yy)
     int ix = f2i(x), iy = f2i(y);
     float4 p00 = texel(T, ix, iy), p10 = texel(T, ix + 1, iy), p01 = texel(T, ix, iy + 1), p11 = texel(T, ix + 1, iy + 1);
     float w00 = (1 - u) * (1 - v), w10 = u * (1 - v), w01 = (1 - u) * v, w11 = u * v;
+    *alpha = p00.w * w00 + p10.w * w10 + p01.w * w01 + p11.w * w11;
     return col(p00.x * w00 + p10.x * w10 + p01.x * w01 + p11.x * w11,
                p00.y * w00 + p10.y * w10 + p01.y * w01 + p11.y * w11,
                p00.z * w00 + p10.z * w10 + p01.z * w01 + p11.z * w11);
 }
 
 // Skybox::sample, skybox.cpp:12-51
-__device__ c3 skybox_sample(const KParams& P, v3 dir)
+__device__ c3 skybox_sample(const KParams& P, v3 dir, float* alpha)
 {
     v3 d2 = mk(dir.x, dir.y, -dir.z);
     v3 da = mk(fabsf(d2.x), fabsf(d2.y), fabsf(d2.z));
@@ -497,7 +499,7 @@ __device__ c3 skybox_sample(const KParams& P, v3 dir)
     }
     u = (float)((double)(u * nf) + 0.5);
     v = (float)((double)(v * nf) + 0.5);
-    return tex_bilinear(P.sky[face], u, v);
+    return tex_bilinear(P.sky[face], u, v, alpha);
 }
 
 __device__ __forceinline__ const float* mat_of(const KParams& P, int id) { return P.mats + (size_t)MAT_STRIDE * id; }
@@ -666,23 +668,24 @@ __device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv)
     return src;
 }
 
-// shade_ray_inter_point (renderer.cpp:556-617) without the reflection term,
-// which the caller adds (reflection > 0 is handled by the recursive path).
-// Returns the colour before the final clamp; *partial receives the pieces the
-// reflection path needs.
-struct ShadeOut {
-    c3 color;      // clamped colour when no reflection is involved
-    c3 pre_refl;   // fc before "+ reflection", after emission
-    bool shadowed;
+// shade_ray_inter_point (renderer.cpp:556-617) up to (not including) the
+// reflection term: for RT_SHADING, fc = diffuse + specular, halved when
+// shadowed, plus emission; for the debug modes fc is the final colour.  The
+// caller adds "+ compute_reflection(..) * reflection" and the ambient term
+// (shade_finish).  Normal mapping overwrites h.normal, which persists in the
+// caller's HitInfo exactly as in the reference (renderer.cpp:571-572).
+struct Direct {
+    c3 fc;
     v3 ip;
+    bool shadowed;
 };
 
-__device__ ShadeOut shade(const KParams& P, v3 ro, v3 rd, Rec& h, uint2* lv)
+__device__ Direct shade_direct(const KParams& P, v3 ro, v3 rd, Rec& h, uint2* lv, unsigned& nshadow)
 {
-    ShadeOut out;
+    Direct out;
     out.shadowed = false;
-    c3 fc = col(0.0f, 0.0f, 0.0f);
     out.ip = mk(0, 0, 0);
+    c3 fc = col(0.0f, 0.0f, 0.0f);
     if (P.shading_method == RT_SHADING) {
         float u = h.u, v = h.v;
         v3 ip = ro + rd * h.t;
@@ -725,14 +728,13 @@ __device__ ShadeOut shade(const KParams& P, v3 ro, v3 rd, Rec& h, uint2* lv)
             }
         }
         fc = fc + spec * (float)(P.enable_specular != 0);
+        if (P.compute_shadows)
+            nshadow++;
         bool sh = is_shadowed(P, ip, h.normal, light, lv);
         out.shadowed = sh;
         if (sh)
             fc = fc * col(0.5f, 0.5f, 0.5f);
         fc = fc + mat_col(m, 9) * (float)(P.enable_emissive != 0);
-        out.pre_refl = fc;
-        float refl = m[12];
-        fc = fc + (col(0.1f, 0.1f, 0.1f) * mat_col(m, 0)) * (1 - refl) * (float)(P.enable_ambient != 0);
     } else if (P.shading_method == ABS_NORMALS) {
         fc = col(fabsf(h.normal.x), fabsf(h.normal.y), fabsf(h.normal.z));
     } else if (P.shading_method == PASTEL_NORMALS) {
@@ -749,20 +751,212 @@ __device__ ShadeOut shade(const KParams& P, v3 ro, v3 rd, Rec& h, uint2* lv)
         }
         fc = c;
     }
-    out.color = col(clamp01(fc.r), clamp01(fc.g), clamp01(fc.b));
+    out.fc = fc;
     return out;
 }
 
-// trace_ray miss colour (renderer.cpp:1052-1065)
-__device__ c3 miss_color(const KParams& P, v3 d)
+__device__ __forceinline__ c3 clamp3(c3 c) { return col(clamp01(c.r), clamp01(c.g), clamp01(c.b)); }
+
+// renderer.cpp:594-616: "+ reflection * reflection" (refl > 0 only), "+ ambient", clamp.
+__device__ __forceinline__ c3 shade_finish(const KParams& P, c3 fc, const float* m, c3 refl_color)
 {
+    float refl = m[12];
+    if (refl > 0.0f)
+        fc = fc + refl_color * refl;
+    fc = fc + (col(0.1f, 0.1f, 0.1f) * mat_col(m, 0)) * (1 - refl) * (float)(P.enable_ambient != 0);
+    return clamp3(fc);
+}
+
+// trace_ray miss colour (renderer.cpp:1052-1065); alpha of the returned Color
+__device__ c3 miss_color(const KParams& P, v3 d, float& alpha)
+{
+    alpha = 1.0f;
     if (P.enable_skysphere) {
         float u = (float)(0.5 + (double)atan2f(-d.z, -d.x) / (2 * M_PI));
         float v = (float)(0.5 + (double)asinf(-d.y) / M_PI);
-        return tex_floor(P.tex[TEX_SKYSPHERE], u, v);
+        return tex_floor(P.tex[TEX_SKYSPHERE], u, v, &alpha);
     } else if (P.enable_skybox)
-        return skybox_sample(P, d);
+        return skybox_sample(P, d, &alpha);
     return background();
+}
+
+// XorShiftGenerator::get_rand / get_rand_bilateral (xorshift.h:43-57) on a
+// per-pixel stream seeded from the pixel index (the reference seeds one stream
+// per OpenMP thread with std::rand()).
+__device__ __forceinline__ uint32_t pixel_seed(uint32_t pixel, uint32_t seed)
+{
+    uint32_t x = pixel * 0x9E3779B9u ^ seed;
+    x ^= x >> 16; x *= 0x7feb352dU;
+    x ^= x >> 15; x *= 0x846ca68bU;
+    x ^= x >> 16;
+    return x ? x : 0x9E3779B9u;
+}
+
+__device__ __forceinline__ float rng_bilateral(uint32_t& s)
+{
+    uint32_t x = s;
+    x ^= x << 13;
+    x ^= x >> 17;
+    x ^= x << 5;
+    s = x;
+    return (float)x / (float)UINT32_MAX * 2 - 1;
+}
+
+// One pending Renderer::compute_reflection call (renderer.cpp:283-338) of the
+// trace at depth d: its samples are traced at depth d + 1 into the shared
+// reflection_hit_info 'rhi' (renderer.cpp:286).
+struct Frame {
+    c3 fc;          // shade_direct colour of the hit that reflects
+    c3 total;
+    v3 ro, perfect, n;
+    float rough;
+    int mat, i, sc;
+    Rec rhi;
+};
+
+constexpr int MAX_FRAMES = 16;   // max_recursion_depth <= 15 with reflective materials
+
+struct PixelOut {
+    c3 color;
+    float alpha;
+    Rec fin;
+    int src;
+    bool found, shadowed;
+};
+
+// Renderer::trace_ray (renderer.cpp:1008-1066) for one primary ray, with the
+// compute_reflection recursion (when REFL) unrolled onto an explicit stack.
+template <bool REFL>
+__device__ PixelOut trace_pixel(const KParams& P, v3 cam, v3 rd0, uint2* lv, uint32_t rng, unsigned& nshadow,
+                                unsigned& nrefl)
+{
+    PixelOut po;
+    po.fin = rec_fresh();
+    po.found = po.shadowed = false;
+    po.alpha = 1.0f;
+    po.src = closest_hit(P, cam, rd0, po.fin, lv);
+    if (!REFL) {
+        if (po.fin.t > 0.1f) {
+            po.found = true;
+            Direct D = shade_direct(P, cam, rd0, po.fin, lv, nshadow);
+            po.shadowed = D.shadowed;
+            po.color = P.shading_method == RT_SHADING ? shade_finish(P, D.fc, mat_of(P, po.fin.mat), col(0, 0, 0))
+                                                      : clamp3(D.fc);
+        } else
+            po.color = miss_color(P, rd0, po.alpha);
+        return po;
+    }
+
+    Frame fr[MAX_FRAMES];
+    const int N = P.rough_reflections_sample_count;
+    enum { S_TRACE, S_RET, S_NEXT };
+    int state, depth = 0, f = 0;
+    v3 ro = cam, rd = rd0;
+    c3 ret = col(0, 0, 0);
+    bool first = true;   // the depth-0 closest hit is already in po.fin
+    state = S_TRACE;
+    for (;;) {
+        if (state == S_TRACE) {
+            // ---- trace_ray(ray, fin, depth) ----
+            Rec& fin = depth == 0 ? po.fin : fr[depth - 1].rhi;
+            if (depth > P.max_recursion_depth) {
+                ret = col(0.0f, 0.0f, 0.0f);
+                state = S_RET;
+                continue;
+            }
+            if (!first)
+                closest_hit(P, ro, rd, fin, lv);
+            first = false;
+            if (fin.t > 0.1f) {
+                if (depth == 0)
+                    po.found = true;
+                Direct D = shade_direct(P, ro, rd, fin, lv, nshadow);
+                if (depth == 0)
+                    po.shadowed = D.shadowed;
+                if (P.shading_method != RT_SHADING) {
+                    ret = clamp3(D.fc);
+                    state = S_RET;
+                    continue;
+                }
+                const float* m = mat_of(P, fin.mat);
+                if (!(m[12] > 0.0f)) {
+                    ret = shade_finish(P, D.fc, m, col(0, 0, 0));
+                    state = S_RET;
+                    continue;
+                }
+                // compute_reflection prologue, renderer.cpp:285-296
+                Frame& F = fr[depth];
+                F.fc = D.fc;
+                F.mat = fin.mat;
+                F.n = fin.normal;
+                F.ro = D.ip + F.n * 0.01f;
+                F.perfect = rd - (2 * dot(rd, F.n)) * F.n;
+                if (P.enable_roughness_mapping) {
+                    float tu, tv;
+                    get_tex_coords(P, fin.tri, fin.u, fin.v, tu, tv);
+                    F.rough = tex_floor(P.tex[TEX_ROUGHNESS], tu, tv).r;
+                } else
+                    F.rough = m[13];
+                F.i = 0;
+                F.sc = 0;
+                F.total = col(0.0f, 0.0f, 0.0f);
+                F.rhi = rec_fresh();
+                f = depth;
+                state = S_NEXT;
+            } else {
+                float a;
+                ret = miss_color(P, rd, a);
+                if (depth == 0)
+                    po.alpha = a;
+                state = S_RET;
+            }
+        } else if (state == S_RET) {
+            // ---- the trace at 'depth' returned ret ----
+            if (depth == 0)
+                break;
+            Frame& F = fr[depth - 1];
+            F.total = F.total + ret;
+            if (F.rough > 0) {
+                F.sc++;
+                F.i++;
+            } else {
+                F.sc = 1;
+                F.i = N;   // pure specular: break
+            }
+            f = depth - 1;
+            state = S_NEXT;
+        } else {
+            // ---- frame f: next sample, or return the reflection colour ----
+            Frame& F = fr[f];
+            if (F.i < N) {
+                v3 dir;
+                if (F.rough > 0) {
+                    float rx = rng_bilateral(rng);
+                    float ry = rng_bilateral(rng);
+                    float rz = rng_bilateral(rng);
+                    v3 rdir = normalize(mk(rx, ry, rz));
+                    if (dot(rdir, F.n) < 0)
+                        rdir = -rdir;
+                    dir = F.rough * rdir + (1 - F.rough) * F.perfect;
+                } else
+                    dir = F.perfect;
+                nrefl++;
+                ro = F.ro;
+                rd = dir;
+                depth = f + 1;
+                state = S_TRACE;
+            } else {
+                const float* m = mat_of(P, F.mat);
+                float sc = (float)F.sc, rf = m[12];
+                c3 R = (F.total / col(sc, sc, sc)) * col(rf, rf, rf);
+                ret = shade_finish(P, F.fc, m, R);
+                depth = f;
+                state = S_RET;
+            }
+        }
+    }
+    po.color = ret;
+    return po;
 }
 
 // Global internal row of a launch-local row (interleaved bands across ranks).
@@ -783,8 +977,9 @@ __device__ __forceinline__ int swizzled_block()
     return (b % 8) * (nb / 8) + (b / 8);
 }
 
-// Renderer::ray_trace (renderer.cpp:1068-1116) for primary + shadow rays with
-// RT/debug shading, no reflections.
+// Renderer::ray_trace (renderer.cpp:1068-1116): one lane per pixel, one wave
+// per 8x8 tile.
+template <bool REFL>
 __global__ __launch_bounds__(BLOCK) void ray_trace_kernel(KParams P)
 {
     extern __shared__ uint2 lds_levels[];
@@ -811,27 +1006,20 @@ __global__ __launch_bounds__(BLOCK) void ray_trace_kernel(KParams P)
     v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
     v3 rd = normalize(ws - cam);
 
-    Rec fin = rec_fresh();
-    int src = closest_hit(P, cam, rd, fin, lv);
-    c3 c;
-    bool found = false, shadowed = false;
-    float min_t = 0.1f;
-    if (fin.t > min_t) {
-        found = true;
-        ShadeOut s = shade(P, cam, rd, fin, lv);
-        shadowed = s.shadowed;
-        c = s.color;
-        if (P.counters && P.compute_shadows && P.shading_method == RT_SHADING)
-            atomicAdd(&P.counters[0], 1ull);
-    } else
-        c = miss_color(P, rd);
+    unsigned nshadow = 0, nrefl = 0;
+    uint32_t rng = REFL ? pixel_seed((uint32_t)(py * P.rw + px), P.rng_seed) : 0u;
+    PixelOut po = trace_pixel<REFL>(P, cam, rd, lv, rng, nshadow, nrefl);
 
     size_t o = (size_t)lr * P.rw + px;
-    if (P.argb) P.argb[o] = color_to_argb(c);
-    if (P.rgba) P.rgba[o] = make_float4(c.r, c.g, c.b, 1.0f);
-    if (P.hit_id) P.hit_id[o] = found ? src : -1;
-    if (P.hit_t) P.hit_t[o] = fin.t;
-    if (P.shadow) P.shadow[o] = (uint8_t)(found && shadowed);
+    if (P.argb) P.argb[o] = color_to_argb(po.color);
+    if (P.rgba) P.rgba[o] = make_float4(po.color.r, po.color.g, po.color.b, po.alpha);
+    if (P.hit_id) P.hit_id[o] = po.found ? po.src : -1;
+    if (P.hit_t) P.hit_t[o] = po.fin.t;
+    if (P.shadow) P.shadow[o] = (uint8_t)(po.found && po.shadowed);
+    if (P.counters) {
+        if (nshadow) atomicAdd(&P.counters[0], (unsigned long long)nshadow);
+        if (nrefl) atomicAdd(&P.counters[1], (unsigned long long)nrefl);
+    }
 }
 
 // ImageUtils::downscale_image_qt_ARGB32 (imageUtils.h:98-147): integer box
@@ -855,7 +1043,57 @@ __global__ __launch_bounds__(256) void downscale_kernel(const uint32_t* __restri
     out[(size_t)y * dw + x] = qrgb(ar / (f * f), ag / (f * f), ab / (f * f));
 }
 
+// BVH::intersect (bvh.cpp:68-71) for a batch of arbitrary rays: the closest-hit
+// query the reference's trace_ray / is_shadowed issue, exposed for callers and
+// for ray-level parity tests.  Brute-force loop when enable_bvh is off.
+__global__ __launch_bounds__(BLOCK) void trace_rays_kernel(KParams P, const float* __restrict__ orig,
+                                                           const float* __restrict__ dir, int n,
+                                                           int32_t* __restrict__ out_id, float* __restrict__ out_t,
+                                                           float* __restrict__ out_u, float* __restrict__ out_v,
+                                                           uint8_t* __restrict__ out_ret)
+{
+    extern __shared__ uint2 lds_levels[];
+    uint2* lv = lds_levels + threadIdx.x;
+    int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n)
+        return;
+    v3 o = mk(orig[3 * i], orig[3 * i + 1], orig[3 * i + 2]);
+    v3 d = mk(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]);
+    TRay R = make_ray(P, o, d);
+    THit h;
+    bool r;
+    if (P.enable_bvh) {
+        r = bvh_closest(P, R, h, lv);
+    } else {
+        h.t = -1.0f; h.u = 1.0f; h.v = 0.0f; h.k = -1;
+        for (int k = 0; k < P.ntri_slots; k++) {
+            float t, u, v;
+            if (tri_test(P.tris, (uint32_t)k, R, t, u, v))
+                if (t < h.t || h.t == -1) {
+                    h.t = t; h.u = u; h.v = v; h.k = k;
+                }
+        }
+        r = h.k >= 0;
+    }
+    out_id[i] = h.k >= 0 ? P.tri_id[h.k] : -1;
+    out_t[i] = h.t;
+    out_u[i] = h.u;
+    out_v[i] = h.v;
+    out_ret[i] = r ? 1 : 0;
+}
+
 }  // namespace rt
+
+extern "C" hipError_t rt_launch_trace_rays(const rt::KParams* P, const float* o, const float* d, int n, int32_t* id,
+                                           float* t, float* u, float* v, uint8_t* ret, hipStream_t stream)
+{
+    if (n <= 0)
+        return hipSuccess;
+    size_t lds = (size_t)(P->levels > 0 ? P->levels : 1) * rt::BLOCK * sizeof(uint2);
+    hipLaunchKernelGGL(rt::trace_rays_kernel, dim3((n + rt::BLOCK - 1) / rt::BLOCK), dim3(rt::BLOCK), lds, stream, *P,
+                       o, d, n, id, t, u, v, ret);
+    return hipGetLastError();
+}
 
 // ---- host-side launch wrappers (called from renderer.cpp) ----
 extern "C" hipError_t rt_launch_ray_trace(const rt::KParams* P, hipStream_t stream)
@@ -863,7 +1101,10 @@ extern "C" hipError_t rt_launch_ray_trace(const rt::KParams* P, hipStream_t stre
     int tiles = P->tiles_x * P->tiles_y;
     int blocks = (tiles + rt::WAVES_PER_BLOCK - 1) / rt::WAVES_PER_BLOCK;
     size_t lds = (size_t)(P->levels > 0 ? P->levels : 1) * rt::BLOCK * sizeof(uint2);
-    hipLaunchKernelGGL(rt::ray_trace_kernel, dim3(blocks), dim3(rt::BLOCK), lds, stream, *P);
+    if (P->has_reflection)
+        hipLaunchKernelGGL(rt::ray_trace_kernel<true>, dim3(blocks), dim3(rt::BLOCK), lds, stream, *P);
+    else
+        hipLaunchKernelGGL(rt::ray_trace_kernel<false>, dim3(blocks), dim3(rt::BLOCK), lds, stream, *P);
     return hipGetLastError();
 }
 

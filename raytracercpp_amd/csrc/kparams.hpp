@@ -60,6 +60,7 @@ struct KParams {
     int32_t parallax_mapping_steps;
     int32_t enable_roughness_mapping, enable_skysphere, enable_skybox;
     uint32_t rng_seed;
+    int32_t has_reflection;   // RT_SHADING with a material whose reflection > 0: recursive kernel
 
     // image: render size (internal, after the SSAA factor) and this launch's rows
     int32_t rw, rh;

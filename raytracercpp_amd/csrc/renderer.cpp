@@ -8,6 +8,8 @@
 #include "host_scene.hpp"
 
 extern "C" hipError_t rt_launch_ray_trace(const rt::KParams* P, hipStream_t stream);
+extern "C" hipError_t rt_launch_trace_rays(const rt::KParams* P, const float* o, const float* d, int n, int32_t* id,
+                                           float* t, float* u, float* v, uint8_t* ret, hipStream_t stream);
 extern "C" hipError_t rt_launch_downscale(const uint32_t* in, int w, int h_rows, int f, uint32_t* out,
                                           hipStream_t stream);
 
@@ -446,6 +448,14 @@ int Renderer::validate() const
     return RT_OK;
 }
 
+static bool any_reflection(const std::vector<float>& mats)
+{
+    for (size_t i = 0; i + MAT_STRIDE <= mats.size(); i += MAT_STRIDE)
+        if (mats[i + 12] > 0.0f)
+            return true;
+    return false;
+}
+
 void Renderer::fill_params(KParams& P) const
 {
     std::memset(&P, 0, sizeof(P));
@@ -505,24 +515,18 @@ void Renderer::fill_params(KParams& P) const
     P.enable_skysphere = s_.enable_skysphere;
     P.enable_skybox = s_.enable_skybox;
     P.rng_seed = s_.rng_seed;
+    P.has_reflection = s_.shading_method == RT_SHADING && any_reflection(mats_);
     render_size(P.rw, P.rh);
 }
 
-static bool any_reflection(const std::vector<float>& mats)
-{
-    for (size_t i = 0; i + MAT_STRIDE <= mats.size(); i += MAT_STRIDE)
-        if (mats[i + 12] > 0.0f)
-            return true;
-    return false;
-}
 
 // Renderer::ray_trace, renderer.cpp:1068-1116
 int Renderer::ray_trace()
 {
     if (validate() != RT_OK)
         return fail(RT_EINVAL, "invalid scene: material index out of range or enabled texture map missing");
-    if (s_.shading_method == RT_SHADING && any_reflection(mats_))
-        return fail(RT_EUNSUPPORTED, "reflective materials: not implemented yet in this build");
+    if (s_.shading_method == RT_SHADING && any_reflection(mats_) && s_.max_recursion_depth > 15)
+        return fail(RT_EUNSUPPORTED, "reflective materials with max_recursion_depth > 15");
     int rc = ensure_device_scene();
     if (rc != RT_OK)
         return rc;
@@ -687,8 +691,8 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
         return fail(RT_EINVAL, "render_bands_device: bad band layout");
     if (validate() != RT_OK)
         return fail(RT_EINVAL, "invalid scene: material index out of range or enabled texture map missing");
-    if (s_.shading_method == RT_SHADING && any_reflection(mats_))
-        return fail(RT_EUNSUPPORTED, "reflective materials: not implemented yet in this build");
+    if (s_.shading_method == RT_SHADING && any_reflection(mats_) && s_.max_recursion_depth > 15)
+        return fail(RT_EUNSUPPORTED, "reflective materials with max_recursion_depth > 15");
     int rc = ensure_device_scene();
     if (rc != RT_OK)
         return rc;
@@ -726,6 +730,47 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
     if (ring_count_ < EV_RING) ring_count_++;
     if (f > 1 && (e = rt_launch_downscale(target, P.rw, P.local_rows, f, d_out, stream)) != hipSuccess)
         return hip_fail(e, "downscale launch");
+    return RT_OK;
+}
+
+int Renderer::trace_rays(const float* orig, const float* dir, int64_t n, int32_t* id, float* t, float* u, float* v,
+                         uint8_t* ret)
+{
+    if (n < 0 || n > (1 << 30) || (n > 0 && (!orig || !dir || !id || !t || !u || !v || !ret)))
+        return fail(RT_EINVAL, "trace_rays: bad arguments");
+    int rc = ensure_device_scene();
+    if (rc != RT_OK)
+        return rc;
+    if (n == 0)
+        return RT_OK;
+    KParams P;
+    fill_params(P);
+    DevBuf din, dout;
+    din.device = dout.device = device_;
+    size_t nb = (size_t)n;
+    hipError_t e;
+    if ((e = din.reserve(nb * 24)) != hipSuccess || (e = dout.reserve(nb * 17)) != hipSuccess)
+        return hip_fail(e, "hipMalloc (rays)");
+    float* d_o = din.as<float>();
+    float* d_d = d_o + 3 * nb;
+    int32_t* d_id = dout.as<int32_t>();
+    float* d_t = reinterpret_cast<float*>(d_id + nb);
+    float* d_u = d_t + nb;
+    float* d_v = d_u + nb;
+    uint8_t* d_r = reinterpret_cast<uint8_t*>(d_v + nb);
+    if ((e = hipMemcpyAsync(d_o, orig, nb * 12, hipMemcpyHostToDevice, stream_)) != hipSuccess ||
+        (e = hipMemcpyAsync(d_d, dir, nb * 12, hipMemcpyHostToDevice, stream_)) != hipSuccess)
+        return hip_fail(e, "upload (rays)");
+    if ((e = rt_launch_trace_rays(&P, d_o, d_d, (int)n, d_id, d_t, d_u, d_v, d_r, stream_)) != hipSuccess)
+        return hip_fail(e, "trace_rays_kernel launch");
+    if ((e = hipMemcpyAsync(id, d_id, nb * 4, hipMemcpyDeviceToHost, stream_)) != hipSuccess ||
+        (e = hipMemcpyAsync(t, d_t, nb * 4, hipMemcpyDeviceToHost, stream_)) != hipSuccess ||
+        (e = hipMemcpyAsync(u, d_u, nb * 4, hipMemcpyDeviceToHost, stream_)) != hipSuccess ||
+        (e = hipMemcpyAsync(v, d_v, nb * 4, hipMemcpyDeviceToHost, stream_)) != hipSuccess ||
+        (e = hipMemcpyAsync(ret, d_r, nb, hipMemcpyDeviceToHost, stream_)) != hipSuccess)
+        return hip_fail(e, "download (rays)");
+    if ((e = hipStreamSynchronize(stream_)) != hipSuccess)
+        return hip_fail(e, "trace_rays_kernel");
     return RT_OK;
 }
 

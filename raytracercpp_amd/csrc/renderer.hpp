@@ -74,6 +74,9 @@ public:
     // bracketed by HIP events on the launch stream (synchronises on them)
     int kernel_times(float* ms, int n);
     int band_counters(unsigned long long out[2]);
+    // BVH::intersect over n host rays (closest hit, reference semantics)
+    int trace_rays(const float* orig, const float* dir, int64_t n, int32_t* id, float* t, float* u, float* v,
+                   uint8_t* ret);
 
     const std::string& error() const { return err_; }
 

@@ -227,6 +227,18 @@ class Renderer:
         self._call("rt_render_bands_device", int(band_rows), int(rank), int(nranks), C.c_void_p(d_out_ptr),
                    C.c_void_p(stream_ptr))
 
+    def trace_rays(self, orig, dirs):
+        """BVH::intersect for a batch of rays -> (tri_id, t, u, v, ret)."""
+        o = f32(orig).reshape(-1, 3)
+        d = f32(dirs).reshape(-1, 3)
+        n = o.shape[0]
+        ids = np.zeros(n, np.int32)
+        t, u, v = np.zeros(n, np.float32), np.zeros(n, np.float32), np.zeros(n, np.float32)
+        ret = np.zeros(n, np.uint8)
+        self._call("rt_trace_rays", ptr(o, _f32p), ptr(d, _f32p), n, ptr(ids, _i32p), ptr(t, _f32p), ptr(u, _f32p),
+                   ptr(v, _f32p), ptr(ret, _u8p))
+        return ids, t, u, v, ret
+
     def kernel_times(self, n):
         ms = np.zeros(n, np.float32)
         self._call("rt_kernel_times", ptr(ms, _f32p), int(n))

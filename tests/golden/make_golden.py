@@ -1,0 +1,256 @@
+"""Generates the golden fixtures in tests/golden/ from the REFERENCE ITSELF.
+
+Run here (where /root/reference exists and `make -C oracle ref` built
+oracle/_ref/libref_harness.so):   python tests/golden/make_golden.py
+
+Every expected output is produced by ref_harness.cpp, i.e. by the reference's
+own compiled Qt-free translation units (BVH / Triangle / Sphere / Plane / Image /
+Skybox / Transform / Camera / read_meshio_data / create_triangles) driven by the
+restated per-pixel loop of Renderer::ray_trace (renderer.cpp:1068-1116).  Camera
+and object matrices and OBJ triangles also come from the reference code.  The
+fixtures hold only data: scene inputs (or the deterministic generator parameters
+plus a SHA-256 of the triangles) and expected outputs.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle.bindings import RefHarness  # noqa: E402
+from raytracercpp_amd import scenes  # noqa: E402
+from raytracercpp_amd.scene import (SHAPE_PLANE, SHAPE_SPHERE, RenderSettings, SceneData, f32_to_bits,  # noqa: E402
+                                    material, ABS_NORMALS_SHADING, PASTEL_NORMALS_SHADING,
+                                    BARYCENTRIC_COORDINATES_SHADING, VISUALIZE_AO, TEX_AO, TEX_DIFFUSE,
+                                    TEX_NORMAL, TEX_DISPLACEMENT, TEX_ROUGHNESS, TEX_SKYSPHERE)
+
+MAX_INLINE_TRIS = 5000
+
+
+class RefT:
+    """Matrices from the reference's Transform / Camera code."""
+
+    def camera_matrices(self, fov, aspect, znear=0.1, zfar=1000.0):
+        return RefHarness.camera_matrices(fov, aspect, znear, zfar)
+
+    def transform(self, kind, x=0.0, y=0.0, z=0.0):
+        return RefHarness.transform(kind, x, y, z)
+
+    def compose(self, a, b):
+        return RefHarness.compose(a, b)
+
+
+T = RefT()
+
+
+def ref_loader(path, xform):
+    return RefHarness.load_obj(path, xform)
+
+
+def ref_threshold(sc: SceneData):
+    for k in range(sc.materials.shape[0]):
+        sc.materials[k, 15] = RefHarness.specular_threshold(sc.materials[k, 6:9], sc.materials[k, 14])
+
+
+def tex(size, seed, kind="rand"):
+    """Small procedural 8-bit texture, texels = byte * (1/255) as read_image produces."""
+    rng = np.random.default_rng(seed)
+    b = rng.integers(0, 256, size=(size, size, 4)).astype(np.uint8)
+    if kind == "smooth":
+        y, x = np.mgrid[0:size, 0:size]
+        v = (128 + 100 * np.sin(x * 0.3) * np.cos(y * 0.2)).astype(np.uint8)
+        b[..., 0] = b[..., 1] = b[..., 2] = v
+    if kind == "normal":
+        b[..., 2] = np.maximum(b[..., 2], 200)
+    b[..., 3] = 255
+    return b.astype(np.float32) * (np.float32(1.0) / np.float32(255))
+
+
+def uv_sphere_geom(nu, nv, bump, texcoords, xform):
+    tri, uv = scenes.uv_sphere_triangles(nu, nv, bump=bump, texcoords=texcoords)
+    return scenes.transform_triangles(xform, tri), uv
+
+
+def base(w, h, **kw):
+    return scenes.base_settings(w, h, **kw)
+
+
+def camera(st):
+    return scenes._camera(T, st)
+
+
+def build_cases():
+    cases = []
+
+    # C1: analytic sphere, 256x256 (CPU-only config of the reference; plumbing)
+    sc, st = scenes.sphere256(T=T)
+    ref_threshold(sc)
+    cases.append(("c1_sphere256", sc, st, None, []))
+
+    # C2 cube / robot (OBJ through read_meshio_data + create_triangles)
+    for name, fn, gen in (("c2_cube", scenes.cube1080, None), ("robot", scenes.robot1080, None)):
+        sc, st = fn(T=T, width=320, height=180, loader=ref_loader)
+        ref_threshold(sc)
+        sc_big, st_big = fn(T=T, width=1920, height=1080, loader=ref_loader)
+        ref_threshold(sc_big)
+        cases.append((name, sc, st, None, [(sc_big, st_big, [0, 300, 540, 777])]))
+
+    # C3 bumpy 70k (generator + hash)
+    m = scenes.object_transform(T, -3.0, scale=1.2)
+    sc, st = scenes.bumpy70k(T=T, width=320, height=180)
+    ref_threshold(sc)
+    gen = {"kind": "uv_sphere", "nu": 264, "nv": 133, "bump": 0.08, "texcoords": False, "xform": f32_to_bits(m)}
+    sc_big, st_big = scenes.bumpy70k(T=T, width=1920, height=1080)
+    ref_threshold(sc_big)
+    cases.append(("c3_bumpy70k", sc, st, gen, [(sc_big, st_big, [420, 540, 666])]))
+
+    # C4 1M tris, SSAA 2 (small frame + full-resolution sample rows)
+    m = scenes.object_transform(T, -3.0, scale=1.5)
+    gen = {"kind": "uv_sphere", "nu": 1000, "nv": 500, "bump": 0.0, "texcoords": True, "xform": f32_to_bits(m)}
+    sc, st = scenes.sphere1m(T=T, width=160, height=90)
+    ref_threshold(sc)
+    sc_big, st_big = scenes.sphere1m(T=T)
+    ref_threshold(sc_big)
+    cases.append(("c4_sphere1m", sc, st, gen, [(sc_big, st_big, [1000, 1080, 1301])]))
+
+    # textured small sphere: normal + displacement (POM) + AO maps, skybox on misses
+    m = scenes.object_transform(T, -3.0, scale=1.3)
+    tri, uv = uv_sphere_geom(48, 24, 0.05, True, m)
+    st = base(160, 90, enable_normal_mapping=True, enable_displacement_mapping=True, enable_ao_mapping=True,
+              enable_skybox=True, parallax_mapping_steps=16, displacement_mapping_strength=0.05)
+    mats = material(diffuse=(0.7, 0.6, 0.2), specular=(0.5, 0.5, 0.5), ns=30.0)[None]
+    sc = scenes._finish(tri, np.zeros(len(tri), np.int32), uv, mats, camera(st),
+                        textures={TEX_NORMAL: tex(64, 1, "normal"), TEX_DISPLACEMENT: tex(64, 2, "smooth"),
+                                  TEX_AO: tex(32, 3)})
+    sc.skybox = [tex(16, 10 + i) for i in range(6)]
+    ref_threshold(sc)
+    cases.append(("textured", sc, st, None, []))
+
+    # diffuse-map + roughness-map + skysphere
+    st = base(160, 90, enable_diffuse_mapping=True, enable_skysphere=True)
+    sc = scenes._finish(tri, np.zeros(len(tri), np.int32), uv, mats, camera(st),
+                        textures={TEX_DIFFUSE: tex(64, 4), TEX_SKYSPHERE: tex(64, 5, "smooth")})
+    ref_threshold(sc)
+    cases.append(("diffuse_map_skysphere", sc, st, None, []))
+
+    # analytic shapes + mirror / rough reflections + brute force
+    m = scenes.object_transform(T, -4.0, scale=0.8)
+    tri2, uv2 = uv_sphere_geom(32, 16, 0.1, True, m)
+    mats = np.stack([material(diffuse=(0.8, 0.3, 0.3), specular=(0.5, 0.5, 0.5), ns=20.0),
+                     material(diffuse=(0.5, 0.5, 0.5), specular=(0.2, 0.2, 0.2), ns=50.0, reflection=0.9),
+                     material(diffuse=(0.3, 0.8, 0.3), specular=(0.5, 0.5, 0.5), ns=10.0, reflection=0.5,
+                              roughness=0.3)])
+    shapes = (np.array([SHAPE_SPHERE, SHAPE_PLANE], np.int32),
+              np.array([[1.2, 0.2, -3.0, 0.6, 0, 0], [0.0, -1.0, 0.0, 0.0, 1.0, 0.0]], np.float32),
+              np.array([1, 2], np.int32))
+    for name, kw in (("mirror", dict(max_recursion_depth=5)),
+                     ("rough", dict(max_recursion_depth=3, rough_reflections_sample_count=4)),
+                     ("brute_force", dict(enable_bvh=False, max_recursion_depth=2))):
+        st = base(120, 68, **kw)
+        mm = mats.copy()
+        if name == "mirror":
+            mm[2, 13] = 0.0
+        sc = scenes._finish(tri2, np.zeros(len(tri2), np.int32), uv2, mm, camera(st), shapes=shapes)
+        ref_threshold(sc)
+        cases.append((name, sc, st, None, []))
+
+    # debug shading modes on the robot
+    for sm in (ABS_NORMALS_SHADING, PASTEL_NORMALS_SHADING, BARYCENTRIC_COORDINATES_SHADING, VISUALIZE_AO):
+        sc, st = scenes.robot1080(T=T, width=160, height=90, loader=ref_loader, shading_method=sm)
+        ref_threshold(sc)
+        if sm == VISUALIZE_AO:
+            st = st.copy(enable_ao_mapping=True)
+            sc.textures = {TEX_AO: tex(32, 7)}
+        cases.append((f"shading_{sm}", sc, st, None, []))
+
+    # SSAA factor 3 on the cube
+    sc, st = scenes.cube1080(T=T, width=100, height=60, loader=ref_loader, enable_ssaa=True, ssaa_factor=3)
+    ref_threshold(sc)
+    cases.append(("ssaa3_cube", sc, st, None, []))
+    return cases
+
+
+def pack_scene(prefix, sc: SceneData, st: RenderSettings, gen, arrays, meta):
+    meta["settings"] = {k: (float(v) if isinstance(v, float) else int(v)) for k, v in vars(st).items()}
+    meta["tri_sha256"] = sc.triangle_hash()
+    meta["ntri"] = sc.ntri
+    if gen is not None and sc.ntri > MAX_INLINE_TRIS:
+        meta["generator"] = gen
+    else:
+        arrays[prefix + "tri"] = sc.tri
+        if sc.tri_uv is not None:
+            arrays[prefix + "tri_uv"] = sc.tri_uv
+    arrays[prefix + "tri_mat"] = sc.tri_mat
+    for k in ("shape_kind", "shape", "shape_mat", "materials", "cam_pos", "proj_inv", "cam_to_world", "light"):
+        arrays[prefix + k] = getattr(sc, k)
+    for slot, img in (sc.textures or {}).items():
+        arrays[f"{prefix}tex{slot}"] = img
+    if sc.skybox is not None:
+        for i, f in enumerate(sc.skybox):
+            arrays[f"{prefix}sky{i}"] = f
+
+
+def main():
+    manifest = {}
+    for name, sc, st, gen, rows in build_cases():
+        arrays, meta = {}, {"name": name}
+        pack_scene("in_", sc, st, gen, arrays, meta)
+        res = RefHarness.render_rows(sc, st)
+        rw, rh = st.render_size()
+        arrays["out_argb"] = res.argb
+        arrays["out_rgba"] = res.rgba
+        arrays["out_hit_id"] = res.hit_id
+        arrays["out_hit_t"] = res.hit_t
+        arrays["out_shadow"] = res.shadow
+        if st.enable_ssaa:
+            arrays["out_final"] = RefHarness.downscale(res.argb, rw, rh, st.ssaa_factor)
+        meta["counters"] = res.counters
+        meta["row_samples"] = []
+        for j, (sc_big, st_big, row_list) in enumerate(rows):
+            bm = {}
+            pack_scene(f"big{j}_", sc_big, st_big, gen, arrays, bm)
+            for row in row_list:
+                rr = RefHarness.render_rows(sc_big, st_big, row, 1)
+                arrays[f"big{j}_row{row}_argb"] = rr.argb
+                arrays[f"big{j}_row{row}_hit_id"] = rr.hit_id
+                arrays[f"big{j}_row{row}_hit_t"] = rr.hit_t
+                arrays[f"big{j}_row{row}_rgba"] = rr.rgba
+            bm["rows"] = row_list
+            meta["row_samples"].append(bm)
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **arrays)
+        manifest[name] = meta
+        hits = int((res.hit_id != -1).sum())
+        print(f"{name:24s} {rw}x{rh} ntri={sc.ntri} hits={hits} shadow_rays={res.counters['shadow_rays']} "
+              f"refl_rays={res.counters['reflection_rays']}", flush=True)
+
+    # Moller-Trumbore known answers of tp2/projets/tests.cpp:87-124 plus positive cases
+    mt = []
+    tA = [0, 0, 0, 1, 0, 0, 0, 1, 0]
+    tB = [1, -1, -9, -1, -1, -9, -1, -1, -11]
+    tC = [-1, 1, -11, -1, 1, -9, 1, 1, -9]
+    rays = {"ray00": ([0, 0, 0], [-0.577350259, 0.577350259, -0.577350259]), "ray": ([0, 0, -1], [0, 0, 1]),
+            "ray2": ([0, 0, 0], [0.103264742, 0.312963158, -0.944134772]), "rayOut": ([-2, 0, -1], [0, 0, 1]),
+            "rayFront": ([0.2, 0.2, 1], [0, 0, -1]), "rayEdge": ([0.5, 0.0, 1], [0, 0, -1])}
+    for tname, tri in (("triangleA", tA), ("triangleB", tB), ("triangleC", tC)):
+        for rname, (o, d) in rays.items():
+            tuv = np.zeros(3, np.float32)
+            hit = RefHarness.lib().ref_triangle_intersect(np.array(tri, np.float32).ctypes.data_as(
+                __import__("ctypes").POINTER(__import__("ctypes").c_float)),
+                np.array(o, np.float32).ctypes.data_as(__import__("ctypes").POINTER(__import__("ctypes").c_float)),
+                np.array(d, np.float32).ctypes.data_as(__import__("ctypes").POINTER(__import__("ctypes").c_float)),
+                tuv.ctypes.data_as(__import__("ctypes").POINTER(__import__("ctypes").c_float)))
+            mt.append({"tri": tname, "ray": rname, "hit": int(hit), "tuv_bits": f32_to_bits(tuv) if hit else None})
+    manifest["_moller_trumbore"] = {"triangles": {"triangleA": tA, "triangleB": tB, "triangleC": tC},
+                                    "rays": rays, "cases": mt}
+    with open(os.path.join(HERE, "manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

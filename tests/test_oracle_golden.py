@@ -1,0 +1,83 @@
+"""The oracle (oracle.c restatement) against the golden fixtures produced by the
+reference's own compiled code (tests/golden/make_golden.py).  CPU only."""
+import numpy as np
+import pytest
+
+from golden_cases import Case, case_names, manifest
+from oracle.bindings import Oracle
+
+CASES = case_names()
+
+
+def bits(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_oracle_full_frame_matches_reference(name):
+    c = Case(name)
+    exp = c.expected()
+    o = Oracle(c.scene, c.settings)
+    res = o.render_rows()
+    assert np.array_equal(res.hit_id, exp["hit_id"])
+    assert np.array_equal(bits(res.hit_t), bits(exp["hit_t"]))
+    assert np.array_equal(res.shadow, exp["shadow"])
+    assert np.array_equal(res.argb, exp["argb"])
+    assert np.array_equal(bits(res.rgba), bits(exp["rgba"]))
+    assert res.counters["shadow_rays"] == c.meta["counters"]["shadow_rays"]
+    assert res.counters["reflection_rays"] == c.meta["counters"]["reflection_rays"]
+    if c.settings.enable_ssaa:
+        rw, rh = c.settings.render_size()
+        final = Oracle.downscale(res.argb, rw, rh, c.settings.ssaa_factor)
+        assert np.array_equal(final, exp["final"])
+
+
+@pytest.mark.parametrize("name", [n for n in CASES if manifest()[n]["row_samples"]])
+def test_oracle_full_resolution_rows_match_reference(name):
+    c = Case(name)
+    for sc, st, rows in c.row_samples():
+        o = Oracle(sc, st)
+        for row, exp in rows.items():
+            res = o.render_rows(row, 1)
+            assert np.array_equal(res.hit_id, exp["hit_id"]), row
+            assert np.array_equal(bits(res.hit_t), bits(exp["hit_t"])), row
+            assert np.array_equal(res.argb, exp["argb"]), row
+            assert np.array_equal(bits(res.rgba), bits(exp["rgba"])), row
+
+
+def test_moller_trumbore_known_answers():
+    """tests.cpp:87-124 negatives (backface culling, misses) + positive cases, through the oracle."""
+    mt = manifest()["_moller_trumbore"]
+    from raytracercpp_amd.scene import RenderSettings, SceneData, empty_shapes, material
+    for case in mt["cases"]:
+        tri = np.array(mt["triangles"][case["tri"]], np.float32)[None]
+        sk, sh, sm = empty_shapes()
+        sc = SceneData(tri=tri, tri_mat=np.zeros(1, np.int32), tri_uv=None, shape_kind=sk, shape=sh, shape_mat=sm,
+                       materials=material()[None], cam_pos=np.zeros(3, np.float32), proj_inv=np.eye(4, dtype=np.float32).ravel(),
+                       cam_to_world=np.eye(4, dtype=np.float32).ravel(), light=np.zeros(3, np.float32))
+        o = Oracle(sc, RenderSettings())
+        orig, d = mt["rays"][case["ray"]]
+        ids, t, u, v, ret, _ = o.bvh_query(np.array([orig], np.float32), np.array([d], np.float32))
+        assert (ids[0] == 0) == bool(case["hit"]), case
+        if case["hit"]:
+            tuv = np.array(case["tuv_bits"], np.uint32)
+            assert np.array_equal(np.array([t[0], u[0], v[0]], np.float32).view(np.uint32), tuv), case
+
+
+def test_reference_negatives_of_tests_cpp():
+    """The four named negative assertions of tests.cpp:107-112 hold in the fixture."""
+    mt = manifest()["_moller_trumbore"]
+    want_miss = {("triangleA", "ray"), ("triangleA", "rayOut"), ("triangleB", "ray00"), ("triangleC", "ray00")}
+    got = {(c["tri"], c["ray"]) for c in mt["cases"] if not c["hit"]}
+    assert want_miss <= got
+
+
+def test_heap_order_ties_match_libstdcxx():
+    """Emulated std::priority_queue pop order on tied keys (oracle side; GPU side is in the GPU suite)."""
+    rng = np.random.default_rng(1)
+    for _ in range(2000):
+        n = int(rng.integers(1, 9))
+        keys = rng.integers(0, 3, size=n).astype(np.float32)
+        order = Oracle.heap_order(keys)
+        assert sorted(order.tolist()) == list(range(n))
+        assert np.all(np.diff(keys[order]) >= 0)
