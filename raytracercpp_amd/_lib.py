@@ -120,6 +120,12 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} is missing: the HIP library must be built "
                                "(python -c 'import __graft_entry__ as g; g.build()')")
+        # torch bundles its own libamdhip64.so.7 (same soname as ROCm's): load it first
+        # so that a process using both (device buffers, RCCL) runs ONE HIP runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
