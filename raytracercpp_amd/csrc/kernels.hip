@@ -1084,7 +1084,7 @@ __global__ __launch_bounds__(BLOCK) void trace_rays_kernel(KParams P, const floa
 
 }  // namespace rt
 
-extern "C" hipError_t rt_launch_trace_rays(const rt::KParams* P, const float* o, const float* d, int n, int32_t* id,
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_trace_rays(const rt::KParams* P, const float* o, const float* d, int n, int32_t* id,
                                            float* t, float* u, float* v, uint8_t* ret, hipStream_t stream)
 {
     if (n <= 0)
@@ -1096,7 +1096,7 @@ extern "C" hipError_t rt_launch_trace_rays(const rt::KParams* P, const float* o,
 }
 
 // ---- host-side launch wrappers (called from renderer.cpp) ----
-extern "C" hipError_t rt_launch_ray_trace(const rt::KParams* P, hipStream_t stream)
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(const rt::KParams* P, hipStream_t stream)
 {
     int tiles = P->tiles_x * P->tiles_y;
     int blocks = (tiles + rt::WAVES_PER_BLOCK - 1) / rt::WAVES_PER_BLOCK;
@@ -1108,7 +1108,7 @@ extern "C" hipError_t rt_launch_ray_trace(const rt::KParams* P, hipStream_t stre
     return hipGetLastError();
 }
 
-extern "C" hipError_t rt_launch_downscale(const uint32_t* in, int w, int h_rows, int f, uint32_t* out,
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_downscale(const uint32_t* in, int w, int h_rows, int f, uint32_t* out,
                                           hipStream_t stream)
 {
     int dw = w / f, dh = h_rows / f;

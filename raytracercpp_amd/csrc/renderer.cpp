@@ -7,10 +7,10 @@
 
 #include "host_scene.hpp"
 
-extern "C" hipError_t rt_launch_ray_trace(const rt::KParams* P, hipStream_t stream);
-extern "C" hipError_t rt_launch_trace_rays(const rt::KParams* P, const float* o, const float* d, int n, int32_t* id,
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(const rt::KParams* P, hipStream_t stream);
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_trace_rays(const rt::KParams* P, const float* o, const float* d, int n, int32_t* id,
                                            float* t, float* u, float* v, uint8_t* ret, hipStream_t stream);
-extern "C" hipError_t rt_launch_downscale(const uint32_t* in, int w, int h_rows, int f, uint32_t* out,
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_downscale(const uint32_t* in, int w, int h_rows, int f, uint32_t* out,
                                           hipStream_t stream);
 
 namespace rt {

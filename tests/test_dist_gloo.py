@@ -1,0 +1,71 @@
+"""The N>1 image-strip path on CPU: world_size-2 (and 3) gloo process groups, each rank
+renders its interleaved bands (the oracle stands in for the GPU kernel here), one
+all_gather of the padded local buffers, re-assembly on rank 0 -- must equal the
+single-process render (imageUtils.h SSAA blocks stay inside bands)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, band, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import torch
+    import torch.distributed as dist
+    from raytracercpp_amd import scenes, strips
+    from oracle.bindings import Oracle
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sc, st = scenes.robot1080(width=96, height=54, enable_ssaa=True, ssaa_factor=2)
+    rw, rh = st.render_size()
+    f = st.ssaa_factor
+    o = Oracle(sc, st)
+    rows = strips.rank_rows(st.image_height, band, rank, world)
+    local = np.zeros((len(rows), st.image_width), np.uint32)
+    for i, g in enumerate(rows):
+        if g < 0:
+            continue
+        res = o.render_rows(g * f, f, nthreads=1)
+        local[i] = Oracle.downscale(res.argb, rw, f, f)
+    t = torch.from_numpy(local.view(np.int32).copy())
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    if rank == 0:
+        img = strips.assemble([p.numpy().view(np.uint32) for p in parts], st.image_height, band)
+        q.put(img)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,band", [(2, 8), (3, 5)])
+def test_gloo_strips_equal_single_process(world, band):
+    from raytracercpp_amd import scenes
+    from oracle.bindings import Oracle
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, band, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    img = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    sc, st = scenes.robot1080(width=96, height=54, enable_ssaa=True, ssaa_factor=2)
+    rw, rh = st.render_size()
+    full = Oracle(sc, st).render_rows()
+    ref = Oracle.downscale(full.argb, rw, rh, 2).reshape(st.image_height, st.image_width)
+    assert np.array_equal(img, ref)
