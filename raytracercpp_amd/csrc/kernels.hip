@@ -154,8 +154,17 @@ struct THit {
 
 // ---- libstdc++ binary heap (push_heap / pop_heap with std::greater), only
 // used when two pending children have equal t_near. ----
-__device__ __noinline__ uint32_t heap_order(const float key[8], const bool valid[8], const uint32_t rank[8], int n)
+__device__ __noinline__ uint32_t heap_order(float k0, float k1, float k2, float k3, float k4, float k5, float k6,
+                                            float k7, uint32_t validmask, uint32_t mask, int n)
 {
+    // keys arrive in registers; the arrays below exist only on this (rare) path
+    float key[8] = {k0, k1, k2, k3, k4, k5, k6, k7};
+    bool valid[8];
+    uint32_t rank[8];
+    for (int s = 0; s < 8; s++) {
+        valid[s] = (validmask >> s) & 1u;
+        rank[s] = __popc(mask & ((1u << s) - 1u));
+    }
     float hk[8];
     uint32_t hr[8];
     int len = 0;
@@ -304,8 +313,13 @@ __device__ bool bvh_closest(const KParams& P, const TRay& R, THit& h, uint2* lv)
                     }
                     order |= rank[s] << (3 * pos);
                 }
-                if (tie)
-                    order = heap_order(key, valid, rank, n);
+                if (tie) {
+                    uint32_t vm = 0;
+#pragma unroll
+                    for (int s = 0; s < 8; s++)
+                        vm |= (valid[s] ? 1u : 0u) << s;
+                    order = heap_order(key[0], key[1], key[2], key[3], key[4], key[5], key[6], key[7], vm, mask, n);
+                }
                 depth++;
                 any_true &= ~(1u << depth);
                 uint32_t first = a + (order & 7u);
@@ -966,60 +980,53 @@ __device__ __forceinline__ int global_row(const KParams& P, int lr)
     return (band * P.nranks + P.rank) * P.band_rows + (lr - band * P.band_rows);
 }
 
-// XCD-aware tile order: blocks b and b+8 share an XCD, so give every XCD a
-// contiguous run of tiles (neighbouring tiles share octree nodes in its L2).
-__device__ __forceinline__ int swizzled_block()
-{
-    int nb = gridDim.x;
-    int b = blockIdx.x;
-    if (nb % 8 != 0)
-        return b;
-    return (b % 8) * (nb / 8) + (b / 8);
-}
-
 // Renderer::ray_trace (renderer.cpp:1068-1116): one lane per pixel, one wave
-// per 8x8 tile.
+// per 8x8 tile.  Waves are persistent and pull tiles from a device-scope
+// counter (P.counters[2]): shadow-ray-heavy tiles cluster around the object, so
+// a static block -> tile (-> XCD) mapping leaves whole XCDs idle while others
+// still trace; dynamic pulling keeps every CU busy until the queue drains.
 template <bool REFL>
 __global__ __launch_bounds__(BLOCK) void ray_trace_kernel(KParams P)
 {
     extern __shared__ uint2 lds_levels[];
     uint2* lv = lds_levels + threadIdx.x;
-    int wave = threadIdx.x >> 6;
     int lane = threadIdx.x & 63;
-    int tile = swizzled_block() * WAVES_PER_BLOCK + wave;
-    if (tile >= P.tiles_x * P.tiles_y)
-        return;
-    int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
-    int px = tx * 8 + (lane & 7);
-    int lr = ty * 8 + (lane >> 3);
-    if (px >= P.rw || lr >= P.local_rows)
-        return;
-    int py = global_row(P, lr);
-    if (py >= P.rh)
-        return;
-
-    // ray generation, renderer.cpp:1086-1098
-    float y_world = ((float)py + 0.5f) / P.rh * 2 - 1;
-    float x_world = ((float)px + 0.5f) / P.rw * 2 - 1;
-    v3 vs = xform_point(P.proj_inv, mk(x_world, y_world, -1));
-    v3 ws = xform_point(P.cam_to_world, vs);
+    const int ntiles = P.tiles_x * P.tiles_y;
     v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
-    v3 rd = normalize(ws - cam);
-
     unsigned nshadow = 0, nrefl = 0;
-    uint32_t rng = REFL ? pixel_seed((uint32_t)(py * P.rw + px), P.rng_seed) : 0u;
-    PixelOut po = trace_pixel<REFL>(P, cam, rd, lv, rng, nshadow, nrefl);
+    for (;;) {
+        int tile = 0;
+        if (lane == 0)
+            tile = (int)atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[2]), 1u);
+        tile = __builtin_amdgcn_readfirstlane(tile);
+        if (tile >= ntiles)
+            break;
+        int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+        int px = tx * 8 + (lane & 7);
+        int lr = ty * 8 + (lane >> 3);
+        int py = lr < P.local_rows ? global_row(P, lr) : P.rh;
+        if (px >= P.rw || py >= P.rh)
+            continue;
 
-    size_t o = (size_t)lr * P.rw + px;
-    if (P.argb) P.argb[o] = color_to_argb(po.color);
-    if (P.rgba) P.rgba[o] = make_float4(po.color.r, po.color.g, po.color.b, po.alpha);
-    if (P.hit_id) P.hit_id[o] = po.found ? po.src : -1;
-    if (P.hit_t) P.hit_t[o] = po.fin.t;
-    if (P.shadow) P.shadow[o] = (uint8_t)(po.found && po.shadowed);
-    if (P.counters) {
-        if (nshadow) atomicAdd(&P.counters[0], (unsigned long long)nshadow);
-        if (nrefl) atomicAdd(&P.counters[1], (unsigned long long)nrefl);
+        // ray generation, renderer.cpp:1086-1098
+        float y_world = ((float)py + 0.5f) / P.rh * 2 - 1;
+        float x_world = ((float)px + 0.5f) / P.rw * 2 - 1;
+        v3 vs = xform_point(P.proj_inv, mk(x_world, y_world, -1));
+        v3 ws = xform_point(P.cam_to_world, vs);
+        v3 rd = normalize(ws - cam);
+
+        uint32_t rng = REFL ? pixel_seed((uint32_t)(py * P.rw + px), P.rng_seed) : 0u;
+        PixelOut po = trace_pixel<REFL>(P, cam, rd, lv, rng, nshadow, nrefl);
+
+        size_t o = (size_t)lr * P.rw + px;
+        if (P.argb) P.argb[o] = color_to_argb(po.color);
+        if (P.rgba) P.rgba[o] = make_float4(po.color.r, po.color.g, po.color.b, po.alpha);
+        if (P.hit_id) P.hit_id[o] = po.found ? po.src : -1;
+        if (P.hit_t) P.hit_t[o] = po.fin.t;
+        if (P.shadow) P.shadow[o] = (uint8_t)(po.found && po.shadowed);
     }
+    if (nshadow) atomicAdd(&P.counters[0], (unsigned long long)nshadow);
+    if (nrefl) atomicAdd(&P.counters[1], (unsigned long long)nrefl);
 }
 
 // ImageUtils::downscale_image_qt_ARGB32 (imageUtils.h:98-147): integer box
@@ -1100,6 +1107,9 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(
 {
     int tiles = P->tiles_x * P->tiles_y;
     int blocks = (tiles + rt::WAVES_PER_BLOCK - 1) / rt::WAVES_PER_BLOCK;
+    // persistent waves: enough blocks to fill every CU (surplus blocks find the queue empty)
+    if (blocks > P->max_blocks && P->max_blocks > 0)
+        blocks = P->max_blocks;
     size_t lds = (size_t)(P->levels > 0 ? P->levels : 1) * rt::BLOCK * sizeof(uint2);
     if (P->has_reflection)
         hipLaunchKernelGGL(rt::ray_trace_kernel<true>, dim3(blocks), dim3(rt::BLOCK), lds, stream, *P);

@@ -68,6 +68,7 @@ struct KParams {
     int32_t nranks, rank;     // bands b with b % nranks == rank are rendered
     int32_t local_rows;       // rows in this launch's (padded) local buffers
     int32_t tiles_x, tiles_y; // 8x8 tiles over (rw, local_rows)
+    int32_t max_blocks;       // persistent grid size (CUs x resident blocks per CU)
 
     // outputs, indexed by local_row * rw + px (nullptr = not requested)
     uint32_t* argb;
@@ -75,7 +76,7 @@ struct KParams {
     int32_t* hit_id;
     float* hit_t;
     uint8_t* shadow;
-    unsigned long long* counters;   // [0] shadow rays, [1] reflection rays
+    unsigned long long* counters;   // [0] shadow rays, [1] reflection rays, [2] tile queue head
 };
 
 }  // namespace rt

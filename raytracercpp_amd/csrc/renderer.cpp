@@ -62,6 +62,8 @@ int Renderer::init(std::string& err)
     hipError_t e = hipSetDevice(device_);
     if (e == hipSuccess)
         e = hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking);
+    if (e == hipSuccess)
+        e = hipDeviceGetAttribute(&num_cus_, hipDeviceAttributeMultiprocessorCount, device_);
     for (int i = 0; i < 4 && e == hipSuccess; i++)
         e = hipEventCreate(&ev_[i]);
     if (e != hipSuccess) {
@@ -516,6 +518,7 @@ void Renderer::fill_params(KParams& P) const
     P.enable_skybox = s_.enable_skybox;
     P.rng_seed = s_.rng_seed;
     P.has_reflection = s_.shading_method == RT_SHADING && any_reflection(mats_);
+    P.max_blocks = num_cus_ * 8;
     render_size(P.rw, P.rh);
 }
 

@@ -90,6 +90,7 @@ private:
     void fill_params(KParams& P) const;
 
     int device_;
+    int num_cus_ = 256;
     hipStream_t stream_ = nullptr;
     hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};
     std::string err_;
