@@ -13,6 +13,9 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "librt_mi355x.so")
+# development only (tools/variants.py): benchmark an alternative build of the same library
+if os.environ.get("RT_LIB_PATH"):
+    LIB_PATH = os.environ["RT_LIB_PATH"]
 
 RT_OK = 0
 ERRORS = {-1: "RT_EINVAL", -2: "RT_EHIP", -3: "RT_ENOMEM", -4: "RT_ESTATE", -5: "RT_EUNSUPPORTED", -6: "RT_EIO"}

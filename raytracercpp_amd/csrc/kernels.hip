@@ -26,11 +26,50 @@ namespace rt {
 constexpr int WAVES_PER_BLOCK = 4;
 constexpr int BLOCK = 64 * WAVES_PER_BLOCK;
 
+#ifndef RT_OCC
+#define RT_OCC 4
+#endif
+
 struct TRay {
     v3 o, d;
     float den[NPLANES], num[NPLANES];
+#ifdef RT_FASTDIV
+    float rcp[NPLANES];   // refined reciprocal of den[i] (the IEEE division's own y1)
+    bool fast;            // every non-zero den[i] in [2^-40, 2^40]
+#endif
     bool nan;
 };
+
+#ifdef RT_FASTDIV
+// gfx950's IEEE fp32 division (what hipcc emits for a / b) is
+//   v_div_scale(b), v_rcp, v_div_scale(a), e = fma(-b', y0, 1), y1 = fma(e, y0, y0),
+//   q0 = a'*y1, r0 = fma(-b', q0, a'), q1 = fma(r0, y1, q0), r1 = fma(-b', q1, a'),
+//   q2 = div_fmas(r1, y1, q1), div_fixup(q2, b, a).
+// With |a|, |b| in [2^-40, 2^40] (or a == 0) neither operand is scaled, the fmas
+// scale factor is 1 and the fixup is the identity, so the core below returns the
+// same bits; y1 depends on b only and is computed once per ray and plane.
+__device__ __forceinline__ float rcp_refined(float b)
+{
+    float y0 = __builtin_amdgcn_rcpf(b);
+    float e = fmaf(-b, y0, 1.0f);
+    return fmaf(e, y0, y0);
+}
+
+__device__ __forceinline__ bool div_operand_ok(float a)
+{
+    uint32_t e = (__float_as_uint(a) >> 23) & 0xffu;   // biased exponent
+    return (e - 87u) <= 80u || (__float_as_uint(a) & 0x7fffffffu) == 0u;   // 2^-40 <= |a| < 2^41, or 0
+}
+
+__device__ __forceinline__ float div_core(float a, float b, float y)
+{
+    float q0 = a * y;
+    float r0 = fmaf(-b, q0, a);
+    float q1 = fmaf(r0, y, q0);
+    float r1 = fmaf(-b, q1, a);
+    return fmaf(r1, y, q1);
+}
+#endif
 
 // HitInfo (hitInfo.h:8-24) reduced to what the kernels need.
 struct Rec {
@@ -63,6 +102,15 @@ __device__ __forceinline__ TRay make_ray(const KParams& P, v3 o, v3 d)
         nan |= (R.den[i] != R.den[i]) || (R.num[i] != R.num[i]);
     }
     R.nan = nan;
+#ifdef RT_FASTDIV
+    bool fast = true;
+#pragma unroll
+    for (int i = 0; i < NPLANES; i++) {
+        R.rcp[i] = rcp_refined(R.den[i]);
+        fast &= R.den[i] == 0.0f || ((((__float_as_uint(R.den[i]) >> 23) & 0xffu) - 87u) <= 80u);
+    }
+    R.fast = fast;
+#endif
     return R;
 }
 
@@ -96,7 +144,7 @@ __device__ __forceinline__ uint2 load_node_link(const GNode* nodes, uint32_t i)
 // BoundingVolume::intersect, bvh.h:79-105.  t_near only ever grows and t_far
 // only shrinks (std::max / std::min never return a NaN second operand), so
 // testing t_far < t_near once after the loop equals the reference's early exit.
-__device__ __forceinline__ bool vol_test(const NodeBox& n, const TRay& R, float& t_near_out)
+__device__ __forceinline__ bool vol_test_div(const NodeBox& n, const TRay& R, float& t_near_out)
 {
     float t_near = -INFINITY, t_far = INFINITY;
 #pragma unroll
@@ -114,6 +162,46 @@ __device__ __forceinline__ bool vol_test(const NodeBox& n, const TRay& R, float&
     t_near_out = t_near;
     return !(t_far < t_near);
 }
+
+#ifdef RT_FASTDIV
+__device__ __noinline__ bool vol_test_slow(NodeBox n, TRay R, float* t_near_out)
+{
+    float t;
+    bool r = vol_test_div(n, R, t);
+    *t_near_out = t;
+    return r;
+}
+
+__device__ __forceinline__ bool vol_test(const NodeBox& n, const TRay& R, float& t_near_out)
+{
+    float t_near = -INFINITY, t_far = INFINITY;
+    bool ok = R.fast;
+#pragma unroll
+    for (int i = 0; i < NPLANES; i++) {
+        float denom = R.den[i];
+        if (denom != 0.0f) {
+            float a0 = n.dn[i] - R.num[i];
+            float a1 = n.df[i] - R.num[i];
+            ok = ok && div_operand_ok(a0) && div_operand_ok(a1);
+            float d0 = div_core(a0, denom, R.rcp[i]);
+            float d1 = div_core(a1, denom, R.rcp[i]);
+            float lo = denom < 0 ? d1 : d0;
+            float hi = denom < 0 ? d0 : d1;
+            t_near = smax(t_near, lo);
+            t_far = smin(t_far, hi);
+        }
+    }
+    if (!ok)
+        return vol_test_slow(n, R, &t_near_out);
+    t_near_out = t_near;
+    return !(t_far < t_near);
+}
+#else
+__device__ __forceinline__ bool vol_test(const NodeBox& n, const TRay& R, float& t_near_out)
+{
+    return vol_test_div(n, R, t_near_out);
+}
+#endif
 
 // Triangle::intersect (Moller-Trumbore, backface culling), triangle.cpp:25-91
 __device__ __forceinline__ bool tri_test(const GTri* tris, uint32_t k, const TRay& R, float& t_out, float& u_out,
@@ -986,7 +1074,7 @@ __device__ __forceinline__ int global_row(const KParams& P, int lr)
 // a static block -> tile (-> XCD) mapping leaves whole XCDs idle while others
 // still trace; dynamic pulling keeps every CU busy until the queue drains.
 template <bool REFL>
-__global__ __launch_bounds__(BLOCK) void ray_trace_kernel(KParams P)
+__global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
 {
     extern __shared__ uint2 lds_levels[];
     uint2* lv = lds_levels + threadIdx.x;
