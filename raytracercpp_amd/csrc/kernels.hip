@@ -29,6 +29,9 @@ constexpr int BLOCK = 64 * WAVES_PER_BLOCK;
 #ifndef RT_OCC
 #define RT_OCC 4
 #endif
+#ifndef RT_WW
+#define RT_WW 0
+#endif
 
 struct TRay {
     v3 o, d;
@@ -203,16 +206,29 @@ __device__ __forceinline__ bool vol_test(const NodeBox& n, const TRay& R, float&
 }
 #endif
 
-// Triangle::intersect (Moller-Trumbore, backface culling), triangle.cpp:25-91
-__device__ __forceinline__ bool tri_test(const GTri* tris, uint32_t k, const TRay& R, float& t_out, float& u_out,
-                                         float& v_out)
+// Triangle::intersect (Moller-Trumbore, backface culling), triangle.cpp:25-91,
+// split into the 48-byte record load and the test so loads can be batched.
+struct TriRec {
+    float4 q0, q1, q2;
+};
+
+__device__ __forceinline__ TriRec load_tri(const GTri* tris, uint32_t k)
 {
     const float4* p = reinterpret_cast<const float4*>(tris + k);
-    float4 q0 = p[0], q1 = p[1], q2 = p[2];
-    v3 a = mk(q0.x, q0.y, q0.z);
-    v3 ab = mk(q0.w, q1.x, q1.y);
-    v3 ac = mk(q1.z, q1.w, q2.x);
-    v3 n = mk(q2.y, q2.z, q2.w);
+    TriRec r;
+    r.q0 = p[0];
+    r.q1 = p[1];
+    r.q2 = p[2];
+    return r;
+}
+
+__device__ __forceinline__ bool tri_test_rec(const TriRec& T, const TRay& R, float& t_out, float& u_out,
+                                             float& v_out)
+{
+    v3 a = mk(T.q0.x, T.q0.y, T.q0.z);
+    v3 ab = mk(T.q0.w, T.q1.x, T.q1.y);
+    v3 ac = mk(T.q1.z, T.q1.w, T.q2.x);
+    v3 n = mk(T.q2.y, T.q2.z, T.q2.w);
     v3 OA = R.o - a;
     v3 nd = -R.d;
     v3 m = cross(nd, OA);
@@ -233,6 +249,12 @@ __device__ __forceinline__ bool tri_test(const GTri* tris, uint32_t k, const TRa
     u_out = u;
     v_out = v;
     return true;
+}
+
+__device__ __forceinline__ bool tri_test(const GTri* tris, uint32_t k, const TRay& R, float& t_out, float& u_out,
+                                         float& v_out)
+{
+    return tri_test_rec(load_tri(tris, k), R, t_out, u_out, v_out);
 }
 
 struct THit {
@@ -311,153 +333,195 @@ __device__ __noinline__ uint32_t heap_order(float k0, float k1, float k2, float 
     return order;
 }
 
-// BVH::intersect (bvh.cpp:68-71) -> OctreeNode::intersect, iteratively.
-// Returns the reference's boolean; h is the query-global HitInfo (t,u,v,slot).
-// lv: this lane's LDS level stack, entry d at lv[d * BLOCK].
-__device__ bool bvh_closest(const KParams& P, const TRay& R, THit& h, uint2* lv)
+// BVH::intersect (bvh.cpp:68-71) -> OctreeNode::intersect, iteratively, as a
+// resumable traversal: trav_begin runs the root prologue, each trav_step VISITs
+// one node (a leaf's triangles, or an inner node's children) and performs the
+// RETURN unwinding that follows it.  T.live turns false once the root returned;
+// T.r is then the reference's boolean and h the query-global HitInfo
+// (t, u, v, GTri slot).  lv: this lane's LDS level stack, entry d at lv[d * BLOCK].
+struct Trav {
+    uint32_t a, b;       // link word of the node to VISIT next
+    int depth;
+    uint32_t any_true;   // bit d: a child at depth d returned true (closest_inter != INFINITY)
+    bool r, live;
+};
+
+__device__ __forceinline__ void trav_begin(const KParams& P, const TRay& R, THit& h, Trav& T)
 {
     h.t = -1.0f;
     h.u = 1.0f;
     h.v = 0.0f;
     h.k = -1;
+    T.r = false;
+    T.live = false;
     if (P.nnodes == 0)
-        return false;
+        return;
     if (R.nan) {
         // every volume passes with t_near = -inf, every triangle "hits" with
         // t = NaN and no leaf ever returns true: the query returns false with
         // a NaN record (NaN rays).
         h.t = __int_as_float(0x7fc00000);
-        return false;
+        return;
     }
     float tn;
     NodeBox nb = load_node(P.nodes, 0);
     if (!vol_test(nb, R, tn))
-        return false;
+        return;
+    T.a = nb.a;
+    T.b = nb.b;
+    T.depth = 0;
+    T.any_true = 0;
+    T.live = true;
+}
 
-    uint32_t a = nb.a, b = nb.b;
-    int depth = 0;
-    uint32_t any_true = 0;
+__device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit& h, Trav& T, uint2* lv)
+{
+    uint32_t a = T.a, b = T.b;
+    int depth = T.depth;
+    uint32_t any_true = T.any_true;
     bool r = false;
-    for (;;) {
-        // ---- VISIT the node whose link word is (a, b) at 'depth' ----
-        bool ret;
-        if (b & LEAF_BIT) {
-            uint32_t cnt = b & ~LEAF_BIT;
-            for (uint32_t k = a; k < a + cnt; k++) {
-                float t, u, v;
-                if (tri_test(P.tris, k, R, t, u, v))
-                    if (t < h.t || h.t == -1) {
-                        h.t = t;
-                        h.u = u;
-                        h.v = v;
-                        h.k = (int)k;
-                    }
+    // ---- VISIT the node whose link word is (a, b) at 'depth' ----
+    if (b & LEAF_BIT) {
+        uint32_t end = a + (b & ~LEAF_BIT);
+        // triangles in leaf order, h updated as in bvh.h:237-243
+        for (uint32_t k = a; k < end; k++) {
+            float t, u, v;
+            if (tri_test(P.tris, k, R, t, u, v))
+                if (t < h.t || h.t == -1) {
+                    h.t = t;
+                    h.u = u;
+                    h.v = v;
+                    h.k = (int)k;
+                }
+        }
+        r = h.t > 0;
+    } else {
+        uint32_t mask = b & 0xffu;
+        float key[8];
+        bool valid[8];
+        uint32_t rank[8];
+        int n = 0;
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            rank[s] = __popc(mask & ((1u << s) - 1u));
+            valid[s] = false;
+            key[s] = INFINITY;
+            if (mask & (1u << s)) {
+                NodeBox c = load_node(P.nodes, a + rank[s]);
+                float t;
+                if (vol_test(c, R, t)) {
+                    valid[s] = true;
+                    key[s] = t;
+                    n++;
+                }
             }
-            r = h.t > 0;
-            ret = true;
-        } else {
-            uint32_t mask = b & 0xffu;
-            float key[8];
-            bool valid[8];
-            uint32_t rank[8];
-            int n = 0;
+        }
+        if (n > 0) {
+            uint32_t order = 0;
+            bool tie = false;
 #pragma unroll
             for (int s = 0; s < 8; s++) {
-                rank[s] = __popc(mask & ((1u << s) - 1u));
-                valid[s] = false;
-                key[s] = INFINITY;
-                if (mask & (1u << s)) {
-                    NodeBox c = load_node(P.nodes, a + rank[s]);
-                    float t;
-                    if (vol_test(c, R, t)) {
-                        valid[s] = true;
-                        key[s] = t;
-                        n++;
-                    }
-                }
-            }
-            if (n == 0) {
-                r = false;
-                ret = true;
-            } else {
-                uint32_t order = 0;
-                bool tie = false;
+                if (!valid[s])
+                    continue;
+                uint32_t pos = 0;
 #pragma unroll
-                for (int s = 0; s < 8; s++) {
-                    if (!valid[s])
+                for (int t2 = 0; t2 < 8; t2++) {
+                    if (t2 == s || !valid[t2])
                         continue;
-                    uint32_t pos = 0;
-#pragma unroll
-                    for (int t2 = 0; t2 < 8; t2++) {
-                        if (t2 == s || !valid[t2])
-                            continue;
-                        if (key[t2] < key[s])
+                    if (key[t2] < key[s])
+                        pos++;
+                    else if (key[t2] == key[s]) {
+                        tie = true;
+                        if (t2 < s)
                             pos++;
-                        else if (key[t2] == key[s]) {
-                            tie = true;
-                            if (t2 < s)
-                                pos++;
-                        }
                     }
-                    order |= rank[s] << (3 * pos);
                 }
-                if (tie) {
-                    uint32_t vm = 0;
+                order |= rank[s] << (3 * pos);
+            }
+            if (tie) {
+                uint32_t vm = 0;
 #pragma unroll
-                    for (int s = 0; s < 8; s++)
-                        vm |= (valid[s] ? 1u : 0u) << s;
-                    order = heap_order(key[0], key[1], key[2], key[3], key[4], key[5], key[6], key[7], vm, mask, n);
-                }
-                depth++;
-                any_true &= ~(1u << depth);
-                uint32_t first = a + (order & 7u);
-                lv[depth * BLOCK] = make_uint2(a, (order >> 3) | ((uint32_t)(n - 1) << 24));
-                uint2 link = load_node_link(P.nodes, first);
-                a = link.x;
-                b = link.y;
-                ret = false;
+                for (int s = 0; s < 8; s++)
+                    vm |= (valid[s] ? 1u : 0u) << s;
+                order = heap_order(key[0], key[1], key[2], key[3], key[4], key[5], key[6], key[7], vm, mask, n);
             }
+            depth++;
+            any_true &= ~(1u << depth);
+            uint32_t first = a + (order & 7u);
+            lv[depth * BLOCK] = make_uint2(a, (order >> 3) | ((uint32_t)(n - 1) << 24));
+            uint2 link = load_node_link(P.nodes, first);
+            T.a = link.x;
+            T.b = link.y;
+            T.depth = depth;
+            T.any_true = any_true;
+            return;
         }
-        if (!ret)
-            continue;
-        // ---- RETURN r from the node at 'depth' to its parent ----
-        for (;;) {
-            if (depth == 0)
-                return r;
-            uint2 e = lv[depth * BLOCK];
-            uint32_t cnt = e.y >> 24;
-            uint32_t ord = e.y & 0xffffffu;
-            if (r) {
-                any_true |= 1u << depth;
-                if (cnt == 0) {
-                    depth--;
-                    continue;   // queue empty: parent returns true
-                }
-                NodeBox nx = load_node(P.nodes, e.x + (ord & 7u));
-                float t_next;
-                vol_test(nx, R, t_next);
-                if (h.t < t_next) {
-                    depth--;    // closest hit nearer than the next child: parent returns true
-                    continue;
-                }
-                lv[depth * BLOCK] = make_uint2(e.x, (ord >> 3) | ((cnt - 1) << 24));
-                a = nx.a;
-                b = nx.b;
-                break;
-            } else {
-                if (cnt == 0) {
-                    r = (any_true >> depth) & 1u;   // closest_inter != INFINITY
-                    depth--;
-                    continue;
-                }
-                uint2 link = load_node_link(P.nodes, e.x + (ord & 7u));
-                lv[depth * BLOCK] = make_uint2(e.x, (ord >> 3) | ((cnt - 1) << 24));
-                a = link.x;
-                b = link.y;
-                break;
+        r = false;
+    }
+    // ---- RETURN r from the node at 'depth' to its parent ----
+    for (;;) {
+        if (depth == 0) {
+            T.r = r;
+            T.live = false;
+            return;
+        }
+        uint2 e = lv[depth * BLOCK];
+        uint32_t cnt = e.y >> 24;
+        uint32_t ord = e.y & 0xffffffu;
+        if (r) {
+            any_true |= 1u << depth;
+            if (cnt == 0) {
+                depth--;
+                continue;   // queue empty: parent returns true
             }
+            NodeBox nx = load_node(P.nodes, e.x + (ord & 7u));
+            float t_next;
+            vol_test(nx, R, t_next);
+            if (h.t < t_next) {
+                depth--;    // closest hit nearer than the next child: parent returns true
+                continue;
+            }
+            lv[depth * BLOCK] = make_uint2(e.x, (ord >> 3) | ((cnt - 1) << 24));
+            a = nx.a;
+            b = nx.b;
+            break;
+        } else {
+            if (cnt == 0) {
+                r = (any_true >> depth) & 1u;   // closest_inter != INFINITY
+                depth--;
+                continue;
+            }
+            uint2 link = load_node_link(P.nodes, e.x + (ord & 7u));
+            lv[depth * BLOCK] = make_uint2(e.x, (ord >> 3) | ((cnt - 1) << 24));
+            a = link.x;
+            b = link.y;
+            break;
         }
     }
+    T.a = a;
+    T.b = b;
+    T.depth = depth;
+    T.any_true = any_true;
+}
+
+__device__ bool bvh_closest(const KParams& P, const TRay& R, THit& h, uint2* lv)
+{
+    Trav T;
+    trav_begin(P, R, h, T);
+#if RT_WW
+    // while-while: lanes at inner nodes keep expanding until every lane of the
+    // wave sits on a leaf (or is done), then the leaves are tested together
+    while (T.live) {
+        while (T.live && !(T.b & LEAF_BIT))
+            trav_step(P, R, h, T, lv);
+        if (T.live)
+            trav_step(P, R, h, T, lv);
+    }
+#else
+    while (T.live)
+        trav_step(P, R, h, T, lv);
+#endif
+    return T.r;
 }
 
 // HitInfo filled by Triangle::intersect for slot k (triangle.cpp:81-88)
@@ -669,6 +733,26 @@ __device__ void parallax_occlusion_mapping(const KParams& P, int tri, float u, f
     nv = (1 - w) * v2 + w * pv;
 }
 
+// The analytic-shape part of is_shadowed (renderer.cpp:385-399); the shapes
+// read the HitInfo the BVH query left behind (t_stale).
+__device__ __forceinline__ bool shapes_shadow(const KParams& P, v3 o, v3 d, float t_stale, v3 p, v3 lp)
+{
+    if (P.nshape > 0) {
+        Rec hi = rec_fresh();
+        hi.t = t_stale;
+        for (int k = 0; k < P.nshape; k++) {
+            bool hk = P.shape_kind[k] == 0 ? sphere_test(P.shape[k], P.shape_mat[k], o, d, hi)
+                                           : plane_test(P.shape[k], P.shape_mat[k], o, d, hi);
+            if (hk) {
+                v3 q = o + d * hi.t;
+                if (length2(p - q) < length2(p - lp))
+                    return true;
+            }
+        }
+    }
+    return false;
+}
+
 // renderer.cpp:340-402
 __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
 {
@@ -698,24 +782,38 @@ __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
             }
         }
     }
-    if (P.nshape > 0) {
-        Rec hi = rec_fresh();
-        hi.t = h.t;
-        for (int k = 0; k < P.nshape; k++) {
-            bool hk = P.shape_kind[k] == 0 ? sphere_test(P.shape[k], P.shape_mat[k], o, d, hi)
-                                           : plane_test(P.shape[k], P.shape_mat[k], o, d, hi);
-            if (hk) {
-                v3 q = o + d * hi.t;
-                if (length2(p - q) < length2(p - lp))
-                    return true;
-            }
-        }
-    }
-    return false;
+    return shapes_shadow(P, o, d, h.t, p, lp);
 }
 
 // BACKGROUND_COLOR, renderer.cpp:19
 __device__ __forceinline__ c3 background() { return col(135.0f / 255.0f, 206.0f / 255.0f, 235.0f / 255.0f); }
+
+// The BVH branch of trace_ray (renderer.cpp:1015-1020): the query-global
+// HitInfo becomes 'local'; fin takes it when the query returned true and it is nearer.
+__device__ __forceinline__ void bvh_record(const KParams& P, const THit& h, bool r, Rec& local, Rec& fin, int& src)
+{
+    if (h.k >= 0)
+        local = tri_record(P, h);
+    else if (h.t != h.t)
+        local.t = h.t;   // NaN ray: stale NaN record
+    if (r && (local.t < fin.t || fin.t == -1)) {
+        fin = local;
+        src = local.tri;
+    }
+}
+
+// The analytic-shape loop of trace_ray (renderer.cpp:1029-1036), reusing 'local'.
+__device__ __forceinline__ void shapes_closest(const KParams& P, v3 o, v3 d, Rec& local, Rec& fin, int& src)
+{
+    for (int k = 0; k < P.nshape; k++) {
+        bool hk = P.shape_kind[k] == 0 ? sphere_test(P.shape[k], P.shape_mat[k], o, d, local)
+                                       : plane_test(P.shape[k], P.shape_mat[k], o, d, local);
+        if (hk && (local.t < fin.t || fin.t == -1)) {
+            fin = local;
+            src = -2 - k;
+        }
+    }
+}
 
 // Closest hit over the BVH then the analytic shapes (renderer.cpp:1015-1037).
 // fin is the caller's HitInfo; returns the source (-1 none, >=0 triangle, -2-k shape k).
@@ -727,14 +825,7 @@ __device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv)
     if (P.enable_bvh) {
         THit h;
         bool r = bvh_closest(P, R, h, lv);
-        if (h.k >= 0)
-            local = tri_record(P, h);
-        else if (h.t != h.t)
-            local.t = h.t;   // NaN ray: stale NaN record
-        if (r && (local.t < fin.t || fin.t == -1)) {
-            fin = local;
-            src = local.tri;
-        }
+        bvh_record(P, h, r, local, fin, src);
     } else {
         // brute-force loop, renderer.cpp:1021-1027: fin takes every hit nearer
         // than itself; local keeps the last triangle that was hit.
@@ -759,14 +850,7 @@ __device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv)
         if (last.k >= 0)
             local = tri_record(P, last);
     }
-    for (int k = 0; k < P.nshape; k++) {
-        bool hk = P.shape_kind[k] == 0 ? sphere_test(P.shape[k], P.shape_mat[k], o, d, local)
-                                       : plane_test(P.shape[k], P.shape_mat[k], o, d, local);
-        if (hk && (local.t < fin.t || fin.t == -1)) {
-            fin = local;
-            src = -2 - k;
-        }
-    }
+    shapes_closest(P, o, d, local, fin, src);
     return src;
 }
 
@@ -782,62 +866,67 @@ struct Direct {
     bool shadowed;
 };
 
-__device__ Direct shade_direct(const KParams& P, v3 ro, v3 rd, Rec& h, uint2* lv, unsigned& nshadow)
+// RT_SHADING up to the shadow test: diffuse + specular at the hit (renderer.cpp:556-590).
+__device__ c3 shade_lit(const KParams& P, v3 ro, v3 rd, Rec& h, v3& ip_out)
 {
-    Direct out;
-    out.shadowed = false;
-    out.ip = mk(0, 0, 0);
     c3 fc = col(0.0f, 0.0f, 0.0f);
-    if (P.shading_method == RT_SHADING) {
-        float u = h.u, v = h.v;
-        v3 ip = ro + rd * h.t;
-        out.ip = ip;
-        v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
-        v3 light = mk(P.light[0], P.light[1], P.light[2]);
-        if (P.enable_displacement_mapping)
-            parallax_occlusion_mapping(P, h.tri, h.u, h.v, normalize(cam - ip), u, v);
-        v3 dl = normalize(light - ip);
-        if (P.enable_normal_mapping)
-            h.normal = normal_mapping(P, h, u, v);
-        const float* m = mat_of(P, h.mat);
-        float ao = 1.0f;
-        if (P.enable_ao_mapping) {
-            float tu, tv;
-            get_tex_coords(P, h.tri, u, v, tu, tv);
-            ao = tex_floor(P.tex[TEX_AO], tu, tv).r;
+    float u = h.u, v = h.v;
+    v3 ip = ro + rd * h.t;
+    ip_out = ip;
+    v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+    v3 light = mk(P.light[0], P.light[1], P.light[2]);
+    if (P.enable_displacement_mapping)
+        parallax_occlusion_mapping(P, h.tri, h.u, h.v, normalize(cam - ip), u, v);
+    v3 dl = normalize(light - ip);
+    if (P.enable_normal_mapping)
+        h.normal = normal_mapping(P, h, u, v);
+    const float* m = mat_of(P, h.mat);
+    float ao = 1.0f;
+    if (P.enable_ao_mapping) {
+        float tu, tv;
+        get_tex_coords(P, h.tri, u, v, tu, tv);
+        ao = tex_floor(P.tex[TEX_AO], tu, tv).r;
+    }
+    c3 dc;
+    if (P.enable_diffuse_mapping) {
+        float tu, tv;
+        get_tex_coords(P, h.tri, u, v, tu, tv);
+        dc = tex_floor(P.tex[TEX_DIFFUSE], tu, tv);
+        float f = smax(0.5f, dot(h.normal, normalize(cam - ip)));
+        dc = dc * col(f, f, f);
+    } else {
+        float f = smax(0.0f, dot(h.normal, dl));   // compute_diffuse, :263-266
+        dc = mat_col(m, 3) * col(f, f, f);
+    }
+    fc = fc + (dc * ao) * (float)(P.enable_diffuse != 0);
+    c3 spec;   // compute_specular, :270-280
+    {
+        v3 hv = normalize(dl - rd);
+        float angle = dot(hv, h.normal);
+        if (angle <= m[15])
+            spec = col(0, 0, 0);
+        else {
+            float pw = powf(smax(0.0f, angle), m[14]);
+            spec = mat_col(m, 6) * col(pw, pw, pw);
         }
-        c3 dc;
-        if (P.enable_diffuse_mapping) {
-            float tu, tv;
-            get_tex_coords(P, h.tri, u, v, tu, tv);
-            dc = tex_floor(P.tex[TEX_DIFFUSE], tu, tv);
-            float f = smax(0.5f, dot(h.normal, normalize(cam - ip)));
-            dc = dc * col(f, f, f);
-        } else {
-            float f = smax(0.0f, dot(h.normal, dl));   // compute_diffuse, :263-266
-            dc = mat_col(m, 3) * col(f, f, f);
-        }
-        fc = fc + (dc * ao) * (float)(P.enable_diffuse != 0);
-        c3 spec;   // compute_specular, :270-280
-        {
-            v3 hv = normalize(dl - rd);
-            float angle = dot(hv, h.normal);
-            if (angle <= m[15])
-                spec = col(0, 0, 0);
-            else {
-                float pw = powf(smax(0.0f, angle), m[14]);
-                spec = mat_col(m, 6) * col(pw, pw, pw);
-            }
-        }
-        fc = fc + spec * (float)(P.enable_specular != 0);
-        if (P.compute_shadows)
-            nshadow++;
-        bool sh = is_shadowed(P, ip, h.normal, light, lv);
-        out.shadowed = sh;
-        if (sh)
-            fc = fc * col(0.5f, 0.5f, 0.5f);
-        fc = fc + mat_col(m, 9) * (float)(P.enable_emissive != 0);
-    } else if (P.shading_method == ABS_NORMALS) {
+    }
+    fc = fc + spec * (float)(P.enable_specular != 0);
+    return fc;
+}
+
+// renderer.cpp:591-593: halve when shadowed, add the emission.
+__device__ __forceinline__ c3 shade_shadow_emit(const KParams& P, c3 fc, const float* m, bool shadowed)
+{
+    if (shadowed)
+        fc = fc * col(0.5f, 0.5f, 0.5f);
+    return fc + mat_col(m, 9) * (float)(P.enable_emissive != 0);
+}
+
+// debug shading methods (renderer.cpp:596-613); the returned colour is final.
+__device__ c3 shade_debug(const KParams& P, const Rec& h)
+{
+    c3 fc = col(0.0f, 0.0f, 0.0f);
+    if (P.shading_method == ABS_NORMALS) {
         fc = col(fabsf(h.normal.x), fabsf(h.normal.y), fabsf(h.normal.z));
     } else if (P.shading_method == PASTEL_NORMALS) {
         fc = (col(h.normal.x, h.normal.y, h.normal.z) + col(1.0f, 1.0f, 1.0f)) * 0.5f;
@@ -853,7 +942,23 @@ __device__ Direct shade_direct(const KParams& P, v3 ro, v3 rd, Rec& h, uint2* lv
         }
         fc = c;
     }
-    out.fc = fc;
+    return fc;
+}
+
+__device__ Direct shade_direct(const KParams& P, v3 ro, v3 rd, Rec& h, uint2* lv, unsigned& nshadow)
+{
+    Direct out;
+    out.shadowed = false;
+    out.ip = mk(0, 0, 0);
+    if (P.shading_method == RT_SHADING) {
+        c3 fc = shade_lit(P, ro, rd, h, out.ip);
+        if (P.compute_shadows)
+            nshadow++;
+        v3 light = mk(P.light[0], P.light[1], P.light[2]);
+        out.shadowed = is_shadowed(P, out.ip, h.normal, light, lv);
+        out.fc = shade_shadow_emit(P, fc, mat_of(P, h.mat), out.shadowed);
+    } else
+        out.fc = shade_debug(P, h);
     return out;
 }
 
@@ -1117,6 +1222,176 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
     if (nrefl) atomicAdd(&P.counters[1], (unsigned long long)nrefl);
 }
 
+// Pixel q of the launch (tile-major: q = tile * 64 + 8 * y + x inside the 8x8
+// tile) -> column and launch-local row.
+__device__ __forceinline__ void tile_pixel(const KParams& P, uint32_t q, int& px, int& lr)
+{
+    uint32_t tile = q >> 6, w = q & 63u;
+    px = (int)(tile % (uint32_t)P.tiles_x) * 8 + (int)(w & 7u);
+    lr = (int)(tile / (uint32_t)P.tiles_x) * 8 + (int)(w >> 3);
+}
+
+__device__ __forceinline__ void write_pixel(const KParams& P, uint32_t q, c3 c, float alpha, int id, float t, bool sh)
+{
+    int px, lr;
+    tile_pixel(P, q, px, lr);
+    size_t o = (size_t)lr * P.rw + px;
+    if (P.argb) P.argb[o] = color_to_argb(c);
+    if (P.rgba) P.rgba[o] = make_float4(c.r, c.g, c.b, alpha);
+    if (P.hit_id) P.hit_id[o] = id;
+    if (P.hit_t) P.hit_t[o] = t;
+    if (P.shadow) P.shadow[o] = (uint8_t)sh;
+}
+
+#ifndef RT_REFILL
+#define RT_REFILL 1
+#endif
+
+// Renderer::ray_trace for scenes without reflections (BVH on), as a per-lane
+// pipeline.  Every lane owns one pixel at a time and walks it through
+//   PRIM: primary-ray traversal -> trace_ray's closest hit + shade_lit
+//   SHAD: shadow-ray traversal  -> is_shadowed + emission + ambient -> framebuffer
+// and takes the next pixel as soon as its own pixel is written.  Both ray kinds
+// advance through the same trav_step, one octree node per lane per iteration,
+// so a wave never idles while one lane's ray is still deep in the octree (the
+// tile-per-wave kernel runs every tile for as long as its slowest ray).  Pixels
+// are handed out in tile order from the device-scope queue, 64 per atomic, so
+// the rays in flight in one wave stay spatially coherent.  Per pixel the
+// results are those of trace_pixel<false>: the same functions in the same order.
+enum : int { ST_IDLE = 0, ST_PRIM = 1, ST_SHAD = 2, ST_NEW = 3, ST_EXIT = 4 };
+
+__global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_pipe_kernel(KParams P)
+{
+    extern __shared__ uint2 lds_levels[];
+    uint2* lv = lds_levels + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const uint32_t ntiles = (uint32_t)(P.tiles_x * P.tiles_y);
+    const v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+    const v3 light = mk(P.light[0], P.light[1], P.light[2]);
+    unsigned nshadow = 0;
+
+    int stage = ST_IDLE;
+    bool drained = false;        // wave-uniform: the pixel queue is empty
+    uint32_t cur = 0, end = 0;   // wave-uniform: unassigned pixels [cur, end) of the wave's tile
+    uint32_t q = 0;              // this lane's pixel
+    TRay R;
+    THit h;
+    Trav T;
+    T.live = false;
+    // state carried from the primary hit to the end of its shadow ray
+    v3 ip = mk(0, 0, 0);
+    c3 fc = col(0, 0, 0);
+    int mat = 0, src = -1;
+    float fin_t = 0.0f;
+
+    for (;;) {
+        // ---- a traversal has returned ----
+        if (stage == ST_PRIM && !T.live) {
+            Rec fin = rec_fresh(), local = rec_fresh();
+            int s = -1;
+            bvh_record(P, h, T.r, local, fin, s);
+            shapes_closest(P, cam, R.d, local, fin, s);
+            if (fin.t > 0.1f) {
+                if (P.shading_method == RT_SHADING) {
+                    fc = shade_lit(P, cam, R.d, fin, ip);
+                    mat = fin.mat;
+                    src = s;
+                    fin_t = fin.t;
+                    if (P.compute_shadows) {
+                        // is_shadowed (renderer.cpp:340-345): the shadow ray's query
+                        nshadow++;
+                        R = make_ray(P, ip + fin.normal * 1.0e-4f, normalize(light - ip));
+                        trav_begin(P, R, h, T);
+                        stage = ST_SHAD;
+                    } else {
+                        const float* m = mat_of(P, mat);
+                        write_pixel(P, q, shade_finish(P, shade_shadow_emit(P, fc, m, false), m, col(0, 0, 0)), 1.0f,
+                                    src, fin_t, false);
+                        stage = ST_IDLE;
+                    }
+                } else {
+                    write_pixel(P, q, clamp3(shade_debug(P, fin)), 1.0f, s, fin.t, false);
+                    stage = ST_IDLE;
+                }
+            } else {
+                float alpha;
+                c3 c = miss_color(P, R.d, alpha);
+                write_pixel(P, q, c, alpha, -1, fin.t, false);
+                stage = ST_IDLE;
+            }
+        } else if (stage == ST_SHAD && !T.live) {
+            // is_shadowed (renderer.cpp:346-401) on the finished query
+            bool sh = false;
+            if (T.r) {
+                v3 qq = R.o + R.d * h.t;
+                sh = length2(ip - qq) < length2(ip - light);
+            }
+            if (!sh)
+                sh = shapes_shadow(P, R.o, R.d, h.t, ip, light);
+            const float* m = mat_of(P, mat);
+            write_pixel(P, q, shade_finish(P, shade_shadow_emit(P, fc, m, sh), m, col(0, 0, 0)), 1.0f, src, fin_t, sh);
+            stage = ST_IDLE;
+        }
+
+        // ---- hand out pixels to idle lanes (wave-uniform control flow) ----
+        uint64_t idle = __ballot(stage == ST_IDLE);
+        if (idle && !drained && (__popcll(idle) >= RT_REFILL || __ballot(T.live) == 0)) {
+            for (;;) {
+                if (cur >= end) {
+                    uint32_t t = 0;
+                    if (lane == 0)
+                        t = atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[2]), 1u);
+                    t = __builtin_amdgcn_readfirstlane(t);
+                    if (t >= ntiles) {
+                        drained = true;
+                        break;
+                    }
+                    cur = t * 64u;
+                    end = cur + 64u;
+                }
+                uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                uint32_t avail = end - cur;
+                if (stage == ST_IDLE && rank < avail) {
+                    q = cur + rank;
+                    stage = ST_NEW;
+                }
+                uint32_t n = (uint32_t)__popcll(idle);
+                cur += n < avail ? n : avail;
+                idle = __ballot(stage == ST_IDLE);
+                if (!idle)
+                    break;
+            }
+        }
+        if (drained && stage == ST_IDLE)
+            stage = ST_EXIT;
+        if (stage == ST_NEW) {
+            int px, lr;
+            tile_pixel(P, q, px, lr);
+            int py = lr < P.local_rows ? global_row(P, lr) : P.rh;
+            if (px < P.rw && py < P.rh) {
+                // ray generation, renderer.cpp:1086-1098
+                float y_world = ((float)py + 0.5f) / P.rh * 2 - 1;
+                float x_world = ((float)px + 0.5f) / P.rw * 2 - 1;
+                v3 vs = xform_point(P.proj_inv, mk(x_world, y_world, -1));
+                v3 ws = xform_point(P.cam_to_world, vs);
+                R = make_ray(P, cam, normalize(ws - cam));
+                trav_begin(P, R, h, T);
+                stage = ST_PRIM;
+            } else
+                stage = drained ? ST_EXIT : ST_IDLE;   // tile padding
+        }
+        if (__ballot(stage != ST_EXIT) == 0)
+            break;
+
+        // ---- one octree node for every lane with a ray in flight ----
+        if (T.live)
+            trav_step(P, R, h, T, lv);
+    }
+    if (nshadow)
+        atomicAdd(&P.counters[0], (unsigned long long)nshadow);
+}
+
 // ImageUtils::downscale_image_qt_ARGB32 (imageUtils.h:98-147): integer box
 // filter of 8-bit channels, truncating division.
 __global__ __launch_bounds__(256) void downscale_kernel(const uint32_t* __restrict__ in, int w, int h_rows, int f,
@@ -1201,6 +1476,8 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(
     size_t lds = (size_t)(P->levels > 0 ? P->levels : 1) * rt::BLOCK * sizeof(uint2);
     if (P->has_reflection)
         hipLaunchKernelGGL(rt::ray_trace_kernel<true>, dim3(blocks), dim3(rt::BLOCK), lds, stream, *P);
+    else if (P->enable_bvh && P->pipeline)
+        hipLaunchKernelGGL(rt::ray_trace_pipe_kernel, dim3(blocks), dim3(rt::BLOCK), lds, stream, *P);
     else
         hipLaunchKernelGGL(rt::ray_trace_kernel<false>, dim3(blocks), dim3(rt::BLOCK), lds, stream, *P);
     return hipGetLastError();

@@ -61,6 +61,7 @@ struct KParams {
     int32_t enable_roughness_mapping, enable_skysphere, enable_skybox;
     uint32_t rng_seed;
     int32_t has_reflection;   // RT_SHADING with a material whose reflection > 0: recursive kernel
+    int32_t pipeline;         // per-lane pipelined kernel for the non-recursive case (RT_PIPELINE=1; default 0)
 
     // image: render size (internal, after the SSAA factor) and this launch's rows
     int32_t rw, rh;

@@ -1,6 +1,8 @@
 // renderer.cpp -- rt::Renderer (see renderer.hpp).
 #include "renderer.hpp"
 
+#include <cstdlib>
+
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -518,6 +520,9 @@ void Renderer::fill_params(KParams& P) const
     P.enable_skybox = s_.enable_skybox;
     P.rng_seed = s_.rng_seed;
     P.has_reflection = s_.shading_method == RT_SHADING && any_reflection(mats_);
+    // RT_PIPELINE=1 selects the per-lane pipelined kernel instead of the tile-per-wave one (A/B runs)
+    const char* pipe_env = getenv("RT_PIPELINE");
+    P.pipeline = pipe_env && pipe_env[0] == '1';
     P.max_blocks = num_cus_ * 8;
     render_size(P.rw, P.rh);
 }

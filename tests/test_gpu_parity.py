@@ -67,6 +67,24 @@ def test_gpu_full_resolution_rows_match_reference(R, name):
             assert float(np.abs(g["rgba"][sl] - exp["rgba"]).max()) <= RGBA_TOL
 
 
+@pytest.mark.parametrize("name", ["c3_bumpy70k", "textured", "shading_1", "robot"])
+def test_pipelined_kernel_matches_reference_golden(R, name, monkeypatch):
+    """The per-lane pipelined kernel (RT_PIPELINE=1, read at every launch) writes the same framebuffer."""
+    if name not in CASES:
+        pytest.skip(f"no golden case {name}")
+    c = Case(name)
+    exp = c.expected()
+    monkeypatch.setenv("RT_PIPELINE", "1")
+    g = gpu_render(R, c.scene, c.settings)
+    monkeypatch.delenv("RT_PIPELINE")
+    assert np.array_equal(g["hit_id"], exp["hit_id"])
+    assert np.array_equal(bits(g["hit_t"]), bits(exp["hit_t"]))
+    assert np.array_equal(g["shadow"], exp["shadow"])
+    assert np.array_equal(g["argb"], exp["argb"])
+    assert float(np.abs(g["rgba"] - exp["rgba"]).max()) <= RGBA_TOL
+    assert R.stats()["shadow_rays"] == c.meta["counters"]["shadow_rays"]
+
+
 def test_c4_full_frame_matches_oracle(R):
     """The benchmark workload at full size: every internal pixel and the SSAA frame."""
     from raytracercpp_amd import scenes
