@@ -27,52 +27,21 @@ constexpr int WAVES_PER_BLOCK = 4;
 constexpr int BLOCK = 64 * WAVES_PER_BLOCK;
 
 #ifndef RT_OCC
-#define RT_OCC 4
+#define RT_OCC 6
 #endif
 #ifndef RT_WW
-#define RT_WW 0
+#define RT_WW 1
+#endif
+#ifndef RT_MT_EARLY
+#define RT_MT_EARLY 2
 #endif
 
 struct TRay {
     v3 o, d;
-    float den[NPLANES], num[NPLANES];
-#ifdef RT_FASTDIV
-    float rcp[NPLANES];   // refined reciprocal of den[i] (the IEEE division's own y1)
-    bool fast;            // every non-zero den[i] in [2^-40, 2^40]
-#endif
+    float den[NPLANES], num[NPLANES];   // num[i] = NaN where den[i] == 0 (see vol_test)
     bool nan;
 };
 
-#ifdef RT_FASTDIV
-// gfx950's IEEE fp32 division (what hipcc emits for a / b) is
-//   v_div_scale(b), v_rcp, v_div_scale(a), e = fma(-b', y0, 1), y1 = fma(e, y0, y0),
-//   q0 = a'*y1, r0 = fma(-b', q0, a'), q1 = fma(r0, y1, q0), r1 = fma(-b', q1, a'),
-//   q2 = div_fmas(r1, y1, q1), div_fixup(q2, b, a).
-// With |a|, |b| in [2^-40, 2^40] (or a == 0) neither operand is scaled, the fmas
-// scale factor is 1 and the fixup is the identity, so the core below returns the
-// same bits; y1 depends on b only and is computed once per ray and plane.
-__device__ __forceinline__ float rcp_refined(float b)
-{
-    float y0 = __builtin_amdgcn_rcpf(b);
-    float e = fmaf(-b, y0, 1.0f);
-    return fmaf(e, y0, y0);
-}
-
-__device__ __forceinline__ bool div_operand_ok(float a)
-{
-    uint32_t e = (__float_as_uint(a) >> 23) & 0xffu;   // biased exponent
-    return (e - 87u) <= 80u || (__float_as_uint(a) & 0x7fffffffu) == 0u;   // 2^-40 <= |a| < 2^41, or 0
-}
-
-__device__ __forceinline__ float div_core(float a, float b, float y)
-{
-    float q0 = a * y;
-    float r0 = fmaf(-b, q0, a);
-    float q1 = fmaf(r0, y, q0);
-    float r1 = fmaf(-b, q1, a);
-    return fmaf(r1, y, q1);
-}
-#endif
 
 // HitInfo (hitInfo.h:8-24) reduced to what the kernels need.
 struct Rec {
@@ -103,17 +72,12 @@ __device__ __forceinline__ TRay make_ray(const KParams& P, v3 o, v3 d)
         R.den[i] = dot(n, d);
         R.num[i] = dot(n, o);
         nan |= (R.den[i] != R.den[i]) || (R.num[i] != R.num[i]);
+        // a plane with denom == 0 is skipped (bvh.h:86-87): a NaN numerator makes
+        // both of its quotients NaN, which the max / min below ignore
+        if (R.den[i] == 0.0f)
+            R.num[i] = __int_as_float(0x7fc00000);
     }
     R.nan = nan;
-#ifdef RT_FASTDIV
-    bool fast = true;
-#pragma unroll
-    for (int i = 0; i < NPLANES; i++) {
-        R.rcp[i] = rcp_refined(R.den[i]);
-        fast &= R.den[i] == 0.0f || ((((__float_as_uint(R.den[i]) >> 23) & 0xffu) - 87u) <= 80u);
-    }
-    R.fast = fast;
-#endif
     return R;
 }
 
@@ -144,67 +108,31 @@ __device__ __forceinline__ uint2 load_node_link(const GNode* nodes, uint32_t i)
     return make_uint2(q3.z, q3.w);
 }
 
-// BoundingVolume::intersect, bvh.h:79-105.  t_near only ever grows and t_far
-// only shrinks (std::max / std::min never return a NaN second operand), so
-// testing t_far < t_near once after the loop equals the reference's early exit.
-__device__ __forceinline__ bool vol_test_div(const NodeBox& n, const TRay& R, float& t_near_out)
+// BoundingVolume::intersect, bvh.h:79-105, branch-free.  Exactly the
+// reference's decision and t_near:
+//  * t_near only grows and t_far only shrinks (std::max / std::min never return
+//    a NaN second operand), so one t_far < t_near test after the loop equals the
+//    early exit inside it;
+//  * every stored volume has d_near[i] <= d_far[i] (a min / max over its
+//    triangles' projections, checked when the octree is flattened), so the
+//    quotient pair ordered by the sign of denom (the std::swap) is (min, max);
+//  * a skipped plane (denom == 0) has num = NaN, its quotients are NaN and
+//    fmaxf / fminf keep the running bound, as std::max / std::min do.
+// fmaxf / fminf differ from std::max / std::min only in the sign of a zero
+// result, which no comparison sees.
+__device__ __forceinline__ bool vol_test(const NodeBox& n, const TRay& R, float& t_near_out)
 {
     float t_near = -INFINITY, t_far = INFINITY;
 #pragma unroll
     for (int i = 0; i < NPLANES; i++) {
-        float denom = R.den[i];
-        if (denom != 0.0f) {
-            float d0 = (n.dn[i] - R.num[i]) / denom;
-            float d1 = (n.df[i] - R.num[i]) / denom;
-            float lo = denom < 0 ? d1 : d0;
-            float hi = denom < 0 ? d0 : d1;
-            t_near = smax(t_near, lo);
-            t_far = smin(t_far, hi);
-        }
+        float d0 = (n.dn[i] - R.num[i]) / R.den[i];
+        float d1 = (n.df[i] - R.num[i]) / R.den[i];
+        t_near = fmaxf(t_near, fminf(d0, d1));
+        t_far = fminf(t_far, fmaxf(d0, d1));
     }
     t_near_out = t_near;
     return !(t_far < t_near);
 }
-
-#ifdef RT_FASTDIV
-__device__ __noinline__ bool vol_test_slow(NodeBox n, TRay R, float* t_near_out)
-{
-    float t;
-    bool r = vol_test_div(n, R, t);
-    *t_near_out = t;
-    return r;
-}
-
-__device__ __forceinline__ bool vol_test(const NodeBox& n, const TRay& R, float& t_near_out)
-{
-    float t_near = -INFINITY, t_far = INFINITY;
-    bool ok = R.fast;
-#pragma unroll
-    for (int i = 0; i < NPLANES; i++) {
-        float denom = R.den[i];
-        if (denom != 0.0f) {
-            float a0 = n.dn[i] - R.num[i];
-            float a1 = n.df[i] - R.num[i];
-            ok = ok && div_operand_ok(a0) && div_operand_ok(a1);
-            float d0 = div_core(a0, denom, R.rcp[i]);
-            float d1 = div_core(a1, denom, R.rcp[i]);
-            float lo = denom < 0 ? d1 : d0;
-            float hi = denom < 0 ? d0 : d1;
-            t_near = smax(t_near, lo);
-            t_far = smin(t_far, hi);
-        }
-    }
-    if (!ok)
-        return vol_test_slow(n, R, &t_near_out);
-    t_near_out = t_near;
-    return !(t_far < t_near);
-}
-#else
-__device__ __forceinline__ bool vol_test(const NodeBox& n, const TRay& R, float& t_near_out)
-{
-    return vol_test_div(n, R, t_near_out);
-}
-#endif
 
 // Triangle::intersect (Moller-Trumbore, backface culling), triangle.cpp:25-91,
 // split into the 48-byte record load and the test so loads can be batched.
@@ -225,6 +153,8 @@ __device__ __forceinline__ TriRec load_tri(const GTri* tris, uint32_t k)
 __device__ __forceinline__ bool tri_test_rec(const TriRec& T, const TRay& R, float& t_out, float& u_out,
                                              float& v_out)
 {
+    // the reference's early returns become one predicate over the same values
+    // (same expressions, same comparisons, so NaNs behave identically)
     v3 a = mk(T.q0.x, T.q0.y, T.q0.z);
     v3 ab = mk(T.q0.w, T.q1.x, T.q1.y);
     v3 ac = mk(T.q1.z, T.q1.w, T.q2.x);
@@ -233,22 +163,27 @@ __device__ __forceinline__ bool tri_test_rec(const TriRec& T, const TRay& R, flo
     v3 nd = -R.d;
     v3 m = cross(nd, OA);
     float Mdet = dot(n, nd);
+#if RT_MT_EARLY
+    // coherent waves often reject a back-facing triangle together: skip the rest
     if (Mdet <= 0)
         return false;
-    Mdet = 1 / Mdet;
-    float u = dot(m, ac) * Mdet;
+#endif
+    float inv = 1 / Mdet;
+    float u = dot(m, ac) * inv;
+#if RT_MT_EARLY >= 2
     if (u < 0 || u > 1)
         return false;
-    float v = dot(m, -ab) * Mdet;
+#endif
+    float v = dot(m, -ab) * inv;
+#if RT_MT_EARLY >= 2
     if (v < 0 || u + v > 1)
         return false;
-    float t = dot(n, OA) * Mdet;
-    if (t < 0)
-        return false;
+#endif
+    float t = dot(n, OA) * inv;
     t_out = t;
     u_out = u;
     v_out = v;
-    return true;
+    return !(Mdet <= 0) & !(u < 0 || u > 1) & !(v < 0 || u + v > 1) & !(t < 0);
 }
 
 __device__ __forceinline__ bool tri_test(const GTri* tris, uint32_t k, const TRay& R, float& t_out, float& u_out,
@@ -264,8 +199,9 @@ struct THit {
 
 // ---- libstdc++ binary heap (push_heap / pop_heap with std::greater), only
 // used when two pending children have equal t_near. ----
+// Children are pushed in octant order, which is their slot order a + j.
 __device__ __noinline__ uint32_t heap_order(float k0, float k1, float k2, float k3, float k4, float k5, float k6,
-                                            float k7, uint32_t validmask, uint32_t mask, int n)
+                                            float k7, uint32_t validmask, int n)
 {
     // keys arrive in registers; the arrays below exist only on this (rare) path
     float key[8] = {k0, k1, k2, k3, k4, k5, k6, k7};
@@ -273,7 +209,7 @@ __device__ __noinline__ uint32_t heap_order(float k0, float k1, float k2, float 
     uint32_t rank[8];
     for (int s = 0; s < 8; s++) {
         valid[s] = (validmask >> s) & 1u;
-        rank[s] = __popc(mask & ((1u << s) - 1u));
+        rank[s] = (uint32_t)s;
     }
     float hk[8];
     uint32_t hr[8];
@@ -396,55 +332,46 @@ __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit&
         }
         r = h.t > 0;
     } else {
-        uint32_t mask = b & 0xffu;
+        // the k non-empty children are nodes a .. a+k-1, in octant order; a
+        // child that is missed keeps a NaN key (no comparison counts it)
+        const uint32_t k = b;
         float key[8];
-        bool valid[8];
-        uint32_t rank[8];
-        int n = 0;
 #pragma unroll
-        for (int s = 0; s < 8; s++) {
-            rank[s] = __popc(mask & ((1u << s) - 1u));
-            valid[s] = false;
-            key[s] = INFINITY;
-            if (mask & (1u << s)) {
-                NodeBox c = load_node(P.nodes, a + rank[s]);
+        for (int j = 0; j < 8; j++) {
+            key[j] = __int_as_float(0x7fc00000);
+            if ((uint32_t)j < k) {
+                NodeBox c = load_node(P.nodes, a + j);
                 float t;
-                if (vol_test(c, R, t)) {
-                    valid[s] = true;
-                    key[s] = t;
-                    n++;
-                }
+                if (vol_test(c, R, t))
+                    key[j] = t;
             }
         }
+        // pop position of child j = number of hit children before it in a
+        // stable sort by t_near; equal keys need the heap's own order
+        uint32_t pos[8];
+        uint32_t vm = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            pos[j] = 0;
+            vm |= (key[j] == key[j] ? 1u : 0u) << j;
+        }
+        bool tie = false;
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+#pragma unroll
+            for (int j2 = j + 1; j2 < 8; j2++) {
+                pos[j] += key[j2] < key[j] ? 1u : 0u;
+                pos[j2] += key[j] <= key[j2] ? 1u : 0u;
+                tie |= key[j] == key[j2];
+            }
+        const int n = __popc(vm);
         if (n > 0) {
             uint32_t order = 0;
-            bool tie = false;
 #pragma unroll
-            for (int s = 0; s < 8; s++) {
-                if (!valid[s])
-                    continue;
-                uint32_t pos = 0;
-#pragma unroll
-                for (int t2 = 0; t2 < 8; t2++) {
-                    if (t2 == s || !valid[t2])
-                        continue;
-                    if (key[t2] < key[s])
-                        pos++;
-                    else if (key[t2] == key[s]) {
-                        tie = true;
-                        if (t2 < s)
-                            pos++;
-                    }
-                }
-                order |= rank[s] << (3 * pos);
-            }
-            if (tie) {
-                uint32_t vm = 0;
-#pragma unroll
-                for (int s = 0; s < 8; s++)
-                    vm |= (valid[s] ? 1u : 0u) << s;
-                order = heap_order(key[0], key[1], key[2], key[3], key[4], key[5], key[6], key[7], vm, mask, n);
-            }
+            for (int j = 0; j < 8; j++)
+                order |= ((vm >> j) & 1u) ? (uint32_t)j << (3 * pos[j]) : 0u;
+            if (tie)
+                order = heap_order(key[0], key[1], key[2], key[3], key[4], key[5], key[6], key[7], vm, n);
             depth++;
             any_true &= ~(1u << depth);
             uint32_t first = a + (order & 7u);

@@ -256,7 +256,7 @@ void build_flat_octree(const float* tri9, int64_t n, int max_depth, int leaf_max
             }
             // g may dangle after emit(): write a/b first
             out.nodes[fi].a = (uint32_t)out.nodes.size();
-            out.nodes[fi].b = mask;
+            out.nodes[fi].b = (uint32_t)__builtin_popcount(mask);
             for (int k = 0; k < 8; k++)
                 if (mask & (1u << k)) {
                     emit(bn.child[k]);
@@ -266,6 +266,13 @@ void build_flat_octree(const float* tri9, int64_t n, int max_depth, int leaf_max
         fi++;
     }
     out.levels = maxd + 1;
+    // the kernels' slab test relies on d_near <= d_far for every stored volume
+    // (true for any node holding a triangle with finite vertices)
+    out.ordered_slabs = true;
+    for (const GNode& g : out.nodes)
+        for (int i = 0; i < NPLANES; i++)
+            if (!(g.dn[i] <= g.df[i]))
+                out.ordered_slabs = false;
 }
 
 }  // namespace rt

@@ -8,8 +8,8 @@
 // Flattened layout (HBM):
 //   GNode[ ]  64 B each: 7 near + 7 far k-DOP slab distances, then
 //             a = first child (inner) or first triangle (leaf),
-//             b = LEAF_BIT | triangle count (leaf) or the 8-bit mask of
-//                 non-empty child octants (inner).
+//             b = LEAF_BIT | triangle count (leaf) or the number of
+//                 non-empty child octants (inner; children a .. a+b-1 in octant order).
 //             The non-empty children of an inner node are contiguous, in octant
 //             order, so heap insertion order (bvh.h:251-256) is rank order.
 //             Empty leaves are dropped: their empty volume (+inf / -inf) can
@@ -58,6 +58,7 @@ struct FlatOctree {
     std::vector<GTri> tris;        // leaf-contiguous
     std::vector<int32_t> tri_id;   // GTri slot -> caller triangle index
     int levels = 0;                // max depth + 1 of the flattened tree
+    bool ordered_slabs = true;     // every node has dn[i] <= df[i] (kernels.hip vol_test)
     OctreeStats stats;             // of the unflattened (reference) tree
 };
 

@@ -355,10 +355,15 @@ int Renderer::ensure_device_scene()
     if (geom_dirty_) {
         auto t0 = std::chrono::steady_clock::now();
         int64_t n = (int64_t)tri_mat_.size();
+        for (float c : tri_)
+            if (!std::isfinite(c))
+                return fail(RT_EINVAL, "triangle with a non-finite vertex coordinate");
         if (s_.enable_bvh) {
             build_flat_octree(tri_.data(), n, s_.bvh_max_depth, s_.bvh_leaf_object_count, oct_);
             if (oct_.levels > 31)
                 return fail(RT_EUNSUPPORTED, "octree deeper than 31 levels");
+            if (!oct_.ordered_slabs)
+                return fail(RT_EINVAL, "octree volume with d_near > d_far");
         } else {
             // brute-force mode (renderer.cpp:1021-1027): triangles in caller order, no nodes
             oct_ = FlatOctree();
