@@ -278,7 +278,7 @@ __device__ __noinline__ uint32_t heap_order(float k0, float k1, float k2, float 
 struct Trav {
     uint32_t a, b;       // link word of the node to VISIT next
     int depth;
-    uint32_t any_true;   // bit d: a child at depth d returned true (closest_inter != INFINITY)
+    uint32_t any_true;   // bit d: closest_inter != INFINITY in the node whose children are at depth d
     bool r, live;
 };
 
@@ -396,7 +396,11 @@ __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit&
         uint32_t cnt = e.y >> 24;
         uint32_t ord = e.y & 0xffffffu;
         if (r) {
-            any_true |= 1u << depth;
+            // closest_inter = min(closest_inter, child t_near); the child's t_near is
+            // the query-global hit t, and a child returning true with t = +inf
+            // (overflow) leaves closest_inter == INFINITY (bvh.h:267, 280-281)
+            if (h.t < INFINITY)
+                any_true |= 1u << depth;
             if (cnt == 0) {
                 depth--;
                 continue;   // queue empty: parent returns true

@@ -130,7 +130,7 @@ def _voxel_scene(n=8, size=0.2, gap=0.05):
     return base
 
 
-@pytest.mark.parametrize("scene_name", ["robot", "voxels", "sphere1m_surface"])
+@pytest.mark.parametrize("scene_name", ["robot", "voxels", "sphere1m_surface", "grazing", "tiny", "huge"])
 def test_trace_rays_match_oracle(R, scene_name):
     """BVH::intersect on arbitrary rays (rt_trace_rays) vs the oracle: ids, t, u, v, return value."""
     from raytracercpp_amd import scenes
@@ -145,6 +145,19 @@ def test_trace_rays_match_oracle(R, scene_name):
         o, d = _random_rays(rng, 50000, np.zeros(3, np.float32), 2.5)
         # axis-aligned directions too (zero denominators are skipped planes)
         d[:10000] = np.eye(3, dtype=np.float32)[rng.integers(0, 3, 10000)] * rng.choice([-1, 1], (10000, 1))
+    elif scene_name == "grazing":
+        # plane denominators below 2^-40 (incl. denormal and zero): vol_test's exact-division path
+        sc, st = scenes.robot1080(width=64, height=36)
+        o, d = _random_rays(rng, 50000, np.array([0, 0, -4], np.float32), 3.0)
+        tiny = rng.choice(np.array([0.0, 1e-13, -1e-13, 1e-30, -1e-41], np.float32), (50000,))
+        axis = rng.integers(0, 3, 50000)
+        d[np.arange(50000), axis] = tiny
+    elif scene_name in ("tiny", "huge"):
+        # every slab value outside [2^-38, 2^39): the whole scene takes the exact-division path
+        f = np.float32(1e-13 if scene_name == "tiny" else 1e13)
+        sc, st = scenes.robot1080(width=64, height=36)
+        sc.tri = (sc.tri * f).astype(np.float32)
+        o, d = _random_rays(rng, 50000, np.array([0, 0, -4], np.float32) * f, 3.0 * f)
     else:
         sc, st = scenes.sphere1m(width=64, height=36)
         idx = rng.integers(0, sc.ntri, 20000)
@@ -207,6 +220,13 @@ def test_render_api_and_errors(R):
     with pytest.raises(RtError):
         R.ray_trace()   # normal map enabled but not set
     R.set_render_settings(st)
+    R.ray_trace()
+    nonfinite = sc.tri.copy()
+    nonfinite[3, 4] = np.nan
+    R.set_triangles(nonfinite, sc.tri_mat, sc.tri_uv)
+    with pytest.raises(RtError, match="non-finite"):
+        R.ray_trace()   # NaN / inf vertices are rejected (slab test)
+    R.set_triangles(sc.tri, sc.tri_mat, sc.tri_uv)
     R.ray_trace()
 
 
