@@ -68,7 +68,7 @@ __device__ __forceinline__ TRay make_ray(const KParams& P, v3 o, v3 d)
     bool nan = false;
 #pragma unroll
     for (int i = 0; i < NPLANES; i++) {
-        v3 n = mk(P.pn[i][0], P.pn[i][1], P.pn[i][2]);
+        v3 n = mk(PLANE_N[i][0], PLANE_N[i][1], PLANE_N[i][2]);
         R.den[i] = dot(n, d);
         R.num[i] = dot(n, o);
         nan |= (R.den[i] != R.den[i]) || (R.num[i] != R.num[i]);

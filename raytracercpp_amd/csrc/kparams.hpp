@@ -30,7 +30,6 @@ struct KParams {
     int32_t nnodes;
     int32_t ntri_slots;       // GTri count (brute-force loop bound when enable_bvh == 0)
     int32_t levels;           // flattened tree depth + 1 (LDS level-stack entries per lane)
-    float pn[NPLANES][3];     // BVH::BoundingVolume::PLANE_NORMALS (bvh.cpp:8-16)
 
     int32_t nshape;
     int32_t shape_kind[MAX_SHAPES];

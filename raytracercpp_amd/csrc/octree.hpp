@@ -28,6 +28,13 @@
 namespace rt {
 
 constexpr int NPLANES = 7;
+// BVH::BoundingVolume::PLANE_NORMALS (bvh.cpp:8-16) as literals: sqrtf(3) / 3 in
+// fp32 is 0x3f13cd3a; plane_normals() computes them the reference's way and the
+// renderer checks the two agree (kernels read the literals).
+constexpr float PN_S = 0x1.279a74p-1f;
+constexpr float PLANE_N[NPLANES][3] = {{1, 0, 0},           {0, 1, 0},           {0, 0, 1},
+                                       {PN_S, PN_S, PN_S},  {-PN_S, PN_S, PN_S}, {-PN_S, -PN_S, PN_S},
+                                       {PN_S, -PN_S, PN_S}};
 constexpr uint32_t LEAF_BIT = 0x80000000u;
 
 struct alignas(16) GNode {

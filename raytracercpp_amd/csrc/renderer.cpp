@@ -428,6 +428,13 @@ int Renderer::ensure_device_scene()
 
 int Renderer::validate() const
 {
+    // the kernels use the PLANE_N literals: they must be the reference's computed normals
+    v3 pn[NPLANES];
+    plane_normals(pn);
+    for (int i = 0; i < NPLANES; i++)
+        if (std::memcmp(&pn[i].x, &PLANE_N[i][0], 4) || std::memcmp(&pn[i].y, &PLANE_N[i][1], 4) ||
+            std::memcmp(&pn[i].z, &PLANE_N[i][2], 4))
+            return RT_EUNSUPPORTED;
     int nmat = material_count();
     if (s_.shading_method == RT_SHADING) {
         for (int32_t m : tri_mat_)
@@ -476,13 +483,6 @@ void Renderer::fill_params(KParams& P) const
     P.nnodes = (int32_t)oct_.nodes.size();
     P.ntri_slots = (int32_t)oct_.tris.size();
     P.levels = oct_.levels > 0 ? oct_.levels : 1;
-    v3 pn[NPLANES];
-    plane_normals(pn);
-    for (int i = 0; i < NPLANES; i++) {
-        P.pn[i][0] = pn[i].x;
-        P.pn[i][1] = pn[i].y;
-        P.pn[i][2] = pn[i].z;
-    }
     P.nshape = (int32_t)shape_kind_.size();
     for (int k = 0; k < P.nshape; k++) {
         P.shape_kind[k] = shape_kind_[k];
