@@ -1,19 +1,24 @@
 #!/bin/bash
-# Runs on the GPU box: kernel-trace stats + PMC passes (separate runs) of bench.py.
+# Runs on the GPU box: kernel-trace stats + PMC passes (one rocprofv3 run per pass,
+# counters never combined with sys/runtime traces) of bench.py.
 # Usage: bash tools/profile_gpu.sh <tag>   -> gpurun_out/prof_<tag>/...
 set -u
 TAG=${1:-r01}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
+B="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
-    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $OUT/trace.log 2>&1 || exit 1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- \
-    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/pmc_fetch.log 2>&1 || exit 2
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- \
-    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/pmc_write.log 2>&1 || exit 3
-timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $OUT/pmc_tcc -o run -- \
-    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/pmc_tcc.log 2>&1 || exit 4
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $OUT/pmc_sq -o run -- \
-    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/pmc_sq.log 2>&1 || exit 5
+    $B > $OUT/trace.log 2>&1 || exit 1
+pass() {   # pass <name> <counters...>
+    local name=$1; shift
+    timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d $OUT/pmc_$name -o run -- \
+        python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/pmc_$name.log 2>&1
+}
+pass fetch FETCH_SIZE || exit 2
+pass write WRITE_SIZE || exit 3
+pass tcc TCC_HIT_sum TCC_MISS_sum || exit 4
+pass sq SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES || exit 5
+pass sq2 SQ_WAIT_ANY SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS || exit 6
+pass sq3 SQ_THREAD_CYCLES_VALU SQ_INSTS_BRANCH GRBM_GUI_ACTIVE || exit 7
 find $OUT -name "*.csv" | sort

@@ -1,0 +1,37 @@
+"""Summarise a tools/profile_gpu.sh run into profiles/<tag>/: kernel stats csv +
+summary.json (per-launch PMC averages of the ray-trace kernel, HBM traffic per
+MI355X_MICROARCH.md: bytes = 2 x FETCH_SIZE[KB] x 1024 + WRITE_SIZE[KB] x 1024).
+   python tools/profile_summary.py gpurun_out/prof_r01 profiles/r01"""
+import collections, csv, glob, json, os, shutil, sys
+
+src, dst = sys.argv[1], sys.argv[2]
+os.makedirs(dst, exist_ok=True)
+out = {"kernels": {}, "pmc_ray_trace_kernel": {}}
+stats = glob.glob(f"{src}/trace/**/run_kernel_stats.csv", recursive=True)
+if stats:
+    shutil.copy(stats[0], os.path.join(dst, "kernel_stats.csv"))
+    for r in csv.DictReader(open(stats[0])):
+        out["kernels"][r["Name"]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                                     "total_ns": float(r["TotalDurationNs"]), "pct": float(r["Percentage"])}
+for f in sorted(glob.glob(f"{src}/pmc_*/**/run_counter_collection.csv", recursive=True)):
+    agg = collections.defaultdict(list)
+    for r in csv.DictReader(open(f)):
+        if "ray_trace_kernel" in r["Kernel_Name"]:
+            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for k, v in agg.items():
+        out["pmc_ray_trace_kernel"][k] = sum(v) / len(v)
+    name = f.split(os.sep)[-3] if "pmc_" in f.split(os.sep)[-3] else os.path.basename(os.path.dirname(f))
+    shutil.copy(f, os.path.join(dst, f"{name}_counters.csv"))
+p = out["pmc_ray_trace_kernel"]
+if "FETCH_SIZE" in p and "WRITE_SIZE" in p:
+    out["hbm_read_bytes_per_launch"] = 2 * p["FETCH_SIZE"] * 1024
+    out["hbm_write_bytes_per_launch"] = p["WRITE_SIZE"] * 1024
+    out["hbm_traffic_bytes_per_launch"] = out["hbm_read_bytes_per_launch"] + out["hbm_write_bytes_per_launch"]
+if "TCC_HIT_sum" in p:
+    out["l2_hit_rate"] = p["TCC_HIT_sum"] / max(1.0, p["TCC_HIT_sum"] + p["TCC_MISS_sum"])
+if "SQ_THREAD_CYCLES_VALU" in p and "SQ_ACTIVE_INST_VALU" in p:
+    out["valu_lane_utilisation"] = p["SQ_THREAD_CYCLES_VALU"] / (64.0 * p["SQ_ACTIVE_INST_VALU"])
+if "SQ_WAIT_ANY" in p and "SQ_WAVE_CYCLES" in p:
+    out["wave_wait_fraction"] = p["SQ_WAIT_ANY"] / p["SQ_WAVE_CYCLES"]
+json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1, sort_keys=True)
+print(json.dumps({k: v for k, v in out.items() if k != "kernels"}, indent=1))
