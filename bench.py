@@ -169,9 +169,14 @@ def main():
 
 
 def cpu_baseline(sc, st, gpu_img, threads):
-    """The oracle's C restatement (OpenMP, oracle/liboracle.so) on the full frame: a bounded
-    sample of ~1-3 s on the box's host cores; also gives max |dpixel| of the GPU frame."""
-    from oracle.bindings import Oracle
+    """CPU baseline on the box's host cores, and max |dpixel| of the GPU frame.
+    * the reference itself (oracle/_ref/libref_harness.so: the reference's own compiled
+      BVH / triangle / vector code driven by the harness's restated pixel loop, OpenMP
+      schedule(dynamic) over rows as renderer.cpp:1082) timed on a bounded sample of row
+      bands spread over the frame (octree build excluded), when that library was built;
+    * the oracle's C restatement (oracle/liboracle.so, OpenMP) on the full frame, which
+      also gives the pixel comparison (and the baseline when the reference is absent)."""
+    from oracle.bindings import Oracle, RefHarness
     threads = threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     o = Oracle(sc, st)
     res = o.render_rows(nthreads=threads)
@@ -181,10 +186,21 @@ def cpu_baseline(sc, st, gpu_img, threads):
     d = 0
     for sh in (16, 8, 0):
         d = max(d, int(np.max(np.abs(((g >> sh) & 0xFF).astype(np.int32) - ((ref >> sh) & 0xFF).astype(np.int32)))))
-    rays = res.counters["primary_rays"] + res.counters["shadow_rays"]
-    base = {"value": round(rays / res.seconds / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+    port_rays = res.counters["primary_rays"] + res.counters["shadow_rays"]
+    port = {"value": round(port_rays / res.seconds / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"full C4 frame ({rw}x{rh} primary + {res.counters['shadow_rays']} shadow rays) "
                       f"in {res.seconds:.2f} s, oracle.c OpenMP x{threads}"}
+    if not RefHarness.available():
+        return port, d
+    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+    stride = 2
+    rr = RefHarness.render_row_sample(sc, st, stride // 2, rh // stride, stride)
+    rays = rr.counters["primary_rays"] + rr.counters["shadow_rays"]
+    base = {"value": round(rays / rr.seconds / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "reference",
+            "sample": f"every {stride}th internal row of the C4 frame ({rh // stride} rows x {rw}: {rr.counters['primary_rays']}"
+                      f" primary + {rr.counters['shadow_rays']} shadow rays in {rr.seconds:.2f} s, octree build "
+                      f"excluded), reference TUs + OpenMP x{threads}",
+            "port_value": port["value"]}
     return base, d
 
 

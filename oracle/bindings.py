@@ -240,6 +240,24 @@ class Oracle:
         return out
 
     @classmethod
+    def render_row_sample(cls, scene, settings, row_begin, row_count, row_stride) -> RenderResult:
+        """Internal rows row_begin + i * row_stride (i < row_count), for CPU timing samples."""
+        pin = _Pinned()
+        sc = make_orc_scene(scene, pin)
+        st = make_orc_settings(settings)
+        rw, _ = settings.render_size()
+        res = RenderResult(rw, row_count)
+        out = res.outputs()
+        cnt = OrcCounters()
+        rc = cls.lib().ref_render_row_sample(C.byref(sc), C.byref(st), row_begin, row_count, row_stride,
+                                             C.byref(out), C.byref(cnt))
+        if rc != 0:
+            raise RuntimeError("ref_render_row_sample failed")
+        res.seconds = cls.lib().ref_last_render_seconds()
+        res.counters = cnt.as_dict()
+        return res
+
+    @classmethod
     def heap_order(cls, keys):
         k = np.ascontiguousarray(keys, np.float32)
         out = np.zeros(len(k), np.int32)
@@ -270,6 +288,8 @@ class RefHarness:
             L.ref_load_obj.restype = C.c_int64
             L.ref_load_obj.argtypes = [C.c_char_p, _f32p, C.c_int, _f32p, _i32p, _f32p, C.c_int64, _i32p, _f32p,
                                        C.c_int32, _i32p]
+            L.ref_last_render_seconds.restype = C.c_double
+            L.ref_last_render_seconds.argtypes = []
             L.ref_specular_threshold.restype = C.c_float
             L.ref_specular_threshold.argtypes = [C.c_float] * 4
             L.ref_triangle_intersect.argtypes = [_f32p, _f32p, _f32p, _f32p]
@@ -367,9 +387,28 @@ class RefHarness:
         cnt = OrcCounters()
         t0 = time.perf_counter()
         rc = cls.lib().ref_render_rows(C.byref(sc), C.byref(st), row_begin, row_count, C.byref(out), C.byref(cnt))
-        res.seconds = time.perf_counter() - t0
+        res.wall_seconds = time.perf_counter() - t0         # includes the reference's octree build
+        res.seconds = cls.lib().ref_last_render_seconds()   # the pixel loop only
         if rc != 0:
             raise RuntimeError("ref_render_rows failed")
+        res.counters = cnt.as_dict()
+        return res
+
+    @classmethod
+    def render_row_sample(cls, scene, settings, row_begin, row_count, row_stride) -> RenderResult:
+        """Internal rows row_begin + i * row_stride (i < row_count), for CPU timing samples."""
+        pin = _Pinned()
+        sc = make_orc_scene(scene, pin)
+        st = make_orc_settings(settings)
+        rw, _ = settings.render_size()
+        res = RenderResult(rw, row_count)
+        out = res.outputs()
+        cnt = OrcCounters()
+        rc = cls.lib().ref_render_row_sample(C.byref(sc), C.byref(st), row_begin, row_count, row_stride,
+                                             C.byref(out), C.byref(cnt))
+        if rc != 0:
+            raise RuntimeError("ref_render_row_sample failed")
+        res.seconds = cls.lib().ref_last_render_seconds()
         res.counters = cnt.as_dict()
         return res
 

@@ -36,6 +36,8 @@
 #include <variant>
 #include <vector>
 
+#include <omp.h>
+
 #include "analyticShape.h"
 #include "bvh.h"
 #include "camera.h"
@@ -637,21 +639,46 @@ void ref_bvh_query(const float* tri9, int64_t ntri, int max_depth, int leaf, con
 
 /* Renderer::ray_trace (renderer.cpp:1068-1116) over internal rows
  * [row_begin, row_begin + row_count), restated on reference primitives. */
+static double g_last_render_seconds = 0.0;
+
+/* Wall time of the last ref_render_rows pixel loop (the octree build excluded). */
+double ref_last_render_seconds(void) { return g_last_render_seconds; }
+
+static int render_rows_strided(const orc_scene* sc, const orc_settings* st, int row_begin, int row_count,
+                               int row_stride, orc_outputs* out, orc_counters* counters);
+
 int ref_render_rows(const orc_scene* sc, const orc_settings* st, int row_begin, int row_count, orc_outputs* out,
                     orc_counters* counters)
+{
+    return render_rows_strided(sc, st, row_begin, row_count, 1, out, counters);
+}
+
+/* Internal rows row_begin + i * row_stride, i < row_count (a frame-wide sample for
+ * CPU timing), written as consecutive output rows. */
+int ref_render_row_sample(const orc_scene* sc, const orc_settings* st, int row_begin, int row_count, int row_stride,
+                          orc_outputs* out, orc_counters* counters)
+{
+    return render_rows_strided(sc, st, row_begin, row_count, row_stride, out, counters);
+}
+
+static int render_rows_strided(const orc_scene* sc, const orc_settings* st, int row_begin, int row_count,
+                               int row_stride, orc_outputs* out, orc_counters* counters)
 {
     HScene H;
     build_scene(H, sc, st);
     int rw, rh;
     render_w_h(st, rw, rh);
-    if (row_begin < 0 || row_begin + row_count > rh)
+    if (row_begin < 0 || row_count < 0 || row_stride < 1 ||
+        (row_count > 0 && row_begin + (int64_t)(row_count - 1) * row_stride >= rh))
         return -1;
     orc_counters total = {};
+    const double t_start = omp_get_wtime();
 #pragma omp parallel
     {
         orc_counters local = {};
 #pragma omp for schedule(dynamic)
-        for (int py = row_begin; py < row_begin + row_count; py++) {
+        for (int row = 0; row < row_count; row++) {
+            const int py = row_begin + row * row_stride;
             Tracer tr(H);
             float y_world = ((float)py + 0.5f) / rh * 2 - 1;
             for (int px = 0; px < rw; px++) {
@@ -668,7 +695,7 @@ int ref_render_rows(const orc_scene* sc, const orc_settings* st, int row_begin, 
                 bool shadowed = false;
                 local.primary_rays++;
                 Color c = tr.trace_ray(ray, hi, 0, found, &src, &local, &shadowed);
-                size_t o = (size_t)(py - row_begin) * rw + px;
+                size_t o = (size_t)row * rw + px;
                 if (out->argb) out->argb[o] = h_color_to_argb(c);
                 if (out->rgba) {
                     out->rgba[4 * o] = c.r;
@@ -688,6 +715,7 @@ int ref_render_rows(const orc_scene* sc, const orc_settings* st, int row_begin, 
             total.reflection_rays += local.reflection_rays;
         }
     }
+    g_last_render_seconds = omp_get_wtime() - t_start;
     if (counters) *counters = total;
     return 0;
 }

@@ -104,3 +104,15 @@ def test_product_obj_loader_matches_reference(obj):
 def test_specular_threshold_formula_matches_reference():
     for spec, ns in (((0.5, 0.5, 0.5), 250.0), ((0.5, 0.5, 0.5), 5.0), ((0.2, 0.3, 0.9), 20.0)):
         assert np.float32(scenes.specular_threshold(spec, ns)) == np.float32(RefHarness.specular_threshold(spec, ns))
+
+
+def test_reference_row_sample_equals_full_render_rows():
+    """bench.py's CPU baseline times ref_render_row_sample: it renders exactly the strided rows."""
+    sc, st = scenes.bumpy70k(width=96, height=54)
+    full = RefHarness.render_rows(sc, st)
+    rw, rh = st.render_size()
+    samp = RefHarness.render_row_sample(sc, st, 1, rh // 4, 4)
+    rows = 1 + 4 * np.arange(rh // 4)
+    assert np.array_equal(samp.argb.reshape(-1, rw), full.argb.reshape(rh, rw)[rows])
+    assert np.array_equal(samp.hit_id.reshape(-1, rw), full.hit_id.reshape(rh, rw)[rows])
+    assert samp.seconds > 0
