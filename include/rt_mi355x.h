@@ -220,6 +220,15 @@ int rt_obj_counts(const rt_obj *o, int64_t *ntri, int32_t *nmat, int32_t *has_uv
 int rt_obj_fetch(const rt_obj *o, float *tri9, int32_t *mat, float *uv6, float *mats16);
 void rt_obj_close(rt_obj *o);
 
+/* ---- Host octree build (BVH::BVH, tp2/projets/bvh.cpp:19-66; bvh.h:141-210), no GPU ----
+ * Builds and flattens the octree over tri9 and returns a 64-bit FNV-1a digest of the
+ * flattened nodes, triangle records and slot -> triangle map, and stats[7] =
+ * {inner, leaves, empty_leaves, max_leaf, max_depth, nodes, flattened levels}.
+ * builder 0: the parallel level-by-level build the renderer uses; 1: the reference's
+ * one-insert-at-a-time algorithm restated.  *ms (optional) gets the build time. */
+int rt_octree_digest(const float *tri9, int64_t n, int32_t max_depth, int32_t leaf_max_obj_count, int32_t builder,
+                     uint64_t *digest, int64_t stats[7], float *ms);
+
 #ifdef __cplusplus
 }
 #endif

@@ -111,6 +111,8 @@ SIGNATURES = {
     "rt_obj_counts": (C.c_int, [_H, _i64p, _i32p, _i32p]),
     "rt_obj_fetch": (C.c_int, [_H, _f32p, _i32p, _f32p, _f32p]),
     "rt_obj_close": (None, [_H]),
+    "rt_octree_digest": (C.c_int, [_f32p, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_uint64), _i64p,
+                                   _f32p]),
 }
 
 _lib = None
@@ -225,3 +227,15 @@ def load_obj(path, xform, mat_offset=0):
         return tri, mat, uv, mats
     finally:
         L.rt_obj_close(h)
+
+
+def octree_digest(tri9, max_depth=12, leaf=40, builder=0):
+    """rt_octree_digest: (digest, stats dict, build ms) of the flattened host octree (no GPU)."""
+    tri9 = f32(tri9).reshape(-1, 9)
+    dg = C.c_uint64()
+    st = np.zeros(7, np.int64)
+    ms = C.c_float()
+    check(lib().rt_octree_digest(ptr(tri9, _f32p), tri9.shape[0], max_depth, leaf, builder, C.byref(dg),
+                                 ptr(st, _i64p), C.byref(ms)), "rt_octree_digest")
+    keys = ("inner", "leaves", "empty_leaves", "max_leaf", "max_depth", "nodes", "levels")
+    return int(dg.value), dict(zip(keys, map(int, st))), float(ms.value)

@@ -6,6 +6,7 @@
 
 #include "../../include/rt_mi355x.h"
 #include "host_scene.hpp"
+#include "octree.hpp"
 #include "renderer.hpp"
 
 namespace {
@@ -349,5 +350,48 @@ int rt_obj_fetch(const rt_obj* o, float* tri9, int32_t* mat, float* uv6, float* 
 }
 
 void rt_obj_close(rt_obj* o) { delete o; }
+
+int rt_octree_digest(const float* tri9, int64_t n, int32_t max_depth, int32_t leaf_max_obj_count, int32_t builder,
+                     uint64_t* digest, int64_t stats[7], float* ms)
+{
+    if (n < 0 || (n > 0 && !tri9) || !digest)
+        return bad("rt_octree_digest: bad arguments");
+    try {
+        rt::FlatOctree f;
+        auto t0 = std::chrono::steady_clock::now();
+        if (builder == 1)
+            rt::build_flat_octree_serial(tri9, n, max_depth, leaf_max_obj_count, f);
+        else
+            rt::build_flat_octree(tri9, n, max_depth, leaf_max_obj_count, f);
+        if (ms)
+            *ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        uint64_t h = 1469598103934665603ull;
+        auto mix = [&h](const void* p, size_t len) {
+            const unsigned char* b = static_cast<const unsigned char*>(p);
+            for (size_t i = 0; i < len; i++) {
+                h ^= b[i];
+                h *= 1099511628211ull;
+            }
+        };
+        mix(f.nodes.data(), f.nodes.size() * sizeof(rt::GNode));
+        mix(f.tris.data(), f.tris.size() * sizeof(rt::GTri));
+        mix(f.tri_id.data(), f.tri_id.size() * sizeof(int32_t));
+        mix(&f.levels, sizeof(f.levels));
+        *digest = h;
+        if (stats) {
+            stats[0] = f.stats.inner;
+            stats[1] = f.stats.leaves;
+            stats[2] = f.stats.empty_leaves;
+            stats[3] = f.stats.max_leaf;
+            stats[4] = f.stats.max_depth;
+            stats[5] = f.stats.nodes;
+            stats[6] = f.levels;
+        }
+        return RT_OK;
+    } catch (const std::bad_alloc&) {
+        g_err = "rt_octree_digest: out of host memory";
+        return RT_ENOMEM;
+    }
+}
 
 }  // extern "C"

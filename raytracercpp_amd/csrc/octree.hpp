@@ -21,6 +21,8 @@
 
 #include <stdint.h>
 
+#include <memory>
+#include <utility>
 #include <vector>
 
 #include "rt_math.hpp"
@@ -56,20 +58,46 @@ static_assert(sizeof(GTri) == 48, "GTri must be 48 B");
 // PLANE_NORMALS (bvh.cpp:8-16), in float, with the reference's expressions.
 void plane_normals(v3 out[NPLANES]);
 
+// std::allocator that default-initialises (no zero fill of arrays about to be overwritten)
+template <class T>
+struct DefaultInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = DefaultInitAlloc<U>;
+    };
+    DefaultInitAlloc() = default;
+    template <class U>
+    DefaultInitAlloc(const DefaultInitAlloc<U>&) {}
+    template <class U>
+    void construct(U* p)
+    {
+        ::new (static_cast<void*>(p)) U;
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a)
+    {
+        ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+    }
+};
+
 struct OctreeStats {
     int64_t inner = 0, leaves = 0, empty_leaves = 0, max_leaf = 0, max_depth = 0, nodes = 0;
 };
 
 struct FlatOctree {
-    std::vector<GNode> nodes;      // nodes[0] = root (empty when there are no triangles)
-    std::vector<GTri> tris;        // leaf-contiguous
-    std::vector<int32_t> tri_id;   // GTri slot -> caller triangle index
+    std::vector<GNode, DefaultInitAlloc<GNode>> nodes;       // nodes[0] = root (empty when there are no triangles)
+    std::vector<GTri, DefaultInitAlloc<GTri>> tris;          // leaf-contiguous
+    std::vector<int32_t, DefaultInitAlloc<int32_t>> tri_id;  // GTri slot -> caller triangle index
     int levels = 0;                // max depth + 1 of the flattened tree
     bool ordered_slabs = true;     // every node has dn[i] <= df[i] (kernels.hip vol_test)
     OctreeStats stats;             // of the unflattened (reference) tree
 };
 
-// Builds the reference octree over tri9 ([n][9] world-space vertices) and flattens it.
+// Builds the reference octree over tri9 ([n][9] world-space vertices) and flattens it
+// (parallel level-by-level build; RT_BUILD_THREADS threads, default min(cores, 16)).
 void build_flat_octree(const float* tri9, int64_t n, int max_depth, int leaf_max_obj_count, FlatOctree& out);
+// The same tree by the reference's one-insert-at-a-time algorithm (the specification
+// the parallel build is tested against: rt_octree_digest).
+void build_flat_octree_serial(const float* tri9, int64_t n, int max_depth, int leaf_max_obj_count, FlatOctree& out);
 
 }  // namespace rt
