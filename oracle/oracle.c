@@ -685,6 +685,7 @@ struct orc_ctx {
 typedef struct {
     const struct orc_ctx *X;
     uint32_t rng;
+    uint32_t frame_key;   /* key of the next compute_reflection frame (see pixel_seed) */
     orc_counters *cnt;
     int ray_kind;   /* 0 primary, 1 shadow, 2 reflection (for counters) */
     float alpha;    /* Color::a of the last trace_ray result (sky textures carry theirs) */
@@ -704,6 +705,25 @@ static uint32_t pixel_seed(uint32_t pixel, uint32_t seed)
     x ^= x >> 16;
     return x ? x : 0x9E3779B9u;
 }
+
+/* Path-keyed streams (ref_harness.cpp HRng): the frame of a primary hit is keyed
+ * pixel_seed(pixel, seed); sample i of a frame draws from sample_state(key, i) and
+ * the frame its hit spawns is keyed child_key(key, i). */
+static uint32_t mix32(uint32_t x)
+{
+    x ^= x >> 16; x *= 0x7feb352dU;
+    x ^= x >> 15; x *= 0x846ca68bU;
+    x ^= x >> 16;
+    return x;
+}
+
+static uint32_t sample_state(uint32_t key, uint32_t i)
+{
+    uint32_t x = mix32(key ^ (0x9E3779B9u * (2u * i + 1u)));
+    return x ? x : 0x9E3779B9u;
+}
+
+static uint32_t child_key(uint32_t key, uint32_t i) { return mix32(key ^ (0x85EBCA6Bu * (2u * i + 2u))); }
 
 /* XorShiftGenerator::get_rand / get_rand_bilateral, xorshift.h:43-57 */
 static float rng_bilateral(otracer *T)
@@ -852,7 +872,10 @@ static c3 compute_reflection(otracer *T, v3 rd_in, v3 ip, const ohit *h, int dep
     v3 perfect = vsub(rd_in, vscale(2 * vdot(rd_in, nn), nn));
     int sample_count = 0;
     c3 total = C(0.0f, 0.0f, 0.0f);
+    const uint32_t key = T->frame_key;
     for (int i = 0; i < X->s.rough_reflections_sample_count; i++) {
+        T->rng = sample_state(key, (uint32_t)i);
+        T->frame_key = child_key(key, (uint32_t)i);
         float roughness;
         if (X->s.enable_roughness_mapping) {
             float tu, tv;
@@ -1116,6 +1139,7 @@ ORC_API int orc_render_rows(const struct orc_ctx *X, int row_begin, int row_coun
         T.cnt = &local;
         T.ray_kind = 0;
         T.rng = 1;
+        T.frame_key = 0;
 #ifdef _OPENMP
 #pragma omp for schedule(dynamic)
 #endif
@@ -1128,7 +1152,7 @@ ORC_API int orc_render_rows(const struct orc_ctx *X, int row_begin, int row_coun
                 v3 rd = vnormalize(vsub(ws, cam));
                 int found = 0, src = -1, shadowed = 0;
                 ohit hi = hit_fresh();
-                T.rng = pixel_seed((uint32_t)(py * rw + px), X->s.rng_seed);
+                T.frame_key = pixel_seed((uint32_t)(py * rw + px), X->s.rng_seed);
                 T.ray_kind = 0;
                 local.primary_rays++;
                 c3 c = trace_ray(&T, cam, rd, &hi, 0, &found, &src, &shadowed);

@@ -98,11 +98,15 @@ uint32_t h_color_to_argb(const Color& c)
     return h_qrgb(h_f2i(c.r * 255), h_f2i(c.g * 255), h_f2i(c.b * 255));
 }
 
-/* Counter-based RNG for rough reflections: one xorshift32 stream per primary
- * pixel (xorshift.h:37-65 semantics), seeded from the pixel index.  The
+/* Path-keyed RNG for rough reflections (xorshift.h:37-65 draws).  The
  * reference seeds one generator per OpenMP thread with std::rand(), so its
  * stream is not reproducible; this one is shared verbatim by the oracle and the
- * HIP kernel. */
+ * HIP kernels.  Every compute_reflection call (a "frame") has a 32-bit key: the
+ * frame of a primary hit is keyed by h_pixel_seed(pixel, seed); sample i of a
+ * frame draws its three randoms from a fresh xorshift32 state
+ * h_sample_state(key, i), and the frame its hit spawns is keyed
+ * h_child_key(key, i).  No draw depends on how many randoms other samples used,
+ * so the samples of a frame can be traced in any order. */
 struct HRng {
     uint32_t state;
     uint32_t next()
@@ -124,6 +128,22 @@ uint32_t h_pixel_seed(uint32_t pixel, uint32_t seed)
     x ^= x >> 16;
     return x ? x : 0x9E3779B9u;
 }
+
+uint32_t h_mix32(uint32_t x)
+{
+    x ^= x >> 16; x *= 0x7feb352dU;
+    x ^= x >> 15; x *= 0x846ca68bU;
+    x ^= x >> 16;
+    return x;
+}
+
+uint32_t h_sample_state(uint32_t key, uint32_t i)
+{
+    uint32_t x = h_mix32(key ^ (0x9E3779B9u * (2u * i + 1u)));
+    return x ? x : 0x9E3779B9u;
+}
+
+uint32_t h_child_key(uint32_t key, uint32_t i) { return h_mix32(key ^ (0x85EBCA6Bu * (2u * i + 2u))); }
 
 struct HScene {
     std::vector<Triangle> tris;
@@ -202,6 +222,7 @@ void build_scene(HScene& H, const orc_scene* sc, const orc_settings* st)
 struct Tracer {
     const HScene& H;
     HRng rng;
+    uint32_t frame_key = 0;   // key of the next compute_reflection frame (see HRng)
 
     explicit Tracer(const HScene& h) : H(h), rng{1} {}
 
@@ -340,7 +361,10 @@ struct Tracer {
         Vector perfect = ray._direction - 2 * dot(ray._direction, nn) * nn;
         int sample_count = 0;
         Color total = Color(0.0f);
+        const uint32_t key = frame_key;
         for (int i = 0; i < H.s.rough_reflections_sample_count; i++) {
+            rng.state = h_sample_state(key, (uint32_t)i);
+            frame_key = h_child_key(key, (uint32_t)i);
             float roughness;
             if (H.s.enable_roughness_mapping) {
                 float tu, tv;
@@ -690,7 +714,7 @@ static int render_rows_strided(const orc_scene* sc, const orc_settings* st, int 
                 Ray ray(cp, rd);
                 bool found = false;
                 HitInfo hi;
-                tr.rng.state = h_pixel_seed((uint32_t)(py * rw + px), st->rng_seed);
+                tr.frame_key = h_pixel_seed((uint32_t)(py * rw + px), st->rng_seed);
                 int src = -1;
                 bool shadowed = false;
                 local.primary_rays++;

@@ -930,6 +930,28 @@ __device__ __forceinline__ uint32_t pixel_seed(uint32_t pixel, uint32_t seed)
     return x ? x : 0x9E3779B9u;
 }
 
+// Path-keyed streams (oracle/ref_harness.cpp HRng): the frame of a primary hit is
+// keyed pixel_seed(pixel, seed); sample i of a frame draws from sample_state(key, i)
+// and the frame its hit spawns is keyed child_key(key, i).
+__device__ __forceinline__ uint32_t mix32(uint32_t x)
+{
+    x ^= x >> 16; x *= 0x7feb352dU;
+    x ^= x >> 15; x *= 0x846ca68bU;
+    x ^= x >> 16;
+    return x;
+}
+
+__device__ __forceinline__ uint32_t sample_state(uint32_t key, uint32_t i)
+{
+    uint32_t x = mix32(key ^ (0x9E3779B9u * (2u * i + 1u)));
+    return x ? x : 0x9E3779B9u;
+}
+
+__device__ __forceinline__ uint32_t child_key(uint32_t key, uint32_t i)
+{
+    return mix32(key ^ (0x85EBCA6Bu * (2u * i + 2u)));
+}
+
 __device__ __forceinline__ float rng_bilateral(uint32_t& s)
 {
     uint32_t x = s;
@@ -949,6 +971,7 @@ struct Frame {
     v3 ro, perfect, n;
     float rough;
     int mat, i, sc;
+    uint32_t key;   // RNG key of this compute_reflection call
     Rec rhi;
 };
 
@@ -965,7 +988,7 @@ struct PixelOut {
 // Renderer::trace_ray (renderer.cpp:1008-1066) for one primary ray, with the
 // compute_reflection recursion (when REFL) unrolled onto an explicit stack.
 template <bool REFL>
-__device__ PixelOut trace_pixel(const KParams& P, v3 cam, v3 rd0, uint2* lv, uint32_t rng, unsigned& nshadow,
+__device__ PixelOut trace_pixel(const KParams& P, v3 cam, v3 rd0, uint2* lv, uint32_t pixel_key, unsigned& nshadow,
                                 unsigned& nrefl)
 {
     PixelOut po;
@@ -992,6 +1015,7 @@ __device__ PixelOut trace_pixel(const KParams& P, v3 cam, v3 rd0, uint2* lv, uin
     v3 ro = cam, rd = rd0;
     c3 ret = col(0, 0, 0);
     bool first = true;   // the depth-0 closest hit is already in po.fin
+    uint32_t next_key = pixel_key;   // key of a frame spawned by the trace in progress
     state = S_TRACE;
     for (;;) {
         if (state == S_TRACE) {
@@ -1038,6 +1062,7 @@ __device__ PixelOut trace_pixel(const KParams& P, v3 cam, v3 rd0, uint2* lv, uin
                 F.i = 0;
                 F.sc = 0;
                 F.total = col(0.0f, 0.0f, 0.0f);
+                F.key = next_key;
                 F.rhi = rec_fresh();
                 f = depth;
                 state = S_NEXT;
@@ -1068,7 +1093,9 @@ __device__ PixelOut trace_pixel(const KParams& P, v3 cam, v3 rd0, uint2* lv, uin
             Frame& F = fr[f];
             if (F.i < N) {
                 v3 dir;
+                next_key = child_key(F.key, (uint32_t)F.i);
                 if (F.rough > 0) {
+                    uint32_t rng = sample_state(F.key, (uint32_t)F.i);
                     float rx = rng_bilateral(rng);
                     float ry = rng_bilateral(rng);
                     float rz = rng_bilateral(rng);
