@@ -1350,6 +1350,314 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_pipe_kernel(KParams P
         atomicAdd(&P.counters[0], (unsigned long long)nshadow);
 }
 
+// ===========================================================================
+// Reflections as frames.  trace_pixel<true> walks one pixel's compute_reflection
+// recursion on one lane, ray after ray: with rough reflections a pixel owns up to
+// N^depth rays and the frame time is set by the costliest pixel's chain.  Here
+// every compute_reflection call is a frame record and the recursion runs level by
+// level (host loop in renderer.cpp, chunks of frames, depth-first over chunks):
+//   gen:    the N sample directions of each frame (path-keyed RNG: no draw
+//           depends on another sample)                 renderer.cpp:296-315
+//   trace:  every sample's closest-hit query, one lane per sample
+//   pass1:  per frame, in sample order: the samples' hits merged into the shared
+//           reflection_hit_info, shade_lit (normal mapping rewrites the shared
+//           record, as in the reference)               renderer.cpp:286, 1015-1044
+//   shadow: every shaded sample's is_shadowed query, one lane per sample
+//   spawn:  reflective hits become the next level's frames
+//   resolve (after the next level): the samples' colours summed in sample order,
+//           (total / sc) * reflection, shade_finish    renderer.cpp:316-337, 594-616
+// Per pixel the results are trace_pixel<true>'s, bit for bit.
+// ===========================================================================
+__device__ __forceinline__ v3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
+__device__ __forceinline__ void st3(float* p, v3 v) { p[0] = v.x; p[1] = v.y; p[2] = v.z; }
+__device__ __forceinline__ void st3(float* p, c3 c) { p[0] = c.r; p[1] = c.g; p[2] = c.b; }
+__device__ __forceinline__ c3 ldc(const float* p) { return col(p[0], p[1], p[2]); }
+
+__device__ __forceinline__ void wave_count_add(unsigned long long* ctr, unsigned v)
+{
+    for (int off = 32; off > 0; off >>= 1)
+        v += __shfl_xor(v, off);
+    if ((threadIdx.x & 63) == 0 && v)
+        atomicAdd(ctr, (unsigned long long)v);
+}
+
+// compute_reflection prologue (renderer.cpp:285-296) for the hit record h
+__device__ __forceinline__ float frame_roughness(const KParams& P, const Rec& h, const float* m)
+{
+    if (P.enable_roughness_mapping) {
+        float tu, tv;
+        get_tex_coords(P, h.tri, h.u, h.v, tu, tv);
+        return tex_floor(P.tex[TEX_ROUGHNESS], tu, tv).r;
+    }
+    return m[13];
+}
+
+__device__ __forceinline__ int frame_nsamp(const KParams& P, float rough)
+{
+    int N = P.rough_reflections_sample_count;
+    return N <= 0 ? 0 : (rough > 0 ? N : 1);
+}
+
+__device__ __forceinline__ void make_frame(const KParams& P, FrameRec& F, v3 ip, v3 n, v3 rd, c3 fc, float rough,
+                                           int mat, uint32_t key, int parent)
+{
+    st3(F.ro, ip + n * 0.01f);
+    st3(F.perfect, rd - (2 * dot(rd, n)) * n);
+    st3(F.n, n);
+    st3(F.fc, fc);
+    F.rough = rough;
+    F.mat = mat;
+    F.key = key;
+    F.nsamp = frame_nsamp(P, rough);
+    F.parent = parent;
+}
+
+// Level 0: the primary ray of every pixel, shaded (with its shadow query); a
+// reflective hit becomes a level-1 frame, any other pixel is finished here.
+__global__ __launch_bounds__(BLOCK, RT_OCC) void refl_level0_kernel(KParams P, FrameRec* fr1, unsigned int* nfr1)
+{
+    extern __shared__ uint2 lds_levels[];
+    uint2* lv = lds_levels + threadIdx.x;
+    int lane = threadIdx.x & 63;
+    const int ntiles = P.tiles_x * P.tiles_y;
+    v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+    unsigned nshadow = 0;
+    for (;;) {
+        int tile = 0;
+        if (lane == 0)
+            tile = (int)atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[2]), 1u);
+        tile = __builtin_amdgcn_readfirstlane(tile);
+        if (tile >= ntiles)
+            break;
+        int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+        int px = tx * 8 + (lane & 7);
+        int lr = ty * 8 + (lane >> 3);
+        int py = lr < P.local_rows ? global_row(P, lr) : P.rh;
+        if (px >= P.rw || py >= P.rh)
+            continue;
+        // ray generation, renderer.cpp:1086-1098
+        float y_world = ((float)py + 0.5f) / P.rh * 2 - 1;
+        float x_world = ((float)px + 0.5f) / P.rw * 2 - 1;
+        v3 vs = xform_point(P.proj_inv, mk(x_world, y_world, -1));
+        v3 ws = xform_point(P.cam_to_world, vs);
+        v3 rd = normalize(ws - cam);
+
+        Rec fin = rec_fresh();
+        int src = closest_hit(P, cam, rd, fin, lv);
+        bool found = false, shadowed = false, deferred = false;
+        c3 color;
+        float alpha = 1.0f;
+        size_t o = (size_t)lr * P.rw + px;
+        if (0 > P.max_recursion_depth) {
+            color = col(0.0f, 0.0f, 0.0f);   // trace_pixel: the depth test after the first closest hit
+        } else if (fin.t > 0.1f) {
+            found = true;
+            Direct D = shade_direct(P, cam, rd, fin, lv, nshadow);
+            shadowed = D.shadowed;
+            const float* m = mat_of(P, fin.mat);
+            if (m[12] > 0.0f) {
+                unsigned idx = atomicAdd(nfr1, 1u);
+                make_frame(P, fr1[idx], D.ip, fin.normal, rd, D.fc, frame_roughness(P, fin, m), fin.mat,
+                           pixel_seed((uint32_t)(py * P.rw + px), P.rng_seed), (int)o);
+                deferred = true;
+            } else
+                color = shade_finish(P, D.fc, m, col(0, 0, 0));
+        } else
+            color = miss_color(P, rd, alpha);
+        if (!deferred) {
+            if (P.argb) P.argb[o] = color_to_argb(color);
+            if (P.rgba) P.rgba[o] = make_float4(color.r, color.g, color.b, alpha);
+        }
+        if (P.hit_id) P.hit_id[o] = found ? src : -1;
+        if (P.hit_t) P.hit_t[o] = fin.t;
+        if (P.shadow) P.shadow[o] = (uint8_t)(found && shadowed);
+    }
+    if (nshadow) atomicAdd(&P.counters[0], (unsigned long long)nshadow);
+}
+
+// gen: one thread per sample slot of the chunk
+__global__ __launch_bounds__(BLOCK) void refl_gen_kernel(KParams P, ReflArgs A)
+{
+    int slot = blockIdx.x * BLOCK + threadIdx.x;
+    int nslot = (A.c1 - A.c0) * A.stride;
+    unsigned count = 0;
+    if (slot < nslot) {
+        int f = A.c0 + slot / A.stride, i = slot % A.stride;
+        const FrameRec& F = A.fr[f];
+        SampleRec& S = A.sm[slot];
+        if (i < F.nsamp) {
+            v3 dir;
+            if (F.rough > 0) {
+                uint32_t rng = sample_state(F.key, (uint32_t)i);
+                float rx = rng_bilateral(rng);
+                float ry = rng_bilateral(rng);
+                float rz = rng_bilateral(rng);
+                v3 rdir = normalize(mk(rx, ry, rz));
+                if (dot(rdir, ld3(F.n)) < 0)
+                    rdir = -rdir;
+                dir = F.rough * rdir + (1 - F.rough) * ld3(F.perfect);
+            } else
+                dir = ld3(F.perfect);
+            st3(S.d, dir);
+            if (A.level > P.max_recursion_depth) {   // trace_ray's depth guard (renderer.cpp:1012-1013)
+                S.kind = 0;
+                st3(S.fc, col(0.0f, 0.0f, 0.0f));
+                S.ray = 0;
+            } else {
+                S.kind = 1;
+                S.ray = 1;
+            }
+            if (i == 0)
+                count = (unsigned)F.nsamp;   // reflection rays
+        } else {
+            S.kind = 2;
+            S.ray = 0;
+        }
+    }
+    wave_count_add(&P.counters[1], count);
+}
+
+// trace: the samples' closest-hit queries
+__global__ __launch_bounds__(BLOCK) void refl_trace_kernel(KParams P, ReflArgs A)
+{
+    extern __shared__ uint2 lds_levels[];
+    uint2* lv = lds_levels + threadIdx.x;
+    int slot = blockIdx.x * BLOCK + threadIdx.x;
+    int nslot = (A.c1 - A.c0) * A.stride;
+    if (slot >= nslot || !A.sm[slot].ray)
+        return;
+    const FrameRec& F = A.fr[A.c0 + slot / A.stride];
+    TRay R = make_ray(P, ld3(F.ro), ld3(A.sm[slot].d));
+    THit h;
+    bool r = bvh_closest(P, R, h, lv);
+    RawHit H;
+    H.t = h.t;
+    H.u = h.u;
+    H.v = h.v;
+    H.k = h.k;
+    H.r = r ? 1 : 0;
+    A.hit[slot] = H;
+}
+
+// pass1: per frame, the samples' trace_ray up to the shadow query, in sample order
+__global__ __launch_bounds__(BLOCK) void refl_pass1_kernel(KParams P, ReflArgs A)
+{
+    int f = A.c0 + blockIdx.x * BLOCK + threadIdx.x;
+    unsigned nshadow = 0;
+    if (f < A.c1) {
+        const FrameRec& F = A.fr[f];
+        v3 ro = ld3(F.ro);
+        Rec rhi = rec_fresh();   // reflection_hit_info, renderer.cpp:286
+        for (int i = 0; i < F.nsamp; i++) {
+            int slot = (f - A.c0) * A.stride + i;
+            SampleRec& S = A.sm[slot];
+            if (!S.ray)
+                continue;   // depth limit: trace_ray returns before touching the record
+            v3 d = ld3(S.d);
+            RawHit H = A.hit[slot];
+            THit h;
+            h.t = H.t;
+            h.u = H.u;
+            h.v = H.v;
+            h.k = H.k;
+            Rec local = rec_fresh();
+            int s = -1;
+            bvh_record(P, h, H.r != 0, local, rhi, s);
+            shapes_closest(P, ro, d, local, rhi, s);
+            if (rhi.t > 0.1f) {
+                v3 ip;
+                c3 fc = shade_lit(P, ro, d, rhi, ip);   // may normal-map rhi.normal (persists)
+                S.kind = 1;
+                st3(S.fc, fc);
+                st3(S.ip, ip);
+                st3(S.nrm, rhi.normal);
+                S.mat = rhi.mat;
+                const float* m = mat_of(P, rhi.mat);
+                S.crough = m[12] > 0.0f ? frame_roughness(P, rhi, m) : 0.0f;
+                if (P.compute_shadows)
+                    nshadow++;
+            } else {
+                float a;
+                S.kind = 0;
+                st3(S.fc, miss_color(P, d, a));
+            }
+        }
+    }
+    wave_count_add(&P.counters[0], nshadow);
+}
+
+// shadow: is_shadowed (renderer.cpp:340-402) for every shaded sample
+__global__ __launch_bounds__(BLOCK) void refl_shadow_kernel(KParams P, ReflArgs A)
+{
+    extern __shared__ uint2 lds_levels[];
+    uint2* lv = lds_levels + threadIdx.x;
+    int slot = blockIdx.x * BLOCK + threadIdx.x;
+    int nslot = (A.c1 - A.c0) * A.stride;
+    if (slot >= nslot)
+        return;
+    SampleRec& S = A.sm[slot];
+    if (!S.ray || S.kind != 1)
+        return;
+    v3 light = mk(P.light[0], P.light[1], P.light[2]);
+    S.sh = is_shadowed(P, ld3(S.ip), ld3(S.nrm), light, lv) ? 1 : 0;
+}
+
+// spawn: reflective hits become frames of the next level
+__global__ __launch_bounds__(BLOCK) void refl_spawn_kernel(KParams P, ReflArgs A)
+{
+    int slot = blockIdx.x * BLOCK + threadIdx.x;
+    int nslot = (A.c1 - A.c0) * A.stride;
+    if (slot >= nslot)
+        return;
+    SampleRec& S = A.sm[slot];
+    S.child = -1;
+    if (!S.ray || S.kind != 1)
+        return;
+    const float* m = mat_of(P, S.mat);
+    if (!(m[12] > 0.0f))
+        return;
+    int f = A.c0 + slot / A.stride, i = slot % A.stride;
+    const FrameRec& F = A.fr[f];
+    unsigned idx = atomicAdd(A.child_count, 1u);
+    c3 dfc = shade_shadow_emit(P, ldc(S.fc), m, S.sh != 0);
+    make_frame(P, A.child_fr[idx], ld3(S.ip), ld3(S.nrm), ld3(S.d), dfc, S.crough, S.mat,
+               child_key(F.key, (uint32_t)i), -1);
+    S.child = (int)idx;
+}
+
+// resolve: compute_reflection's sum in sample order, then the frame's hit colour
+__global__ __launch_bounds__(BLOCK) void refl_resolve_kernel(KParams P, ReflArgs A)
+{
+    int f = A.c0 + blockIdx.x * BLOCK + threadIdx.x;
+    if (f >= A.c1)
+        return;
+    const FrameRec& F = A.fr[f];
+    c3 total = col(0.0f, 0.0f, 0.0f);
+    for (int i = 0; i < F.nsamp; i++) {
+        const SampleRec& S = A.sm[(f - A.c0) * A.stride + i];
+        c3 ret;
+        if (S.kind == 0)
+            ret = ldc(S.fc);
+        else if (S.child >= 0)
+            ret = ldc(A.child_ret + 3 * (size_t)S.child);
+        else {
+            const float* m = mat_of(P, S.mat);
+            ret = shade_finish(P, shade_shadow_emit(P, ldc(S.fc), m, S.sh != 0), m, col(0, 0, 0));
+        }
+        total = total + ret;
+    }
+    const float* m = mat_of(P, F.mat);
+    float sc = (float)F.nsamp, rf = m[12];
+    c3 R = (total / col(sc, sc, sc)) * col(rf, rf, rf);
+    c3 c = shade_finish(P, ldc(F.fc), m, R);
+    if (A.level == 1) {
+        size_t o = (size_t)F.parent;
+        if (P.argb) P.argb[o] = color_to_argb(c);
+        if (P.rgba) P.rgba[o] = make_float4(c.r, c.g, c.b, 1.0f);
+    } else
+        st3(A.ret + 3 * (size_t)f, c);
+}
+
 // ImageUtils::downscale_image_qt_ARGB32 (imageUtils.h:98-147): integer box
 // filter of 8-bit channels, truncating division.
 __global__ __launch_bounds__(256) void downscale_kernel(const uint32_t* __restrict__ in, int w, int h_rows, int f,
@@ -1449,5 +1757,41 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_downscale(
         return hipSuccess;
     dim3 grid((dw + 255) / 256, dh);
     hipLaunchKernelGGL(rt::downscale_kernel, grid, dim3(256), 0, stream, in, w, h_rows, f, out);
+    return hipGetLastError();
+}
+
+// ---- reflection engine launchers (renderer.cpp drives the levels) ----
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_level0(const rt::KParams* P, rt::FrameRec* fr1,
+                                                                           unsigned int* nfr1, hipStream_t stream)
+{
+    int tiles = P->tiles_x * P->tiles_y;
+    int blocks = (tiles + rt::WAVES_PER_BLOCK - 1) / rt::WAVES_PER_BLOCK;
+    if (blocks > P->max_blocks && P->max_blocks > 0)
+        blocks = P->max_blocks;
+    if (blocks < 1)
+        return hipSuccess;
+    size_t lds = (size_t)(P->levels > 0 ? P->levels : 1) * rt::BLOCK * sizeof(uint2);
+    hipLaunchKernelGGL(rt::refl_level0_kernel, dim3(blocks), dim3(rt::BLOCK), lds, stream, *P, fr1, nfr1);
+    return hipGetLastError();
+}
+
+// stage: 0 gen, 1 trace, 2 pass1, 3 shadow, 4 spawn, 5 resolve
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_stage(int stage, const rt::KParams* P,
+                                                                          const rt::ReflArgs* A, hipStream_t stream)
+{
+    int nframes = A->c1 - A->c0;
+    if (nframes <= 0)
+        return hipSuccess;
+    int nslot = nframes * A->stride;
+    dim3 gs((nslot + rt::BLOCK - 1) / rt::BLOCK), gf((nframes + rt::BLOCK - 1) / rt::BLOCK);
+    size_t lds = (size_t)(P->levels > 0 ? P->levels : 1) * rt::BLOCK * sizeof(uint2);
+    switch (stage) {
+    case 0: hipLaunchKernelGGL(rt::refl_gen_kernel, gs, dim3(rt::BLOCK), 0, stream, *P, *A); break;
+    case 1: hipLaunchKernelGGL(rt::refl_trace_kernel, gs, dim3(rt::BLOCK), lds, stream, *P, *A); break;
+    case 2: hipLaunchKernelGGL(rt::refl_pass1_kernel, gf, dim3(rt::BLOCK), 0, stream, *P, *A); break;
+    case 3: hipLaunchKernelGGL(rt::refl_shadow_kernel, gs, dim3(rt::BLOCK), lds, stream, *P, *A); break;
+    case 4: hipLaunchKernelGGL(rt::refl_spawn_kernel, gs, dim3(rt::BLOCK), 0, stream, *P, *A); break;
+    default: hipLaunchKernelGGL(rt::refl_resolve_kernel, gf, dim3(rt::BLOCK), 0, stream, *P, *A); break;
+    }
     return hipGetLastError();
 }

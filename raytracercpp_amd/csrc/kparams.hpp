@@ -79,4 +79,51 @@ struct KParams {
     unsigned long long* counters;   // [0] shadow rays, [1] reflection rays, [2] tile queue head
 };
 
+// ---- reflection engine (kernels.hip, "Reflections as frames") ----
+// One Renderer::compute_reflection call (renderer.cpp:283-338) of one pixel.
+struct FrameRec {
+    float ro[3];        // hit point + n * 0.01
+    float perfect[3];   // perfect reflection direction
+    float n[3];         // (normal-mapped) normal of the hit that reflects
+    float fc[3];        // shade_direct colour of that hit (shadow and emission applied)
+    float rough;
+    int32_t mat;
+    uint32_t key;       // RNG key (path-keyed streams)
+    int32_t nsamp;      // samples it traces: N (rough > 0), 1 (rough <= 0), 0 (N == 0)
+    int32_t parent;     // launch-local pixel (level 1 frames)
+};
+
+// One sample of a frame: trace_ray(depth + 1) into the frame's shared HitInfo.
+struct SampleRec {
+    float d[3];         // direction
+    int32_t kind;       // 0: colour final in fc (miss / depth limit), 1: shaded hit, 2: no sample
+    float fc[3];        // shade_lit colour (kind 1) or the returned colour (kind 0)
+    float ip[3];        // hit point
+    float nrm[3];       // shading normal after normal mapping
+    int32_t mat;
+    float crough;       // roughness of the frame this hit spawns (reflective material)
+    int32_t sh;         // is_shadowed
+    int32_t child;      // frame index at the next level
+    int32_t ray;        // 1: closest-hit query to trace
+};
+
+struct RawHit {
+    float t, u, v;
+    int32_t k;          // GTri slot, -1 none
+    int32_t r;          // the query's return value
+};
+
+struct ReflArgs {
+    FrameRec* fr;            // this level's frames
+    SampleRec* sm;           // the chunk's samples, (f - c0) * stride + i
+    RawHit* hit;             // per sample
+    float* ret;              // per frame of this level: colour returned to the parent sample (3 floats)
+    const float* child_ret;  // the next level's ret
+    FrameRec* child_fr;      // the next level's frames
+    unsigned int* child_count;
+    int32_t c0, c1;          // frames [c0, c1) of this level
+    int32_t level;           // samples trace at depth = level
+    int32_t stride;          // max(N, 1)
+};
+
 }  // namespace rt

@@ -3,6 +3,7 @@
 
 #include <cstdlib>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -10,6 +11,10 @@
 #include "host_scene.hpp"
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(const rt::KParams* P, hipStream_t stream);
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_level0(const rt::KParams* P, rt::FrameRec* fr1,
+                                                                           unsigned int* nfr1, hipStream_t stream);
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_stage(int stage, const rt::KParams* P,
+                                                                          const rt::ReflArgs* A, hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_trace_rays(const rt::KParams* P, const float* o, const float* d, int n, int32_t* id,
                                            float* t, float* u, float* v, uint8_t* ret, hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_downscale(const uint32_t* in, int w, int h_rows, int f, uint32_t* out,
@@ -533,6 +538,88 @@ void Renderer::fill_params(KParams& P) const
 }
 
 
+// The trace of one launch (ray_trace / render_bands_device).  Reflective scenes
+// with the BVH run the reflection engine (kernels.hip, "Reflections as frames"):
+// level 0 shades every primary hit and turns the reflective ones into frames; each
+// level then traces its frames' samples in chunks, depth-first over chunks.
+// RT_REFL_ENGINE=0 selects the one-lane-per-pixel recursive kernel instead.
+int Renderer::launch_trace(const KParams& P, hipStream_t stream)
+{
+    hipError_t e;
+    const char* env = getenv("RT_REFL_ENGINE");
+    bool engine = P.has_reflection && P.enable_bvh && !(env && env[0] == '0');
+    if (!engine) {
+        if ((e = rt_launch_ray_trace(&P, stream)) != hipSuccess)
+            return hip_fail(e, "ray_trace_kernel launch");
+        return RT_OK;
+    }
+    for (auto& L : refl_)
+        L.fr.device = L.ret.device = L.sm.device = L.hit.device = L.cnt.device = device_;
+    size_t npx = (size_t)P.rw * P.local_rows;
+    ReflLevel& L1 = refl_[1];
+    if ((e = L1.fr.reserve(npx * sizeof(FrameRec))) != hipSuccess || (e = L1.cnt.reserve(64)) != hipSuccess)
+        return hip_fail(e, "hipMalloc (reflection frames)");
+    if ((e = hipMemsetAsync(L1.cnt.p, 0, 4, stream)) != hipSuccess)
+        return hip_fail(e, "hipMemsetAsync");
+    if ((e = rt_launch_refl_level0(&P, L1.fr.as<FrameRec>(), L1.cnt.as<unsigned int>(), stream)) != hipSuccess)
+        return hip_fail(e, "refl_level0_kernel launch");
+    unsigned n1 = 0;
+    if ((e = hipMemcpyAsync(&n1, L1.cnt.p, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(stream)) != hipSuccess)
+        return hip_fail(e, "refl_level0_kernel");
+    return refl_level(P, 1, (int)n1, stream);
+}
+
+// Frames [0, nframes) of 'level' (their samples trace at depth 'level'), in chunks;
+// each chunk's child frames are resolved (recursively) before its own resolve.
+int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t stream)
+{
+    const int N = P.rough_reflections_sample_count;
+    const int stride = N > 0 ? N : 1;
+    const int chunk = std::max(1024, (1 << 21) / stride);   // about 2M sample slots per chunk
+    if (level + 1 >= REFL_LEVELS)
+        return fail(RT_EUNSUPPORTED, "reflection recursion deeper than the engine's levels");
+    ReflLevel& L = refl_[level];
+    ReflLevel& C = refl_[level + 1];
+    size_t slots = (size_t)std::min(nframes, chunk) * stride;
+    hipError_t e;
+    if ((e = L.ret.reserve((size_t)nframes * 12)) != hipSuccess || (e = L.sm.reserve(slots * sizeof(SampleRec))) != hipSuccess ||
+        (e = L.hit.reserve(slots * sizeof(RawHit))) != hipSuccess || (e = L.cnt.reserve(64)) != hipSuccess ||
+        (e = C.fr.reserve(slots * sizeof(FrameRec))) != hipSuccess || (e = C.ret.reserve(slots * 12)) != hipSuccess)
+        return hip_fail(e, "hipMalloc (reflection level)");
+    for (int c0 = 0; c0 < nframes; c0 += chunk) {
+        ReflArgs A;
+        A.fr = L.fr.as<FrameRec>();
+        A.sm = L.sm.as<SampleRec>();
+        A.hit = L.hit.as<RawHit>();
+        A.ret = L.ret.as<float>();
+        A.child_ret = C.ret.as<float>();
+        A.child_fr = C.fr.as<FrameRec>();
+        A.child_count = L.cnt.as<unsigned int>();
+        A.c0 = c0;
+        A.c1 = std::min(nframes, c0 + chunk);
+        A.level = level;
+        A.stride = stride;
+        if ((e = hipMemsetAsync(L.cnt.p, 0, 4, stream)) != hipSuccess)
+            return hip_fail(e, "hipMemsetAsync");
+        for (int stage = 0; stage <= 4; stage++)
+            if ((e = rt_launch_refl_stage(stage, &P, &A, stream)) != hipSuccess)
+                return hip_fail(e, "reflection stage launch");
+        unsigned nchild = 0;
+        if ((e = hipMemcpyAsync(&nchild, L.cnt.p, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+            (e = hipStreamSynchronize(stream)) != hipSuccess)
+            return hip_fail(e, "reflection stages");
+        if (nchild > 0) {
+            int rc = refl_level(P, level + 1, (int)nchild, stream);
+            if (rc != RT_OK)
+                return rc;
+        }
+        if ((e = rt_launch_refl_stage(5, &P, &A, stream)) != hipSuccess)
+            return hip_fail(e, "refl_resolve_kernel launch");
+    }
+    return RT_OK;
+}
+
 // Renderer::ray_trace, renderer.cpp:1068-1116
 int Renderer::ray_trace()
 {
@@ -567,7 +654,7 @@ int Renderer::ray_trace()
     P.counters = d_counters_.as<unsigned long long>();
     if ((e = hipMemsetAsync(d_counters_.p, 0, 64, stream_)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
     hipEventRecord(ev_[0], stream_);
-    if ((e = rt_launch_ray_trace(&P, stream_)) != hipSuccess) return hip_fail(e, "ray_trace_kernel launch");
+    if ((rc = launch_trace(P, stream_)) != RT_OK) return rc;
     hipEventRecord(ev_[1], stream_);
     unsigned long long cnt[2] = {0, 0};
     if ((e = hipMemcpyAsync(cnt, d_counters_.p, sizeof(cnt), hipMemcpyDeviceToHost, stream_)) != hipSuccess)
@@ -737,7 +824,7 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
     }
     if ((e = hipMemsetAsync(d_counters_.p, 0, 64, stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
     hipEventRecord(ring_[2 * ring_next_], stream);
-    if ((e = rt_launch_ray_trace(&P, stream)) != hipSuccess) return hip_fail(e, "ray_trace_kernel launch");
+    if ((rc = launch_trace(P, stream)) != RT_OK) return rc;
     hipEventRecord(ring_[2 * ring_next_ + 1], stream);
     ring_next_ = (ring_next_ + 1) % EV_RING;
     if (ring_count_ < EV_RING) ring_count_++;

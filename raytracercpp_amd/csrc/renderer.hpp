@@ -88,6 +88,9 @@ private:
     int ensure_device_scene();
     int validate() const;
     void fill_params(KParams& P) const;
+    // the trace of one launch: the ray-trace kernel, or the reflection engine (frames by level)
+    int launch_trace(const KParams& P, hipStream_t stream);
+    int refl_level(const KParams& P, int level, int nframes, hipStream_t stream);
 
     int device_;
     int num_cus_ = 256;
@@ -126,6 +129,13 @@ private:
     int img_w_ = 0, img_h_ = 0;
     bool img_is_internal_ = false;
     bool rendered_ = false;
+
+    // reflection engine buffers, per level (frames, results, chunk samples / hits, child counter)
+    struct ReflLevel {
+        DevBuf fr, ret, sm, hit, cnt;
+    };
+    static constexpr int REFL_LEVELS = 18;   // max_recursion_depth <= 15: frames at levels 1..16, +1 child slot
+    ReflLevel refl_[REFL_LEVELS];
 
     // event ring for render_bands_device kernel timing
     static constexpr int EV_RING = 256;
