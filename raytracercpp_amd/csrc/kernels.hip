@@ -1475,6 +1475,35 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void refl_level0_kernel(KParams P, F
     if (nshadow) atomicAdd(&P.counters[0], (unsigned long long)nshadow);
 }
 
+// keys: 30-bit Morton code of each frame's origin in the scene box (the root's
+// axis slabs), so that a level's frames can be sorted for ray coherence
+__device__ __forceinline__ uint32_t spread10(uint32_t v)
+{
+    v &= 0x3ffu;
+    v = (v | (v << 16)) & 0x030000ffu;
+    v = (v | (v << 8)) & 0x0300f00fu;
+    v = (v | (v << 4)) & 0x030c30c3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+
+__global__ __launch_bounds__(BLOCK) void refl_keys_kernel(KParams P, const FrameRec* fr, int n, uint32_t* keys,
+                                                          int32_t* idx)
+{
+    int f = blockIdx.x * BLOCK + threadIdx.x;
+    if (f >= n)
+        return;
+    uint32_t q[3];
+    for (int a = 0; a < 3; a++) {
+        float lo = P.nodes[0].dn[a], hi = P.nodes[0].df[a];
+        float t = (fr[f].ro[a] - lo) / (hi - lo);
+        t = t == t ? fminf(fmaxf(t, 0.0f), 1.0f) : 0.0f;
+        q[a] = (uint32_t)(t * 1023.0f);
+    }
+    keys[f] = spread10(q[0]) | (spread10(q[1]) << 1) | (spread10(q[2]) << 2);
+    idx[f] = f;
+}
+
 // gen: one thread per sample slot of the chunk
 __global__ __launch_bounds__(BLOCK) void refl_gen_kernel(KParams P, ReflArgs A)
 {
@@ -1482,7 +1511,7 @@ __global__ __launch_bounds__(BLOCK) void refl_gen_kernel(KParams P, ReflArgs A)
     int nslot = (A.c1 - A.c0) * A.stride;
     unsigned count = 0;
     if (slot < nslot) {
-        int f = A.c0 + slot / A.stride, i = slot % A.stride;
+        int f = A.order[A.c0 + slot / A.stride], i = slot % A.stride;
         const FrameRec& F = A.fr[f];
         SampleRec& S = A.sm[slot];
         if (i < F.nsamp) {
@@ -1526,7 +1555,7 @@ __global__ __launch_bounds__(BLOCK) void refl_trace_kernel(KParams P, ReflArgs A
     int nslot = (A.c1 - A.c0) * A.stride;
     if (slot >= nslot || !A.sm[slot].ray)
         return;
-    const FrameRec& F = A.fr[A.c0 + slot / A.stride];
+    const FrameRec& F = A.fr[A.order[A.c0 + slot / A.stride]];
     TRay R = make_ray(P, ld3(F.ro), ld3(A.sm[slot].d));
     THit h;
     bool r = bvh_closest(P, R, h, lv);
@@ -1542,14 +1571,14 @@ __global__ __launch_bounds__(BLOCK) void refl_trace_kernel(KParams P, ReflArgs A
 // pass1: per frame, the samples' trace_ray up to the shadow query, in sample order
 __global__ __launch_bounds__(BLOCK) void refl_pass1_kernel(KParams P, ReflArgs A)
 {
-    int f = A.c0 + blockIdx.x * BLOCK + threadIdx.x;
+    int p = A.c0 + blockIdx.x * BLOCK + threadIdx.x;
     unsigned nshadow = 0;
-    if (f < A.c1) {
-        const FrameRec& F = A.fr[f];
+    if (p < A.c1) {
+        const FrameRec& F = A.fr[A.order[p]];
         v3 ro = ld3(F.ro);
         Rec rhi = rec_fresh();   // reflection_hit_info, renderer.cpp:286
         for (int i = 0; i < F.nsamp; i++) {
-            int slot = (f - A.c0) * A.stride + i;
+            int slot = (p - A.c0) * A.stride + i;
             SampleRec& S = A.sm[slot];
             if (!S.ray)
                 continue;   // depth limit: trace_ray returns before touching the record
@@ -1586,18 +1615,36 @@ __global__ __launch_bounds__(BLOCK) void refl_pass1_kernel(KParams P, ReflArgs A
     wave_count_add(&P.counters[0], nshadow);
 }
 
-// shadow: is_shadowed (renderer.cpp:340-402) for every shaded sample
+// list: the shaded samples (the only ones with a shadow query), compacted so that
+// the shadow pass runs on full waves (one atomic per wave)
+__global__ __launch_bounds__(BLOCK) void refl_list_kernel(KParams P, ReflArgs A)
+{
+    int slot = blockIdx.x * BLOCK + threadIdx.x;
+    int nslot = (A.c1 - A.c0) * A.stride;
+    bool need = slot < nslot && A.sm[slot].ray && A.sm[slot].kind == 1;
+    if (slot < nslot && !need)
+        A.sm[slot].sh = 0;
+    uint64_t m = __ballot(need);
+    if (!m)
+        return;
+    uint32_t base = 0;
+    int leader = __ffsll((unsigned long long)m) - 1;
+    if ((threadIdx.x & 63) == leader)
+        base = atomicAdd(A.list_count, (unsigned)__popcll(m));
+    base = __shfl(base, leader);
+    if (need)
+        A.list[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = slot;
+}
+
+// shadow: is_shadowed (renderer.cpp:340-402) for every shaded sample (via the list)
 __global__ __launch_bounds__(BLOCK) void refl_shadow_kernel(KParams P, ReflArgs A)
 {
     extern __shared__ uint2 lds_levels[];
     uint2* lv = lds_levels + threadIdx.x;
-    int slot = blockIdx.x * BLOCK + threadIdx.x;
-    int nslot = (A.c1 - A.c0) * A.stride;
-    if (slot >= nslot)
+    unsigned t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= *A.list_count)
         return;
-    SampleRec& S = A.sm[slot];
-    if (!S.ray || S.kind != 1)
-        return;
+    SampleRec& S = A.sm[A.list[t]];
     v3 light = mk(P.light[0], P.light[1], P.light[2]);
     S.sh = is_shadowed(P, ld3(S.ip), ld3(S.nrm), light, lv) ? 1 : 0;
 }
@@ -1616,7 +1663,7 @@ __global__ __launch_bounds__(BLOCK) void refl_spawn_kernel(KParams P, ReflArgs A
     const float* m = mat_of(P, S.mat);
     if (!(m[12] > 0.0f))
         return;
-    int f = A.c0 + slot / A.stride, i = slot % A.stride;
+    int f = A.order[A.c0 + slot / A.stride], i = slot % A.stride;
     const FrameRec& F = A.fr[f];
     unsigned idx = atomicAdd(A.child_count, 1u);
     c3 dfc = shade_shadow_emit(P, ldc(S.fc), m, S.sh != 0);
@@ -1628,13 +1675,14 @@ __global__ __launch_bounds__(BLOCK) void refl_spawn_kernel(KParams P, ReflArgs A
 // resolve: compute_reflection's sum in sample order, then the frame's hit colour
 __global__ __launch_bounds__(BLOCK) void refl_resolve_kernel(KParams P, ReflArgs A)
 {
-    int f = A.c0 + blockIdx.x * BLOCK + threadIdx.x;
-    if (f >= A.c1)
+    int p = A.c0 + blockIdx.x * BLOCK + threadIdx.x;
+    if (p >= A.c1)
         return;
+    const int f = A.order[p];
     const FrameRec& F = A.fr[f];
     c3 total = col(0.0f, 0.0f, 0.0f);
     for (int i = 0; i < F.nsamp; i++) {
-        const SampleRec& S = A.sm[(f - A.c0) * A.stride + i];
+        const SampleRec& S = A.sm[(p - A.c0) * A.stride + i];
         c3 ret;
         if (S.kind == 0)
             ret = ldc(S.fc);
@@ -1775,7 +1823,7 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_level
     return hipGetLastError();
 }
 
-// stage: 0 gen, 1 trace, 2 pass1, 3 shadow, 4 spawn, 5 resolve
+// stage: 0 gen, 1 trace, 2 pass1, 3 shadow, 4 spawn, 5 resolve, 6 list
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_stage(int stage, const rt::KParams* P,
                                                                           const rt::ReflArgs* A, hipStream_t stream)
 {
@@ -1791,7 +1839,19 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_stage
     case 2: hipLaunchKernelGGL(rt::refl_pass1_kernel, gf, dim3(rt::BLOCK), 0, stream, *P, *A); break;
     case 3: hipLaunchKernelGGL(rt::refl_shadow_kernel, gs, dim3(rt::BLOCK), lds, stream, *P, *A); break;
     case 4: hipLaunchKernelGGL(rt::refl_spawn_kernel, gs, dim3(rt::BLOCK), 0, stream, *P, *A); break;
+    case 6: hipLaunchKernelGGL(rt::refl_list_kernel, gs, dim3(rt::BLOCK), 0, stream, *P, *A); break;
     default: hipLaunchKernelGGL(rt::refl_resolve_kernel, gf, dim3(rt::BLOCK), 0, stream, *P, *A); break;
     }
+    return hipGetLastError();
+}
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_keys(const rt::KParams* P, const rt::FrameRec* fr,
+                                                                         int n, uint32_t* keys, int32_t* idx,
+                                                                         hipStream_t stream)
+{
+    if (n <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(rt::refl_keys_kernel, dim3((n + rt::BLOCK - 1) / rt::BLOCK), dim3(rt::BLOCK), 0, stream, *P, fr,
+                       n, keys, idx);
     return hipGetLastError();
 }

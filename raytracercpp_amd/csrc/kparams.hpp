@@ -115,13 +115,16 @@ struct RawHit {
 
 struct ReflArgs {
     FrameRec* fr;            // this level's frames
-    SampleRec* sm;           // the chunk's samples, (f - c0) * stride + i
+    SampleRec* sm;           // the chunk's samples, (p - c0) * stride + i for sorted position p
     RawHit* hit;             // per sample
     float* ret;              // per frame of this level: colour returned to the parent sample (3 floats)
     const float* child_ret;  // the next level's ret
     FrameRec* child_fr;      // the next level's frames
     unsigned int* child_count;
-    int32_t c0, c1;          // frames [c0, c1) of this level
+    const int32_t* order;    // frame at sorted position p is order[p] (spatially sorted)
+    int32_t* list;           // compacted sample slots with a shadow query
+    unsigned int* list_count;
+    int32_t c0, c1;          // sorted positions [c0, c1) of this level
     int32_t level;           // samples trace at depth = level
     int32_t stride;          // max(N, 1)
 };

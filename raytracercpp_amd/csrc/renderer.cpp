@@ -1,6 +1,8 @@
 // renderer.cpp -- rt::Renderer (see renderer.hpp).
 #include "renderer.hpp"
 
+#include <hipcub/hipcub.hpp>
+
 #include <cstdlib>
 
 #include <algorithm>
@@ -15,6 +17,9 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_level
                                                                            unsigned int* nfr1, hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_stage(int stage, const rt::KParams* P,
                                                                           const rt::ReflArgs* A, hipStream_t stream);
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_keys(const rt::KParams* P, const rt::FrameRec* fr,
+                                                                         int n, uint32_t* keys, int32_t* idx,
+                                                                         hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_trace_rays(const rt::KParams* P, const float* o, const float* d, int n, int32_t* id,
                                            float* t, float* u, float* v, uint8_t* ret, hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_downscale(const uint32_t* in, int w, int h_rows, int f, uint32_t* out,
@@ -554,7 +559,8 @@ int Renderer::launch_trace(const KParams& P, hipStream_t stream)
         return RT_OK;
     }
     for (auto& L : refl_)
-        L.fr.device = L.ret.device = L.sm.device = L.hit.device = L.cnt.device = device_;
+        L.fr.device = L.ret.device = L.sm.device = L.hit.device = L.cnt.device = L.list.device = L.sort.device =
+            L.sort_tmp.device = device_;
     size_t npx = (size_t)P.rw * P.local_rows;
     ReflLevel& L1 = refl_[1];
     if ((e = L1.fr.reserve(npx * sizeof(FrameRec))) != hipSuccess || (e = L1.cnt.reserve(64)) != hipSuccess)
@@ -585,10 +591,33 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
     hipError_t e;
     if ((e = L.ret.reserve((size_t)nframes * 12)) != hipSuccess || (e = L.sm.reserve(slots * sizeof(SampleRec))) != hipSuccess ||
         (e = L.hit.reserve(slots * sizeof(RawHit))) != hipSuccess || (e = L.cnt.reserve(64)) != hipSuccess ||
+        (e = L.list.reserve(slots * 4)) != hipSuccess ||
         (e = C.fr.reserve(slots * sizeof(FrameRec))) != hipSuccess || (e = C.ret.reserve(slots * 12)) != hipSuccess)
         return hip_fail(e, "hipMalloc (reflection level)");
+    // the level's frames in Morton order of their origins (coherent sample and shadow rays)
+    if ((e = L.sort.reserve((size_t)nframes * 16)) != hipSuccess)
+        return hip_fail(e, "hipMalloc (frame sort)");
+    uint32_t* keys_in = L.sort.as<uint32_t>();
+    uint32_t* keys_out = keys_in + nframes;
+    int32_t* idx_in = reinterpret_cast<int32_t*>(keys_out + nframes);
+    int32_t* idx_out = idx_in + nframes;
+    if ((e = rt_launch_refl_keys(&P, L.fr.as<FrameRec>(), nframes, keys_in, idx_in, stream)) != hipSuccess)
+        return hip_fail(e, "refl_keys_kernel launch");
+    const int32_t* order = idx_in;
+    const char* sort_env = getenv("RT_REFL_SORT");
+    if (!(sort_env && sort_env[0] == '0')) {
+        size_t tb = 0;
+        if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys_in, keys_out, idx_in, idx_out, nframes, 0, 30,
+                                                    stream)) != hipSuccess ||
+            (e = L.sort_tmp.reserve(tb)) != hipSuccess ||
+            (e = hipcub::DeviceRadixSort::SortPairs(L.sort_tmp.p, tb, keys_in, keys_out, idx_in, idx_out, nframes, 0,
+                                                    30, stream)) != hipSuccess)
+            return hip_fail(e, "frame sort");
+        order = idx_out;
+    }
     for (int c0 = 0; c0 < nframes; c0 += chunk) {
         ReflArgs A;
+        A.order = order;
         A.fr = L.fr.as<FrameRec>();
         A.sm = L.sm.as<SampleRec>();
         A.hit = L.hit.as<RawHit>();
@@ -596,13 +625,15 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
         A.child_ret = C.ret.as<float>();
         A.child_fr = C.fr.as<FrameRec>();
         A.child_count = L.cnt.as<unsigned int>();
+        A.list = L.list.as<int32_t>();
+        A.list_count = L.cnt.as<unsigned int>() + 1;
         A.c0 = c0;
         A.c1 = std::min(nframes, c0 + chunk);
         A.level = level;
         A.stride = stride;
-        if ((e = hipMemsetAsync(L.cnt.p, 0, 4, stream)) != hipSuccess)
+        if ((e = hipMemsetAsync(L.cnt.p, 0, 8, stream)) != hipSuccess)
             return hip_fail(e, "hipMemsetAsync");
-        for (int stage = 0; stage <= 4; stage++)
+        for (int stage : {0, 1, 2, 6, 3, 4})
             if ((e = rt_launch_refl_stage(stage, &P, &A, stream)) != hipSuccess)
                 return hip_fail(e, "reflection stage launch");
         unsigned nchild = 0;
