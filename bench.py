@@ -83,7 +83,7 @@ def main():
     step()   # first call builds + uploads the octree
     torch.cuda.synchronize()
     t_first = time.perf_counter() - t_build0
-    shadow_local, _ = r.band_counters()
+    shadow_local, refl_local = r.band_counters()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -101,7 +101,7 @@ def main():
     ktimes = r.kernel_times(args.steps)
     k_mean = float(np.mean(ktimes))
 
-    t = torch.tensor([elapsed, float(shadow_local), k_mean], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, float(shadow_local), k_mean, float(refl_local)], dtype=torch.float64, device=dev)
     if world > 1:
         tm = t.clone()
         dist.all_reduce(tm, op=dist.ReduceOp.MAX)
@@ -110,18 +110,22 @@ def main():
         elapsed_max = float(tm[0])
         shadow_total = int(ts[1])
         k_mean_max = float(tm[2])
+        refl_total = int(ts[3])
     else:
-        elapsed_max, shadow_total, k_mean_max = elapsed, int(shadow_local), k_mean
+        elapsed_max, shadow_total, k_mean_max, refl_total = elapsed, int(shadow_local), k_mean, int(refl_local)
+    c5 = args.config == "sphere1m_refl"
     frame = assemble_torch(parts, H, band) if rank == 0 else None
 
     if rank == 0:
         primary = rw * rh
-        rays = primary + shadow_total
+        rays = primary + shadow_total + (refl_total if c5 else 0)
         ms_per_step = 1e3 * elapsed_max / args.steps
         value = rays * args.steps / elapsed_max / 1e6
         img = frame.cpu().numpy().view(np.uint32)
+        metric = ("Mrays/sec (primary+shadow+reflection) at 1920x1080, 1M-tri scene + rough reflections (C5)" if c5
+                  else "Mrays/sec (primary+shadow) at 1920x1080, 1M-tri scene; max |dpixel|")
         res = {
-            "metric": "Mrays/sec (primary+shadow) at 1920x1080, 1M-tri scene; max |dpixel|",
+            "metric": metric,
             "value": round(value, 3),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -133,10 +137,12 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (deterministic 1M-tri UV sphere, SURVEY.md 8(d) C4)",
-            "config": {"workload": "C4 sphere1m: 1,000,000 tris, 1920x1080, ssaa_factor 2 (3840x2160 rays), "
-                                   "primary + shadow, octree 12/40", "image": [W, H], "render": [rw, rh],
+            "config": {"workload": ("C5 sphere1m_refl: C4 + reflection 0.5 / roughness 0.3, 16 samples, depth 5, "
+                                    "normal + parallax maps" if c5 else
+                                    "C4 sphere1m: 1,000,000 tris, 1920x1080, ssaa_factor 2 (3840x2160 rays), "
+                                    "primary + shadow, octree 12/40"), "image": [W, H], "render": [rw, rh],
                        "rays_per_frame": rays, "primary_rays": primary, "shadow_rays": shadow_total,
-                       "band_rows": band, "parallelism": f"image strips x{world}"},
+                       "reflection_rays": refl_total, "band_rows": band, "parallelism": f"image strips x{world}"},
             "kernel_ms": round(k_mean_max, 4),
             "first_call_s": round(t_first, 3),
         }
@@ -162,7 +168,10 @@ def main():
                                "traffic": int(traffic) if traffic else None,
                                "algorithmic_bytes_per_frame": nbytes}
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"], res["max_abs_dpixel"] = cpu_baseline(sc, st, img, args.cpu_threads)
+            if c5:
+                res["cpu_baseline"] = cpu_baseline_c5(sc, st, args.cpu_threads)
+            else:
+                res["cpu_baseline"], res["max_abs_dpixel"] = cpu_baseline(sc, st, img, args.cpu_threads)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -202,6 +211,24 @@ def cpu_baseline(sc, st, gpu_img, threads):
                       f"excluded), reference TUs + OpenMP x{threads}",
             "port_value": port["value"]}
     return base, d
+
+
+def cpu_baseline_c5(sc, st, threads):
+    """C5: the reference harness on every 128th internal row (primary + shadow + reflection rays)."""
+    from oracle.bindings import RefHarness
+    threads = threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    if not RefHarness.available():
+        return None
+    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+    rw, rh = st.render_size()
+    stride = 128
+    rr = RefHarness.render_row_sample(sc, st, stride // 2, rh // stride, stride)
+    c = rr.counters
+    rays = c["primary_rays"] + c["shadow_rays"] + c["reflection_rays"]
+    return {"value": round(rays / rr.seconds / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "reference",
+            "sample": f"every {stride}th internal row ({rh // stride} rows x {rw}: {c['primary_rays']} primary + "
+                      f"{c['shadow_rays']} shadow + {c['reflection_rays']} reflection rays in {rr.seconds:.2f} s), "
+                      f"reference TUs + OpenMP x{threads}"}
 
 
 if __name__ == "__main__":
