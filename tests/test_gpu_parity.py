@@ -177,12 +177,18 @@ def test_trace_rays_match_oracle(R, scene_name):
     assert np.array_equal(bits(gu), bits(ou)) and np.array_equal(bits(gv), bits(ov))
 
 
-def test_bands_reassemble_to_full_frame(R):
-    """Image strips (multi-GPU layout) rendered on one GPU and re-assembled == the full render."""
+@pytest.mark.parametrize("scene_name", ["bumpy70k", "c5_small"])
+def test_bands_reassemble_to_full_frame(R, scene_name):
+    """Image strips (multi-GPU layout) rendered on one GPU and re-assembled == the full render
+    (also through the reflection engine: pixel seeds use global rows, frames write local rows)."""
     import torch
     from raytracercpp_amd import scenes
     from raytracercpp_amd.strips import assemble
-    sc, st = scenes.bumpy70k(width=320, height=180, enable_ssaa=True, ssaa_factor=2)
+    if scene_name == "bumpy70k":
+        sc, st = scenes.bumpy70k(width=320, height=180, enable_ssaa=True, ssaa_factor=2)
+    else:
+        sc, st = scenes.sphere1m_refl(width=80, height=45, samples=4)
+        st = st.copy(max_recursion_depth=2)
     R.load_scene(sc, st)
     R.ray_trace()
     R.post_process()
