@@ -208,12 +208,10 @@ int rt_get_image(rt_renderer* r, uint32_t* argb, int32_t* w, int32_t* h)
 int rt_render(rt_renderer* r, float* ms)
 {
     return guarded(R(r), [&] {
-        auto t0 = std::chrono::steady_clock::now();
-        int rc = R(r)->ray_trace();
-        if (rc == RT_OK)
-            rc = R(r)->post_process();
+        int rc = RT_OK;
+        float t = rt::render(*R(r), &rc);
         if (ms)
-            *ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            *ms = t;
         return rc;
     });
 }

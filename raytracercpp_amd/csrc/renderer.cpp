@@ -928,4 +928,15 @@ int Renderer::band_counters(unsigned long long out[2])
     return RT_OK;
 }
 
+float render(Renderer& renderer, int* rc)
+{
+    auto t0 = std::chrono::steady_clock::now();
+    int r = renderer.ray_trace();
+    if (r == RT_OK)
+        r = renderer.post_process();
+    if (rc)
+        *rc = r;
+    return std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
 }  // namespace rt

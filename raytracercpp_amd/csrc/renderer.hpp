@@ -147,4 +147,9 @@ private:
     float kernel_ms_ = 0, post_ms_ = 0, build_ms_ = 0;
 };
 
+// render(Renderer&) (tp2/projets/utils/mainUtils.cpp:6-21): ray_trace then post_process;
+// returns the elapsed milliseconds (*rc gets the status; on an error the remaining
+// steps are skipped).  The hybrid raster branch is not provided.
+float render(Renderer& renderer, int* rc = nullptr);
+
 }  // namespace rt
