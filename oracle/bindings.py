@@ -37,6 +37,7 @@ class OrcScene(C.Structure):
         ("light", C.c_float * 3),
         ("tex_w", C.c_int32 * NTEX), ("tex_h", C.c_int32 * NTEX), ("tex", _f32p * NTEX),
         ("sky_w", C.c_int32 * 6), ("sky_h", C.c_int32 * 6), ("sky", _f32p * 6),
+        ("proj", C.c_float * 16), ("world_to_cam", C.c_float * 16),
     ]
 
 
@@ -53,7 +54,7 @@ class OrcSettings(C.Structure):
         ("enable_normal_mapping", C.c_int32), ("enable_displacement_mapping", C.c_int32),
         ("displacement_mapping_strength", C.c_float), ("parallax_mapping_steps", C.c_int32),
         ("enable_roughness_mapping", C.c_int32), ("enable_skysphere", C.c_int32),
-        ("enable_skybox", C.c_int32), ("rng_seed", C.c_uint32),
+        ("enable_skybox", C.c_int32), ("rng_seed", C.c_uint32), ("enable_clipping", C.c_int32),
     ]
 
 
@@ -109,6 +110,10 @@ def make_orc_scene(scene, pin: _Pinned) -> OrcScene:
     s.proj_inv[:] = [float(x) for x in np.asarray(scene.proj_inv, np.float32)]
     s.cam_to_world[:] = [float(x) for x in np.asarray(scene.cam_to_world, np.float32)]
     s.light[:] = [float(x) for x in np.asarray(scene.light, np.float32)]
+    if getattr(scene, "proj", None) is not None:
+        s.proj[:] = [float(x) for x in np.asarray(scene.proj, np.float32)]
+    if getattr(scene, "world_to_cam", None) is not None:
+        s.world_to_cam[:] = [float(x) for x in np.asarray(scene.world_to_cam, np.float32)]
     for slot in range(NTEX):
         img = scene.textures.get(slot) if scene.textures else None
         if img is not None:
@@ -169,6 +174,7 @@ class Oracle:
             L.orc_destroy.argtypes = [C.c_void_p]
             L.orc_render_rows.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(OrcOutputs),
                                           C.POINTER(OrcCounters), C.c_int]
+            L.orc_raster.argtypes = [C.c_void_p, C.POINTER(OrcOutputs), C.POINTER(OrcCounters), C.c_int]
             L.orc_downscale_argb.argtypes = [_u32p, C.c_int, C.c_int, C.c_int, _u32p]
             L.orc_bvh_query.argtypes = [C.c_void_p, _f32p, _f32p, C.c_int64, _i32p, _f32p, _f32p, _f32p, _u8p, _i64p]
             L.orc_bvh_stats.argtypes = [C.c_void_p, _i64p]
@@ -211,6 +217,20 @@ class Oracle:
         res.counters = cnt.as_dict()
         return res
 
+    def raster(self, nthreads=0) -> RenderResult:
+        """Renderer::raster_trace restated (sequential triangle order), the whole render."""
+        rw, rh = self.settings.render_size()
+        res = RenderResult(rw, rh)
+        cnt = OrcCounters()
+        out = res.outputs()
+        t0 = time.perf_counter()
+        rc = self.lib().orc_raster(self._h, C.byref(out), C.byref(cnt), nthreads)
+        res.seconds = time.perf_counter() - t0
+        if rc != 0:
+            raise RuntimeError("orc_raster failed")
+        res.counters = cnt.as_dict()
+        return res
+
     def bvh_query(self, orig, dirs):
         orig = np.ascontiguousarray(orig, np.float32)
         dirs = np.ascontiguousarray(dirs, np.float32)
@@ -238,24 +258,6 @@ class Oracle:
         if rc != 0:
             raise ValueError("size not divisible by factor")
         return out
-
-    @classmethod
-    def render_row_sample(cls, scene, settings, row_begin, row_count, row_stride) -> RenderResult:
-        """Internal rows row_begin + i * row_stride (i < row_count), for CPU timing samples."""
-        pin = _Pinned()
-        sc = make_orc_scene(scene, pin)
-        st = make_orc_settings(settings)
-        rw, _ = settings.render_size()
-        res = RenderResult(rw, row_count)
-        out = res.outputs()
-        cnt = OrcCounters()
-        rc = cls.lib().ref_render_row_sample(C.byref(sc), C.byref(st), row_begin, row_count, row_stride,
-                                             C.byref(out), C.byref(cnt))
-        if rc != 0:
-            raise RuntimeError("ref_render_row_sample failed")
-        res.seconds = cls.lib().ref_last_render_seconds()
-        res.counters = cnt.as_dict()
-        return res
 
     @classmethod
     def heap_order(cls, keys):
@@ -297,6 +299,8 @@ class RefHarness:
                                         _f32p, _f32p, _u8p]
             L.ref_render_rows.argtypes = [C.POINTER(OrcScene), C.POINTER(OrcSettings), C.c_int, C.c_int,
                                           C.POINTER(OrcOutputs), C.POINTER(OrcCounters)]
+            L.ref_raster.argtypes = [C.POINTER(OrcScene), C.POINTER(OrcSettings), C.POINTER(OrcOutputs),
+                                     C.POINTER(OrcCounters)]
             L.ref_downscale_argb.argtypes = [_u32p, C.c_int, C.c_int, C.c_int, _u32p]
             L.ref_heap_order.argtypes = [_f32p, C.c_int, _i32p]
             cls._lib = L
@@ -391,6 +395,21 @@ class RefHarness:
         res.seconds = cls.lib().ref_last_render_seconds()   # the pixel loop only
         if rc != 0:
             raise RuntimeError("ref_render_rows failed")
+        res.counters = cnt.as_dict()
+        return res
+
+    @classmethod
+    def raster(cls, scene, settings) -> RenderResult:
+        """raster_trace on the reference's vec4 / Triangle4 / Transform / Triangle code."""
+        pin = _Pinned()
+        sc = make_orc_scene(scene, pin)
+        st = make_orc_settings(settings)
+        rw, rh = settings.render_size()
+        res = RenderResult(rw, rh)
+        out = res.outputs()
+        cnt = OrcCounters()
+        if cls.lib().ref_raster(C.byref(sc), C.byref(st), C.byref(out), C.byref(cnt)) != 0:
+            raise RuntimeError("ref_raster failed")
         res.counters = cnt.as_dict()
         return res
 

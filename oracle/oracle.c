@@ -671,6 +671,7 @@ static c3 skybox_sample(const oimg *faces, v3 dir, float *alpha)
 /* ------------------------------------------------------------------------- */
 /* Renderer (tp2/projets/renderer/renderer.cpp)                                */
 /* ------------------------------------------------------------------------- */
+#define ORC_RASTER_SLOTS 256
 struct orc_ctx {
     orc_scene sc;
     orc_settings s;
@@ -1057,7 +1058,8 @@ ORC_API struct orc_ctx *orc_create(const orc_scene *sc, const orc_settings *s)
     X->sc = *sc;
     X->s = *s;
     X->ntri = sc->ntri;
-    X->tris = (otri *)calloc(sc->ntri > 0 ? (size_t)sc->ntri : 1, sizeof(otri));
+    /* + ORC_RASTER_SLOTS: per-thread temporary triangles of raster_trace's shading */
+    X->tris = (otri *)calloc((size_t)sc->ntri + ORC_RASTER_SLOTS, sizeof(otri));
     for (int64_t i = 0; i < sc->ntri; i++) {
         const float *t = sc->tri + 9 * i;
         otri *T = &X->tris[i];
@@ -1114,6 +1116,367 @@ static void add_counters(orc_counters *a, const orc_counters *b)
     a->tri_tests_refl += b->tri_tests_refl;
     a->child_tests_primary += b->child_tests_primary;
     a->child_tests_shadow += b->child_tests_shadow;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Renderer::raster_trace (renderer.cpp:869-1006): hybrid rasterisation.       */
+/* The reference runs the triangle loop under OpenMP with an unsynchronised    */
+/* z-test-and-write, so overlapping triangles race; the oracle (like the GPU)  */
+/* defines the sequential result: triangles (and their clipped pieces) in      */
+/* order, a pixel keeps the first candidate with the smallest z (strict <).    */
+/* Every z-test pass shades the pixel in the reference; only the last one      */
+/* survives, so only the winner is shaded here (its shading is per-pixel       */
+/* deterministic, rough reflections included).                                 */
+/* ------------------------------------------------------------------------- */
+typedef struct { float x, y, z, w; } v4;
+static inline v4 V4(float x, float y, float z, float w) { v4 r = {x, y, z, w}; return r; }
+static inline v4 v4add(v4 a, v4 b) { return V4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }  /* vec.cpp:123-126 */
+static inline v4 v4sub(v4 a, v4 b) { return V4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w); }  /* vec.cpp:128-131 */
+static inline v4 v4mul(float t, v4 u) { return V4(u.x * t, u.y * t, u.z * t, u.w * t); }      /* vec.cpp:133-141 */
+static inline float v4c(v4 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
+
+/* Transform::operator()(vec4), mat.cpp:118-131 */
+static inline v4 xform4(const float *m, v4 v)
+{
+    return V4(m[0] * v.x + m[1] * v.y + m[2] * v.z + m[3] * v.w, m[4] * v.x + m[5] * v.y + m[6] * v.z + m[7] * v.w,
+              m[8] * v.x + m[9] * v.y + m[10] * v.z + m[11] * v.w,
+              m[12] * v.x + m[13] * v.y + m[14] * v.z + m[15] * v.w);
+}
+
+typedef struct { v4 a, b, c; v3 tu, tv; } otri4;   /* Triangle4, triangle.h:24-40 */
+
+#define ORC_CLIP_MAX 64
+
+static inline int in_half(v4 p, int i, int sgn) { return sgn > 0 ? v4c(p, i) < p.w : v4c(p, i) > -p.w; }
+
+/* clip_triangles_to_plane<i, sgn> (renderer.cpp:669-850); in may alias out when n == 1 */
+static int clip_plane(const otri4 *in, int n, otri4 *out, int i, int sgn)
+{
+    int k = 0;
+    const float fs = (float)sgn;
+    for (int t = 0; t < n; t++) {
+        const otri4 T = in[t];
+        int ia = in_half(T.a, i, sgn), ib = in_half(T.b, i, sgn), ic = in_half(T.c, i, sgn);
+        int cnt = ia + ib + ic;
+        if (cnt == 3) {
+            if (k < ORC_CLIP_MAX) out[k] = T;
+            k++;
+        } else if (cnt == 1) {
+            /* (kept, lost1, lost2) rotated so the kept vertex leads, texcoords alike */
+            v4 p0, p1, p2;
+            float u0, u1, u2, w0, w1, w2;
+            if (ia) { p0 = T.a; p1 = T.b; p2 = T.c; u0 = T.tu.x; u1 = T.tu.y; u2 = T.tu.z; w0 = T.tv.x; w1 = T.tv.y; w2 = T.tv.z; }
+            else if (ib) { p0 = T.b; p1 = T.c; p2 = T.a; u0 = T.tu.y; u1 = T.tu.z; u2 = T.tu.x; w0 = T.tv.y; w1 = T.tv.z; w2 = T.tv.x; }
+            else { p0 = T.c; p1 = T.a; p2 = T.b; u0 = T.tu.z; u1 = T.tu.x; u2 = T.tu.y; w0 = T.tv.z; w1 = T.tv.x; w2 = T.tv.y; }
+            float d0 = v4c(p0, i) - p0.w * fs, d1 = v4c(p1, i) - p1.w * fs, d2 = v4c(p2, i) - p2.w * fs;
+            float t1 = d1 / (d1 - d0), t2 = d2 / (d2 - d0);
+            otri4 R;
+            R.a = p0;
+            R.b = v4add(p1, v4mul(t1 - 0.0f, v4sub(p0, p1)));
+            R.c = v4add(p2, v4mul(t2 - 0.0f, v4sub(p0, p2)));
+            R.tu = V(u0, u1 + (t1 - 0.0f) * (u0 - u1), u2 + (t2 - 0.0f) * (u0 - u2));
+            R.tv = V(w0, w1 + (t1 - 0.0f) * (w0 - w1), w2 + (t2 - 0.0f) * (w0 - w2));
+            if (k < ORC_CLIP_MAX) out[k] = R;
+            k++;
+        } else if (cnt == 2) {
+            /* (kept1, kept2, lost): the lost vertex's successors lead */
+            v4 q1, q2, q0;
+            float u0, u1, u2, w0, w1, w2;
+            if (!ia) { q0 = T.a; q1 = T.b; q2 = T.c; u0 = T.tu.y; u1 = T.tu.z; u2 = T.tu.x; w0 = T.tv.y; w1 = T.tv.z; w2 = T.tv.x; }
+            else if (!ib) { q0 = T.b; q1 = T.c; q2 = T.a; u0 = T.tu.z; u1 = T.tu.x; u2 = T.tu.y; w0 = T.tv.z; w1 = T.tv.x; w2 = T.tv.y; }
+            else { q0 = T.c; q1 = T.a; q2 = T.b; u0 = T.tu.x; u1 = T.tu.y; u2 = T.tu.z; w0 = T.tv.x; w1 = T.tv.y; w2 = T.tv.z; }
+            float e1 = v4c(q1, i) - q1.w * fs, e2 = v4c(q2, i) - q2.w * fs, e0 = v4c(q0, i) - q0.w * fs;
+            float t1 = e0 / (e0 - e1), t2 = e0 / (e0 - e2);
+            v4 P1 = v4add(q0, v4mul(t1 - 0.0f, v4sub(q1, q0)));
+            v4 P2 = v4add(q0, v4mul(t2 - 0.0f, v4sub(q2, q0)));
+            otri4 R1, R2;
+            R1.a = q1; R1.b = q2; R1.c = P2;
+            R1.tu = V(u0, u1, u2 + (t2 - 0.0f) * (u1 - u2));
+            R1.tv = V(w0, w1, w2 + (t2 - 0.0f) * (w1 - w2));
+            R2.a = q1; R2.b = P2; R2.c = P1;
+            R2.tu = V(u0, u2 + (t2 - 0.0f) * (u1 - u2), u2 + (t1 - 0.0f) * (u0 - u2));
+            R2.tv = V(w0, w2 + (t2 - 0.0f) * (w1 - w2), w2 + (t1 - 0.0f) * (w0 - w2));
+            if (k < ORC_CLIP_MAX) out[k] = R1;
+            k++;
+            if (k < ORC_CLIP_MAX) out[k] = R2;
+            k++;
+        }
+    }
+    return k < ORC_CLIP_MAX ? k : ORC_CLIP_MAX;
+}
+
+/* one clipped piece, everything raster_trace derives from it */
+typedef struct {
+    int tri, piece;
+    v3 na, nb, nc;           /* Triangle(Triangle4) in NDC (triangle.cpp:12-23) */
+    v3 tu, tv;
+    float inv_area;
+    int x0, y0, x1, y1;      /* pixel bounding box */
+    float za, zb, zc;        /* matrix_transform_z(cam_to_world, proj_inv(vertex)) */
+    otri world;              /* _camera_to_world_mat(proj_inv(NDC triangle)) */
+    otri cam;                /* proj_inv(NDC triangle) */
+} opiece;
+
+/* (int)(double): cvttsd2si, INT_MIN out of range / NaN */
+static inline int d2i(double d)
+{
+    if (!(d > -2147483649.0 && d < 2147483648.0))
+        return INT32_MIN;
+    return (int)d;
+}
+
+/* Renderer::matrix_transform_z, renderer.cpp:856-867 (a division, not a reciprocal) */
+static inline float xform_z(const float *m, v3 p)
+{
+    float zt = m[8] * p.x + m[9] * p.y + m[10] * p.z + m[11];
+    float wt = m[12] * p.x + m[13] * p.y + m[14] * p.z + m[15];
+    if (wt == 1.0f)
+        return zt;
+    return zt / wt;
+}
+
+static otri tri_from(v3 a, v3 b, v3 c, int mat, v3 tu, v3 tv)   /* Triangle(Point...) ctor */
+{
+    otri t;
+    t.a = a; t.b = b; t.c = c;
+    t.n = vcross(vsub(b, a), vsub(c, a));
+    t.mat = mat;
+    t.tu = tu; t.tv = tv;
+    return t;
+}
+
+static int make_pieces(const struct orc_ctx *X, int64_t ti, opiece *out)
+{
+    const otri *O = &X->tris[ti];
+    const float *W2C = X->sc.world_to_cam, *PR = X->sc.proj, *PI = X->sc.proj_inv, *C2W = X->sc.cam_to_world;
+    /* _world_to_camera_mat(original_triangle), then perspective_projection(vec4(point)) */
+    v3 ca = xform_point(W2C, O->a), cb = xform_point(W2C, O->b), cc = xform_point(W2C, O->c);
+    otri4 A[ORC_CLIP_MAX], B[ORC_CLIP_MAX];
+    A[0].a = xform4(PR, V4(ca.x, ca.y, ca.z, 1.0f));
+    A[0].b = xform4(PR, V4(cb.x, cb.y, cb.z, 1.0f));
+    A[0].c = xform4(PR, V4(cc.x, cc.y, cc.z, 1.0f));
+    A[0].tu = O->tu;
+    A[0].tv = O->tv;
+    int n = 1;
+    const otri4 *res = A;
+    if (X->s.enable_clipping) {   /* clip_triangle, renderer.cpp:833-854 */
+        n = clip_plane(A, n, A, 0, 1);
+        n = clip_plane(A, n, B, 0, -1);
+        n = clip_plane(B, n, A, 1, 1);
+        n = clip_plane(A, n, B, 1, -1);
+        n = clip_plane(B, n, A, 2, 1);
+        n = clip_plane(A, n, B, 2, -1);
+        res = B;
+    }
+    const int rw = X->rw, rh = X->rh;
+    for (int k = 0; k < n; k++) {
+        const otri4 *Q = &res[k];
+        opiece *P = &out[k];
+        P->tri = (int)ti;
+        P->piece = k;
+        float iaw = 1.0f / Q->a.w, ibw = 1.0f / Q->b.w, icw = 1.0f / Q->c.w;
+        P->na = V(Q->a.x * iaw, Q->a.y * iaw, Q->a.z * iaw);
+        P->nb = V(Q->b.x * ibw, Q->b.y * ibw, Q->b.z * ibw);
+        P->nc = V(Q->c.x * icw, Q->c.y * icw, Q->c.z * icw);
+        P->tu = Q->tu;
+        P->tv = Q->tv;
+        P->cam = tri_from(xform_point(PI, P->na), xform_point(PI, P->nb), xform_point(PI, P->nc), O->mat, Q->tu, Q->tv);
+        P->world = tri_from(xform_point(C2W, P->cam.a), xform_point(C2W, P->cam.b), xform_point(C2W, P->cam.c), O->mat,
+                            Q->tu, Q->tv);
+        v3 a = P->na, b = P->nb, c = P->nc;
+        P->inv_area = 1 / ((b.x - a.x) * (c.y - a.y) - (b.y - a.y) * (c.x - a.x));
+        float mnx = smin(a.x, smin(b.x, c.x)), mny = smin(a.y, smin(b.y, c.y));
+        float mxx = smax(a.x, smax(b.x, c.x)), mxy = smax(a.y, smax(b.y, c.y));
+        int x0 = d2i((double)(mnx + 1) * 0.5 * rw), y0 = d2i((double)(mny + 1) * 0.5 * rh);
+        int x1 = d2i((double)(mxx + 1) * 0.5 * rw), y1 = d2i((double)(mxy + 1) * 0.5 * rh);
+        P->x0 = x0 > 0 ? x0 : 0;
+        P->y0 = y0 > 0 ? y0 : 0;
+        P->x1 = rw - 1 < x1 ? rw - 1 : x1;
+        P->y1 = rh - 1 < y1 ? rh - 1 : y1;
+        P->za = xform_z(C2W, xform_point(PI, P->na));
+        P->zb = xform_z(C2W, xform_point(PI, P->nb));
+        P->zc = xform_z(C2W, xform_point(PI, P->nc));
+    }
+    return n;
+}
+
+/* Triangle::edge_function, triangle.h:65-68 */
+static inline float edge_fn(float px, float py, v3 a, v3 b) { return (b.x - a.x) * (py - a.y) - (b.y - a.y) * (px - a.x); }
+
+/* the sample point of pixel (px, py) as raster_trace's incremental loops reach it for piece P */
+static void piece_sample(const opiece *P, int rw, int rh, int px, int py, float *sx, float *sy)
+{
+    const float hs = 1.0f / rh * 2, ws = 1.0f / rw * 2;
+    float iy = P->y0 * hs - 1;
+    for (int y = P->y0; y < py; y++)
+        iy += hs;
+    float ix = P->x0 * ws - 1;
+    for (int x = P->x0; x < px; x++)
+        ix += ws;
+    *sx = ix + ws * 0.5f;
+    *sy = iy + hs * 0.5f;
+}
+
+static int piece_bary(const opiece *P, float sx, float sy, float *u, float *v, float *w)
+{
+    float U = edge_fn(sx, sy, P->nc, P->na);
+    if (U < 0) return 0;
+    float Vv = edge_fn(sx, sy, P->na, P->nb);
+    if (Vv < 0) return 0;
+    float Ww = edge_fn(sx, sy, P->nb, P->nc);
+    if (Ww < 0) return 0;
+    *u = U * P->inv_area;
+    *v = Vv * P->inv_area;
+    *w = Ww * P->inv_area;
+    return 1;
+}
+
+static inline float piece_z(const opiece *P, float u, float v, float w)
+{
+    return -1 / (1 / P->za * w + 1 / P->zb * u + 1 / P->zc * v);
+}
+
+/* raster_trace over the whole render: outputs are internal rows 0..rh-1.  hit_id =
+ * winning triangle (-1: background), hit_t = its z, shadow = the shaded hit's flag. */
+ORC_API int orc_raster(const struct orc_ctx *X, orc_outputs *out, orc_counters *counters, int nthreads)
+{
+    const int rw = X->rw, rh = X->rh;
+    const size_t npx = (size_t)rw * rh;
+    float *zb = (float *)malloc(npx * sizeof(float));
+    int64_t *win = (int64_t *)malloc(npx * sizeof(int64_t));
+    size_t cap = (size_t)(X->ntri > 0 ? X->ntri : 1) + 16, np = 0;
+    opiece *pieces = (opiece *)malloc(cap * sizeof(opiece));
+    if (!zb || !win || !pieces) {
+        free(zb); free(win); free(pieces);
+        return -1;
+    }
+    for (size_t i = 0; i < npx; i++) {
+        zb[i] = INFINITY;
+        win[i] = -1;
+    }
+    opiece tmp[ORC_CLIP_MAX];
+    const float hs = 1.0f / rh * 2, ws = 1.0f / rw * 2;
+    for (int64_t ti = 0; ti < X->ntri; ti++) {
+        int n = make_pieces(X, ti, tmp);
+        for (int k = 0; k < n; k++) {
+            if (np == cap) {
+                cap *= 2;
+                opiece *np2 = (opiece *)realloc(pieces, cap * sizeof(opiece));
+                if (!np2) { free(zb); free(win); free(pieces); return -1; }
+                pieces = np2;
+            }
+            const opiece *P = &tmp[k];
+            pieces[np] = *P;
+            float iy = P->y0 * hs - 1;
+            for (int py = P->y0; py <= P->y1; py++, iy += hs) {
+                float ix = P->x0 * ws - 1;
+                for (int px = P->x0; px <= P->x1; px++, ix += ws) {
+                    float u, v, w;
+                    if (!piece_bary(P, ix + ws * 0.5f, iy + hs * 0.5f, &u, &v, &w))
+                        continue;
+                    float z = piece_z(P, u, v, w);
+                    size_t o = (size_t)py * rw + px;
+                    if (z < zb[o]) {
+                        zb[o] = z;
+                        win[o] = (int64_t)np;
+                    }
+                }
+            }
+            np++;
+        }
+    }
+    orc_counters total;
+    memset(&total, 0, sizeof(total));
+    v3 cam = V(X->sc.cam_pos[0], X->sc.cam_pos[1], X->sc.cam_pos[2]);
+#ifdef _OPENMP
+    if (nthreads <= 0)
+        nthreads = omp_get_max_threads();
+    if (nthreads > ORC_RASTER_SLOTS)
+        nthreads = ORC_RASTER_SLOTS;
+#pragma omp parallel num_threads(nthreads)
+#endif
+    {
+        orc_counters local;
+        memset(&local, 0, sizeof(local));
+        int slot = 0;
+#ifdef _OPENMP
+        slot = omp_get_thread_num();
+#endif
+        otri *temp = (otri *)&X->tris[X->ntri + slot];
+        otracer T;
+        T.X = X;
+        T.cnt = &local;
+        T.ray_kind = 0;
+        T.rng = 1;
+        T.frame_key = 0;
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic)
+#endif
+        for (int py = 0; py < rh; py++) {
+            for (int px = 0; px < rw; px++) {
+                size_t o = (size_t)py * rw + px;
+                c3 c = background_color();
+                int sh = 0;
+                int64_t wi = win[o];
+                if (wi >= 0) {
+                    const opiece *P = &pieces[wi];
+                    float sx, sy, u = 0, v = 0, w = 0;
+                    piece_sample(P, rw, rh, px, py, &sx, &sy);
+                    piece_bary(P, sx, sy, &u, &v, &w);
+                    const otri *O = &X->tris[P->tri];
+                    const orc_settings *S = &X->s;
+                    if (S->shading_method == ORC_RT_SHADING) {
+                        /* trace_triangle(Ray(cam, normalize(c2w(proj_inv(p)) - cam)), world piece, 0) */
+                        v3 pw = xform_point(X->sc.cam_to_world, xform_point(X->sc.proj_inv, V(sx, sy, -1)));
+                        v3 rd = vnormalize(vsub(pw, cam));
+                        *temp = P->world;
+                        ohit h = hit_fresh();
+                        c = C(0, 0, 0);
+                        if (tri_intersect(temp, (int)(X->ntri + slot), cam, rd, &h)) {
+                            T.frame_key = pixel_seed((uint32_t)(py * rw + px), S->rng_seed);
+                            local.primary_rays++;
+                            c = shade(&T, cam, rd, &h, 0, &sh);
+                        }
+                    } else if (S->shading_method == ORC_ABS_NORMALS_SHADING) {
+                        v3 nn = vnormalize(O->n);
+                        c = C(fabsf(nn.x), fabsf(nn.y), fabsf(nn.z));
+                    } else if (S->shading_method == ORC_PASTEL_NORMALS_SHADING) {
+                        v3 nn = vnormalize(O->n);
+                        c = cmulf(cadd(C(nn.x, nn.y, nn.z), C(1.0f, 1.0f, 1.0f)), 0.5f);
+                    } else if (S->shading_method == ORC_BARYCENTRIC_COORDINATES_SHADING) {
+                        c = cadd(cadd(cmulf(C(1, 0, 0), u), cmulf(C(0, 1.0f, 0), v)), cmulf(C(0, 0, 1), 1 - u - v));
+                    } else if (S->shading_method == ORC_VISUALIZE_AO) {
+                        c = C(0.9f, 0.9f, 0.9f);
+                        if (S->enable_ao_mapping) {
+                            float tu, tv;
+                            tri_interp(&P->cam, u, v, &tu, &tv);
+                            float a = tex_floor(&X->tex[ORC_TEX_AO], tu, tv).r;
+                            c = cmul(c, C(a, a, a));
+                        }
+                    }
+                }
+                if (out->argb) out->argb[o] = qrgb(f2i(c.r * 255), f2i(c.g * 255), f2i(c.b * 255));
+                if (out->rgba) {
+                    out->rgba[4 * o] = c.r;
+                    out->rgba[4 * o + 1] = c.g;
+                    out->rgba[4 * o + 2] = c.b;
+                    out->rgba[4 * o + 3] = 1.0f;
+                }
+                if (out->hit_id) out->hit_id[o] = wi >= 0 ? pieces[wi].tri : -1;
+                if (out->hit_t) out->hit_t[o] = zb[o];
+                if (out->shadow) out->shadow[o] = (uint8_t)sh;
+            }
+        }
+#ifdef _OPENMP
+#pragma omp critical
+#endif
+        add_counters(&total, &local);
+    }
+    if (counters) *counters = total;
+    free(zb);
+    free(win);
+    free(pieces);
+    return 0;
 }
 
 /* Renderer::ray_trace, renderer.cpp:1068-1116, rows [row_begin, row_begin+row_count) */

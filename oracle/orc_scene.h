@@ -84,6 +84,10 @@ typedef struct orc_scene {
     /* skybox faces: right, left, top, bottom, back, front (skybox.h:12-16) */
     int32_t sky_w[6], sky_h[6];
     const float *sky[6];
+
+    /* hybrid rasterisation (Renderer::raster_trace, renderer.cpp:869-1006) */
+    float proj[16];         /* Camera::_perspective_proj_mat, row-major */
+    float world_to_cam[16]; /* Camera::_world_to_camera_mat, row-major */
 } orc_scene;
 
 typedef struct orc_settings {
@@ -102,6 +106,7 @@ typedef struct orc_settings {
     int32_t enable_roughness_mapping;
     int32_t enable_skysphere, enable_skybox;
     uint32_t rng_seed; /* counter-based RNG seed for rough reflections */
+    int32_t enable_clipping; /* raster_trace: clip against the 6 frustum planes */
 } orc_settings;
 
 /* per-internal-pixel outputs; any pointer may be NULL.  Arrays cover the

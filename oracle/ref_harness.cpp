@@ -153,6 +153,7 @@ struct HScene {
     Materials materials;
     Point cam_pos;
     Transform proj_inv, cam_to_world;
+    Transform proj, world_to_cam;   // raster_trace
     Point light;
     Image tex[ORC_TEX_COUNT];
     Skybox skybox;
@@ -210,6 +211,8 @@ void build_scene(HScene& H, const orc_scene* sc, const orc_settings* st)
     H.cam_pos = Point(sc->cam_pos[0], sc->cam_pos[1], sc->cam_pos[2]);
     to_transform(sc->proj_inv, H.proj_inv);
     to_transform(sc->cam_to_world, H.cam_to_world);
+    to_transform(sc->proj, H.proj);
+    to_transform(sc->world_to_cam, H.world_to_cam);
     H.light = Point(sc->light[0], sc->light[1], sc->light[2]);
     for (int i = 0; i < ORC_TEX_COUNT; i++)
         H.tex[i] = make_image(sc->tex_w[i], sc->tex_h[i], sc->tex[i]);
@@ -740,6 +743,247 @@ static int render_rows_strided(const orc_scene* sc, const orc_settings* st, int 
         }
     }
     g_last_render_seconds = omp_get_wtime() - t_start;
+    if (counters) *counters = total;
+    return 0;
+}
+
+/* Renderer::raster_trace (renderer.cpp:869-1006) on the reference's own vec4 /
+ * Triangle4 / Transform / Triangle code.  The reference's OpenMP triangle loop
+ * races on the z-buffer; the sequential result is defined here: triangles and
+ * their clipped pieces in order, strict z-test, only the winner shaded (see
+ * oracle.c).  hit_id = winning triangle (-1 background), hit_t = its z. */
+namespace {
+
+bool h_in_half(const vec4& p, int i, int sgn) { return sgn > 0 ? p(i) < p.w : p(i) > -p.w; }
+
+// clip_triangles_to_plane<i, sgn> (renderer.cpp:669-850); in may alias out when n == 1
+int h_clip_plane(const Triangle4* in, int n, Triangle4* out, int i, int sgn)
+{
+    const int CAP = 64;
+    int k = 0;
+    for (int t = 0; t < n; t++) {
+        const Triangle4 T = in[t];
+        bool ia = h_in_half(T._a, i, sgn), ib = h_in_half(T._b, i, sgn), ic = h_in_half(T._c, i, sgn);
+        int cnt = (int)ia + (int)ib + (int)ic;
+        if (cnt == 3) {
+            if (k < CAP) out[k] = T;
+            k++;
+        } else if (cnt == 1) {
+            const vec4& p0 = ia ? T._a : (ib ? T._b : T._c);
+            const vec4& p1 = ia ? T._b : (ib ? T._c : T._a);
+            const vec4& p2 = ia ? T._c : (ib ? T._a : T._b);
+            float u[3] = {ia ? T._tex_coords_u.x : (ib ? T._tex_coords_u.y : T._tex_coords_u.z),
+                          ia ? T._tex_coords_u.y : (ib ? T._tex_coords_u.z : T._tex_coords_u.x),
+                          ia ? T._tex_coords_u.z : (ib ? T._tex_coords_u.x : T._tex_coords_u.y)};
+            float v[3] = {ia ? T._tex_coords_v.x : (ib ? T._tex_coords_v.y : T._tex_coords_v.z),
+                          ia ? T._tex_coords_v.y : (ib ? T._tex_coords_v.z : T._tex_coords_v.x),
+                          ia ? T._tex_coords_v.z : (ib ? T._tex_coords_v.x : T._tex_coords_v.y)};
+            float d0 = p0(i) - p0.w * sgn, d1 = p1(i) - p1.w * sgn, d2 = p2(i) - p2.w * sgn;
+            float t1 = d1 / (d1 - d0), t2 = d2 / (d2 - d0);
+            const float eps = 0;
+            vec4 q1 = p1 + (t1 - eps) * (p0 - p1);
+            vec4 q2 = p2 + (t2 - eps) * (p0 - p2);
+            Point nu(u[0], u[1] + (t1 - eps) * (u[0] - u[1]), u[2] + (t2 - eps) * (u[0] - u[2]));
+            Point nv(v[0], v[1] + (t1 - eps) * (v[0] - v[1]), v[2] + (t2 - eps) * (v[0] - v[2]));
+            if (k < CAP) out[k] = Triangle4(p0, q1, q2, nu, nv);
+            k++;
+        } else if (cnt == 2) {
+            const vec4& lost = !ia ? T._a : (!ib ? T._b : T._c);
+            const vec4& k1 = !ia ? T._b : (!ib ? T._c : T._a);
+            const vec4& k2 = !ia ? T._c : (!ib ? T._a : T._b);
+            float u[3] = {!ia ? T._tex_coords_u.y : (!ib ? T._tex_coords_u.z : T._tex_coords_u.x),
+                          !ia ? T._tex_coords_u.z : (!ib ? T._tex_coords_u.x : T._tex_coords_u.y),
+                          !ia ? T._tex_coords_u.x : (!ib ? T._tex_coords_u.y : T._tex_coords_u.z)};
+            float v[3] = {!ia ? T._tex_coords_v.y : (!ib ? T._tex_coords_v.z : T._tex_coords_v.x),
+                          !ia ? T._tex_coords_v.z : (!ib ? T._tex_coords_v.x : T._tex_coords_v.y),
+                          !ia ? T._tex_coords_v.x : (!ib ? T._tex_coords_v.y : T._tex_coords_v.z)};
+            float e1 = k1(i) - k1.w * sgn, e2 = k2(i) - k2.w * sgn, e0 = lost(i) - lost.w * sgn;
+            float t1 = e0 / (e0 - e1), t2 = e0 / (e0 - e2);
+            const float eps = 0;
+            vec4 P1 = lost + (t1 - eps) * (k1 - lost);
+            vec4 P2 = lost + (t2 - eps) * (k2 - lost);
+            Point u1(u[0], u[1], u[2] + (t2 - eps) * (u[1] - u[2]));
+            Point v1(v[0], v[1], v[2] + (t2 - eps) * (v[1] - v[2]));
+            Point u2(u[0], u[2] + (t2 - eps) * (u[1] - u[2]), u[2] + (t1 - eps) * (u[0] - u[2]));
+            Point v2(v[0], v[2] + (t2 - eps) * (v[1] - v[2]), v[2] + (t1 - eps) * (v[0] - v[2]));
+            Triangle4 A(k1, k2, P2, u1, v1), B(k1, P2, P1, u2, v2);
+            if (k < CAP) out[k] = A;
+            k++;
+            if (k < CAP) out[k] = B;
+            k++;
+        }
+    }
+    return k < CAP ? k : CAP;
+}
+
+int h_d2i(double d)
+{
+    if (!(d > -2147483649.0 && d < 2147483648.0))
+        return INT32_MIN;
+    return (int)d;
+}
+
+// Renderer::matrix_transform_z, renderer.cpp:856-867
+float h_matrix_z(const Transform& m, const Point& p)
+{
+    const float* d = m.data();
+    float zt = d[8] * p.x + d[9] * p.y + d[10] * p.z + d[11];
+    float wt = d[12] * p.x + d[13] * p.y + d[14] * p.z + d[15];
+    if (wt == 1.0f)
+        return zt;
+    return zt / wt;
+}
+
+struct HPiece {
+    int tri;
+    Triangle ndc, cam, world;
+    float inv_area;
+    int x0, y0, x1, y1;
+    float za, zb, zc;
+};
+
+}  // namespace
+
+int ref_raster(const orc_scene* sc, const orc_settings* st, orc_outputs* out, orc_counters* counters)
+{
+    HScene H;
+    build_scene(H, sc, st);
+    int rw, rh;
+    render_w_h(st, rw, rh);
+    const size_t npx = (size_t)rw * rh;
+    std::vector<float> zb(npx, INFINITY);
+    std::vector<int64_t> win(npx, -1);
+    std::vector<HPiece> pieces;
+    const float hs = 1.0f / rh * 2, ws = 1.0f / rw * 2;
+    for (size_t ti = 0; ti < H.tris.size(); ti++) {
+        const Triangle& O = H.tris[ti];
+        Triangle tc = H.world_to_cam(O);
+        Triangle4 A[64], B[64];
+        A[0] = Triangle4(H.proj(vec4(tc._a)), H.proj(vec4(tc._b)), H.proj(vec4(tc._c)), tc._tex_coords_u,
+                         tc._tex_coords_v);
+        int n = 1;
+        const Triangle4* res = A;
+        if (st->enable_clipping) {
+            n = h_clip_plane(A, n, A, 0, 1);
+            n = h_clip_plane(A, n, B, 0, -1);
+            n = h_clip_plane(B, n, A, 1, 1);
+            n = h_clip_plane(A, n, B, 1, -1);
+            n = h_clip_plane(B, n, A, 2, 1);
+            n = h_clip_plane(A, n, B, 2, -1);
+            res = B;
+        }
+        for (int k = 0; k < n; k++) {
+            HPiece P;
+            P.tri = (int)ti;
+            P.ndc = Triangle(res[k], O._materialIndex, res[k]._tex_coords_u, res[k]._tex_coords_v);
+            P.cam = H.proj_inv(P.ndc);
+            P.world = H.cam_to_world(P.cam);
+            const Point &a = P.ndc._a, &b = P.ndc._b, &c = P.ndc._c;
+            P.inv_area = 1 / ((b.x - a.x) * (c.y - a.y) - (b.y - a.y) * (c.x - a.x));
+            float mnx = std::min(a.x, std::min(b.x, c.x)), mny = std::min(a.y, std::min(b.y, c.y));
+            float mxx = std::max(a.x, std::max(b.x, c.x)), mxy = std::max(a.y, std::max(b.y, c.y));
+            P.x0 = std::max(h_d2i((mnx + 1) * 0.5 * rw), 0);
+            P.y0 = std::max(h_d2i((mny + 1) * 0.5 * rh), 0);
+            P.x1 = std::min(rw - 1, h_d2i((mxx + 1) * 0.5 * rw));
+            P.y1 = std::min(rh - 1, h_d2i((mxy + 1) * 0.5 * rh));
+            P.za = h_matrix_z(H.cam_to_world, H.proj_inv(a));
+            P.zb = h_matrix_z(H.cam_to_world, H.proj_inv(b));
+            P.zc = h_matrix_z(H.cam_to_world, H.proj_inv(c));
+            float iy = P.y0 * hs - 1;
+            for (int py = P.y0; py <= P.y1; py++, iy += hs) {
+                float ix = P.x0 * ws - 1;
+                for (int px = P.x0; px <= P.x1; px++, ix += ws) {
+                    Point s(ix + ws * 0.5f, iy + hs * 0.5f, -1);
+                    float u = Triangle::edge_function(s, c, a);
+                    if (u < 0) continue;
+                    float v = Triangle::edge_function(s, a, b);
+                    if (v < 0) continue;
+                    float w = Triangle::edge_function(s, b, c);
+                    if (w < 0) continue;
+                    u *= P.inv_area;
+                    v *= P.inv_area;
+                    w *= P.inv_area;
+                    float z = -1 / (1 / P.za * w + 1 / P.zb * u + 1 / P.zc * v);
+                    size_t o = (size_t)py * rw + px;
+                    if (z < zb[o]) {
+                        zb[o] = z;
+                        win[o] = (int64_t)pieces.size();
+                    }
+                }
+            }
+            pieces.push_back(P);
+        }
+    }
+    orc_counters total = {};
+#pragma omp parallel
+    {
+        orc_counters local = {};
+        Tracer tr(H);
+#pragma omp for schedule(dynamic)
+        for (int py = 0; py < rh; py++) {
+            for (int px = 0; px < rw; px++) {
+                size_t o = (size_t)py * rw + px;
+                Color c = H_BACKGROUND_COLOR;
+                bool sh = false;
+                int64_t wi = win[o];
+                if (wi >= 0) {
+                    const HPiece& P = pieces[(size_t)wi];
+                    float iy = P.y0 * hs - 1;
+                    for (int y = P.y0; y < py; y++) iy += hs;
+                    float ix = P.x0 * ws - 1;
+                    for (int x = P.x0; x < px; x++) ix += ws;
+                    Point s(ix + ws * 0.5f, iy + hs * 0.5f, -1);
+                    const Point &a = P.ndc._a, &b = P.ndc._b, &cc = P.ndc._c;
+                    float u = Triangle::edge_function(s, cc, a) * P.inv_area;
+                    float v = Triangle::edge_function(s, a, b) * P.inv_area;
+                    const Triangle& O = H.tris[(size_t)P.tri];
+                    int sm = st->shading_method;
+                    if (sm == ORC_RT_SHADING) {
+                        // trace_triangle (renderer.cpp:619-628)
+                        Ray ray(H.cam_pos, normalize(H.cam_to_world(H.proj_inv(s)) - H.cam_pos));
+                        HitInfo hi;
+                        c = Color(0, 0, 0);
+                        if (P.world.intersect(ray, hi)) {
+                            tr.frame_key = h_pixel_seed((uint32_t)(py * rw + px), st->rng_seed);
+                            local.primary_rays++;
+                            c = tr.shade(ray, hi, 0, &sh, &local);
+                        }
+                    } else if (sm == ORC_ABS_NORMALS_SHADING) {
+                        Vector n = normalize(O._normal);
+                        c = Color(std::abs(n.x), std::abs(n.y), std::abs(n.z));
+                    } else if (sm == ORC_PASTEL_NORMALS_SHADING) {
+                        Vector n = normalize(O._normal);
+                        c = (Color(n.x, n.y, n.z) + Color(1.0f, 1.0f, 1.0f)) * 0.5;
+                    } else if (sm == ORC_BARYCENTRIC_COORDINATES_SHADING) {
+                        c = Color(1, 0, 0) * u + Color(0, 1.0, 0) * v + Color(0, 0, 1) * (1 - u - v);
+                    } else if (sm == ORC_VISUALIZE_AO) {
+                        c = Color(0.9f, 0.9f, 0.9f);
+                        if (st->enable_ao_mapping) {
+                            float tu, tv;
+                            P.cam.interpolate_texcoords(u, v, tu, tv);
+                            c = c * Color(tr.sample_texture(H.tex[ORC_TEX_AO], tu, tv).r);
+                        }
+                    }
+                }
+                if (out->argb) out->argb[o] = h_color_to_argb(c);
+                if (out->rgba) {
+                    out->rgba[4 * o] = c.r;
+                    out->rgba[4 * o + 1] = c.g;
+                    out->rgba[4 * o + 2] = c.b;
+                    out->rgba[4 * o + 3] = 1.0f;
+                }
+                if (out->hit_id) out->hit_id[o] = wi >= 0 ? pieces[(size_t)wi].tri : -1;
+                if (out->hit_t) out->hit_t[o] = zb[o];
+                if (out->shadow) out->shadow[o] = (uint8_t)sh;
+            }
+        }
+#pragma omp critical
+        {
+            total.primary_rays += local.primary_rays;
+            total.shadow_rays += local.shadow_rays;
+            total.reflection_rays += local.reflection_rays;
+        }
+    }
     if (counters) *counters = total;
     return 0;
 }

@@ -66,6 +66,8 @@ class RenderSettings:
     enable_skysphere: bool = False
     enable_skybox: bool = False
     rng_seed: int = 0x5EED1234
+    enable_clipping: bool = True                 # raster_trace frustum clipping
+    hybrid_rasterization_tracing: bool = False   # render(): raster_trace instead of ray_trace
 
     def render_size(self):
         """Renderer::get_render_width_height (renderer.cpp:116-120)."""
@@ -107,6 +109,8 @@ class SceneData:
     light: np.ndarray                     # (3,) float32
     textures: Dict[int, np.ndarray] = field(default_factory=dict)   # slot -> (h, w, 4) float32
     skybox: Optional[List[np.ndarray]] = None                        # 6 faces (h, w, 4) float32
+    proj: Optional[np.ndarray] = None           # (16,) Camera::_perspective_proj_mat (raster_trace)
+    world_to_cam: Optional[np.ndarray] = None   # (16,) Camera::_world_to_camera_mat (raster_trace)
 
     @property
     def ntri(self) -> int:

@@ -143,6 +143,10 @@ class _ProductTransforms:
         from . import _lib
         return _lib.compose(a, b)
 
+    def inverse(self, m):
+        from . import _lib
+        return _lib.inverse(m)
+
 
 def default_transforms():
     return _ProductTransforms()
@@ -181,14 +185,17 @@ def base_settings(w, h, **kw) -> RenderSettings:
 
 
 def _camera(T, st: RenderSettings):
+    """Camera(Point(0,0,0), 80) with set_aspect_ratio(render_w / render_h): position, projection
+    inverse, camera-to-world, projection, world-to-camera (camera.cpp:5-19, renderer.cpp:226-241)."""
     rw, rh = st.render_size()
-    _, pinv = T.camera_matrices(80.0, np.float32(rw) / np.float32(rh))
+    proj, pinv = T.camera_matrices(80.0, np.float32(rw) / np.float32(rh))
     ident = T.transform("identity")
-    return np.zeros(3, np.float32), pinv, ident
+    return np.zeros(3, np.float32), pinv, ident, proj, T.inverse(ident)
 
 
 def _finish(tri, mat_idx, uv, mats, cam, light=(3.0, 3.0, 2.0), shapes=None, textures=None):
-    cam_pos, pinv, c2w = cam
+    cam_pos, pinv, c2w = cam[:3]
+    proj, w2c = (cam[3], cam[4]) if len(cam) > 3 else (None, None)
     sk, sh, sm = shapes if shapes is not None else empty_shapes()
     return SceneData(tri=np.ascontiguousarray(tri, np.float32).reshape(-1, 9),
                      tri_mat=np.ascontiguousarray(mat_idx, np.int32),
@@ -197,7 +204,9 @@ def _finish(tri, mat_idx, uv, mats, cam, light=(3.0, 3.0, 2.0), shapes=None, tex
                      materials=np.ascontiguousarray(mats, np.float32).reshape(-1, 16),
                      cam_pos=np.asarray(cam_pos, np.float32), proj_inv=np.asarray(pinv, np.float32),
                      cam_to_world=np.asarray(c2w, np.float32), light=np.asarray(light, np.float32),
-                     textures=textures or {})
+                     textures=textures or {},
+                     proj=None if proj is None else np.asarray(proj, np.float32),
+                     world_to_cam=None if w2c is None else np.asarray(w2c, np.float32))
 
 
 def sphere256(T=None, width=256, height=256):

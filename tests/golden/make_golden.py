@@ -45,6 +45,9 @@ class RefT:
     def compose(self, a, b):
         return RefHarness.compose(a, b)
 
+    def inverse(self, m):
+        return RefHarness.inverse(m)
+
 
 T = RefT()
 
@@ -173,6 +176,30 @@ def build_cases():
     sc, st = scenes.cube1080(T=T, width=100, height=60, loader=ref_loader, enable_ssaa=True, ssaa_factor=3)
     ref_threshold(sc)
     cases.append(("ssaa3_cube", sc, st, None, []))
+
+    # hybrid rasterisation (Renderer::raster_trace, renderer.cpp:869-1006)
+    sc, st = scenes.robot1080(T=T, width=160, height=90, loader=ref_loader, hybrid_rasterization_tracing=True)
+    ref_threshold(sc)
+    cases.append(("raster_robot", sc, st, None, []))
+    # the robot pulled through the near plane and past the sides: every clip case
+    sc, st = scenes.robot1080(T=T, width=160, height=90, loader=ref_loader, hybrid_rasterization_tracing=True)
+    ref_threshold(sc)
+    t = sc.tri.reshape(-1, 3, 3).astype(np.float32)
+    t = t * np.float32(2.5) + np.array([0.3, -0.4, 6.2], np.float32)
+    sc.tri = np.ascontiguousarray(t.reshape(-1, 9), np.float32)
+    cases.append(("raster_clip", sc, st, None, []))
+    cases.append(("raster_clip_bary", sc, st.copy(shading_method=BARYCENTRIC_COORDINATES_SHADING), None, []))
+    cases.append(("raster_noclip_bary", sc, st.copy(shading_method=BARYCENTRIC_COORDINATES_SHADING,
+                                                     enable_clipping=False), None, []))
+    # reflections through the raster path, and SSAA
+    st = base(120, 68, max_recursion_depth=3, rough_reflections_sample_count=4, hybrid_rasterization_tracing=True)
+    sc = scenes._finish(tri2, np.zeros(len(tri2), np.int32), uv2, mats, camera(st), shapes=shapes)
+    ref_threshold(sc)
+    cases.append(("raster_rough", sc, st, None, []))
+    sc, st = scenes.cube1080(T=T, width=100, height=60, loader=ref_loader, enable_ssaa=True, ssaa_factor=2,
+                             hybrid_rasterization_tracing=True)
+    ref_threshold(sc)
+    cases.append(("raster_ssaa_cube", sc, st, None, []))
     return cases
 
 
@@ -187,8 +214,10 @@ def pack_scene(prefix, sc: SceneData, st: RenderSettings, gen, arrays, meta):
         if sc.tri_uv is not None:
             arrays[prefix + "tri_uv"] = sc.tri_uv
     arrays[prefix + "tri_mat"] = sc.tri_mat
-    for k in ("shape_kind", "shape", "shape_mat", "materials", "cam_pos", "proj_inv", "cam_to_world", "light"):
-        arrays[prefix + k] = getattr(sc, k)
+    for k in ("shape_kind", "shape", "shape_mat", "materials", "cam_pos", "proj_inv", "cam_to_world", "light",
+              "proj", "world_to_cam"):
+        if getattr(sc, k) is not None:
+            arrays[prefix + k] = getattr(sc, k)
     for slot, img in (sc.textures or {}).items():
         arrays[f"{prefix}tex{slot}"] = img
     if sc.skybox is not None:
@@ -201,7 +230,7 @@ def main():
     for name, sc, st, gen, rows in build_cases():
         arrays, meta = {}, {"name": name}
         pack_scene("in_", sc, st, gen, arrays, meta)
-        res = RefHarness.render_rows(sc, st)
+        res = RefHarness.raster(sc, st) if st.hybrid_rasterization_tracing else RefHarness.render_rows(sc, st)
         rw, rh = st.render_size()
         arrays["out_argb"] = res.argb
         arrays["out_rgba"] = res.rgba

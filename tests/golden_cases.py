@@ -49,7 +49,8 @@ def _scene(z, prefix, meta) -> SceneData:
                    shape=z[prefix + "shape"], shape_mat=z[prefix + "shape_mat"], materials=z[prefix + "materials"],
                    cam_pos=z[prefix + "cam_pos"], proj_inv=z[prefix + "proj_inv"],
                    cam_to_world=z[prefix + "cam_to_world"], light=z[prefix + "light"], textures=textures,
-                   skybox=sky)
+                   skybox=sky, proj=z[prefix + "proj"] if prefix + "proj" in z else None,
+                   world_to_cam=z[prefix + "world_to_cam"] if prefix + "world_to_cam" in z else None)
     assert sc.triangle_hash() == meta["tri_sha256"], "rebuilt triangles differ from the fixture's"
     return sc
 

@@ -18,7 +18,7 @@ def test_oracle_full_frame_matches_reference(name):
     c = Case(name)
     exp = c.expected()
     o = Oracle(c.scene, c.settings)
-    res = o.render_rows()
+    res = o.raster() if c.settings.hybrid_rasterization_tracing else o.render_rows()
     assert np.array_equal(res.hit_id, exp["hit_id"])
     assert np.array_equal(bits(res.hit_t), bits(exp["hit_t"]))
     assert np.array_equal(res.shadow, exp["shadow"])
