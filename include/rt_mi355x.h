@@ -59,7 +59,7 @@ typedef struct rt_settings {
     int32_t image_width, image_height;
     int32_t enable_ssaa, ssaa_factor;
     int32_t enable_clipping;
-    int32_t hybrid_rasterization_tracing;   /* must be 0: raster path out of scope */
+    int32_t hybrid_rasterization_tracing;   /* rt_render: raster_trace instead of ray_trace */
     int32_t shading_method;
     int32_t compute_shadows;
     int32_t max_recursion_depth;
@@ -141,6 +141,11 @@ int rt_apply_transformation_to_camera(rt_renderer *r, const float m[16]);
 int rt_set_camera_matrices(rt_renderer *r, const float pos[3], const float proj_inv[16], const float cam_to_world[16]);
 int rt_get_camera_matrices(rt_renderer *r, float pos[3], float proj_inv[16], float cam_to_world[16]);
 
+/* Camera::_perspective_proj_mat and Camera::_world_to_camera_mat (scene/camera.h:19-30),
+ * which the raster path uses (renderer.cpp:833-838, 877-879), as the caller computed
+ * them.  Default: perspective(fov, aspect) and the inverse of cam_to_world. */
+int rt_set_camera_projection(rt_renderer *r, const float proj[16], const float world_to_cam[16]);
+
 /* Renderer::set_object_transform / reset_previous_transform (renderer.cpp:212-224) */
 int rt_set_object_transform(rt_renderer *r, const float m[16]);
 int rt_reset_previous_transform(rt_renderer *r);
@@ -161,6 +166,13 @@ int rt_destroy_bvh(rt_renderer *r);
  * internal image on the GPU (synchronous). */
 int rt_ray_trace(rt_renderer *r);
 
+/* Renderer::raster_trace (renderer.cpp:869-1006): the hybrid path -- primary visibility
+ * by rasterising the clipped triangles (z-buffer; the sequential z-test's winner, first of
+ * equal z), shading by trace_triangle (shadow and reflection rays through the octree).
+ * Reflective materials need enable_bvh (RT_EUNSUPPORTED otherwise).  Same outputs as
+ * rt_ray_trace: hit_id = the winning triangle, hit_t = its z-buffer depth. */
+int rt_raster_trace(rt_renderer *r);
+
 /* Renderer::post_process (renderer.cpp:1118-1124): SSAA downscale when enabled
  * (SSAO is out of scope and rejected in rt_set_settings). */
 int rt_post_process(rt_renderer *r);
@@ -169,7 +181,8 @@ int rt_post_process(rt_renderer *r);
  * (image_width x image_height after post_process) to argb; w/h receive its size. */
 int rt_get_image(rt_renderer *r, uint32_t *argb, int32_t *w, int32_t *h);
 
-/* render(Renderer&) (utils/mainUtils.cpp:6-21): ray_trace + post_process;
+/* render(Renderer&) (utils/mainUtils.cpp:6-21): raster_trace (hybrid_rasterization_tracing)
+ * or ray_trace, then post_process;
  * *ms receives the wall time in milliseconds (may be NULL). */
 int rt_render(rt_renderer *r, float *ms);
 

@@ -1145,7 +1145,7 @@ static inline v4 xform4(const float *m, v4 v)
 
 typedef struct { v4 a, b, c; v3 tu, tv; } otri4;   /* Triangle4, triangle.h:24-40 */
 
-#define ORC_CLIP_MAX 64
+#define ORC_CLIP_MAX 12   /* std::array<Triangle4, 12> (renderer.h:304-309); more pieces are UB there and dropped here */
 
 static inline int in_half(v4 p, int i, int sgn) { return sgn > 0 ? v4c(p, i) < p.w : v4c(p, i) > -p.w; }
 

@@ -759,7 +759,7 @@ bool h_in_half(const vec4& p, int i, int sgn) { return sgn > 0 ? p(i) < p.w : p(
 // clip_triangles_to_plane<i, sgn> (renderer.cpp:669-850); in may alias out when n == 1
 int h_clip_plane(const Triangle4* in, int n, Triangle4* out, int i, int sgn)
 {
-    const int CAP = 64;
+    const int CAP = 12;   // std::array<Triangle4, 12>: more pieces are UB in the reference and dropped here
     int k = 0;
     for (int t = 0; t < n; t++) {
         const Triangle4 T = in[t];
@@ -858,7 +858,7 @@ int ref_raster(const orc_scene* sc, const orc_settings* st, orc_outputs* out, or
     for (size_t ti = 0; ti < H.tris.size(); ti++) {
         const Triangle& O = H.tris[ti];
         Triangle tc = H.world_to_cam(O);
-        Triangle4 A[64], B[64];
+        Triangle4 A[12], B[12];
         A[0] = Triangle4(H.proj(vec4(tc._a)), H.proj(vec4(tc._b)), H.proj(vec4(tc._c)), tc._tex_coords_u,
                          tc._tex_coords_v);
         int n = 1;

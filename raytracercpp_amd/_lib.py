@@ -83,6 +83,7 @@ SIGNATURES = {
     "rt_set_camera_transform": (C.c_int, [_H, _f32p]),
     "rt_apply_transformation_to_camera": (C.c_int, [_H, _f32p]),
     "rt_set_camera_matrices": (C.c_int, [_H, _f32p, _f32p, _f32p]),
+    "rt_set_camera_projection": (C.c_int, [_H, _f32p, _f32p]),
     "rt_get_camera_matrices": (C.c_int, [_H, _f32p, _f32p, _f32p]),
     "rt_set_object_transform": (C.c_int, [_H, _f32p]),
     "rt_reset_previous_transform": (C.c_int, [_H]),
@@ -91,6 +92,7 @@ SIGNATURES = {
     "rt_reconstruct_bvh_new": (C.c_int, [_H]),
     "rt_destroy_bvh": (C.c_int, [_H]),
     "rt_ray_trace": (C.c_int, [_H]),
+    "rt_raster_trace": (C.c_int, [_H]),
     "rt_post_process": (C.c_int, [_H]),
     "rt_get_image": (C.c_int, [_H, _u32p, _i32p, _i32p]),
     "rt_render": (C.c_int, [_H, _f32p]),

@@ -162,6 +162,10 @@ int rt_set_camera_matrices(rt_renderer* r, const float pos[3], const float proj_
 {
     return guarded(R(r), [&] { return (pos && proj_inv && c2w) ? R(r)->set_camera_matrices(pos, proj_inv, c2w) : RT_EINVAL; });
 }
+int rt_set_camera_projection(rt_renderer* r, const float proj[16], const float w2c[16])
+{
+    return guarded(R(r), [&] { return (proj && w2c) ? R(r)->set_camera_projection(proj, w2c) : RT_EINVAL; });
+}
 int rt_get_camera_matrices(rt_renderer* r, float pos[3], float proj_inv[16], float c2w[16])
 {
     return guarded(R(r), [&] {
@@ -196,6 +200,10 @@ int rt_destroy_bvh(rt_renderer* r)
 int rt_ray_trace(rt_renderer* r)
 {
     return guarded(R(r), [&] { return R(r)->ray_trace(); });
+}
+int rt_raster_trace(rt_renderer* r)
+{
+    return guarded(R(r), [&] { return R(r)->raster_trace(); });
 }
 int rt_post_process(rt_renderer* r)
 {

@@ -1706,6 +1706,395 @@ __global__ __launch_bounds__(BLOCK) void refl_resolve_kernel(KParams P, ReflArgs
         st3(A.ret + 3 * (size_t)f, c);
 }
 
+// ===========================================================================
+// Renderer::raster_trace (renderer.cpp:869-1006): hybrid rasterisation of the
+// primary visibility, then trace_triangle's shading (shadows / reflections through
+// the octree).  The reference's OpenMP triangle loop races on the z-buffer; the
+// defined result is the sequential one (triangles and their clipped pieces in
+// order, strict z-test), which the per-pixel 64-bit atomicMin of
+// (order-preserving z, piece index) reproduces: pieces are numbered in
+// (triangle, piece) order, so among equal z the first one wins.
+// ===========================================================================
+struct V4 {
+    float x, y, z, w;
+};
+__device__ __forceinline__ V4 v4(float x, float y, float z, float w) { V4 r = {x, y, z, w}; return r; }
+__device__ __forceinline__ V4 v4add(V4 a, V4 b) { return v4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }   // vec.cpp:123
+__device__ __forceinline__ V4 v4sub(V4 a, V4 b) { return v4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w); }   // vec.cpp:128
+__device__ __forceinline__ V4 v4mul(float t, V4 u) { return v4(u.x * t, u.y * t, u.z * t, u.w * t); }       // vec.cpp:133-141
+__device__ __forceinline__ float v4c(V4 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
+// Transform::operator()(vec4), mat.cpp:118-131
+__device__ __forceinline__ V4 xform4(const float* m, V4 v)
+{
+    return v4(m[0] * v.x + m[1] * v.y + m[2] * v.z + m[3] * v.w, m[4] * v.x + m[5] * v.y + m[6] * v.z + m[7] * v.w,
+              m[8] * v.x + m[9] * v.y + m[10] * v.z + m[11] * v.w, m[12] * v.x + m[13] * v.y + m[14] * v.z + m[15] * v.w);
+}
+// Renderer::matrix_transform_z, renderer.cpp:856-867 (a division, not a reciprocal)
+__device__ __forceinline__ float xform_z(const float* m, v3 p)
+{
+    float zt = m[8] * p.x + m[9] * p.y + m[10] * p.z + m[11];
+    float wt = m[12] * p.x + m[13] * p.y + m[14] * p.z + m[15];
+    if (wt == 1.0f)
+        return zt;
+    return zt / wt;
+}
+
+struct Tri4 {   // Triangle4, triangle.h:24-40
+    V4 a, b, c;
+    v3 tu, tv;
+};
+
+constexpr int CLIP_MAX = 12;   // std::array<Triangle4, 12>: more pieces are UB in the reference, dropped here
+
+__device__ __forceinline__ bool in_half(V4 p, int i, int sgn) { return sgn > 0 ? v4c(p, i) < p.w : v4c(p, i) > -p.w; }
+
+// clip_triangles_to_plane<i, sgn>, renderer.cpp:669-850 (in may alias out when n == 1)
+__device__ int clip_plane(const Tri4* in, int n, Tri4* out, int i, int sgn)
+{
+    int k = 0;
+    const float fs = (float)sgn;
+    for (int t = 0; t < n; t++) {
+        const Tri4 T = in[t];
+        bool ia = in_half(T.a, i, sgn), ib = in_half(T.b, i, sgn), ic = in_half(T.c, i, sgn);
+        int cnt = (int)ia + (int)ib + (int)ic;
+        if (cnt == 3) {
+            if (k < CLIP_MAX) out[k] = T;
+            k++;
+        } else if (cnt == 1) {
+            V4 p0 = ia ? T.a : (ib ? T.b : T.c), p1 = ia ? T.b : (ib ? T.c : T.a), p2 = ia ? T.c : (ib ? T.a : T.b);
+            float u0 = ia ? T.tu.x : (ib ? T.tu.y : T.tu.z), u1 = ia ? T.tu.y : (ib ? T.tu.z : T.tu.x),
+                  u2 = ia ? T.tu.z : (ib ? T.tu.x : T.tu.y);
+            float w0 = ia ? T.tv.x : (ib ? T.tv.y : T.tv.z), w1 = ia ? T.tv.y : (ib ? T.tv.z : T.tv.x),
+                  w2 = ia ? T.tv.z : (ib ? T.tv.x : T.tv.y);
+            float d0 = v4c(p0, i) - p0.w * fs, d1 = v4c(p1, i) - p1.w * fs, d2 = v4c(p2, i) - p2.w * fs;
+            float t1 = d1 / (d1 - d0), t2 = d2 / (d2 - d0);
+            Tri4 R;
+            R.a = p0;
+            R.b = v4add(p1, v4mul(t1 - 0.0f, v4sub(p0, p1)));
+            R.c = v4add(p2, v4mul(t2 - 0.0f, v4sub(p0, p2)));
+            R.tu = mk(u0, u1 + (t1 - 0.0f) * (u0 - u1), u2 + (t2 - 0.0f) * (u0 - u2));
+            R.tv = mk(w0, w1 + (t1 - 0.0f) * (w0 - w1), w2 + (t2 - 0.0f) * (w0 - w2));
+            if (k < CLIP_MAX) out[k] = R;
+            k++;
+        } else if (cnt == 2) {
+            V4 q0 = !ia ? T.a : (!ib ? T.b : T.c), q1 = !ia ? T.b : (!ib ? T.c : T.a), q2 = !ia ? T.c : (!ib ? T.a : T.b);
+            float u0 = !ia ? T.tu.y : (!ib ? T.tu.z : T.tu.x), u1 = !ia ? T.tu.z : (!ib ? T.tu.x : T.tu.y),
+                  u2 = !ia ? T.tu.x : (!ib ? T.tu.y : T.tu.z);
+            float w0 = !ia ? T.tv.y : (!ib ? T.tv.z : T.tv.x), w1 = !ia ? T.tv.z : (!ib ? T.tv.x : T.tv.y),
+                  w2 = !ia ? T.tv.x : (!ib ? T.tv.y : T.tv.z);
+            float e1 = v4c(q1, i) - q1.w * fs, e2 = v4c(q2, i) - q2.w * fs, e0 = v4c(q0, i) - q0.w * fs;
+            float t1 = e0 / (e0 - e1), t2 = e0 / (e0 - e2);
+            V4 P1 = v4add(q0, v4mul(t1 - 0.0f, v4sub(q1, q0)));
+            V4 P2 = v4add(q0, v4mul(t2 - 0.0f, v4sub(q2, q0)));
+            Tri4 R1, R2;
+            R1.a = q1; R1.b = q2; R1.c = P2;
+            R1.tu = mk(u0, u1, u2 + (t2 - 0.0f) * (u1 - u2));
+            R1.tv = mk(w0, w1, w2 + (t2 - 0.0f) * (w1 - w2));
+            R2.a = q1; R2.b = P2; R2.c = P1;
+            R2.tu = mk(u0, u2 + (t2 - 0.0f) * (u1 - u2), u2 + (t1 - 0.0f) * (u0 - u2));
+            R2.tv = mk(w0, w2 + (t2 - 0.0f) * (w1 - w2), w2 + (t1 - 0.0f) * (w0 - w2));
+            if (k < CLIP_MAX) out[k] = R1;
+            k++;
+            if (k < CLIP_MAX) out[k] = R2;
+            k++;
+        }
+    }
+    return k < CLIP_MAX ? k : CLIP_MAX;
+}
+
+// _world_to_camera_mat(triangle), perspective_projection(vec4(vertex)), clip_triangle (renderer.cpp:833-854)
+__device__ int clip_triangle(const KParams& P, const RasterArgs& A, int64_t t, Tri4* buf0, Tri4* buf1, const Tri4** res)
+{
+    const float* q = A.tri9 + 9 * t;
+    v3 ca = xform_point(A.w2c, mk(q[0], q[1], q[2]));
+    v3 cb = xform_point(A.w2c, mk(q[3], q[4], q[5]));
+    v3 cc = xform_point(A.w2c, mk(q[6], q[7], q[8]));
+    buf0[0].a = xform4(A.proj, v4(ca.x, ca.y, ca.z, 1.0f));
+    buf0[0].b = xform4(A.proj, v4(cb.x, cb.y, cb.z, 1.0f));
+    buf0[0].c = xform4(A.proj, v4(cc.x, cc.y, cc.z, 1.0f));
+    if (P.tri_uv) {
+        const float* uv = P.tri_uv + 6 * t;
+        buf0[0].tu = mk(uv[0], uv[1], uv[2]);
+        buf0[0].tv = mk(uv[3], uv[4], uv[5]);
+    } else {
+        buf0[0].tu = mk(-1, -1, -1);
+        buf0[0].tv = mk(-1, -1, -1);
+    }
+    int n = 1;
+    *res = buf0;
+    if (A.clipping) {
+        n = clip_plane(buf0, n, buf0, 0, 1);
+        n = clip_plane(buf0, n, buf1, 0, -1);
+        n = clip_plane(buf1, n, buf0, 1, 1);
+        n = clip_plane(buf0, n, buf1, 1, -1);
+        n = clip_plane(buf1, n, buf0, 2, 1);
+        n = clip_plane(buf0, n, buf1, 2, -1);
+        *res = buf1;
+    }
+    return n;
+}
+
+__global__ __launch_bounds__(BLOCK) void raster_count_kernel(KParams P, RasterArgs A)
+{
+    int64_t t = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= A.ntri)
+        return;
+    Tri4 b0[CLIP_MAX], b1[CLIP_MAX];
+    const Tri4* res;
+    A.count[t] = clip_triangle(P, A, t, b0, b1, &res);
+}
+
+// (int)(double), x86 cvttsd2si semantics: INT_MIN out of range / NaN
+__device__ __forceinline__ int d2i(double d) { return (d > -2147483649.0 && d < 2147483648.0) ? (int)d : INT_MIN; }
+
+__global__ __launch_bounds__(BLOCK) void raster_write_kernel(KParams P, RasterArgs A)
+{
+    int64_t t = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= A.ntri)
+        return;
+    Tri4 b0[CLIP_MAX], b1[CLIP_MAX];
+    const Tri4* res;
+    int n = clip_triangle(P, A, t, b0, b1, &res);
+    for (int k = 0; k < n; k++) {
+        const Tri4& Q = res[k];
+        int idx = A.offset[t] + k;
+        RasterPiece& R = A.pieces[idx];
+        // Triangle(Triangle4), triangle.cpp:12-23
+        float iaw = 1.0f / Q.a.w, ibw = 1.0f / Q.b.w, icw = 1.0f / Q.c.w;
+        v3 a = mk(Q.a.x * iaw, Q.a.y * iaw, Q.a.z * iaw);
+        v3 b = mk(Q.b.x * ibw, Q.b.y * ibw, Q.b.z * ibw);
+        v3 c = mk(Q.c.x * icw, Q.c.y * icw, Q.c.z * icw);
+        st3(R.na, a);
+        st3(R.nb, b);
+        st3(R.nc, c);
+        v3 pa = xform_point(P.proj_inv, a), pb = xform_point(P.proj_inv, b), pc = xform_point(P.proj_inv, c);
+        st3(R.wa, xform_point(P.cam_to_world, pa));
+        st3(R.wb, xform_point(P.cam_to_world, pb));
+        st3(R.wc, xform_point(P.cam_to_world, pc));
+        R.inv_area = 1 / ((b.x - a.x) * (c.y - a.y) - (b.y - a.y) * (c.x - a.x));
+        float mnx = smin(a.x, smin(b.x, c.x)), mny = smin(a.y, smin(b.y, c.y));
+        float mxx = smax(a.x, smax(b.x, c.x)), mxy = smax(a.y, smax(b.y, c.y));
+        int x0 = d2i((double)(mnx + 1) * 0.5 * P.rw), y0 = d2i((double)(mny + 1) * 0.5 * P.rh);
+        int x1 = d2i((double)(mxx + 1) * 0.5 * P.rw), y1 = d2i((double)(mxy + 1) * 0.5 * P.rh);
+        R.x0 = x0 > 0 ? x0 : 0;
+        R.y0 = y0 > 0 ? y0 : 0;
+        R.x1 = P.rw - 1 < x1 ? P.rw - 1 : x1;
+        R.y1 = P.rh - 1 < y1 ? P.rh - 1 : y1;
+        R.za = xform_z(P.cam_to_world, pa);
+        R.zb = xform_z(P.cam_to_world, pb);
+        R.zc = xform_z(P.cam_to_world, pc);
+        R.tri = (int32_t)t;
+        float* uv = A.piece_uv + 6 * (size_t)idx;
+        uv[0] = Q.tu.x; uv[1] = Q.tu.y; uv[2] = Q.tu.z;
+        uv[3] = Q.tv.x; uv[4] = Q.tv.y; uv[5] = Q.tv.z;
+    }
+}
+
+// Triangle::edge_function, triangle.h:65-68
+__device__ __forceinline__ float edge_fn(float px, float py, v3 a, v3 b)
+{
+    return (b.x - a.x) * (py - a.y) - (b.y - a.y) * (px - a.x);
+}
+
+// launch-local row of a global row (-1: another rank's band)
+__device__ __forceinline__ int local_row(const KParams& P, int py)
+{
+    int band = py / P.band_rows;
+    if (band % P.nranks != P.rank)
+        return -1;
+    return (band / P.nranks) * P.band_rows + (py - band * P.band_rows);
+}
+
+__device__ __forceinline__ uint32_t z_order(float z)
+{
+    if (z == 0.0f)
+        z = 0.0f;   // -0 == +0 in the reference's z-test
+    uint32_t u = __float_as_uint(z);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+constexpr int RASTER_BIG = 2048;   // bounding-box pixels above which a piece gets a workgroup
+
+// raster_trace's loops over rows y_first, y_first + ystep, .. of one piece's bounding
+// box: every covered sample's candidate goes into the z-key buffer.  The sample
+// coordinates accumulate exactly as the reference's loops do (iy += hs per row from
+// y0, ix += ws per column from x0).
+__device__ void raster_rows(const KParams& P, const RasterArgs& A, int idx, int y_first, int ystep)
+{
+    const RasterPiece& R = A.pieces[idx];
+    v3 a = ld3(R.na), b = ld3(R.nb), c = ld3(R.nc);
+    const float inv_area = R.inv_area, za = R.za, zb = R.zb, zc = R.zc;
+    const int x0 = R.x0, x1 = R.x1, y0 = R.y0, y1 = R.y1;
+    const float hs = 1.0f / P.rh * 2, ws = 1.0f / P.rw * 2;
+    float iy = y0 * hs - 1;
+    int yc = y0;
+    for (int py = y_first; py <= y1; py += ystep) {
+        for (; yc < py; yc++) iy += hs;
+        int lr = local_row(P, py);
+        if (lr < 0)
+            continue;
+        unsigned long long* zrow = A.zkey + (size_t)lr * P.rw;
+        float ix = x0 * ws - 1;
+        for (int px = x0; px <= x1; px++, ix += ws) {
+            float sx = ix + ws * 0.5f, sy = iy + hs * 0.5f;
+            float u = edge_fn(sx, sy, c, a);
+            if (u < 0) continue;
+            float v = edge_fn(sx, sy, a, b);
+            if (v < 0) continue;
+            float w = edge_fn(sx, sy, b, c);
+            if (w < 0) continue;
+            u *= inv_area;
+            v *= inv_area;
+            w *= inv_area;
+            float z = -1 / (1 / za * w + 1 / zb * u + 1 / zc * v);
+            if (!(z < INFINITY))
+                continue;   // NaN / +inf never pass the z-test against the INFINITY-filled buffer
+            unsigned long long key = ((unsigned long long)z_order(z) << 32) | (uint32_t)idx;
+            atomicMin(&zrow[px], key);
+        }
+    }
+}
+
+// the raster loops of raster_trace for one piece: candidates into the z-key buffer
+__global__ __launch_bounds__(BLOCK) void raster_fill_kernel(KParams P, RasterArgs A, int npieces)
+{
+    int idx = blockIdx.x * BLOCK + threadIdx.x;
+    if (idx >= npieces)
+        return;
+    const RasterPiece& R = A.pieces[idx];
+    if (R.y1 >= R.y0 && R.x1 >= R.x0 && (int64_t)(R.y1 - R.y0 + 1) * (R.x1 - R.x0 + 1) > RASTER_BIG) {
+        A.big[atomicAdd(A.nbig, 1u)] = idx;
+        return;
+    }
+    raster_rows(P, A, idx, R.y0, 1);
+}
+
+// big pieces: the workgroup's threads take the bounding box's rows round-robin
+__global__ __launch_bounds__(BLOCK) void raster_fill_big_kernel(KParams P, RasterArgs A)
+{
+    const unsigned n = *A.nbig;
+    for (unsigned k = blockIdx.x; k < n; k += gridDim.x) {
+        const int idx = A.big[k];
+        raster_rows(P, A, idx, A.pieces[idx].y0 + (int)threadIdx.x, BLOCK);
+    }
+}
+
+// per pixel: the winning piece's shading (trace_triangle / debug shadings), reflective
+// hits become level-1 frames of the reflection engine.  P.tri_uv is the piece_uv table
+// and Rec::tri a piece index here (trace_triangle's temporary triangle).
+__global__ __launch_bounds__(BLOCK, RT_OCC) void raster_shade_kernel(KParams P, RasterArgs A,
+                                                                     FrameRec* fr1, unsigned int* nfr1)
+{
+    extern __shared__ uint2 lds_levels[];
+    uint2* lv = lds_levels + threadIdx.x;
+    int lane = threadIdx.x & 63;
+    const int ntiles = P.tiles_x * P.tiles_y;
+    v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+    const float hs = 1.0f / P.rh * 2, ws = 1.0f / P.rw * 2;
+    unsigned nshadow = 0;
+    for (;;) {
+        int tile = 0;
+        if (lane == 0)
+            tile = (int)atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[2]), 1u);
+        tile = __builtin_amdgcn_readfirstlane(tile);
+        if (tile >= ntiles)
+            break;
+        int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+        int px = tx * 8 + (lane & 7);
+        int lr = ty * 8 + (lane >> 3);
+        int py = lr < P.local_rows ? global_row(P, lr) : P.rh;
+        if (px >= P.rw || py >= P.rh)
+            continue;
+        size_t o = (size_t)lr * P.rw + px;
+        unsigned long long key = A.zkey[o];
+        c3 color = background();
+        bool sh = false, deferred = false;
+        int hit = -1;
+        float zt = INFINITY;
+        if (key != ~0ull) {
+            int idx = (int)(uint32_t)key;
+            uint32_t zo = (uint32_t)(key >> 32);
+            zt = __uint_as_float((zo & 0x80000000u) ? (zo & 0x7fffffffu) : ~zo);
+            const RasterPiece& R = A.pieces[idx];
+            hit = R.tri;
+            float iy = R.y0 * hs - 1;
+            for (int y = R.y0; y < py; y++) iy += hs;
+            float ix = R.x0 * ws - 1;
+            for (int x = R.x0; x < px; x++) ix += ws;
+            float sx = ix + ws * 0.5f, sy = iy + hs * 0.5f;
+            v3 a = ld3(R.na), b = ld3(R.nb), c = ld3(R.nc);
+            float u = edge_fn(sx, sy, c, a) * R.inv_area;
+            float v = edge_fn(sx, sy, a, b) * R.inv_area;
+            const float* q = A.tri9 + 9 * (size_t)R.tri;
+            if (P.shading_method == RT_SHADING) {
+                // trace_triangle (renderer.cpp:619-628): Triangle::intersect with the world piece
+                v3 pw = xform_point(P.cam_to_world, xform_point(P.proj_inv, mk(sx, sy, -1)));
+                v3 rd = normalize(pw - cam);
+                v3 wa = ld3(R.wa), wb = ld3(R.wb), wc = ld3(R.wc);
+                v3 ab = wb - wa, ac = wc - wa;
+                v3 nn = cross(wb - wa, wc - wa);
+                TriRec T;
+                T.q0 = make_float4(wa.x, wa.y, wa.z, ab.x);
+                T.q1 = make_float4(ab.y, ab.z, ac.x, ac.y);
+                T.q2 = make_float4(ac.z, nn.x, nn.y, nn.z);
+                TRay Rr = make_ray(P, cam, rd);
+                float tt, uu, vv;
+                color = col(0, 0, 0);
+                if (tri_test_rec(T, Rr, tt, uu, vv)) {
+                    // the HitInfo Triangle::intersect fills (triangle.cpp:81-88), texcoords of the piece
+                    Rec fin = rec_fresh();
+                    fin.tri = idx;
+                    fin.t = tt;
+                    fin.u = uu;
+                    fin.v = vv;
+                    fin.mat = P.tri_mat[R.tri];
+                    fin.normal = normalize(nn);
+                    const float* uvp = P.tri_uv + 6 * (size_t)idx;
+                    float u1 = uvp[0], u2 = uvp[1], u3 = uvp[2], v1 = uvp[3], v2 = uvp[4], v3_ = uvp[5];
+                    float dU1 = u2 - u1, dV1 = v2 - v1, dU2 = u3 - u1, dV2 = v3_ - v1;
+                    float f = 1.0f / (dU1 * dV2 - dU2 * dV1);
+                    fin.tangent.x = f * (dV2 * ab.x - dV1 * ac.x);
+                    fin.tangent.y = f * (dV2 * ab.y - dV1 * ac.y);
+                    fin.tangent.z = f * (dV2 * ab.z - dV1 * ac.z);
+                    Direct D = shade_direct(P, cam, rd, fin, lv, nshadow);
+                    sh = D.shadowed;
+                    const float* m = mat_of(P, fin.mat);
+                    if (m[12] > 0.0f) {
+                        unsigned fi = atomicAdd(nfr1, 1u);
+                        make_frame(P, fr1[fi], D.ip, fin.normal, rd, D.fc, frame_roughness(P, fin, m), fin.mat,
+                                   pixel_seed((uint32_t)(py * P.rw + px), P.rng_seed), (int)o);
+                        deferred = true;
+                    } else
+                        color = shade_finish(P, D.fc, m, col(0, 0, 0));
+                }
+            } else if (P.shading_method == ABS_NORMALS || P.shading_method == PASTEL_NORMALS) {
+                v3 ta = mk(q[0], q[1], q[2]), tb = mk(q[3], q[4], q[5]), tc = mk(q[6], q[7], q[8]);
+                v3 nn = normalize(cross(tb - ta, tc - ta));
+                color = P.shading_method == ABS_NORMALS ? col(fabsf(nn.x), fabsf(nn.y), fabsf(nn.z))
+                                                         : (col(nn.x, nn.y, nn.z) + col(1.0f, 1.0f, 1.0f)) * 0.5f;
+            } else if (P.shading_method == BARYCENTRIC) {
+                color = (col(1, 0, 0) * u + col(0, 1.0f, 0) * v) + col(0, 0, 1) * (1 - u - v);
+            } else if (P.shading_method == VISUALIZE_AO) {
+                color = col(0.9f, 0.9f, 0.9f);
+                if (P.enable_ao_mapping) {
+                    float tu, tv;
+                    get_tex_coords(P, idx, u, v, tu, tv);
+                    float ao = tex_floor(P.tex[TEX_AO], tu, tv).r;
+                    color = color * col(ao, ao, ao);
+                }
+            }
+        }
+        if (!deferred) {
+            if (P.argb) P.argb[o] = color_to_argb(color);
+            if (P.rgba) P.rgba[o] = make_float4(color.r, color.g, color.b, 1.0f);
+        }
+        if (P.hit_id) P.hit_id[o] = hit;
+        if (P.hit_t) P.hit_t[o] = zt;
+        if (P.shadow) P.shadow[o] = (uint8_t)sh;
+    }
+    if (nshadow) atomicAdd(&P.counters[0], (unsigned long long)nshadow);
+}
+
 // ImageUtils::downscale_image_qt_ARGB32 (imageUtils.h:98-147): integer box
 // filter of 8-bit channels, truncating division.
 __global__ __launch_bounds__(256) void downscale_kernel(const uint32_t* __restrict__ in, int w, int h_rows, int f,
@@ -1853,5 +2242,49 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_keys(
         return hipSuccess;
     hipLaunchKernelGGL(rt::refl_keys_kernel, dim3((n + rt::BLOCK - 1) / rt::BLOCK), dim3(rt::BLOCK), 0, stream, *P, fr,
                        n, keys, idx);
+    return hipGetLastError();
+}
+
+// ---- raster launchers (renderer.cpp raster path) ----
+// stage: 0 count, 1 write, 2 fill (small pieces), 3 fill (big pieces)
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_raster_stage(int stage, const rt::KParams* P,
+                                                                            const rt::RasterArgs* A, int npieces,
+                                                                            hipStream_t stream)
+{
+    if (stage < 2) {
+        if (A->ntri <= 0)
+            return hipSuccess;
+        dim3 g((unsigned)((A->ntri + rt::BLOCK - 1) / rt::BLOCK));
+        if (stage == 0)
+            hipLaunchKernelGGL(rt::raster_count_kernel, g, dim3(rt::BLOCK), 0, stream, *P, *A);
+        else
+            hipLaunchKernelGGL(rt::raster_write_kernel, g, dim3(rt::BLOCK), 0, stream, *P, *A);
+    } else if (stage == 2) {
+        if (npieces <= 0)
+            return hipSuccess;
+        hipLaunchKernelGGL(rt::raster_fill_kernel, dim3((npieces + rt::BLOCK - 1) / rt::BLOCK), dim3(rt::BLOCK), 0,
+                           stream, *P, *A, npieces);
+    } else {
+        if (npieces <= 0)
+            return hipSuccess;
+        hipLaunchKernelGGL(rt::raster_fill_big_kernel, dim3(P->max_blocks > 0 ? P->max_blocks : 1024),
+                           dim3(rt::BLOCK), 0, stream, *P, *A);
+    }
+    return hipGetLastError();
+}
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_raster_shade(const rt::KParams* P,
+                                                                            const rt::RasterArgs* A,
+                                                                            rt::FrameRec* fr1,
+                                                                            unsigned int* nfr1, hipStream_t stream)
+{
+    int tiles = P->tiles_x * P->tiles_y;
+    int blocks = (tiles + rt::WAVES_PER_BLOCK - 1) / rt::WAVES_PER_BLOCK;
+    if (blocks > P->max_blocks && P->max_blocks > 0)
+        blocks = P->max_blocks;
+    if (blocks < 1)
+        return hipSuccess;
+    size_t lds = (size_t)(P->levels > 0 ? P->levels : 1) * rt::BLOCK * sizeof(uint2);
+    hipLaunchKernelGGL(rt::raster_shade_kernel, dim3(blocks), dim3(rt::BLOCK), lds, stream, *P, *A, fr1, nfr1);
     return hipGetLastError();
 }

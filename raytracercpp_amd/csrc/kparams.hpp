@@ -129,4 +129,31 @@ struct ReflArgs {
     int32_t stride;          // max(N, 1)
 };
 
+// ---- hybrid rasterisation (kernels.hip "Renderer::raster_trace") ----
+// One clipped piece of a triangle, as raster_trace (renderer.cpp:869-1006) derives it.
+struct RasterPiece {
+    float na[3], nb[3], nc[3];   // Triangle(Triangle4): NDC vertices
+    float wa[3], wb[3], wc[3];   // _camera_to_world_mat(proj_inv(NDC triangle)): trace_triangle's triangle
+    float inv_area;
+    float za, zb, zc;            // matrix_transform_z(cam_to_world, proj_inv(vertex))
+    int32_t x0, y0, x1, y1;      // pixel bounding box (clamped)
+    int32_t tri;                 // caller triangle index
+    int32_t pad;
+};
+
+struct RasterArgs {
+    const float* tri9;                 // caller triangles (world space), caller order
+    int64_t ntri;
+    float proj[16];                    // Camera::_perspective_proj_mat
+    float w2c[16];                     // Camera::_world_to_camera_mat
+    int32_t clipping;                  // RenderSettings::enable_clipping
+    int32_t* count;                    // pieces per triangle
+    const int32_t* offset;             // exclusive scan of count: first piece of each triangle
+    RasterPiece* pieces;               // in (triangle, piece) order
+    float* piece_uv;                   // [6] per piece: u0 u1 u2 v0 v1 v2 (the piece's texcoords)
+    unsigned long long* zkey;          // per launch-local pixel: (ordered z << 32) | piece, min wins
+    int32_t* big;                      // pieces whose bounding box is rasterised by a whole workgroup
+    unsigned int* nbig;
+};
+
 }  // namespace rt

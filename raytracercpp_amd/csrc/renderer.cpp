@@ -22,6 +22,13 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_keys(
                                                                          hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_trace_rays(const rt::KParams* P, const float* o, const float* d, int n, int32_t* id,
                                            float* t, float* u, float* v, uint8_t* ret, hipStream_t stream);
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_raster_stage(int stage, const rt::KParams* P,
+                                                                            const rt::RasterArgs* A, int npieces,
+                                                                            hipStream_t stream);
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_raster_shade(const rt::KParams* P,
+                                                                            const rt::RasterArgs* A,
+                                                                            rt::FrameRec* fr1, unsigned int* nfr1,
+                                                                            hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_downscale(const uint32_t* in, int w, int h_rows, int f, uint32_t* out,
                                           hipStream_t stream);
 
@@ -82,8 +89,9 @@ int Renderer::init(std::string& err)
         err = std::string("HIP init failed: ") + hipGetErrorString(e);
         return RT_EHIP;
     }
-    DevBuf* all[] = {&d_nodes_, &d_tris_, &d_tri_id_, &d_tri_mat_, &d_tri_uv_, &d_mats_, &d_internal_, &d_image_,
-                     &d_rgba_, &d_hit_id_, &d_hit_t_, &d_shadow_, &d_counters_, &d_band_tmp_};
+    DevBuf* all[] = {&d_nodes_, &d_tris_,  &d_tri_id_, &d_tri_mat_, &d_tri_uv_, &d_mats_,   &d_internal_,
+                     &d_image_, &d_rgba_,  &d_hit_id_, &d_hit_t_,   &d_shadow_, &d_counters_, &d_band_tmp_,
+                     &d_tri9_,  &d_rcount_, &d_roff_,  &d_pieces_,  &d_piece_uv_, &d_zkey_, &d_big_, &d_scan_tmp_};
     for (DevBuf* b : all) b->device = device_;
     for (auto& b : d_tex_) b.device = device_;
     for (auto& b : d_sky_) b.device = device_;
@@ -128,8 +136,6 @@ void Renderer::update_camera_projection()
 
 int Renderer::set_settings(const rt_settings& s)
 {
-    if (s.hybrid_rasterization_tracing)
-        return fail(RT_EUNSUPPORTED, "hybrid_rasterization_tracing: the raster path is out of scope");
     if (s.enable_ssao)
         return fail(RT_EUNSUPPORTED, "enable_ssao: SSAO post-processing is out of scope (stubbed)");
     if (s.image_width <= 0 || s.image_height <= 0 || (s.enable_ssaa && s.ssaa_factor <= 0))
@@ -278,6 +284,13 @@ int Renderer::set_camera_matrices(const float pos[3], const float proj_inv[16], 
     return RT_OK;
 }
 
+int Renderer::set_camera_projection(const float proj[16], const float w2c[16])
+{
+    std::memcpy(proj_, proj, sizeof(proj_));
+    std::memcpy(w2c_, w2c, sizeof(w2c_));
+    return RT_OK;
+}
+
 void Renderer::get_camera_matrices(float pos[3], float proj_inv[16], float c2w[16]) const
 {
     std::memcpy(pos, cam_pos_, sizeof(cam_pos_));
@@ -410,6 +423,7 @@ int Renderer::ensure_device_scene()
         if (e != hipSuccess)
             return hip_fail(e, "upload (scene)");
         geom_dirty_ = false;
+        tri9_dirty_ = true;
         build_ms_ = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     if (mats_dirty_) {
@@ -651,13 +665,129 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
     return RT_OK;
 }
 
+// The raster path: raster_trace (renderer.cpp:869-1006) for one launch (whole frame or
+// this rank's bands).  Every triangle is clipped (clip_triangle, :833-854) into pieces
+// numbered in (triangle, piece) order; the pieces' covered samples race for each pixel
+// through a 64-bit atomicMin of (order-preserving z, piece index), which is the
+// sequential z-test's winner (strict <: the first of equal z wins); then every pixel is
+// shaded from its winning piece, and reflective hits go through the frame engine.
+int Renderer::launch_raster(const KParams& P, hipStream_t stream)
+{
+    hipError_t e;
+    const int64_t n = (int64_t)tri_mat_.size();
+    if (tri9_dirty_) {
+        if ((e = d_tri9_.reserve(tri_.size() * 4)) != hipSuccess) return hip_fail(e, "hipMalloc (raster triangles)");
+        if (!tri_.empty() &&
+            (e = hipMemcpyAsync(d_tri9_.p, tri_.data(), tri_.size() * 4, hipMemcpyHostToDevice, stream)) != hipSuccess)
+            return hip_fail(e, "upload (raster triangles)");
+        tri9_dirty_ = false;
+    }
+    RasterArgs A;
+    std::memset(&A, 0, sizeof(A));
+    A.tri9 = d_tri9_.as<float>();
+    A.ntri = n;
+    std::memcpy(A.proj, proj_, sizeof(A.proj));
+    std::memcpy(A.w2c, w2c_, sizeof(A.w2c));
+    A.clipping = s_.enable_clipping;
+    if ((e = d_rcount_.reserve((size_t)(n + 1) * 4)) != hipSuccess || (e = d_roff_.reserve((size_t)(n + 1) * 4)) != hipSuccess)
+        return hip_fail(e, "hipMalloc (raster counts)");
+    A.count = d_rcount_.as<int32_t>();
+    A.offset = d_roff_.as<int32_t>();
+    if ((e = hipMemsetAsync(A.count, 0, (size_t)(n + 1) * 4, stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+    if ((e = rt_launch_raster_stage(0, &P, &A, 0, stream)) != hipSuccess) return hip_fail(e, "raster_count_kernel launch");
+    size_t tb = 0;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, A.count, d_roff_.as<int32_t>(), (int)(n + 1), stream)) !=
+            hipSuccess ||
+        (e = d_scan_tmp_.reserve(tb)) != hipSuccess ||
+        (e = hipcub::DeviceScan::ExclusiveSum(d_scan_tmp_.p, tb, A.count, d_roff_.as<int32_t>(), (int)(n + 1),
+                                              stream)) != hipSuccess)
+        return hip_fail(e, "piece scan");
+    int32_t npieces = 0;
+    if ((e = hipMemcpyAsync(&npieces, d_roff_.as<int32_t>() + n, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(stream)) != hipSuccess)
+        return hip_fail(e, "raster_count_kernel");
+    size_t npx = (size_t)P.rw * P.local_rows;
+    if ((e = d_pieces_.reserve((size_t)npieces * sizeof(RasterPiece))) != hipSuccess ||
+        (e = d_piece_uv_.reserve((size_t)npieces * 24)) != hipSuccess ||
+        (e = d_big_.reserve((size_t)npieces * 4 + 64)) != hipSuccess || (e = d_zkey_.reserve(npx * 8)) != hipSuccess)
+        return hip_fail(e, "hipMalloc (raster pieces)");
+    A.pieces = d_pieces_.as<RasterPiece>();
+    A.piece_uv = d_piece_uv_.as<float>();
+    A.zkey = d_zkey_.as<unsigned long long>();
+    A.nbig = d_big_.as<unsigned int>();
+    A.big = d_big_.as<int32_t>() + 16;
+    if ((e = hipMemsetAsync(A.zkey, 0xff, npx * 8, stream)) != hipSuccess ||
+        (e = hipMemsetAsync(A.nbig, 0, 4, stream)) != hipSuccess)
+        return hip_fail(e, "hipMemsetAsync");
+    for (int stage = 1; stage <= 3; stage++)
+        if ((e = rt_launch_raster_stage(stage, &P, &A, npieces, stream)) != hipSuccess)
+            return hip_fail(e, "raster kernel launch");
+    // shading reads texcoords through Rec::tri = piece index: the piece table stands in
+    // for tri_uv (trace_triangle's temporary Triangle carries the clipped texcoords)
+    KParams PS = P;
+    PS.tri_uv = A.piece_uv;
+    for (auto& L : refl_)
+        L.fr.device = L.ret.device = L.sm.device = L.hit.device = L.cnt.device = L.list.device = L.sort.device =
+            L.sort_tmp.device = device_;
+    ReflLevel& L1 = refl_[1];
+    const bool frames = P.has_reflection;
+    if (frames) {
+        if ((e = L1.fr.reserve(npx * sizeof(FrameRec))) != hipSuccess || (e = L1.cnt.reserve(64)) != hipSuccess)
+            return hip_fail(e, "hipMalloc (reflection frames)");
+        if ((e = hipMemsetAsync(L1.cnt.p, 0, 4, stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+    }
+    if ((e = rt_launch_raster_shade(&PS, &A, frames ? L1.fr.as<FrameRec>() : nullptr,
+                                    frames ? L1.cnt.as<unsigned int>() : nullptr, stream)) != hipSuccess)
+        return hip_fail(e, "raster_shade_kernel launch");
+    if (!frames)
+        return RT_OK;
+    unsigned n1 = 0;
+    if ((e = hipMemcpyAsync(&n1, L1.cnt.p, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(stream)) != hipSuccess)
+        return hip_fail(e, "raster_shade_kernel");
+    return n1 ? refl_level(P, 1, (int)n1, stream) : RT_OK;
+}
+
+// the checks ray_trace / raster_trace / render_bands_device make before a launch
+int Renderer::check_frame() const
+{
+    if (s_.shading_method == RT_SHADING && any_reflection(mats_) && s_.max_recursion_depth > 15)
+        return RT_EUNSUPPORTED;
+    if (s_.hybrid_rasterization_tracing) {
+        if (tri_mat_.size() >= ((size_t)1 << 27))
+            return RT_EUNSUPPORTED;   // 12 pieces per triangle must index in 31 bits
+        if (s_.shading_method == RT_SHADING && any_reflection(mats_) && !s_.enable_bvh)
+            return RT_EUNSUPPORTED;   // the frame engine traces through the octree
+    }
+    return RT_OK;
+}
+
 // Renderer::ray_trace, renderer.cpp:1068-1116
 int Renderer::ray_trace()
 {
+    rt_settings keep = s_;
+    s_.hybrid_rasterization_tracing = 0;
+    int rc = trace_frame();
+    s_.hybrid_rasterization_tracing = keep.hybrid_rasterization_tracing;
+    return rc;
+}
+
+int Renderer::raster_trace()
+{
+    rt_settings keep = s_;
+    s_.hybrid_rasterization_tracing = 1;
+    int rc = trace_frame();
+    s_.hybrid_rasterization_tracing = keep.hybrid_rasterization_tracing;
+    return rc;
+}
+
+int Renderer::trace_frame()
+{
     if (validate() != RT_OK)
         return fail(RT_EINVAL, "invalid scene: material index out of range or enabled texture map missing");
-    if (s_.shading_method == RT_SHADING && any_reflection(mats_) && s_.max_recursion_depth > 15)
-        return fail(RT_EUNSUPPORTED, "reflective materials with max_recursion_depth > 15");
+    if (check_frame() != RT_OK)
+        return fail(RT_EUNSUPPORTED, "reflective materials with max_recursion_depth > 15, a raster frame with "
+                                     "reflections and no BVH, or more than 2^27 triangles to rasterise");
     int rc = ensure_device_scene();
     if (rc != RT_OK)
         return rc;
@@ -685,7 +815,7 @@ int Renderer::ray_trace()
     P.counters = d_counters_.as<unsigned long long>();
     if ((e = hipMemsetAsync(d_counters_.p, 0, 64, stream_)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
     hipEventRecord(ev_[0], stream_);
-    if ((rc = launch_trace(P, stream_)) != RT_OK) return rc;
+    if ((rc = launch_frame(P, stream_)) != RT_OK) return rc;
     hipEventRecord(ev_[1], stream_);
     unsigned long long cnt[2] = {0, 0};
     if ((e = hipMemcpyAsync(cnt, d_counters_.p, sizeof(cnt), hipMemcpyDeviceToHost, stream_)) != hipSuccess)
@@ -822,8 +952,9 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
         return fail(RT_EINVAL, "render_bands_device: bad band layout");
     if (validate() != RT_OK)
         return fail(RT_EINVAL, "invalid scene: material index out of range or enabled texture map missing");
-    if (s_.shading_method == RT_SHADING && any_reflection(mats_) && s_.max_recursion_depth > 15)
-        return fail(RT_EUNSUPPORTED, "reflective materials with max_recursion_depth > 15");
+    if (check_frame() != RT_OK)
+        return fail(RT_EUNSUPPORTED, "reflective materials with max_recursion_depth > 15, a raster frame with "
+                                     "reflections and no BVH, or more than 2^27 triangles to rasterise");
     int rc = ensure_device_scene();
     if (rc != RT_OK)
         return rc;
@@ -855,7 +986,7 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
     }
     if ((e = hipMemsetAsync(d_counters_.p, 0, 64, stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
     hipEventRecord(ring_[2 * ring_next_], stream);
-    if ((rc = launch_trace(P, stream)) != RT_OK) return rc;
+    if ((rc = launch_frame(P, stream)) != RT_OK) return rc;
     hipEventRecord(ring_[2 * ring_next_ + 1], stream);
     ring_next_ = (ring_next_ + 1) % EV_RING;
     if (ring_count_ < EV_RING) ring_count_++;
@@ -931,7 +1062,8 @@ int Renderer::band_counters(unsigned long long out[2])
 float render(Renderer& renderer, int* rc)
 {
     auto t0 = std::chrono::steady_clock::now();
-    int r = renderer.ray_trace();
+    // mainUtils.cpp:10-13: raster_trace or ray_trace by the settings
+    int r = renderer.render_settings().hybrid_rasterization_tracing ? renderer.raster_trace() : renderer.ray_trace();
     if (r == RT_OK)
         r = renderer.post_process();
     if (rc)

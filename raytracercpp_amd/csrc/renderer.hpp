@@ -54,6 +54,8 @@ public:
     int apply_transformation_to_camera(const float m[16]);
     int set_camera_matrices(const float pos[3], const float proj_inv[16], const float c2w[16]);
     void get_camera_matrices(float pos[3], float proj_inv[16], float c2w[16]) const;
+    // Camera::_perspective_proj_mat / _world_to_camera_mat as the caller computed them (raster path)
+    int set_camera_projection(const float proj[16], const float w2c[16]);
     int set_object_transform(const float m[16]);
     int reset_previous_transform();
     int set_texture(int slot, int w, int h, const float* rgba);
@@ -61,6 +63,9 @@ public:
     int reconstruct_bvh_new();
     int destroy_bvh();
     int ray_trace();
+    // Renderer::raster_trace (renderer.cpp:869-1006): rasterised primary visibility,
+    // trace_triangle shading (shadows / reflections through the octree)
+    int raster_trace();
     int post_process();
     int get_image(uint32_t* argb, int32_t* w, int32_t* h);
     int request_aux(bool rgba, bool hit, bool shadow);
@@ -90,6 +95,15 @@ private:
     void fill_params(KParams& P) const;
     // the trace of one launch: the ray-trace kernel, or the reflection engine (frames by level)
     int launch_trace(const KParams& P, hipStream_t stream);
+    // the raster path of one launch: clip + piece table, z-keys, shading, then the
+    // reflection engine for the reflective pixels
+    int launch_raster(const KParams& P, hipStream_t stream);
+    int launch_frame(const KParams& P, hipStream_t stream)
+    {
+        return s_.hybrid_rasterization_tracing ? launch_raster(P, stream) : launch_trace(P, stream);
+    }
+    int check_frame() const;
+    int trace_frame();
     int refl_level(const KParams& P, int level, int nframes, hipStream_t stream);
 
     int device_;
@@ -123,6 +137,10 @@ private:
     DevBuf d_nodes_, d_tris_, d_tri_id_, d_tri_mat_, d_tri_uv_, d_mats_;
     DevBuf d_tex_[TEX_SLOTS], d_sky_[6];
     DevBuf d_internal_, d_image_, d_rgba_, d_hit_id_, d_hit_t_, d_shadow_, d_counters_, d_band_tmp_;
+    // raster path: caller-order triangles, per-triangle piece counts / offsets, the piece
+    // table and its texcoords, the z-key buffer, the big-piece list, scan scratch
+    DevBuf d_tri9_, d_rcount_, d_roff_, d_pieces_, d_piece_uv_, d_zkey_, d_big_, d_scan_tmp_;
+    bool tri9_dirty_ = true;
     bool want_rgba_ = false, want_hit_ = false, want_shadow_ = false;
     bool aux_valid_ = false;
     // current image (Renderer::_image): internal after ray_trace, downscaled after post_process
@@ -149,7 +167,7 @@ private:
 
 // render(Renderer&) (tp2/projets/utils/mainUtils.cpp:6-21): ray_trace then post_process;
 // returns the elapsed milliseconds (*rc gets the status; on an error the remaining
-// steps are skipped).  The hybrid raster branch is not provided.
+// steps are skipped); raster_trace instead of ray_trace when hybrid_rasterization_tracing.
 float render(Renderer& renderer, int* rc = nullptr);
 
 }  // namespace rt

@@ -130,6 +130,11 @@ class Renderer:
         pos, pi, cw = f32(pos), f32(proj_inv), f32(cam_to_world)
         self._call("rt_set_camera_matrices", ptr(pos, _f32p), ptr(pi, _f32p), ptr(cw, _f32p))
 
+    def set_camera_projection(self, proj, world_to_cam):
+        """Camera::_perspective_proj_mat / _world_to_camera_mat, used by raster_trace."""
+        pr, wc = f32(proj), f32(world_to_cam)
+        self._call("rt_set_camera_projection", ptr(pr, _f32p), ptr(wc, _f32p))
+
     def get_camera_matrices(self):
         pos, pi, cw = np.zeros(3, np.float32), np.zeros(16, np.float32), np.zeros(16, np.float32)
         self._call("rt_get_camera_matrices", ptr(pos, _f32p), ptr(pi, _f32p), ptr(cw, _f32p))
@@ -182,6 +187,10 @@ class Renderer:
     # -- rendering (renderer.h:149-154) ---------------------------------------------
     def ray_trace(self):
         self._call("rt_ray_trace")
+
+    def raster_trace(self):
+        """Renderer::raster_trace (renderer.cpp:869-1006): the hybrid raster + trace path."""
+        self._call("rt_raster_trace")
 
     def post_process(self):
         self._call("rt_post_process")
@@ -255,6 +264,8 @@ class Renderer:
         self.set_render_settings(st)
         self.change_render_size(st.image_width, st.image_height)
         self.set_camera_matrices(sc.cam_pos, sc.proj_inv, sc.cam_to_world)
+        if sc.proj is not None and sc.world_to_cam is not None:
+            self.set_camera_projection(sc.proj, sc.world_to_cam)
         self.set_light_position(sc.light)
         self.set_materials(sc.materials)
         self.clear_geometry()
