@@ -38,6 +38,7 @@ class OrcScene(C.Structure):
         ("tex_w", C.c_int32 * NTEX), ("tex_h", C.c_int32 * NTEX), ("tex", _f32p * NTEX),
         ("sky_w", C.c_int32 * 6), ("sky_h", C.c_int32 * 6), ("sky", _f32p * 6),
         ("proj", C.c_float * 16), ("world_to_cam", C.c_float * 16),
+        ("cam_fov", C.c_float), ("cam_aspect", C.c_float),
     ]
 
 
@@ -55,11 +56,14 @@ class OrcSettings(C.Structure):
         ("displacement_mapping_strength", C.c_float), ("parallax_mapping_steps", C.c_int32),
         ("enable_roughness_mapping", C.c_int32), ("enable_skysphere", C.c_int32),
         ("enable_skybox", C.c_int32), ("rng_seed", C.c_uint32), ("enable_clipping", C.c_int32),
+        ("enable_ssao", C.c_int32), ("ssao_sample_count", C.c_int32),
+        ("ssao_radius", C.c_float), ("ssao_amount", C.c_float),
     ]
 
 
 class OrcOutputs(C.Structure):
-    _fields_ = [("argb", _u32p), ("rgba", _f32p), ("hit_id", _i32p), ("hit_t", _f32p), ("shadow", _u8p)]
+    _fields_ = [("argb", _u32p), ("rgba", _f32p), ("hit_id", _i32p), ("hit_t", _f32p), ("shadow", _u8p),
+                ("zbuf", _f32p), ("nbuf", _f32p)]
 
 
 class OrcCounters(C.Structure):
@@ -92,8 +96,10 @@ class _Pinned:
         return a
 
 
-def make_orc_scene(scene, pin: _Pinned) -> OrcScene:
+def make_orc_scene(scene, pin: _Pinned, settings=None) -> OrcScene:
     s = OrcScene()
+    if settings is not None:
+        s.cam_fov, s.cam_aspect = scene.lens(settings)
     tri = pin.arr(scene.tri.reshape(-1, 9), np.float32)
     s.ntri = tri.shape[0]
     s.tri = _ptr(tri, _f32p)
@@ -130,9 +136,9 @@ def make_orc_scene(scene, pin: _Pinned) -> OrcScene:
 
 def make_orc_settings(st) -> OrcSettings:
     o = OrcSettings()
-    for name, _ in OrcSettings._fields_:
+    for name, typ in OrcSettings._fields_:
         v = getattr(st, name)
-        setattr(o, name, float(v) if name == "displacement_mapping_strength" else int(v))
+        setattr(o, name, float(v) if typ is C.c_float else int(v))
     return o
 
 
@@ -145,6 +151,8 @@ class RenderResult:
         self.hit_id = np.zeros(n, np.int32)
         self.hit_t = np.zeros(n, np.float32)
         self.shadow = np.zeros(n, np.uint8)
+        self.zbuf = np.zeros(n, np.float32)
+        self.nbuf = np.zeros((n, 3), np.float32)
         self.counters = {}
         self.seconds = 0.0
 
@@ -155,6 +163,8 @@ class RenderResult:
         o.hit_id = _ptr(self.hit_id, _i32p)
         o.hit_t = _ptr(self.hit_t, _f32p)
         o.shadow = _ptr(self.shadow, _u8p)
+        o.zbuf = _ptr(self.zbuf, _f32p)
+        o.nbuf = _ptr(self.nbuf, _f32p)
         return o
 
 
@@ -180,13 +190,14 @@ class Oracle:
             L.orc_bvh_stats.argtypes = [C.c_void_p, _i64p]
             L.orc_bvh_node.argtypes = [C.c_void_p, C.c_int, _f32p, _f32p, _i32p, _i32p, _i32p]
             L.orc_heap_order.argtypes = [_f32p, C.c_int, _i32p]
+            L.orc_ssao.argtypes = [C.c_void_p, _f32p, _f32p, _u32p, _i32p, C.c_int]
             cls._lib = L
         return cls._lib
 
     def __init__(self, scene, settings):
         L = self.lib()
         self._pin = _Pinned()
-        self._sc = make_orc_scene(scene, self._pin)
+        self._sc = make_orc_scene(scene, self._pin, settings)
         self._st = make_orc_settings(settings)
         self.settings = settings
         self._h = L.orc_create(C.byref(self._sc), C.byref(self._st))
@@ -230,6 +241,17 @@ class Oracle:
             raise RuntimeError("orc_raster failed")
         res.counters = cnt.as_dict()
         return res
+
+    def ssao(self, res: RenderResult, nthreads=0):
+        """post_process_ssao_SIMD on a full internal frame (res from render_rows() or raster()):
+        returns (argb after the SSAO blur, per-pixel occlusion counts)."""
+        argb = res.argb.copy()
+        ao = np.zeros(res.argb.shape[0], np.int32)
+        rc = self.lib().orc_ssao(self._h, _ptr(res.zbuf, _f32p), _ptr(res.nbuf, _f32p), _ptr(argb, _u32p),
+                                 _ptr(ao, _i32p), nthreads)
+        if rc != 0:
+            raise RuntimeError("orc_ssao failed")
+        return argb, ao
 
     def bvh_query(self, orig, dirs):
         orig = np.ascontiguousarray(orig, np.float32)
@@ -303,6 +325,7 @@ class RefHarness:
                                      C.POINTER(OrcCounters)]
             L.ref_downscale_argb.argtypes = [_u32p, C.c_int, C.c_int, C.c_int, _u32p]
             L.ref_heap_order.argtypes = [_f32p, C.c_int, _i32p]
+            L.ref_ssao.argtypes = [C.POINTER(OrcScene), C.POINTER(OrcSettings), _f32p, _f32p, _u32p, _i32p]
             cls._lib = L
         return cls._lib
 
@@ -381,7 +404,7 @@ class RefHarness:
     @classmethod
     def render_rows(cls, scene, settings, row_begin=0, row_count=None) -> RenderResult:
         pin = _Pinned()
-        sc = make_orc_scene(scene, pin)
+        sc = make_orc_scene(scene, pin, settings)
         st = make_orc_settings(settings)
         rw, rh = settings.render_size()
         if row_count is None:
@@ -402,7 +425,7 @@ class RefHarness:
     def raster(cls, scene, settings) -> RenderResult:
         """raster_trace on the reference's vec4 / Triangle4 / Transform / Triangle code."""
         pin = _Pinned()
-        sc = make_orc_scene(scene, pin)
+        sc = make_orc_scene(scene, pin, settings)
         st = make_orc_settings(settings)
         rw, rh = settings.render_size()
         res = RenderResult(rw, rh)
@@ -417,7 +440,7 @@ class RefHarness:
     def render_row_sample(cls, scene, settings, row_begin, row_count, row_stride) -> RenderResult:
         """Internal rows row_begin + i * row_stride (i < row_count), for CPU timing samples."""
         pin = _Pinned()
-        sc = make_orc_scene(scene, pin)
+        sc = make_orc_scene(scene, pin, settings)
         st = make_orc_settings(settings)
         rw, _ = settings.render_size()
         res = RenderResult(rw, row_count)
@@ -430,6 +453,19 @@ class RefHarness:
         res.seconds = cls.lib().ref_last_render_seconds()
         res.counters = cnt.as_dict()
         return res
+
+    @classmethod
+    def ssao(cls, scene, settings, res: RenderResult):
+        """post_process_ssao_SIMD (renderer.cpp:1229-1434) on the reference's SIMD helpers."""
+        pin = _Pinned()
+        sc = make_orc_scene(scene, pin, settings)
+        st = make_orc_settings(settings)
+        argb = res.argb.copy()
+        ao = np.zeros(res.argb.shape[0], np.int32)
+        if cls.lib().ref_ssao(C.byref(sc), C.byref(st), _ptr(res.zbuf, _f32p), _ptr(res.nbuf, _f32p),
+                              _ptr(argb, _u32p), _ptr(ao, _i32p)) != 0:
+            raise RuntimeError("ref_ssao failed")
+        return argb, ao
 
     @classmethod
     def heap_order(cls, keys):

@@ -1465,6 +1465,14 @@ ORC_API int orc_raster(const struct orc_ctx *X, orc_outputs *out, orc_counters *
                 if (out->hit_id) out->hit_id[o] = wi >= 0 ? pieces[wi].tri : -1;
                 if (out->hit_t) out->hit_t[o] = zb[o];
                 if (out->shadow) out->shadow[o] = (uint8_t)sh;
+                /* renderer.cpp:975-979: the z-test winner's z and original_triangle._normal */
+                if (out->zbuf) out->zbuf[o] = zb[o];
+                if (out->nbuf) {
+                    v3 nn = wi >= 0 ? X->tris[pieces[wi].tri].n : V(0, 0, 0);
+                    out->nbuf[3 * o] = nn.x;
+                    out->nbuf[3 * o + 1] = nn.y;
+                    out->nbuf[3 * o + 2] = nn.z;
+                }
             }
         }
 #ifdef _OPENMP
@@ -1530,6 +1538,15 @@ ORC_API int orc_render_rows(const struct orc_ctx *X, int row_begin, int row_coun
                 if (out->hit_id) out->hit_id[o] = found ? src : -1;
                 if (out->hit_t) out->hit_t[o] = hi.t;
                 if (out->shadow) out->shadow[o] = (uint8_t)(found && shadowed);
+                /* renderer.cpp:1104-1110: hits write the z / normal buffers; the others keep
+                 * the cleared values (the UI clears both before every render, mainwindow.cpp:184-185) */
+                if (out->zbuf) out->zbuf[o] = found ? -(cam.z + rd.z * hi.t) : INFINITY;
+                if (out->nbuf) {
+                    v3 nn = found ? hi.normal : V(0, 0, 0);
+                    out->nbuf[3 * o] = nn.x;
+                    out->nbuf[3 * o + 1] = nn.y;
+                    out->nbuf[3 * o + 2] = nn.z;
+                }
             }
         }
 #ifdef _OPENMP
@@ -1539,6 +1556,206 @@ ORC_API int orc_render_rows(const struct orc_ctx *X, int row_begin, int row_coun
     }
     if (counters)
         *counters = total;
+    return 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Renderer::post_process_ssao_SIMD (renderer.cpp:1229-1434)                   */
+/* ------------------------------------------------------------------------- */
+/* The reference seeds one 8-lane xorshift32 generator (xorshift.h:8-35) and one
+ * scalar generator (:37-65) per OpenMP thread with std::rand() (renderer.cpp:1250-
+ * 1261), so its occlusion noise is not reproducible run to run.  Here every pixel
+ * owns a fresh xorshift32 state ssao_state(pixel, seed); the SIMD columns draw from
+ * it as their 8-lane generator's lane would (signed conversion, / (float)INT32_MAX),
+ * the leftover columns (render_width % 8) as the scalar generator would.  Per
+ * sample the draws are x, y, z, then the lateral one, as renderer.cpp:1299-1304.  */
+static uint32_t ssao_state(uint32_t pixel, uint32_t seed)
+{
+    uint32_t x = mix32(pixel * 0x9E3779B9u ^ seed ^ 0x5A0C1D3Bu);
+    return x ? x : 0x9E3779B9u;
+}
+
+static inline uint32_t xs32(uint32_t *s)   /* xorshift.h:13-22 / :43-52 */
+{
+    uint32_t x = *s;
+    x ^= x << 13;
+    x ^= x >> 17;
+    x ^= x << 5;
+    return *s = x;
+}
+
+/* _mm256_cvtps_epi32 under the default MXCSR: round to nearest even; NaN and
+ * out-of-range values give INT_MIN */
+static inline int cvt_rne(float f)
+{
+    if (!(f >= -2147483648.0f && f < 2147483648.0f))
+        return INT32_MIN;
+    return (int)rintf(f);
+}
+
+/* one lane of the SIMD loop body, renderer.cpp:1263-1361 */
+static int ssao_simd_pixel(const struct orc_ctx *X, const float *zb, const float *nb, int x, int y, uint32_t st,
+                           float fovm)
+{
+    const int W = X->rw, H = X->rh;
+    const orc_settings *S = &X->s;
+    const float *pm = X->sc.proj;
+    float view_z = zb[(size_t)y * W + x];
+    int valid = view_z != INFINITY && view_z == view_z;   /* _CMP_NEQ_OQ */
+    float y_ndc = (float)y / (float)H;
+    y_ndc = y_ndc * 2.0f;
+    y_ndc = y_ndc - 1.0f;
+    float x_ndc = (float)x / (float)W;
+    x_ndc = x_ndc * 2.0f;
+    x_ndc = x_ndc - 1.0f;
+    float vrx = x_ndc * (fovm * X->sc.cam_aspect);
+    float vry = y_ndc * fovm;
+    v3 csp = V(view_z * vrx, view_z * vry, view_z * -1.0f);
+    const float *np = nb + 3 * ((size_t)y * W + x);
+    v3 n = V(np[0], np[1], np[2]);
+    {   /* _mm256_normalize: a * (1 / sqrt(x*x + (y*y + z*z))) (m256Vector.cpp:73-108) */
+        float len = sqrtf(n.x * n.x + (n.y * n.y + n.z * n.z));
+        float inv = 1.0f / len;
+        n = V(n.x * inv, n.y * inv, n.z * inv);
+    }
+    int occ = 0;
+    for (int i = 0; i < S->ssao_sample_count; i++) {
+        float rx = (float)(int32_t)xs32(&st) / 2147483648.0f;
+        float ry = (float)(int32_t)xs32(&st) / 2147483648.0f;
+        float rz = (float)(int32_t)xs32(&st) / 2147483648.0f;
+        float len = sqrtf(rx * rx + (ry * ry + rz * rz));
+        float inv = 1.0f / len;
+        v3 rs = V(rx * inv, ry * inv, rz * inv);
+        float lat = ((float)(int32_t)xs32(&st) / 2147483648.0f + 1.0f) * 0.5f;
+        float k = lat + 0.0001f;
+        rs = V(rs.x * k, rs.y * k, rs.z * k);
+        rs = V(rs.x * S->ssao_radius, rs.y * S->ssao_radius, rs.z * S->ssao_radius);
+        rs = V(rs.x + csp.x, rs.y + csp.y, rs.z + csp.z);
+        v3 vd = V(rs.x - csp.x, rs.y - csp.y, rs.z - csp.z);
+        float dt = vd.x * n.x + (vd.y * n.y + vd.z * n.z);
+        float mask = dt < 0.0f ? 1.0f : 0.0f;
+        v3 bf = V((csp.x - rs.x) * 2.0f, (csp.y - rs.y) * 2.0f, (csp.z - rs.z) * 2.0f);
+        rs = V(rs.x + bf.x * mask, rs.y + bf.y * mask, rs.z + bf.z * mask);
+        /* __m256Point::transform (m256Point.cpp:3-37): fused multiply-adds, w = 1 / wt */
+        float xt = fmaf(pm[0], rs.x, fmaf(pm[1], rs.y, fmaf(pm[2], rs.z, pm[3])));
+        float yt = fmaf(pm[4], rs.x, fmaf(pm[5], rs.y, fmaf(pm[6], rs.z, pm[7])));
+        float wt = fmaf(pm[12], rs.x, fmaf(pm[13], rs.y, fmaf(pm[14], rs.z, pm[15])));
+        float w = 1.0f / wt;
+        float ndx = xt * w, ndy = yt * w;
+        int px = cvt_rne(((ndx + 1.0f) * 0.5f) * (float)W);
+        int py = cvt_rne(((ndy + 1.0f) * 0.5f) * (float)H);
+        int wm1 = cvt_rne((float)W - 1.0f), hm1 = cvt_rne((float)H - 1.0f);
+        px = px < wm1 ? px : wm1;
+        px = px > 0 ? px : 0;
+        py = py < hm1 ? py : hm1;
+        py = py > 0 ? py : 0;
+        int off = (int)((uint32_t)px + (uint32_t)py * (uint32_t)cvt_rne((float)W));
+        float sgd = -1.0f * zb[off];
+        float dz = fabsf(sgd - csp.z);
+        int range = dz <= S->ssao_radius;
+        int depth = rs.z < sgd;
+        occ += (range && depth && valid) ? 1 : 0;
+    }
+    return occ;
+}
+
+/* the scalar loop over the leftover columns, renderer.cpp:1363-1413 */
+static int ssao_scalar_pixel(const struct orc_ctx *X, const float *zb, const float *nb, int x, int y, uint32_t st,
+                             float tanv)
+{
+    const int W = X->rw, H = X->rh;
+    const orc_settings *S = &X->s;
+    float view_z = zb[(size_t)y * W + x];
+    if (view_z == INFINITY)
+        return 0;
+    float x_ndc = (float)x / W * 2 - 1;
+    float y_ndc = (float)y / H * 2 - 1;
+    float vrx = x_ndc * X->sc.cam_aspect * tanv;
+    float vry = y_ndc * tanv;
+    v3 csp = V(vrx * view_z, vry * view_z, -view_z);
+    const float *np = nb + 3 * ((size_t)y * W + x);
+    v3 n = vnormalize(V(np[0], np[1], np[2]));
+    int16_t occ = 0;
+    for (int i = 0; i < S->ssao_sample_count; i++) {
+        float rx = xs32(&st) / (float)UINT32_MAX * 2 - 1;
+        float ry = xs32(&st) / (float)UINT32_MAX * 2 - 1;
+        float rz = xs32(&st) / (float)UINT32_MAX * 2 - 1;
+        v3 rs = vnormalize(V(rx, ry, rz));
+        rs = vscale(xs32(&st) / (float)UINT32_MAX + 0.0001f, rs);
+        rs = vscale(S->ssao_radius, rs);
+        rs = vadd(rs, csp);
+        if (vdot(vsub(rs, csp), n) < 0)
+            rs = vadd(rs, vscale(2, vsub(csp, rs)));
+        v3 ndc = xform_point(X->sc.proj, rs);
+        int px = d2i((ndc.x + 1) * 0.5 * W);
+        int py = d2i((ndc.y + 1) * 0.5 * H);
+        px = px > 0 ? px : 0;
+        px = px < W - 1 ? px : W - 1;
+        py = py > 0 ? py : 0;
+        py = py < H - 1 ? py : H - 1;
+        float sgd = -zb[(size_t)py * W + px];
+        if (fabsf(sgd - csp.z) > S->ssao_radius)
+            continue;
+        if (rs.z < sgd)
+            occ = (int16_t)(occ + 1);
+    }
+    return occ;
+}
+
+/* SSAO on the internal ARGB image, before the SSAA downscale (renderer.cpp:1118-1124):
+ * per-pixel occlusion counts, then the 7x7 box blur applied to the image
+ * (renderer.cpp:1416-1431).  fovm = (float)tan(fov / 2 / 180 * M_PI) (renderer.cpp:1245)
+ * and tanv = tan(radians(fov / 2)) (renderer.cpp:1379) come from the host libm. */
+ORC_API int orc_ssao(const struct orc_ctx *X, const float *zb, const float *nb, uint32_t *argb, int32_t *ao_out,
+                     int nthreads)
+{
+    const int W = X->rw, H = X->rh;
+    const orc_settings *S = &X->s;
+    const float fov = X->sc.cam_fov;
+    const float fovm = (float)tan(fov / 2 / 180 * M_PI);
+    const float tanv = tanf(((float)M_PI / 180) * (fov / 2));
+    const int simd_w = W - W % 8;
+    int32_t *ao = (int32_t *)calloc((size_t)W * H, sizeof(int32_t));
+    if (!ao)
+        return -1;
+#ifdef _OPENMP
+    if (nthreads <= 0)
+        nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(static) num_threads(nthreads)
+#endif
+    for (int y = 0; y < H; y++)
+        for (int x = 0; x < W; x++) {
+            uint32_t st = ssao_state((uint32_t)(y * W + x), S->rng_seed);
+            ao[(size_t)y * W + x] = x < simd_w ? ssao_simd_pixel(X, zb, nb, x, y, st, fovm)
+                                               : ssao_scalar_pixel(X, zb, nb, x, y, st, tanv);
+        }
+    const int blur = 7, half = blur / 2;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static) num_threads(nthreads)
+#endif
+    for (int y = half; y < H - half; y++)
+        for (int x = half; x < W - half; x++) {
+            size_t o = (size_t)y * W + x;
+            if (zb[o] == INFINITY)
+                continue;
+            int sum = 0;
+            for (int dy = -half; dy <= half; dy++)
+                for (int dx = -half; dx <= half; dx++)
+                    sum += ao[(size_t)(y + dy) * W + x + dx];
+            float cm = 1 - ((float)sum / (float)(blur * blur) / (float)S->ssao_sample_count * S->ssao_amount);
+            uint32_t p = argb[o];
+            /* QColor(int, int, int) from float products (truncated); an out-of-range
+             * channel makes the colour invalid and QImage::setPixelColor ignores it */
+            int r = f2i((float)((p >> 16) & 0xff) * cm);
+            int g = f2i((float)((p >> 8) & 0xff) * cm);
+            int b = f2i((float)(p & 0xff) * cm);
+            if (r < 0 || r > 255 || g < 0 || g > 255 || b < 0 || b > 255)
+                continue;
+            argb[o] = qrgb(r, g, b);
+        }
+    if (ao_out)
+        memcpy(ao_out, ao, (size_t)W * H * sizeof(int32_t));
+    free(ao);
     return 0;
 }
 

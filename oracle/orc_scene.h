@@ -88,6 +88,10 @@ typedef struct orc_scene {
     /* hybrid rasterisation (Renderer::raster_trace, renderer.cpp:869-1006) */
     float proj[16];         /* Camera::_perspective_proj_mat, row-major */
     float world_to_cam[16]; /* Camera::_world_to_camera_mat, row-major */
+
+    /* Camera::_fov / _aspect_ratio (scene/camera.h:22-23), read by the SSAO pass
+     * (renderer.cpp:1245, 1281-1282, 1378-1379) */
+    float cam_fov, cam_aspect;
 } orc_scene;
 
 typedef struct orc_settings {
@@ -107,6 +111,9 @@ typedef struct orc_settings {
     int32_t enable_skysphere, enable_skybox;
     uint32_t rng_seed; /* counter-based RNG seed for rough reflections */
     int32_t enable_clipping; /* raster_trace: clip against the 6 frustum planes */
+    /* post_process_ssao_SIMD (renderer.cpp:1229-1434), rendererSettings.h:66-73 */
+    int32_t enable_ssao, ssao_sample_count;
+    float ssao_radius, ssao_amount;
 } orc_settings;
 
 /* per-internal-pixel outputs; any pointer may be NULL.  Arrays cover the
@@ -117,6 +124,11 @@ typedef struct orc_outputs {
     int32_t *hit_id;  /* primary closest hit: triangle index, -2-k for shape k, -1 miss (t <= 0.1) */
     float *hit_t;     /* final_hit_info.t of the primary ray (-1 when nothing) */
     uint8_t *shadow;  /* 1 when the primary hit point is shadowed */
+    /* Renderer::_z_buffer / _normal_buffer as ray_trace (renderer.cpp:1107-1110) or
+     * raster_trace (:975-979) leave them for SSAO, starting from clear_z_buffer /
+     * clear_normal_buffer (INFINITY / Vector(0,0,0), renderer.cpp:165-173) */
+    float *zbuf;      /* [px] */
+    float *nbuf;      /* [px][3] */
 } orc_outputs;
 
 /* counters (ray + traversal statistics) */

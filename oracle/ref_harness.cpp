@@ -733,6 +733,14 @@ static int render_rows_strided(const orc_scene* sc, const orc_settings* st, int 
                 if (out->hit_id) out->hit_id[o] = found ? src : -1;
                 if (out->hit_t) out->hit_t[o] = hi.t;
                 if (out->shadow) out->shadow[o] = found && shadowed;
+                // renderer.cpp:1104-1110 (buffers cleared before the render, mainwindow.cpp:184-185)
+                if (out->zbuf) out->zbuf[o] = found ? -(ray._origin.z + ray._direction.z * hi.t) : INFINITY;
+                if (out->nbuf) {
+                    Vector nn = found ? hi.normal_at_intersection : Vector(0, 0, 0);
+                    out->nbuf[3 * o] = nn.x;
+                    out->nbuf[3 * o + 1] = nn.y;
+                    out->nbuf[3 * o + 2] = nn.z;
+                }
             }
         }
 #pragma omp critical
@@ -975,6 +983,14 @@ int ref_raster(const orc_scene* sc, const orc_settings* st, orc_outputs* out, or
                 if (out->hit_id) out->hit_id[o] = wi >= 0 ? pieces[(size_t)wi].tri : -1;
                 if (out->hit_t) out->hit_t[o] = zb[o];
                 if (out->shadow) out->shadow[o] = (uint8_t)sh;
+                // renderer.cpp:975-979: _z_buffer and _normal_buffer = original_triangle._normal
+                if (out->zbuf) out->zbuf[o] = zb[o];
+                if (out->nbuf) {
+                    Vector nn = wi >= 0 ? H.tris[(size_t)pieces[(size_t)wi].tri]._normal : Vector(0, 0, 0);
+                    out->nbuf[3 * o] = nn.x;
+                    out->nbuf[3 * o + 1] = nn.y;
+                    out->nbuf[3 * o + 2] = nn.z;
+                }
             }
         }
 #pragma omp critical

@@ -68,6 +68,10 @@ class RenderSettings:
     rng_seed: int = 0x5EED1234
     enable_clipping: bool = True                 # raster_trace frustum clipping
     hybrid_rasterization_tracing: bool = False   # render(): raster_trace instead of ray_trace
+    enable_ssao: bool = False                    # post_process: SSAO before the SSAA downscale
+    ssao_sample_count: int = 64
+    ssao_radius: float = 0.5
+    ssao_amount: float = 1.0
 
     def render_size(self):
         """Renderer::get_render_width_height (renderer.cpp:116-120)."""
@@ -111,6 +115,16 @@ class SceneData:
     skybox: Optional[List[np.ndarray]] = None                        # 6 faces (h, w, 4) float32
     proj: Optional[np.ndarray] = None           # (16,) Camera::_perspective_proj_mat (raster_trace)
     world_to_cam: Optional[np.ndarray] = None   # (16,) Camera::_world_to_camera_mat (raster_trace)
+    cam_fov: float = 80.0                       # Camera::_fov (SSAO, renderer.cpp:1245, 1379)
+    cam_aspect: Optional[float] = None          # Camera::_aspect_ratio; None: render_w / render_h
+
+    def lens(self, st: "RenderSettings"):
+        """(Camera::_fov, Camera::_aspect_ratio) as float32; the aspect defaults to
+        set_aspect_ratio(render_w / render_h) (renderer.cpp:93, 260)."""
+        if self.cam_aspect is not None:
+            return float(np.float32(self.cam_fov)), float(np.float32(self.cam_aspect))
+        rw, rh = st.render_size()
+        return float(np.float32(self.cam_fov)), float(np.float32(rw) / np.float32(rh))
 
     @property
     def ntri(self) -> int:

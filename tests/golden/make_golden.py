@@ -200,6 +200,32 @@ def build_cases():
                              hybrid_rasterization_tracing=True)
     ref_threshold(sc)
     cases.append(("raster_ssaa_cube", sc, st, None, []))
+
+    # SSAO (post_process_ssao_SIMD, renderer.cpp:1229-1434): render widths with
+    # render_width % 8 != 0 exercise the scalar tail loop (renderer.cpp:1363-1413)
+    sc, st = scenes.bumpy70k(T=T, width=203, height=97, enable_ssao=True, ssao_sample_count=16)
+    ref_threshold(sc)
+    cases.append(("ssao_bumpy", sc, st, {"kind": "uv_sphere", "nu": 264, "nv": 133, "bump": 0.08,
+                                          "texcoords": False,
+                                          "xform": f32_to_bits(scenes.object_transform(T, -3.0, scale=1.2))}, []))
+    # normal-mapped hits (the normal buffer holds the mapped normal) + SSAA 2, a wide radius
+    st = base(120, 68, enable_normal_mapping=True, enable_ssaa=True, ssaa_factor=2, enable_ssao=True,
+              ssao_sample_count=24, ssao_radius=0.8)
+    mats1 = material(diffuse=(0.7, 0.6, 0.2), specular=(0.5, 0.5, 0.5), ns=30.0)[None]
+    sc = scenes._finish(tri, np.zeros(len(tri), np.int32), uv, mats1, camera(st),
+                        textures={TEX_NORMAL: tex(64, 1, "normal")})
+    ref_threshold(sc)
+    cases.append(("ssao_normal_map_ssaa", sc, st, None, []))
+    # the hybrid raster path's buffers (z-test winner's z, unnormalised triangle normal)
+    sc, st = scenes.robot1080(T=T, width=162, height=90, loader=ref_loader, hybrid_rasterization_tracing=True,
+                              enable_ssao=True, ssao_sample_count=32)
+    ref_threshold(sc)
+    cases.append(("ssao_raster_robot", sc, st, None, []))
+    # ssao_amount > 1: negative multipliers (most pixels) give invalid QColors, which leave the pixel
+    sc, st = scenes.robot1080(T=T, width=96, height=60, loader=ref_loader, enable_ssao=True, ssao_sample_count=8,
+                              ssao_amount=12.0, ssao_radius=1.5)
+    ref_threshold(sc)
+    cases.append(("ssao_invalid_colour", sc, st, None, []))
     return cases
 
 
@@ -218,6 +244,9 @@ def pack_scene(prefix, sc: SceneData, st: RenderSettings, gen, arrays, meta):
               "proj", "world_to_cam"):
         if getattr(sc, k) is not None:
             arrays[prefix + k] = getattr(sc, k)
+    if sc.cam_fov != 80.0 or sc.cam_aspect is not None:
+        arrays[prefix + "cam_lens"] = np.array([sc.cam_fov, np.nan if sc.cam_aspect is None else sc.cam_aspect],
+                                               np.float32)
     for slot, img in (sc.textures or {}).items():
         arrays[f"{prefix}tex{slot}"] = img
     if sc.skybox is not None:
@@ -237,8 +266,15 @@ def main():
         arrays["out_hit_id"] = res.hit_id
         arrays["out_hit_t"] = res.hit_t
         arrays["out_shadow"] = res.shadow
+        frame = res.argb
+        if st.enable_ssao:
+            frame, ao = RefHarness.ssao(sc, st, res)
+            arrays["out_zbuf"] = res.zbuf
+            arrays["out_nbuf"] = res.nbuf
+            arrays["out_ao"] = ao
+            arrays["out_ssao"] = frame
         if st.enable_ssaa:
-            arrays["out_final"] = RefHarness.downscale(res.argb, rw, rh, st.ssaa_factor)
+            arrays["out_final"] = RefHarness.downscale(frame, rw, rh, st.ssaa_factor)
         meta["counters"] = res.counters
         meta["row_samples"] = []
         for j, (sc_big, st_big, row_list) in enumerate(rows):

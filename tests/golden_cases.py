@@ -51,6 +51,10 @@ def _scene(z, prefix, meta) -> SceneData:
                    cam_to_world=z[prefix + "cam_to_world"], light=z[prefix + "light"], textures=textures,
                    skybox=sky, proj=z[prefix + "proj"] if prefix + "proj" in z else None,
                    world_to_cam=z[prefix + "world_to_cam"] if prefix + "world_to_cam" in z else None)
+    if prefix + "cam_lens" in z:
+        fov, aspect = (float(x) for x in z[prefix + "cam_lens"])
+        sc.cam_fov = fov
+        sc.cam_aspect = None if np.isnan(aspect) else aspect
     assert sc.triangle_hash() == meta["tri_sha256"], "rebuilt triangles differ from the fixture's"
     return sc
 

@@ -26,9 +26,17 @@ def test_oracle_full_frame_matches_reference(name):
     assert np.array_equal(bits(res.rgba), bits(exp["rgba"]))
     assert res.counters["shadow_rays"] == c.meta["counters"]["shadow_rays"]
     assert res.counters["reflection_rays"] == c.meta["counters"]["reflection_rays"]
+    frame = res.argb
+    if c.settings.enable_ssao:
+        # post_process_ssao_SIMD (renderer.cpp:1229-1434) on the z / normal buffers
+        assert np.array_equal(bits(res.zbuf), bits(exp["zbuf"]))
+        assert np.array_equal(bits(res.nbuf), bits(exp["nbuf"]))
+        frame, ao = o.ssao(res)
+        assert np.array_equal(ao, exp["ao"])
+        assert np.array_equal(frame, exp["ssao"])
     if c.settings.enable_ssaa:
         rw, rh = c.settings.render_size()
-        final = Oracle.downscale(res.argb, rw, rh, c.settings.ssaa_factor)
+        final = Oracle.downscale(frame, rw, rh, c.settings.ssaa_factor)
         assert np.array_equal(final, exp["final"])
 
 

@@ -116,3 +116,24 @@ def test_reference_row_sample_equals_full_render_rows():
     assert np.array_equal(samp.argb.reshape(-1, rw), full.argb.reshape(rh, rw)[rows])
     assert np.array_equal(samp.hit_id.reshape(-1, rw), full.hit_id.reshape(rh, rw)[rows])
     assert samp.seconds > 0
+
+
+@pytest.mark.parametrize("raster,w,h,kw", [
+    (False, 211, 101, dict(ssao_sample_count=24, ssao_radius=0.3, rng_seed=99)),
+    (False, 96, 56, dict(ssao_sample_count=12, ssao_radius=0.9, ssao_amount=0.6, enable_ssaa=True, ssaa_factor=2)),
+    (True, 165, 93, dict(ssao_sample_count=20, ssao_radius=0.6)),
+])
+def test_oracle_ssao_matches_reference_simd_helpers(raster, w, h, kw):
+    """post_process_ssao_SIMD (renderer.cpp:1229-1434): the oracle's scalar restatement of
+    the AVX2 lanes and scalar tail against the reference's own __m256 helpers."""
+    sc, st = scenes.bumpy70k(width=w, height=h, enable_ssao=True, hybrid_rasterization_tracing=raster, **kw)
+    o = Oracle(sc, st)
+    res = o.raster() if raster else o.render_rows()
+    ref = RefHarness.raster(sc, st) if raster else RefHarness.render_rows(sc, st)
+    assert np.array_equal(u32(res.zbuf), u32(ref.zbuf))
+    assert np.array_equal(u32(res.nbuf), u32(ref.nbuf))
+    a1, ao1 = o.ssao(res)
+    a2, ao2 = RefHarness.ssao(sc, st, ref)
+    assert ao1.max() > 0
+    assert np.array_equal(ao1, ao2)
+    assert np.array_equal(a1, a2)
