@@ -54,7 +54,7 @@ extern "C" {
 #define RT_TEX_SKYSPHERE 5
 
 /* RenderSettings, field for field (tp2/projets/renderer/rendererSettings.h:6-105);
- * the raster / SSAO / clipping fields are accepted but those paths are out of scope. */
+ * every field is honoured (SSAO: full-frame rendering only). */
 typedef struct rt_settings {
     int32_t image_width, image_height;
     int32_t enable_ssaa, ssaa_factor;
@@ -64,7 +64,7 @@ typedef struct rt_settings {
     int32_t compute_shadows;
     int32_t max_recursion_depth;
     int32_t enable_bvh, bvh_max_depth, bvh_leaf_object_count;
-    int32_t enable_ssao;                    /* must be 0: SSAO out of scope (stubbed) */
+    int32_t enable_ssao;                    /* post_process: SSAO before SSAA (not with rt_render_bands_device) */
     int32_t ssao_sample_count;
     float ssao_radius, ssao_amount;
     int32_t enable_ambient, enable_diffuse, enable_specular, enable_emissive;
@@ -146,6 +146,12 @@ int rt_get_camera_matrices(rt_renderer *r, float pos[3], float proj_inv[16], flo
  * them.  Default: perspective(fov, aspect) and the inverse of cam_to_world. */
 int rt_set_camera_projection(rt_renderer *r, const float proj[16], const float world_to_cam[16]);
 
+/* Camera::_fov and Camera::_aspect_ratio (scene/camera.h:22-23) as the caller holds them,
+ * without recomputing any matrix: the SSAO pass reads them (renderer.cpp:1245, 1281-1282,
+ * 1378-1379).  Default: the fov / aspect of the last change_camera_fov /
+ * change_camera_aspect_ratio / change_render_size. */
+int rt_set_camera_lens(rt_renderer *r, float fov, float aspect);
+
 /* Renderer::set_object_transform / reset_previous_transform (renderer.cpp:212-224) */
 int rt_set_object_transform(rt_renderer *r, const float m[16]);
 int rt_reset_previous_transform(rt_renderer *r);
@@ -173,8 +179,15 @@ int rt_ray_trace(rt_renderer *r);
  * rt_ray_trace: hit_id = the winning triangle, hit_t = its z-buffer depth. */
 int rt_raster_trace(rt_renderer *r);
 
-/* Renderer::post_process (renderer.cpp:1118-1124): SSAA downscale when enabled
- * (SSAO is out of scope and rejected in rt_set_settings). */
+/* Diagnostics (no reference equivalent; Renderer::_z_buffer / _normal_buffer are private,
+ * renderer.h:319-320): the internal-size z buffer, the normal buffer as 4 floats per pixel
+ * (xyz, 0) and the occlusion counts of the last SSAO pass; any pointer may be NULL. */
+int rt_get_ssao_buffers(rt_renderer *r, float *z, float *n4, int32_t *ao);
+
+/* Renderer::post_process (renderer.cpp:1118-1124): post_process_ssao_SIMD (renderer.cpp:
+ * 1229-1434) on the internal image when enable_ssao, then the SSAA downscale when enabled.
+ * The z / normal buffers SSAO reads are those of the last rt_ray_trace / rt_raster_trace,
+ * cleared before each (mainwindow.cpp:184-185); RT_ESTATE if that frame had SSAO off. */
 int rt_post_process(rt_renderer *r);
 
 /* Renderer::get_image (renderer.cpp:106-109): copies the current image

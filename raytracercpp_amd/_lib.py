@@ -84,6 +84,8 @@ SIGNATURES = {
     "rt_apply_transformation_to_camera": (C.c_int, [_H, _f32p]),
     "rt_set_camera_matrices": (C.c_int, [_H, _f32p, _f32p, _f32p]),
     "rt_set_camera_projection": (C.c_int, [_H, _f32p, _f32p]),
+    "rt_set_camera_lens": (C.c_int, [_H, C.c_float, C.c_float]),
+    "rt_get_ssao_buffers": (C.c_int, [_H, _f32p, _f32p, _i32p]),
     "rt_get_camera_matrices": (C.c_int, [_H, _f32p, _f32p, _f32p]),
     "rt_set_object_transform": (C.c_int, [_H, _f32p]),
     "rt_reset_previous_transform": (C.c_int, [_H]),

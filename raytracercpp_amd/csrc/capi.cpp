@@ -166,6 +166,14 @@ int rt_set_camera_projection(rt_renderer* r, const float proj[16], const float w
 {
     return guarded(R(r), [&] { return (proj && w2c) ? R(r)->set_camera_projection(proj, w2c) : RT_EINVAL; });
 }
+int rt_get_ssao_buffers(rt_renderer* r, float* z, float* n4, int32_t* ao)
+{
+    return guarded(R(r), [&] { return R(r)->get_ssao_buffers(z, n4, ao); });
+}
+int rt_set_camera_lens(rt_renderer* r, float fov, float aspect)
+{
+    return guarded(R(r), [&] { return R(r)->set_camera_lens(fov, aspect); });
+}
 int rt_get_camera_matrices(rt_renderer* r, float pos[3], float proj_inv[16], float c2w[16])
 {
     return guarded(R(r), [&] {

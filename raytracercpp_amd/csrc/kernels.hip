@@ -1124,6 +1124,16 @@ __device__ PixelOut trace_pixel(const KParams& P, v3 cam, v3 rd0, uint2* lv, uin
     return po;
 }
 
+// renderer.cpp:1104-1110: a primary hit writes _z_buffer = -(o.z + d.z * t) and the
+// (normal-mapped) hit normal; other pixels keep the cleared INFINITY / Vector(0)
+// (the UI clears both before every render, mainwindow.cpp:184-185).
+__device__ __forceinline__ void write_ssao_buffers(const KParams& P, size_t o, bool found, v3 cam, v3 rd,
+                                                   const Rec& fin)
+{
+    P.zbuf[o] = found ? -(cam.z + rd.z * fin.t) : INFINITY;
+    P.nbuf[o] = found ? make_float4(fin.normal.x, fin.normal.y, fin.normal.z, 0.0f) : make_float4(0, 0, 0, 0);
+}
+
 // Global internal row of a launch-local row (interleaved bands across ranks).
 __device__ __forceinline__ int global_row(const KParams& P, int lr)
 {
@@ -1175,6 +1185,7 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
         if (P.hit_id) P.hit_id[o] = po.found ? po.src : -1;
         if (P.hit_t) P.hit_t[o] = po.fin.t;
         if (P.shadow) P.shadow[o] = (uint8_t)(po.found && po.shadowed);
+        if (P.zbuf) write_ssao_buffers(P, o, po.found, cam, rd, po.fin);
     }
     if (nshadow) atomicAdd(&P.counters[0], (unsigned long long)nshadow);
     if (nrefl) atomicAdd(&P.counters[1], (unsigned long long)nrefl);
@@ -1471,6 +1482,7 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void refl_level0_kernel(KParams P, F
         if (P.hit_id) P.hit_id[o] = found ? src : -1;
         if (P.hit_t) P.hit_t[o] = fin.t;
         if (P.shadow) P.shadow[o] = (uint8_t)(found && shadowed);
+        if (P.zbuf) write_ssao_buffers(P, o, found, cam, rd, fin);
     }
     if (nshadow) atomicAdd(&P.counters[0], (unsigned long long)nshadow);
 }
@@ -2091,8 +2103,200 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void raster_shade_kernel(KParams P, 
         if (P.hit_id) P.hit_id[o] = hit;
         if (P.hit_t) P.hit_t[o] = zt;
         if (P.shadow) P.shadow[o] = (uint8_t)sh;
+        if (P.zbuf) {
+            // renderer.cpp:975-979: the z-test winner's z and original_triangle._normal
+            // (cross(b - a, c - a), triangle.cpp:9-10, unnormalised)
+            P.zbuf[o] = zt;
+            v3 nn = mk(0, 0, 0);
+            if (hit >= 0) {
+                const float* q = A.tri9 + 9 * (size_t)hit;
+                v3 ta = mk(q[0], q[1], q[2]), tb = mk(q[3], q[4], q[5]), tc = mk(q[6], q[7], q[8]);
+                nn = cross(tb - ta, tc - ta);
+            }
+            P.nbuf[o] = make_float4(nn.x, nn.y, nn.z, 0.0f);
+        }
     }
     if (nshadow) atomicAdd(&P.counters[0], (unsigned long long)nshadow);
+}
+
+// ===========================================================================
+// Renderer::post_process_ssao_SIMD (renderer.cpp:1229-1434): screen-space
+// ambient occlusion on the internal image, before the SSAA downscale.  One
+// lane per pixel.  Columns x < w - w % 8 follow the 8-lane AVX2 loop's
+// arithmetic (signed-lane randoms, the fused __m256Point::transform,
+// round-to-nearest _mm256_cvtps_epi32), the w % 8 tail columns follow the
+// scalar loop (unsigned randoms, Transform::operator(), truncating double ->
+// int).  The reference's per-thread std::rand()-seeded generators are not
+// reproducible; each pixel here owns the xorshift32 stream ssao_state(pixel),
+// drawn x, y, z then lateral per sample, as the oracle and the reference
+// harness do.  Then the 7x7 box blur of the counts is
+// applied to the image (renderer.cpp:1416-1431).
+// ===========================================================================
+__device__ __forceinline__ uint32_t ssao_state(uint32_t pixel, uint32_t seed)
+{
+    uint32_t x = mix32(pixel * 0x9E3779B9u ^ seed ^ 0x5A0C1D3Bu);
+    return x ? x : 0x9E3779B9u;
+}
+
+__device__ __forceinline__ uint32_t xs32(uint32_t& s)   // xorshift.h:13-22 / 43-52
+{
+    uint32_t x = s;
+    x ^= x << 13;
+    x ^= x >> 17;
+    x ^= x << 5;
+    s = x;
+    return x;
+}
+
+// _mm256_cvtps_epi32 under the default MXCSR: nearest-even; NaN / out of range -> INT_MIN
+__device__ __forceinline__ int cvt_rne(float f)
+{
+    if (!(f >= -2147483648.0f && f < 2147483648.0f))
+        return INT_MIN;
+    return (int)__builtin_rintf(f);
+}
+
+__device__ int ssao_simd_pixel(const SsaoArgs& A, int x, int y, float view_z, uint32_t st)
+{
+    const bool valid = view_z != INFINITY && view_z == view_z;   // _CMP_NEQ_OQ against INFINITY
+    float y_ndc = (float)y / (float)A.h * 2.0f - 1.0f;
+    float x_ndc = (float)x / (float)A.w * 2.0f - 1.0f;
+    float vrx = x_ndc * (A.fovm * A.aspect);
+    float vry = y_ndc * A.fovm;
+    v3 csp = mk(view_z * vrx, view_z * vry, view_z * -1.0f);
+    float4 nq = A.n[(size_t)y * A.w + x];
+    v3 n = mk(nq.x, nq.y, nq.z);
+    {   // _mm256_normalize (m256Vector.cpp:73-108): a * (1 / sqrt(x*x + (y*y + z*z)))
+        float inv = 1.0f / sqrtf(n.x * n.x + (n.y * n.y + n.z * n.z));
+        n = mk(n.x * inv, n.y * inv, n.z * inv);
+    }
+    const float* pm = A.proj;
+    const int wm1 = cvt_rne((float)A.w - 1.0f), hm1 = cvt_rne((float)A.h - 1.0f), wi = cvt_rne((float)A.w);
+    int occ = 0;
+    for (int i = 0; i < A.count; i++) {
+        float rx = (float)(int32_t)xs32(st) / 2147483648.0f;
+        float ry = (float)(int32_t)xs32(st) / 2147483648.0f;
+        float rz = (float)(int32_t)xs32(st) / 2147483648.0f;
+        float inv = 1.0f / sqrtf(rx * rx + (ry * ry + rz * rz));
+        v3 rs = mk(rx * inv, ry * inv, rz * inv);
+        float k = ((float)(int32_t)xs32(st) / 2147483648.0f + 1.0f) * 0.5f + 0.0001f;
+        rs = mk(rs.x * k, rs.y * k, rs.z * k);
+        rs = mk(rs.x * A.radius, rs.y * A.radius, rs.z * A.radius);
+        rs = mk(rs.x + csp.x, rs.y + csp.y, rs.z + csp.z);
+        v3 vd = mk(rs.x - csp.x, rs.y - csp.y, rs.z - csp.z);
+        float dt = vd.x * n.x + (vd.y * n.y + vd.z * n.z);
+        float flip = dt < 0.0f ? 1.0f : 0.0f;
+        v3 bf = mk((csp.x - rs.x) * 2.0f, (csp.y - rs.y) * 2.0f, (csp.z - rs.z) * 2.0f);
+        rs = mk(rs.x + bf.x * flip, rs.y + bf.y * flip, rs.z + bf.z * flip);
+        // __m256Point::transform (m256Point.cpp:3-37): fused multiply-adds, w = 1 / wt
+        float xt = __builtin_fmaf(pm[0], rs.x, __builtin_fmaf(pm[1], rs.y, __builtin_fmaf(pm[2], rs.z, pm[3])));
+        float yt = __builtin_fmaf(pm[4], rs.x, __builtin_fmaf(pm[5], rs.y, __builtin_fmaf(pm[6], rs.z, pm[7])));
+        float wt = __builtin_fmaf(pm[12], rs.x, __builtin_fmaf(pm[13], rs.y, __builtin_fmaf(pm[14], rs.z, pm[15])));
+        float w = 1.0f / wt;
+        int px = cvt_rne(((xt * w + 1.0f) * 0.5f) * (float)A.w);
+        int py = cvt_rne(((yt * w + 1.0f) * 0.5f) * (float)A.h);
+        px = px < wm1 ? px : wm1;
+        px = px > 0 ? px : 0;
+        py = py < hm1 ? py : hm1;
+        py = py > 0 ? py : 0;
+        float sgd = -1.0f * A.z[(int)((uint32_t)px + (uint32_t)py * (uint32_t)wi)];
+        occ += (fabsf(sgd - csp.z) <= A.radius && rs.z < sgd && valid) ? 1 : 0;
+    }
+    return occ;
+}
+
+__device__ int ssao_scalar_pixel(const SsaoArgs& A, int x, int y, float view_z, uint32_t st)
+{
+    if (view_z == INFINITY)
+        return 0;
+    float x_ndc = (float)x / A.w * 2 - 1;
+    float y_ndc = (float)y / A.h * 2 - 1;
+    float vrx = x_ndc * A.aspect * A.tanv;
+    float vry = y_ndc * A.tanv;
+    v3 csp = mk(vrx * view_z, vry * view_z, -view_z);
+    float4 nq = A.n[(size_t)y * A.w + x];
+    v3 n = normalize(mk(nq.x, nq.y, nq.z));
+    int16_t occ = 0;
+    for (int i = 0; i < A.count; i++) {
+        float rx = xs32(st) / (float)UINT32_MAX * 2 - 1;
+        float ry = xs32(st) / (float)UINT32_MAX * 2 - 1;
+        float rz = xs32(st) / (float)UINT32_MAX * 2 - 1;
+        v3 rs = normalize(mk(rx, ry, rz));
+        rs = rs * (xs32(st) / (float)UINT32_MAX + 0.0001f);
+        rs = rs * A.radius;
+        rs = rs + csp;
+        if (dot(rs - csp, n) < 0)
+            rs = rs + 2.0f * (csp - rs);
+        v3 ndc = xform_point(A.proj, rs);
+        int px = d2i((ndc.x + 1) * 0.5 * A.w);
+        int py = d2i((ndc.y + 1) * 0.5 * A.h);
+        px = px > 0 ? px : 0;
+        px = px < A.w - 1 ? px : A.w - 1;
+        py = py > 0 ? py : 0;
+        py = py < A.h - 1 ? py : A.h - 1;
+        float sgd = -A.z[(size_t)py * A.w + px];
+        if (fabsf(sgd - csp.z) > A.radius)
+            continue;
+        if (rs.z < sgd)
+            occ = (int16_t)(occ + 1);
+    }
+    return occ;
+}
+
+constexpr int SSAO_TX = 16, SSAO_TY = 16;   // 16x4-pixel waves: the sample gathers stay local
+
+__global__ __launch_bounds__(256) void ssao_occlusion_kernel(SsaoArgs A)
+{
+    int x = blockIdx.x * SSAO_TX + threadIdx.x, y = blockIdx.y * SSAO_TY + threadIdx.y;
+    if (x >= A.w || y >= A.h)
+        return;
+    size_t o = (size_t)y * A.w + x;
+    float view_z = A.z[o];
+    uint32_t st = ssao_state((uint32_t)o, A.seed);
+    A.ao[o] = x < A.simd_w ? ssao_simd_pixel(A, x, y, view_z, st) : ssao_scalar_pixel(A, x, y, view_z, st);
+}
+
+// 7x7 box blur of the counts (integer sums: separable in LDS, exact), applied to
+// the interior pixels with a hit: c * (1 - sum / 49 / count * amount) per channel,
+// written as QColor(int, int, int) -- an out-of-range channel makes the colour
+// invalid and QImage::setPixelColor leaves the pixel.
+constexpr int BLUR_X = 32, BLUR_Y = 8, BLUR_H = 3;
+
+__global__ __launch_bounds__(256) void ssao_blur_kernel(SsaoArgs A)
+{
+    __shared__ int tile[BLUR_Y + 2 * BLUR_H][BLUR_X + 2 * BLUR_H];
+    __shared__ int rows[BLUR_Y + 2 * BLUR_H][BLUR_X];
+    const int x0 = blockIdx.x * BLUR_X, y0 = blockIdx.y * BLUR_Y;
+    const int tid = threadIdx.y * BLUR_X + threadIdx.x;
+    constexpr int TW = BLUR_X + 2 * BLUR_H, TH = BLUR_Y + 2 * BLUR_H;
+    for (int i = tid; i < TW * TH; i += BLUR_X * BLUR_Y) {
+        int ly = i / TW, lx = i - ly * TW;
+        int gx = x0 + lx - BLUR_H, gy = y0 + ly - BLUR_H;
+        tile[ly][lx] = (gx >= 0 && gx < A.w && gy >= 0 && gy < A.h) ? A.ao[(size_t)gy * A.w + gx] : 0;
+    }
+    __syncthreads();
+    for (int i = tid; i < BLUR_X * TH; i += BLUR_X * BLUR_Y) {
+        int ly = i / BLUR_X, lx = i - ly * BLUR_X;
+        int s = 0;
+        for (int k = 0; k < 2 * BLUR_H + 1; k++) s += tile[ly][lx + k];
+        rows[ly][lx] = s;
+    }
+    __syncthreads();
+    int x = x0 + threadIdx.x, y = y0 + threadIdx.y;
+    if (x < BLUR_H || x >= A.w - BLUR_H || y < BLUR_H || y >= A.h - BLUR_H)
+        return;
+    size_t o = (size_t)y * A.w + x;
+    if (A.z[o] == INFINITY)
+        return;
+    int sum = 0;
+    for (int k = 0; k < 2 * BLUR_H + 1; k++) sum += rows[threadIdx.y + k][threadIdx.x];
+    const int bs = 2 * BLUR_H + 1;
+    float cm = 1 - ((float)sum / (float)(bs * bs) / (float)A.count * A.amount);
+    uint32_t p = A.argb[o];
+    int r = f2i((float)((p >> 16) & 0xff) * cm), g = f2i((float)((p >> 8) & 0xff) * cm), b = f2i((float)(p & 0xff) * cm);
+    if (r < 0 || r > 255 || g < 0 || g > 255 || b < 0 || b > 255)
+        return;
+    A.argb[o] = qrgb(r, g, b);
 }
 
 // ImageUtils::downscale_image_qt_ARGB32 (imageUtils.h:98-147): integer box
@@ -2286,5 +2490,20 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_raster_sha
         return hipSuccess;
     size_t lds = (size_t)(P->levels > 0 ? P->levels : 1) * rt::BLOCK * sizeof(uint2);
     hipLaunchKernelGGL(rt::raster_shade_kernel, dim3(blocks), dim3(rt::BLOCK), lds, stream, *P, *A, fr1, nfr1);
+    return hipGetLastError();
+}
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ssao(const rt::SsaoArgs* A, hipStream_t stream)
+{
+    if (A->w <= 0 || A->h <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(rt::ssao_occlusion_kernel,
+                       dim3((A->w + rt::SSAO_TX - 1) / rt::SSAO_TX, (A->h + rt::SSAO_TY - 1) / rt::SSAO_TY),
+                       dim3(rt::SSAO_TX, rt::SSAO_TY), 0, stream, *A);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return e;
+    hipLaunchKernelGGL(rt::ssao_blur_kernel, dim3((A->w + rt::BLUR_X - 1) / rt::BLUR_X, (A->h + rt::BLUR_Y - 1) / rt::BLUR_Y),
+                       dim3(rt::BLUR_X, rt::BLUR_Y), 0, stream, *A);
     return hipGetLastError();
 }

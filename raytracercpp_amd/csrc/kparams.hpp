@@ -77,6 +77,26 @@ struct KParams {
     float* hit_t;
     uint8_t* shadow;
     unsigned long long* counters;   // [0] shadow rays, [1] reflection rays, [2] tile queue head
+    // SSAO inputs (enable_ssao): Renderer::_z_buffer / _normal_buffer, renderer.cpp:1107-1110, 975-979
+    float* zbuf;
+    float4* nbuf;
+};
+
+// ---- SSAO (kernels.hip "Renderer::post_process_ssao_SIMD") ----
+struct SsaoArgs {
+    const float* z;          // _z_buffer, INFINITY where nothing was hit
+    const float4* n;         // _normal_buffer (xyz)
+    int32_t* ao;             // per-pixel occlusion counts
+    uint32_t* argb;          // the internal image, blurred occlusion applied in place
+    int32_t w, h;            // render size
+    int32_t simd_w;          // w - w % 8: columns of the 8-lane loop; the rest take the scalar tail
+    int32_t count;           // ssao_sample_count
+    float radius, amount;    // ssao_radius, ssao_amount
+    float fovm;              // (float)tan(fov / 2 / 180 * M_PI), renderer.cpp:1245 (double tan)
+    float tanv;              // tanf(radians(fov / 2)), renderer.cpp:1379
+    float aspect;            // Camera::_aspect_ratio
+    uint32_t seed;
+    float proj[16];          // Camera::_perspective_proj_mat
 };
 
 // ---- reflection engine (kernels.hip, "Reflections as frames") ----

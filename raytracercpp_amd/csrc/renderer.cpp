@@ -29,6 +29,7 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_raster_sha
                                                                             const rt::RasterArgs* A,
                                                                             rt::FrameRec* fr1, unsigned int* nfr1,
                                                                             hipStream_t stream);
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ssao(const rt::SsaoArgs* A, hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_downscale(const uint32_t* in, int w, int h_rows, int f, uint32_t* out,
                                           hipStream_t stream);
 
@@ -91,7 +92,8 @@ int Renderer::init(std::string& err)
     }
     DevBuf* all[] = {&d_nodes_, &d_tris_,  &d_tri_id_, &d_tri_mat_, &d_tri_uv_, &d_mats_,   &d_internal_,
                      &d_image_, &d_rgba_,  &d_hit_id_, &d_hit_t_,   &d_shadow_, &d_counters_, &d_band_tmp_,
-                     &d_tri9_,  &d_rcount_, &d_roff_,  &d_pieces_,  &d_piece_uv_, &d_zkey_, &d_big_, &d_scan_tmp_};
+                     &d_tri9_,  &d_rcount_, &d_roff_,  &d_pieces_,  &d_piece_uv_, &d_zkey_, &d_big_, &d_scan_tmp_,
+                     &d_zbuf_,  &d_nbuf_,   &d_ao_};
     for (DevBuf* b : all) b->device = device_;
     for (auto& b : d_tex_) b.device = device_;
     for (auto& b : d_sky_) b.device = device_;
@@ -136,8 +138,6 @@ void Renderer::update_camera_projection()
 
 int Renderer::set_settings(const rt_settings& s)
 {
-    if (s.enable_ssao)
-        return fail(RT_EUNSUPPORTED, "enable_ssao: SSAO post-processing is out of scope (stubbed)");
     if (s.image_width <= 0 || s.image_height <= 0 || (s.enable_ssaa && s.ssaa_factor <= 0))
         return fail(RT_EINVAL, "invalid image size / ssaa_factor");
     if (s.bvh_max_depth > 30)
@@ -281,6 +281,13 @@ int Renderer::set_camera_matrices(const float pos[3], const float proj_inv[16], 
     std::memcpy(proj_inv_, proj_inv, sizeof(proj_inv_));
     std::memcpy(c2w_, c2w, sizeof(c2w_));
     mat::inverse(c2w_, w2c_);
+    return RT_OK;
+}
+
+int Renderer::set_camera_lens(float fov, float aspect)
+{
+    fov_ = fov;
+    aspect_ = aspect;
     return RT_OK;
 }
 
@@ -551,7 +558,7 @@ void Renderer::fill_params(KParams& P) const
     P.has_reflection = s_.shading_method == RT_SHADING && any_reflection(mats_);
     // RT_PIPELINE=1 selects the per-lane pipelined kernel instead of the tile-per-wave one (A/B runs)
     const char* pipe_env = getenv("RT_PIPELINE");
-    P.pipeline = pipe_env && pipe_env[0] == '1';
+    P.pipeline = pipe_env && pipe_env[0] == '1' && !s_.enable_ssao;
     P.max_blocks = num_cus_ * 8;
     render_size(P.rw, P.rh);
 }
@@ -801,6 +808,10 @@ int Renderer::trace_frame()
     if (want_hit_ && ((e = d_hit_id_.reserve(npx * 4)) != hipSuccess || (e = d_hit_t_.reserve(npx * 4)) != hipSuccess))
         return hip_fail(e, "hipMalloc (hit)");
     if (want_shadow_ && (e = d_shadow_.reserve(npx)) != hipSuccess) return hip_fail(e, "hipMalloc (shadow)");
+    if (s_.enable_ssao && ((e = d_zbuf_.reserve(npx * 4)) != hipSuccess || (e = d_nbuf_.reserve(npx * 16)) != hipSuccess))
+        return hip_fail(e, "hipMalloc (z / normal buffers)");
+    P.zbuf = s_.enable_ssao ? d_zbuf_.as<float>() : nullptr;
+    P.nbuf = s_.enable_ssao ? d_nbuf_.as<float4>() : nullptr;
     P.band_rows = P.rh;
     P.nranks = 1;
     P.rank = 0;
@@ -830,6 +841,7 @@ int Renderer::trace_frame()
     img_is_internal_ = true;
     rendered_ = true;
     aux_valid_ = true;
+    ssao_ready_ = s_.enable_ssao;
     post_ms_ = 0;
     return RT_OK;
 }
@@ -839,25 +851,93 @@ int Renderer::post_process()
 {
     if (!rendered_)
         return fail(RT_ESTATE, "post_process before ray_trace");
-    if (!s_.enable_ssaa || !img_is_internal_)
+    if (!img_is_internal_)
+        return RT_OK;
+    hipError_t e = hipSetDevice(device_);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    post_ms_ = 0;
+    if (s_.enable_ssao) {
+        if (!ssao_ready_)
+            return fail(RT_ESTATE, "post_process: enable_ssao but the last frame was rendered without it");
+        int rc = launch_ssao();
+        if (rc != RT_OK)
+            return rc;
+    }
+    if (!s_.enable_ssaa)
         return RT_OK;
     int f = s_.ssaa_factor;
     if (img_w_ % f != 0 || img_h_ % f != 0)
         return RT_OK;   // downscale_image_qt_ARGB32 prints and leaves the output untouched
-    hipError_t e = hipSetDevice(device_);
     int dw = img_w_ / f, dh = img_h_ / f;
-    if (e == hipSuccess) e = d_image_.reserve((size_t)dw * dh * 4);
-    if (e != hipSuccess) return hip_fail(e, "hipMalloc (ssaa)");
+    if ((e = d_image_.reserve((size_t)dw * dh * 4)) != hipSuccess) return hip_fail(e, "hipMalloc (ssaa)");
     hipEventRecord(ev_[2], stream_);
     if ((e = rt_launch_downscale(d_internal_.as<uint32_t>(), img_w_, img_h_, f, d_image_.as<uint32_t>(), stream_)) !=
         hipSuccess)
         return hip_fail(e, "downscale launch");
     hipEventRecord(ev_[3], stream_);
     if ((e = hipStreamSynchronize(stream_)) != hipSuccess) return hip_fail(e, "downscale");
-    hipEventElapsedTime(&post_ms_, ev_[2], ev_[3]);
+    float ms = 0;
+    hipEventElapsedTime(&ms, ev_[2], ev_[3]);
+    post_ms_ += ms;
     img_w_ = dw;
     img_h_ = dh;
     img_is_internal_ = false;
+    return RT_OK;
+}
+
+// Renderer::post_process_ssao_SIMD (renderer.cpp:1229-1434) on the internal image,
+// from the z / normal buffers of the last frame.  The two tangents come from the
+// host libm exactly as the reference evaluates them: the SIMD loop's double tan
+// (renderer.cpp:1245) and the scalar tail's tanf(radians(fov / 2)) (:1379).
+int Renderer::launch_ssao()
+{
+    hipError_t e;
+    size_t npx = (size_t)img_w_ * img_h_;
+    if ((e = d_ao_.reserve(npx * 4)) != hipSuccess) return hip_fail(e, "hipMalloc (ssao)");
+    SsaoArgs A;
+    std::memset(&A, 0, sizeof(A));
+    A.z = d_zbuf_.as<float>();
+    A.n = d_nbuf_.as<float4>();
+    A.ao = d_ao_.as<int32_t>();
+    A.argb = d_internal_.as<uint32_t>();
+    A.w = img_w_;
+    A.h = img_h_;
+    A.simd_w = img_w_ - img_w_ % 8;
+    A.count = s_.ssao_sample_count;
+    A.radius = s_.ssao_radius;
+    A.amount = s_.ssao_amount;
+    const double pi = 3.14159265358979323846;
+    A.fovm = (float)std::tan(fov_ / 2 / 180 * pi);
+    A.tanv = std::tan(((float)pi / 180) * (fov_ / 2));
+    A.aspect = aspect_;
+    A.seed = s_.rng_seed;
+    std::memcpy(A.proj, proj_, sizeof(A.proj));
+    hipEventRecord(ev_[2], stream_);
+    if ((e = rt_launch_ssao(&A, stream_)) != hipSuccess) return hip_fail(e, "ssao launch");
+    hipEventRecord(ev_[3], stream_);
+    if ((e = hipStreamSynchronize(stream_)) != hipSuccess) return hip_fail(e, "ssao");
+    float ms = 0;
+    hipEventElapsedTime(&ms, ev_[2], ev_[3]);
+    post_ms_ += ms;
+    return RT_OK;
+}
+
+int Renderer::get_ssao_buffers(float* z, float* n4, int32_t* ao)
+{
+    if (!ssao_ready_)
+        return fail(RT_ESTATE, "get_ssao_buffers: the last frame was rendered without enable_ssao");
+    hipSetDevice(device_);
+    int rw, rh;
+    render_size(rw, rh);
+    size_t n = (size_t)rw * rh;
+    hipError_t e = hipSuccess;
+    if (z) e = hipMemcpy(z, d_zbuf_.p, n * 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && n4) e = hipMemcpy(n4, d_nbuf_.p, n * 16, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && ao) {
+        if (d_ao_.bytes < n * 4) return fail(RT_ESTATE, "get_ssao_buffers: no SSAO pass yet (post_process)");
+        e = hipMemcpy(ao, d_ao_.p, n * 4, hipMemcpyDeviceToHost);
+    }
+    if (e != hipSuccess) return hip_fail(e, "get_ssao_buffers");
     return RT_OK;
 }
 
@@ -950,6 +1030,8 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
     int lrows = local_rows(band_rows, rank, nranks);
     if (lrows < 0 || !d_out)
         return fail(RT_EINVAL, "render_bands_device: bad band layout");
+    if (s_.enable_ssao)   // its samples and 7x7 blur read across bands
+        return fail(RT_EUNSUPPORTED, "render_bands_device: SSAO needs the whole frame (use rt_render)");
     if (validate() != RT_OK)
         return fail(RT_EINVAL, "invalid scene: material index out of range or enabled texture map missing");
     if (check_frame() != RT_OK)

@@ -56,6 +56,8 @@ public:
     void get_camera_matrices(float pos[3], float proj_inv[16], float c2w[16]) const;
     // Camera::_perspective_proj_mat / _world_to_camera_mat as the caller computed them (raster path)
     int set_camera_projection(const float proj[16], const float w2c[16]);
+    // Camera::_fov / _aspect_ratio as the caller holds them (read by SSAO), matrices untouched
+    int set_camera_lens(float fov, float aspect);
     int set_object_transform(const float m[16]);
     int reset_previous_transform();
     int set_texture(int slot, int w, int h, const float* rgba);
@@ -68,6 +70,8 @@ public:
     int raster_trace();
     int post_process();
     int get_image(uint32_t* argb, int32_t* w, int32_t* h);
+    // diagnostics: _z_buffer, _normal_buffer (xyz + pad) and the last SSAO pass's counts
+    int get_ssao_buffers(float* z, float* n4, int32_t* ao);
     int request_aux(bool rgba, bool hit, bool shadow);
     int get_internal(uint32_t* argb, float* rgba, int32_t* hit_id, float* hit_t, uint8_t* shadow);
     int get_stats(rt_stats* out) const;
@@ -103,6 +107,7 @@ private:
         return s_.hybrid_rasterization_tracing ? launch_raster(P, stream) : launch_trace(P, stream);
     }
     int check_frame() const;
+    int launch_ssao();
     int trace_frame();
     int refl_level(const KParams& P, int level, int nframes, hipStream_t stream);
 
@@ -137,6 +142,9 @@ private:
     DevBuf d_nodes_, d_tris_, d_tri_id_, d_tri_mat_, d_tri_uv_, d_mats_;
     DevBuf d_tex_[TEX_SLOTS], d_sky_[6];
     DevBuf d_internal_, d_image_, d_rgba_, d_hit_id_, d_hit_t_, d_shadow_, d_counters_, d_band_tmp_;
+    // SSAO: _z_buffer, _normal_buffer (float4) and the occlusion counts of the internal image
+    DevBuf d_zbuf_, d_nbuf_, d_ao_;
+    bool ssao_ready_ = false;   // the buffers hold the last frame's z / normals
     // raster path: caller-order triangles, per-triangle piece counts / offsets, the piece
     // table and its texcoords, the z-key buffer, the big-piece list, scan scratch
     DevBuf d_tri9_, d_rcount_, d_roff_, d_pieces_, d_piece_uv_, d_zkey_, d_big_, d_scan_tmp_;

@@ -135,6 +135,10 @@ class Renderer:
         pr, wc = f32(proj), f32(world_to_cam)
         self._call("rt_set_camera_projection", ptr(pr, _f32p), ptr(wc, _f32p))
 
+    def set_camera_lens(self, fov: float, aspect: float):
+        """Camera::_fov / _aspect_ratio without touching the matrices (read by SSAO)."""
+        self._call("rt_set_camera_lens", float(fov), float(aspect))
+
     def get_camera_matrices(self):
         pos, pi, cw = np.zeros(3, np.float32), np.zeros(16, np.float32), np.zeros(16, np.float32)
         self._call("rt_get_camera_matrices", ptr(pos, _f32p), ptr(pi, _f32p), ptr(cw, _f32p))
@@ -221,6 +225,16 @@ class Renderer:
                 out[k] = v
         return out
 
+    def get_ssao_buffers(self, ao=True):
+        """(z, normals (n, 3), occlusion counts or None) of the last frame / SSAO pass."""
+        st = self.stats()
+        n = st["render_width"] * st["render_height"]
+        z = np.zeros(n, np.float32)
+        n4 = np.zeros((n, 4), np.float32)
+        a = np.zeros(n, np.int32) if ao else None
+        self._call("rt_get_ssao_buffers", ptr(z, _f32p), ptr(n4, _f32p), ptr(a, _i32p))
+        return z, np.ascontiguousarray(n4[:, :3]), a
+
     def stats(self) -> dict:
         s = RtStats()
         self._call("rt_get_stats", C.byref(s))
@@ -266,6 +280,7 @@ class Renderer:
         self.set_camera_matrices(sc.cam_pos, sc.proj_inv, sc.cam_to_world)
         if sc.proj is not None and sc.world_to_cam is not None:
             self.set_camera_projection(sc.proj, sc.world_to_cam)
+        self.set_camera_lens(*sc.lens(st))
         self.set_light_position(sc.light)
         self.set_materials(sc.materials)
         self.clear_geometry()

@@ -48,12 +48,19 @@ def test_gpu_matches_reference_golden(R, name):
     st = R.stats()
     assert st["shadow_rays"] == c.meta["counters"]["shadow_rays"]
     assert st["reflection_rays"] == c.meta["counters"]["reflection_rays"]
+    if c.settings.enable_ssao:
+        z, n, _ = R.get_ssao_buffers(ao=False)
+        assert np.array_equal(bits(z), bits(exp["zbuf"]))
+        assert np.array_equal(bits(n), bits(exp["nbuf"]))
     R.post_process()
     img = R.get_image().ravel()
+    if c.settings.enable_ssao:
+        _, _, ao = R.get_ssao_buffers()
+        assert np.array_equal(ao, exp["ao"]), f"{int((ao != exp['ao']).sum())} occlusion-count mismatches"
     if c.settings.enable_ssaa:
         assert np.array_equal(img, exp["final"])
     else:
-        assert np.array_equal(img, exp["argb"])
+        assert np.array_equal(img, exp["ssao"] if c.settings.enable_ssao else exp["argb"])
 
 
 @pytest.mark.parametrize("name", [n for n in CASES if manifest()[n]["row_samples"]])
@@ -374,3 +381,54 @@ def test_raster_errors_and_dispatch(R):
     R.load_scene(sc, st)
     with pytest.raises(RtError):
         R.raster_trace()
+
+
+@pytest.mark.parametrize("raster,w,h,kw", [
+    (False, 331, 187, dict(ssao_sample_count=32, ssao_radius=0.4)),
+    (False, 160, 90, dict(ssao_sample_count=16, ssao_radius=0.7, enable_ssaa=True, ssaa_factor=2,
+                          enable_normal_mapping=True)),
+    (True, 245, 131, dict(ssao_sample_count=24, ssao_radius=0.5, ssao_amount=0.8)),
+])
+def test_ssao_matches_oracle(R, raster, w, h, kw):
+    """post_process_ssao_SIMD on the GPU (occlusion kernel + LDS blur) against the oracle,
+    bit-exact: z / normal buffers, per-pixel counts, the internal and the final image."""
+    from raytracercpp_amd import scenes
+    if kw.get("enable_normal_mapping"):
+        # C5 features: normal-mapped buffers, reflective hits through the frame engine's level 0
+        sc, st = scenes.sphere1m_refl(width=w, height=h, samples=2)
+        st = st.copy(enable_ssao=True, max_recursion_depth=3, **kw)
+    else:
+        sc, st = scenes.bumpy70k(width=w, height=h, enable_ssao=True, hybrid_rasterization_tracing=raster, **kw)
+    o = Oracle(sc, st)
+    ref = o.raster() if raster else o.render_rows()
+    ref_img, ref_ao = o.ssao(ref)
+    g = gpu_render(R, sc, st, aux=False)
+    assert np.array_equal(g["argb"], ref.argb)
+    z, n, _ = R.get_ssao_buffers(ao=False)
+    assert np.array_equal(bits(z), bits(ref.zbuf))
+    assert np.array_equal(bits(n), bits(ref.nbuf))
+    R.post_process()
+    _, _, ao = R.get_ssao_buffers()
+    assert ref_ao.max() > 0
+    assert np.array_equal(ao, ref_ao), f"{int((ao != ref_ao).sum())} occlusion-count mismatches"
+    img = R.get_image().ravel()
+    if st.enable_ssaa:
+        rw, rh = st.render_size()
+        ref_img = Oracle.downscale(ref_img, rw, rh, st.ssaa_factor)
+    assert np.array_equal(img, ref_img)
+
+
+def test_ssao_errors(R):
+    """SSAO needs the whole frame: band rendering refuses it; post_process refuses stale buffers."""
+    import torch
+    from raytracercpp_amd import scenes
+    from raytracercpp_amd._lib import RtError
+    sc, st = scenes.bumpy70k(width=64, height=40)
+    R.load_scene(sc, st)
+    R.ray_trace()
+    R.set_render_settings(st.copy(enable_ssao=True))
+    with pytest.raises(RtError):
+        R.post_process()   # the frame was traced without z / normal buffers
+    out = torch.empty((R.local_rows(8, 0, 1), 64), dtype=torch.int32, device="cuda")
+    with pytest.raises(RtError):
+        R.render_bands_device(8, 0, 1, out.data_ptr())
