@@ -88,6 +88,8 @@ typedef struct rt_stats {
     int64_t octree_inner, octree_leaves, octree_empty_leaves, octree_max_leaf, octree_max_depth;
     int64_t gpu_nodes, gpu_tris;
     int32_t render_width, render_height;
+    float seg_scale;           /* scene scale of the last frame's segment queries (kernels.hip seg_margin);
+                                  0: shadow / reflection queries walked the whole line */
 } rt_stats;
 
 typedef struct rt_renderer rt_renderer;

@@ -53,7 +53,7 @@ class RtStats(C.Structure):
         ("octree_inner", C.c_int64), ("octree_leaves", C.c_int64), ("octree_empty_leaves", C.c_int64),
         ("octree_max_leaf", C.c_int64), ("octree_max_depth", C.c_int64),
         ("gpu_nodes", C.c_int64), ("gpu_tris", C.c_int64),
-        ("render_width", C.c_int32), ("render_height", C.c_int32),
+        ("render_width", C.c_int32), ("render_height", C.c_int32), ("seg_scale", C.c_float),
     ]
 
     def as_dict(self):

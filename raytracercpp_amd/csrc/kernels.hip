@@ -40,6 +40,7 @@ struct TRay {
     v3 o, d;
     float den[NPLANES], num[NPLANES];   // num[i] = NaN where den[i] == 0 (see vol_test)
     bool nan;
+    float lo, hi;   // query segment of a SEG traversal (seg_margin): volumes outside [lo, hi] are not entered
 };
 
 
@@ -78,6 +79,8 @@ __device__ __forceinline__ TRay make_ray(const KParams& P, v3 o, v3 d)
             R.num[i] = __int_as_float(0x7fc00000);
     }
     R.nan = nan;
+    R.lo = -INFINITY;
+    R.hi = INFINITY;
     return R;
 }
 
@@ -120,6 +123,9 @@ __device__ __forceinline__ uint2 load_node_link(const GNode* nodes, uint32_t i)
 //    fmaxf / fminf keep the running bound, as std::max / std::min do.
 // fmaxf / fminf differ from std::max / std::min only in the sign of a zero
 // result, which no comparison sees.
+// SEG (segment queries): a volume that passes but lies
+// wholly outside [R.lo, R.hi] is treated as missed.
+template <bool SEG = false>
 __device__ __forceinline__ bool vol_test(const NodeBox& n, const TRay& R, float& t_near_out)
 {
     float t_near = -INFINITY, t_far = INFINITY;
@@ -131,6 +137,8 @@ __device__ __forceinline__ bool vol_test(const NodeBox& n, const TRay& R, float&
         t_far = fminf(t_far, fmaxf(d0, d1));
     }
     t_near_out = t_near;
+    if (SEG)
+        return !(t_far < t_near) & !(t_far < R.lo) & !(t_near > R.hi);
     return !(t_far < t_near);
 }
 
@@ -282,6 +290,7 @@ struct Trav {
     bool r, live;
 };
 
+template <bool SEG = false>
 __device__ __forceinline__ void trav_begin(const KParams& P, const TRay& R, THit& h, Trav& T)
 {
     h.t = -1.0f;
@@ -301,7 +310,7 @@ __device__ __forceinline__ void trav_begin(const KParams& P, const TRay& R, THit
     }
     float tn;
     NodeBox nb = load_node(P.nodes, 0);
-    if (!vol_test(nb, R, tn))
+    if (!vol_test<SEG>(nb, R, tn))
         return;
     T.a = nb.a;
     T.b = nb.b;
@@ -310,6 +319,7 @@ __device__ __forceinline__ void trav_begin(const KParams& P, const TRay& R, THit
     T.live = true;
 }
 
+template <bool SEG = false>
 __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit& h, Trav& T, uint2* lv)
 {
     uint32_t a = T.a, b = T.b;
@@ -342,7 +352,7 @@ __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit&
             if ((uint32_t)j < k) {
                 NodeBox c = load_node(P.nodes, a + j);
                 float t;
-                if (vol_test(c, R, t))
+                if (vol_test<SEG>(c, R, t))
                     key[j] = t;
             }
         }
@@ -435,24 +445,57 @@ __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit&
     T.any_true = any_true;
 }
 
+template <bool SEG = false>
 __device__ bool bvh_closest(const KParams& P, const TRay& R, THit& h, uint2* lv)
 {
     Trav T;
-    trav_begin(P, R, h, T);
+    trav_begin<SEG>(P, R, h, T);
 #if RT_WW
     // while-while: lanes at inner nodes keep expanding until every lane of the
     // wave sits on a leaf (or is done), then the leaves are tested together
     while (T.live) {
         while (T.live && !(T.b & LEAF_BIT))
-            trav_step(P, R, h, T, lv);
+            trav_step<SEG>(P, R, h, T, lv);
         if (T.live)
-            trav_step(P, R, h, T, lv);
+            trav_step<SEG>(P, R, h, T, lv);
     }
 #else
     while (T.live)
-        trav_step(P, R, h, T, lv);
+        trav_step<SEG>(P, R, h, T, lv);
 #endif
     return T.r;
+}
+
+// Segment queries.  A shadow query's answer depends only on
+// hits in front of its origin and not beyond the light; a reflection sample's closest
+// hit only on hits in front of its origin.  Under the assumption the reference's own
+// early-out makes (bvh.h:270: a triangle's hit t lies inside its volumes' [t_near,
+// t_far]), a volume wholly outside the query segment holds no hit that changes the
+// query-global record or the root's return value, so it need not be entered.  The
+// segment is widened on both sides by seg_margin, a bound on the rounding of a k-DOP
+// quotient and of a Moller-Trumbore t in a scene of scale P.seg_scale.  Queries that
+// end with the record at t == 0, +inf or NaN (where the reference's return value
+// depends on the leaves visited) are re-run over the whole line.
+__device__ __forceinline__ float seg_margin(const KParams& P, const TRay& R)
+{
+    float dmin = INFINITY;
+#pragma unroll
+    for (int i = 0; i < NPLANES; i++)
+        if (R.den[i] != 0.0f)
+            dmin = fminf(dmin, fabsf(R.den[i]));
+    float om = fmaxf(fabsf(R.o.x), fmaxf(fabsf(R.o.y), fabsf(R.o.z)));
+    return 0x1p-8f * P.seg_scale + 0x1p-14f * (P.seg_scale + om) / dmin;
+}
+
+__device__ __forceinline__ bool bvh_closest_seg(const KParams& P, TRay& R, THit& h, uint2* lv)
+{
+    bool r = bvh_closest<true>(P, R, h, lv);
+    if (h.k >= 0 && !(h.t > 0.0f && h.t < INFINITY)) {
+        R.lo = -INFINITY;
+        R.hi = INFINITY;
+        r = bvh_closest<true>(P, R, h, lv);
+    }
+    return r;
 }
 
 // HitInfo filled by Triangle::intersect for slot k (triangle.cpp:81-88)
@@ -695,7 +738,16 @@ __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
     THit h;
     bool r;
     if (P.enable_bvh) {
-        r = bvh_closest(P, R, h, lv);
+        if (P.seg_scale > 0.0f) {
+            // segment [-m, past the light]: a hit beyond hi fails the distance test below
+            // (|p - q| >= t - |n| * 1e-4), one behind the origin does not exist (t >= 0)
+            float m = seg_margin(P, R);
+            float nl = fabsf(n.x) + fabsf(n.y) + fabsf(n.z);
+            R.lo = -m;
+            R.hi = (sqrtf(length2(p - lp)) + 1.0e-4f * nl) * (1.0f + 0x1p-10f) + m;
+            r = bvh_closest_seg(P, R, h, lv);
+        } else
+            r = bvh_closest(P, R, h, lv);
         if (r) {
             v3 q = o + d * h.t;
             if (length2(p - q) < length2(p - lp))
@@ -1570,7 +1622,12 @@ __global__ __launch_bounds__(BLOCK) void refl_trace_kernel(KParams P, ReflArgs A
     const FrameRec& F = A.fr[A.order[A.c0 + slot / A.stride]];
     TRay R = make_ray(P, ld3(F.ro), ld3(A.sm[slot].d));
     THit h;
-    bool r = bvh_closest(P, R, h, lv);
+    bool r;
+    if (P.seg_scale > 0.0f) {
+        R.lo = -seg_margin(P, R);   // nothing behind the origin can be hit (t >= 0)
+        r = bvh_closest_seg(P, R, h, lv);
+    } else
+        r = bvh_closest(P, R, h, lv);
     RawHit H;
     H.t = h.t;
     H.u = h.u;

@@ -61,6 +61,8 @@ struct KParams {
     uint32_t rng_seed;
     int32_t has_reflection;   // RT_SHADING with a material whose reflection > 0: recursive kernel
     int32_t pipeline;         // per-lane pipelined kernel for the non-recursive case (RT_PIPELINE=1; default 0)
+    float seg_scale;          // > 0: shadow / reflection queries are segment queries (kernels.hip seg_margin),
+                              // the scene's largest |coordinate|; 0: every query walks the whole line
 
     // image: render size (internal, after the SSAA factor) and this launch's rows
     int32_t rw, rh;

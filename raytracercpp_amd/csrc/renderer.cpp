@@ -559,6 +559,20 @@ void Renderer::fill_params(KParams& P) const
     // RT_PIPELINE=1 selects the per-lane pipelined kernel instead of the tile-per-wave one (A/B runs)
     const char* pipe_env = getenv("RT_PIPELINE");
     P.pipeline = pipe_env && pipe_env[0] == '1' && !s_.enable_ssao;
+    // segment queries (RT_SEG=0 turns them off): only when the
+    // queries' results depend on the triangles alone (analytic shapes read the stale
+    // record) and the scene's scale keeps Moller-Trumbore's products far from overflow
+    // and underflow, so that the rounding bound of seg_margin holds
+    P.seg_scale = 0.0f;
+    const char* seg_env = getenv("RT_SEG");
+    if (!(seg_env && seg_env[0] == '0') && P.nshape == 0 && !oct_.nodes.empty()) {
+        const GNode& root = oct_.nodes[0];
+        float S = 0.0f;
+        for (int a = 0; a < 3; a++)   // the axis slabs are the vertices' coordinate range
+            S = std::max(S, std::max(std::fabs(root.dn[a]), std::fabs(root.df[a])));
+        if (S > 0x1p-20f && S < 0x1p20f)
+            P.seg_scale = S;
+    }
     P.max_blocks = num_cus_ * 8;
     render_size(P.rw, P.rh);
 }
@@ -800,6 +814,7 @@ int Renderer::trace_frame()
         return rc;
     KParams P;
     fill_params(P);
+    last_seg_ = P.seg_scale;
     size_t npx = (size_t)P.rw * P.rh;
     hipError_t e;
     if ((e = d_internal_.reserve(npx * 4)) != hipSuccess || (e = d_counters_.reserve(64)) != hipSuccess)
@@ -1013,6 +1028,7 @@ int Renderer::get_stats(rt_stats* out) const
     out->gpu_nodes = (int64_t)oct_.nodes.size();
     out->gpu_tris = (int64_t)oct_.tris.size();
     render_size(out->render_width, out->render_height);
+    out->seg_scale = last_seg_;
     return RT_OK;
 }
 
@@ -1044,6 +1060,7 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
         stream = stream_;
     KParams P;
     fill_params(P);
+    last_seg_ = P.seg_scale;
     int f = s_.enable_ssaa ? s_.ssaa_factor : 1;
     P.band_rows = band_rows * f;
     P.nranks = nranks;

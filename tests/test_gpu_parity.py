@@ -109,6 +109,7 @@ def test_c4_full_frame_matches_oracle(R):
     rw, rh = st.render_size()
     assert np.array_equal(R.get_image().ravel(), Oracle.downscale(o.argb, rw, rh, 2))
     assert R.stats()["shadow_rays"] == o.counters["shadow_rays"]
+    assert R.stats()["seg_scale"] > 0   # the shadow queries ran as segment queries
 
 
 def _random_rays(rng, n, center, spread):
@@ -432,3 +433,78 @@ def test_ssao_errors(R):
     out = torch.empty((R.local_rows(8, 0, 1), 64), dtype=torch.int32, device="cuda")
     with pytest.raises(RtError):
         R.render_bands_device(8, 0, 1, out.data_ptr())
+
+
+@pytest.mark.parametrize("name", ["c2_cube", "robot", "c3_bumpy70k", "mirror", "rough", "textured", "raster_rough"])
+def test_whole_line_queries_match_reference_golden(R, name, monkeypatch):
+    """RT_SEG=0: shadow and reflection queries walk the whole line as the reference does
+    (no segment culling); the framebuffer is the same."""
+    if name not in CASES:
+        pytest.skip(f"no golden case {name}")
+    c = Case(name)
+    exp = c.expected()
+    monkeypatch.setenv("RT_SEG", "0")
+    g = gpu_render(R, c.scene, c.settings)
+    assert R.stats()["seg_scale"] == 0
+    monkeypatch.delenv("RT_SEG")
+    assert np.array_equal(g["hit_id"], exp["hit_id"])
+    assert np.array_equal(bits(g["hit_t"]), bits(exp["hit_t"]))
+    assert np.array_equal(g["shadow"], exp["shadow"])
+    assert np.array_equal(g["argb"], exp["argb"])
+    assert float(np.abs(g["rgba"] - exp["rgba"]).max()) <= RGBA_TOL
+
+
+def _soup_scene(rng, n=4000):
+    """Random triangles in front of the camera -- a third of them slivers (nearly collinear
+    vertices), some degenerate (a repeated vertex) -- over a tessellated ground plane y = -1.5."""
+    from raytracercpp_amd import scenes
+    from raytracercpp_amd.scene import SceneData, empty_shapes
+    base, st = scenes.bumpy70k(width=8, height=8)
+    c = rng.uniform([-2.0, -1.4, -7.0], [2.0, 1.5, -2.5], (n, 3))
+    e1 = rng.normal(size=(n, 3)) * 0.25
+    e2 = rng.normal(size=(n, 3)) * 0.25
+    sl = rng.random(n) < 0.33
+    e2[sl] = e1[sl] * rng.uniform(0.5, 2.0, (int(sl.sum()), 1)) + rng.normal(size=(int(sl.sum()), 3)) * 1e-6
+    dg = rng.random(n) < 0.05
+    e2[dg] = e1[dg]
+    soup = np.concatenate([c, c + e1, c + e2], axis=1)
+    g = np.linspace(-6.0, 6.0, 25)
+    ground = []
+    for i in range(24):
+        for k in range(24):
+            a, b = (g[i], -1.5, g[k] - 6), (g[i + 1], -1.5, g[k] - 6)
+            cc, d = (g[i + 1], -1.5, g[k + 1] - 6), (g[i], -1.5, g[k + 1] - 6)
+            ground += [a + d + cc, a + cc + b]   # facing +y
+    tri = np.concatenate([soup, np.array(ground)], axis=0).astype(np.float32)
+    sc = SceneData(**{**vars(base), "tri": tri, "tri_mat": np.zeros(len(tri), np.int32), "tri_uv": None})
+    sc.shape_kind, sc.shape, sc.shape_mat = empty_shapes()
+    return sc, st
+
+
+@pytest.mark.parametrize("scene_name,light", [
+    ("soup", (3.0, 3.0, 2.0)), ("soup", (0.0, 0.0, -4.5)), ("soup", (60.0, -1.4999, -4.0)),
+    ("soup", (30.0, -1.5, -4.0)), ("voxels", (3.0, 3.0, 2.0)), ("voxels", (0.01, 0.02, 0.03)),
+    ("voxels", (0.3, 0.0, 0.0)),
+])
+def test_segment_queries_match_oracle(R, scene_name, light):
+    """Segment-culled shadow queries against the oracle's whole-line traversal
+    on scenes built to stress the culling margins: slivers and degenerate triangles, lights
+    inside the geometry, a light grazing (and one exactly in) a tessellated ground plane,
+    axis-aligned voxels whose k-DOP slabs coincide."""
+    from raytracercpp_amd.scene import empty_shapes
+    rng = np.random.default_rng(11)
+    if scene_name == "soup":
+        sc, st = _soup_scene(rng)
+        st = st.copy(image_width=240, image_height=160)
+    else:
+        sc = _voxel_scene(n=6)
+        sc.shape_kind, sc.shape, sc.shape_mat = empty_shapes()
+        from raytracercpp_amd import scenes
+        _, st = scenes.bumpy70k(width=240, height=160)
+        st = st.copy(bvh_leaf_object_count=8)
+    sc.light = np.asarray(light, np.float32)
+    o = Oracle(sc, st).render_rows()
+    g = gpu_render(R, sc, st)
+    assert R.stats()["seg_scale"] > 0
+    assert int(o.shadow.sum()) > 0
+    _check_vs_oracle(g, o, f"{scene_name} {light}", R=R)
