@@ -167,6 +167,17 @@ def main():
                                "frac": round(achieved / PEAK_HBM_GBS, 4),
                                "traffic": int(traffic) if traffic else None,
                                "algorithmic_bytes_per_frame": nbytes}
+            # the same byte model over the tests the kernel actually executes (segment queries
+            # enter fewer volumes than the reference's whole-line walk): RT_COUNT=1 build counts,
+            # tools/count_gpu_work.py -> profiles/work_counts.json "gpu_executed"
+            ex = counts.get("gpu_executed") if os.environ.get("RT_SEG", "1") != "0" else \
+                counts.get("gpu_executed_whole_line")
+            if ex:
+                xb = NODE_BYTES * (ex["vol_tests_whole_line"] + ex["vol_tests_segment"]) + \
+                     TRI_BYTES * (ex["tri_tests_whole_line"] + ex["tri_tests_segment"]) + PIXEL_BYTES * primary
+                xa = xb * share / (k_mean_max * 1e-3) / 1e9
+                res["roofline"]["executed"] = {"bytes_per_frame": xb, "achieved": round(xa, 1),
+                                               "frac": round(xa / PEAK_HBM_GBS, 4)}
         if world == 1 and not args.no_cpu_baseline:
             if c5:
                 res["cpu_baseline"] = cpu_baseline_c5(sc, st, args.cpu_threads)

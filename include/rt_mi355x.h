@@ -90,6 +90,8 @@ typedef struct rt_stats {
     int32_t render_width, render_height;
     float seg_scale;           /* scene scale of the last frame's segment queries (kernels.hip seg_margin);
                                   0: shadow / reflection queries walked the whole line */
+    int64_t work[4];           /* diagnostic builds (-DRT_COUNT=1) only, else 0: the last frame's k-DOP and
+                                  Moller-Trumbore tests of whole-line queries, then of segment queries */
 } rt_stats;
 
 typedef struct rt_renderer rt_renderer;

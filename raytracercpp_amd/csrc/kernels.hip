@@ -35,6 +35,12 @@ constexpr int BLOCK = 64 * WAVES_PER_BLOCK;
 #ifndef RT_MT_EARLY
 #define RT_MT_EARLY 2
 #endif
+// RT_COUNT=1 (diagnostic builds only, tools/count_gpu_work.py): every traversal adds
+// its k-DOP and Moller-Trumbore test counts to P.counters[4..7] (whole-line queries:
+// 4 / 5, segment queries: 6 / 7), the work the kernel actually did
+#ifndef RT_COUNT
+#define RT_COUNT 0
+#endif
 
 struct TRay {
     v3 o, d;
@@ -288,6 +294,9 @@ struct Trav {
     int depth;
     uint32_t any_true;   // bit d: closest_inter != INFINITY in the node whose children are at depth d
     bool r, live;
+#if RT_COUNT
+    uint32_t nvol, ntri;
+#endif
 };
 
 template <bool SEG = false>
@@ -299,6 +308,10 @@ __device__ __forceinline__ void trav_begin(const KParams& P, const TRay& R, THit
     h.k = -1;
     T.r = false;
     T.live = false;
+#if RT_COUNT
+    T.nvol = 1;
+    T.ntri = 0;
+#endif
     if (P.nnodes == 0)
         return;
     if (R.nan) {
@@ -329,6 +342,9 @@ __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit&
     // ---- VISIT the node whose link word is (a, b) at 'depth' ----
     if (b & LEAF_BIT) {
         uint32_t end = a + (b & ~LEAF_BIT);
+#if RT_COUNT
+        T.ntri += end - a;
+#endif
         // triangles in leaf order, h updated as in bvh.h:237-243
         for (uint32_t k = a; k < end; k++) {
             float t, u, v;
@@ -345,6 +361,9 @@ __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit&
         // the k non-empty children are nodes a .. a+k-1, in octant order; a
         // child that is missed keeps a NaN key (no comparison counts it)
         const uint32_t k = b;
+#if RT_COUNT
+        T.nvol += k;
+#endif
         float key[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) {
@@ -418,6 +437,9 @@ __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit&
             NodeBox nx = load_node(P.nodes, e.x + (ord & 7u));
             float t_next;
             vol_test(nx, R, t_next);
+#if RT_COUNT
+            T.nvol++;
+#endif
             if (h.t < t_next) {
                 depth--;    // closest hit nearer than the next child: parent returns true
                 continue;
@@ -462,6 +484,12 @@ __device__ bool bvh_closest(const KParams& P, const TRay& R, THit& h, uint2* lv)
 #else
     while (T.live)
         trav_step<SEG>(P, R, h, T, lv);
+#endif
+#if RT_COUNT
+    if (P.counters) {
+        atomicAdd(&P.counters[SEG ? 6 : 4], (unsigned long long)T.nvol);
+        atomicAdd(&P.counters[SEG ? 7 : 5], (unsigned long long)T.ntri);
+    }
 #endif
     return T.r;
 }

@@ -843,7 +843,7 @@ int Renderer::trace_frame()
     hipEventRecord(ev_[0], stream_);
     if ((rc = launch_frame(P, stream_)) != RT_OK) return rc;
     hipEventRecord(ev_[1], stream_);
-    unsigned long long cnt[2] = {0, 0};
+    unsigned long long cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if ((e = hipMemcpyAsync(cnt, d_counters_.p, sizeof(cnt), hipMemcpyDeviceToHost, stream_)) != hipSuccess)
         return hip_fail(e, "counters");
     if ((e = hipStreamSynchronize(stream_)) != hipSuccess) return hip_fail(e, "ray_trace_kernel");
@@ -851,6 +851,7 @@ int Renderer::trace_frame()
     last_primary_ = (int64_t)npx;
     last_shadow_ = (int64_t)cnt[0];
     last_refl_ = (int64_t)cnt[1];
+    for (int i = 0; i < 4; i++) last_work_[i] = (int64_t)cnt[4 + i];
     img_w_ = P.rw;
     img_h_ = P.rh;
     img_is_internal_ = true;
@@ -1029,6 +1030,7 @@ int Renderer::get_stats(rt_stats* out) const
     out->gpu_tris = (int64_t)oct_.tris.size();
     render_size(out->render_width, out->render_height);
     out->seg_scale = last_seg_;
+    for (int i = 0; i < 4; i++) out->work[i] = last_work_[i];
     return RT_OK;
 }
 

@@ -171,6 +171,7 @@ private:
     // stats
     int64_t last_primary_ = 0, last_shadow_ = 0, last_refl_ = 0;
     float last_seg_ = 0;   // KParams::seg_scale of the last frame
+    int64_t last_work_[4] = {0, 0, 0, 0};   // RT_COUNT builds: traversal test counts of the last frame
     float kernel_ms_ = 0, post_ms_ = 0, build_ms_ = 0;
 };
 

@@ -1,0 +1,25 @@
+"""Traversal work the GPU kernels actually do (k-DOP tests, Moller-Trumbore tests) on a
+benchmark workload, from the diagnostic build (-DRT_COUNT=1):
+    python tools/variants.py build count="-DRT_COUNT=1"        (here)
+    RT_LIB_PATH=_variants/librt_count.so python tools/count_gpu_work.py [config]   (GPU box)
+Prints one JSON line per mode: segment queries on (default) and off (RT_SEG=0)."""
+import json, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from raytracercpp_amd import scenes
+from raytracercpp_amd.renderer import Renderer
+
+name = sys.argv[1] if len(sys.argv) > 1 else "sphere1m"
+sc, st = scenes.CONFIGS[name]()
+r = Renderer(0)
+r.load_scene(sc, st)
+for mode in ("seg", "whole_line"):
+    if mode == "whole_line":
+        os.environ["RT_SEG"] = "0"
+    r.ray_trace()
+    s = r.stats()
+    w = s["work"]
+    print(json.dumps({"config": name, "mode": mode, "seg_scale": s["seg_scale"], "primary_rays": s["primary_rays"],
+                      "shadow_rays": s["shadow_rays"], "reflection_rays": s["reflection_rays"],
+                      "vol_tests_whole_line": w[0], "tri_tests_whole_line": w[1],
+                      "vol_tests_segment": w[2], "tri_tests_segment": w[3], "kernel_ms": s["kernel_ms"]}), flush=True)

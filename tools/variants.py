@@ -3,7 +3,7 @@
    python tools/variants.py run name1 name2 ...                  (GPU box)"""
 import json, os, subprocess, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-VDIR = os.path.join(ROOT, "build", "variants")
+VDIR = os.path.join(ROOT, "_variants")   # git-ignored, not gpurun-ignored: travels to the box
 
 def build(specs):
     for spec in specs:
