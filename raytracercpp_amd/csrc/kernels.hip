@@ -211,6 +211,28 @@ struct THit {
     int k;   // GTri slot, -1 none
 };
 
+// Leaf normal cones.  P.cones[a] for the leaf whose triangles
+// start at slot a: a unit axis and the cosine c of a cone holding every normalised
+// triangle normal of the leaf (c = -2: no cone).  If the ray direction's angle to the
+// axis plus the cone's half-angle stays below 90 degrees by a margin, every triangle
+// of the leaf has n.d > 1e-4 |n| |d|, so the computed Mdet = dot(n, -d) of
+// Triangle::intersect (triangle.cpp:39-40) is negative for each of them and the whole
+// leaf is rejected exactly as the reference's loop rejects it, one triangle at a time.
+__device__ __forceinline__ bool leaf_backfacing(const KParams& P, uint32_t a, const TRay& R)
+{
+    if (!P.cones)
+        return false;
+    const float4 c = reinterpret_cast<const float4*>(P.cones)[a];
+    const float dd = R.d.x * R.d.x + R.d.y * R.d.y + R.d.z * R.d.z;
+    // |d| in [1e-10, 1e10]: the products of dot(n, -d) neither underflow nor overflow
+    if (!(c.w > 0.0f && dd > 1.0e-20f && dd < 1.0e20f))
+        return false;
+    const float ad = (c.x * R.d.x + c.y * R.d.y + c.z * R.d.z) / sqrtf(dd);   // cos(phi)
+    // n.d / |d| >= cos(theta + phi) = cos(theta) cos(phi) - sin(theta) sin(phi) for theta, phi < 90 deg
+    const float lb = c.w * ad - sqrtf(fmaxf(0.0f, 1.0f - c.w * c.w)) * sqrtf(fmaxf(0.0f, 1.0f - ad * ad));
+    return ad > 0.0f && lb > 1.0e-4f;
+}
+
 // ---- libstdc++ binary heap (push_heap / pop_heap with std::greater), only
 // used when two pending children have equal t_near. ----
 // Children are pushed in octant order, which is their slot order a + j.
@@ -342,6 +364,8 @@ __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit&
     // ---- VISIT the node whose link word is (a, b) at 'depth' ----
     if (b & LEAF_BIT) {
         uint32_t end = a + (b & ~LEAF_BIT);
+        if (leaf_backfacing(P, a, R))
+            end = a;   // every triangle back-facing: each Triangle::intersect returns false
 #if RT_COUNT
         T.ntri += end - a;
 #endif

@@ -27,6 +27,8 @@ struct KParams {
     const int32_t* tri_id;    // GTri slot -> caller triangle index
     const int32_t* tri_mat;   // caller index -> material
     const float* tri_uv;      // caller index -> u0 u1 u2 v0 v1 v2 (nullptr: (-1,-1,-1))
+    const float* cones;       // [4] per GTri slot, set at each leaf's first slot: normal cone (axis, cos);
+                              // nullptr: no cones (kernels.hip leaf_backfacing)
     int32_t nnodes;
     int32_t ntri_slots;       // GTri count (brute-force loop bound when enable_bvh == 0)
     int32_t levels;           // flattened tree depth + 1 (LDS level-stack entries per lane)

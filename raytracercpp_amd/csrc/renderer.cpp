@@ -93,7 +93,7 @@ int Renderer::init(std::string& err)
     DevBuf* all[] = {&d_nodes_, &d_tris_,  &d_tri_id_, &d_tri_mat_, &d_tri_uv_, &d_mats_,   &d_internal_,
                      &d_image_, &d_rgba_,  &d_hit_id_, &d_hit_t_,   &d_shadow_, &d_counters_, &d_band_tmp_,
                      &d_tri9_,  &d_rcount_, &d_roff_,  &d_pieces_,  &d_piece_uv_, &d_zkey_, &d_big_, &d_scan_tmp_,
-                     &d_zbuf_,  &d_nbuf_,   &d_ao_};
+                     &d_zbuf_,  &d_nbuf_,   &d_ao_,     &d_cones_};
     for (DevBuf* b : all) b->device = device_;
     for (auto& b : d_tex_) b.device = device_;
     for (auto& b : d_sky_) b.device = device_;
@@ -377,6 +377,59 @@ int Renderer::destroy_bvh()
     return RT_OK;
 }
 
+// Leaf normal cones (kernels.hip leaf_backfacing): per leaf, the
+// normalised mean of its triangles' stored normals (triangle.cpp:9-10) and the smallest
+// cosine between it and any of them, less 1e-6.  Triangles with n == 0 never hit (Mdet ==
+// 0) and are left out; a leaf with a normal too small or too large for the kernel's
+// rounding argument, or a cone of 90 degrees or more, gets no cone (cos = -2).
+static void leaf_cones(const FlatOctree& o, std::vector<float>& out)
+{
+    out.assign(4 * o.tris.size(), 0.0f);
+    for (const GNode& g : o.nodes) {
+        if (!(g.b & LEAF_BIT))
+            continue;
+        const uint32_t a = g.a, cnt = g.b & ~LEAF_BIT;
+        float* c = &out[4 * (size_t)a];
+        c[3] = -2.0f;
+        double sx = 0, sy = 0, sz = 0;
+        bool ok = cnt > 0;
+        for (uint32_t k = a; k < a + cnt && ok; k++) {
+            const float* n = o.tris[k].n;
+            double len = std::sqrt((double)n[0] * n[0] + (double)n[1] * n[1] + (double)n[2] * n[2]);
+            if (len == 0.0)
+                continue;
+            if (!(len > 1e-30 && len < 1e27)) {
+                ok = false;
+                break;
+            }
+            sx += n[0] / len;
+            sy += n[1] / len;
+            sz += n[2] / len;
+        }
+        double sl = std::sqrt(sx * sx + sy * sy + sz * sz);
+        if (!ok || !(sl > 1e-9))
+            continue;
+        sx /= sl;
+        sy /= sl;
+        sz /= sl;
+        double cmin = 1.0;
+        for (uint32_t k = a; k < a + cnt; k++) {
+            const float* n = o.tris[k].n;
+            double len = std::sqrt((double)n[0] * n[0] + (double)n[1] * n[1] + (double)n[2] * n[2]);
+            if (len == 0.0)
+                continue;
+            cmin = std::min(cmin, (n[0] * sx + n[1] * sy + n[2] * sz) / len);
+        }
+        cmin -= 1e-6;
+        if (!(cmin > 0.0))
+            continue;
+        c[0] = (float)sx;
+        c[1] = (float)sy;
+        c[2] = (float)sz;
+        c[3] = std::nextafter((float)cmin, 0.0f);   // rounded toward 0: never narrower than computed
+    }
+}
+
 int Renderer::ensure_device_scene()
 {
     hipError_t e = hipSetDevice(device_);
@@ -411,6 +464,10 @@ int Renderer::ensure_device_scene()
                 oct_.tri_id[(size_t)i] = (int32_t)i;
             }
         }
+        if (s_.enable_bvh)
+            leaf_cones(oct_, cones_);
+        else
+            cones_.clear();
         size_t nb = oct_.nodes.size() * sizeof(GNode), tb = oct_.tris.size() * sizeof(GTri);
         if ((e = d_nodes_.reserve(nb)) != hipSuccess || (e = d_tris_.reserve(tb)) != hipSuccess ||
             (e = d_tri_id_.reserve(oct_.tri_id.size() * 4)) != hipSuccess ||
@@ -419,6 +476,10 @@ int Renderer::ensure_device_scene()
             return hip_fail(e, "hipMalloc (scene)");
         if (nb) e = hipMemcpyAsync(d_nodes_.p, oct_.nodes.data(), nb, hipMemcpyHostToDevice, stream_);
         if (e == hipSuccess && tb) e = hipMemcpyAsync(d_tris_.p, oct_.tris.data(), tb, hipMemcpyHostToDevice, stream_);
+        if (e == hipSuccess && !cones_.empty()) {
+            if ((e = d_cones_.reserve(cones_.size() * 4)) == hipSuccess)
+                e = hipMemcpyAsync(d_cones_.p, cones_.data(), cones_.size() * 4, hipMemcpyHostToDevice, stream_);
+        }
         if (e == hipSuccess && !oct_.tri_id.empty())
             e = hipMemcpyAsync(d_tri_id_.p, oct_.tri_id.data(), oct_.tri_id.size() * 4, hipMemcpyHostToDevice, stream_);
         if (e == hipSuccess && !tri_mat_.empty())
@@ -511,6 +572,8 @@ void Renderer::fill_params(KParams& P) const
     P.tri_id = d_tri_id_.as<int32_t>();
     P.tri_mat = d_tri_mat_.as<int32_t>();
     P.tri_uv = tri_uv_.empty() ? nullptr : d_tri_uv_.as<float>();
+    const char* cone_env = getenv("RT_CONES");   // RT_CONES=0: every leaf's triangles are tested
+    P.cones = (cones_.empty() || (cone_env && cone_env[0] == '0')) ? nullptr : d_cones_.as<float>();
     P.nnodes = (int32_t)oct_.nodes.size();
     P.ntri_slots = (int32_t)oct_.tris.size();
     P.levels = oct_.levels > 0 ? oct_.levels : 1;

@@ -144,6 +144,9 @@ private:
     DevBuf d_internal_, d_image_, d_rgba_, d_hit_id_, d_hit_t_, d_shadow_, d_counters_, d_band_tmp_;
     // SSAO: _z_buffer, _normal_buffer (float4) and the occlusion counts of the internal image
     DevBuf d_zbuf_, d_nbuf_, d_ao_;
+    // leaf normal cones, [4] per GTri slot (renderer.cpp leaf_cones)
+    std::vector<float> cones_;
+    DevBuf d_cones_;
     bool ssao_ready_ = false;   // the buffers hold the last frame's z / normals
     // raster path: caller-order triangles, per-triangle piece counts / offsets, the piece
     // table and its texcoords, the z-key buffer, the big-piece list, scan scratch

@@ -437,16 +437,19 @@ def test_ssao_errors(R):
 
 @pytest.mark.parametrize("name", ["c2_cube", "robot", "c3_bumpy70k", "mirror", "rough", "textured", "raster_rough"])
 def test_whole_line_queries_match_reference_golden(R, name, monkeypatch):
-    """RT_SEG=0: shadow and reflection queries walk the whole line as the reference does
-    (no segment culling); the framebuffer is the same."""
+    """RT_SEG=0 RT_CONES=0: every query walks the whole line and tests every triangle of
+    every leaf it enters, as the reference does (no segment culling, DESIGN.md 5.2, no leaf
+    normal cones, 5.3); the framebuffer is the same."""
     if name not in CASES:
         pytest.skip(f"no golden case {name}")
     c = Case(name)
     exp = c.expected()
     monkeypatch.setenv("RT_SEG", "0")
+    monkeypatch.setenv("RT_CONES", "0")
     g = gpu_render(R, c.scene, c.settings)
     assert R.stats()["seg_scale"] == 0
     monkeypatch.delenv("RT_SEG")
+    monkeypatch.delenv("RT_CONES")
     assert np.array_equal(g["hit_id"], exp["hit_id"])
     assert np.array_equal(bits(g["hit_t"]), bits(exp["hit_t"]))
     assert np.array_equal(g["shadow"], exp["shadow"])
