@@ -27,7 +27,7 @@ constexpr int WAVES_PER_BLOCK = 4;
 constexpr int BLOCK = 64 * WAVES_PER_BLOCK;
 
 #ifndef RT_OCC
-#define RT_OCC 6
+#define RT_OCC 5
 #endif
 #ifndef RT_WW
 #define RT_WW 1
@@ -40,6 +40,13 @@ constexpr int BLOCK = 64 * WAVES_PER_BLOCK;
 // 4 / 5, segment queries: 6 / 7), the work the kernel actually did
 #ifndef RT_COUNT
 #define RT_COUNT 0
+#endif
+// software prefetch of the next child node / the next leaf triangle (A/B knobs)
+#ifndef RT_CHILD_PF
+#define RT_CHILD_PF 0
+#endif
+#ifndef RT_TRI_PF
+#define RT_TRI_PF 1
 #endif
 
 struct TRay {
@@ -370,6 +377,44 @@ __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit&
         T.ntri += end - a;
 #endif
         // triangles in leaf order, h updated as in bvh.h:237-243
+#if RT_TRI_PF >= 2
+        // the next two triangles' records are in flight while this one is tested
+        TriRec cur, nx1;
+        if (a < end)
+            cur = load_tri(P.tris, a);
+        if (a + 1 < end)
+            nx1 = load_tri(P.tris, a + 1);
+        for (uint32_t k = a; k < end; k++) {
+            TriRec nx2 = load_tri(P.tris, k + 2 < end ? k + 2 : k);
+            float t, u, v;
+            if (tri_test_rec(cur, R, t, u, v))
+                if (t < h.t || h.t == -1) {
+                    h.t = t;
+                    h.u = u;
+                    h.v = v;
+                    h.k = (int)k;
+                }
+            cur = nx1;
+            nx1 = nx2;
+        }
+#elif RT_TRI_PF
+        // the next triangle's record is loaded while this one is tested
+        TriRec cur;
+        if (a < end)
+            cur = load_tri(P.tris, a);
+        for (uint32_t k = a; k < end; k++) {
+            TriRec nxt = load_tri(P.tris, k + 1 < end ? k + 1 : k);
+            float t, u, v;
+            if (tri_test_rec(cur, R, t, u, v))
+                if (t < h.t || h.t == -1) {
+                    h.t = t;
+                    h.u = u;
+                    h.v = v;
+                    h.k = (int)k;
+                }
+            cur = nxt;
+        }
+#else
         for (uint32_t k = a; k < end; k++) {
             float t, u, v;
             if (tri_test(P.tris, k, R, t, u, v))
@@ -380,6 +425,7 @@ __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit&
                     h.k = (int)k;
                 }
         }
+#endif
         r = h.t > 0;
     } else {
         // the k non-empty children are nodes a .. a+k-1, in octant order; a
@@ -389,6 +435,23 @@ __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit&
         T.nvol += k;
 #endif
         float key[8];
+#if RT_CHILD_PF
+        // child j + 1's node is loaded while child j is tested (k >= 1 for an inner node)
+        NodeBox cur = load_node(P.nodes, a);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            key[j] = __int_as_float(0x7fc00000);
+            if ((uint32_t)j < k) {
+                NodeBox nxt = cur;
+                if ((uint32_t)(j + 1) < k)
+                    nxt = load_node(P.nodes, a + j + 1);
+                float t;
+                if (vol_test<SEG>(cur, R, t))
+                    key[j] = t;
+                cur = nxt;
+            }
+        }
+#else
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             key[j] = __int_as_float(0x7fc00000);
@@ -399,6 +462,7 @@ __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit&
                     key[j] = t;
             }
         }
+#endif
         // pop position of child j = number of hit children before it in a
         // stable sort by t_near; equal keys need the heap's own order
         uint32_t pos[8];
