@@ -1685,58 +1685,58 @@ __global__ __launch_bounds__(BLOCK) void refl_keys_kernel(KParams P, const Frame
 }
 
 // gen: one thread per sample slot of the chunk
-__global__ __launch_bounds__(BLOCK) void refl_gen_kernel(KParams P, ReflArgs A)
+// gen + trace: each sample slot's direction (path-keyed RNG: no draw depends on another
+// sample, renderer.cpp:296-315) written to its record, then the sample's closest-hit query.
+// One kernel, so that the record writes overlap the traversals.
+__device__ __forceinline__ bool refl_gen(const KParams& P, const ReflArgs& A, int slot, v3& dir, unsigned& count)
 {
-    int slot = blockIdx.x * BLOCK + threadIdx.x;
-    int nslot = (A.c1 - A.c0) * A.stride;
-    unsigned count = 0;
-    if (slot < nslot) {
-        int f = A.order[A.c0 + slot / A.stride], i = slot % A.stride;
-        const FrameRec& F = A.fr[f];
-        SampleRec& S = A.sm[slot];
-        if (i < F.nsamp) {
-            v3 dir;
-            if (F.rough > 0) {
-                uint32_t rng = sample_state(F.key, (uint32_t)i);
-                float rx = rng_bilateral(rng);
-                float ry = rng_bilateral(rng);
-                float rz = rng_bilateral(rng);
-                v3 rdir = normalize(mk(rx, ry, rz));
-                if (dot(rdir, ld3(F.n)) < 0)
-                    rdir = -rdir;
-                dir = F.rough * rdir + (1 - F.rough) * ld3(F.perfect);
-            } else
-                dir = ld3(F.perfect);
-            st3(S.d, dir);
-            if (A.level > P.max_recursion_depth) {   // trace_ray's depth guard (renderer.cpp:1012-1013)
-                S.kind = 0;
-                st3(S.fc, col(0.0f, 0.0f, 0.0f));
-                S.ray = 0;
-            } else {
-                S.kind = 1;
-                S.ray = 1;
-            }
-            if (i == 0)
-                count = (unsigned)F.nsamp;   // reflection rays
-        } else {
-            S.kind = 2;
-            S.ray = 0;
-        }
+    int f = A.order[A.c0 + slot / A.stride], i = slot % A.stride;
+    const FrameRec& F = A.fr[f];
+    SampleRec& S = A.sm[slot];
+    if (i >= F.nsamp) {
+        S.kind = 2;
+        S.ray = 0;
+        return false;
     }
-    wave_count_add(&P.counters[1], count);
+    if (F.rough > 0) {
+        uint32_t rng = sample_state(F.key, (uint32_t)i);
+        float rx = rng_bilateral(rng);
+        float ry = rng_bilateral(rng);
+        float rz = rng_bilateral(rng);
+        v3 rdir = normalize(mk(rx, ry, rz));
+        if (dot(rdir, ld3(F.n)) < 0)
+            rdir = -rdir;
+        dir = F.rough * rdir + (1 - F.rough) * ld3(F.perfect);
+    } else
+        dir = ld3(F.perfect);
+    st3(S.d, dir);
+    if (i == 0)
+        count = (unsigned)F.nsamp;   // reflection rays
+    if (A.level > P.max_recursion_depth) {   // trace_ray's depth guard (renderer.cpp:1012-1013)
+        S.kind = 0;
+        st3(S.fc, col(0.0f, 0.0f, 0.0f));
+        S.ray = 0;
+        return false;
+    }
+    S.kind = 1;
+    S.ray = 1;
+    return true;
 }
 
-// trace: the samples' closest-hit queries
 __global__ __launch_bounds__(BLOCK) void refl_trace_kernel(KParams P, ReflArgs A)
 {
     extern __shared__ uint2 lds_levels[];
     uint2* lv = lds_levels + threadIdx.x;
     int slot = blockIdx.x * BLOCK + threadIdx.x;
     int nslot = (A.c1 - A.c0) * A.stride;
-    if (slot >= nslot || !A.sm[slot].ray)
+    unsigned count = 0;
+    v3 dir = mk(0, 0, 0);
+    bool ray = slot < nslot && refl_gen(P, A, slot, dir, count);
+    wave_count_add(&P.counters[1], count);
+    if (!ray)
         return;
     const FrameRec& F = A.fr[A.order[A.c0 + slot / A.stride]];
-    TRay R = make_ray(P, ld3(F.ro), ld3(A.sm[slot].d));
+    TRay R = make_ray(P, ld3(F.ro), dir);
     THit h;
     bool r;
     if (P.seg_scale > 0.0f) {
@@ -2589,7 +2589,7 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_level
     return hipGetLastError();
 }
 
-// stage: 0 gen, 1 trace, 2 pass1, 3 shadow, 4 spawn, 5 resolve, 6 list
+// stage: 1 gen + trace, 2 pass1, 3 shadow, 4 spawn, 5 resolve, 6 list
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_stage(int stage, const rt::KParams* P,
                                                                           const rt::ReflArgs* A, hipStream_t stream)
 {
@@ -2600,7 +2600,6 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_stage
     dim3 gs((nslot + rt::BLOCK - 1) / rt::BLOCK), gf((nframes + rt::BLOCK - 1) / rt::BLOCK);
     size_t lds = (size_t)(P->levels > 0 ? P->levels : 1) * rt::BLOCK * sizeof(uint2);
     switch (stage) {
-    case 0: hipLaunchKernelGGL(rt::refl_gen_kernel, gs, dim3(rt::BLOCK), 0, stream, *P, *A); break;
     case 1: hipLaunchKernelGGL(rt::refl_trace_kernel, gs, dim3(rt::BLOCK), lds, stream, *P, *A); break;
     case 2: hipLaunchKernelGGL(rt::refl_pass1_kernel, gf, dim3(rt::BLOCK), 0, stream, *P, *A); break;
     case 3: hipLaunchKernelGGL(rt::refl_shadow_kernel, gs, dim3(rt::BLOCK), lds, stream, *P, *A); break;

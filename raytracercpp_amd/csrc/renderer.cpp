@@ -731,7 +731,7 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
         A.stride = stride;
         if ((e = hipMemsetAsync(L.cnt.p, 0, 8, stream)) != hipSuccess)
             return hip_fail(e, "hipMemsetAsync");
-        for (int stage : {0, 1, 2, 6, 3, 4})
+        for (int stage : {1, 2, 6, 3, 4})
             if ((e = rt_launch_refl_stage(stage, &P, &A, stream)) != hipSuccess)
                 return hip_fail(e, "reflection stage launch");
         unsigned nchild = 0;
