@@ -218,6 +218,34 @@ struct THit {
     int k;   // GTri slot, -1 none
 };
 
+// Leaf slabs.  P.lslab[a] for the leaf whose triangles start at
+// slot a: the box of its vertices (lo, hi) and the range [smin, smax] of their projections
+// on the leaf's cone axis (P.cones[a].xyz).  A curved-surface patch is thin along its mean
+// normal, so a line that grazes the surface (a silhouette ray) passes above most patches
+// near it: if the line's parameter intervals inside the box and inside the slab, both
+// widened by a margin far above their rounding, do not overlap (within the query segment),
+// no triangle of the leaf lies on the line and none can be hit.
+__device__ __forceinline__ bool leaf_missed(const KParams& P, uint32_t a, const TRay& R)
+{
+    if (!P.lslab)
+        return false;
+    const float4* L = reinterpret_cast<const float4*>(P.lslab) + 2 * (size_t)a;
+    const float4 lo = L[0], hi = L[1];
+    const float4 c = reinterpret_cast<const float4*>(P.cones)[a];
+    const float m = 0x1p-16f * (fmaxf(fabsf(R.o.x), fmaxf(fabsf(R.o.y), fabsf(R.o.z))) + P.scene_scale);
+    const float ix = 1.0f / R.d.x, iy = 1.0f / R.d.y, iz = 1.0f / R.d.z;
+    float tx0 = (lo.x - m - R.o.x) * ix, tx1 = (hi.x + m - R.o.x) * ix;
+    float ty0 = (lo.y - m - R.o.y) * iy, ty1 = (hi.y + m - R.o.y) * iy;
+    float tz0 = (lo.z - m - R.o.z) * iz, tz1 = (hi.z + m - R.o.z) * iz;
+    const float da = c.x * R.d.x + c.y * R.d.y + c.z * R.d.z;
+    const float oa = c.x * R.o.x + c.y * R.o.y + c.z * R.o.z;
+    float s0 = (lo.w - m - oa) / da, s1 = (hi.w + m - oa) / da;
+    // NaN quotients (a zero component on a boundary) constrain nothing
+    float tmin = fmaxf(fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), fminf(s0, s1))), R.lo);
+    float tmax = fminf(fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), fmaxf(s0, s1))), R.hi);
+    return tmax < tmin;
+}
+
 // Leaf normal cones.  P.cones[a] for the leaf whose triangles
 // start at slot a: a unit axis and the cosine c of a cone holding every normalised
 // triangle normal of the leaf (c = -2: no cone).  If the ray direction's angle to the
@@ -371,8 +399,8 @@ __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit&
     // ---- VISIT the node whose link word is (a, b) at 'depth' ----
     if (b & LEAF_BIT) {
         uint32_t end = a + (b & ~LEAF_BIT);
-        if (leaf_backfacing(P, a, R))
-            end = a;   // every triangle back-facing: each Triangle::intersect returns false
+        if (leaf_backfacing(P, a, R) || leaf_missed(P, a, R))
+            end = a;   // every triangle back-facing, or the line misses them all: no Triangle::intersect succeeds
 #if RT_COUNT
         T.ntri += end - a;
 #endif
@@ -1345,13 +1373,21 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
         v3 rd = normalize(ws - cam);
 
         uint32_t rng = REFL ? pixel_seed((uint32_t)(py * P.rw + px), P.rng_seed) : 0u;
+#if RT_TILE_TIME
+        const uint64_t t_start = wall_clock64();
+#endif
         PixelOut po = trace_pixel<REFL>(P, cam, rd, lv, rng, nshadow, nrefl);
 
         size_t o = (size_t)lr * P.rw + px;
         if (P.argb) P.argb[o] = color_to_argb(po.color);
         if (P.rgba) P.rgba[o] = make_float4(po.color.r, po.color.g, po.color.b, po.alpha);
         if (P.hit_id) P.hit_id[o] = po.found ? po.src : -1;
+#if RT_TILE_TIME
+        // diagnostic build: hit_t holds the pixel's trace time in wall-clock ticks
+        if (P.hit_t) P.hit_t[o] = (float)(wall_clock64() - t_start);
+#else
         if (P.hit_t) P.hit_t[o] = po.fin.t;
+#endif
         if (P.shadow) P.shadow[o] = (uint8_t)(po.found && po.shadowed);
         if (P.zbuf) write_ssao_buffers(P, o, po.found, cam, rd, po.fin);
     }

@@ -29,6 +29,9 @@ struct KParams {
     const float* tri_uv;      // caller index -> u0 u1 u2 v0 v1 v2 (nullptr: (-1,-1,-1))
     const float* cones;       // [4] per GTri slot, set at each leaf's first slot: normal cone (axis, cos);
                               // nullptr: no cones (kernels.hip leaf_backfacing)
+    const float* lslab;       // [8] per GTri slot, at each leaf's first slot: box lo xyz, smin, hi xyz, smax
+                              // along the cone axis; nullptr: none (kernels.hip leaf_missed)
+    float scene_scale;        // largest |vertex coordinate| (leaf_missed's margin)
     int32_t nnodes;
     int32_t ntri_slots;       // GTri count (brute-force loop bound when enable_bvh == 0)
     int32_t levels;           // flattened tree depth + 1 (LDS level-stack entries per lane)

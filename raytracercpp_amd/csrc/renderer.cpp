@@ -93,7 +93,7 @@ int Renderer::init(std::string& err)
     DevBuf* all[] = {&d_nodes_, &d_tris_,  &d_tri_id_, &d_tri_mat_, &d_tri_uv_, &d_mats_,   &d_internal_,
                      &d_image_, &d_rgba_,  &d_hit_id_, &d_hit_t_,   &d_shadow_, &d_counters_, &d_band_tmp_,
                      &d_tri9_,  &d_rcount_, &d_roff_,  &d_pieces_,  &d_piece_uv_, &d_zkey_, &d_big_, &d_scan_tmp_,
-                     &d_zbuf_,  &d_nbuf_,   &d_ao_,     &d_cones_};
+                     &d_zbuf_,  &d_nbuf_,   &d_ao_,     &d_cones_, &d_lslab_};
     for (DevBuf* b : all) b->device = device_;
     for (auto& b : d_tex_) b.device = device_;
     for (auto& b : d_sky_) b.device = device_;
@@ -377,20 +377,65 @@ int Renderer::destroy_bvh()
     return RT_OK;
 }
 
+// Leaf slabs (kernels.hip leaf_missed): the box of the leaf's
+// triangles a, a + ab, a + ac (rounded outward) and, once the cone axis is known, the range of
+// their projections on it (rounded outward; the kernel adds its own margin).  Without an
+// axis the slab is [-inf, +inf] (no constraint).
+static void leaf_slab(const FlatOctree& o, uint32_t a, uint32_t cnt, float* out)
+{
+    double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (uint32_t k = a; k < a + cnt; k++) {
+        const GTri& t = o.tris[k];
+        for (int c = 0; c < 3; c++) {
+            double p0 = t.a[c], p1 = p0 + t.ab[c], p2 = p0 + t.ac[c];
+            mn[c] = std::min(mn[c], std::min(p0, std::min(p1, p2)));
+            mx[c] = std::max(mx[c], std::max(p0, std::max(p1, p2)));
+        }
+    }
+    for (int c = 0; c < 3; c++) {
+        out[c] = std::nextafter((float)mn[c], -INFINITY);
+        out[4 + c] = std::nextafter((float)mx[c], INFINITY);
+    }
+    out[3] = -INFINITY;
+    out[7] = INFINITY;
+}
+
+static void leaf_slab_axis(const FlatOctree& o, uint32_t a, uint32_t cnt, double ax, double ay, double az, float* out)
+{
+    // the projections use the float axis the kernel reads
+    const double fx = (float)ax, fy = (float)ay, fz = (float)az;
+    double smin = INFINITY, smax = -INFINITY;
+    for (uint32_t k = a; k < a + cnt; k++) {
+        const GTri& t = o.tris[k];
+        for (int v = 0; v < 3; v++) {
+            double p[3];
+            for (int c = 0; c < 3; c++)
+                p[c] = (double)t.a[c] + (v == 1 ? (double)t.ab[c] : v == 2 ? (double)t.ac[c] : 0.0);
+            double d = fx * p[0] + fy * p[1] + fz * p[2];
+            smin = std::min(smin, d);
+            smax = std::max(smax, d);
+        }
+    }
+    out[3] = std::nextafter((float)smin, -INFINITY);
+    out[7] = std::nextafter((float)smax, INFINITY);
+}
+
 // Leaf normal cones (kernels.hip leaf_backfacing): per leaf, the
 // normalised mean of its triangles' stored normals (triangle.cpp:9-10) and the smallest
 // cosine between it and any of them, less 1e-6.  Triangles with n == 0 never hit (Mdet ==
 // 0) and are left out; a leaf with a normal too small or too large for the kernel's
 // rounding argument, or a cone of 90 degrees or more, gets no cone (cos = -2).
-static void leaf_cones(const FlatOctree& o, std::vector<float>& out)
+static void leaf_cones(const FlatOctree& o, std::vector<float>& out, std::vector<float>& slab)
 {
     out.assign(4 * o.tris.size(), 0.0f);
+    slab.assign(8 * o.tris.size(), 0.0f);
     for (const GNode& g : o.nodes) {
         if (!(g.b & LEAF_BIT))
             continue;
         const uint32_t a = g.a, cnt = g.b & ~LEAF_BIT;
         float* c = &out[4 * (size_t)a];
         c[3] = -2.0f;
+        leaf_slab(o, a, cnt, &slab[8 * (size_t)a]);
         double sx = 0, sy = 0, sz = 0;
         bool ok = cnt > 0;
         for (uint32_t k = a; k < a + cnt && ok; k++) {
@@ -412,6 +457,7 @@ static void leaf_cones(const FlatOctree& o, std::vector<float>& out)
         sx /= sl;
         sy /= sl;
         sz /= sl;
+        leaf_slab_axis(o, a, cnt, sx, sy, sz, &slab[8 * (size_t)a]);
         double cmin = 1.0;
         for (uint32_t k = a; k < a + cnt; k++) {
             const float* n = o.tris[k].n;
@@ -421,11 +467,11 @@ static void leaf_cones(const FlatOctree& o, std::vector<float>& out)
             cmin = std::min(cmin, (n[0] * sx + n[1] * sy + n[2] * sz) / len);
         }
         cmin -= 1e-6;
-        if (!(cmin > 0.0))
-            continue;
-        c[0] = (float)sx;
+        c[0] = (float)sx;   // the axis is kept for leaf_missed's slab even without a cone
         c[1] = (float)sy;
         c[2] = (float)sz;
+        if (!(cmin > 0.0))
+            continue;
         c[3] = std::nextafter((float)cmin, 0.0f);   // rounded toward 0: never narrower than computed
     }
 }
@@ -465,9 +511,11 @@ int Renderer::ensure_device_scene()
             }
         }
         if (s_.enable_bvh)
-            leaf_cones(oct_, cones_);
-        else
+            leaf_cones(oct_, cones_, lslab_);
+        else {
             cones_.clear();
+            lslab_.clear();
+        }
         size_t nb = oct_.nodes.size() * sizeof(GNode), tb = oct_.tris.size() * sizeof(GTri);
         if ((e = d_nodes_.reserve(nb)) != hipSuccess || (e = d_tris_.reserve(tb)) != hipSuccess ||
             (e = d_tri_id_.reserve(oct_.tri_id.size() * 4)) != hipSuccess ||
@@ -476,6 +524,10 @@ int Renderer::ensure_device_scene()
             return hip_fail(e, "hipMalloc (scene)");
         if (nb) e = hipMemcpyAsync(d_nodes_.p, oct_.nodes.data(), nb, hipMemcpyHostToDevice, stream_);
         if (e == hipSuccess && tb) e = hipMemcpyAsync(d_tris_.p, oct_.tris.data(), tb, hipMemcpyHostToDevice, stream_);
+        if (e == hipSuccess && !lslab_.empty()) {
+            if ((e = d_lslab_.reserve(lslab_.size() * 4)) == hipSuccess)
+                e = hipMemcpyAsync(d_lslab_.p, lslab_.data(), lslab_.size() * 4, hipMemcpyHostToDevice, stream_);
+        }
         if (e == hipSuccess && !cones_.empty()) {
             if ((e = d_cones_.reserve(cones_.size() * 4)) == hipSuccess)
                 e = hipMemcpyAsync(d_cones_.p, cones_.data(), cones_.size() * 4, hipMemcpyHostToDevice, stream_);
@@ -574,6 +626,12 @@ void Renderer::fill_params(KParams& P) const
     P.tri_uv = tri_uv_.empty() ? nullptr : d_tri_uv_.as<float>();
     const char* cone_env = getenv("RT_CONES");   // RT_CONES=0: every leaf's triangles are tested
     P.cones = (cones_.empty() || (cone_env && cone_env[0] == '0')) ? nullptr : d_cones_.as<float>();
+    const char* slab_env = getenv("RT_LSLAB");   // RT_LSLAB=0: no leaf slabs (they read the cone axis)
+    P.lslab = (!P.cones || lslab_.empty() || (slab_env && slab_env[0] == '0')) ? nullptr : d_lslab_.as<float>();
+    P.scene_scale = 0.0f;
+    if (!oct_.nodes.empty())
+        for (int c = 0; c < 3; c++)
+            P.scene_scale = std::max(P.scene_scale, std::max(std::fabs(oct_.nodes[0].dn[c]), std::fabs(oct_.nodes[0].df[c])));
     P.nnodes = (int32_t)oct_.nodes.size();
     P.ntri_slots = (int32_t)oct_.tris.size();
     P.levels = oct_.levels > 0 ? oct_.levels : 1;

@@ -147,6 +147,9 @@ private:
     // leaf normal cones, [4] per GTri slot (renderer.cpp leaf_cones)
     std::vector<float> cones_;
     DevBuf d_cones_;
+    // leaf slabs, [8] per GTri slot (renderer.cpp leaf_slab)
+    std::vector<float> lslab_;
+    DevBuf d_lslab_;
     bool ssao_ready_ = false;   // the buffers hold the last frame's z / normals
     // raster path: caller-order triangles, per-triangle piece counts / offsets, the piece
     // table and its texcoords, the z-key buffer, the big-piece list, scan scratch
