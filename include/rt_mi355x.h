@@ -92,6 +92,8 @@ typedef struct rt_stats {
                                   0: shadow / reflection queries walked the whole line */
     int64_t work[4];           /* diagnostic builds (-DRT_COUNT=1) only, else 0: the last frame's k-DOP and
                                   Moller-Trumbore tests of whole-line queries, then of segment queries */
+    int64_t deferred_pixels;   /* pixels of the last ray_trace whose primary query exceeded RT_DEFER_BUDGET and
+                                  were traced by the ray-group pass; 0 when deferral is off */
 } rt_stats;
 
 typedef struct rt_renderer rt_renderer;

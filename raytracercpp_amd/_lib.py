@@ -54,7 +54,7 @@ class RtStats(C.Structure):
         ("octree_max_leaf", C.c_int64), ("octree_max_depth", C.c_int64),
         ("gpu_nodes", C.c_int64), ("gpu_tris", C.c_int64),
         ("render_width", C.c_int32), ("render_height", C.c_int32), ("seg_scale", C.c_float),
-        ("work", C.c_int64 * 4),
+        ("work", C.c_int64 * 4), ("deferred_pixels", C.c_int64),
     ]
 
     def as_dict(self):

@@ -41,6 +41,11 @@ constexpr int BLOCK = 64 * WAVES_PER_BLOCK;
 #ifndef RT_COUNT
 #define RT_COUNT 0
 #endif
+#if RT_COUNT == 2
+// RT_COUNT=2 (tools/pixel_work.py): per-thread k-DOP / MT counts of the pixel being traced
+__device__ uint2 g_pixel_work[1 << 20];
+__device__ __forceinline__ uint32_t pixel_work_slot() { return (blockIdx.x * blockDim.x + threadIdx.x) & ((1u << 20) - 1); }
+#endif
 // software prefetch of the next child node / the next leaf triangle (A/B knobs)
 #ifndef RT_CHILD_PF
 #define RT_CHILD_PF 0
@@ -356,6 +361,64 @@ struct Trav {
 #endif
 };
 
+// Ray groups.  In the deferred pass the 1 << P.grp_shift lanes of a
+// group trace the same ray in lockstep (identical inputs, identical decisions) and split
+// each leaf's triangles: lane g tests slots a + g, a + g + G, ...  Every lane folds its
+// hits as bvh.h:237-243 does, the group then takes the smallest (t, slot), and that
+// replaces h under the reference's own rule.  This equals the sequential fold whenever no
+// hit has t = NaN (t < h.t is then a total order and the first of equal t is the lowest
+// slot); a NaN hit anywhere in the leaf sends the whole group through the sequential loop.
+__device__ __forceinline__ void leaf_group(const KParams& P, const TRay& R, THit& h, uint32_t a, uint32_t end)
+{
+    const uint32_t G = 1u << P.grp_shift;
+    const uint32_t g = __lane_id() & (G - 1);
+    float bt = -1.0f, bu = 1.0f, bv = 0.0f;
+    int bk = -1;
+    int nan_hit = 0;
+    for (uint32_t k = a + g; k < end; k += G) {
+        float t, u, v;
+        if (tri_test(P.tris, k, R, t, u, v)) {
+            nan_hit |= t != t;
+            if (t < bt || bk < 0) {
+                bt = t;
+                bu = u;
+                bv = v;
+                bk = (int)k;
+            }
+        }
+    }
+    for (uint32_t off = 1; off < G; off <<= 1) {
+        float ot = __shfl_xor(bt, off), ou = __shfl_xor(bu, off), ov = __shfl_xor(bv, off);
+        int ok = __shfl_xor(bk, off);
+        nan_hit |= __shfl_xor(nan_hit, off);
+        if (ok >= 0 && (bk < 0 || ot < bt || (ot == bt && ok < bk))) {
+            bt = ot;
+            bu = ou;
+            bv = ov;
+            bk = ok;
+        }
+    }
+    if (nan_hit) {
+        for (uint32_t k = a; k < end; k++) {
+            float t, u, v;
+            if (tri_test(P.tris, k, R, t, u, v))
+                if (t < h.t || h.t == -1) {
+                    h.t = t;
+                    h.u = u;
+                    h.v = v;
+                    h.k = (int)k;
+                }
+        }
+        return;
+    }
+    if (bk >= 0 && (bt < h.t || h.t == -1)) {
+        h.t = bt;
+        h.u = bu;
+        h.v = bv;
+        h.k = bk;
+    }
+}
+
 template <bool SEG = false>
 __device__ __forceinline__ void trav_begin(const KParams& P, const TRay& R, THit& h, Trav& T)
 {
@@ -404,6 +467,9 @@ __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit&
 #if RT_COUNT
         T.ntri += end - a;
 #endif
+        if (P.grp_shift)
+            leaf_group(P, R, h, a, end);
+        else {
         // triangles in leaf order, h updated as in bvh.h:237-243
 #if RT_TRI_PF >= 2
         // the next two triangles' records are in flight while this one is tested
@@ -454,6 +520,7 @@ __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit&
                 }
         }
 #endif
+        }
         r = h.t > 0;
     } else {
         // the k non-empty children are nodes a .. a+k-1, in octant order; a
@@ -583,19 +650,31 @@ __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit&
     T.any_true = any_true;
 }
 
+// budget > 0: the query is abandoned (*aborted = true, h and the result meaningless) once
+// its inner-node visits plus leaf triangle slots exceed budget (deferred pixels, section 5.5)
 template <bool SEG = false>
-__device__ bool bvh_closest(const KParams& P, const TRay& R, THit& h, uint2* lv)
+__device__ bool bvh_closest(const KParams& P, const TRay& R, THit& h, uint2* lv, uint32_t budget = 0,
+                            bool* aborted = nullptr)
 {
     Trav T;
     trav_begin<SEG>(P, R, h, T);
 #if RT_WW
     // while-while: lanes at inner nodes keep expanding until every lane of the
     // wave sits on a leaf (or is done), then the leaves are tested together
+    uint32_t cost = 0;
     while (T.live) {
-        while (T.live && !(T.b & LEAF_BIT))
+        while (T.live && !(T.b & LEAF_BIT)) {
             trav_step<SEG>(P, R, h, T, lv);
-        if (T.live)
+            cost++;
+        }
+        if (T.live) {
+            cost += T.b & ~LEAF_BIT;
             trav_step<SEG>(P, R, h, T, lv);
+        }
+        if (budget && cost > budget && T.live) {
+            T.live = false;
+            *aborted = true;
+        }
     }
 #else
     while (T.live)
@@ -606,6 +685,10 @@ __device__ bool bvh_closest(const KParams& P, const TRay& R, THit& h, uint2* lv)
         atomicAdd(&P.counters[SEG ? 6 : 4], (unsigned long long)T.nvol);
         atomicAdd(&P.counters[SEG ? 7 : 5], (unsigned long long)T.ntri);
     }
+#endif
+#if RT_COUNT == 2
+    g_pixel_work[pixel_work_slot()].x += T.nvol;
+    g_pixel_work[pixel_work_slot()].y += T.ntri;
 #endif
     return T.r;
 }
@@ -944,14 +1027,17 @@ __device__ __forceinline__ void shapes_closest(const KParams& P, v3 o, v3 d, Rec
 
 // Closest hit over the BVH then the analytic shapes (renderer.cpp:1015-1037).
 // fin is the caller's HitInfo; returns the source (-1 none, >=0 triangle, -2-k shape k).
-__device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv)
+__device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv, uint32_t budget = 0,
+                           bool* aborted = nullptr)
 {
     Rec local = rec_fresh();
     TRay R = make_ray(P, o, d);
     int src = -1;
     if (P.enable_bvh) {
         THit h;
-        bool r = bvh_closest(P, R, h, lv);
+        bool r = bvh_closest(P, R, h, lv, budget, aborted);
+        if (budget && *aborted)
+            return -1;
         bvh_record(P, h, r, local, fin, src);
     } else {
         // brute-force loop, renderer.cpp:1021-1027: fin takes every hit nearer
@@ -1179,20 +1265,23 @@ struct PixelOut {
     Rec fin;
     int src;
     bool found, shadowed;
+    bool deferred;   // the primary query exceeded the budget: nothing else was computed
 };
 
 // Renderer::trace_ray (renderer.cpp:1008-1066) for one primary ray, with the
 // compute_reflection recursion (when REFL) unrolled onto an explicit stack.
 template <bool REFL>
 __device__ PixelOut trace_pixel(const KParams& P, v3 cam, v3 rd0, uint2* lv, uint32_t pixel_key, unsigned& nshadow,
-                                unsigned& nrefl)
+                                unsigned& nrefl, uint32_t budget = 0)
 {
     PixelOut po;
     po.fin = rec_fresh();
-    po.found = po.shadowed = false;
+    po.found = po.shadowed = po.deferred = false;
     po.alpha = 1.0f;
-    po.src = closest_hit(P, cam, rd0, po.fin, lv);
+    po.src = closest_hit(P, cam, rd0, po.fin, lv, REFL ? 0u : budget, &po.deferred);
     if (!REFL) {
+        if (po.deferred)
+            return po;
         if (po.fin.t > 0.1f) {
             po.found = true;
             Direct D = shade_direct(P, cam, rd0, po.fin, lv, nshadow);
@@ -1376,15 +1465,28 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
 #if RT_TILE_TIME
         const uint64_t t_start = wall_clock64();
 #endif
-        PixelOut po = trace_pixel<REFL>(P, cam, rd, lv, rng, nshadow, nrefl);
-
+#if RT_COUNT == 2
+        g_pixel_work[pixel_work_slot()] = make_uint2(0u, 0u);
+#endif
+        PixelOut po = trace_pixel<REFL>(P, cam, rd, lv, rng, nshadow, nrefl, REFL ? 0u : P.trav_budget);
         size_t o = (size_t)lr * P.rw + px;
+        if (!REFL && po.deferred) {
+            // the deferred pass (ray_trace_defer_kernel) traces it with a ray group; the
+            // host sizes defer_cap >= the launch's pixels, and a pixel defers at most once
+            uint32_t idx = atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[3]), 1u);
+            P.defer[idx] = (uint32_t)o;
+            continue;
+        }
+
         if (P.argb) P.argb[o] = color_to_argb(po.color);
         if (P.rgba) P.rgba[o] = make_float4(po.color.r, po.color.g, po.color.b, po.alpha);
         if (P.hit_id) P.hit_id[o] = po.found ? po.src : -1;
 #if RT_TILE_TIME
         // diagnostic build: hit_t holds the pixel's trace time in wall-clock ticks
         if (P.hit_t) P.hit_t[o] = (float)(wall_clock64() - t_start);
+#elif RT_COUNT == 2
+        if (P.hit_t) P.hit_t[o] = (float)g_pixel_work[pixel_work_slot()].x;
+        if (P.argb) P.argb[o] = g_pixel_work[pixel_work_slot()].y;
 #else
         if (P.hit_t) P.hit_t[o] = po.fin.t;
 #endif
@@ -1393,6 +1495,44 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
     }
     if (nshadow) atomicAdd(&P.counters[0], (unsigned long long)nshadow);
     if (nrefl) atomicAdd(&P.counters[1], (unsigned long long)nrefl);
+}
+
+// The deferred pass: every pixel whose primary query exceeded
+// P.trav_budget in ray_trace_kernel is traced again from the start by a ray group of
+// 1 << P.grp_shift lanes (leaf_group); the group's lane 0 writes the pixel.
+__global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_defer_kernel(KParams P)
+{
+    extern __shared__ uint2 lds_levels[];
+    uint2* lv = lds_levels + threadIdx.x;
+    const uint32_t n = min(*reinterpret_cast<const unsigned int*>(&P.counters[3]), P.defer_cap);
+    const int gs = P.grp_shift;
+    const uint32_t g = threadIdx.x & ((1u << gs) - 1);
+    const uint32_t stride = (gridDim.x * (uint32_t)BLOCK) >> gs;
+    v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+    unsigned nshadow = 0, nrefl = 0;
+    for (uint32_t i = (blockIdx.x * (uint32_t)BLOCK + threadIdx.x) >> gs; i < n; i += stride) {
+        const uint32_t o = P.defer[i];
+        const int lr = (int)(o / (uint32_t)P.rw), px = (int)(o % (uint32_t)P.rw);
+        const int py = global_row(P, lr);
+        // ray generation, renderer.cpp:1086-1098 (as ray_trace_kernel)
+        float y_world = ((float)py + 0.5f) / P.rh * 2 - 1;
+        float x_world = ((float)px + 0.5f) / P.rw * 2 - 1;
+        v3 vs = xform_point(P.proj_inv, mk(x_world, y_world, -1));
+        v3 ws = xform_point(P.cam_to_world, vs);
+        v3 rd = normalize(ws - cam);
+        unsigned ns = 0;
+        PixelOut po = trace_pixel<false>(P, cam, rd, lv, 0u, ns, nrefl, 0u);
+        if (g != 0)
+            continue;
+        nshadow += ns;
+        if (P.argb) P.argb[o] = color_to_argb(po.color);
+        if (P.rgba) P.rgba[o] = make_float4(po.color.r, po.color.g, po.color.b, po.alpha);
+        if (P.hit_id) P.hit_id[o] = po.found ? po.src : -1;
+        if (P.hit_t) P.hit_t[o] = po.fin.t;
+        if (P.shadow) P.shadow[o] = (uint8_t)(po.found && po.shadowed);
+        if (P.zbuf) write_ssao_buffers(P, o, po.found, cam, rd, po.fin);
+    }
+    if (nshadow) atomicAdd(&P.counters[0], (unsigned long long)nshadow);
 }
 
 // Pixel q of the launch (tile-major: q = tile * 64 + 8 * y + x inside the 8x8
@@ -2594,8 +2734,16 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(
         hipLaunchKernelGGL(rt::ray_trace_kernel<true>, dim3(blocks), dim3(rt::BLOCK), lds, stream, *P);
     else if (P->enable_bvh && P->pipeline)
         hipLaunchKernelGGL(rt::ray_trace_pipe_kernel, dim3(blocks), dim3(rt::BLOCK), lds, stream, *P);
-    else
-        hipLaunchKernelGGL(rt::ray_trace_kernel<false>, dim3(blocks), dim3(rt::BLOCK), lds, stream, *P);
+    else {
+        rt::KParams A = *P;
+        A.grp_shift = 0;   // one lane per pixel; the groups are the deferred pass's
+        hipLaunchKernelGGL(rt::ray_trace_kernel<false>, dim3(blocks), dim3(rt::BLOCK), lds, stream, A);
+        if (P->trav_budget && P->defer && P->defer_cap) {
+            // deferred pixels: a persistent grid of ray groups over the list ray_trace_kernel left
+            int db = P->max_blocks > 0 ? P->max_blocks : 1024;
+            hipLaunchKernelGGL(rt::ray_trace_defer_kernel, dim3(db), dim3(rt::BLOCK), lds, stream, *P);
+        }
+    }
     return hipGetLastError();
 }
 

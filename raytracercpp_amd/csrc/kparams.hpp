@@ -76,6 +76,14 @@ struct KParams {
     int32_t local_rows;       // rows in this launch's (padded) local buffers
     int32_t tiles_x, tiles_y; // 8x8 tiles over (rw, local_rows)
     int32_t max_blocks;       // persistent grid size (CUs x resident blocks per CU)
+    // Deferred pixels (kernels.hip "Ray groups").  trav_budget > 0: a primary query whose
+    // traversal work exceeds it is abandoned and its pixel appended to defer[] (count in
+    // counters[3]); the deferred pass then traces each such pixel with 1 << grp_shift lanes
+    // that split every leaf's triangles between them.  0 / 0: off.
+    uint32_t trav_budget;
+    int32_t grp_shift;
+    uint32_t* defer;
+    uint32_t defer_cap;
 
     // outputs, indexed by local_row * rw + px (nullptr = not requested)
     uint32_t* argb;

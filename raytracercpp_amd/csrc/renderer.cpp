@@ -91,7 +91,7 @@ int Renderer::init(std::string& err)
         return RT_EHIP;
     }
     DevBuf* all[] = {&d_nodes_, &d_tris_,  &d_tri_id_, &d_tri_mat_, &d_tri_uv_, &d_mats_,   &d_internal_,
-                     &d_image_, &d_rgba_,  &d_hit_id_, &d_hit_t_,   &d_shadow_, &d_counters_, &d_band_tmp_,
+                     &d_image_, &d_rgba_,  &d_hit_id_, &d_hit_t_,   &d_shadow_, &d_counters_, &d_band_tmp_, &d_defer_,
                      &d_tri9_,  &d_rcount_, &d_roff_,  &d_pieces_,  &d_piece_uv_, &d_zkey_, &d_big_, &d_scan_tmp_,
                      &d_zbuf_,  &d_nbuf_,   &d_ao_,     &d_cones_, &d_lslab_};
     for (DevBuf* b : all) b->device = device_;
@@ -710,7 +710,25 @@ int Renderer::launch_trace(const KParams& P, hipStream_t stream)
     const char* env = getenv("RT_REFL_ENGINE");
     bool engine = P.has_reflection && P.enable_bvh && !(env && env[0] == '0');
     if (!engine) {
-        if ((e = rt_launch_ray_trace(&P, stream)) != hipSuccess)
+        // deferred pixels (kernels.hip ray_trace_defer_kernel):
+        // RT_DEFER_BUDGET (default 750; 0 = off) and RT_GROUP_SHIFT (default 4: 16 lanes per ray)
+        KParams Q = P;
+        if (P.enable_bvh && !P.has_reflection && !P.pipeline) {
+            const char* bs = getenv("RT_DEFER_BUDGET");
+            const char* gs = getenv("RT_GROUP_SHIFT");
+            long budget = bs ? atol(bs) : 750;
+            long shift = gs ? atol(gs) : 4;
+            size_t npx = (size_t)P.rw * P.local_rows;
+            if (budget > 0 && shift >= 1 && shift <= 6 && npx > 0 && npx < (1ull << 32)) {
+                if ((e = d_defer_.reserve(npx * 4)) != hipSuccess)
+                    return hip_fail(e, "hipMalloc (deferred pixels)");
+                Q.trav_budget = (uint32_t)budget;
+                Q.grp_shift = (int32_t)shift;
+                Q.defer = d_defer_.as<uint32_t>();
+                Q.defer_cap = (uint32_t)npx;   // >= the launch's pixels: the list cannot overflow
+            }
+        }
+        if ((e = rt_launch_ray_trace(&Q, stream)) != hipSuccess)
             return hip_fail(e, "ray_trace_kernel launch");
         return RT_OK;
     }
@@ -973,6 +991,7 @@ int Renderer::trace_frame()
     last_shadow_ = (int64_t)cnt[0];
     last_refl_ = (int64_t)cnt[1];
     for (int i = 0; i < 4; i++) last_work_[i] = (int64_t)cnt[4 + i];
+    last_deferred_ = (int64_t)(cnt[3] & 0xffffffffull);
     img_w_ = P.rw;
     img_h_ = P.rh;
     img_is_internal_ = true;
@@ -1152,6 +1171,7 @@ int Renderer::get_stats(rt_stats* out) const
     render_size(out->render_width, out->render_height);
     out->seg_scale = last_seg_;
     for (int i = 0; i < 4; i++) out->work[i] = last_work_[i];
+    out->deferred_pixels = last_deferred_;
     return RT_OK;
 }
 

@@ -141,7 +141,7 @@ private:
     bool geom_dirty_ = true, mats_dirty_ = true, tex_dirty_ = true;
     DevBuf d_nodes_, d_tris_, d_tri_id_, d_tri_mat_, d_tri_uv_, d_mats_;
     DevBuf d_tex_[TEX_SLOTS], d_sky_[6];
-    DevBuf d_internal_, d_image_, d_rgba_, d_hit_id_, d_hit_t_, d_shadow_, d_counters_, d_band_tmp_;
+    DevBuf d_internal_, d_image_, d_rgba_, d_hit_id_, d_hit_t_, d_shadow_, d_counters_, d_band_tmp_, d_defer_;
     // SSAO: _z_buffer, _normal_buffer (float4) and the occlusion counts of the internal image
     DevBuf d_zbuf_, d_nbuf_, d_ao_;
     // leaf normal cones, [4] per GTri slot (renderer.cpp leaf_cones)
@@ -177,6 +177,7 @@ private:
     // stats
     int64_t last_primary_ = 0, last_shadow_ = 0, last_refl_ = 0;
     float last_seg_ = 0;   // KParams::seg_scale of the last frame
+    int64_t last_deferred_ = 0;               // pixels the last frame handed to the ray-group pass
     int64_t last_work_[4] = {0, 0, 0, 0};   // RT_COUNT builds: traversal test counts of the last frame
     float kernel_ms_ = 0, post_ms_ = 0, build_ms_ = 0;
 };

@@ -511,3 +511,28 @@ def test_segment_queries_match_oracle(R, scene_name, light):
     assert R.stats()["seg_scale"] > 0
     assert int(o.shadow.sum()) > 0
     _check_vs_oracle(g, o, f"{scene_name} {light}", R=R)
+
+
+@pytest.mark.parametrize("budget,shift", [(1, 2), (8, 4), (64, 6)])
+def test_deferred_ray_groups_match_reference_golden(R, monkeypatch, budget, shift):
+    """Deferred pixels: with a tiny traversal budget nearly every
+    primary query is abandoned in ray_trace_kernel and re-traced by a ray group of
+    1 << shift lanes splitting each leaf's triangles; the frame must stay bit-exact."""
+    monkeypatch.setenv("RT_DEFER_BUDGET", str(budget))
+    monkeypatch.setenv("RT_GROUP_SHIFT", str(shift))
+    ran = deferred = 0
+    for name in CASES:
+        c = Case(name)
+        st = c.settings
+        if st.hybrid_rasterization_tracing or not st.enable_bvh or c.meta["counters"]["reflection_rays"]:
+            continue
+        exp = c.expected()
+        g = gpu_render(R, c.scene, st)
+        assert np.array_equal(g["hit_id"], exp["hit_id"]), f"{name}: {int((g['hit_id'] != exp['hit_id']).sum())} hit-ID mismatches"
+        assert np.array_equal(bits(g["hit_t"]), bits(exp["hit_t"])), name
+        assert np.array_equal(g["shadow"], exp["shadow"]), name
+        assert np.array_equal(g["argb"], exp["argb"]), f"{name}: {int((g['argb'] != exp['argb']).sum())} ARGB mismatches"
+        assert R.stats()["shadow_rays"] == c.meta["counters"]["shadow_rays"], name
+        ran += 1
+        deferred += R.stats()["deferred_pixels"]
+    assert ran > 0 and deferred > 0

@@ -19,6 +19,7 @@ r.request_aux(hit=True)
 r.ray_trace()
 r.ray_trace()
 g = r.get_internal(argb=False, hit=True)
+hid = g["hit_id"].reshape(st.render_size()[1], st.render_size()[0])
 rw, rh = st.render_size()
 t = g["hit_t"].reshape(rh, rw).astype(np.float64) / 100.0   # wall clock at 100 MHz -> us
 tiles = t[: rh // 8 * 8, : rw // 8 * 8].reshape(rh // 8, 8, rw // 8, 8).max(axis=(1, 3))
@@ -32,3 +33,7 @@ ty, tx = np.unravel_index(np.argsort(tiles.ravel())[::-1][:12], tiles.shape)
 for a, b in zip(ty, tx):
     print(f"  tile row {a:4d} col {b:4d}  {tiles[a, b]:9.1f} us  (pixel y {a * 8}, x {b * 8})")
 np.save(os.path.join(ROOT, "gpurun_out", "tile_times.npy"), tiles.astype(np.float32))
+a, b = ty[0], tx[0]
+print("heaviest tile, per-pixel us (hit id < 0: miss):")
+for yy in range(8):
+    print("  " + " ".join(f"{t[a * 8 + yy, b * 8 + xx]:7.0f}{'*' if hid[a * 8 + yy, b * 8 + xx] >= 0 else ' '}" for xx in range(8)))
