@@ -419,7 +419,7 @@ __device__ __forceinline__ void leaf_group(const KParams& P, const TRay& R, THit
     }
 }
 
-template <bool SEG = false>
+template <bool SEG = false, bool GRP = false>
 __device__ __forceinline__ void trav_begin(const KParams& P, const TRay& R, THit& h, Trav& T)
 {
     h.t = -1.0f;
@@ -452,7 +452,7 @@ __device__ __forceinline__ void trav_begin(const KParams& P, const TRay& R, THit
     T.live = true;
 }
 
-template <bool SEG = false>
+template <bool SEG = false, bool GRP = false>
 __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit& h, Trav& T, uint2* lv)
 {
     uint32_t a = T.a, b = T.b;
@@ -467,7 +467,7 @@ __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit&
 #if RT_COUNT
         T.ntri += end - a;
 #endif
-        if (P.grp_shift)
+        if (GRP)
             leaf_group(P, R, h, a, end);
         else {
         // triangles in leaf order, h updated as in bvh.h:237-243
@@ -652,24 +652,24 @@ __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit&
 
 // budget > 0: the query is abandoned (*aborted = true, h and the result meaningless) once
 // its inner-node visits plus leaf triangle slots exceed budget (deferred pixels, section 5.5)
-template <bool SEG = false>
+template <bool SEG = false, bool GRP = false>
 __device__ bool bvh_closest(const KParams& P, const TRay& R, THit& h, uint2* lv, uint32_t budget = 0,
                             bool* aborted = nullptr)
 {
     Trav T;
-    trav_begin<SEG>(P, R, h, T);
+    trav_begin<SEG, GRP>(P, R, h, T);
 #if RT_WW
     // while-while: lanes at inner nodes keep expanding until every lane of the
     // wave sits on a leaf (or is done), then the leaves are tested together
     uint32_t cost = 0;
     while (T.live) {
         while (T.live && !(T.b & LEAF_BIT)) {
-            trav_step<SEG>(P, R, h, T, lv);
+            trav_step<SEG, GRP>(P, R, h, T, lv);
             cost++;
         }
         if (T.live) {
             cost += T.b & ~LEAF_BIT;
-            trav_step<SEG>(P, R, h, T, lv);
+            trav_step<SEG, GRP>(P, R, h, T, lv);
         }
         if (budget && cost > budget && T.live) {
             T.live = false;
@@ -678,7 +678,7 @@ __device__ bool bvh_closest(const KParams& P, const TRay& R, THit& h, uint2* lv,
     }
 #else
     while (T.live)
-        trav_step<SEG>(P, R, h, T, lv);
+        trav_step<SEG, GRP>(P, R, h, T, lv);
 #endif
 #if RT_COUNT
     if (P.counters) {
@@ -714,13 +714,14 @@ __device__ __forceinline__ float seg_margin(const KParams& P, const TRay& R)
     return 0x1p-8f * P.seg_scale + 0x1p-14f * (P.seg_scale + om) / dmin;
 }
 
+template <bool GRP = false>
 __device__ __forceinline__ bool bvh_closest_seg(const KParams& P, TRay& R, THit& h, uint2* lv)
 {
-    bool r = bvh_closest<true>(P, R, h, lv);
+    bool r = bvh_closest<true, GRP>(P, R, h, lv);
     if (h.k >= 0 && !(h.t > 0.0f && h.t < INFINITY)) {
         R.lo = -INFINITY;
         R.hi = INFINITY;
-        r = bvh_closest<true>(P, R, h, lv);
+        r = bvh_closest<true, GRP>(P, R, h, lv);
     }
     return r;
 }
@@ -955,6 +956,7 @@ __device__ __forceinline__ bool shapes_shadow(const KParams& P, v3 o, v3 d, floa
 }
 
 // renderer.cpp:340-402
+template <bool GRP = false>
 __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
 {
     if (!P.compute_shadows)
@@ -972,9 +974,9 @@ __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
             float nl = fabsf(n.x) + fabsf(n.y) + fabsf(n.z);
             R.lo = -m;
             R.hi = (sqrtf(length2(p - lp)) + 1.0e-4f * nl) * (1.0f + 0x1p-10f) + m;
-            r = bvh_closest_seg(P, R, h, lv);
+            r = bvh_closest_seg<GRP>(P, R, h, lv);
         } else
-            r = bvh_closest(P, R, h, lv);
+            r = bvh_closest<false, GRP>(P, R, h, lv);
         if (r) {
             v3 q = o + d * h.t;
             if (length2(p - q) < length2(p - lp))
@@ -1027,6 +1029,7 @@ __device__ __forceinline__ void shapes_closest(const KParams& P, v3 o, v3 d, Rec
 
 // Closest hit over the BVH then the analytic shapes (renderer.cpp:1015-1037).
 // fin is the caller's HitInfo; returns the source (-1 none, >=0 triangle, -2-k shape k).
+template <bool GRP = false>
 __device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv, uint32_t budget = 0,
                            bool* aborted = nullptr)
 {
@@ -1035,7 +1038,7 @@ __device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv, ui
     int src = -1;
     if (P.enable_bvh) {
         THit h;
-        bool r = bvh_closest(P, R, h, lv, budget, aborted);
+        bool r = bvh_closest<false, GRP>(P, R, h, lv, budget, aborted);
         if (budget && *aborted)
             return -1;
         bvh_record(P, h, r, local, fin, src);
@@ -1158,6 +1161,7 @@ __device__ c3 shade_debug(const KParams& P, const Rec& h)
     return fc;
 }
 
+template <bool GRP = false>
 __device__ Direct shade_direct(const KParams& P, v3 ro, v3 rd, Rec& h, uint2* lv, unsigned& nshadow)
 {
     Direct out;
@@ -1168,7 +1172,7 @@ __device__ Direct shade_direct(const KParams& P, v3 ro, v3 rd, Rec& h, uint2* lv
         if (P.compute_shadows)
             nshadow++;
         v3 light = mk(P.light[0], P.light[1], P.light[2]);
-        out.shadowed = is_shadowed(P, out.ip, h.normal, light, lv);
+        out.shadowed = is_shadowed<GRP>(P, out.ip, h.normal, light, lv);
         out.fc = shade_shadow_emit(P, fc, mat_of(P, h.mat), out.shadowed);
     } else
         out.fc = shade_debug(P, h);
@@ -1270,7 +1274,7 @@ struct PixelOut {
 
 // Renderer::trace_ray (renderer.cpp:1008-1066) for one primary ray, with the
 // compute_reflection recursion (when REFL) unrolled onto an explicit stack.
-template <bool REFL>
+template <bool REFL, bool GRP = false>
 __device__ PixelOut trace_pixel(const KParams& P, v3 cam, v3 rd0, uint2* lv, uint32_t pixel_key, unsigned& nshadow,
                                 unsigned& nrefl, uint32_t budget = 0)
 {
@@ -1278,13 +1282,13 @@ __device__ PixelOut trace_pixel(const KParams& P, v3 cam, v3 rd0, uint2* lv, uin
     po.fin = rec_fresh();
     po.found = po.shadowed = po.deferred = false;
     po.alpha = 1.0f;
-    po.src = closest_hit(P, cam, rd0, po.fin, lv, REFL ? 0u : budget, &po.deferred);
+    po.src = closest_hit<GRP>(P, cam, rd0, po.fin, lv, REFL ? 0u : budget, &po.deferred);
     if (!REFL) {
         if (po.deferred)
             return po;
         if (po.fin.t > 0.1f) {
             po.found = true;
-            Direct D = shade_direct(P, cam, rd0, po.fin, lv, nshadow);
+            Direct D = shade_direct<GRP>(P, cam, rd0, po.fin, lv, nshadow);
             po.shadowed = D.shadowed;
             po.color = P.shading_method == RT_SHADING ? shade_finish(P, D.fc, mat_of(P, po.fin.mat), col(0, 0, 0))
                                                       : clamp3(D.fc);
@@ -1521,7 +1525,7 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_defer_kernel(KParams 
         v3 ws = xform_point(P.cam_to_world, vs);
         v3 rd = normalize(ws - cam);
         unsigned ns = 0;
-        PixelOut po = trace_pixel<false>(P, cam, rd, lv, 0u, ns, nrefl, 0u);
+        PixelOut po = trace_pixel<false, true>(P, cam, rd, lv, 0u, ns, nrefl, 0u);
         if (g != 0)
             continue;
         nshadow += ns;
