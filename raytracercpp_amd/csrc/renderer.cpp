@@ -711,13 +711,13 @@ int Renderer::launch_trace(const KParams& P, hipStream_t stream)
     bool engine = P.has_reflection && P.enable_bvh && !(env && env[0] == '0');
     if (!engine) {
         // deferred pixels (kernels.hip ray_trace_defer_kernel):
-        // RT_DEFER_BUDGET (default 750; 0 = off) and RT_GROUP_SHIFT (default 4: 16 lanes per ray)
+        // RT_DEFER_BUDGET (default 1000; 0 = off) and RT_GROUP_SHIFT (default 5: 32 lanes per ray)
         KParams Q = P;
         if (P.enable_bvh && !P.has_reflection && !P.pipeline) {
             const char* bs = getenv("RT_DEFER_BUDGET");
             const char* gs = getenv("RT_GROUP_SHIFT");
-            long budget = bs ? atol(bs) : 750;
-            long shift = gs ? atol(gs) : 4;
+            long budget = bs ? atol(bs) : 1000;
+            long shift = gs ? atol(gs) : 5;
             size_t npx = (size_t)P.rw * P.local_rows;
             if (budget > 0 && shift >= 1 && shift <= 6 && npx > 0 && npx < (1ull << 32)) {
                 if ((e = d_defer_.reserve(npx * 4)) != hipSuccess)
