@@ -94,6 +94,8 @@ typedef struct rt_stats {
                                   Moller-Trumbore tests of whole-line queries, then of segment queries */
     int64_t deferred_pixels;   /* pixels of the last ray_trace whose primary query exceeded RT_DEFER_BUDGET and
                                   were traced by the ray-group pass; 0 when deferral is off */
+    int64_t work_abandoned[2]; /* diagnostic builds only: k-DOP and Moller-Trumbore tests of primary queries
+                                  abandoned over the budget (re-traced by the deferred pass, counted in work) */
 } rt_stats;
 
 typedef struct rt_renderer rt_renderer;

@@ -681,9 +681,13 @@ __device__ bool bvh_closest(const KParams& P, const TRay& R, THit& h, uint2* lv,
         trav_step<SEG, GRP>(P, R, h, T, lv);
 #endif
 #if RT_COUNT
-    if (P.counters) {
-        atomicAdd(&P.counters[SEG ? 6 : 4], (unsigned long long)T.nvol);
-        atomicAdd(&P.counters[SEG ? 7 : 5], (unsigned long long)T.ntri);
+    // a ray group's lanes run one query in lockstep: its work is counted once, by the
+    // group's lane 0 (T.ntri holds the whole leaf, which the group tests between them).
+    // Abandoned (budget-exceeded) queries go to counters[8..9], not to the executed work.
+    if (P.counters && (!GRP || (__lane_id() & ((1u << P.grp_shift) - 1)) == 0)) {
+        const bool ab = budget && *aborted;
+        atomicAdd(&P.counters[ab ? 8 : (SEG ? 6 : 4)], (unsigned long long)T.nvol);
+        atomicAdd(&P.counters[ab ? 9 : (SEG ? 7 : 5)], (unsigned long long)T.ntri);
     }
 #endif
 #if RT_COUNT == 2

@@ -11,6 +11,7 @@ namespace rt {
 constexpr int TEX_SLOTS = 6;   // ao, diffuse, normal, displacement, roughness, skysphere (renderer.h:77-84)
 constexpr int MAT_STRIDE = 16; // see include/rt_mi355x.h
 constexpr int MAX_SHAPES = 64;
+constexpr int NCOUNTERS = 16;  // KParams::counters entries (u64)
 
 enum TexSlot { TEX_AO = 0, TEX_DIFFUSE = 1, TEX_NORMAL = 2, TEX_DISPLACEMENT = 3, TEX_ROUGHNESS = 4, TEX_SKYSPHERE = 5 };
 enum Shading { RT_SHADING = 0, ABS_NORMALS = 1, PASTEL_NORMALS = 2, BARYCENTRIC = 3, VISUALIZE_AO = 4 };
@@ -91,7 +92,9 @@ struct KParams {
     int32_t* hit_id;
     float* hit_t;
     uint8_t* shadow;
-    unsigned long long* counters;   // [0] shadow rays, [1] reflection rays, [2] tile queue head
+    unsigned long long* counters;   // [NCOUNTERS]: [0] shadow rays, [1] reflection rays, [2] tile queue head,
+                                    // [3] deferred-pixel list head, [4..7] executed k-DOP / MT tests of
+                                    // whole-line / segment queries and [8..9] of abandoned queries (RT_COUNT)
     // SSAO inputs (enable_ssao): Renderer::_z_buffer / _normal_buffer, renderer.cpp:1107-1110, 975-979
     float* zbuf;
     float4* nbuf;

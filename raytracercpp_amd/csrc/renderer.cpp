@@ -716,8 +716,17 @@ int Renderer::launch_trace(const KParams& P, hipStream_t stream)
         if (P.enable_bvh && !P.has_reflection && !P.pipeline) {
             const char* bs = getenv("RT_DEFER_BUDGET");
             const char* gs = getenv("RT_GROUP_SHIFT");
-            long budget = bs ? atol(bs) : 1000;
-            long shift = gs ? atol(gs) : 5;
+            // out-of-range values (negative, above 2^32 - 1, not a number) turn deferral off
+            char* end = nullptr;
+            long long budget = 1000, shift = 5;
+            if (bs) {
+                budget = strtoll(bs, &end, 10);
+                if (end == bs || *end != '\0' || budget < 0 || budget > (long long)UINT32_MAX) budget = 0;
+            }
+            if (gs) {
+                shift = strtoll(gs, &end, 10);
+                if (end == gs || *end != '\0') shift = 0;
+            }
             size_t npx = (size_t)P.rw * P.local_rows;
             if (budget > 0 && shift >= 1 && shift <= 6 && npx > 0 && npx < (1ull << 32)) {
                 if ((e = d_defer_.reserve(npx * 4)) != hipSuccess)
@@ -956,7 +965,7 @@ int Renderer::trace_frame()
     last_seg_ = P.seg_scale;
     size_t npx = (size_t)P.rw * P.rh;
     hipError_t e;
-    if ((e = d_internal_.reserve(npx * 4)) != hipSuccess || (e = d_counters_.reserve(64)) != hipSuccess)
+    if ((e = d_internal_.reserve(npx * 4)) != hipSuccess || (e = d_counters_.reserve(NCOUNTERS * 8)) != hipSuccess)
         return hip_fail(e, "hipMalloc (image)");
     if (want_rgba_ && (e = d_rgba_.reserve(npx * 16)) != hipSuccess) return hip_fail(e, "hipMalloc (rgba)");
     if (want_hit_ && ((e = d_hit_id_.reserve(npx * 4)) != hipSuccess || (e = d_hit_t_.reserve(npx * 4)) != hipSuccess))
@@ -978,20 +987,17 @@ int Renderer::trace_frame()
     P.hit_t = want_hit_ ? d_hit_t_.as<float>() : nullptr;
     P.shadow = want_shadow_ ? d_shadow_.as<uint8_t>() : nullptr;
     P.counters = d_counters_.as<unsigned long long>();
-    if ((e = hipMemsetAsync(d_counters_.p, 0, 64, stream_)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+    if ((e = hipMemsetAsync(d_counters_.p, 0, NCOUNTERS * 8, stream_)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
     hipEventRecord(ev_[0], stream_);
     if ((rc = launch_frame(P, stream_)) != RT_OK) return rc;
     hipEventRecord(ev_[1], stream_);
-    unsigned long long cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long cnt[NCOUNTERS] = {};
     if ((e = hipMemcpyAsync(cnt, d_counters_.p, sizeof(cnt), hipMemcpyDeviceToHost, stream_)) != hipSuccess)
         return hip_fail(e, "counters");
     if ((e = hipStreamSynchronize(stream_)) != hipSuccess) return hip_fail(e, "ray_trace_kernel");
     hipEventElapsedTime(&kernel_ms_, ev_[0], ev_[1]);
     last_primary_ = (int64_t)npx;
-    last_shadow_ = (int64_t)cnt[0];
-    last_refl_ = (int64_t)cnt[1];
-    for (int i = 0; i < 4; i++) last_work_[i] = (int64_t)cnt[4 + i];
-    last_deferred_ = (int64_t)(cnt[3] & 0xffffffffull);
+    take_counters(cnt);
     img_w_ = P.rw;
     img_h_ = P.rh;
     img_is_internal_ = true;
@@ -1171,6 +1177,7 @@ int Renderer::get_stats(rt_stats* out) const
     render_size(out->render_width, out->render_height);
     out->seg_scale = last_seg_;
     for (int i = 0; i < 4; i++) out->work[i] = last_work_[i];
+    for (int i = 0; i < 2; i++) out->work_abandoned[i] = last_work_[4 + i];
     out->deferred_pixels = last_deferred_;
     return RT_OK;
 }
@@ -1212,7 +1219,7 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
     P.tiles_x = (P.rw + 7) / 8;
     P.tiles_y = (P.local_rows + 7) / 8;
     hipError_t e;
-    if ((e = d_counters_.reserve(64)) != hipSuccess) return hip_fail(e, "hipMalloc (counters)");
+    if ((e = d_counters_.reserve(NCOUNTERS * 8)) != hipSuccess) return hip_fail(e, "hipMalloc (counters)");
     uint32_t* target = d_out;
     if (f > 1) {
         if ((e = d_band_tmp_.reserve((size_t)P.rw * P.local_rows * 4)) != hipSuccess)
@@ -1226,7 +1233,7 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
         for (auto& ev : ring_)
             if ((e = hipEventCreate(&ev)) != hipSuccess) return hip_fail(e, "hipEventCreate");
     }
-    if ((e = hipMemsetAsync(d_counters_.p, 0, 64, stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+    if ((e = hipMemsetAsync(d_counters_.p, 0, NCOUNTERS * 8, stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
     hipEventRecord(ring_[2 * ring_next_], stream);
     if ((rc = launch_frame(P, stream)) != RT_OK) return rc;
     hipEventRecord(ring_[2 * ring_next_ + 1], stream);
@@ -1292,13 +1299,27 @@ int Renderer::kernel_times(float* ms, int n)
     return RT_OK;
 }
 
+// the counters of the last band launch; they also become the stats of the last frame
+// (deferred pixels, RT_COUNT work), as after ray_trace
 int Renderer::band_counters(unsigned long long out[2])
 {
     hipSetDevice(device_);
+    unsigned long long cnt[NCOUNTERS] = {};
     hipError_t e = hipDeviceSynchronize();
-    if (e == hipSuccess) e = hipMemcpy(out, d_counters_.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(cnt, d_counters_.p, sizeof(cnt), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return hip_fail(e, "band_counters");
+    out[0] = cnt[0];
+    out[1] = cnt[1];
+    take_counters(cnt);
     return RT_OK;
+}
+
+void Renderer::take_counters(const unsigned long long* cnt)
+{
+    last_shadow_ = (int64_t)cnt[0];
+    last_refl_ = (int64_t)cnt[1];
+    for (int i = 0; i < 6; i++) last_work_[i] = (int64_t)cnt[i < 4 ? 4 + i : 8 + (i - 4)];
+    last_deferred_ = (int64_t)(cnt[3] & 0xffffffffull);
 }
 
 float render(Renderer& renderer, int* rc)

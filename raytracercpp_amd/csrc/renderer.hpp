@@ -178,7 +178,9 @@ private:
     int64_t last_primary_ = 0, last_shadow_ = 0, last_refl_ = 0;
     float last_seg_ = 0;   // KParams::seg_scale of the last frame
     int64_t last_deferred_ = 0;               // pixels the last frame handed to the ray-group pass
-    int64_t last_work_[4] = {0, 0, 0, 0};   // RT_COUNT builds: traversal test counts of the last frame
+    int64_t last_work_[6] = {0, 0, 0, 0, 0, 0};   // RT_COUNT builds: traversal test counts of the last frame
+                                                   // (executed: whole-line, segment; then abandoned queries)
+    void take_counters(const unsigned long long* cnt);
     float kernel_ms_ = 0, post_ms_ = 0, build_ms_ = 0;
 };
 

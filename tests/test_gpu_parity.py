@@ -513,7 +513,7 @@ def test_segment_queries_match_oracle(R, scene_name, light):
     _check_vs_oracle(g, o, f"{scene_name} {light}", R=R)
 
 
-@pytest.mark.parametrize("budget,shift", [(1, 2), (8, 4), (64, 6)])
+@pytest.mark.parametrize("budget,shift", [(1, 2), (8, 4), (64, 6), (1, 5)])
 def test_deferred_ray_groups_match_reference_golden(R, monkeypatch, budget, shift):
     """Deferred pixels: with a tiny traversal budget nearly every
     primary query is abandoned in ray_trace_kernel and re-traced by a ray group of
@@ -536,3 +536,78 @@ def test_deferred_ray_groups_match_reference_golden(R, monkeypatch, budget, shif
         ran += 1
         deferred += R.stats()["deferred_pixels"]
     assert ran > 0 and deferred > 0
+
+
+@pytest.mark.parametrize("case", ["soup", "voxels", "huge", "ssao", "bands"])
+def test_forced_deferral_matches_oracle(R, monkeypatch, case):
+    """Every primary query deferred (RT_DEFER_BUDGET=1) with the default 32-lane ray groups,
+    on the paths the golden cases do not reach: the segment-query stress scenes (shadow rays
+    of deferred pixels run as group segment queries, incl. the whole-line re-run), a scene
+    scaled by 1e13 whose Moller-Trumbore products overflow (NaN hits: the group falls back to
+    the sequential leaf loop), the SSAO z / normal writes of the deferred pass, and band
+    rendering (render_bands_device) re-assembled into the full frame."""
+    import torch
+    from raytracercpp_amd import scenes
+    from raytracercpp_amd.scene import empty_shapes
+    from raytracercpp_amd.strips import assemble
+    monkeypatch.setenv("RT_DEFER_BUDGET", "1")
+    monkeypatch.setenv("RT_GROUP_SHIFT", "5")
+    rng = np.random.default_rng(11)
+    if case == "soup":
+        sc, st = _soup_scene(rng)
+        st = st.copy(image_width=160, image_height=96)
+        sc.light = np.asarray((60.0, -1.4999, -4.0), np.float32)
+    elif case == "voxels":
+        sc = _voxel_scene(n=6)
+        sc.shape_kind, sc.shape, sc.shape_mat = empty_shapes()
+        _, st = scenes.bumpy70k(width=160, height=96)
+        st = st.copy(bvh_leaf_object_count=8)
+        sc.light = np.asarray((0.3, 0.0, 0.0), np.float32)
+    elif case == "huge":
+        f = np.float32(1e13)
+        sc, st = scenes.robot1080(width=96, height=54)
+        sc.tri = (sc.tri * f).astype(np.float32)
+        sc.light = (np.asarray(sc.light, np.float32) * f).astype(np.float32)
+    elif case == "ssao":
+        sc, st = scenes.bumpy70k(width=131, height=77, enable_ssao=True, ssao_sample_count=16, ssao_radius=0.5)
+    else:
+        sc, st = scenes.bumpy70k(width=160, height=90, enable_ssaa=True, ssaa_factor=2)
+    if case == "bands":
+        R.load_scene(sc, st)
+        R.ray_trace()
+        assert R.stats()["deferred_pixels"] > 0
+        R.post_process()
+        full = R.get_image()
+        o = Oracle(sc, st).render_rows()
+        rw, rh = st.render_size()
+        assert np.array_equal(full.ravel(), Oracle.downscale(o.argb, rw, rh, 2))
+        for nranks, band in ((2, 8), (3, 5)):
+            parts = []
+            for rank in range(nranks):
+                n = R.local_rows(band, rank, nranks)
+                buf = torch.zeros((n, st.image_width), dtype=torch.int32, device="cuda:0")
+                R.render_bands_device(band, rank, nranks, buf.data_ptr(), 0)
+                torch.cuda.synchronize()
+                sh, _ = R.band_counters()
+                assert R.stats()["deferred_pixels"] > 0   # band launches report their deferred pixels
+                parts.append(buf.cpu().numpy().view(np.uint32))
+            assert np.array_equal(assemble(parts, st.image_height, band), full), (nranks, band)
+        return
+    o = Oracle(sc, st)
+    ref = o.render_rows()
+    g = gpu_render(R, sc, st, aux=case != "ssao")
+    assert R.stats()["deferred_pixels"] > 0
+    if case == "ssao":
+        assert np.array_equal(g["argb"], ref.argb)
+        z, n, _ = R.get_ssao_buffers(ao=False)
+        assert np.array_equal(bits(z), bits(ref.zbuf))
+        assert np.array_equal(bits(n), bits(ref.nbuf))
+        ref_img, ref_ao = o.ssao(ref)
+        R.post_process()
+        _, _, ao = R.get_ssao_buffers()
+        assert np.array_equal(ao, ref_ao)
+        assert np.array_equal(R.get_image().ravel(), ref_img)
+        return
+    if case != "huge":
+        assert R.stats()["seg_scale"] > 0
+    _check_vs_oracle(g, ref, case, R=R)

@@ -2,7 +2,8 @@
 benchmark workload, from the diagnostic build (-DRT_COUNT=1):
     python tools/variants.py build count="-DRT_COUNT=1"        (here)
     RT_LIB_PATH=_variants/librt_count.so python tools/count_gpu_work.py [config]   (GPU box)
-Prints one JSON line per mode: segment queries on (default) and off (RT_SEG=0)."""
+Prints one JSON line per mode: segment queries on (default) and off (RT_SEG=0).  A ray group's
+work is counted once; queries abandoned over RT_DEFER_BUDGET are counted apart (*_abandoned)."""
 import json, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -22,4 +23,6 @@ for mode in ("seg", "whole_line"):
     print(json.dumps({"config": name, "mode": mode, "seg_scale": s["seg_scale"], "primary_rays": s["primary_rays"],
                       "shadow_rays": s["shadow_rays"], "reflection_rays": s["reflection_rays"],
                       "vol_tests_whole_line": w[0], "tri_tests_whole_line": w[1],
-                      "vol_tests_segment": w[2], "tri_tests_segment": w[3], "kernel_ms": s["kernel_ms"]}), flush=True)
+                      "vol_tests_segment": w[2], "tri_tests_segment": w[3],
+                      "vol_tests_abandoned": s["work_abandoned"][0], "tri_tests_abandoned": s["work_abandoned"][1],
+                      "deferred_pixels": s["deferred_pixels"], "kernel_ms": s["kernel_ms"]}), flush=True)

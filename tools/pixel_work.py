@@ -12,6 +12,9 @@ import numpy as np
 from raytracercpp_amd import scenes
 from raytracercpp_amd.renderer import Renderer
 
+# the deferred pass writes real hit t / colours, not the diagnostic values: keep every
+# pixel in the main pass (ray_trace_defer_kernel has no RT_COUNT==2 / RT_TILE_TIME writes)
+os.environ["RT_DEFER_BUDGET"] = "0"
 sc, st = scenes.sphere1m()
 r = Renderer(0)
 r.load_scene(sc, st)
