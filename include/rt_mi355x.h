@@ -96,6 +96,8 @@ typedef struct rt_stats {
                                   were traced by the ray-group pass; 0 when deferral is off */
     int64_t work_abandoned[2]; /* diagnostic builds only: k-DOP and Moller-Trumbore tests of primary queries
                                   abandoned over the budget (re-traced by the deferred pass, counted in work) */
+    int64_t work_wide[3];      /* diagnostic builds only: wide-BVH node visits, triangle tests, and the closest-hit
+                                  queries it could not certify (traced through the octree instead) */
 } rt_stats;
 
 typedef struct rt_renderer rt_renderer;
@@ -262,6 +264,18 @@ void rt_obj_close(rt_obj *o);
  * one-insert-at-a-time algorithm restated.  *ms (optional) gets the build time. */
 int rt_octree_digest(const float *tri9, int64_t n, int32_t max_depth, int32_t leaf_max_obj_count, int32_t builder,
                      uint64_t *digest, int64_t stats[7], float *ms);
+
+/* ---- Wide-BVH certified closest hit, on the host, no GPU ----
+ * Builds the octree over tri9 and the 4-wide SAH BVH over its triangle records, then runs,
+ * for each ray, the traversal and certificate the primary-ray kernel runs (wbvh.hpp).
+ * status[i]: 0 = certified no hit (BVH::intersect returns false, record untouched),
+ * 1 = certified hit (id / t / u / v = BVH::intersect's record, bvh.h:212-287, returns true),
+ * 2 = not certified (the kernel re-traces it through the octree).  stats[8] = {wide nodes,
+ * leaves, max leaf, depth, node visits, triangle tests, structural violations (check_wbvh),
+ * SAH cost x 1000}; ms[2] (optional) = {octree build, wide-BVH build} milliseconds. */
+int rt_wbvh_query(const float *tri9, int64_t n, int32_t max_depth, int32_t leaf_max_obj_count, const float *orig,
+                  const float *dir, int64_t nrays, int32_t *status, int32_t *id, float *t, float *u, float *v,
+                  int64_t stats[8], float *ms);
 
 #ifdef __cplusplus
 }

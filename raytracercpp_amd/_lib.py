@@ -55,6 +55,7 @@ class RtStats(C.Structure):
         ("gpu_nodes", C.c_int64), ("gpu_tris", C.c_int64),
         ("render_width", C.c_int32), ("render_height", C.c_int32), ("seg_scale", C.c_float),
         ("work", C.c_int64 * 4), ("deferred_pixels", C.c_int64), ("work_abandoned", C.c_int64 * 2),
+        ("work_wide", C.c_int64 * 3),
     ]
 
     def as_dict(self):
@@ -119,6 +120,8 @@ SIGNATURES = {
     "rt_obj_close": (None, [_H]),
     "rt_octree_digest": (C.c_int, [_f32p, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_uint64), _i64p,
                                    _f32p]),
+    "rt_wbvh_query": (C.c_int, [_f32p, C.c_int64, C.c_int32, C.c_int32, _f32p, _f32p, C.c_int64, _i32p, _i32p, _f32p,
+                                _f32p, _f32p, _i64p, _f32p]),
 }
 
 _lib = None
@@ -233,6 +236,26 @@ def load_obj(path, xform, mat_offset=0):
         return tri, mat, uv, mats
     finally:
         L.rt_obj_close(h)
+
+
+def wbvh_query(tri9, orig, dirs, max_depth=12, leaf=40):
+    """rt_wbvh_query: the wide-BVH certified closest hit on the host (no GPU).  Returns
+    (status, id, t, u, v, stats dict, (octree ms, wide-BVH ms)); status 0 certified miss,
+    1 certified hit, 2 not certified."""
+    tri9 = f32(tri9).reshape(-1, 9)
+    o = f32(orig).reshape(-1, 3)
+    d = f32(dirs).reshape(-1, 3)
+    n = o.shape[0]
+    st = np.zeros(n, np.int32)
+    ids = np.zeros(n, np.int32)
+    t, u, v = (np.zeros(n, np.float32) for _ in range(3))
+    stats = np.zeros(8, np.int64)
+    ms = np.zeros(2, np.float32)
+    check(lib().rt_wbvh_query(ptr(tri9, _f32p), tri9.shape[0], max_depth, leaf, ptr(o, _f32p), ptr(d, _f32p), n,
+                              ptr(st, _i32p), ptr(ids, _i32p), ptr(t, _f32p), ptr(u, _f32p), ptr(v, _f32p),
+                              ptr(stats, _i64p), ptr(ms, _f32p)), "rt_wbvh_query")
+    keys = ("nodes", "leaves", "max_leaf", "depth", "node_visits", "tri_tests", "violations", "sah_x1000")
+    return st, ids, t, u, v, dict(zip(keys, map(int, stats))), (float(ms[0]), float(ms[1]))
 
 
 def octree_digest(tri9, max_depth=12, leaf=40, builder=0):

@@ -1,5 +1,8 @@
 // capi.cpp -- extern "C" boundary (include/rt_mi355x.h).  No exception crosses it.
+#include <atomic>
 #include <chrono>
+#include <cmath>
+#include <thread>
 #include <cstring>
 #include <new>
 #include <string>
@@ -7,6 +10,7 @@
 #include "../../include/rt_mi355x.h"
 #include "host_scene.hpp"
 #include "octree.hpp"
+#include "wbvh.hpp"
 #include "renderer.hpp"
 
 namespace {
@@ -404,6 +408,99 @@ int rt_octree_digest(const float* tri9, int64_t n, int32_t max_depth, int32_t le
         return RT_OK;
     } catch (const std::bad_alloc&) {
         g_err = "rt_octree_digest: out of host memory";
+        return RT_ENOMEM;
+    }
+}
+
+int rt_wbvh_query(const float* tri9, int64_t n, int32_t max_depth, int32_t leaf_max_obj_count, const float* orig,
+                  const float* dir, int64_t nrays, int32_t* status, int32_t* id, float* t, float* u, float* v,
+                  int64_t stats[8], float* ms)
+{
+    if (n < 0 || (n > 0 && !tri9) || nrays < 0 || (nrays > 0 && (!orig || !dir || !status || !id || !t || !u || !v)))
+        return bad("rt_wbvh_query: bad arguments");
+    try {
+        rt::FlatOctree f;
+        rt::WBvh w;
+        auto t0 = std::chrono::steady_clock::now();
+        rt::build_flat_octree(tri9, n, max_depth, leaf_max_obj_count, f);
+        auto t1 = std::chrono::steady_clock::now();
+        rt::build_wbvh(f, w);
+        if (ms) {
+            ms[0] = std::chrono::duration<float, std::milli>(t1 - t0).count();
+            ms[1] = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t1).count();
+        }
+        float S = 0.0f;
+        if (!f.nodes.empty())
+            for (int a = 0; a < 3; a++)
+                S = std::max(S, std::max(std::fabs(f.nodes[0].dn[a]), std::fabs(f.nodes[0].df[a])));
+        const bool usable = !w.nodes.empty() && S > 0x1p-20f && S < 0x1p20f;
+        std::atomic<int64_t> work_n{0}, work_t{0};
+        auto body = [&](int64_t b, int64_t e) {
+            rt::WStackLocal stk;
+            uint32_t wk[2] = {0, 0};
+            for (int64_t i = b; i < e; i++) {
+                rt::v3 o = rt::mk(orig[3 * i], orig[3 * i + 1], orig[3 * i + 2]);
+                rt::v3 d = rt::mk(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]);
+                bool nan = false;
+                for (int p = 0; p < rt::NPLANES; p++) {
+                    rt::v3 pn = rt::mk(rt::PLANE_N[p][0], rt::PLANE_N[p][1], rt::PLANE_N[p][2]);
+                    float den = rt::dot(pn, d), num = rt::dot(pn, o);
+                    nan |= den != den || num != num;
+                }
+                id[i] = -1;
+                t[i] = -1.0f;
+                u[i] = 1.0f;
+                v[i] = 0.0f;
+                if (f.nodes.empty()) {
+                    status[i] = rt::W_MISS;
+                    continue;
+                }
+                if (!usable || nan) {
+                    status[i] = rt::W_UNCERT;
+                    continue;
+                }
+                float om = std::max(std::fabs(o.x), std::max(std::fabs(o.y), std::fabs(o.z)));
+                float m = 0x1p-16f * (om + S);
+                rt::WHit h;
+                int st = rt::wbvh_closest(w.nodes.data(), w.tris.data(), o, d, m, stk, h, wk);
+                if (st == rt::W_HIT) {
+                    int32_t slot = w.slot[(size_t)h.k];
+                    if (rt::kdop_certifies(f.nodes[w.leaf_of_slot[(size_t)slot]], o, d, h.t)) {
+                        id[i] = f.tri_id[(size_t)slot];
+                        t[i] = h.t;
+                        u[i] = h.u;
+                        v[i] = h.v;
+                    } else
+                        st = rt::W_UNCERT;
+                }
+                status[i] = st;
+            }
+            work_n += wk[0];
+            work_t += wk[1];
+        };
+        unsigned hc = std::max(1u, std::min(std::thread::hardware_concurrency(), 16u));
+        std::vector<std::thread> th;
+        int64_t chunk = (nrays + hc - 1) / hc;
+        for (unsigned k = 0; k < hc; k++) {
+            int64_t b = (int64_t)k * chunk, e = std::min(nrays, b + chunk);
+            if (b < e)
+                th.emplace_back(body, b, e);
+        }
+        for (auto& x : th)
+            x.join();
+        if (stats) {
+            stats[0] = w.stats.nodes;
+            stats[1] = w.stats.leaves;
+            stats[2] = w.stats.max_leaf;
+            stats[3] = w.stats.depth;
+            stats[4] = work_n.load();
+            stats[5] = work_t.load();
+            stats[6] = rt::check_wbvh(f, w);
+            stats[7] = (int64_t)(w.stats.sah * 1000.0f);
+        }
+        return RT_OK;
+    } catch (const std::bad_alloc&) {
+        g_err = "rt_wbvh_query: out of host memory";
         return RT_ENOMEM;
     }
 }

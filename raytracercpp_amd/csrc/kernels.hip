@@ -20,6 +20,7 @@
 // bit-identical to the reference compiled with -ffp-contract=off.
 #include "kparams.hpp"
 #include "rt_math.hpp"
+#include "wbvh.hpp"
 
 namespace rt {
 
@@ -1031,8 +1032,63 @@ __device__ __forceinline__ void shapes_closest(const KParams& P, v3 o, v3 d, Rec
     }
 }
 
+// The lane's wide-BVH traversal stack: entry i at lv[i * BLOCK] (the LDS of the octree
+// level stack, which is not live during the wide-BVH query).
+struct WStackLds {
+    uint2* base;
+    __device__ __forceinline__ void put(int i, uint2 v) { base[i * BLOCK] = v; }
+    __device__ __forceinline__ uint2 get(int i) const { return base[i * BLOCK]; }
+};
+
+// BVH::intersect through the wide BVH and its certificate (wbvh.hpp).
+// Returns true with (h, r) = the reference's record and boolean when the query is
+// certified; false when it must be traced through the octree.
+__device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit& h, bool& r, uint2* lv)
+{
+    const float om = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
+    WStackLds stk{lv};
+    WHit w;
+#if RT_COUNT
+    uint32_t wk[2] = {0, 0};
+    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk);
+    if (P.counters) {
+        atomicAdd(&P.counters[10], (unsigned long long)wk[0]);
+        atomicAdd(&P.counters[11], (unsigned long long)wk[1]);
+    }
+#else
+    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w);
+#endif
+    if (st == W_MISS) {
+        h.t = -1.0f;
+        h.u = 1.0f;
+        h.v = 0.0f;
+        h.k = -1;
+        r = false;
+        return true;
+    }
+    if (st == W_HIT) {
+        const int32_t slot = P.wslot[w.k];
+        const GNode leaf = P.nodes[P.wleaf[slot]];
+        if (kdop_certifies(leaf, o, d, w.t)) {
+            h.t = w.t;
+            h.u = w.u;
+            h.v = w.v;
+            h.k = slot;
+            r = true;
+            return true;
+        }
+    }
+#if RT_COUNT
+    if (P.counters)
+        atomicAdd(&P.counters[12], 1ull);
+#endif
+    return false;
+}
+
 // Closest hit over the BVH then the analytic shapes (renderer.cpp:1015-1037).
 // fin is the caller's HitInfo; returns the source (-1 none, >=0 triangle, -2-k shape k).
+// With the wide BVH (P.wnodes), a certified query takes its answer; one it cannot certify
+// is deferred to the ray-group pass (budget > 0) or traced through the octree here.
 template <bool GRP = false>
 __device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv, uint32_t budget = 0,
                            bool* aborted = nullptr)
@@ -1042,9 +1098,17 @@ __device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv, ui
     int src = -1;
     if (P.enable_bvh) {
         THit h;
-        bool r = bvh_closest<false, GRP>(P, R, h, lv, budget, aborted);
-        if (budget && *aborted)
-            return -1;
+        bool r = false;
+        const bool wide = !GRP && P.wnodes && P.nnodes > 0 && !R.nan;
+        if (!(wide && wide_closest(P, o, d, h, r, lv))) {
+            if (wide && budget) {
+                *aborted = true;   // not certified: the deferred pass traces it through the octree
+                return -1;
+            }
+            r = bvh_closest<false, GRP>(P, R, h, lv, budget, aborted);
+            if (budget && *aborted)
+                return -1;
+        }
         bvh_record(P, h, r, local, fin, src);
     } else {
         // brute-force loop, renderer.cpp:1021-1027: fin takes every hit nearer
@@ -1434,9 +1498,40 @@ __device__ __forceinline__ int global_row(const KParams& P, int lr)
     return (band * P.nranks + P.rank) * P.band_rows + (lr - band * P.band_rows);
 }
 
+// The persistent tile queue, sharded: shard s owns tiles [s T / 8, (s + 1) T / 8) (bands
+// of image rows) and its head counter sits on its own 128-B line.  A wave starts on the
+// shard of its block's XCD group (blockIdx % 8: blocks b and b + 8 share an XCD, so a
+// band's rays share that XCD's L2) and moves to the next shard when its own is empty;
+// it is done once it has found all eight empty.  One head word serves ~88 dequeues per
+// microsecond (MI355X_MICROARCH.md, dequeue row), under the frame's 130K tiles at ~2 ms.
+struct TileQueue {
+    int shard, empty;
+};
+
+__device__ __forceinline__ TileQueue tile_queue_begin() { return TileQueue{(int)(blockIdx.x & (TILE_SHARDS - 1)), 0}; }
+
+// next tile for the calling wave (wave-uniform), or -1 when every shard is empty
+__device__ __forceinline__ int tile_queue_next(const KParams& P, TileQueue& q, int ntiles)
+{
+    const int lane = threadIdx.x & 63;
+    while (q.empty < TILE_SHARDS) {
+        const int b0 = (int)((long long)ntiles * q.shard / TILE_SHARDS);
+        const int b1 = (int)((long long)ntiles * (q.shard + 1) / TILE_SHARDS);
+        int t = 0;
+        if (lane == 0)
+            t = (int)atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[NCOUNTERS + 16 * q.shard]), 1u);
+        t = __builtin_amdgcn_readfirstlane(t);
+        if (b0 + t < b1)
+            return b0 + t;
+        q.empty++;
+        q.shard = (q.shard + 1) & (TILE_SHARDS - 1);
+    }
+    return -1;
+}
+
 // Renderer::ray_trace (renderer.cpp:1068-1116): one lane per pixel, one wave
-// per 8x8 tile.  Waves are persistent and pull tiles from a device-scope
-// counter (P.counters[2]): shadow-ray-heavy tiles cluster around the object, so
+// per 8x8 tile.  Waves are persistent and pull tiles from the sharded device-scope
+// queue (tile_queue_next): shadow-ray-heavy tiles cluster around the object, so
 // a static block -> tile (-> XCD) mapping leaves whole XCDs idle while others
 // still trace; dynamic pulling keeps every CU busy until the queue drains.
 template <bool REFL>
@@ -1448,12 +1543,10 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
     const int ntiles = P.tiles_x * P.tiles_y;
     v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
     unsigned nshadow = 0, nrefl = 0;
+    TileQueue q = tile_queue_begin();
     for (;;) {
-        int tile = 0;
-        if (lane == 0)
-            tile = (int)atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[2]), 1u);
-        tile = __builtin_amdgcn_readfirstlane(tile);
-        if (tile >= ntiles)
+        const int tile = tile_queue_next(P, q, ntiles);
+        if (tile < 0)
             break;
         int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
         int px = tx * 8 + (lane & 7);
@@ -2716,6 +2809,16 @@ __global__ __launch_bounds__(BLOCK) void trace_rays_kernel(KParams P, const floa
     out_ret[i] = r ? 1 : 0;
 }
 
+// dynamic LDS of the traversal kernels: the octree level stack, or the wide-BVH stack
+// (the same memory; a lane uses one at a time)
+size_t lds_bytes(const KParams& P)
+{
+    int entries = P.levels > 0 ? P.levels : 1;
+    if (P.wnodes && entries < W_STACK)
+        entries = W_STACK;
+    return (size_t)entries * BLOCK * sizeof(uint2);
+}
+
 }  // namespace rt
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_trace_rays(const rt::KParams* P, const float* o, const float* d, int n, int32_t* id,
@@ -2723,7 +2826,7 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_trace_rays
 {
     if (n <= 0)
         return hipSuccess;
-    size_t lds = (size_t)(P->levels > 0 ? P->levels : 1) * rt::BLOCK * sizeof(uint2);
+    size_t lds = rt::lds_bytes(*P);
     hipLaunchKernelGGL(rt::trace_rays_kernel, dim3((n + rt::BLOCK - 1) / rt::BLOCK), dim3(rt::BLOCK), lds, stream, *P,
                        o, d, n, id, t, u, v, ret);
     return hipGetLastError();
@@ -2737,7 +2840,7 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(
     // persistent waves: enough blocks to fill every CU (surplus blocks find the queue empty)
     if (blocks > P->max_blocks && P->max_blocks > 0)
         blocks = P->max_blocks;
-    size_t lds = (size_t)(P->levels > 0 ? P->levels : 1) * rt::BLOCK * sizeof(uint2);
+    size_t lds = rt::lds_bytes(*P);
     if (P->has_reflection)
         hipLaunchKernelGGL(rt::ray_trace_kernel<true>, dim3(blocks), dim3(rt::BLOCK), lds, stream, *P);
     else if (P->enable_bvh && P->pipeline)
@@ -2776,7 +2879,7 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_level
         blocks = P->max_blocks;
     if (blocks < 1)
         return hipSuccess;
-    size_t lds = (size_t)(P->levels > 0 ? P->levels : 1) * rt::BLOCK * sizeof(uint2);
+    size_t lds = rt::lds_bytes(*P);
     hipLaunchKernelGGL(rt::refl_level0_kernel, dim3(blocks), dim3(rt::BLOCK), lds, stream, *P, fr1, nfr1);
     return hipGetLastError();
 }
@@ -2790,7 +2893,7 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_stage
         return hipSuccess;
     int nslot = nframes * A->stride;
     dim3 gs((nslot + rt::BLOCK - 1) / rt::BLOCK), gf((nframes + rt::BLOCK - 1) / rt::BLOCK);
-    size_t lds = (size_t)(P->levels > 0 ? P->levels : 1) * rt::BLOCK * sizeof(uint2);
+    size_t lds = rt::lds_bytes(*P);
     switch (stage) {
     case 1: hipLaunchKernelGGL(rt::refl_trace_kernel, gs, dim3(rt::BLOCK), lds, stream, *P, *A); break;
     case 2: hipLaunchKernelGGL(rt::refl_pass1_kernel, gf, dim3(rt::BLOCK), 0, stream, *P, *A); break;
@@ -2852,7 +2955,7 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_raster_sha
         blocks = P->max_blocks;
     if (blocks < 1)
         return hipSuccess;
-    size_t lds = (size_t)(P->levels > 0 ? P->levels : 1) * rt::BLOCK * sizeof(uint2);
+    size_t lds = rt::lds_bytes(*P);
     hipLaunchKernelGGL(rt::raster_shade_kernel, dim3(blocks), dim3(rt::BLOCK), lds, stream, *P, *A, fr1, nfr1);
     return hipGetLastError();
 }

@@ -5,13 +5,16 @@
 #include <stdint.h>
 
 #include "octree.hpp"
+#include "wbvh.hpp"
 
 namespace rt {
 
 constexpr int TEX_SLOTS = 6;   // ao, diffuse, normal, displacement, roughness, skysphere (renderer.h:77-84)
 constexpr int MAT_STRIDE = 16; // see include/rt_mi355x.h
 constexpr int MAX_SHAPES = 64;
-constexpr int NCOUNTERS = 16;  // KParams::counters entries (u64)
+constexpr int NCOUNTERS = 16;  // KParams::counters entries (u64) before the tile-queue heads
+constexpr int TILE_SHARDS = 8; // tile-queue shards (one per XCD group, blockIdx % 8)
+constexpr int NCOUNTER_WORDS = NCOUNTERS + 16 * TILE_SHARDS;   // + one 128-B line per shard head
 
 enum TexSlot { TEX_AO = 0, TEX_DIFFUSE = 1, TEX_NORMAL = 2, TEX_DISPLACEMENT = 3, TEX_ROUGHNESS = 4, TEX_SKYSPHERE = 5 };
 enum Shading { RT_SHADING = 0, ABS_NORMALS = 1, PASTEL_NORMALS = 2, BARYCENTRIC = 3, VISUALIZE_AO = 4 };
@@ -33,6 +36,11 @@ struct KParams {
     const float* lslab;       // [8] per GTri slot, at each leaf's first slot: box lo xyz, smin, hi xyz, smax
                               // along the cone axis; nullptr: none (kernels.hip leaf_missed)
     float scene_scale;        // largest |vertex coordinate| (leaf_missed's margin)
+    // the wide BVH (wbvh.hpp; nullptr: off) -- closest-hit queries certified against the octree
+    const WNode* wnodes;
+    const GTri* wtris;           // octree records in wide-BVH leaf order
+    const int32_t* wslot;        // wide-BVH triangle -> octree GTri slot
+    const uint32_t* wleaf;       // octree GTri slot -> flattened octree leaf node
     int32_t nnodes;
     int32_t ntri_slots;       // GTri count (brute-force loop bound when enable_bvh == 0)
     int32_t levels;           // flattened tree depth + 1 (LDS level-stack entries per lane)
@@ -94,7 +102,9 @@ struct KParams {
     uint8_t* shadow;
     unsigned long long* counters;   // [NCOUNTERS]: [0] shadow rays, [1] reflection rays, [2] tile queue head,
                                     // [3] deferred-pixel list head, [4..7] executed k-DOP / MT tests of
-                                    // whole-line / segment queries and [8..9] of abandoned queries (RT_COUNT)
+                                    // whole-line / segment queries and [8..9] of abandoned queries, [10..11]
+                                    // wide-BVH node visits / triangle tests, [12] uncertified queries (RT_COUNT);
+                                    // then the tile-queue heads, shard s at counters[NCOUNTERS + 16 s]
     // SSAO inputs (enable_ssao): Renderer::_z_buffer / _normal_buffer, renderer.cpp:1107-1110, 975-979
     float* zbuf;
     float4* nbuf;

@@ -93,7 +93,8 @@ int Renderer::init(std::string& err)
     DevBuf* all[] = {&d_nodes_, &d_tris_,  &d_tri_id_, &d_tri_mat_, &d_tri_uv_, &d_mats_,   &d_internal_,
                      &d_image_, &d_rgba_,  &d_hit_id_, &d_hit_t_,   &d_shadow_, &d_counters_, &d_band_tmp_, &d_defer_,
                      &d_tri9_,  &d_rcount_, &d_roff_,  &d_pieces_,  &d_piece_uv_, &d_zkey_, &d_big_, &d_scan_tmp_,
-                     &d_zbuf_,  &d_nbuf_,   &d_ao_,     &d_cones_, &d_lslab_};
+                     &d_zbuf_,  &d_nbuf_,   &d_ao_,     &d_cones_, &d_lslab_, &d_wnodes_, &d_wtris_, &d_wslot_,
+                     &d_wleaf_};
     for (DevBuf* b : all) b->device = device_;
     for (auto& b : d_tex_) b.device = device_;
     for (auto& b : d_sky_) b.device = device_;
@@ -516,6 +517,26 @@ int Renderer::ensure_device_scene()
             cones_.clear();
             lslab_.clear();
         }
+        // the wide BVH (wbvh.hpp): RT_WBVH=0 (at build time) skips it
+        const char* wenv = getenv("RT_WBVH");
+        if (s_.enable_bvh && !(wenv && wenv[0] == '0'))
+            build_wbvh(oct_, wb_);
+        else
+            wb_ = WBvh();
+        if (!wb_.nodes.empty()) {
+            size_t wn = wb_.nodes.size() * sizeof(WNode), wt = wb_.tris.size() * sizeof(GTri);
+            if ((e = d_wnodes_.reserve(wn)) != hipSuccess || (e = d_wtris_.reserve(wt)) != hipSuccess ||
+                (e = d_wslot_.reserve(wb_.slot.size() * 4)) != hipSuccess ||
+                (e = d_wleaf_.reserve(wb_.leaf_of_slot.size() * 4)) != hipSuccess)
+                return hip_fail(e, "hipMalloc (wide BVH)");
+            if ((e = hipMemcpyAsync(d_wnodes_.p, wb_.nodes.data(), wn, hipMemcpyHostToDevice, stream_)) != hipSuccess ||
+                (e = hipMemcpyAsync(d_wtris_.p, wb_.tris.data(), wt, hipMemcpyHostToDevice, stream_)) != hipSuccess ||
+                (e = hipMemcpyAsync(d_wslot_.p, wb_.slot.data(), wb_.slot.size() * 4, hipMemcpyHostToDevice,
+                                    stream_)) != hipSuccess ||
+                (e = hipMemcpyAsync(d_wleaf_.p, wb_.leaf_of_slot.data(), wb_.leaf_of_slot.size() * 4,
+                                    hipMemcpyHostToDevice, stream_)) != hipSuccess)
+                return hip_fail(e, "upload (wide BVH)");
+        }
         size_t nb = oct_.nodes.size() * sizeof(GNode), tb = oct_.tris.size() * sizeof(GTri);
         if ((e = d_nodes_.reserve(nb)) != hipSuccess || (e = d_tris_.reserve(tb)) != hipSuccess ||
             (e = d_tri_id_.reserve(oct_.tri_id.size() * 4)) != hipSuccess ||
@@ -632,6 +653,16 @@ void Renderer::fill_params(KParams& P) const
     if (!oct_.nodes.empty())
         for (int c = 0; c < 3; c++)
             P.scene_scale = std::max(P.scene_scale, std::max(std::fabs(oct_.nodes[0].dn[c]), std::fabs(oct_.nodes[0].df[c])));
+    // wide BVH: closest-hit queries certified against the octree, when it
+    // was built, the scene's scale keeps the certificate's rounding margins (as for the
+    // segment queries), and RT_WBVH is not 0
+    const char* wenv = getenv("RT_WBVH");
+    if (!wb_.nodes.empty() && !(wenv && wenv[0] == '0') && P.scene_scale > 0x1p-20f && P.scene_scale < 0x1p20f) {
+        P.wnodes = d_wnodes_.as<WNode>();
+        P.wtris = d_wtris_.as<GTri>();
+        P.wslot = d_wslot_.as<int32_t>();
+        P.wleaf = d_wleaf_.as<uint32_t>();
+    }
     P.nnodes = (int32_t)oct_.nodes.size();
     P.ntri_slots = (int32_t)oct_.tris.size();
     P.levels = oct_.levels > 0 ? oct_.levels : 1;
@@ -713,7 +744,9 @@ int Renderer::launch_trace(const KParams& P, hipStream_t stream)
         // deferred pixels (kernels.hip ray_trace_defer_kernel):
         // RT_DEFER_BUDGET (default 1000; 0 = off) and RT_GROUP_SHIFT (default 5: 32 lanes per ray)
         KParams Q = P;
-        if (P.enable_bvh && !P.has_reflection && !P.pipeline) {
+        // with the wide BVH the primary queries it cannot certify are a handful per frame
+        // (DESIGN.md 5.6): they are traced in place, and deferral stays off
+        if (P.enable_bvh && !P.has_reflection && !P.pipeline && !P.wnodes) {
             const char* bs = getenv("RT_DEFER_BUDGET");
             const char* gs = getenv("RT_GROUP_SHIFT");
             // out-of-range values (negative, above 2^32 - 1, not a number) turn deferral off
@@ -965,7 +998,7 @@ int Renderer::trace_frame()
     last_seg_ = P.seg_scale;
     size_t npx = (size_t)P.rw * P.rh;
     hipError_t e;
-    if ((e = d_internal_.reserve(npx * 4)) != hipSuccess || (e = d_counters_.reserve(NCOUNTERS * 8)) != hipSuccess)
+    if ((e = d_internal_.reserve(npx * 4)) != hipSuccess || (e = d_counters_.reserve(NCOUNTER_WORDS * 8)) != hipSuccess)
         return hip_fail(e, "hipMalloc (image)");
     if (want_rgba_ && (e = d_rgba_.reserve(npx * 16)) != hipSuccess) return hip_fail(e, "hipMalloc (rgba)");
     if (want_hit_ && ((e = d_hit_id_.reserve(npx * 4)) != hipSuccess || (e = d_hit_t_.reserve(npx * 4)) != hipSuccess))
@@ -987,7 +1020,7 @@ int Renderer::trace_frame()
     P.hit_t = want_hit_ ? d_hit_t_.as<float>() : nullptr;
     P.shadow = want_shadow_ ? d_shadow_.as<uint8_t>() : nullptr;
     P.counters = d_counters_.as<unsigned long long>();
-    if ((e = hipMemsetAsync(d_counters_.p, 0, NCOUNTERS * 8, stream_)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+    if ((e = hipMemsetAsync(d_counters_.p, 0, NCOUNTER_WORDS * 8, stream_)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
     hipEventRecord(ev_[0], stream_);
     if ((rc = launch_frame(P, stream_)) != RT_OK) return rc;
     hipEventRecord(ev_[1], stream_);
@@ -1178,6 +1211,7 @@ int Renderer::get_stats(rt_stats* out) const
     out->seg_scale = last_seg_;
     for (int i = 0; i < 4; i++) out->work[i] = last_work_[i];
     for (int i = 0; i < 2; i++) out->work_abandoned[i] = last_work_[4 + i];
+    for (int i = 0; i < 3; i++) out->work_wide[i] = last_work_[6 + i];
     out->deferred_pixels = last_deferred_;
     return RT_OK;
 }
@@ -1219,7 +1253,7 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
     P.tiles_x = (P.rw + 7) / 8;
     P.tiles_y = (P.local_rows + 7) / 8;
     hipError_t e;
-    if ((e = d_counters_.reserve(NCOUNTERS * 8)) != hipSuccess) return hip_fail(e, "hipMalloc (counters)");
+    if ((e = d_counters_.reserve(NCOUNTER_WORDS * 8)) != hipSuccess) return hip_fail(e, "hipMalloc (counters)");
     uint32_t* target = d_out;
     if (f > 1) {
         if ((e = d_band_tmp_.reserve((size_t)P.rw * P.local_rows * 4)) != hipSuccess)
@@ -1233,7 +1267,7 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
         for (auto& ev : ring_)
             if ((e = hipEventCreate(&ev)) != hipSuccess) return hip_fail(e, "hipEventCreate");
     }
-    if ((e = hipMemsetAsync(d_counters_.p, 0, NCOUNTERS * 8, stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+    if ((e = hipMemsetAsync(d_counters_.p, 0, NCOUNTER_WORDS * 8, stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
     hipEventRecord(ring_[2 * ring_next_], stream);
     if ((rc = launch_frame(P, stream)) != RT_OK) return rc;
     hipEventRecord(ring_[2 * ring_next_ + 1], stream);
@@ -1318,7 +1352,7 @@ void Renderer::take_counters(const unsigned long long* cnt)
 {
     last_shadow_ = (int64_t)cnt[0];
     last_refl_ = (int64_t)cnt[1];
-    for (int i = 0; i < 6; i++) last_work_[i] = (int64_t)cnt[i < 4 ? 4 + i : 8 + (i - 4)];
+    for (int i = 0; i < 9; i++) last_work_[i] = (int64_t)cnt[4 + i];
     last_deferred_ = (int64_t)(cnt[3] & 0xffffffffull);
 }
 

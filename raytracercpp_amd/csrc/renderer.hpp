@@ -13,6 +13,7 @@
 #include "../../include/rt_mi355x.h"
 #include "kparams.hpp"
 #include "octree.hpp"
+#include "wbvh.hpp"
 
 namespace rt {
 
@@ -150,6 +151,9 @@ private:
     // leaf slabs, [8] per GTri slot (renderer.cpp leaf_slab)
     std::vector<float> lslab_;
     DevBuf d_lslab_;
+    // the wide BVH (wbvh.hpp): nodes, triangle records in its leaf order, slot maps
+    WBvh wb_;
+    DevBuf d_wnodes_, d_wtris_, d_wslot_, d_wleaf_;
     bool ssao_ready_ = false;   // the buffers hold the last frame's z / normals
     // raster path: caller-order triangles, per-triangle piece counts / offsets, the piece
     // table and its texcoords, the z-key buffer, the big-piece list, scan scratch
@@ -178,8 +182,8 @@ private:
     int64_t last_primary_ = 0, last_shadow_ = 0, last_refl_ = 0;
     float last_seg_ = 0;   // KParams::seg_scale of the last frame
     int64_t last_deferred_ = 0;               // pixels the last frame handed to the ray-group pass
-    int64_t last_work_[6] = {0, 0, 0, 0, 0, 0};   // RT_COUNT builds: traversal test counts of the last frame
-                                                   // (executed: whole-line, segment; then abandoned queries)
+    int64_t last_work_[9] = {};   // RT_COUNT builds: counters[4..12] of the last frame (executed k-DOP / MT
+                                  // tests: whole-line, segment, abandoned; wide-BVH nodes, triangles, uncertified)
     void take_counters(const unsigned long long* cnt);
     float kernel_ms_ = 0, post_ms_ = 0, build_ms_ = 0;
 };

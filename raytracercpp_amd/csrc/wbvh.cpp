@@ -1,0 +1,441 @@
+// wbvh.cpp -- host build of the 4-wide SAH BVH (wbvh.hpp) over the octree's triangle
+// records: binned SAH binary tree (16 bins per axis, parallel over subtrees), collapsed
+// to 4-wide nodes by repeatedly opening the child with the largest surface area.
+#include "wbvh.hpp"
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+
+namespace rt {
+
+namespace {
+
+struct Box {
+    float lo[3], hi[3];
+};
+
+inline Box empty_box() { return Box{{INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY}}; }
+inline void grow(Box& b, const Box& o)
+{
+    for (int a = 0; a < 3; a++) {
+        b.lo[a] = std::min(b.lo[a], o.lo[a]);
+        b.hi[a] = std::max(b.hi[a], o.hi[a]);
+    }
+}
+inline float area(const Box& b)
+{
+    float dx = b.hi[0] - b.lo[0], dy = b.hi[1] - b.lo[1], dz = b.hi[2] - b.lo[2];
+    if (!(dx >= 0 && dy >= 0 && dz >= 0))
+        return 0.0f;
+    return 2.0f * (dx * dy + dy * dz + dz * dx);
+}
+
+// float lower / upper bound of a double
+inline float down(double x)
+{
+    float f = (float)x;
+    return (double)f > x ? std::nextafter(f, -INFINITY) : f;
+}
+inline float up(double x)
+{
+    float f = (float)x;
+    return (double)f < x ? std::nextafter(f, INFINITY) : f;
+}
+
+// the box of a record's vertices a, a + ab, a + ac (exact sums in double, rounded outward)
+Box tri_box(const GTri& g)
+{
+    Box b;
+    for (int c = 0; c < 3; c++) {
+        double a = g.a[c], p = a + (double)g.ab[c], q = a + (double)g.ac[c];
+        b.lo[c] = down(std::min(a, std::min(p, q)));
+        b.hi[c] = up(std::max(a, std::max(p, q)));
+    }
+    return b;
+}
+
+struct BNode {
+    Box box;
+    int32_t left, right;   // left < 0: leaf
+    int32_t first, count;
+};
+
+constexpr int NBINS = 16;
+constexpr int64_t PAR_BIN = 1 << 17;     // nodes with more primitives bin with all threads
+constexpr int64_t PAR_TASK = 1 << 14;    // subtrees at least this large run on their own thread
+
+int wbvh_threads()
+{
+    if (const char* e = std::getenv("RT_BUILD_THREADS")) {
+        int v = std::atoi(e);
+        if (v >= 1)
+            return v;
+    }
+    unsigned hc = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(hc, 16u));
+}
+
+struct Builder {
+    const std::vector<Box>& pb;      // primitive boxes
+    const std::vector<float>& pc;    // primitive centroids [3 * i]
+    std::vector<int32_t>& idx;
+    std::vector<BNode>& nodes;       // preallocated, 2n - 1 nodes at most
+    std::atomic<int32_t> next{1};
+    std::atomic<int> spare;          // threads that may still be started
+
+    struct Bins {
+        int32_t cnt[3][NBINS];
+        Box box[3][NBINS];
+        void clear()
+        {
+            for (int a = 0; a < 3; a++)
+                for (int i = 0; i < NBINS; i++) {
+                    cnt[a][i] = 0;
+                    box[a][i] = empty_box();
+                }
+        }
+        void add(const Bins& o)
+        {
+            for (int a = 0; a < 3; a++)
+                for (int i = 0; i < NBINS; i++) {
+                    cnt[a][i] += o.cnt[a][i];
+                    grow(box[a][i], o.box[a][i]);
+                }
+        }
+    };
+
+    Builder(const std::vector<Box>& b, const std::vector<float>& c, std::vector<int32_t>& i, std::vector<BNode>& n,
+            int threads)
+        : pb(b), pc(c), idx(i), nodes(n), spare(threads - 1)
+    {
+    }
+
+    static int bin_of(float c, float lo, float scale)
+    {
+        int k = (int)((c - lo) * scale);
+        return k < 0 ? 0 : (k >= NBINS ? NBINS - 1 : k);
+    }
+
+    void bin_range(int32_t b, int32_t e, const float* clo, const float* scale, Bins& B) const
+    {
+        B.clear();
+        for (int32_t i = b; i < e; i++) {
+            const int32_t p = idx[(size_t)i];
+            for (int a = 0; a < 3; a++) {
+                int k = bin_of(pc[3 * (size_t)p + a], clo[a], scale[a]);
+                B.cnt[a][k]++;
+                grow(B.box[a][k], pb[(size_t)p]);
+            }
+        }
+    }
+
+    void build(int32_t ni, int32_t b, int32_t e)
+    {
+        BNode& N = nodes[(size_t)ni];
+        const int32_t n = e - b;
+        Box box = empty_box(), cb = empty_box();
+        for (int32_t i = b; i < e; i++) {
+            const int32_t p = idx[(size_t)i];
+            grow(box, pb[(size_t)p]);
+            for (int a = 0; a < 3; a++) {
+                cb.lo[a] = std::min(cb.lo[a], pc[3 * (size_t)p + a]);
+                cb.hi[a] = std::max(cb.hi[a], pc[3 * (size_t)p + a]);
+            }
+        }
+        N.box = box;
+        N.first = b;
+        N.count = n;
+        N.left = N.right = -1;
+        if (n <= 1)
+            return;
+        float scale[3];
+        bool any = false;
+        for (int a = 0; a < 3; a++) {
+            float ext = cb.hi[a] - cb.lo[a];
+            scale[a] = ext > 0 ? (float)NBINS / ext : 0.0f;
+            any |= ext > 0;
+        }
+        int best_axis = -1, best_split = -1;
+        float best_cost = INFINITY;
+        if (any) {
+            Bins B;
+            if (n >= PAR_BIN) {
+                const int nt = wbvh_threads();
+                std::vector<Bins> part((size_t)nt);
+                std::vector<std::thread> th;
+                const int32_t chunk = (n + nt - 1) / nt;
+                for (int t = 0; t < nt; t++)
+                    th.emplace_back([&, t] {
+                        int32_t cb0 = b + t * chunk, ce = std::min(e, cb0 + chunk);
+                        if (cb0 < ce)
+                            bin_range(cb0, ce, cb.lo, scale, part[(size_t)t]);
+                        else
+                            part[(size_t)t].clear();
+                    });
+                for (auto& t : th)
+                    t.join();
+                B = part[0];
+                for (int t = 1; t < nt; t++)
+                    B.add(part[(size_t)t]);
+            } else
+                bin_range(b, e, cb.lo, scale, B);
+            const float pa = area(box);
+            for (int a = 0; a < 3; a++) {
+                if (scale[a] == 0.0f)
+                    continue;
+                float ra[NBINS];
+                int32_t rc[NBINS];
+                Box acc = empty_box();
+                int32_t c = 0;
+                for (int i = NBINS - 1; i >= 1; i--) {
+                    grow(acc, B.box[a][i]);
+                    c += B.cnt[a][i];
+                    ra[i] = area(acc);
+                    rc[i] = c;
+                }
+                acc = empty_box();
+                c = 0;
+                for (int i = 0; i < NBINS - 1; i++) {
+                    grow(acc, B.box[a][i]);
+                    c += B.cnt[a][i];
+                    if (c == 0 || rc[i + 1] == 0)
+                        continue;
+                    float cost = 1.0f + (area(acc) * (float)c + ra[i + 1] * (float)rc[i + 1]) / (pa > 0 ? pa : 1.0f);
+                    if (cost < best_cost) {
+                        best_cost = cost;
+                        best_axis = a;
+                        best_split = i;
+                    }
+                }
+            }
+        }
+        int32_t mid;
+        if (best_axis >= 0) {
+            if (n <= W_MAX_LEAF && (float)n <= best_cost)
+                return;   // a leaf is no more expensive than the best split
+            const int a = best_axis;
+            const float lo = cb.lo[a], sc = scale[a];
+            auto it = std::partition(idx.begin() + b, idx.begin() + e,
+                                     [&](int32_t p) { return bin_of(pc[3 * (size_t)p + a], lo, sc) <= best_split; });
+            mid = (int32_t)(it - idx.begin());
+        } else {
+            // every centroid equal: a leaf if it fits, else halves in index order
+            if (n <= W_MAX_LEAF)
+                return;
+            mid = b + n / 2;
+        }
+        if (mid == b || mid == e)
+            mid = b + n / 2;
+        const int32_t l = next.fetch_add(2);
+        N.left = l;
+        N.right = l + 1;
+        const bool big = (mid - b) >= PAR_TASK && (e - mid) >= PAR_TASK;
+        const bool par = big && spare.fetch_sub(1) > 0;
+        if (big && !par)
+            spare.fetch_add(1);   // no thread left: give the claim back
+        if (par) {
+            std::thread t([&, l, b, mid] { build(l, b, mid); });
+            build(l + 1, mid, e);
+            t.join();
+            spare.fetch_add(1);
+        } else {
+            build(l, b, mid);
+            build(l + 1, mid, e);
+        }
+    }
+};
+
+struct Collapser {
+    const std::vector<BNode>& bn;
+    WBvh& out;
+    int64_t max_depth = 0;
+
+    uint32_t leaf_ref(const BNode& L) const
+    {
+        return W_LEAF | ((uint32_t)L.first << 3) | (uint32_t)(L.count - 1);
+    }
+
+    uint32_t emit(int32_t bi, int depth)
+    {
+        max_depth = std::max<int64_t>(max_depth, depth);
+        int32_t c[4];
+        int nc = 0;
+        const BNode& N = bn[(size_t)bi];
+        if (N.left < 0)
+            c[nc++] = bi;   // a leaf root: one child
+        else {
+            c[nc++] = N.left;
+            c[nc++] = N.right;
+            while (nc < 4) {
+                int pick = -1;
+                float pa = -1.0f;
+                for (int j = 0; j < nc; j++) {
+                    const BNode& C = bn[(size_t)c[j]];
+                    if (C.left >= 0 && area(C.box) > pa) {
+                        pa = area(C.box);
+                        pick = j;
+                    }
+                }
+                if (pick < 0)
+                    break;
+                const BNode& C = bn[(size_t)c[pick]];
+                c[pick] = C.left;
+                c[nc++] = C.right;
+            }
+        }
+        const uint32_t me = (uint32_t)out.nodes.size();
+        out.nodes.emplace_back();
+        WNode w;
+        for (int j = 0; j < 4; j++) {
+            w.lox[j] = w.loy[j] = w.loz[j] = 0.0f;
+            w.hix[j] = w.hiy[j] = w.hiz[j] = 0.0f;
+            w.child[j] = W_EMPTY;
+            w.pad[j] = 0;
+        }
+        for (int j = 0; j < nc; j++) {
+            const BNode& C = bn[(size_t)c[j]];
+            w.lox[j] = C.box.lo[0]; w.hix[j] = C.box.hi[0];
+            w.loy[j] = C.box.lo[1]; w.hiy[j] = C.box.hi[1];
+            w.loz[j] = C.box.lo[2]; w.hiz[j] = C.box.hi[2];
+            if (C.left < 0) {
+                w.child[j] = leaf_ref(C);
+                out.stats.leaves++;
+                out.stats.max_leaf = std::max<int64_t>(out.stats.max_leaf, C.count);
+            } else
+                w.child[j] = emit(c[j], depth + 1);
+        }
+        out.nodes[me] = w;
+        return me;
+    }
+};
+
+}  // namespace
+
+void build_wbvh(const FlatOctree& oct, WBvh& out)
+{
+    out = WBvh();
+    const int64_t n = (int64_t)oct.tris.size();
+    out.leaf_of_slot.assign((size_t)n, 0u);
+    for (size_t i = 0; i < oct.nodes.size(); i++) {
+        const GNode& g = oct.nodes[i];
+        if (g.b & LEAF_BIT)
+            for (uint32_t s = g.a; s < g.a + (g.b & ~LEAF_BIT); s++)
+                out.leaf_of_slot[s] = (uint32_t)i;
+    }
+    if (n == 0 || n >= ((int64_t)1 << 28))
+        return;
+    std::vector<Box> pb((size_t)n);
+    std::vector<float> pc(3 * (size_t)n);
+    std::vector<int32_t> idx((size_t)n);
+    for (int64_t i = 0; i < n; i++) {
+        pb[(size_t)i] = tri_box(oct.tris[(size_t)i]);
+        for (int a = 0; a < 3; a++)
+            pc[3 * (size_t)i + a] = 0.5f * pb[(size_t)i].lo[a] + 0.5f * pb[(size_t)i].hi[a];
+        idx[(size_t)i] = (int32_t)i;
+    }
+    std::vector<BNode> bn((size_t)(2 * n));
+    const int nt = wbvh_threads();
+    Builder B(pb, pc, idx, bn, nt);
+    B.build(0, 0, (int32_t)n);
+    bn.resize((size_t)B.next.load());
+    // SAH cost of the binary tree (diagnostic)
+    {
+        const float ra = area(bn[0].box) > 0 ? area(bn[0].box) : 1.0f;
+        double s = 0;
+        for (const BNode& N : bn)
+            s += (N.left < 0 ? (double)N.count : 1.0) * area(N.box) / ra;
+        out.stats.sah = (float)s;
+    }
+    Collapser C{bn, out};
+    out.nodes.reserve(bn.size() / 2 + 1);
+    C.emit(0, 1);
+    out.stats.nodes = (int64_t)out.nodes.size();
+    out.stats.depth = C.max_depth;
+    out.stats.tris = n;
+    out.tris.resize((size_t)n);
+    out.slot.resize((size_t)n);
+    for (int64_t i = 0; i < n; i++) {
+        out.tris[(size_t)i] = oct.tris[(size_t)idx[(size_t)i]];
+        out.slot[(size_t)i] = idx[(size_t)i];
+    }
+}
+
+int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)
+{
+    int64_t bad = 0;
+    const size_t n = oct.tris.size();
+    if (w.tris.size() != n || w.slot.size() != n || w.leaf_of_slot.size() != n)
+        return 1;
+    if (n == 0)
+        return w.nodes.empty() ? 0 : 1;
+    std::vector<uint8_t> seen(n, 0), used(w.tris.size(), 0);
+    for (size_t i = 0; i < n; i++) {
+        int32_t s = w.slot[i];
+        if (s < 0 || (size_t)s >= n || seen[(size_t)s]++)
+            bad++;
+        else if (std::memcmp(&w.tris[i], &oct.tris[(size_t)s], sizeof(GTri)))
+            bad++;
+    }
+    for (size_t s = 0; s < n; s++) {
+        uint32_t L = w.leaf_of_slot[s];
+        if (L >= oct.nodes.size() || !(oct.nodes[L].b & LEAF_BIT) || s < oct.nodes[L].a ||
+            s >= oct.nodes[L].a + (oct.nodes[L].b & ~LEAF_BIT))
+            bad++;
+    }
+    // every child box holds its subtree: node boxes and triangle vertices (a, a + ab, a + ac)
+    struct Item {
+        uint32_t ref;
+        Box box;
+    };
+    std::vector<Item> stack;
+    Box all = {{-INFINITY, -INFINITY, -INFINITY}, {INFINITY, INFINITY, INFINITY}};
+    stack.push_back({0u, all});
+    auto inside = [](const Box& b, const Box& outer) {
+        for (int a = 0; a < 3; a++)
+            if (!(b.lo[a] >= outer.lo[a] && b.hi[a] <= outer.hi[a]))
+                return false;
+        return true;
+    };
+    size_t visited = 0;
+    while (!stack.empty()) {
+        Item it = stack.back();
+        stack.pop_back();
+        if (it.ref & W_LEAF) {
+            uint32_t first = (it.ref >> 3) & 0x0FFFFFFFu, cnt = (it.ref & 7u) + 1u;
+            if ((size_t)first + cnt > n) {
+                bad++;
+                continue;
+            }
+            for (uint32_t k = first; k < first + cnt; k++) {
+                if (used[k]++)
+                    bad++;
+                if (!inside(tri_box(w.tris[k]), it.box))
+                    bad++;
+            }
+            continue;
+        }
+        if (it.ref >= w.nodes.size() || ++visited > w.nodes.size()) {
+            bad++;
+            continue;
+        }
+        const WNode& N = w.nodes[it.ref];
+        for (int j = 0; j < 4; j++) {
+            if (N.child[j] == W_EMPTY)
+                continue;
+            Box cb = {{N.lox[j], N.loy[j], N.loz[j]}, {N.hix[j], N.hiy[j], N.hiz[j]}};
+            if (!inside(cb, it.box))
+                bad++;
+            stack.push_back({N.child[j], cb});
+        }
+    }
+    for (size_t k = 0; k < n; k++)
+        if (!used[k])
+            bad++;
+    return bad;
+}
+
+}  // namespace rt

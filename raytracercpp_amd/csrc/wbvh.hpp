@@ -1,0 +1,274 @@
+// wbvh.hpp -- a 4-wide SAH bounding-volume hierarchy over the octree's triangle records,
+// used to find primary-ray hits fast, and the certificate that makes its answer the
+// reference's.
+//
+// The reference's BVH::intersect (tp2/projets/bvh.h:212-287) returns the closest hit
+// among the triangles of the octree leaves it visits, folded in its visit order.  The
+// wide BVH below finds the minimum-t hit t* over ALL triangles (its boxes contain every
+// point Moller-Trumbore can report as a hit; the kernel widens them by a margin far above
+// the rounding of the test).  That is the reference's record when
+//   (1) t* is finite and > 0, no other triangle hits at exactly t*, and no tested hit is NaN;
+//   (2) the octree leaf L holding t*'s triangle passes the reference's own k-DOP test
+//       (BoundingVolume::intersect, bvh.h:79-105, the same IEEE arithmetic) with t_near <= t*.
+// Every ancestor's slabs contain L's (min / max over more triangles), and rounding is
+// monotone, so each ancestor's computed t_near is <= L's and its t_far >= L's: every node
+// on the path passes and none is skipped by the early-out (bvh.h:270: that needs an
+// earlier record t_A < t_near <= t*, and t* is the minimum).  The reference therefore
+// tests t*'s triangle and its record ends at t* with the same (t, u, v), and every node on
+// the path returns true.  A query the certificate does not cover (ties, t* <= 0 or
+// infinite, a NaN hit, a traversal stack overflow, (2) failing) is re-traced by the exact
+// octree traversal.  With no hit at all, the reference finds none either and returns false
+// with a fresh record.
+//
+// Layout (HBM): WNode 128 B = the four children's boxes as SoA (lo x / hi x / lo y /
+// hi y / lo z / hi z, four floats each), then four child links:
+//   inner child:  node index (bit 31 clear);
+//   leaf child:   W_LEAF | first << 3 | (count - 1), triangles first .. first + count - 1
+//                 of the wide BVH's own triangle order (count <= 8);
+//   no child:     W_EMPTY.
+// Triangles: GTri records (octree.hpp) copied in leaf order, plus slot[] = the octree GTri
+// slot of each, and leaf_of_slot[] = the flattened octree leaf node holding each slot.
+#pragma once
+
+#include <stdint.h>
+
+#include <vector>
+
+#include "octree.hpp"
+
+namespace rt {
+
+constexpr uint32_t W_LEAF = 0x80000000u;
+constexpr uint32_t W_EMPTY = 0xFFFFFFFFu;
+constexpr int W_MAX_LEAF = 8;
+#ifndef RT_W_STACK
+#define RT_W_STACK 16
+#endif
+constexpr int W_STACK = RT_W_STACK;   // traversal stack entries per lane (overflow: the query is not certified)
+
+struct alignas(16) WNode {
+    float lox[4], hix[4], loy[4], hiy[4], loz[4], hiz[4];
+    uint32_t child[4];
+    uint32_t pad[4];
+};
+static_assert(sizeof(WNode) == 128, "WNode must be 128 B");
+
+struct WStats {
+    int64_t nodes = 0, leaves = 0, tris = 0, max_leaf = 0, depth = 0;
+    float sah = 0.0f;   // SAH cost of the binary tree (traversal 1, triangle 1), for diagnostics
+};
+
+struct WBvh {
+    std::vector<WNode> nodes;          // nodes[0] = root (empty when there are no triangles)
+    std::vector<GTri> tris;            // octree records in leaf order
+    std::vector<int32_t> slot;         // wide-BVH triangle -> octree GTri slot
+    std::vector<uint32_t> leaf_of_slot;   // octree GTri slot -> flattened octree leaf node
+    WStats stats;
+};
+
+// Binned-SAH binary build over the octree's triangle records, collapsed to 4-wide nodes
+// (RT_BUILD_THREADS threads, as the octree build).  Boxes are the records' vertices a,
+// a + ab, a + ac rounded outward to float.
+void build_wbvh(const FlatOctree& oct, WBvh& out);
+
+// Structural check (CPU tests): every octree slot exactly once, each child box holds its
+// subtree's boxes / its triangles' vertices, leaf sizes within W_MAX_LEAF, leaf_of_slot
+// consistent with the octree.  Returns the number of violations.
+int64_t check_wbvh(const FlatOctree& oct, const WBvh& w);
+
+// ---------------------------------------------------------------------------------
+// Traversal (host and device).  One query: the closest Moller-Trumbore hit over the
+// wide BVH, then the certificate against the octree.
+
+// Triangle::intersect, triangle.cpp:25-91 (backface culling), on a GTri record: the
+// same expressions in the same order as the reference (and kernels.hip tri_test_rec).
+RT_HD bool mt_record(const GTri& T, v3 o, v3 d, float& t_out, float& u_out, float& v_out)
+{
+    v3 a = mk(T.a[0], T.a[1], T.a[2]);
+    v3 ab = mk(T.ab[0], T.ab[1], T.ab[2]);
+    v3 ac = mk(T.ac[0], T.ac[1], T.ac[2]);
+    v3 n = mk(T.n[0], T.n[1], T.n[2]);
+    v3 OA = o - a;
+    v3 nd = -d;
+    v3 m = cross(nd, OA);
+    float Mdet = dot(n, nd);
+    if (Mdet <= 0)
+        return false;
+    float inv = 1 / Mdet;
+    float u = dot(m, ac) * inv;
+    if (u < 0 || u > 1)
+        return false;
+    float v = dot(m, -ab) * inv;
+    if (v < 0 || u + v > 1)
+        return false;
+    float t = dot(n, OA) * inv;
+    t_out = t;
+    u_out = u;
+    v_out = v;
+    return !(t < 0);
+}
+
+// BoundingVolume::intersect (bvh.h:79-105) with the ray's plane products as
+// OctreeNode::intersect computes them (bvh.h:216-223), branch-free as kernels.hip
+// vol_test: returns pass && t_near <= t.
+RT_HD bool kdop_certifies(const GNode& nd, v3 o, v3 d, float t)
+{
+    float t_near = -INFINITY, t_far = INFINITY;
+#pragma unroll
+    for (int i = 0; i < NPLANES; i++) {
+        v3 n = mk(PLANE_N[i][0], PLANE_N[i][1], PLANE_N[i][2]);
+        float den = dot(n, d);
+        float num = dot(n, o);
+        if (den == 0.0f)
+            num = __builtin_nanf("");   // skipped plane (bvh.h:86-87): NaN quotients are ignored
+        float d0 = (nd.dn[i] - num) / den;
+        float d1 = (nd.df[i] - num) / den;
+        t_near = fmaxf(t_near, fminf(d0, d1));
+        t_far = fminf(t_far, fmaxf(d0, d1));
+    }
+    return !(t_far < t_near) && t_near <= t;
+}
+
+RT_HD uint32_t fbits(float f) { return __builtin_bit_cast(uint32_t, f); }
+RT_HD float bitsf(uint32_t u) { return __builtin_bit_cast(float, u); }
+
+enum WStatus : int { W_MISS = 0, W_HIT = 1, W_UNCERT = 2 };
+
+struct WHit {
+    float t, u, v;
+    int32_t k;   // wide-BVH triangle index (W_HIT)
+};
+
+// A lane's traversal stack: entry (child link, entry t).
+struct WStackLocal {   // host
+    uint2 e[W_STACK];
+    RT_HD void put(int i, uint2 v) { e[i] = v; }
+    RT_HD uint2 get(int i) const { return e[i]; }
+};
+
+// Closest hit over the wide BVH for the ray (o, d).  m: box margin (2^-16 (max|o| + scene
+// scale), the leaf-slab margin of kernels.hip leaf_missed).  Returns W_MISS (no triangle
+// hits), W_HIT (h = the unique minimum-t hit, finite and > 0: still to be certified by
+// kdop_certifies on its octree leaf) or W_UNCERT.  work (optional): {nodes, triangles}.
+template <class Stack>
+RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m, Stack& stk, WHit& h,
+                       uint32_t* work = nullptr)
+{
+    h.t = INFINITY;
+    h.u = 1.0f;
+    h.v = 0.0f;
+    h.k = -1;
+    // slab parameters: t = (lo - (o + m)) / d and (hi - (o - m)) / d over the box widened by m
+    const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
+    const float olx = o.x + m, oly = o.y + m, olz = o.z + m;
+    const float ohx = o.x - m, ohy = o.y - m, ohz = o.z - m;
+    constexpr float SL = 0x1p-20f;   // relative slack over the rounding of a slab parameter (<= 3 ulp)
+    float best_s = INFINITY;         // h.t plus slack: a child entered at or below it may hold a hit <= h.t
+    bool tie = false, nanhit = false, infhit = false, overflow = false;
+    int sp = 0;
+    uint32_t cur = 0;   // root node
+    uint32_t nn = 0, nt = 0;
+    while (cur != W_EMPTY) {
+        // ---- inner nodes: test the four child boxes, go to the nearest, push the others ----
+        while (cur != W_EMPTY && !(cur & W_LEAF)) {
+            nn++;
+            const float4* p = reinterpret_cast<const float4*>(nodes + cur);
+            const float4 LX = p[0], HX = p[1], LY = p[2], HY = p[3], LZ = p[4], HZ = p[5];
+            const uint4 CH = reinterpret_cast<const uint4*>(p)[6];
+            const float lx[4] = {LX.x, LX.y, LX.z, LX.w}, hx[4] = {HX.x, HX.y, HX.z, HX.w};
+            const float ly[4] = {LY.x, LY.y, LY.z, LY.w}, hy[4] = {HY.x, HY.y, HY.z, HY.w};
+            const float lz[4] = {LZ.x, LZ.y, LZ.z, LZ.w}, hz[4] = {HZ.x, HZ.y, HZ.z, HZ.w};
+            const uint32_t ch[4] = {CH.x, CH.y, CH.z, CH.w};
+            float key[4];
+            uint32_t ref[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                float ax = (lx[j] - olx) * ix, bx = (hx[j] - ohx) * ix;
+                float ay = (ly[j] - oly) * iy, by = (hy[j] - ohy) * iy;
+                float az = (lz[j] - olz) * iz, bz = (hz[j] - ohz) * iz;
+                float tmin = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+                float tmax = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+                float tmax_s = tmax + fabsf(tmax) * SL;
+                bool ok = ch[j] != W_EMPTY && tmin <= tmax_s && tmin <= best_s && tmax_s >= 0.0f;
+                key[j] = ok ? fminf(tmin, 3.0e38f) : INFINITY;
+                ref[j] = ch[j];
+            }
+            // sort the four (key, ref) pairs ascending: misses (INFINITY) go last
+#define W_CSWAP(a, b)                                                              \
+    if (key[b] < key[a]) {                                                         \
+        float tk = key[a]; key[a] = key[b]; key[b] = tk;                           \
+        uint32_t tr = ref[a]; ref[a] = ref[b]; ref[b] = tr;                        \
+    }
+            W_CSWAP(0, 1) W_CSWAP(2, 3) W_CSWAP(0, 2) W_CSWAP(1, 3) W_CSWAP(1, 2)
+#undef W_CSWAP
+            if (key[0] < INFINITY) {
+                cur = ref[0];
+#pragma unroll
+                for (int j = 3; j >= 1; j--)
+                    if (key[j] < INFINITY) {
+                        if (sp < W_STACK)
+                            stk.put(sp++, make_uint2(ref[j], fbits(key[j])));
+                        else
+                            overflow = true;
+                    }
+            } else {
+                cur = W_EMPTY;
+                while (sp > 0) {
+                    uint2 e = stk.get(--sp);
+                    if (bitsf(e.y) <= best_s) {
+                        cur = e.x;
+                        break;
+                    }
+                }
+            }
+        }
+        if (cur == W_EMPTY)
+            break;
+        // ---- a leaf: its triangles, closest hit kept; equal t from another triangle is a tie ----
+        const uint32_t first = (cur >> 3) & 0x0FFFFFFFu, cnt = (cur & 7u) + 1u;
+        for (uint32_t k = first; k < first + cnt; k++) {
+            nt++;
+            float t, u, v;
+            if (mt_record(tris[k], o, d, t, u, v)) {
+                if (t != t)
+                    nanhit = true;
+                else if (t == INFINITY)
+                    infhit = true;   // overflowed t: only matters when no finite hit exists
+                else if (t < h.t) {
+                    h.t = t;
+                    h.u = u;
+                    h.v = v;
+                    h.k = (int32_t)k;
+                    tie = false;
+                    best_s = t + fabsf(t) * SL;
+                } else if (t == h.t)
+                    tie = true;
+            }
+        }
+        cur = W_EMPTY;
+        while (sp > 0) {
+            uint2 e = stk.get(--sp);
+            if (bitsf(e.y) <= best_s) {
+                cur = e.x;
+                break;
+            }
+        }
+    }
+    if (work) {
+        work[0] += nn;
+        work[1] += nt;
+    }
+    if (overflow || nanhit)
+        return W_UNCERT;
+    if (h.k < 0) {
+        if (infhit)
+            return W_UNCERT;
+        h.t = -1.0f;   // HitInfo() (hitInfo.h:8-24): t = -1, u = 1, v = 0
+        return W_MISS;
+    }
+    if (tie || !(h.t > 0.0f && h.t < INFINITY))
+        return W_UNCERT;
+    return W_HIT;
+}
+
+}  // namespace rt

@@ -1,0 +1,130 @@
+"""The wide-BVH certified closest hit (raytracercpp_amd/csrc/wbvh.hpp), run on
+the host through rt_wbvh_query (the same traversal and certificate code the primary-ray
+kernel compiles), against the oracle's BVH::intersect (bvh.h:212-287): every CERTIFIED
+query must return the reference's record and boolean bit for bit; queries it cannot
+certify go to the exact octree traversal on the GPU.  CPU only (no GPU call)."""
+import numpy as np
+import pytest
+
+from oracle.bindings import Oracle
+from raytracercpp_amd import _lib, scenes
+from raytracercpp_amd.scene import RenderSettings
+
+
+def bits(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+def _rays(rng, n, center, spread):
+    o = (center + rng.uniform(-spread, spread, size=(n, 3))).astype(np.float32)
+    d = rng.standard_normal((n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    return o, d.astype(np.float32)
+
+
+def _voxels(n=8, size=0.2, gap=0.05):
+    cube = np.array([[0, 0, 0], [1, 0, 0], [1, 1, 0], [0, 1, 0], [0, 0, 1], [1, 0, 1], [1, 1, 1], [0, 1, 1]], np.float32)
+    faces = [(0, 2, 1), (0, 3, 2), (4, 5, 6), (4, 6, 7), (0, 1, 5), (0, 5, 4), (3, 6, 2), (3, 7, 6), (0, 4, 7),
+             (0, 7, 3), (1, 2, 6), (1, 6, 5)]
+    tris = []
+    for i in range(n):
+        for j in range(n):
+            for k in range(n):
+                v = cube * size + np.array([i, j, k], np.float32) * (size + gap) - n * (size + gap) / 2
+                tris += [np.concatenate([v[f[0]], v[f[1]], v[f[2]]]) for f in faces]
+    return np.array(tris, np.float32)
+
+
+def _soup(rng, n=4000):
+    c = rng.uniform([-2.0, -1.4, -7.0], [2.0, 1.5, -2.5], (n, 3))
+    e1 = rng.normal(size=(n, 3)) * 0.25
+    e2 = rng.normal(size=(n, 3)) * 0.25
+    sl = rng.random(n) < 0.33
+    e2[sl] = e1[sl] * rng.uniform(0.5, 2.0, (int(sl.sum()), 1)) + rng.normal(size=(int(sl.sum()), 3)) * 1e-6
+    dg = rng.random(n) < 0.05
+    e2[dg] = e1[dg]
+    return np.concatenate([c, c + e1, c + e2], axis=1).astype(np.float32)
+
+
+def _check(tri, o, d, depth=12, leaf=40, max_uncert=0.01):
+    status, ids, t, u, v, stats, _ = _lib.wbvh_query(tri, o, d, depth, leaf)
+    assert stats["violations"] == 0
+    base, _ = scenes.robot1080(width=8, height=8)
+    import dataclasses
+    sc = dataclasses.replace(base, tri=np.ascontiguousarray(tri, np.float32), tri_mat=np.zeros(len(tri), np.int32),
+                             tri_uv=None)
+    oi, ot, ou, ov, orr, _ = Oracle(sc, RenderSettings(bvh_max_depth=depth, bvh_leaf_object_count=leaf)).bvh_query(o, d)
+    cert = status != 2
+    hit = status == 1
+    assert np.array_equal((orr != 0)[cert], hit[cert]), "return value"
+    assert np.array_equal(ids[hit], oi[hit]), f"{int((ids[hit] != oi[hit]).sum())} hit-ID mismatches"
+    for a, b in ((t, ot), (u, ou), (v, ov)):
+        assert np.array_equal(bits(a[hit]), bits(b[hit]))
+    assert (status == 2).mean() <= max_uncert, f"{(status == 2).mean():.4f} not certified"
+    return status, stats
+
+
+@pytest.mark.parametrize("scene_name", ["robot", "voxels", "sphere1m_surface", "grazing", "soup", "bumpy_camera"])
+def test_certified_queries_match_oracle(scene_name):
+    rng = np.random.default_rng(7)
+    max_uncert = 0.01
+    if scene_name == "robot":
+        tri = scenes.robot1080()[0].tri
+        o, d = _rays(rng, 50000, np.array([0, 0, -4], np.float32), 3.0)
+    elif scene_name == "voxels":
+        # coinciding slabs and exactly tied hits (shared cube edges and faces): ties are not certified
+        tri = _voxels()
+        o, d = _rays(rng, 50000, np.zeros(3, np.float32), 2.5)
+        d[:10000] = np.eye(3, dtype=np.float32)[rng.integers(0, 3, 10000)] * rng.choice([-1, 1], (10000, 1))
+        max_uncert = 0.2
+    elif scene_name == "grazing":
+        # tiny / zero / denormal direction components: zero slab denominators in both structures
+        tri = scenes.robot1080()[0].tri
+        o, d = _rays(rng, 50000, np.array([0, 0, -4], np.float32), 3.0)
+        tiny = rng.choice(np.array([0.0, 1e-13, -1e-13, 1e-30, -1e-41], np.float32), (50000,))
+        d[np.arange(50000), rng.integers(0, 3, 50000)] = tiny
+    elif scene_name == "soup":
+        # slivers (nearly collinear vertices) and degenerate triangles
+        tri = _soup(rng)
+        o, d = _rays(rng, 50000, np.array([0, 0, -1], np.float32), 1.0)
+    elif scene_name == "bumpy_camera":
+        sc, st = scenes.bumpy70k(width=480, height=270)
+        import tools.wbvh_probe as wp
+        o, d = wp.camera_rays(sc, st, 1)
+        tri = sc.tri
+    else:
+        # shadow-ray-like queries leaving the 1M-triangle sphere's surface
+        sc, _ = scenes.sphere1m(width=64, height=36)
+        tri = sc.tri
+        idx = rng.integers(0, sc.ntri, 20000)
+        t9 = tri[idx].reshape(-1, 3, 3).astype(np.float64)
+        p = t9.mean(axis=1)
+        n = np.cross(t9[:, 1] - t9[:, 0], t9[:, 2] - t9[:, 0])
+        n /= np.maximum(np.linalg.norm(n, axis=1, keepdims=True), 1e-30)
+        o = (p + 1e-4 * n).astype(np.float32)
+        dd = rng.standard_normal((20000, 3))
+        d = (dd / np.linalg.norm(dd, axis=1, keepdims=True)).astype(np.float32)
+    status, _ = _check(tri, o, d, max_uncert=max_uncert)
+    assert (status == 1).sum() > 0
+
+
+def test_scaled_scenes_are_not_certified():
+    """Outside 2^-20 < scale < 2^20 the certificate's rounding margins are not claimed:
+    every query goes to the exact traversal."""
+    rng = np.random.default_rng(3)
+    tri = scenes.robot1080()[0].tri
+    for f in (np.float32(1e-13), np.float32(1e13)):
+        o, d = _rays(rng, 2000, np.array([0, 0, -4], np.float32) * f, 3.0 * f)
+        status, *_ = _lib.wbvh_query(tri * f, o, d)
+        assert (status == 2).all()
+
+
+def test_structure_on_degenerate_inputs():
+    """All-equal centroids, duplicated and zero-area triangles, a single triangle."""
+    rng = np.random.default_rng(5)
+    t = rng.uniform(-1, 1, (3000, 9)).astype(np.float32)
+    t[:500] = t[0]                    # 500 copies of one triangle
+    t[500:800, 3:6] = t[500:800, 0:3]   # degenerate
+    for tri in (t, t[:1], np.repeat(t[:1], 40, axis=0)):
+        o, d = _rays(rng, 5000, np.zeros(3, np.float32), 1.5)
+        _check(tri, o, d, max_uncert=1.0)
