@@ -940,98 +940,6 @@ __device__ void parallax_occlusion_mapping(const KParams& P, int tri, float u, f
     nv = (1 - w) * v2 + w * pv;
 }
 
-// The analytic-shape part of is_shadowed (renderer.cpp:385-399); the shapes
-// read the HitInfo the BVH query left behind (t_stale).
-__device__ __forceinline__ bool shapes_shadow(const KParams& P, v3 o, v3 d, float t_stale, v3 p, v3 lp)
-{
-    if (P.nshape > 0) {
-        Rec hi = rec_fresh();
-        hi.t = t_stale;
-        for (int k = 0; k < P.nshape; k++) {
-            bool hk = P.shape_kind[k] == 0 ? sphere_test(P.shape[k], P.shape_mat[k], o, d, hi)
-                                           : plane_test(P.shape[k], P.shape_mat[k], o, d, hi);
-            if (hk) {
-                v3 q = o + d * hi.t;
-                if (length2(p - q) < length2(p - lp))
-                    return true;
-            }
-        }
-    }
-    return false;
-}
-
-// renderer.cpp:340-402
-template <bool GRP = false>
-__device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
-{
-    if (!P.compute_shadows)
-        return false;
-    v3 o = p + n * 1.0e-4f;
-    v3 d = normalize(lp - p);
-    TRay R = make_ray(P, o, d);
-    THit h;
-    bool r;
-    if (P.enable_bvh) {
-        if (P.seg_scale > 0.0f) {
-            // segment [-m, past the light]: a hit beyond hi fails the distance test below
-            // (|p - q| >= t - |n| * 1e-4), one behind the origin does not exist (t >= 0)
-            float m = seg_margin(P, R);
-            float nl = fabsf(n.x) + fabsf(n.y) + fabsf(n.z);
-            R.lo = -m;
-            R.hi = (sqrtf(length2(p - lp)) + 1.0e-4f * nl) * (1.0f + 0x1p-10f) + m;
-            r = bvh_closest_seg<GRP>(P, R, h, lv);
-        } else
-            r = bvh_closest<false, GRP>(P, R, h, lv);
-        if (r) {
-            v3 q = o + d * h.t;
-            if (length2(p - q) < length2(p - lp))
-                return true;
-        }
-    } else {
-        h.t = -1.0f;
-        for (int k = 0; k < P.ntri_slots; k++) {
-            float t, u, v;
-            if (tri_test(P.tris, (uint32_t)k, R, t, u, v)) {
-                h.t = t;
-                v3 q = o + d * h.t;
-                if (length2(p - q) < length2(p - lp))
-                    return true;
-            }
-        }
-    }
-    return shapes_shadow(P, o, d, h.t, p, lp);
-}
-
-// BACKGROUND_COLOR, renderer.cpp:19
-__device__ __forceinline__ c3 background() { return col(135.0f / 255.0f, 206.0f / 255.0f, 235.0f / 255.0f); }
-
-// The BVH branch of trace_ray (renderer.cpp:1015-1020): the query-global
-// HitInfo becomes 'local'; fin takes it when the query returned true and it is nearer.
-__device__ __forceinline__ void bvh_record(const KParams& P, const THit& h, bool r, Rec& local, Rec& fin, int& src)
-{
-    if (h.k >= 0)
-        local = tri_record(P, h);
-    else if (h.t != h.t)
-        local.t = h.t;   // NaN ray: stale NaN record
-    if (r && (local.t < fin.t || fin.t == -1)) {
-        fin = local;
-        src = local.tri;
-    }
-}
-
-// The analytic-shape loop of trace_ray (renderer.cpp:1029-1036), reusing 'local'.
-__device__ __forceinline__ void shapes_closest(const KParams& P, v3 o, v3 d, Rec& local, Rec& fin, int& src)
-{
-    for (int k = 0; k < P.nshape; k++) {
-        bool hk = P.shape_kind[k] == 0 ? sphere_test(P.shape[k], P.shape_mat[k], o, d, local)
-                                       : plane_test(P.shape[k], P.shape_mat[k], o, d, local);
-        if (hk && (local.t < fin.t || fin.t == -1)) {
-            fin = local;
-            src = -2 - k;
-        }
-    }
-}
-
 // The lane's wide-BVH traversal stack: entry i at lv[i * BLOCK] (the LDS of the octree
 // level stack, which is not live during the wide-BVH query).
 struct WStackLds {
@@ -1083,6 +991,138 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
         atomicAdd(&P.counters[12], 1ull);
 #endif
     return false;
+}
+
+// is_shadowed's BVH part through the wide BVH: the decision depends only
+// on the reference's record t.  No hit at t <= hi: every hit lies beyond the segment
+// end, which fails the distance test, so the point is lit whatever the record is.  A
+// minimum hit t* <= hi whose octree leaf certifies it is the reference's record t.
+// Returns true when decided (shadowed in *sh); false: take the octree segment query.
+__device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float hi, v3 p, v3 lp, uint2* lv, bool* sh)
+{
+    const float om = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
+    WStackLds stk{lv};
+    WHit w;
+#if RT_COUNT
+    uint32_t wk[2] = {0, 0};
+    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, hi, false);
+    if (P.counters) {
+        atomicAdd(&P.counters[10], (unsigned long long)wk[0]);
+        atomicAdd(&P.counters[11], (unsigned long long)wk[1]);
+    }
+#else
+    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, hi, false);
+#endif
+    if (st == W_MISS) {
+        *sh = false;
+        return true;
+    }
+    if (st == W_HIT && kdop_certifies(P.nodes[P.wleaf[P.wslot[w.k]]], o, d, w.t)) {
+        v3 q = o + d * w.t;
+        *sh = length2(p - q) < length2(p - lp);
+        return true;
+    }
+#if RT_COUNT
+    if (P.counters)
+        atomicAdd(&P.counters[12], 1ull);
+#endif
+    return false;
+}
+
+// The analytic-shape part of is_shadowed (renderer.cpp:385-399); the shapes
+// read the HitInfo the BVH query left behind (t_stale).
+__device__ __forceinline__ bool shapes_shadow(const KParams& P, v3 o, v3 d, float t_stale, v3 p, v3 lp)
+{
+    if (P.nshape > 0) {
+        Rec hi = rec_fresh();
+        hi.t = t_stale;
+        for (int k = 0; k < P.nshape; k++) {
+            bool hk = P.shape_kind[k] == 0 ? sphere_test(P.shape[k], P.shape_mat[k], o, d, hi)
+                                           : plane_test(P.shape[k], P.shape_mat[k], o, d, hi);
+            if (hk) {
+                v3 q = o + d * hi.t;
+                if (length2(p - q) < length2(p - lp))
+                    return true;
+            }
+        }
+    }
+    return false;
+}
+
+// renderer.cpp:340-402
+template <bool GRP = false>
+__device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
+{
+    if (!P.compute_shadows)
+        return false;
+    v3 o = p + n * 1.0e-4f;
+    v3 d = normalize(lp - p);
+    TRay R = make_ray(P, o, d);
+    THit h;
+    bool r;
+    if (P.enable_bvh) {
+        if (P.seg_scale > 0.0f) {
+            // segment [-m, past the light]: a hit beyond hi fails the distance test below
+            // (|p - q| >= t - |n| * 1e-4), one behind the origin does not exist (t >= 0)
+            float m = seg_margin(P, R);
+            float nl = fabsf(n.x) + fabsf(n.y) + fabsf(n.z);
+            R.lo = -m;
+            R.hi = (sqrtf(length2(p - lp)) + 1.0e-4f * nl) * (1.0f + 0x1p-10f) + m;
+            // (seg_scale > 0: no analytic shapes, so shapes_shadow below has nothing to add)
+            bool sh;
+            if (!GRP && P.wnodes && P.nnodes > 0 && !R.nan && wide_shadow(P, o, d, R.hi, p, lp, lv, &sh))
+                return sh;
+            r = bvh_closest_seg<GRP>(P, R, h, lv);
+        } else
+            r = bvh_closest<false, GRP>(P, R, h, lv);
+        if (r) {
+            v3 q = o + d * h.t;
+            if (length2(p - q) < length2(p - lp))
+                return true;
+        }
+    } else {
+        h.t = -1.0f;
+        for (int k = 0; k < P.ntri_slots; k++) {
+            float t, u, v;
+            if (tri_test(P.tris, (uint32_t)k, R, t, u, v)) {
+                h.t = t;
+                v3 q = o + d * h.t;
+                if (length2(p - q) < length2(p - lp))
+                    return true;
+            }
+        }
+    }
+    return shapes_shadow(P, o, d, h.t, p, lp);
+}
+
+// BACKGROUND_COLOR, renderer.cpp:19
+__device__ __forceinline__ c3 background() { return col(135.0f / 255.0f, 206.0f / 255.0f, 235.0f / 255.0f); }
+
+// The BVH branch of trace_ray (renderer.cpp:1015-1020): the query-global
+// HitInfo becomes 'local'; fin takes it when the query returned true and it is nearer.
+__device__ __forceinline__ void bvh_record(const KParams& P, const THit& h, bool r, Rec& local, Rec& fin, int& src)
+{
+    if (h.k >= 0)
+        local = tri_record(P, h);
+    else if (h.t != h.t)
+        local.t = h.t;   // NaN ray: stale NaN record
+    if (r && (local.t < fin.t || fin.t == -1)) {
+        fin = local;
+        src = local.tri;
+    }
+}
+
+// The analytic-shape loop of trace_ray (renderer.cpp:1029-1036), reusing 'local'.
+__device__ __forceinline__ void shapes_closest(const KParams& P, v3 o, v3 d, Rec& local, Rec& fin, int& src)
+{
+    for (int k = 0; k < P.nshape; k++) {
+        bool hk = P.shape_kind[k] == 0 ? sphere_test(P.shape[k], P.shape_mat[k], o, d, local)
+                                       : plane_test(P.shape[k], P.shape_mat[k], o, d, local);
+        if (hk && (local.t < fin.t || fin.t == -1)) {
+            fin = local;
+            src = -2 - k;
+        }
+    }
 }
 
 // Closest hit over the BVH then the analytic shapes (renderer.cpp:1015-1037).
@@ -2016,7 +2056,9 @@ __global__ __launch_bounds__(BLOCK) void refl_trace_kernel(KParams P, ReflArgs A
     TRay R = make_ray(P, ld3(F.ro), dir);
     THit h;
     bool r;
-    if (P.seg_scale > 0.0f) {
+    if (P.wnodes && P.nnodes > 0 && !R.nan && wide_closest(P, ld3(F.ro), dir, h, r, lv))
+        ;   // certified by the wide BVH
+    else if (P.seg_scale > 0.0f) {
         R.lo = -seg_margin(P, R);   // nothing behind the origin can be hit (t >= 0)
         r = bvh_closest_seg(P, R, h, lv);
     } else

@@ -146,13 +146,15 @@ struct WStackLocal {   // host
     RT_HD uint2 get(int i) const { return e[i]; }
 };
 
-// Closest hit over the wide BVH for the ray (o, d).  m: box margin (2^-16 (max|o| + scene
-// scale), the leaf-slab margin of kernels.hip leaf_missed).  Returns W_MISS (no triangle
-// hits), W_HIT (h = the unique minimum-t hit, finite and > 0: still to be certified by
-// kdop_certifies on its octree leaf) or W_UNCERT.  work (optional): {nodes, triangles}.
+// Closest hit over the wide BVH for the ray (o, d) among hits with t <= hi.  m: box margin
+// (2^-16 (max|o| + scene scale), the leaf-slab margin of kernels.hip leaf_missed).
+// Returns W_MISS (no triangle hits at t <= hi), W_HIT (h = the minimum-t hit, finite and
+// > 0, unique when ties: still to be certified by kdop_certifies on its octree leaf) or
+// W_UNCERT.  Shadow queries (hi = the segment end of kernels.hip is_shadowed, ties false)
+// read only the record's t.  work (optional): {nodes, triangles}.
 template <class Stack>
 RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m, Stack& stk, WHit& h,
-                       uint32_t* work = nullptr)
+                       uint32_t* work = nullptr, float hi = INFINITY, bool ties = true)
 {
     h.t = INFINITY;
     h.u = 1.0f;
@@ -163,7 +165,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
     const float olx = o.x + m, oly = o.y + m, olz = o.z + m;
     const float ohx = o.x - m, ohy = o.y - m, ohz = o.z - m;
     constexpr float SL = 0x1p-20f;   // relative slack over the rounding of a slab parameter (<= 3 ulp)
-    float best_s = INFINITY;         // h.t plus slack: a child entered at or below it may hold a hit <= h.t
+    float best_s = hi + fabsf(hi) * SL;   // h.t (or hi) plus slack: a child entered at or below it may hold a hit
     bool tie = false, nanhit = false, infhit = false, overflow = false;
     int sp = 0;
     uint32_t cur = 0;   // root node
@@ -232,6 +234,8 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
             if (mt_record(tris[k], o, d, t, u, v)) {
                 if (t != t)
                     nanhit = true;
+                else if (!(t <= hi))
+                    ;   // beyond the segment
                 else if (t == INFINITY)
                     infhit = true;   // overflowed t: only matters when no finite hit exists
                 else if (t < h.t) {
@@ -266,7 +270,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
         h.t = -1.0f;   // HitInfo() (hitInfo.h:8-24): t = -1, u = 1, v = 0
         return W_MISS;
     }
-    if (tie || !(h.t > 0.0f && h.t < INFINITY))
+    if ((ties && tie) || !(h.t > 0.0f && h.t < INFINITY))
         return W_UNCERT;
     return W_HIT;
 }
