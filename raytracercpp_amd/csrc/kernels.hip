@@ -111,7 +111,7 @@ struct NodeBox {
 __device__ __forceinline__ NodeBox load_node(const GNode* nodes, uint32_t i)
 {
     const float4* p = reinterpret_cast<const float4*>(nodes + i);
-    float4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+    float4 q0 = ldg(p), q1 = ldg(p + 1), q2 = ldg(p + 2), q3 = ldg(p + 3);
     NodeBox n;
     n.dn[0] = q0.x; n.dn[1] = q0.y; n.dn[2] = q0.z; n.dn[3] = q0.w;
     n.dn[4] = q1.x; n.dn[5] = q1.y; n.dn[6] = q1.z;
@@ -126,7 +126,7 @@ __device__ __forceinline__ NodeBox load_node(const GNode* nodes, uint32_t i)
 __device__ __forceinline__ uint2 load_node_link(const GNode* nodes, uint32_t i)
 {
     const uint4* p = reinterpret_cast<const uint4*>(nodes + i);
-    uint4 q3 = p[3];
+    uint4 q3 = ldg(p + 3);
     return make_uint2(q3.z, q3.w);
 }
 
@@ -171,9 +171,9 @@ __device__ __forceinline__ TriRec load_tri(const GTri* tris, uint32_t k)
 {
     const float4* p = reinterpret_cast<const float4*>(tris + k);
     TriRec r;
-    r.q0 = p[0];
-    r.q1 = p[1];
-    r.q2 = p[2];
+    r.q0 = ldg(p);
+    r.q1 = ldg(p + 1);
+    r.q2 = ldg(p + 2);
     return r;
 }
 
@@ -236,8 +236,8 @@ __device__ __forceinline__ bool leaf_missed(const KParams& P, uint32_t a, const 
     if (!P.lslab)
         return false;
     const float4* L = reinterpret_cast<const float4*>(P.lslab) + 2 * (size_t)a;
-    const float4 lo = L[0], hi = L[1];
-    const float4 c = reinterpret_cast<const float4*>(P.cones)[a];
+    const float4 lo = ldg(L), hi = ldg(L + 1);
+    const float4 c = ldg(reinterpret_cast<const float4*>(P.cones) + a);
     const float m = 0x1p-16f * (fmaxf(fabsf(R.o.x), fmaxf(fabsf(R.o.y), fabsf(R.o.z))) + P.scene_scale);
     const float ix = 1.0f / R.d.x, iy = 1.0f / R.d.y, iz = 1.0f / R.d.z;
     float tx0 = (lo.x - m - R.o.x) * ix, tx1 = (hi.x + m - R.o.x) * ix;
@@ -263,7 +263,7 @@ __device__ __forceinline__ bool leaf_backfacing(const KParams& P, uint32_t a, co
 {
     if (!P.cones)
         return false;
-    const float4 c = reinterpret_cast<const float4*>(P.cones)[a];
+    const float4 c = ldg(reinterpret_cast<const float4*>(P.cones) + a);
     const float dd = R.d.x * R.d.x + R.d.y * R.d.y + R.d.z * R.d.z;
     // |d| in [1e-10, 1e10]: the products of dot(n, -d) neither underflow nor overflow
     if (!(c.w > 0.0f && dd > 1.0e-20f && dd < 1.0e20f))
@@ -963,6 +963,10 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
         atomicAdd(&P.counters[10], (unsigned long long)wk[0]);
         atomicAdd(&P.counters[11], (unsigned long long)wk[1]);
     }
+#if RT_COUNT == 2
+    g_pixel_work[pixel_work_slot()].x += wk[0];
+    g_pixel_work[pixel_work_slot()].y += wk[1];
+#endif
 #else
     const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w);
 #endif
@@ -975,8 +979,8 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
         return true;
     }
     if (st == W_HIT) {
-        const int32_t slot = P.wslot[w.k];
-        const GNode leaf = P.nodes[P.wleaf[slot]];
+        const int32_t slot = ldg(P.wslot + w.k);
+        const GNode leaf = load_gnode(P.nodes + ldg(P.wleaf + slot));
         if (kdop_certifies(leaf, o, d, w.t)) {
             h.t = w.t;
             h.u = w.u;
@@ -1010,6 +1014,10 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
         atomicAdd(&P.counters[10], (unsigned long long)wk[0]);
         atomicAdd(&P.counters[11], (unsigned long long)wk[1]);
     }
+#if RT_COUNT == 2
+    g_pixel_work[pixel_work_slot()].x += wk[0];
+    g_pixel_work[pixel_work_slot()].y += wk[1];
+#endif
 #else
     const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, hi, false);
 #endif
@@ -1017,7 +1025,7 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
         *sh = false;
         return true;
     }
-    if (st == W_HIT && kdop_certifies(P.nodes[P.wleaf[P.wslot[w.k]]], o, d, w.t)) {
+    if (st == W_HIT && kdop_certifies(load_gnode(P.nodes + ldg(P.wleaf + ldg(P.wslot + w.k))), o, d, w.t)) {
         v3 q = o + d * w.t;
         *sh = length2(p - q) < length2(p - lp);
         return true;
@@ -1050,8 +1058,11 @@ __device__ __forceinline__ bool shapes_shadow(const KParams& P, v3 o, v3 d, floa
 }
 
 // renderer.cpp:340-402
-template <bool GRP = false>
-__device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
+// WIDE (the lean wide-BVH kernel; launched only with segment queries on, so the scene
+// has no analytic shapes): the decision comes from wide_shadow, or *defer is set and the
+// pixel goes to the exact pass -- no octree traversal is compiled in.
+template <bool GRP = false, bool WIDE = false>
+__device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv, bool* defer = nullptr)
 {
     if (!P.compute_shadows)
         return false;
@@ -1072,15 +1083,28 @@ __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
             bool sh;
             if (!GRP && P.wnodes && P.nnodes > 0 && !R.nan && wide_shadow(P, o, d, R.hi, p, lp, lv, &sh))
                 return sh;
+            if (WIDE) {
+                *defer = true;
+                return false;
+            }
             r = bvh_closest_seg<GRP>(P, R, h, lv);
-        } else
+        } else {
+            if (WIDE) {
+                *defer = true;
+                return false;
+            }
             r = bvh_closest<false, GRP>(P, R, h, lv);
+        }
         if (r) {
             v3 q = o + d * h.t;
             if (length2(p - q) < length2(p - lp))
                 return true;
         }
     } else {
+        if (WIDE) {
+            *defer = true;
+            return false;
+        }
         h.t = -1.0f;
         for (int k = 0; k < P.ntri_slots; k++) {
             float t, u, v;
@@ -1129,14 +1153,23 @@ __device__ __forceinline__ void shapes_closest(const KParams& P, v3 o, v3 d, Rec
 // fin is the caller's HitInfo; returns the source (-1 none, >=0 triangle, -2-k shape k).
 // With the wide BVH (P.wnodes), a certified query takes its answer; one it cannot certify
 // is deferred to the ray-group pass (budget > 0) or traced through the octree here.
-template <bool GRP = false>
+// WIDE: only the wide BVH is compiled in; an uncertified query sets *aborted (deferred).
+template <bool GRP = false, bool WIDE = false>
 __device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv, uint32_t budget = 0,
                            bool* aborted = nullptr)
 {
     Rec local = rec_fresh();
     TRay R = make_ray(P, o, d);
     int src = -1;
-    if (P.enable_bvh) {
+    if (WIDE) {
+        THit h;
+        bool r = false;
+        if (!(P.enable_bvh && P.nnodes > 0 && !R.nan && wide_closest(P, o, d, h, r, lv))) {
+            *aborted = true;
+            return -1;
+        }
+        bvh_record(P, h, r, local, fin, src);
+    } else if (P.enable_bvh) {
         THit h;
         bool r = false;
         const bool wide = !GRP && P.wnodes && P.nnodes > 0 && !R.nan;
@@ -1269,8 +1302,9 @@ __device__ c3 shade_debug(const KParams& P, const Rec& h)
     return fc;
 }
 
-template <bool GRP = false>
-__device__ Direct shade_direct(const KParams& P, v3 ro, v3 rd, Rec& h, uint2* lv, unsigned& nshadow)
+template <bool GRP = false, bool WIDE = false>
+__device__ Direct shade_direct(const KParams& P, v3 ro, v3 rd, Rec& h, uint2* lv, unsigned& nshadow,
+                               bool* defer = nullptr)
 {
     Direct out;
     out.shadowed = false;
@@ -1280,7 +1314,7 @@ __device__ Direct shade_direct(const KParams& P, v3 ro, v3 rd, Rec& h, uint2* lv
         if (P.compute_shadows)
             nshadow++;
         v3 light = mk(P.light[0], P.light[1], P.light[2]);
-        out.shadowed = is_shadowed<GRP>(P, out.ip, h.normal, light, lv);
+        out.shadowed = is_shadowed<GRP, WIDE>(P, out.ip, h.normal, light, lv, defer);
         out.fc = shade_shadow_emit(P, fc, mat_of(P, h.mat), out.shadowed);
     } else
         out.fc = shade_debug(P, h);
@@ -1382,7 +1416,10 @@ struct PixelOut {
 
 // Renderer::trace_ray (renderer.cpp:1008-1066) for one primary ray, with the
 // compute_reflection recursion (when REFL) unrolled onto an explicit stack.
-template <bool REFL, bool GRP = false>
+// WIDE (REFL false): the lean wide-BVH kernel; any query the wide BVH cannot certify sets
+// po.deferred and the pixel is re-done from scratch by the exact pass (its shadow ray is
+// counted there, not here).
+template <bool REFL, bool GRP = false, bool WIDE = false>
 __device__ PixelOut trace_pixel(const KParams& P, v3 cam, v3 rd0, uint2* lv, uint32_t pixel_key, unsigned& nshadow,
                                 unsigned& nrefl, uint32_t budget = 0)
 {
@@ -1390,13 +1427,17 @@ __device__ PixelOut trace_pixel(const KParams& P, v3 cam, v3 rd0, uint2* lv, uin
     po.fin = rec_fresh();
     po.found = po.shadowed = po.deferred = false;
     po.alpha = 1.0f;
-    po.src = closest_hit<GRP>(P, cam, rd0, po.fin, lv, REFL ? 0u : budget, &po.deferred);
+    po.src = closest_hit<GRP, WIDE && !REFL>(P, cam, rd0, po.fin, lv, REFL ? 0u : budget, &po.deferred);
     if (!REFL) {
         if (po.deferred)
             return po;
         if (po.fin.t > 0.1f) {
             po.found = true;
-            Direct D = shade_direct<GRP>(P, cam, rd0, po.fin, lv, nshadow);
+            unsigned ns = 0;
+            Direct D = shade_direct<GRP, WIDE>(P, cam, rd0, po.fin, lv, ns, &po.deferred);
+            if (po.deferred)
+                return po;
+            nshadow += ns;
             po.shadowed = D.shadowed;
             po.color = P.shading_method == RT_SHADING ? shade_finish(P, D.fc, mat_of(P, po.fin.mat), col(0, 0, 0))
                                                       : clamp3(D.fc);
@@ -1574,7 +1615,9 @@ __device__ __forceinline__ int tile_queue_next(const KParams& P, TileQueue& q, i
 // queue (tile_queue_next): shadow-ray-heavy tiles cluster around the object, so
 // a static block -> tile (-> XCD) mapping leaves whole XCDs idle while others
 // still trace; dynamic pulling keeps every CU busy until the queue drains.
-template <bool REFL>
+// WIDE: the lean kernel (wide BVH only) -- pixels it cannot certify go to
+// the deferred list and the exact pass (ray_trace_defer_kernel).
+template <bool REFL, bool WIDE = false>
 __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
 {
     extern __shared__ uint2 lds_levels[];
@@ -1609,7 +1652,7 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
 #if RT_COUNT == 2
         g_pixel_work[pixel_work_slot()] = make_uint2(0u, 0u);
 #endif
-        PixelOut po = trace_pixel<REFL>(P, cam, rd, lv, rng, nshadow, nrefl, REFL ? 0u : P.trav_budget);
+        PixelOut po = trace_pixel<REFL, false, WIDE>(P, cam, rd, lv, rng, nshadow, nrefl, REFL ? 0u : P.trav_budget);
         size_t o = (size_t)lr * P.rw + px;
         if (!REFL && po.deferred) {
             // the deferred pass (ray_trace_defer_kernel) traces it with a ray group; the
@@ -2884,14 +2927,17 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(
         blocks = P->max_blocks;
     size_t lds = rt::lds_bytes(*P);
     if (P->has_reflection)
-        hipLaunchKernelGGL(rt::ray_trace_kernel<true>, dim3(blocks), dim3(rt::BLOCK), lds, stream, *P);
+        hipLaunchKernelGGL((rt::ray_trace_kernel<true, false>), dim3(blocks), dim3(rt::BLOCK), lds, stream, *P);
     else if (P->enable_bvh && P->pipeline)
         hipLaunchKernelGGL(rt::ray_trace_pipe_kernel, dim3(blocks), dim3(rt::BLOCK), lds, stream, *P);
     else {
         rt::KParams A = *P;
         A.grp_shift = 0;   // one lane per pixel; the groups are the deferred pass's
-        hipLaunchKernelGGL(rt::ray_trace_kernel<false>, dim3(blocks), dim3(rt::BLOCK), lds, stream, A);
-        if (P->trav_budget && P->defer && P->defer_cap) {
+        if (P->wide_lean && P->defer && P->defer_cap)
+            hipLaunchKernelGGL((rt::ray_trace_kernel<false, true>), dim3(blocks), dim3(rt::BLOCK), lds, stream, A);
+        else
+            hipLaunchKernelGGL((rt::ray_trace_kernel<false, false>), dim3(blocks), dim3(rt::BLOCK), lds, stream, A);
+        if (P->defer && P->defer_cap) {
             // deferred pixels: a persistent grid of ray groups over the list ray_trace_kernel left
             int db = P->max_blocks > 0 ? P->max_blocks : 1024;
             hipLaunchKernelGGL(rt::ray_trace_defer_kernel, dim3(db), dim3(rt::BLOCK), lds, stream, *P);

@@ -91,6 +91,7 @@ struct KParams {
     // that split every leaf's triangles between them.  0 / 0: off.
     uint32_t trav_budget;
     int32_t grp_shift;
+    int32_t wide_lean;        // 1: the lean wide-BVH kernel, everything it cannot certify deferred (needs defer[])
     uint32_t* defer;
     uint32_t defer_cap;
 

@@ -744,9 +744,24 @@ int Renderer::launch_trace(const KParams& P, hipStream_t stream)
         // deferred pixels (kernels.hip ray_trace_defer_kernel):
         // RT_DEFER_BUDGET (default 1000; 0 = off) and RT_GROUP_SHIFT (default 5: 32 lanes per ray)
         KParams Q = P;
-        // with the wide BVH the primary queries it cannot certify are a handful per frame
-        // (DESIGN.md 5.6): they are traced in place, and deferral stays off
-        if (P.enable_bvh && !P.has_reflection && !P.pipeline && !P.wnodes) {
+        // With the wide BVH and segment queries (no analytic shapes, scene scale in range) the
+        // lean kernel runs: the few pixels it cannot certify go to the deferred
+        // list and the exact ray-group pass.  RT_WIDE_LEAN=0: the full kernel, which traces
+        // those queries through the octree in place.
+        const char* lean_env = getenv("RT_WIDE_LEAN");
+        size_t npx_all = (size_t)P.rw * P.local_rows;
+        if (P.wnodes && P.seg_scale > 0.0f && P.enable_bvh && !P.has_reflection && !P.pipeline &&
+            !(lean_env && lean_env[0] == '0') && npx_all > 0 && npx_all < (1ull << 32)) {
+            if ((e = d_defer_.reserve(npx_all * 4)) != hipSuccess)
+                return hip_fail(e, "hipMalloc (deferred pixels)");
+            const char* gs = getenv("RT_GROUP_SHIFT");
+            long shift = gs ? atol(gs) : 5;
+            Q.wide_lean = 1;
+            Q.trav_budget = 0;
+            Q.grp_shift = (shift >= 1 && shift <= 6) ? (int32_t)shift : 5;
+            Q.defer = d_defer_.as<uint32_t>();
+            Q.defer_cap = (uint32_t)npx_all;
+        } else if (P.enable_bvh && !P.has_reflection && !P.pipeline && !P.wnodes) {
             const char* bs = getenv("RT_DEFER_BUDGET");
             const char* gs = getenv("RT_GROUP_SHIFT");
             // out-of-range values (negative, above 2^32 - 1, not a number) turn deferral off

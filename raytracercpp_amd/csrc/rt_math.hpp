@@ -22,6 +22,20 @@ struct v3 {
     float x, y, z;
 };
 
+// A load through the global address space: pointers read out of the KParams argument
+// are generic, and a generic load is a FLAT instruction (counted in both vmcnt and
+// lgkmcnt, so LDS waits also wait for it); this one is a global_load.
+template <class T>
+RT_HD T ldg(const T* p)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(1))) T GT;
+    return *(GT*)p;
+#else
+    return *p;
+#endif
+}
+
 RT_HD v3 mk(float x, float y, float z) { return v3{x, y, z}; }
 RT_HD v3 operator-(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
 RT_HD v3 operator+(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }

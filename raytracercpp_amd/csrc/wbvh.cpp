@@ -249,6 +249,66 @@ struct Builder {
     }
 };
 
+// One 4-wide node: the children's float boxes quantised to 8 bits per plane against the
+// node box's low corner, low planes rounded down and high planes up (exact in double:
+// origin, q and the power-of-two step are all representable), so each decoded box holds
+// its float box.
+WNode quantise(const Box* cb, const uint32_t* link, int nc)
+{
+    WNode w;
+    std::memset(&w, 0, sizeof(w));
+    Box nb = empty_box();
+    for (int j = 0; j < nc; j++)
+        grow(nb, cb[j]);
+    const float org[3] = {nb.lo[0], nb.lo[1], nb.lo[2]};
+    w.ox = org[0];
+    w.oy = org[1];
+    w.oz = org[2];
+    w.exps = 0;
+    for (int a = 0; a < 3; a++) {
+        const double ext = (double)nb.hi[a] - (double)org[a];
+        int k = -100;
+        if (ext > 0) {
+            int e;
+            std::frexp(ext / 255.0, &e);   // ext / 255 <= 2^e
+            k = std::max(-100, std::min(127, e - 1));
+            while (k < 127 && std::ldexp(255.0, k) < ext)
+                k++;
+        }
+        w.exps |= (uint32_t)(127 + k) << (8 * a);
+        const double st = std::ldexp(1.0, k);
+        for (int j = 0; j < 4; j++) {
+            if (j >= nc) {
+                w.qlo[a][j] = 0;
+                w.qhi[a][j] = 0;
+                continue;
+            }
+            double lo = std::floor(((double)cb[j].lo[a] - org[a]) / st);
+            double hi = std::ceil(((double)cb[j].hi[a] - org[a]) / st);
+            w.qlo[a][j] = (uint8_t)std::max(0.0, std::min(255.0, lo));
+            w.qhi[a][j] = (uint8_t)std::max(0.0, std::min(255.0, hi));
+        }
+    }
+    for (int j = 0; j < 4; j++)
+        w.child[j] = link[j];
+    return w;
+}
+
+// the decoded box of child j (double, exact)
+Box decode(const WNode& w, int j, double lo[3], double hi[3])
+{
+    const float org[3] = {w.ox, w.oy, w.oz};
+    Box b;
+    for (int a = 0; a < 3; a++) {
+        const double st = std::ldexp(1.0, (int)((w.exps >> (8 * a)) & 0xffu) - 127);
+        lo[a] = org[a] + w.qlo[a][j] * st;
+        hi[a] = org[a] + w.qhi[a][j] * st;
+        b.lo[a] = down(lo[a]);
+        b.hi[a] = up(hi[a]);
+    }
+    return b;
+}
+
 struct Collapser {
     const std::vector<BNode>& bn;
     WBvh& out;
@@ -289,25 +349,23 @@ struct Collapser {
         }
         const uint32_t me = (uint32_t)out.nodes.size();
         out.nodes.emplace_back();
-        WNode w;
+        Box cb[4];
+        uint32_t link[4];
         for (int j = 0; j < 4; j++) {
-            w.lox[j] = w.loy[j] = w.loz[j] = 0.0f;
-            w.hix[j] = w.hiy[j] = w.hiz[j] = 0.0f;
-            w.child[j] = W_EMPTY;
-            w.pad[j] = 0;
+            cb[j] = empty_box();
+            link[j] = W_EMPTY;
         }
         for (int j = 0; j < nc; j++) {
             const BNode& C = bn[(size_t)c[j]];
-            w.lox[j] = C.box.lo[0]; w.hix[j] = C.box.hi[0];
-            w.loy[j] = C.box.lo[1]; w.hiy[j] = C.box.hi[1];
-            w.loz[j] = C.box.lo[2]; w.hiz[j] = C.box.hi[2];
+            cb[j] = C.box;
             if (C.left < 0) {
-                w.child[j] = leaf_ref(C);
+                link[j] = leaf_ref(C);
                 out.stats.leaves++;
                 out.stats.max_leaf = std::max<int64_t>(out.stats.max_leaf, C.count);
             } else
-                w.child[j] = emit(c[j], depth + 1);
+                link[j] = emit(c[j], depth + 1);
         }
+        WNode w = quantise(cb, link, nc);
         out.nodes[me] = w;
         return me;
     }
@@ -426,10 +484,17 @@ int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)
         for (int j = 0; j < 4; j++) {
             if (N.child[j] == W_EMPTY)
                 continue;
-            Box cb = {{N.lox[j], N.loy[j], N.loz[j]}, {N.hix[j], N.hiy[j], N.hiz[j]}};
-            if (!inside(cb, it.box))
-                bad++;
-            stack.push_back({N.child[j], cb});
+            double lo[3], hi[3];
+            Box cb = decode(N, j, lo, hi);
+            // the decoded box (outward-rounded to float) need not sit inside the parent's, but the
+            // triangles below must sit inside every decoded box on their path: tested at the leaves
+            // against the intersection of the path's boxes
+            Box path = cb;
+            for (int a = 0; a < 3; a++) {
+                path.lo[a] = std::max(cb.lo[a], it.box.lo[a]);
+                path.hi[a] = std::min(cb.hi[a], it.box.hi[a]);
+            }
+            stack.push_back({N.child[j], path});
         }
     }
     for (size_t k = 0; k < n; k++)

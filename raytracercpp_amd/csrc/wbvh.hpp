@@ -20,12 +20,19 @@
 // octree traversal.  With no hit at all, the reference finds none either and returns false
 // with a fresh record.
 //
-// Layout (HBM): WNode 128 B = the four children's boxes as SoA (lo x / hi x / lo y /
-// hi y / lo z / hi z, four floats each), then four child links:
-//   inner child:  node index (bit 31 clear);
-//   leaf child:   W_LEAF | first << 3 | (count - 1), triangles first .. first + count - 1
-//                 of the wide BVH's own triangle order (count <= 8);
-//   no child:     W_EMPTY.
+// Layout (HBM): WNode 64 B, the four children's boxes quantised to 8 bits per plane
+// against the node's own frame (Ylitie et al.'s compressed wide nodes, 4-wide):
+//   float4 0: origin x, y, z (the node box's low corner) and the three scale exponents
+//             (byte a = biased exponent of the power-of-two step s_a along axis a);
+//   float4 1: q_lo x[4], q_lo y[4], q_lo z[4], q_hi x[4] (one byte per child);
+//   float4 2: q_hi y[4], q_hi z[4], two unused words;
+//   float4 3: the four child links:
+//     inner child:  node index (bit 31 clear);
+//     leaf child:   W_LEAF | first << 3 | (count - 1), triangles first .. first + count - 1
+//                   of the wide BVH's own triangle order (count <= 8);
+//     no child:     W_EMPTY.
+// Child box = [origin + q_lo s, origin + q_hi s] with q_lo rounded down and q_hi up, so
+// it holds the float box exactly (checked in double by check_wbvh).
 // Triangles: GTri records (octree.hpp) copied in leaf order, plus slot[] = the octree GTri
 // slot of each, and leaf_of_slot[] = the flattened octree leaf node holding each slot.
 #pragma once
@@ -44,14 +51,20 @@ constexpr int W_MAX_LEAF = 8;
 #ifndef RT_W_STACK
 #define RT_W_STACK 16
 #endif
-constexpr int W_STACK = RT_W_STACK;   // traversal stack entries per lane (overflow: the query is not certified)
+constexpr int W_STACK = RT_W_STACK;
+#ifndef RT_W_LOOP
+#define RT_W_LOOP 2   // 1: while-while, 2: if-if, 3: if-if with one triangle per step (wbvh_closest)
+#endif   // traversal stack entries per lane (overflow: the query is not certified)
 
 struct alignas(16) WNode {
-    float lox[4], hix[4], loy[4], hiy[4], loz[4], hiz[4];
+    float ox, oy, oz;
+    uint32_t exps;        // byte a: biased exponent (127 + k) of the step 2^k along axis a
+    uint8_t qlo[3][4];    // [axis][child]
+    uint8_t qhi[3][4];
+    uint32_t pad[2];
     uint32_t child[4];
-    uint32_t pad[4];
 };
-static_assert(sizeof(WNode) == 128, "WNode must be 128 B");
+static_assert(sizeof(WNode) == 64, "WNode must be 64 B");
 
 struct WStats {
     int64_t nodes = 0, leaves = 0, tris = 0, max_leaf = 0, depth = 0;
@@ -108,6 +121,32 @@ RT_HD bool mt_record(const GTri& T, v3 o, v3 d, float& t_out, float& u_out, floa
     return !(t < 0);
 }
 
+RT_HD GTri load_gtri(const GTri* p)
+{
+    const float4* q = reinterpret_cast<const float4*>(p);
+    float4 a = ldg(q), b = ldg(q + 1), c = ldg(q + 2);
+    GTri g;
+    g.a[0] = a.x; g.a[1] = a.y; g.a[2] = a.z;
+    g.ab[0] = a.w; g.ab[1] = b.x; g.ab[2] = b.y;
+    g.ac[0] = b.z; g.ac[1] = b.w; g.ac[2] = c.x;
+    g.n[0] = c.y; g.n[1] = c.z; g.n[2] = c.w;
+    return g;
+}
+
+RT_HD GNode load_gnode(const GNode* p)
+{
+    const float4* q = reinterpret_cast<const float4*>(p);
+    float4 a = ldg(q), b = ldg(q + 1), c = ldg(q + 2), d = ldg(q + 3);
+    GNode g;
+    g.dn[0] = a.x; g.dn[1] = a.y; g.dn[2] = a.z; g.dn[3] = a.w;
+    g.dn[4] = b.x; g.dn[5] = b.y; g.dn[6] = b.z;
+    g.df[0] = b.w; g.df[1] = c.x; g.df[2] = c.y; g.df[3] = c.z; g.df[4] = c.w;
+    g.df[5] = d.x; g.df[6] = d.y;
+    g.a = __builtin_bit_cast(uint32_t, d.z);
+    g.b = __builtin_bit_cast(uint32_t, d.w);
+    return g;
+}
+
 // BoundingVolume::intersect (bvh.h:79-105) with the ray's plane products as
 // OctreeNode::intersect computes them (bvh.h:216-223), branch-free as kernels.hip
 // vol_test: returns pass && t_near <= t.
@@ -160,8 +199,14 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
     h.u = 1.0f;
     h.v = 0.0f;
     h.k = -1;
-    // slab parameters: t = (lo - (o + m)) / d and (hi - (o - m)) / d over the box widened by m
-    const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
+    // slab parameters: t = (lo - (o + m)) / d and (hi - (o - m)) / d over the box widened by m.
+    // A direction component below 2^-100 in magnitude (or 0) is treated as +-2^-100: the
+    // slab's t range then exceeds 2^70 m / |d| on the far side, far beyond the scene's, so
+    // it constrains only as much as the true one does (the margin covers the origin's side).
+    const float DMIN = 0x1p-100f;
+    const float ix = 1.0f / (fabsf(d.x) < DMIN ? copysignf(DMIN, d.x) : d.x);
+    const float iy = 1.0f / (fabsf(d.y) < DMIN ? copysignf(DMIN, d.y) : d.y);
+    const float iz = 1.0f / (fabsf(d.z) < DMIN ? copysignf(DMIN, d.z) : d.z);
     const float olx = o.x + m, oly = o.y + m, olz = o.z + m;
     const float ohx = o.x - m, ohy = o.y - m, ohz = o.z - m;
     constexpr float SL = 0x1p-20f;   // relative slack over the rounding of a slab parameter (<= 3 ulp)
@@ -172,24 +217,38 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
     uint32_t nn = 0, nt = 0;
     while (cur != W_EMPTY) {
         // ---- inner nodes: test the four child boxes, go to the nearest, push the others ----
+#if RT_W_LOOP >= 2
+        // if-if: every lane takes one step (inner node or leaf) per iteration
+        if (!(cur & W_LEAF)) {
+#else
+        // while-while: lanes at inner nodes expand until every lane sits on a leaf (or is done)
         while (cur != W_EMPTY && !(cur & W_LEAF)) {
+#endif
             nn++;
             const float4* p = reinterpret_cast<const float4*>(nodes + cur);
-            const float4 LX = p[0], HX = p[1], LY = p[2], HY = p[3], LZ = p[4], HZ = p[5];
-            const uint4 CH = reinterpret_cast<const uint4*>(p)[6];
-            const float lx[4] = {LX.x, LX.y, LX.z, LX.w}, hx[4] = {HX.x, HX.y, HX.z, HX.w};
-            const float ly[4] = {LY.x, LY.y, LY.z, LY.w}, hy[4] = {HY.x, HY.y, HY.z, HY.w};
-            const float lz[4] = {LZ.x, LZ.y, LZ.z, LZ.w}, hz[4] = {HZ.x, HZ.y, HZ.z, HZ.w};
+            const float4 Q0 = ldg(p);
+            const uint4 Q1 = ldg(reinterpret_cast<const uint4*>(p) + 1), Q2 = ldg(reinterpret_cast<const uint4*>(p) + 2);
+            const uint4 CH = ldg(reinterpret_cast<const uint4*>(p) + 3);
+            const uint32_t ex = fbits(Q0.w);
+            // t of a plane origin + q s (widened by m) = q (s / d) + (origin -+ m - o) / d
+            const float sx = bitsf((ex & 0xffu) << 23) * ix, sy = bitsf(((ex >> 8) & 0xffu) << 23) * iy,
+                        sz = bitsf(((ex >> 16) & 0xffu) << 23) * iz;
+            const float ax = (Q0.x - olx) * ix, ay = (Q0.y - oly) * iy, az = (Q0.z - olz) * iz;
+            const float bx = (Q0.x - ohx) * ix, by = (Q0.y - ohy) * iy, bz = (Q0.z - ohz) * iz;
             const uint32_t ch[4] = {CH.x, CH.y, CH.z, CH.w};
             float key[4];
             uint32_t ref[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                float ax = (lx[j] - olx) * ix, bx = (hx[j] - ohx) * ix;
-                float ay = (ly[j] - oly) * iy, by = (hy[j] - ohy) * iy;
-                float az = (lz[j] - olz) * iz, bz = (hz[j] - ohz) * iz;
-                float tmin = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-                float tmax = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+                const int sh = 8 * j;
+                float tlx = __builtin_fmaf((float)((Q1.x >> sh) & 0xffu), sx, ax);
+                float tly = __builtin_fmaf((float)((Q1.y >> sh) & 0xffu), sy, ay);
+                float tlz = __builtin_fmaf((float)((Q1.z >> sh) & 0xffu), sz, az);
+                float thx = __builtin_fmaf((float)((Q1.w >> sh) & 0xffu), sx, bx);
+                float thy = __builtin_fmaf((float)((Q2.x >> sh) & 0xffu), sy, by);
+                float thz = __builtin_fmaf((float)((Q2.y >> sh) & 0xffu), sz, bz);
+                float tmin = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fminf(tlz, thz));
+                float tmax = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fmaxf(tlz, thz));
                 float tmax_s = tmax + fabsf(tmax) * SL;
                 bool ok = ch[j] != W_EMPTY && tmin <= tmax_s && tmin <= best_s && tmax_s >= 0.0f;
                 key[j] = ok ? fminf(tmin, 3.0e38f) : INFINITY;
@@ -224,14 +283,25 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                 }
             }
         }
+#if RT_W_LOOP >= 2
+        else {
+#else
         if (cur == W_EMPTY)
             break;
+        {
+#endif
         // ---- a leaf: its triangles, closest hit kept; equal t from another triangle is a tie ----
         const uint32_t first = (cur >> 3) & 0x0FFFFFFFu, cnt = (cur & 7u) + 1u;
-        for (uint32_t k = first; k < first + cnt; k++) {
+#if RT_W_LOOP == 3
+        // one triangle per step: the leaf link advances to the next triangle
+        const uint32_t kend = first + 1;
+#else
+        const uint32_t kend = first + cnt;
+#endif
+        for (uint32_t k = first; k < kend; k++) {
             nt++;
             float t, u, v;
-            if (mt_record(tris[k], o, d, t, u, v)) {
+            if (mt_record(load_gtri(tris + k), o, d, t, u, v)) {
                 if (t != t)
                     nanhit = true;
                 else if (!(t <= hi))
@@ -249,6 +319,12 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                     tie = true;
             }
         }
+#if RT_W_LOOP == 3
+        if (cnt > 1) {
+            cur = W_LEAF | ((first + 1) << 3) | (cnt - 2);
+            continue;
+        }
+#endif
         cur = W_EMPTY;
         while (sp > 0) {
             uint2 e = stk.get(--sp);
@@ -256,6 +332,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                 cur = e.x;
                 break;
             }
+        }
         }
     }
     if (work) {

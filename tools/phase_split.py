@@ -18,6 +18,8 @@ VARIANTS = [
     ("primary+shadow, no deferral", {}, {"RT_DEFER_BUDGET": "0"}),
     ("primary only, no deferral", {"compute_shadows": False}, {"RT_DEFER_BUDGET": "0"}),
     ("primary+shadow, RT_WBVH=0 RT_SEG=0 RT_CONES=0", {}, {"RT_WBVH": "0", "RT_SEG": "0", "RT_CONES": "0"}),
+    ("primary only, barycentric shading", {"compute_shadows": False, "shading_method": 3}, {}),
+    ("all rays miss (sphere behind the camera)", {"compute_shadows": False}, {"_behind": "1"}),
 ]
 want = sys.argv[1:]
 sc, st = scenes.sphere1m()
@@ -27,8 +29,14 @@ for label, kw, env in VARIANTS:
         continue
     for k in ("RT_SEG", "RT_CONES", "RT_WBVH", "RT_DEFER_BUDGET"):
         os.environ.pop(k, None)
+    behind = env.pop("_behind", None) if "_behind" in env else None
     os.environ.update(env)
-    r.load_scene(sc, st.copy(**kw))
+    if behind:
+        import dataclasses
+        sc2 = dataclasses.replace(sc, tri=(sc.tri + np.tile(np.float32([0, 0, 100]), 3)).astype(np.float32))
+        r.load_scene(sc2, st.copy(**kw))
+    else:
+        r.load_scene(sc, st.copy(**kw))
     ts = []
     for i in range(8):
         r.ray_trace()

@@ -35,3 +35,13 @@ for (py, px) in ((992, 1176), (995, 1180), (912, 1192), (430, 1560)):
 for (py, px) in ((440, 1528), (992, 1176)):
     blk = slice(py, py + 8), slice(px, px + 8)
     print(f"tile y {py} x {px} k-DOP per pixel:\n{vol[blk].astype(np.int64)}\nMT per pixel:\n{tri[blk].astype(np.int64)}")
+# heaviest tiles by the largest per-pixel node work, and the tiles named on the command line
+tv = vol[: rh // 8 * 8, : rw // 8 * 8].reshape(rh // 8, 8, rw // 8, 8).max(axis=(1, 3))
+tt = tri[: rh // 8 * 8, : rw // 8 * 8].reshape(rh // 8, 8, rw // 8, 8).max(axis=(1, 3))
+ty, tx = np.unravel_index(np.argsort(tv.ravel())[::-1][:8], tv.shape)
+for a, b in zip(ty, tx):
+    print(f"  heavy tile row {a} col {b}: max node/k-DOP {tv[a, b]:.0f}  max MT {tt[a, b]:.0f}")
+for arg in sys.argv[1:]:
+    a, b = map(int, arg.split(","))
+    blk = slice(a * 8, a * 8 + 8), slice(b * 8, b * 8 + 8)
+    print(f"tile row {a} col {b} node/k-DOP per pixel:\n{vol[blk].astype(np.int64)}\nMT per pixel:\n{tri[blk].astype(np.int64)}")
