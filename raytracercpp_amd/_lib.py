@@ -55,7 +55,7 @@ class RtStats(C.Structure):
         ("gpu_nodes", C.c_int64), ("gpu_tris", C.c_int64),
         ("render_width", C.c_int32), ("render_height", C.c_int32), ("seg_scale", C.c_float),
         ("work", C.c_int64 * 4), ("deferred_pixels", C.c_int64), ("work_abandoned", C.c_int64 * 2),
-        ("work_wide", C.c_int64 * 3),
+        ("work_wide", C.c_int64 * 3), ("exact_pixels", C.c_int64),
     ]
 
     def as_dict(self):

@@ -958,7 +958,8 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
     WHit w;
 #if RT_COUNT
     uint32_t wk[2] = {0, 0};
-    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk);
+    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, INFINITY, true,
+                                P.wide_budget);
     if (P.counters) {
         atomicAdd(&P.counters[10], (unsigned long long)wk[0]);
         atomicAdd(&P.counters[11], (unsigned long long)wk[1]);
@@ -968,7 +969,8 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
     g_pixel_work[pixel_work_slot()].y += wk[1];
 #endif
 #else
-    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w);
+    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, INFINITY,
+                                true, P.wide_budget);
 #endif
     if (st == W_MISS) {
         h.t = -1.0f;
@@ -1009,7 +1011,8 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
     WHit w;
 #if RT_COUNT
     uint32_t wk[2] = {0, 0};
-    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, hi, false);
+    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, hi, false,
+                                P.wide_budget);
     if (P.counters) {
         atomicAdd(&P.counters[10], (unsigned long long)wk[0]);
         atomicAdd(&P.counters[11], (unsigned long long)wk[1]);
@@ -1019,7 +1022,8 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
     g_pixel_work[pixel_work_slot()].y += wk[1];
 #endif
 #else
-    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, hi, false);
+    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, hi, false,
+                                P.wide_budget);
 #endif
     if (st == W_MISS) {
         *sh = false;
@@ -1591,23 +1595,83 @@ struct TileQueue {
 
 __device__ __forceinline__ TileQueue tile_queue_begin() { return TileQueue{(int)(blockIdx.x & (TILE_SHARDS - 1)), 0}; }
 
-// next tile for the calling wave (wave-uniform), or -1 when every shard is empty
+// next tile for the calling wave (wave-uniform), or -1 when every shard is empty.  With
+// P.tile_order (tiles sorted by estimated cost, heaviest first: tile_probe_kernel) shard s
+// takes sorted positions s, s + 8, s + 16, ... so every shard starts on heavy tiles.
 __device__ __forceinline__ int tile_queue_next(const KParams& P, TileQueue& q, int ntiles)
 {
     const int lane = threadIdx.x & 63;
     while (q.empty < TILE_SHARDS) {
-        const int b0 = (int)((long long)ntiles * q.shard / TILE_SHARDS);
-        const int b1 = (int)((long long)ntiles * (q.shard + 1) / TILE_SHARDS);
         int t = 0;
         if (lane == 0)
             t = (int)atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[NCOUNTERS + 16 * q.shard]), 1u);
         t = __builtin_amdgcn_readfirstlane(t);
-        if (b0 + t < b1)
-            return b0 + t;
+        if (P.tile_order) {
+            const int pos = q.shard + TILE_SHARDS * t;
+            if (pos < ntiles)
+                return (int)(ldg(P.tile_order + pos) & TILE_ID_MASK);
+        } else {
+            const int b0 = (int)((long long)ntiles * q.shard / TILE_SHARDS);
+            const int b1 = (int)((long long)ntiles * (q.shard + 1) / TILE_SHARDS);
+            if (b0 + t < b1)
+                return b0 + t;
+        }
         q.empty++;
         q.shard = (q.shard + 1) & (TILE_SHARDS - 1);
     }
     return -1;
+}
+
+// Tile cost probe (the tile order above).  One ray per tile, through the tile's centre
+// pixel, is traced through the wide BVH with a small iteration budget; its node visits +
+// triangle tests (capped) estimate the tile's work.  Silhouette tiles, whose grazing rays
+// are the frame's longest, probe high.  The order changes only when tiles start, never
+// what they compute.
+__global__ __launch_bounds__(BLOCK) void tile_probe_kernel(KParams P, uint32_t* cost)
+{
+    extern __shared__ uint2 lds_levels[];
+    uint2* lv = lds_levels + threadIdx.x;
+    const int ntiles = P.tiles_x * P.tiles_y;
+    const int tile = blockIdx.x * BLOCK + threadIdx.x;
+    if (tile >= ntiles)
+        return;
+    const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+    const int px = min(tx * 8 + 4, P.rw - 1);
+    const int lr = min(ty * 8 + 4, P.local_rows - 1);
+    const int py = min(global_row(P, lr), P.rh - 1);
+    const v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+    float y_world = ((float)py + 0.5f) / P.rh * 2 - 1;
+    float x_world = ((float)px + 0.5f) / P.rw * 2 - 1;
+    v3 vs = xform_point(P.proj_inv, mk(x_world, y_world, -1));
+    v3 ws = xform_point(P.cam_to_world, vs);
+    v3 rd = normalize(ws - cam);
+    const float om = fmaxf(fabsf(cam.x), fmaxf(fabsf(cam.y), fabsf(cam.z)));
+    WStackLds stk{lv};
+    WHit w;
+    uint32_t wk[2] = {0, 0};
+    wbvh_closest(P.wnodes, P.wtris, cam, rd, 0x1p-16f * (om + P.scene_scale), stk, w, wk, INFINITY, true,
+                 TILE_PROBE_BUDGET);
+    cost[tile] = wk[0] + wk[1];
+}
+
+// sort keys: the largest probe cost among the tile and its 8 neighbours (a silhouette
+// crosses neighbouring tiles), descending, then the tile index
+__global__ __launch_bounds__(BLOCK) void tile_key_kernel(KParams P, const uint32_t* cost, uint32_t* keys)
+{
+    const int ntiles = P.tiles_x * P.tiles_y;
+    const int tile = blockIdx.x * BLOCK + threadIdx.x;
+    if (tile >= ntiles)
+        return;
+    const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+    uint32_t c = 0;
+    for (int dy = -1; dy <= 1; dy++)
+        for (int dx = -1; dx <= 1; dx++) {
+            const int x = tx + dx, y = ty + dy;
+            if (x >= 0 && x < P.tiles_x && y >= 0 && y < P.tiles_y)
+                c = max(c, cost[y * P.tiles_x + x]);
+        }
+    c = min(c, TILE_COST_MAX);
+    keys[tile] = ((TILE_COST_MAX - c) << TILE_ID_BITS) | (uint32_t)tile;
 }
 
 // Renderer::ray_trace (renderer.cpp:1068-1116): one lane per pixel, one wave
@@ -1657,7 +1721,7 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
         if (!REFL && po.deferred) {
             // the deferred pass (ray_trace_defer_kernel) traces it with a ray group; the
             // host sizes defer_cap >= the launch's pixels, and a pixel defers at most once
-            uint32_t idx = atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[3]), 1u);
+            uint32_t idx = atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[P.defer_head]), 1u);
             P.defer[idx] = (uint32_t)o;
             continue;
         }
@@ -1666,8 +1730,10 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
         if (P.rgba) P.rgba[o] = make_float4(po.color.r, po.color.g, po.color.b, po.alpha);
         if (P.hit_id) P.hit_id[o] = po.found ? po.src : -1;
 #if RT_TILE_TIME
-        // diagnostic build: hit_t holds the pixel's trace time in wall-clock ticks
+        // diagnostic build: hit_t holds the pixel's trace time in wall-clock ticks, rgba.w its
+        // start tick (low 32 bits, as raw bits)
         if (P.hit_t) P.hit_t[o] = (float)(wall_clock64() - t_start);
+        if (P.rgba) P.rgba[o].w = __uint_as_float((uint32_t)t_start);
 #elif RT_COUNT == 2
         if (P.hit_t) P.hit_t[o] = (float)g_pixel_work[pixel_work_slot()].x;
         if (P.argb) P.argb[o] = g_pixel_work[pixel_work_slot()].y;
@@ -1688,14 +1754,14 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_defer_kernel(KParams 
 {
     extern __shared__ uint2 lds_levels[];
     uint2* lv = lds_levels + threadIdx.x;
-    const uint32_t n = min(*reinterpret_cast<const unsigned int*>(&P.counters[3]), P.defer_cap);
+    const uint32_t n = min(*reinterpret_cast<const unsigned int*>(&P.counters[P.defer_in_head]), P.defer_cap);
     const int gs = P.grp_shift;
     const uint32_t g = threadIdx.x & ((1u << gs) - 1);
     const uint32_t stride = (gridDim.x * (uint32_t)BLOCK) >> gs;
     v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
     unsigned nshadow = 0, nrefl = 0;
     for (uint32_t i = (blockIdx.x * (uint32_t)BLOCK + threadIdx.x) >> gs; i < n; i += stride) {
-        const uint32_t o = P.defer[i];
+        const uint32_t o = P.defer_in[i];
         const int lr = (int)(o / (uint32_t)P.rw), px = (int)(o % (uint32_t)P.rw);
         const int py = global_row(P, lr);
         // ray generation, renderer.cpp:1086-1098 (as ray_trace_kernel)
@@ -1709,6 +1775,43 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_defer_kernel(KParams 
         if (g != 0)
             continue;
         nshadow += ns;
+        if (P.argb) P.argb[o] = color_to_argb(po.color);
+        if (P.rgba) P.rgba[o] = make_float4(po.color.r, po.color.g, po.color.b, po.alpha);
+        if (P.hit_id) P.hit_id[o] = po.found ? po.src : -1;
+        if (P.hit_t) P.hit_t[o] = po.fin.t;
+        if (P.shadow) P.shadow[o] = (uint8_t)(po.found && po.shadowed);
+        if (P.zbuf) write_ssao_buffers(P, o, po.found, cam, rd, po.fin);
+    }
+    if (nshadow) atomicAdd(&P.counters[0], (unsigned long long)nshadow);
+}
+
+// The heavy-pixel pass of the lean kernel: pixels whose wide-BVH queries
+// exceeded P.wide_budget there (silhouette rays that graze many boxes) are traced again,
+// one lane per pixel and without a budget, so that a wave holds 64 heavy rays instead of
+// one heavy ray among 63 finished lanes; what the wide BVH cannot certify goes on to the
+// exact pass (ray_trace_defer_kernel) through P.defer.
+__global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_retry_kernel(KParams P)
+{
+    extern __shared__ uint2 lds_levels[];
+    uint2* lv = lds_levels + threadIdx.x;
+    const uint32_t n = min(*reinterpret_cast<const unsigned int*>(&P.counters[P.defer_in_head]), P.defer_cap);
+    v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+    unsigned nshadow = 0, nrefl = 0;
+    for (uint32_t i = blockIdx.x * (uint32_t)BLOCK + threadIdx.x; i < n; i += gridDim.x * (uint32_t)BLOCK) {
+        const uint32_t o = P.defer_in[i];
+        const int lr = (int)(o / (uint32_t)P.rw), px = (int)(o % (uint32_t)P.rw);
+        const int py = global_row(P, lr);
+        float y_world = ((float)py + 0.5f) / P.rh * 2 - 1;
+        float x_world = ((float)px + 0.5f) / P.rw * 2 - 1;
+        v3 vs = xform_point(P.proj_inv, mk(x_world, y_world, -1));
+        v3 ws = xform_point(P.cam_to_world, vs);
+        v3 rd = normalize(ws - cam);
+        PixelOut po = trace_pixel<false, false, true>(P, cam, rd, lv, 0u, nshadow, nrefl, 0u);
+        if (po.deferred) {
+            uint32_t idx = atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[P.defer_head]), 1u);
+            P.defer[idx] = o;
+            continue;
+        }
         if (P.argb) P.argb[o] = color_to_argb(po.color);
         if (P.rgba) P.rgba[o] = make_float4(po.color.r, po.color.g, po.color.b, po.alpha);
         if (P.hit_id) P.hit_id[o] = po.found ? po.src : -1;
@@ -2917,6 +3020,21 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_trace_rays
     return hipGetLastError();
 }
 
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_tile_probe(const rt::KParams* P, uint32_t* cost,
+                                                                                uint32_t* keys, hipStream_t stream)
+{
+    int ntiles = P->tiles_x * P->tiles_y;
+    if (ntiles <= 0)
+        return hipSuccess;
+    dim3 g((ntiles + rt::BLOCK - 1) / rt::BLOCK);
+    hipLaunchKernelGGL(rt::tile_probe_kernel, g, dim3(rt::BLOCK), rt::lds_bytes(*P), stream, *P, cost);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return e;
+    hipLaunchKernelGGL(rt::tile_key_kernel, g, dim3(rt::BLOCK), 0, stream, *P, cost, keys);
+    return hipGetLastError();
+}
+
 // ---- host-side launch wrappers (called from renderer.cpp) ----
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(const rt::KParams* P, hipStream_t stream)
 {
@@ -2933,14 +3051,32 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(
     else {
         rt::KParams A = *P;
         A.grp_shift = 0;   // one lane per pixel; the groups are the deferred pass's
-        if (P->wide_lean && P->defer && P->defer_cap)
+        A.defer_head = 3;
+        const int db = P->max_blocks > 0 ? P->max_blocks : 1024;
+        if (P->wide_lean && P->defer && P->defer2 && P->defer_cap) {
+            // lean kernel (list 1: over-budget or uncertified pixels, head counters[3]) -> heavy-pixel
+            // pass (list 2: uncertified, head counters[13]) -> exact ray-group pass over list 2
             hipLaunchKernelGGL((rt::ray_trace_kernel<false, true>), dim3(blocks), dim3(rt::BLOCK), lds, stream, A);
-        else
+            rt::KParams B = *P;
+            B.wide_budget = 0;
+            B.defer_in = P->defer;
+            B.defer_in_head = 3;
+            B.defer = P->defer2;
+            B.defer_head = 13;
+            hipLaunchKernelGGL(rt::ray_trace_retry_kernel, dim3(db), dim3(rt::BLOCK), lds, stream, B);
+            rt::KParams C = *P;
+            C.defer_in = P->defer2;
+            C.defer_in_head = 13;
+            hipLaunchKernelGGL(rt::ray_trace_defer_kernel, dim3(db), dim3(rt::BLOCK), lds, stream, C);
+        } else {
             hipLaunchKernelGGL((rt::ray_trace_kernel<false, false>), dim3(blocks), dim3(rt::BLOCK), lds, stream, A);
-        if (P->defer && P->defer_cap) {
-            // deferred pixels: a persistent grid of ray groups over the list ray_trace_kernel left
-            int db = P->max_blocks > 0 ? P->max_blocks : 1024;
-            hipLaunchKernelGGL(rt::ray_trace_defer_kernel, dim3(db), dim3(rt::BLOCK), lds, stream, *P);
+            if (P->defer && P->defer_cap) {
+                // deferred pixels: a persistent grid of ray groups over the list ray_trace_kernel left
+                rt::KParams C = *P;
+                C.defer_in = P->defer;
+                C.defer_in_head = 3;
+                hipLaunchKernelGGL(rt::ray_trace_defer_kernel, dim3(db), dim3(rt::BLOCK), lds, stream, C);
+            }
         }
     }
     return hipGetLastError();

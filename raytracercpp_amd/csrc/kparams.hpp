@@ -15,6 +15,11 @@ constexpr int MAX_SHAPES = 64;
 constexpr int NCOUNTERS = 16;  // KParams::counters entries (u64) before the tile-queue heads
 constexpr int TILE_SHARDS = 8; // tile-queue shards (one per XCD group, blockIdx % 8)
 constexpr int NCOUNTER_WORDS = NCOUNTERS + 16 * TILE_SHARDS;   // + one 128-B line per shard head
+// tile order (kernels.hip tile_probe_kernel): key = (TILE_COST_MAX - cost) << TILE_ID_BITS | tile
+constexpr uint32_t TILE_ID_BITS = 20;
+constexpr uint32_t TILE_ID_MASK = (1u << TILE_ID_BITS) - 1;
+constexpr uint32_t TILE_COST_MAX = 2047;
+constexpr uint32_t TILE_PROBE_BUDGET = 96;
 
 enum TexSlot { TEX_AO = 0, TEX_DIFFUSE = 1, TEX_NORMAL = 2, TEX_DISPLACEMENT = 3, TEX_ROUGHNESS = 4, TEX_SKYSPHERE = 5 };
 enum Shading { RT_SHADING = 0, ABS_NORMALS = 1, PASTEL_NORMALS = 2, BARYCENTRIC = 3, VISUALIZE_AO = 4 };
@@ -85,6 +90,7 @@ struct KParams {
     int32_t local_rows;       // rows in this launch's (padded) local buffers
     int32_t tiles_x, tiles_y; // 8x8 tiles over (rw, local_rows)
     int32_t max_blocks;       // persistent grid size (CUs x resident blocks per CU)
+    const uint32_t* tile_order;   // tiles in descending estimated cost (low TILE_ID_BITS bits), or nullptr
     // Deferred pixels (kernels.hip "Ray groups").  trav_budget > 0: a primary query whose
     // traversal work exceeds it is abandoned and its pixel appended to defer[] (count in
     // counters[3]); the deferred pass then traces each such pixel with 1 << grp_shift lanes
@@ -92,8 +98,13 @@ struct KParams {
     uint32_t trav_budget;
     int32_t grp_shift;
     int32_t wide_lean;        // 1: the lean wide-BVH kernel, everything it cannot certify deferred (needs defer[])
-    uint32_t* defer;
+    uint32_t* defer;          // output list of deferred pixels, head counters[defer_head]
     uint32_t defer_cap;
+    int32_t defer_head;
+    const uint32_t* defer_in; // input list of a deferred pass, count counters[defer_in_head]
+    int32_t defer_in_head;
+    uint32_t* defer2;         // lean mode: the second list (pixels the wide BVH cannot certify)
+    uint32_t wide_budget;     // lean kernel: wide-BVH loop iterations per query before it is deferred (0: none)
 
     // outputs, indexed by local_row * rw + px (nullptr = not requested)
     uint32_t* argb;
@@ -104,7 +115,8 @@ struct KParams {
     unsigned long long* counters;   // [NCOUNTERS]: [0] shadow rays, [1] reflection rays, [2] tile queue head,
                                     // [3] deferred-pixel list head, [4..7] executed k-DOP / MT tests of
                                     // whole-line / segment queries and [8..9] of abandoned queries, [10..11]
-                                    // wide-BVH node visits / triangle tests, [12] uncertified queries (RT_COUNT);
+                                    // wide-BVH node visits / triangle tests, [12] uncertified queries (RT_COUNT),
+                                    // [13] head of the lean mode's second deferred list;
                                     // then the tile-queue heads, shard s at counters[NCOUNTERS + 16 s]
     // SSAO inputs (enable_ssao): Renderer::_z_buffer / _normal_buffer, renderer.cpp:1107-1110, 975-979
     float* zbuf;

@@ -13,6 +13,8 @@
 #include "host_scene.hpp"
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(const rt::KParams* P, hipStream_t stream);
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_tile_probe(const rt::KParams* P, uint32_t* cost,
+                                                                                uint32_t* keys, hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_level0(const rt::KParams* P, rt::FrameRec* fr1,
                                                                            unsigned int* nfr1, hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_stage(int stage, const rt::KParams* P,
@@ -94,7 +96,7 @@ int Renderer::init(std::string& err)
                      &d_image_, &d_rgba_,  &d_hit_id_, &d_hit_t_,   &d_shadow_, &d_counters_, &d_band_tmp_, &d_defer_,
                      &d_tri9_,  &d_rcount_, &d_roff_,  &d_pieces_,  &d_piece_uv_, &d_zkey_, &d_big_, &d_scan_tmp_,
                      &d_zbuf_,  &d_nbuf_,   &d_ao_,     &d_cones_, &d_lslab_, &d_wnodes_, &d_wtris_, &d_wslot_,
-                     &d_wleaf_};
+                     &d_wleaf_, &d_defer2_, &d_tile_sort_, &d_tile_sort_tmp_};
     for (DevBuf* b : all) b->device = device_;
     for (auto& b : d_tex_) b.device = device_;
     for (auto& b : d_sky_) b.device = device_;
@@ -744,18 +746,25 @@ int Renderer::launch_trace(const KParams& P, hipStream_t stream)
         // deferred pixels (kernels.hip ray_trace_defer_kernel):
         // RT_DEFER_BUDGET (default 1000; 0 = off) and RT_GROUP_SHIFT (default 5: 32 lanes per ray)
         KParams Q = P;
-        // With the wide BVH and segment queries (no analytic shapes, scene scale in range) the
-        // lean kernel runs: the few pixels it cannot certify go to the deferred
-        // list and the exact ray-group pass.  RT_WIDE_LEAN=0: the full kernel, which traces
-        // those queries through the octree in place.
+        // RT_WIDE_LEAN=1, with the wide BVH and segment queries (no analytic shapes, scene scale
+        // in range): the lean kernel (no octree code) -- pixels over RT_WIDE_BUDGET
+        // go to a heavy-pixel pass and those the wide BVH cannot certify to the exact ray-group
+        // pass.  Measured slower than the default full kernel, which traces the few uncertified
+        // queries through the octree in place (each extra pass waits on its slowest ray).
         const char* lean_env = getenv("RT_WIDE_LEAN");
         size_t npx_all = (size_t)P.rw * P.local_rows;
         if (P.wnodes && P.seg_scale > 0.0f && P.enable_bvh && !P.has_reflection && !P.pipeline &&
-            !(lean_env && lean_env[0] == '0') && npx_all > 0 && npx_all < (1ull << 32)) {
-            if ((e = d_defer_.reserve(npx_all * 4)) != hipSuccess)
+            (lean_env && lean_env[0] == '1') && npx_all > 0 && npx_all < (1ull << 32)) {
+            if ((e = d_defer_.reserve(npx_all * 4)) != hipSuccess || (e = d_defer2_.reserve(npx_all * 4)) != hipSuccess)
                 return hip_fail(e, "hipMalloc (deferred pixels)");
             const char* gs = getenv("RT_GROUP_SHIFT");
             long shift = gs ? atol(gs) : 5;
+            // RT_WIDE_BUDGET: wide-BVH loop iterations per query in the lean kernel before the
+            // pixel moves to the heavy-pixel pass (default 64; 0: no budget)
+            const char* wb = getenv("RT_WIDE_BUDGET");
+            long wbud = wb ? atol(wb) : 0;
+            Q.wide_budget = (uint32_t)std::max(0L, std::min(wbud, 1L << 30));
+            Q.defer2 = d_defer2_.as<uint32_t>();
             Q.wide_lean = 1;
             Q.trav_budget = 0;
             Q.grp_shift = (shift >= 1 && shift <= 6) ? (int32_t)shift : 5;
@@ -784,6 +793,28 @@ int Renderer::launch_trace(const KParams& P, hipStream_t stream)
                 Q.defer = d_defer_.as<uint32_t>();
                 Q.defer_cap = (uint32_t)npx;   // >= the launch's pixels: the list cannot overflow
             }
+        }
+        // tiles in descending estimated cost (kernels.hip tile_probe_kernel): the silhouette
+        // tiles, whose grazing rays are the frame's longest, start first instead of ending it.
+        // RT_TILE_ORDER=0: natural order.
+        const char* to_env = getenv("RT_TILE_ORDER");
+        const int ntiles = P.tiles_x * P.tiles_y;
+        if (P.wnodes && !P.pipeline && !P.has_reflection && !(to_env && to_env[0] == '0') && ntiles > 0 &&
+            ntiles <= (int)TILE_ID_MASK) {
+            const size_t nt = (size_t)ntiles;
+            if ((e = d_tile_sort_.reserve(nt * 12)) != hipSuccess)
+                return hip_fail(e, "hipMalloc (tile order)");
+            uint32_t* cost = d_tile_sort_.as<uint32_t>();
+            uint32_t* keys = cost + nt;
+            uint32_t* sorted = keys + nt;
+            size_t tb = 0;
+            if ((e = rt_launch_tile_probe(&Q, cost, keys, stream)) != hipSuccess ||
+                (e = hipcub::DeviceRadixSort::SortKeys(nullptr, tb, keys, sorted, ntiles, 0, 31, stream)) != hipSuccess ||
+                (e = d_tile_sort_tmp_.reserve(tb)) != hipSuccess ||
+                (e = hipcub::DeviceRadixSort::SortKeys(d_tile_sort_tmp_.p, tb, keys, sorted, ntiles, 0, 31, stream)) !=
+                    hipSuccess)
+                return hip_fail(e, "tile order");
+            Q.tile_order = sorted;
         }
         if ((e = rt_launch_ray_trace(&Q, stream)) != hipSuccess)
             return hip_fail(e, "ray_trace_kernel launch");
@@ -1228,6 +1259,7 @@ int Renderer::get_stats(rt_stats* out) const
     for (int i = 0; i < 2; i++) out->work_abandoned[i] = last_work_[4 + i];
     for (int i = 0; i < 3; i++) out->work_wide[i] = last_work_[6 + i];
     out->deferred_pixels = last_deferred_;
+    out->exact_pixels = last_exact_;
     return RT_OK;
 }
 
@@ -1369,6 +1401,7 @@ void Renderer::take_counters(const unsigned long long* cnt)
     last_refl_ = (int64_t)cnt[1];
     for (int i = 0; i < 9; i++) last_work_[i] = (int64_t)cnt[4 + i];
     last_deferred_ = (int64_t)(cnt[3] & 0xffffffffull);
+    last_exact_ = (int64_t)(cnt[13] & 0xffffffffull);
 }
 
 float render(Renderer& renderer, int* rc)

@@ -153,7 +153,8 @@ private:
     DevBuf d_lslab_;
     // the wide BVH (wbvh.hpp): nodes, triangle records in its leaf order, slot maps
     WBvh wb_;
-    DevBuf d_wnodes_, d_wtris_, d_wslot_, d_wleaf_;
+    DevBuf d_wnodes_, d_wtris_, d_wslot_, d_wleaf_, d_defer2_;
+    DevBuf d_tile_sort_, d_tile_sort_tmp_;   // tile probe costs, sort keys, sorted order; radix-sort scratch
     bool ssao_ready_ = false;   // the buffers hold the last frame's z / normals
     // raster path: caller-order triangles, per-triangle piece counts / offsets, the piece
     // table and its texcoords, the z-key buffer, the big-piece list, scan scratch
@@ -182,6 +183,7 @@ private:
     int64_t last_primary_ = 0, last_shadow_ = 0, last_refl_ = 0;
     float last_seg_ = 0;   // KParams::seg_scale of the last frame
     int64_t last_deferred_ = 0;               // pixels the last frame handed to the ray-group pass
+    int64_t last_exact_ = 0;                  // lean mode: pixels traced through the octree (exact pass)
     int64_t last_work_[9] = {};   // RT_COUNT builds: counters[4..12] of the last frame (executed k-DOP / MT
                                   // tests: whole-line, segment, abandoned; wide-BVH nodes, triangles, uncertified)
     void take_counters(const unsigned long long* cnt);

@@ -190,10 +190,11 @@ struct WStackLocal {   // host
 // Returns W_MISS (no triangle hits at t <= hi), W_HIT (h = the minimum-t hit, finite and
 // > 0, unique when ties: still to be certified by kdop_certifies on its octree leaf) or
 // W_UNCERT.  Shadow queries (hi = the segment end of kernels.hip is_shadowed, ties false)
-// read only the record's t.  work (optional): {nodes, triangles}.
+// read only the record's t.  work (optional): {nodes, triangles}.  budget > 0: a query that
+// needs more loop iterations is abandoned (W_UNCERT).
 template <class Stack>
 RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m, Stack& stk, WHit& h,
-                       uint32_t* work = nullptr, float hi = INFINITY, bool ties = true)
+                       uint32_t* work = nullptr, float hi = INFINITY, bool ties = true, uint32_t budget = 0)
 {
     h.t = INFINITY;
     h.u = 1.0f;
@@ -215,7 +216,12 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
     int sp = 0;
     uint32_t cur = 0;   // root node
     uint32_t nn = 0, nt = 0;
+    uint32_t steps = 0;   // loop iterations (node or leaf visits): budget > 0 caps them
     while (cur != W_EMPTY) {
+        if (budget && ++steps > budget) {
+            overflow = true;   // over budget: not certified here (the caller re-traces it)
+            break;
+        }
         // ---- inner nodes: test the four child boxes, go to the nearest, push the others ----
 #if RT_W_LOOP >= 2
         // if-if: every lane takes one step (inner node or leaf) per iteration
