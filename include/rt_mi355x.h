@@ -92,12 +92,16 @@ typedef struct rt_stats {
                                   0: shadow / reflection queries walked the whole line */
     int64_t work[4];           /* diagnostic builds (-DRT_COUNT=1) only, else 0: the last frame's k-DOP and
                                   Moller-Trumbore tests of whole-line queries, then of segment queries */
-    int64_t deferred_pixels;   /* pixels of the last ray_trace whose primary query exceeded RT_DEFER_BUDGET and
-                                  were traced by the ray-group pass; 0 when deferral is off */
+    int64_t deferred_pixels;   /* pixels of the last ray_trace handed from the main kernel to a second pass: with
+                                  the wide BVH, queries over RT_WIDE_BUDGET or uncertified, else
+                                  primary queries over RT_DEFER_BUDGET (the ray-group pass, 5.5) */
     int64_t work_abandoned[2]; /* diagnostic builds only: k-DOP and Moller-Trumbore tests of primary queries
                                   abandoned over the budget (re-traced by the deferred pass, counted in work) */
-    int64_t work_wide[3];      /* diagnostic builds only: wide-BVH node visits, triangle tests, and the closest-hit
-                                  queries it could not certify (traced through the octree instead) */
+    int64_t work_wide[4];      /* diagnostic builds only: wide-BVH node visits, triangle tests, the queries it could
+                                  not certify (traced through the octree instead), and the
+                                  certificates' octree k-DOP tests */
+    int64_t exact_pixels;      /* pixels of the last frame whose queries the wide BVH could not certify, traced
+                                  through the octree by the exact pass */
 } rt_stats;
 
 typedef struct rt_renderer rt_renderer;
@@ -216,6 +220,11 @@ int rt_request_aux(rt_renderer *r, int32_t want_rgba, int32_t want_hit, int32_t 
 int rt_get_internal(rt_renderer *r, uint32_t *argb, float *rgba, int32_t *hit_id, float *hit_t, uint8_t *shadow);
 
 int rt_get_stats(rt_renderer *r, rt_stats *out);
+
+/* Diagnostic builds (-DRT_WAVE_STATS=1, with RT_DEBUG_WAVES set in the environment): the last
+ * ray_trace's per-wave records {first dequeue tick, exit tick, tiles, busy ticks} (100 MHz
+ * wall clock), n = 4 x waves values.  RT_EINVAL when no record buffer exists. */
+int rt_debug_read(rt_renderer *r, uint64_t *out, int64_t n);
 
 /* Image-strip rendering for multi-GPU (one process per GPU): renders the bands of
  * band_rows OUTPUT rows with band % nranks == rank into the device buffer d_out

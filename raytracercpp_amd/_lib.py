@@ -55,7 +55,7 @@ class RtStats(C.Structure):
         ("gpu_nodes", C.c_int64), ("gpu_tris", C.c_int64),
         ("render_width", C.c_int32), ("render_height", C.c_int32), ("seg_scale", C.c_float),
         ("work", C.c_int64 * 4), ("deferred_pixels", C.c_int64), ("work_abandoned", C.c_int64 * 2),
-        ("work_wide", C.c_int64 * 3), ("exact_pixels", C.c_int64),
+        ("work_wide", C.c_int64 * 4), ("exact_pixels", C.c_int64),
     ]
 
     def as_dict(self):
@@ -120,6 +120,7 @@ SIGNATURES = {
     "rt_obj_close": (None, [_H]),
     "rt_octree_digest": (C.c_int, [_f32p, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_uint64), _i64p,
                                    _f32p]),
+    "rt_debug_read": (C.c_int, [_H, C.POINTER(C.c_uint64), C.c_int64]),
     "rt_wbvh_query": (C.c_int, [_f32p, C.c_int64, C.c_int32, C.c_int32, _f32p, _f32p, C.c_int64, _i32p, _i32p, _f32p,
                                 _f32p, _f32p, _i64p, _f32p]),
 }

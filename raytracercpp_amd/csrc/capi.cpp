@@ -247,6 +247,10 @@ int rt_get_stats(rt_renderer* r, rt_stats* out)
 {
     return guarded(R(r), [&] { return out ? R(r)->get_stats(out) : RT_EINVAL; });
 }
+int rt_debug_read(rt_renderer* r, uint64_t* out, int64_t n)
+{
+    return guarded(R(r), [&] { return out ? R(r)->debug_read(out, n) : RT_EINVAL; });
+}
 int rt_local_rows(rt_renderer* r, int32_t band_rows, int32_t rank, int32_t nranks, int32_t* rows_out)
 {
     return guarded(R(r), [&] {

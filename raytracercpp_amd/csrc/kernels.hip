@@ -42,6 +42,9 @@ constexpr int BLOCK = 64 * WAVES_PER_BLOCK;
 #ifndef RT_COUNT
 #define RT_COUNT 0
 #endif
+#ifndef RT_WAVE_STATS
+#define RT_WAVE_STATS 0
+#endif
 #if RT_COUNT == 2
 // RT_COUNT=2 (tools/pixel_work.py): per-thread k-DOP / MT counts of the pixel being traced
 __device__ uint2 g_pixel_work[1 << 20];
@@ -980,6 +983,10 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
         r = false;
         return true;
     }
+#if RT_COUNT
+    if (st == W_HIT && P.counters)
+        atomicAdd(&P.counters[14], 1ull);   // the certificate's k-DOP test
+#endif
     if (st == W_HIT) {
         const int32_t slot = ldg(P.wslot + w.k);
         const GNode leaf = load_gnode(P.nodes + ldg(P.wleaf + slot));
@@ -1029,6 +1036,10 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
         *sh = false;
         return true;
     }
+#if RT_COUNT
+    if (st == W_HIT && P.counters)
+        atomicAdd(&P.counters[14], 1ull);
+#endif
     if (st == W_HIT && kdop_certifies(load_gnode(P.nodes + ldg(P.wleaf + ldg(P.wslot + w.k))), o, d, w.t)) {
         v3 q = o + d * w.t;
         *sh = length2(p - q) < length2(p - lp);
@@ -1589,11 +1600,15 @@ __device__ __forceinline__ int global_row(const KParams& P, int lr)
 // band's rays share that XCD's L2) and moves to the next shard when its own is empty;
 // it is done once it has found all eight empty.  One head word serves ~88 dequeues per
 // microsecond (MI355X_MICROARCH.md, dequeue row), under the frame's 130K tiles at ~2 ms.
+#ifndef RT_TILE_BATCH
+#define RT_TILE_BATCH 1   // tiles per dequeue (natural order)
+#endif
 struct TileQueue {
     int shard, empty;
+    int next, left;   // tiles of the last dequeue not yet handed out
 };
 
-__device__ __forceinline__ TileQueue tile_queue_begin() { return TileQueue{(int)(blockIdx.x & (TILE_SHARDS - 1)), 0}; }
+__device__ __forceinline__ TileQueue tile_queue_begin() { return TileQueue{(int)(blockIdx.x & (TILE_SHARDS - 1)), 0, 0, 0}; }
 
 // next tile for the calling wave (wave-uniform), or -1 when every shard is empty.  With
 // P.tile_order (tiles sorted by estimated cost, heaviest first: tile_probe_kernel) shard s
@@ -1601,10 +1616,15 @@ __device__ __forceinline__ TileQueue tile_queue_begin() { return TileQueue{(int)
 __device__ __forceinline__ int tile_queue_next(const KParams& P, TileQueue& q, int ntiles)
 {
     const int lane = threadIdx.x & 63;
+    if (q.left > 0) {
+        q.left--;
+        return q.next++;
+    }
     while (q.empty < TILE_SHARDS) {
         int t = 0;
         if (lane == 0)
-            t = (int)atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[NCOUNTERS + 16 * q.shard]), 1u);
+            t = (int)atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[NCOUNTERS + 16 * q.shard]),
+                               P.tile_order ? 1u : (unsigned)RT_TILE_BATCH);
         t = __builtin_amdgcn_readfirstlane(t);
         if (P.tile_order) {
             const int pos = q.shard + TILE_SHARDS * t;
@@ -1613,8 +1633,11 @@ __device__ __forceinline__ int tile_queue_next(const KParams& P, TileQueue& q, i
         } else {
             const int b0 = (int)((long long)ntiles * q.shard / TILE_SHARDS);
             const int b1 = (int)((long long)ntiles * (q.shard + 1) / TILE_SHARDS);
-            if (b0 + t < b1)
+            if (b0 + t < b1) {
+                q.next = b0 + t + 1;
+                q.left = min(RT_TILE_BATCH, b1 - (b0 + t)) - 1;
                 return b0 + t;
+            }
         }
         q.empty++;
         q.shard = (q.shard + 1) & (TILE_SHARDS - 1);
@@ -1691,10 +1714,19 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
     v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
     unsigned nshadow = 0, nrefl = 0;
     TileQueue q = tile_queue_begin();
+#if RT_WAVE_STATS
+    // diagnostic: per wave {first dequeue tick, exit tick, tiles, sum of tile ticks}
+    const uint64_t w_begin = wall_clock64();
+    uint64_t w_busy = 0, w_tiles = 0;
+#endif
     for (;;) {
         const int tile = tile_queue_next(P, q, ntiles);
         if (tile < 0)
             break;
+#if RT_WAVE_STATS
+        const uint64_t w_t0 = wall_clock64();
+        w_tiles++;
+#endif
         int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
         int px = tx * 8 + (lane & 7);
         int lr = ty * 8 + (lane >> 3);
@@ -1742,7 +1774,21 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
 #endif
         if (P.shadow) P.shadow[o] = (uint8_t)(po.found && po.shadowed);
         if (P.zbuf) write_ssao_buffers(P, o, po.found, cam, rd, po.fin);
+#if RT_WAVE_STATS
+        w_busy += wall_clock64() - w_t0;
+#endif
     }
+#if RT_WAVE_STATS
+    {
+        const int wid = (int)(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
+        if (P.dbg && lane == 0 && wid < DBG_WAVES) {
+            P.dbg[4 * wid + 0] = w_begin;
+            P.dbg[4 * wid + 1] = wall_clock64();
+            P.dbg[4 * wid + 2] = w_tiles;
+            P.dbg[4 * wid + 3] = w_busy;
+        }
+    }
+#endif
     if (nshadow) atomicAdd(&P.counters[0], (unsigned long long)nshadow);
     if (nrefl) atomicAdd(&P.counters[1], (unsigned long long)nrefl);
 }

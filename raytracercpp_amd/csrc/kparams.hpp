@@ -20,6 +20,7 @@ constexpr uint32_t TILE_ID_BITS = 20;
 constexpr uint32_t TILE_ID_MASK = (1u << TILE_ID_BITS) - 1;
 constexpr uint32_t TILE_COST_MAX = 2047;
 constexpr uint32_t TILE_PROBE_BUDGET = 96;
+constexpr int DBG_WAVES = 16384;   // per-wave diagnostic records (RT_WAVE_STATS builds)
 
 enum TexSlot { TEX_AO = 0, TEX_DIFFUSE = 1, TEX_NORMAL = 2, TEX_DISPLACEMENT = 3, TEX_ROUGHNESS = 4, TEX_SKYSPHERE = 5 };
 enum Shading { RT_SHADING = 0, ABS_NORMALS = 1, PASTEL_NORMALS = 2, BARYCENTRIC = 3, VISUALIZE_AO = 4 };
@@ -116,8 +117,10 @@ struct KParams {
                                     // [3] deferred-pixel list head, [4..7] executed k-DOP / MT tests of
                                     // whole-line / segment queries and [8..9] of abandoned queries, [10..11]
                                     // wide-BVH node visits / triangle tests, [12] uncertified queries (RT_COUNT),
-                                    // [13] head of the lean mode's second deferred list;
+                                    // [13] head of the lean mode's second deferred list, [14] certificate k-DOP
+                                    // tests (RT_COUNT);
                                     // then the tile-queue heads, shard s at counters[NCOUNTERS + 16 s]
+    unsigned long long* dbg;        // diagnostic builds (RT_WAVE_STATS): per wave [DBG_WAVES][4], else nullptr
     // SSAO inputs (enable_ssao): Renderer::_z_buffer / _normal_buffer, renderer.cpp:1107-1110, 975-979
     float* zbuf;
     float4* nbuf;

@@ -96,7 +96,7 @@ int Renderer::init(std::string& err)
                      &d_image_, &d_rgba_,  &d_hit_id_, &d_hit_t_,   &d_shadow_, &d_counters_, &d_band_tmp_, &d_defer_,
                      &d_tri9_,  &d_rcount_, &d_roff_,  &d_pieces_,  &d_piece_uv_, &d_zkey_, &d_big_, &d_scan_tmp_,
                      &d_zbuf_,  &d_nbuf_,   &d_ao_,     &d_cones_, &d_lslab_, &d_wnodes_, &d_wtris_, &d_wslot_,
-                     &d_wleaf_, &d_defer2_, &d_tile_sort_, &d_tile_sort_tmp_};
+                     &d_wleaf_, &d_defer2_, &d_tile_sort_, &d_tile_sort_tmp_, &d_dbg_};
     for (DevBuf* b : all) b->device = device_;
     for (auto& b : d_tex_) b.device = device_;
     for (auto& b : d_sky_) b.device = device_;
@@ -794,12 +794,12 @@ int Renderer::launch_trace(const KParams& P, hipStream_t stream)
                 Q.defer_cap = (uint32_t)npx;   // >= the launch's pixels: the list cannot overflow
             }
         }
-        // tiles in descending estimated cost (kernels.hip tile_probe_kernel): the silhouette
-        // tiles, whose grazing rays are the frame's longest, start first instead of ending it.
-        // RT_TILE_ORDER=0: natural order.
+        // RT_TILE_ORDER=1: tiles in descending estimated cost (kernels.hip tile_probe_kernel), so
+        // that the silhouette tiles, whose grazing rays are the frame's longest, start first.
+        // Measured no faster than the natural order: off by default.
         const char* to_env = getenv("RT_TILE_ORDER");
         const int ntiles = P.tiles_x * P.tiles_y;
-        if (P.wnodes && !P.pipeline && !P.has_reflection && !(to_env && to_env[0] == '0') && ntiles > 0 &&
+        if (P.wnodes && !P.pipeline && !P.has_reflection && (to_env && to_env[0] == '1') && ntiles > 0 &&
             ntiles <= (int)TILE_ID_MASK) {
             const size_t nt = (size_t)ntiles;
             if ((e = d_tile_sort_.reserve(nt * 12)) != hipSuccess)
@@ -1067,6 +1067,12 @@ int Renderer::trace_frame()
     P.shadow = want_shadow_ ? d_shadow_.as<uint8_t>() : nullptr;
     P.counters = d_counters_.as<unsigned long long>();
     if ((e = hipMemsetAsync(d_counters_.p, 0, NCOUNTER_WORDS * 8, stream_)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+    if (getenv("RT_DEBUG_WAVES")) {   // diagnostic builds: per-wave records (rt_debug_read)
+        if ((e = d_dbg_.reserve((size_t)DBG_WAVES * 32)) != hipSuccess ||
+            (e = hipMemsetAsync(d_dbg_.p, 0, (size_t)DBG_WAVES * 32, stream_)) != hipSuccess)
+            return hip_fail(e, "debug buffer");
+        P.dbg = d_dbg_.as<unsigned long long>();
+    }
     hipEventRecord(ev_[0], stream_);
     if ((rc = launch_frame(P, stream_)) != RT_OK) return rc;
     hipEventRecord(ev_[1], stream_);
@@ -1237,6 +1243,14 @@ int Renderer::get_internal(uint32_t* argb, float* rgba, int32_t* hit_id, float* 
     return RT_OK;
 }
 
+int Renderer::debug_read(uint64_t* out, int64_t n)
+{
+    if (!d_dbg_.p || n < 0 || n > (int64_t)DBG_WAVES * 4)
+        return fail(RT_EINVAL, "debug_read: no debug buffer (RT_DEBUG_WAVES) or bad size");
+    hipError_t e = hipMemcpy(out, d_dbg_.p, (size_t)n * 8, hipMemcpyDeviceToHost);
+    return e == hipSuccess ? RT_OK : hip_fail(e, "debug_read");
+}
+
 int Renderer::get_stats(rt_stats* out) const
 {
     std::memset(out, 0, sizeof(*out));
@@ -1257,7 +1271,7 @@ int Renderer::get_stats(rt_stats* out) const
     out->seg_scale = last_seg_;
     for (int i = 0; i < 4; i++) out->work[i] = last_work_[i];
     for (int i = 0; i < 2; i++) out->work_abandoned[i] = last_work_[4 + i];
-    for (int i = 0; i < 3; i++) out->work_wide[i] = last_work_[6 + i];
+    for (int i = 0; i < 4; i++) out->work_wide[i] = last_work_[6 + i];
     out->deferred_pixels = last_deferred_;
     out->exact_pixels = last_exact_;
     return RT_OK;
@@ -1400,6 +1414,7 @@ void Renderer::take_counters(const unsigned long long* cnt)
     last_shadow_ = (int64_t)cnt[0];
     last_refl_ = (int64_t)cnt[1];
     for (int i = 0; i < 9; i++) last_work_[i] = (int64_t)cnt[4 + i];
+    last_work_[9] = (int64_t)cnt[14];
     last_deferred_ = (int64_t)(cnt[3] & 0xffffffffull);
     last_exact_ = (int64_t)(cnt[13] & 0xffffffffull);
 }

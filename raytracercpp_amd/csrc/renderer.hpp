@@ -84,6 +84,7 @@ public:
     // bracketed by HIP events on the launch stream (synchronises on them)
     int kernel_times(float* ms, int n);
     int band_counters(unsigned long long out[2]);
+    int debug_read(uint64_t* out, int64_t n);   // diagnostic builds: the per-wave records of the last frame
     // BVH::intersect over n host rays (closest hit, reference semantics)
     int trace_rays(const float* orig, const float* dir, int64_t n, int32_t* id, float* t, float* u, float* v,
                    uint8_t* ret);
@@ -155,6 +156,7 @@ private:
     WBvh wb_;
     DevBuf d_wnodes_, d_wtris_, d_wslot_, d_wleaf_, d_defer2_;
     DevBuf d_tile_sort_, d_tile_sort_tmp_;   // tile probe costs, sort keys, sorted order; radix-sort scratch
+    DevBuf d_dbg_;                           // diagnostic per-wave records (RT_DEBUG_WAVES)
     bool ssao_ready_ = false;   // the buffers hold the last frame's z / normals
     // raster path: caller-order triangles, per-triangle piece counts / offsets, the piece
     // table and its texcoords, the z-key buffer, the big-piece list, scan scratch
@@ -184,8 +186,9 @@ private:
     float last_seg_ = 0;   // KParams::seg_scale of the last frame
     int64_t last_deferred_ = 0;               // pixels the last frame handed to the ray-group pass
     int64_t last_exact_ = 0;                  // lean mode: pixels traced through the octree (exact pass)
-    int64_t last_work_[9] = {};   // RT_COUNT builds: counters[4..12] of the last frame (executed k-DOP / MT
-                                  // tests: whole-line, segment, abandoned; wide-BVH nodes, triangles, uncertified)
+    int64_t last_work_[10] = {};  // RT_COUNT builds: counters[4..12], [14] of the last frame (executed k-DOP / MT
+                                  // tests: whole-line, segment, abandoned; wide-BVH nodes, triangles, uncertified,
+                                  // certificates)
     void take_counters(const unsigned long long* cnt);
     float kernel_ms_ = 0, post_ms_ = 0, build_ms_ = 0;
 };

@@ -253,7 +253,16 @@ struct Builder {
 // node box's low corner, low planes rounded down and high planes up (exact in double:
 // origin, q and the power-of-two step are all representable), so each decoded box holds
 // its float box.
-WNode quantise(const Box* cb, const uint32_t* link, int nc)
+// Per child: the area-weighted normal of its subtree's triangles and its vertices (for the
+// orientation slabs, wbvh.hpp)
+struct ChildGeom {
+    double n[3];
+    const int32_t* idx;   // the subtree's triangles: idx[first .. first + count)
+    int32_t first, count;
+};
+
+WNode quantise(const Box* cb, const uint32_t* link, int nc, const ChildGeom* cg,
+               const std::vector<GTri, DefaultInitAlloc<GTri>>* tris)
 {
     WNode w;
     std::memset(&w, 0, sizeof(w));
@@ -291,6 +300,63 @@ WNode quantise(const Box* cb, const uint32_t* link, int nc)
     }
     for (int j = 0; j < 4; j++)
         w.child[j] = link[j];
+#if RT_W_SLAB
+    // slabs: N_j = round(127 n / |n|) (integer), range of N_j . (v - origin) over the vertices
+    // in double (exact: integer N, float vertices and origin), quantised outward on 16 bits
+    double smin[4], smax[4];
+    int nq[4][3];
+    double lo_all = INFINITY, hi_all = -INFINITY;
+    for (int j = 0; j < nc; j++) {
+        const ChildGeom& g = cg[j];
+        double len = std::sqrt(g.n[0] * g.n[0] + g.n[1] * g.n[1] + g.n[2] * g.n[2]);
+        for (int a = 0; a < 3; a++)
+            nq[j][a] = len > 0 ? (int)std::lround(127.0 * g.n[a] / len) : (a == 0 ? 1 : 0);
+        if (nq[j][0] == 0 && nq[j][1] == 0 && nq[j][2] == 0)
+            nq[j][0] = 1;
+        smin[j] = INFINITY;
+        smax[j] = -INFINITY;
+        for (int32_t i = g.first; i < g.first + g.count; i++) {
+            const GTri& t = (*tris)[(size_t)g.idx[i]];
+            for (int v = 0; v < 3; v++) {
+                double s = 0;
+                for (int a = 0; a < 3; a++) {
+                    double x = (double)t.a[a] + (v == 1 ? (double)t.ab[a] : v == 2 ? (double)t.ac[a] : 0.0);
+                    s += nq[j][a] * (x - (double)org[a]);
+                }
+                smin[j] = std::min(smin[j], s);
+                smax[j] = std::max(smax[j], s);
+            }
+        }
+        lo_all = std::min(lo_all, smin[j]);
+        hi_all = std::max(hi_all, smax[j]);
+    }
+    // slo: a float at or below every smin; s: a power of two with 65535 s covering the range
+    float slo = down(lo_all);
+    double ext = hi_all - (double)slo;
+    int k = -100;
+    if (ext > 0) {
+        int e;
+        std::frexp(ext / 65535.0, &e);
+        k = std::max(-100, std::min(127, e - 1));
+        while (k < 127 && std::ldexp(65535.0, k) < ext)
+            k++;
+    }
+    const double st = std::ldexp(1.0, k);
+    w.s = (float)st;
+    w.slo = slo;
+    for (int j = 0; j < 4; j++) {
+        if (j >= nc) {
+            w.nrm[j] = 128u | (128u << 8) | (128u << 16);
+            w.slab[j] = 0;
+            continue;
+        }
+        w.nrm[j] = (uint32_t)(nq[j][0] + 128) | ((uint32_t)(nq[j][1] + 128) << 8) | ((uint32_t)(nq[j][2] + 128) << 16);
+        double q0 = std::floor((smin[j] - (double)slo) / st), q1 = std::ceil((smax[j] - (double)slo) / st);
+        q0 = std::max(0.0, std::min(65535.0, q0));
+        q1 = std::max(0.0, std::min(65535.0, q1));
+        w.slab[j] = (uint32_t)q0 | ((uint32_t)q1 << 16);
+    }
+#endif
     return w;
 }
 
@@ -312,6 +378,8 @@ Box decode(const WNode& w, int j, double lo[3], double hi[3])
 struct Collapser {
     const std::vector<BNode>& bn;
     WBvh& out;
+    const std::vector<int32_t>& idx;
+    const std::vector<GTri, DefaultInitAlloc<GTri>>& tris;
     int64_t max_depth = 0;
 
     uint32_t leaf_ref(const BNode& L) const
@@ -365,7 +433,22 @@ struct Collapser {
             } else
                 link[j] = emit(c[j], depth + 1);
         }
-        WNode w = quantise(cb, link, nc);
+        ChildGeom cg[4];
+        for (int j = 0; j < nc; j++) {
+            const BNode& C = bn[(size_t)c[j]];
+            cg[j].idx = idx.data();
+            cg[j].first = C.first;
+            cg[j].count = C.count;
+            cg[j].n[0] = cg[j].n[1] = cg[j].n[2] = 0;
+#if RT_W_SLAB
+            for (int32_t i = C.first; i < C.first + C.count; i++) {
+                const GTri& t = tris[(size_t)idx[(size_t)i]];
+                for (int a = 0; a < 3; a++)
+                    cg[j].n[a] += t.n[a];
+            }
+#endif
+        }
+        WNode w = quantise(cb, link, nc, cg, &tris);
         out.nodes[me] = w;
         return me;
     }
@@ -408,7 +491,7 @@ void build_wbvh(const FlatOctree& oct, WBvh& out)
             s += (N.left < 0 ? (double)N.count : 1.0) * area(N.box) / ra;
         out.stats.sah = (float)s;
     }
-    Collapser C{bn, out};
+    Collapser C{bn, out, idx, oct.tris};
     out.nodes.reserve(bn.size() / 2 + 1);
     C.emit(0, 1);
     out.stats.nodes = (int64_t)out.nodes.size();

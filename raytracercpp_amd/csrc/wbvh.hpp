@@ -49,22 +49,38 @@ constexpr uint32_t W_LEAF = 0x80000000u;
 constexpr uint32_t W_EMPTY = 0xFFFFFFFFu;
 constexpr int W_MAX_LEAF = 8;
 #ifndef RT_W_STACK
-#define RT_W_STACK 16
+#define RT_W_STACK 12
 #endif
 constexpr int W_STACK = RT_W_STACK;
 #ifndef RT_W_LOOP
 #define RT_W_LOOP 2   // 1: while-while, 2: if-if, 3: if-if with one triangle per step (wbvh_closest)
 #endif   // traversal stack entries per lane (overflow: the query is not certified)
 
+#ifndef RT_W_SLAB
+#define RT_W_SLAB 1   // per-child orientation slabs (below)
+#endif
+
 struct alignas(16) WNode {
     float ox, oy, oz;
     uint32_t exps;        // byte a: biased exponent (127 + k) of the step 2^k along axis a
     uint8_t qlo[3][4];    // [axis][child]
     uint8_t qhi[3][4];
+#if RT_W_SLAB
+    // Orientation slab of child j: every vertex v below it has
+    //   slo + q0 s  <=  N_j . (v - origin)  <=  slo + q1 s,
+    // N_j = (nrm bytes 0..2) - 128 (the subtree's area-weighted normal, quantised; an
+    // integer vector), q0 / q1 the low / high 16 bits of slab[j].  A curved patch is thin
+    // along its mean normal, so a ray that grazes the surface misses most patches' slabs
+    // although it crosses their boxes (silhouette rays).
+    float s, slo;
+    uint32_t nrm[4];
+    uint32_t slab[4];
+#else
     uint32_t pad[2];
+#endif
     uint32_t child[4];
 };
-static_assert(sizeof(WNode) == 64, "WNode must be 64 B");
+static_assert(sizeof(WNode) == (RT_W_SLAB ? 96 : 64), "WNode size");
 
 struct WStats {
     int64_t nodes = 0, leaves = 0, tris = 0, max_leaf = 0, depth = 0;
@@ -210,6 +226,9 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
     const float iz = 1.0f / (fabsf(d.z) < DMIN ? copysignf(DMIN, d.z) : d.z);
     const float olx = o.x + m, oly = o.y + m, olz = o.z + m;
     const float ohx = o.x - m, ohy = o.y - m, ohz = o.z - m;
+#if RT_W_SLAB
+    const float m3 = 384.0f * m;   // |N|_1 <= 3 * 128: the spatial margin in slab units
+#endif
     constexpr float SL = 0x1p-20f;   // relative slack over the rounding of a slab parameter (<= 3 ulp)
     float best_s = hi + fabsf(hi) * SL;   // h.t (or hi) plus slack: a child entered at or below it may hold a hit
     bool tie = false, nanhit = false, infhit = false, overflow = false;
@@ -234,7 +253,15 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
             const float4* p = reinterpret_cast<const float4*>(nodes + cur);
             const float4 Q0 = ldg(p);
             const uint4 Q1 = ldg(reinterpret_cast<const uint4*>(p) + 1), Q2 = ldg(reinterpret_cast<const uint4*>(p) + 2);
+#if RT_W_SLAB
+            const uint4 NR = ldg(reinterpret_cast<const uint4*>(p) + 3), SB = ldg(reinterpret_cast<const uint4*>(p) + 4);
+            const uint4 CH = ldg(reinterpret_cast<const uint4*>(p) + 5);
+            const float ss = bitsf(Q2.z), slo = bitsf(Q2.w);
+            const float Dx = Q0.x - o.x, Dy = Q0.y - o.y, Dz = Q0.z - o.z;   // origin - o
+            const uint32_t nr[4] = {NR.x, NR.y, NR.z, NR.w}, sb[4] = {SB.x, SB.y, SB.z, SB.w};
+#else
             const uint4 CH = ldg(reinterpret_cast<const uint4*>(p) + 3);
+#endif
             const uint32_t ex = fbits(Q0.w);
             // t of a plane origin + q s (widened by m) = q (s / d) + (origin -+ m - o) / d
             const float sx = bitsf((ex & 0xffu) << 23) * ix, sy = bitsf(((ex >> 8) & 0xffu) << 23) * iy,
@@ -255,6 +282,22 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                 float thz = __builtin_fmaf((float)((Q2.y >> sh) & 0xffu), sz, bz);
                 float tmin = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fminf(tlz, thz));
                 float tmax = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fmaxf(tlz, thz));
+#if RT_W_SLAB
+                {
+                    // N . (o + t d - origin) in [c0, c1] widened by m3 >= |N|_1 m: t between
+                    // (c0 - m3 + b) / a and (c1 + m3 + b) / a, b = N . (origin - o), a = N . d
+                    const float nx = (float)(nr[j] & 0xffu) - 128.0f, ny = (float)((nr[j] >> 8) & 0xffu) - 128.0f,
+                                nz = (float)((nr[j] >> 16) & 0xffu) - 128.0f;
+                    const float a = nx * d.x + ny * d.y + nz * d.z;
+                    const float b = nx * Dx + ny * Dy + nz * Dz;
+                    const float ia = 1.0f / a;
+                    const float c0 = __builtin_fmaf((float)(sb[j] & 0xffffu), ss, slo) - m3 + b;
+                    const float c1 = __builtin_fmaf((float)(sb[j] >> 16), ss, slo) + m3 + b;
+                    const float s0 = c0 * ia, s1 = c1 * ia;
+                    tmin = fmaxf(tmin, fminf(s0, s1));
+                    tmax = fminf(tmax, fmaxf(s0, s1));
+                }
+#endif
                 float tmax_s = tmax + fabsf(tmax) * SL;
                 bool ok = ch[j] != W_EMPTY && tmin <= tmax_s && tmin <= best_s && tmax_s >= 0.0f;
                 key[j] = ok ? fminf(tmin, 3.0e38f) : INFINITY;

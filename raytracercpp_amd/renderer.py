@@ -235,6 +235,12 @@ class Renderer:
         self._call("rt_get_ssao_buffers", ptr(z, _f32p), ptr(n4, _f32p), ptr(a, _i32p))
         return z, np.ascontiguousarray(n4[:, :3]), a
 
+    def debug_read(self, n):
+        """Diagnostic builds: the last frame's per-wave records (rt_debug_read)."""
+        out = np.zeros(n, np.uint64)
+        self._call("rt_debug_read", out.ctypes.data_as(C.POINTER(C.c_uint64)), n)
+        return out
+
     def stats(self) -> dict:
         s = RtStats()
         self._call("rt_get_stats", C.byref(s))

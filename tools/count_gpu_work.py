@@ -2,7 +2,8 @@
 benchmark workload, from the diagnostic build (-DRT_COUNT=1):
     python tools/variants.py build count="-DRT_COUNT=1"        (here)
     RT_LIB_PATH=_variants/librt_count.so python tools/count_gpu_work.py [config]   (GPU box)
-Prints one JSON line per mode: segment queries on (default) and off (RT_SEG=0).  A ray group's
+Prints one JSON line per mode: the default (wide BVH + segment queries) and the octree's
+literal whole-line traversal (RT_WBVH=0 RT_SEG=0).  A ray group's
 work is counted once; queries abandoned over RT_DEFER_BUDGET are counted apart (*_abandoned)."""
 import json, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -17,6 +18,7 @@ r.load_scene(sc, st)
 for mode in ("seg", "whole_line"):
     if mode == "whole_line":
         os.environ["RT_SEG"] = "0"
+        os.environ["RT_WBVH"] = "0"
     r.ray_trace()
     s = r.stats()
     w = s["work"]
@@ -25,4 +27,7 @@ for mode in ("seg", "whole_line"):
                       "vol_tests_whole_line": w[0], "tri_tests_whole_line": w[1],
                       "vol_tests_segment": w[2], "tri_tests_segment": w[3],
                       "vol_tests_abandoned": s["work_abandoned"][0], "tri_tests_abandoned": s["work_abandoned"][1],
+                      "wide_node_visits": s["work_wide"][0], "wide_tri_tests": s["work_wide"][1],
+                      "wide_uncertified": s["work_wide"][2], "wide_certificates": s["work_wide"][3],
+                      "exact_pixels": s["exact_pixels"],
                       "deferred_pixels": s["deferred_pixels"], "kernel_ms": s["kernel_ms"]}), flush=True)
