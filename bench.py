@@ -25,12 +25,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md)
-NODE_BYTES = 56              # one k-DOP test reads 14 floats
+NODE_BYTES = 56              # one octree k-DOP test reads 14 floats
 TRI_BYTES = 48               # one Moller-Trumbore test reads a, b-a, c-a, n
+WIDE_NODE_BYTES = 96         # one wide-BVH node visit reads the 96-B node (6 x 16-B loads)
+CERT_BYTES = 72              # one certificate: the octree leaf's 64-B node + two 4-B slot maps
 PIXEL_BYTES = 4              # ARGB32 write per internal pixel
 COUNTS_FILE = os.path.join(ROOT, "profiles", "work_counts.json")
 # rocprofv3 PMC summary of this kernel on the same command (tools/profile_gpu.sh + profile_summary.py)
-PROFILE_SUMMARY = os.path.join(ROOT, "profiles", "r01", "summary.json")
+PROFILE_SUMMARY = os.path.join(ROOT, "profiles", "r02", "summary.json")
 
 
 def parse():
@@ -151,44 +153,37 @@ def main():
             with open(COUNTS_FILE) as f:
                 counts = json.load(f).get(args.config)
         share = 1.0 / world
-        # the same byte model over the tests the kernel actually executes (segment queries and
-        # leaf normal cones skip work the reference's traversal does): RT_COUNT=1 build counts,
-        # tools/count_gpu_work.py -> profiles/work_counts.json "gpu_executed"
-        ex = None
-        if counts and os.environ.get("RT_CONES", "1") != "0":
-            ex = counts.get("gpu_executed") if os.environ.get("RT_SEG", "1") != "0" else \
-                counts.get("gpu_executed_whole_line")
-        executed = None
-        if ex:
-            xb = NODE_BYTES * (ex["vol_tests_whole_line"] + ex["vol_tests_segment"]) + \
-                 TRI_BYTES * (ex["tri_tests_whole_line"] + ex["tri_tests_segment"]) + PIXEL_BYTES * primary
+        # Roofline: the bytes the launch's traversal reads, per the counted units of
+        # the RT_COUNT build (tools/count_gpu_work.py -> profiles/work_counts.json "gpu_executed"):
+        # WIDE_NODE_BYTES per wide-BVH node visit, TRI_BYTES per Moller-Trumbore test, CERT_BYTES per
+        # certificate, NODE_BYTES per octree k-DOP test (uncertified queries), PIXEL_BYTES per pixel,
+        # over the mean kernel time; "traffic" is the measured HBM bytes per launch (PMC, 2 x
+        # FETCH_SIZE + WRITE_SIZE) -- the ~90 MB scene lives in L2 / Infinity Cache.
+        ex = counts.get("gpu_executed") if counts else None
+        default_path = all(os.environ.get(k, "1") != "0" for k in ("RT_WBVH", "RT_SEG", "RT_CONES"))
+        if ex and default_path:
+            xb = (WIDE_NODE_BYTES * ex.get("wide_node_visits", 0) + TRI_BYTES * ex.get("wide_tri_tests", 0) +
+                  CERT_BYTES * ex.get("wide_certificates", 0) +
+                  NODE_BYTES * (ex["vol_tests_whole_line"] + ex["vol_tests_segment"]) +
+                  TRI_BYTES * (ex["tri_tests_whole_line"] + ex["tri_tests_segment"]) + PIXEL_BYTES * primary)
             xa = xb * share / (k_mean_max * 1e-3) / 1e9
-            executed = {"bytes_per_frame": xb, "achieved": round(xa, 1), "frac": round(xa / PEAK_HBM_GBS, 4)}
-        if counts and "child_tests_primary" in counts:
-            tests = counts["child_tests_primary"] + counts["child_tests_shadow"]
-            tris = counts["tri_tests_primary"] + counts["tri_tests_shadow"]
-            nbytes = NODE_BYTES * tests + TRI_BYTES * tris + PIXEL_BYTES * primary
-            achieved = nbytes * share / (k_mean_max * 1e-3) / 1e9
             traffic = None
             if world == 1 and args.config == "sphere1m" and os.path.exists(PROFILE_SUMMARY):
                 with open(PROFILE_SUMMARY) as f:
                     traffic = json.load(f).get("hbm_traffic_bytes_per_launch")
-            # achieved = algorithmic bytes (the reference traversal's tests) / kernel
-            # time.  The ~62 MB scene is cache resident (traffic = measured HBM bytes per launch,
-            # 2 x FETCH_SIZE + WRITE_SIZE) and the kernel skips part of the reference's work, so
-            # frac exceeds 1; "executed" prices the work actually done.
-            res["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                               "frac": round(achieved / PEAK_HBM_GBS, 4),
-                               "traffic": int(traffic) if traffic else None,
-                               "algorithmic_bytes_per_frame": nbytes}
-            if executed:
-                res["roofline"]["executed"] = executed
-        elif executed:
-            # C5: no reference-traversal count (the oracle's count mode would take hours); the
-            # roofline is over the executed tests of the whole frame engine
-            res["roofline"] = {"bound": "hbm", "achieved": executed["achieved"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                               "frac": executed["frac"], "traffic": None,
-                               "algorithmic_bytes_per_frame": executed["bytes_per_frame"], "basis": "executed tests"}
+            res["roofline"] = {"bound": "hbm", "achieved": round(xa, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                               "frac": round(xa / PEAK_HBM_GBS, 4), "traffic": int(traffic) if traffic else None,
+                               "algorithmic_bytes_per_frame": xb,
+                               "basis": "bytes read by the executed traversal (wide-BVH nodes 96 B, triangles 48 B, "
+                                        "certificates 72 B, octree k-DOPs 56 B) + 4 B/pixel; RT_COUNT counts"}
+            if counts and "child_tests_primary" in counts:
+                # SURVEY.md 8(d)'s model priced on the REFERENCE's traversal (oracle count mode): the work
+                # the reference's octree walk would read, per second of this kernel
+                tests = counts["child_tests_primary"] + counts["child_tests_shadow"]
+                tris = counts["tri_tests_primary"] + counts["tri_tests_shadow"]
+                nbytes = NODE_BYTES * tests + TRI_BYTES * tris + PIXEL_BYTES * primary
+                res["roofline"]["reference_traversal_equivalent"] = {
+                    "bytes_per_frame": nbytes, "achieved": round(nbytes * share / (k_mean_max * 1e-3) / 1e9, 1)}
         if world == 1 and not args.no_cpu_baseline:
             if c5:
                 res["cpu_baseline"] = cpu_baseline_c5(sc, st, args.cpu_threads)

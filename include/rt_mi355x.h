@@ -100,6 +100,9 @@ typedef struct rt_stats {
     int64_t work_wide[4];      /* diagnostic builds only: wide-BVH node visits, triangle tests, the queries it could
                                   not certify (traced through the octree instead), and the
                                   certificates' octree k-DOP tests */
+    int64_t uncertified[6];    /* diagnostic builds only: uncertified wide-BVH queries by reason -- stack overflow,
+                                  NaN hit, only overflowed hits, tie, minimum t outside (0, inf), failed
+                                  certificate */
     int64_t exact_pixels;      /* pixels of the last frame whose queries the wide BVH could not certify, traced
                                   through the octree by the exact pass */
 } rt_stats;

@@ -45,6 +45,12 @@ constexpr int BLOCK = 64 * WAVES_PER_BLOCK;
 #ifndef RT_WAVE_STATS
 #define RT_WAVE_STATS 0
 #endif
+#ifndef RT_OCC_PRIM
+#define RT_OCC_PRIM 5
+#endif
+#ifndef RT_OCC_SHADE
+#define RT_OCC_SHADE 5
+#endif
 #if RT_COUNT == 2
 // RT_COUNT=2 (tools/pixel_work.py): per-thread k-DOP / MT counts of the pixel being traced
 __device__ uint2 g_pixel_work[1 << 20];
@@ -104,6 +110,19 @@ __device__ __forceinline__ TRay make_ray(const KParams& P, v3 o, v3 d)
     R.lo = -INFINITY;
     R.hi = INFINITY;
     return R;
+}
+
+// make_ray's R.nan alone (the primary pass needs no plane products)
+__device__ __forceinline__ bool ray_is_nan(v3 o, v3 d)
+{
+    bool nan = false;
+#pragma unroll
+    for (int i = 0; i < NPLANES; i++) {
+        v3 n = mk(PLANE_N[i][0], PLANE_N[i][1], PLANE_N[i][2]);
+        float den = dot(n, d), num = dot(n, o);
+        nan |= (den != den) || (num != num);
+    }
+    return nan;
 }
 
 struct NodeBox {
@@ -960,12 +979,15 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
     WStackLds stk{lv};
     WHit w;
 #if RT_COUNT
-    uint32_t wk[2] = {0, 0};
+    uint32_t wk[3] = {0, 0, 0};
     const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, INFINITY, true,
                                 P.wide_budget);
     if (P.counters) {
         atomicAdd(&P.counters[10], (unsigned long long)wk[0]);
         atomicAdd(&P.counters[11], (unsigned long long)wk[1]);
+        for (int c = 0; c < 5; c++)
+            if ((wk[2] >> c) & 1u)
+                atomicAdd(&P.counters[16 + c], 1ull);   // uncertified, by reason (wbvh_closest)
     }
 #if RT_COUNT == 2
     g_pixel_work[pixel_work_slot()].x += wk[0];
@@ -1000,8 +1022,11 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
         }
     }
 #if RT_COUNT
-    if (P.counters)
+    if (P.counters) {
         atomicAdd(&P.counters[12], 1ull);
+        if (st == W_HIT)
+            atomicAdd(&P.counters[21], 1ull);   // the certificate's k-DOP test failed
+    }
 #endif
     return false;
 }
@@ -1017,12 +1042,15 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
     WStackLds stk{lv};
     WHit w;
 #if RT_COUNT
-    uint32_t wk[2] = {0, 0};
+    uint32_t wk[3] = {0, 0, 0};
     const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, hi, false,
                                 P.wide_budget);
     if (P.counters) {
         atomicAdd(&P.counters[10], (unsigned long long)wk[0]);
         atomicAdd(&P.counters[11], (unsigned long long)wk[1]);
+        for (int c = 0; c < 5; c++)
+            if ((wk[2] >> c) & 1u)
+                atomicAdd(&P.counters[16 + c], 1ull);   // uncertified, by reason (wbvh_closest)
     }
 #if RT_COUNT == 2
     g_pixel_work[pixel_work_slot()].x += wk[0];
@@ -1046,8 +1074,11 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
         return true;
     }
 #if RT_COUNT
-    if (P.counters)
+    if (P.counters) {
         atomicAdd(&P.counters[12], 1ull);
+        if (st == W_HIT)
+            atomicAdd(&P.counters[21], 1ull);   // the certificate's k-DOP test failed
+    }
 #endif
     return false;
 }
@@ -1623,7 +1654,7 @@ __device__ __forceinline__ int tile_queue_next(const KParams& P, TileQueue& q, i
     while (q.empty < TILE_SHARDS) {
         int t = 0;
         if (lane == 0)
-            t = (int)atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[NCOUNTERS + 16 * q.shard]),
+            t = (int)atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[P.tq_base + 16 * q.shard]),
                                P.tile_order ? 1u : (unsigned)RT_TILE_BATCH);
         t = __builtin_amdgcn_readfirstlane(t);
         if (P.tile_order) {
@@ -1671,7 +1702,7 @@ __global__ __launch_bounds__(BLOCK) void tile_probe_kernel(KParams P, uint32_t* 
     const float om = fmaxf(fabsf(cam.x), fmaxf(fabsf(cam.y), fabsf(cam.z)));
     WStackLds stk{lv};
     WHit w;
-    uint32_t wk[2] = {0, 0};
+    uint32_t wk[3] = {0, 0, 0};
     wbvh_closest(P.wnodes, P.wtris, cam, rd, 0x1p-16f * (om + P.scene_scale), stk, w, wk, INFINITY, true,
                  TILE_PROBE_BUDGET);
     cost[tile] = wk[0] + wk[1];
@@ -1791,6 +1822,158 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
 #endif
     if (nshadow) atomicAdd(&P.counters[0], (unsigned long long)nshadow);
     if (nrefl) atomicAdd(&P.counters[1], (unsigned long long)nrefl);
+}
+
+// ---- Split frame ----
+// Pass 1 (primary_kernel): per pixel, the primary ray's closest hit through the wide BVH
+// and its certificate, stored as a PrimRec.  Pass 2 (shade_kernel): the rest of trace_ray
+// from that record -- shading, the shadow ray through the wide BVH, the framebuffer.  The
+// pixels either pass cannot certify are rendered from scratch by the exact pass
+// (ray_trace_defer_kernel): pass 1's on a second stream while pass 2 runs, pass 2's after
+// it.  Each pass holds only its own state, so neither spills the traversal's registers.
+__device__ __forceinline__ v3 primary_dir(const KParams& P, int px, int py, v3 cam)
+{
+    // ray generation, renderer.cpp:1086-1098
+    float y_world = ((float)py + 0.5f) / P.rh * 2 - 1;
+    float x_world = ((float)px + 0.5f) / P.rw * 2 - 1;
+    v3 vs = xform_point(P.proj_inv, mk(x_world, y_world, -1));
+    v3 ws = xform_point(P.cam_to_world, vs);
+    return normalize(ws - cam);
+}
+
+__global__ __launch_bounds__(BLOCK, RT_OCC_PRIM) void primary_kernel(KParams P)
+{
+    extern __shared__ uint2 lds_levels[];
+    uint2* lv = lds_levels + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int ntiles = P.tiles_x * P.tiles_y;
+    const v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+    TileQueue q = tile_queue_begin();
+    for (;;) {
+        const int tile = tile_queue_next(P, q, ntiles);
+        if (tile < 0)
+            break;
+        const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+        const int px = tx * 8 + (lane & 7);
+        const int lr = ty * 8 + (lane >> 3);
+        const int py = lr < P.local_rows ? global_row(P, lr) : P.rh;
+        if (px >= P.rw || py >= P.rh)
+            continue;
+        const v3 rd = primary_dir(P, px, py, cam);
+        PrimRec rec;
+        rec.t = -1.0f;
+        rec.u = 1.0f;
+        rec.v = 0.0f;
+        rec.k = PRIM_MISS;
+        if (P.nnodes > 0) {
+            THit h;
+            bool r;
+            if (ray_is_nan(cam, rd)) {
+                rec.t = __int_as_float(0x7fc00000);
+                rec.k = PRIM_NAN;
+            } else if (wide_closest(P, cam, rd, h, r, lv)) {
+                rec.t = h.t;
+                rec.u = h.u;
+                rec.v = h.v;
+                rec.k = h.k >= 0 ? h.k : PRIM_MISS;
+            } else {
+                rec.k = PRIM_EXACT;
+                uint32_t idx = atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[P.defer_head]), 1u);
+                P.defer[idx] = (uint32_t)(lr * P.rw + px);
+            }
+        }
+        reinterpret_cast<float4*>(P.prim)[(size_t)lr * P.rw + px] = make_float4(rec.t, rec.u, rec.v, __int_as_float(rec.k));
+    }
+}
+
+__global__ __launch_bounds__(BLOCK, RT_OCC_SHADE) void shade_kernel(KParams P)
+{
+    extern __shared__ uint2 lds_levels[];
+    uint2* lv = lds_levels + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int ntiles = P.tiles_x * P.tiles_y;
+    const v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+    unsigned nshadow = 0;
+    TileQueue q = tile_queue_begin();
+    for (;;) {
+        const int tile = tile_queue_next(P, q, ntiles);
+        if (tile < 0)
+            break;
+        const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+        const int px = tx * 8 + (lane & 7);
+        const int lr = ty * 8 + (lane >> 3);
+        const int py = lr < P.local_rows ? global_row(P, lr) : P.rh;
+        if (px >= P.rw || py >= P.rh)
+            continue;
+        const size_t o = (size_t)lr * P.rw + px;
+        const float4 pr = ldg(reinterpret_cast<const float4*>(P.prim) + o);
+        const int32_t k = __float_as_int(pr.w);
+        if (k == PRIM_EXACT)
+            continue;   // the exact pass renders it
+        const v3 rd = primary_dir(P, px, py, cam);
+        // trace_ray's closest hit (renderer.cpp:1015-1020) from the record, as closest_hit
+        PixelOut po;
+        po.fin = rec_fresh();
+        po.found = po.shadowed = po.deferred = false;
+        po.alpha = 1.0f;
+        {
+            THit h;
+            h.t = pr.x;
+            h.u = pr.y;
+            h.v = pr.z;
+            h.k = k >= 0 ? k : -1;
+            Rec local = rec_fresh();
+            int src = -1;
+            bvh_record(P, h, k >= 0, local, po.fin, src);
+            shapes_closest(P, cam, rd, local, po.fin, src);
+            po.src = src;
+        }
+        // everything but the colour and the shadow flag is final before the shadow ray: write it
+        // now, so that only the shading colour stays live across the shadow traversal
+        po.found = po.fin.t > 0.1f;
+        if (P.hit_id) P.hit_id[o] = po.found ? po.src : -1;
+        if (!po.found) {
+            po.color = miss_color(P, rd, po.alpha);
+            if (P.hit_t) P.hit_t[o] = po.fin.t;
+            if (P.argb) P.argb[o] = color_to_argb(po.color);
+            if (P.rgba) P.rgba[o] = make_float4(po.color.r, po.color.g, po.color.b, po.alpha);
+            if (P.shadow) P.shadow[o] = 0;
+            if (P.zbuf) write_ssao_buffers(P, o, false, cam, rd, po.fin);
+            continue;
+        }
+        if (P.shading_method != RT_SHADING) {
+            po.color = clamp3(shade_debug(P, po.fin));
+            if (P.hit_t) P.hit_t[o] = po.fin.t;
+            if (P.argb) P.argb[o] = color_to_argb(po.color);
+            if (P.rgba) P.rgba[o] = make_float4(po.color.r, po.color.g, po.color.b, 1.0f);
+            if (P.shadow) P.shadow[o] = 0;
+            if (P.zbuf) write_ssao_buffers(P, o, true, cam, rd, po.fin);
+            continue;
+        }
+        // shade_direct (RT_SHADING), renderer.cpp:556-593
+        v3 ip;
+        const c3 lit = shade_lit(P, cam, rd, po.fin, ip);
+        if (P.hit_t) P.hit_t[o] = po.fin.t;
+        if (P.zbuf) write_ssao_buffers(P, o, true, cam, rd, po.fin);   // normal-mapped normal
+        const int mat = po.fin.mat;
+        const v3 nrm = po.fin.normal;
+        const v3 light = mk(P.light[0], P.light[1], P.light[2]);
+        bool defer = false;
+        const bool sh = is_shadowed<false, true>(P, ip, nrm, light, lv, &defer);
+        if (defer) {
+            uint32_t idx = atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[P.defer_head]), 1u);
+            P.defer[idx] = (uint32_t)o;
+            continue;
+        }
+        if (P.compute_shadows)
+            nshadow++;
+        const float* m = mat_of(P, mat);
+        const c3 color = shade_finish(P, shade_shadow_emit(P, lit, m, sh), m, col(0, 0, 0));
+        if (P.argb) P.argb[o] = color_to_argb(color);
+        if (P.rgba) P.rgba[o] = make_float4(color.r, color.g, color.b, 1.0f);
+        if (P.shadow) P.shadow[o] = (uint8_t)sh;
+    }
+    if (nshadow) atomicAdd(&P.counters[0], (unsigned long long)nshadow);
 }
 
 // The deferred pass: every pixel whose primary query exceeded
@@ -3081,6 +3264,35 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_tile_probe
     return hipGetLastError();
 }
 
+// split frame: pass 1 (stage 0), pass 2 (stage 1), the exact pass over a list (stage 2:
+// list P->defer_in, count counters[P->defer_in_head])
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_split(int stage, const rt::KParams* P,
+                                                                           hipStream_t stream)
+{
+    const int tiles = P->tiles_x * P->tiles_y;
+    int blocks = (tiles + rt::WAVES_PER_BLOCK - 1) / rt::WAVES_PER_BLOCK;
+    if (blocks > P->max_blocks && P->max_blocks > 0)
+        blocks = P->max_blocks;
+    if (blocks < 1)
+        return hipSuccess;
+    const size_t lds = rt::lds_bytes(*P);
+    rt::KParams A = *P;
+    if (stage == 0) {
+        A.tq_base = rt::NCOUNTERS;
+        A.grp_shift = 0;
+        hipLaunchKernelGGL(rt::primary_kernel, dim3(blocks), dim3(rt::BLOCK), lds, stream, A);
+    } else if (stage == 1) {
+        A.tq_base = rt::NCOUNTERS2;
+        A.grp_shift = 0;
+        hipLaunchKernelGGL(rt::shade_kernel, dim3(blocks), dim3(rt::BLOCK), lds, stream, A);
+    } else {
+        // few pixels (ties, stack overflows): a small grid, so that it fits beside the shade pass
+        const int db = 256;
+        hipLaunchKernelGGL(rt::ray_trace_defer_kernel, dim3(db), dim3(rt::BLOCK), lds, stream, A);
+    }
+    return hipGetLastError();
+}
+
 // ---- host-side launch wrappers (called from renderer.cpp) ----
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(const rt::KParams* P, hipStream_t stream)
 {
@@ -3098,6 +3310,7 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(
         rt::KParams A = *P;
         A.grp_shift = 0;   // one lane per pixel; the groups are the deferred pass's
         A.defer_head = 3;
+        A.tq_base = rt::NCOUNTERS;
         const int db = P->max_blocks > 0 ? P->max_blocks : 1024;
         if (P->wide_lean && P->defer && P->defer2 && P->defer_cap) {
             // lean kernel (list 1: over-budget or uncertified pixels, head counters[3]) -> heavy-pixel

@@ -12,9 +12,13 @@ namespace rt {
 constexpr int TEX_SLOTS = 6;   // ao, diffuse, normal, displacement, roughness, skysphere (renderer.h:77-84)
 constexpr int MAT_STRIDE = 16; // see include/rt_mi355x.h
 constexpr int MAX_SHAPES = 64;
-constexpr int NCOUNTERS = 16;  // KParams::counters entries (u64) before the tile-queue heads
-constexpr int TILE_SHARDS = 8; // tile-queue shards (one per XCD group, blockIdx % 8)
-constexpr int NCOUNTER_WORDS = NCOUNTERS + 16 * TILE_SHARDS;   // + one 128-B line per shard head
+constexpr int NCOUNTERS = 32;  // KParams::counters entries (u64) before the tile-queue heads
+#ifndef RT_TILE_SHARDS
+#define RT_TILE_SHARDS 8
+#endif
+constexpr int TILE_SHARDS = RT_TILE_SHARDS;   // tile-queue shards (blockIdx % TILE_SHARDS; a power of 2)
+constexpr int NCOUNTERS2 = NCOUNTERS + 16 * TILE_SHARDS;      // a second set of heads (split frame's shade pass)
+constexpr int NCOUNTER_WORDS = NCOUNTERS2 + 16 * TILE_SHARDS;  // one 128-B line per shard head
 // tile order (kernels.hip tile_probe_kernel): key = (TILE_COST_MAX - cost) << TILE_ID_BITS | tile
 constexpr uint32_t TILE_ID_BITS = 20;
 constexpr uint32_t TILE_ID_MASK = (1u << TILE_ID_BITS) - 1;
@@ -29,6 +33,15 @@ struct KTex {
     const float4* px;   // row-major texels (Image, tp2/src/image.h:20-135), nullptr when absent
     int w, h;
 };
+
+// Split frame: the primary pass's record of one pixel
+struct PrimRec {
+    float t, u, v;
+    int32_t k;   // >= 0: the certified hit's GTri slot; PRIM_MISS / PRIM_NAN / PRIM_EXACT
+};
+constexpr int32_t PRIM_MISS = -1;    // certified: no triangle hit (BVH::intersect returns false)
+constexpr int32_t PRIM_EXACT = -2;   // not certified: the exact pass renders the pixel
+constexpr int32_t PRIM_NAN = -3;     // NaN ray: NaN record, returns false (trav_begin)
 
 struct KParams {
     // geometry (flattened octree, octree.hpp)
@@ -118,9 +131,12 @@ struct KParams {
                                     // whole-line / segment queries and [8..9] of abandoned queries, [10..11]
                                     // wide-BVH node visits / triangle tests, [12] uncertified queries (RT_COUNT),
                                     // [13] head of the lean mode's second deferred list, [14] certificate k-DOP
-                                    // tests (RT_COUNT);
+                                    // tests, [16..21] uncertified queries by reason (RT_COUNT: overflow, NaN,
+                                    // overflowed-only, tie, t outside (0, inf), certificate failed);
                                     // then the tile-queue heads, shard s at counters[NCOUNTERS + 16 s]
     unsigned long long* dbg;        // diagnostic builds (RT_WAVE_STATS): per wave [DBG_WAVES][4], else nullptr
+    PrimRec* prim;            // split frame: one record per launch pixel (lr * rw + px), else nullptr
+    int32_t tq_base;          // first counters[] word of this launch's tile-queue heads (NCOUNTERS or NCOUNTERS2)
     // SSAO inputs (enable_ssao): Renderer::_z_buffer / _normal_buffer, renderer.cpp:1107-1110, 975-979
     float* zbuf;
     float4* nbuf;

@@ -13,6 +13,8 @@
 #include "host_scene.hpp"
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(const rt::KParams* P, hipStream_t stream);
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_split(int stage, const rt::KParams* P,
+                                                                           hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_tile_probe(const rt::KParams* P, uint32_t* cost,
                                                                                 uint32_t* keys, hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_level0(const rt::KParams* P, rt::FrameRec* fr1,
@@ -96,7 +98,7 @@ int Renderer::init(std::string& err)
                      &d_image_, &d_rgba_,  &d_hit_id_, &d_hit_t_,   &d_shadow_, &d_counters_, &d_band_tmp_, &d_defer_,
                      &d_tri9_,  &d_rcount_, &d_roff_,  &d_pieces_,  &d_piece_uv_, &d_zkey_, &d_big_, &d_scan_tmp_,
                      &d_zbuf_,  &d_nbuf_,   &d_ao_,     &d_cones_, &d_lslab_, &d_wnodes_, &d_wtris_, &d_wslot_,
-                     &d_wleaf_, &d_defer2_, &d_tile_sort_, &d_tile_sort_tmp_, &d_dbg_};
+                     &d_wleaf_, &d_defer2_, &d_tile_sort_, &d_tile_sort_tmp_, &d_dbg_, &d_prim_};
     for (DevBuf* b : all) b->device = device_;
     for (auto& b : d_tex_) b.device = device_;
     for (auto& b : d_sky_) b.device = device_;
@@ -110,6 +112,9 @@ Renderer::~Renderer()
         if (e) hipEventDestroy(e);
     for (auto& e : ring_)
         if (e) hipEventDestroy(e);
+    if (fork_) hipEventDestroy(fork_);
+    if (join_) hipEventDestroy(join_);
+    if (stream2_) hipStreamDestroy(stream2_);
     if (stream_) hipStreamDestroy(stream_);
 }
 
@@ -728,6 +733,7 @@ void Renderer::fill_params(KParams& P) const
             P.seg_scale = S;
     }
     P.max_blocks = num_cus_ * 8;
+    P.tq_base = NCOUNTERS;
     render_size(P.rw, P.rh);
 }
 
@@ -742,6 +748,58 @@ int Renderer::launch_trace(const KParams& P, hipStream_t stream)
     hipError_t e;
     const char* env = getenv("RT_REFL_ENGINE");
     bool engine = P.has_reflection && P.enable_bvh && !(env && env[0] == '0');
+    split_last_ = false;
+    const char* split_env = getenv("RT_SPLIT");
+    const size_t npx_split = (size_t)P.rw * P.local_rows;
+    if (!engine && P.wnodes && P.seg_scale > 0.0f && P.enable_bvh && !P.has_reflection && !P.pipeline &&
+        (split_env && split_env[0] == '1') && npx_split > 0 && npx_split < (1ull << 32)) {
+        // RT_SPLIT=1, split frame: primary pass -> records; the exact pass over the
+        // pixels it could not certify runs on stream2_ while the shade pass runs on 'stream'; then
+        // the exact pass over the shade pass's uncertified shadow queries; join.  Measured slower
+        // than the fused kernel (each pass pays the per-pixel and queue costs): off by default.
+        if ((e = d_prim_.reserve(npx_split * sizeof(PrimRec))) != hipSuccess ||
+            (e = d_defer_.reserve(npx_split * 4)) != hipSuccess || (e = d_defer2_.reserve(npx_split * 4)) != hipSuccess)
+            return hip_fail(e, "hipMalloc (split frame)");
+        if (!stream2_) {
+            // high priority: its few blocks are dispatched ahead of the shade pass's persistent grid
+            int lo = 0, hi = 0;
+            if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess)
+                hi = 0;
+            if ((e = hipStreamCreateWithPriority(&stream2_, hipStreamNonBlocking, hi)) != hipSuccess)
+                return hip_fail(e, "hipStreamCreate");
+        }
+        if (!fork_ && ((e = hipEventCreateWithFlags(&fork_, hipEventDisableTiming)) != hipSuccess ||
+                       (e = hipEventCreateWithFlags(&join_, hipEventDisableTiming)) != hipSuccess))
+            return hip_fail(e, "hipEventCreate");
+        const char* gs = getenv("RT_GROUP_SHIFT");
+        long shift = gs ? atol(gs) : 5;
+        KParams Q = P;
+        Q.prim = d_prim_.as<PrimRec>();
+        Q.grp_shift = (shift >= 1 && shift <= 6) ? (int32_t)shift : 5;
+        Q.defer_cap = (uint32_t)npx_split;
+        Q.trav_budget = 0;
+        Q.defer = d_defer_.as<uint32_t>();
+        Q.defer_head = 3;
+        if ((e = rt_launch_split(0, &Q, stream)) != hipSuccess) return hip_fail(e, "primary_kernel launch");
+        if ((e = hipEventRecord(fork_, stream)) != hipSuccess || (e = hipStreamWaitEvent(stream2_, fork_, 0)) != hipSuccess)
+            return hip_fail(e, "split fork");
+        KParams C = Q;
+        C.defer_in = d_defer_.as<uint32_t>();
+        C.defer_in_head = 3;
+        if ((e = rt_launch_split(2, &C, stream2_)) != hipSuccess) return hip_fail(e, "exact pass launch");
+        if ((e = hipEventRecord(join_, stream2_)) != hipSuccess) return hip_fail(e, "split join");
+        KParams B = Q;
+        B.defer = d_defer2_.as<uint32_t>();
+        B.defer_head = 13;
+        if ((e = rt_launch_split(1, &B, stream)) != hipSuccess) return hip_fail(e, "shade_kernel launch");
+        KParams D = Q;
+        D.defer_in = d_defer2_.as<uint32_t>();
+        D.defer_in_head = 13;
+        if ((e = rt_launch_split(2, &D, stream)) != hipSuccess) return hip_fail(e, "exact pass launch");
+        if ((e = hipStreamWaitEvent(stream, join_, 0)) != hipSuccess) return hip_fail(e, "split join");
+        split_last_ = true;
+        return RT_OK;
+    }
     if (!engine) {
         // deferred pixels (kernels.hip ray_trace_defer_kernel):
         // RT_DEFER_BUDGET (default 1000; 0 = off) and RT_GROUP_SHIFT (default 5: 32 lanes per ray)
@@ -1272,6 +1330,7 @@ int Renderer::get_stats(rt_stats* out) const
     for (int i = 0; i < 4; i++) out->work[i] = last_work_[i];
     for (int i = 0; i < 2; i++) out->work_abandoned[i] = last_work_[4 + i];
     for (int i = 0; i < 4; i++) out->work_wide[i] = last_work_[6 + i];
+    for (int i = 0; i < 6; i++) out->uncertified[i] = last_uncert_[i];
     out->deferred_pixels = last_deferred_;
     out->exact_pixels = last_exact_;
     return RT_OK;
@@ -1415,8 +1474,11 @@ void Renderer::take_counters(const unsigned long long* cnt)
     last_refl_ = (int64_t)cnt[1];
     for (int i = 0; i < 9; i++) last_work_[i] = (int64_t)cnt[4 + i];
     last_work_[9] = (int64_t)cnt[14];
+    for (int i = 0; i < 6; i++) last_uncert_[i] = (int64_t)cnt[16 + i];
     last_deferred_ = (int64_t)(cnt[3] & 0xffffffffull);
-    last_exact_ = (int64_t)(cnt[13] & 0xffffffffull);
+    last_exact_ = (int64_t)(cnt[13] & 0xffffffffull) + (split_last_ ? (int64_t)(cnt[3] & 0xffffffffull) : 0);
+    if (split_last_)
+        last_deferred_ = 0;
 }
 
 float render(Renderer& renderer, int* rc)

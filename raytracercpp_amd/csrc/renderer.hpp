@@ -117,6 +117,10 @@ private:
     int num_cus_ = 256;
     hipStream_t stream_ = nullptr;
     hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};
+    // split frame: the exact pass's stream and the fork / join events
+    hipStream_t stream2_ = nullptr;
+    hipEvent_t fork_ = nullptr, join_ = nullptr;
+    bool split_last_ = false;   // the last frame ran split (exact_pixels = both lists)
     std::string err_;
 
     rt_settings s_;
@@ -157,6 +161,7 @@ private:
     DevBuf d_wnodes_, d_wtris_, d_wslot_, d_wleaf_, d_defer2_;
     DevBuf d_tile_sort_, d_tile_sort_tmp_;   // tile probe costs, sort keys, sorted order; radix-sort scratch
     DevBuf d_dbg_;                           // diagnostic per-wave records (RT_DEBUG_WAVES)
+    DevBuf d_prim_;                          // split frame: the primary pass's records (PrimRec per pixel)
     bool ssao_ready_ = false;   // the buffers hold the last frame's z / normals
     // raster path: caller-order triangles, per-triangle piece counts / offsets, the piece
     // table and its texcoords, the z-key buffer, the big-piece list, scan scratch
@@ -189,6 +194,7 @@ private:
     int64_t last_work_[10] = {};  // RT_COUNT builds: counters[4..12], [14] of the last frame (executed k-DOP / MT
                                   // tests: whole-line, segment, abandoned; wide-BVH nodes, triangles, uncertified,
                                   // certificates)
+    int64_t last_uncert_[6] = {};   // RT_COUNT builds: uncertified wide-BVH queries by reason
     void take_counters(const unsigned long long* cnt);
     float kernel_ms_ = 0, post_ms_ = 0, build_ms_ = 0;
 };

@@ -52,6 +52,9 @@ constexpr int W_MAX_LEAF = 8;
 #define RT_W_STACK 12
 #endif
 constexpr int W_STACK = RT_W_STACK;
+#ifndef RT_W_SCHED_BARRIER
+#define RT_W_SCHED_BARRIER 1
+#endif
 #ifndef RT_W_LOOP
 #define RT_W_LOOP 2   // 1: while-while, 2: if-if, 3: if-if with one triangle per step (wbvh_closest)
 #endif   // traversal stack entries per lane (overflow: the query is not certified)
@@ -184,6 +187,17 @@ RT_HD bool kdop_certifies(const GNode& nd, v3 o, v3 d, float t)
     return !(t_far < t_near) && t_near <= t;
 }
 
+RT_HD float fast_rcp(float a)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcpf(a);
+#else
+    // host emulation: the correctly rounded reciprocal (the device's is within 1 ulp of it;
+    // both stay inside the slab margin)
+    return 1.0f / a;
+#endif
+}
+
 RT_HD uint32_t fbits(float f) { return __builtin_bit_cast(uint32_t, f); }
 RT_HD float bitsf(uint32_t u) { return __builtin_bit_cast(float, u); }
 
@@ -206,7 +220,8 @@ struct WStackLocal {   // host
 // Returns W_MISS (no triangle hits at t <= hi), W_HIT (h = the minimum-t hit, finite and
 // > 0, unique when ties: still to be certified by kdop_certifies on its octree leaf) or
 // W_UNCERT.  Shadow queries (hi = the segment end of kernels.hip is_shadowed, ties false)
-// read only the record's t.  work (optional): {nodes, triangles}.  budget > 0: a query that
+// read only the record's t.  work (optional, 3 entries): {nodes, triangles} added, [2] = the
+// reasons a query is not certified.  budget > 0: a query that
 // needs more loop iterations is abandoned (W_UNCERT).
 template <class Stack>
 RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m, Stack& stk, WHit& h,
@@ -256,7 +271,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
 #if RT_W_SLAB
             const uint4 NR = ldg(reinterpret_cast<const uint4*>(p) + 3), SB = ldg(reinterpret_cast<const uint4*>(p) + 4);
             const uint4 CH = ldg(reinterpret_cast<const uint4*>(p) + 5);
-            const float ss = bitsf(Q2.z), slo = bitsf(Q2.w);
+            const float ss = bitsf(Q2.z), slo_lo = bitsf(Q2.w) - m3, slo_hi = bitsf(Q2.w) + m3;
             const float Dx = Q0.x - o.x, Dy = Q0.y - o.y, Dz = Q0.z - o.z;   // origin - o
             const uint32_t nr[4] = {NR.x, NR.y, NR.z, NR.w}, sb[4] = {SB.x, SB.y, SB.z, SB.w};
 #else
@@ -290,9 +305,11 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                                 nz = (float)((nr[j] >> 16) & 0xffu) - 128.0f;
                     const float a = nx * d.x + ny * d.y + nz * d.z;
                     const float b = nx * Dx + ny * Dy + nz * Dz;
-                    const float ia = 1.0f / a;
-                    const float c0 = __builtin_fmaf((float)(sb[j] & 0xffffu), ss, slo) - m3 + b;
-                    const float c1 = __builtin_fmaf((float)(sb[j] >> 16), ss, slo) + m3 + b;
+                    // the hardware reciprocal (1 ulp): its error moves the slab's t by a relative
+                    // 2^-23, a distance far inside the margin m3 over the scene
+                    const float ia = fast_rcp(a);
+                    const float c0 = __builtin_fmaf((float)(sb[j] & 0xffffu), ss, slo_lo) + b;
+                    const float c1 = __builtin_fmaf((float)(sb[j] >> 16), ss, slo_hi) + b;
                     const float s0 = c0 * ia, s1 = c1 * ia;
                     tmin = fmaxf(tmin, fminf(s0, s1));
                     tmax = fminf(tmax, fmaxf(s0, s1));
@@ -302,6 +319,11 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                 bool ok = ch[j] != W_EMPTY && tmin <= tmax_s && tmin <= best_s && tmax_s >= 0.0f;
                 key[j] = ok ? fminf(tmin, 3.0e38f) : INFINITY;
                 ref[j] = ch[j];
+#if defined(__HIP_DEVICE_COMPILE__) && RT_W_SCHED_BARRIER
+                // one child at a time: the scheduler would interleave the four children's
+                // temporaries (VALU latency is hidden by the other waves anyway)
+                __builtin_amdgcn_sched_barrier(0);
+#endif
             }
             // sort the four (key, ref) pairs ascending: misses (INFINITY) go last
 #define W_CSWAP(a, b)                                                              \
@@ -387,6 +409,10 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
     if (work) {
         work[0] += nn;
         work[1] += nt;
+        // why a query is not certified (diagnostics): 1 stack overflow / budget, 2 NaN hit,
+        // 4 only overflowed hits, 8 tie, 16 minimum t not in (0, inf)
+        work[2] = (overflow ? 1u : 0u) | (nanhit ? 2u : 0u) | (h.k < 0 && infhit ? 4u : 0u) |
+                  (h.k >= 0 && ties && tie ? 8u : 0u) | (h.k >= 0 && !(h.t > 0.0f && h.t < INFINITY) ? 16u : 0u);
     }
     if (overflow || nanhit)
         return W_UNCERT;

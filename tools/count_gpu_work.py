@@ -12,10 +12,11 @@ from raytracercpp_amd import scenes
 from raytracercpp_amd.renderer import Renderer
 
 name = sys.argv[1] if len(sys.argv) > 1 else "sphere1m"
+modes = sys.argv[2:] or ["seg", "whole_line"]
 sc, st = scenes.CONFIGS[name]()
 r = Renderer(0)
 r.load_scene(sc, st)
-for mode in ("seg", "whole_line"):
+for mode in modes:
     if mode == "whole_line":
         os.environ["RT_SEG"] = "0"
         os.environ["RT_WBVH"] = "0"
@@ -29,5 +30,5 @@ for mode in ("seg", "whole_line"):
                       "vol_tests_abandoned": s["work_abandoned"][0], "tri_tests_abandoned": s["work_abandoned"][1],
                       "wide_node_visits": s["work_wide"][0], "wide_tri_tests": s["work_wide"][1],
                       "wide_uncertified": s["work_wide"][2], "wide_certificates": s["work_wide"][3],
-                      "exact_pixels": s["exact_pixels"],
+                      "exact_pixels": s["exact_pixels"], "uncertified_by_reason": s["uncertified"],
                       "deferred_pixels": s["deferred_pixels"], "kernel_ms": s["kernel_ms"]}), flush=True)
