@@ -1107,7 +1107,7 @@ __device__ __forceinline__ bool shapes_shadow(const KParams& P, v3 o, v3 d, floa
 // WIDE (the lean wide-BVH kernel; launched only with segment queries on, so the scene
 // has no analytic shapes): the decision comes from wide_shadow, or *defer is set and the
 // pixel goes to the exact pass -- no octree traversal is compiled in.
-template <bool GRP = false, bool WIDE = false>
+template <bool GRP = false, bool WIDE = false, bool PLAIN = false>
 __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv, bool* defer = nullptr)
 {
     if (!P.compute_shadows)
@@ -1162,6 +1162,8 @@ __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv, bool
             }
         }
     }
+    if (PLAIN)
+        return false;   // no analytic shapes
     return shapes_shadow(P, o, d, h.t, p, lp);
 }
 
@@ -1200,7 +1202,7 @@ __device__ __forceinline__ void shapes_closest(const KParams& P, v3 o, v3 d, Rec
 // With the wide BVH (P.wnodes), a certified query takes its answer; one it cannot certify
 // is deferred to the ray-group pass (budget > 0) or traced through the octree here.
 // WIDE: only the wide BVH is compiled in; an uncertified query sets *aborted (deferred).
-template <bool GRP = false, bool WIDE = false>
+template <bool GRP = false, bool WIDE = false, bool PLAIN = false>
 __device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv, uint32_t budget = 0,
                            bool* aborted = nullptr)
 {
@@ -1253,7 +1255,8 @@ __device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv, ui
         if (last.k >= 0)
             local = tri_record(P, last);
     }
-    shapes_closest(P, o, d, local, fin, src);
+    if (!PLAIN)
+        shapes_closest(P, o, d, local, fin, src);
     return src;
 }
 
@@ -1270,6 +1273,8 @@ struct Direct {
 };
 
 // RT_SHADING up to the shadow test: diffuse + specular at the hit (renderer.cpp:556-590).
+// PLAIN: the scene enables no texture map (the kernel's plain specialisation).
+template <bool PLAIN = false>
 __device__ c3 shade_lit(const KParams& P, v3 ro, v3 rd, Rec& h, v3& ip_out)
 {
     c3 fc = col(0.0f, 0.0f, 0.0f);
@@ -1278,20 +1283,20 @@ __device__ c3 shade_lit(const KParams& P, v3 ro, v3 rd, Rec& h, v3& ip_out)
     ip_out = ip;
     v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
     v3 light = mk(P.light[0], P.light[1], P.light[2]);
-    if (P.enable_displacement_mapping)
+    if (!PLAIN && P.enable_displacement_mapping)
         parallax_occlusion_mapping(P, h.tri, h.u, h.v, normalize(cam - ip), u, v);
     v3 dl = normalize(light - ip);
-    if (P.enable_normal_mapping)
+    if (!PLAIN && P.enable_normal_mapping)
         h.normal = normal_mapping(P, h, u, v);
     const float* m = mat_of(P, h.mat);
     float ao = 1.0f;
-    if (P.enable_ao_mapping) {
+    if (!PLAIN && P.enable_ao_mapping) {
         float tu, tv;
         get_tex_coords(P, h.tri, u, v, tu, tv);
         ao = tex_floor(P.tex[TEX_AO], tu, tv).r;
     }
     c3 dc;
-    if (P.enable_diffuse_mapping) {
+    if (!PLAIN && P.enable_diffuse_mapping) {
         float tu, tv;
         get_tex_coords(P, h.tri, u, v, tu, tv);
         dc = tex_floor(P.tex[TEX_DIFFUSE], tu, tv);
@@ -1348,19 +1353,19 @@ __device__ c3 shade_debug(const KParams& P, const Rec& h)
     return fc;
 }
 
-template <bool GRP = false, bool WIDE = false>
+template <bool GRP = false, bool WIDE = false, bool PLAIN = false>
 __device__ Direct shade_direct(const KParams& P, v3 ro, v3 rd, Rec& h, uint2* lv, unsigned& nshadow,
                                bool* defer = nullptr)
 {
     Direct out;
     out.shadowed = false;
     out.ip = mk(0, 0, 0);
-    if (P.shading_method == RT_SHADING) {
-        c3 fc = shade_lit(P, ro, rd, h, out.ip);
+    if (PLAIN || P.shading_method == RT_SHADING) {
+        c3 fc = shade_lit<PLAIN>(P, ro, rd, h, out.ip);
         if (P.compute_shadows)
             nshadow++;
         v3 light = mk(P.light[0], P.light[1], P.light[2]);
-        out.shadowed = is_shadowed<GRP, WIDE>(P, out.ip, h.normal, light, lv, defer);
+        out.shadowed = is_shadowed<GRP, WIDE, PLAIN>(P, out.ip, h.normal, light, lv, defer);
         out.fc = shade_shadow_emit(P, fc, mat_of(P, h.mat), out.shadowed);
     } else
         out.fc = shade_debug(P, h);
@@ -1380,9 +1385,12 @@ __device__ __forceinline__ c3 shade_finish(const KParams& P, c3 fc, const float*
 }
 
 // trace_ray miss colour (renderer.cpp:1052-1065); alpha of the returned Color
+template <bool PLAIN = false>
 __device__ c3 miss_color(const KParams& P, v3 d, float& alpha)
 {
     alpha = 1.0f;
+    if (PLAIN)
+        return background();
     if (P.enable_skysphere) {
         float u = (float)(0.5 + (double)atan2f(-d.z, -d.x) / (2 * M_PI));
         float v = (float)(0.5 + (double)asinf(-d.y) / M_PI);
@@ -1465,7 +1473,7 @@ struct PixelOut {
 // WIDE (REFL false): the lean wide-BVH kernel; any query the wide BVH cannot certify sets
 // po.deferred and the pixel is re-done from scratch by the exact pass (its shadow ray is
 // counted there, not here).
-template <bool REFL, bool GRP = false, bool WIDE = false>
+template <bool REFL, bool GRP = false, bool WIDE = false, bool PLAIN = false>
 __device__ PixelOut trace_pixel(const KParams& P, v3 cam, v3 rd0, uint2* lv, uint32_t pixel_key, unsigned& nshadow,
                                 unsigned& nrefl, uint32_t budget = 0)
 {
@@ -1473,22 +1481,24 @@ __device__ PixelOut trace_pixel(const KParams& P, v3 cam, v3 rd0, uint2* lv, uin
     po.fin = rec_fresh();
     po.found = po.shadowed = po.deferred = false;
     po.alpha = 1.0f;
-    po.src = closest_hit<GRP, WIDE && !REFL>(P, cam, rd0, po.fin, lv, REFL ? 0u : budget, &po.deferred);
+    po.src = closest_hit<GRP, WIDE && !REFL, PLAIN && !REFL>(P, cam, rd0, po.fin, lv, REFL ? 0u : budget,
+                                                             &po.deferred);
     if (!REFL) {
         if (po.deferred)
             return po;
         if (po.fin.t > 0.1f) {
             po.found = true;
             unsigned ns = 0;
-            Direct D = shade_direct<GRP, WIDE>(P, cam, rd0, po.fin, lv, ns, &po.deferred);
+            Direct D = shade_direct<GRP, WIDE, PLAIN>(P, cam, rd0, po.fin, lv, ns, &po.deferred);
             if (po.deferred)
                 return po;
             nshadow += ns;
             po.shadowed = D.shadowed;
-            po.color = P.shading_method == RT_SHADING ? shade_finish(P, D.fc, mat_of(P, po.fin.mat), col(0, 0, 0))
-                                                      : clamp3(D.fc);
+            po.color = PLAIN || P.shading_method == RT_SHADING
+                           ? shade_finish(P, D.fc, mat_of(P, po.fin.mat), col(0, 0, 0))
+                           : clamp3(D.fc);
         } else
-            po.color = miss_color(P, rd0, po.alpha);
+            po.color = miss_color<PLAIN>(P, rd0, po.alpha);
         return po;
     }
 
@@ -1735,7 +1745,9 @@ __global__ __launch_bounds__(BLOCK) void tile_key_kernel(KParams P, const uint32
 // still trace; dynamic pulling keeps every CU busy until the queue drains.
 // WIDE: the lean kernel (wide BVH only) -- pixels it cannot certify go to
 // the deferred list and the exact pass (ray_trace_defer_kernel).
-template <bool REFL, bool WIDE = false>
+// PLAIN: no texture map, sky, analytic shape, debug shading or SSAO buffer (host-checked,
+// KParams::plain): those code paths are compiled out.
+template <bool REFL, bool WIDE = false, bool PLAIN = false>
 __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
 {
     extern __shared__ uint2 lds_levels[];
@@ -1779,7 +1791,8 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
 #if RT_COUNT == 2
         g_pixel_work[pixel_work_slot()] = make_uint2(0u, 0u);
 #endif
-        PixelOut po = trace_pixel<REFL, false, WIDE>(P, cam, rd, lv, rng, nshadow, nrefl, REFL ? 0u : P.trav_budget);
+        PixelOut po = trace_pixel<REFL, false, WIDE, PLAIN>(P, cam, rd, lv, rng, nshadow, nrefl,
+                                                            REFL ? 0u : P.trav_budget);
         size_t o = (size_t)lr * P.rw + px;
         if (!REFL && po.deferred) {
             // the deferred pass (ray_trace_defer_kernel) traces it with a ray group; the
@@ -1804,7 +1817,7 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
         if (P.hit_t) P.hit_t[o] = po.fin.t;
 #endif
         if (P.shadow) P.shadow[o] = (uint8_t)(po.found && po.shadowed);
-        if (P.zbuf) write_ssao_buffers(P, o, po.found, cam, rd, po.fin);
+        if (!PLAIN && P.zbuf) write_ssao_buffers(P, o, po.found, cam, rd, po.fin);
 #if RT_WAVE_STATS
         w_busy += wall_clock64() - w_t0;
 #endif
@@ -3328,7 +3341,10 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(
             C.defer_in_head = 13;
             hipLaunchKernelGGL(rt::ray_trace_defer_kernel, dim3(db), dim3(rt::BLOCK), lds, stream, C);
         } else {
-            hipLaunchKernelGGL((rt::ray_trace_kernel<false, false>), dim3(blocks), dim3(rt::BLOCK), lds, stream, A);
+            if (P->plain && !P->zbuf && !P->nbuf)
+                hipLaunchKernelGGL((rt::ray_trace_kernel<false, false, true>), dim3(blocks), dim3(rt::BLOCK), lds, stream, A);
+            else
+                hipLaunchKernelGGL((rt::ray_trace_kernel<false, false>), dim3(blocks), dim3(rt::BLOCK), lds, stream, A);
             if (P->defer && P->defer_cap) {
                 // deferred pixels: a persistent grid of ray groups over the list ray_trace_kernel left
                 rt::KParams C = *P;

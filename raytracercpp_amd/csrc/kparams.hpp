@@ -112,6 +112,8 @@ struct KParams {
     uint32_t trav_budget;
     int32_t grp_shift;
     int32_t wide_lean;        // 1: the lean wide-BVH kernel, everything it cannot certify deferred (needs defer[])
+    int32_t plain;            // 1: no texture map, sky, analytic shape, debug shading or SSAO buffers
+                              // (ray_trace_kernel's plain specialisation)
     uint32_t* defer;          // output list of deferred pixels, head counters[defer_head]
     uint32_t defer_cap;
     int32_t defer_head;

@@ -734,6 +734,11 @@ void Renderer::fill_params(KParams& P) const
     }
     P.max_blocks = num_cus_ * 8;
     P.tq_base = NCOUNTERS;
+    // the plain specialisation (RT_PLAIN=0 turns it off); SSAO (zbuf) is checked at launch
+    const char* plain_env = getenv("RT_PLAIN");
+    P.plain = !(plain_env && plain_env[0] == '0') && P.shading_method == RT_SHADING && P.nshape == 0 &&
+              !P.enable_ao_mapping && !P.enable_diffuse_mapping && !P.enable_normal_mapping &&
+              !P.enable_displacement_mapping && !P.enable_skysphere && !P.enable_skybox && !P.has_reflection;
     render_size(P.rw, P.rh);
 }
 

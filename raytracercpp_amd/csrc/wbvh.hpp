@@ -239,11 +239,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
     const float ix = 1.0f / (fabsf(d.x) < DMIN ? copysignf(DMIN, d.x) : d.x);
     const float iy = 1.0f / (fabsf(d.y) < DMIN ? copysignf(DMIN, d.y) : d.y);
     const float iz = 1.0f / (fabsf(d.z) < DMIN ? copysignf(DMIN, d.z) : d.z);
-    const float olx = o.x + m, oly = o.y + m, olz = o.z + m;
-    const float ohx = o.x - m, ohy = o.y - m, ohz = o.z - m;
-#if RT_W_SLAB
-    const float m3 = 384.0f * m;   // |N|_1 <= 3 * 128: the spatial margin in slab units
-#endif
+
     constexpr float SL = 0x1p-20f;   // relative slack over the rounding of a slab parameter (<= 3 ulp)
     float best_s = hi + fabsf(hi) * SL;   // h.t (or hi) plus slack: a child entered at or below it may hold a hit
     bool tie = false, nanhit = false, infhit = false, overflow = false;
@@ -271,8 +267,8 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
 #if RT_W_SLAB
             const uint4 NR = ldg(reinterpret_cast<const uint4*>(p) + 3), SB = ldg(reinterpret_cast<const uint4*>(p) + 4);
             const uint4 CH = ldg(reinterpret_cast<const uint4*>(p) + 5);
+            const float m3 = 384.0f * m;   // |N|_1 <= 3 * 128: the spatial margin in slab units
             const float ss = bitsf(Q2.z), slo_lo = bitsf(Q2.w) - m3, slo_hi = bitsf(Q2.w) + m3;
-            const float Dx = Q0.x - o.x, Dy = Q0.y - o.y, Dz = Q0.z - o.z;   // origin - o
             const uint32_t nr[4] = {NR.x, NR.y, NR.z, NR.w}, sb[4] = {SB.x, SB.y, SB.z, SB.w};
 #else
             const uint4 CH = ldg(reinterpret_cast<const uint4*>(p) + 3);
@@ -281,8 +277,11 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
             // t of a plane origin + q s (widened by m) = q (s / d) + (origin -+ m - o) / d
             const float sx = bitsf((ex & 0xffu) << 23) * ix, sy = bitsf(((ex >> 8) & 0xffu) << 23) * iy,
                         sz = bitsf(((ex >> 16) & 0xffu) << 23) * iz;
-            const float ax = (Q0.x - olx) * ix, ay = (Q0.y - oly) * iy, az = (Q0.z - olz) * iz;
-            const float bx = (Q0.x - ohx) * ix, by = (Q0.y - ohy) * iy, bz = (Q0.z - ohz) * iz;
+            // origin - o per axis, then the planes widened by m on either side (no per-ray
+            // widened origins kept live: they would hold six registers through the loop)
+            const float Dx = Q0.x - o.x, Dy = Q0.y - o.y, Dz = Q0.z - o.z;
+            const float ax = (Dx - m) * ix, ay = (Dy - m) * iy, az = (Dz - m) * iz;
+            const float bx = (Dx + m) * ix, by = (Dy + m) * iy, bz = (Dz + m) * iz;
             const uint32_t ch[4] = {CH.x, CH.y, CH.z, CH.w};
             float key[4];
             uint32_t ref[4];
