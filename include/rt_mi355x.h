@@ -105,6 +105,9 @@ typedef struct rt_stats {
                                   certificate */
     int64_t exact_pixels;      /* pixels of the last frame whose queries the wide BVH could not certify, traced
                                   through the octree by the exact pass */
+    int64_t wave_steps[6];     /* diagnostic builds only: wide-BVH traversal loop iterations of primary queries --
+                                  summed over waves (each wave's longest lane), summed over lanes, wave calls --
+                                  then the same for shadow queries (SIMD efficiency = lanes / (64 waves)) */
 } rt_stats;
 
 typedef struct rt_renderer rt_renderer;

@@ -56,11 +56,12 @@ class RtStats(C.Structure):
         ("render_width", C.c_int32), ("render_height", C.c_int32), ("seg_scale", C.c_float),
         ("work", C.c_int64 * 4), ("deferred_pixels", C.c_int64), ("work_abandoned", C.c_int64 * 2),
         ("work_wide", C.c_int64 * 4), ("uncertified", C.c_int64 * 6), ("exact_pixels", C.c_int64),
+        ("wave_steps", C.c_int64 * 6),
     ]
 
     def as_dict(self):
         return {n: (float(getattr(self, n)) if t is C.c_float else
-                    [int(x) for x in getattr(self, n)] if n.startswith("work") or n == "uncertified" else int(getattr(self, n))) for n, t in self._fields_}
+                    [int(x) for x in getattr(self, n)] if n.startswith(("work", "wave")) or n == "uncertified" else int(getattr(self, n))) for n, t in self._fields_}
 
 
 # every exported symbol and its ctypes signature (restype, argtypes); tests check

@@ -441,7 +441,7 @@ int rt_wbvh_query(const float* tri9, int64_t n, int32_t max_depth, int32_t leaf_
         std::atomic<int64_t> work_n{0}, work_t{0};
         auto body = [&](int64_t b, int64_t e) {
             rt::WStackLocal stk;
-            uint32_t wk[3] = {0, 0, 0};
+            uint32_t wk[4] = {0, 0, 0, 0};
             for (int64_t i = b; i < e; i++) {
                 rt::v3 o = rt::mk(orig[3 * i], orig[3 * i + 1], orig[3 * i + 2]);
                 rt::v3 d = rt::mk(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]);

@@ -970,6 +970,28 @@ struct WStackLds {
     __device__ __forceinline__ uint2 get(int i) const { return base[i * BLOCK]; }
 };
 
+#if RT_COUNT
+// counters[base]: the wave's longest lane's loop iterations, [base + 1]: every lane's, [base + 2]:
+// wave calls (SIMD efficiency of the if-if loop; diagnostic builds only)
+__device__ void count_wave_steps(const KParams& P, int base, uint32_t steps)
+{
+    if (!P.counters)
+        return;
+    uint64_t act = __ballot(1), a = act;
+    uint32_t mx = 0;
+    while (a) {
+        const int l = __ffsll((unsigned long long)a) - 1;
+        a &= a - 1;
+        mx = max(mx, (uint32_t)__builtin_amdgcn_readlane((int)steps, l));
+    }
+    if ((int)__lane_id() == __ffsll((unsigned long long)act) - 1) {
+        atomicAdd(&P.counters[base], (unsigned long long)mx);
+        atomicAdd(&P.counters[base + 2], 1ull);
+    }
+    atomicAdd(&P.counters[base + 1], (unsigned long long)steps);
+}
+#endif
+
 // BVH::intersect through the wide BVH and its certificate (wbvh.hpp).
 // Returns true with (h, r) = the reference's record and boolean when the query is
 // certified; false when it must be traced through the octree.
@@ -979,9 +1001,10 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
     WStackLds stk{lv};
     WHit w;
 #if RT_COUNT
-    uint32_t wk[3] = {0, 0, 0};
+    uint32_t wk[4] = {0, 0, 0, 0};
     const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, INFINITY, true,
                                 P.wide_budget);
+    count_wave_steps(P, 22, wk[3]);
     if (P.counters) {
         atomicAdd(&P.counters[10], (unsigned long long)wk[0]);
         atomicAdd(&P.counters[11], (unsigned long long)wk[1]);
@@ -1042,9 +1065,10 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
     WStackLds stk{lv};
     WHit w;
 #if RT_COUNT
-    uint32_t wk[3] = {0, 0, 0};
+    uint32_t wk[4] = {0, 0, 0, 0};
     const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, hi, false,
                                 P.wide_budget);
+    count_wave_steps(P, 25, wk[3]);
     if (P.counters) {
         atomicAdd(&P.counters[10], (unsigned long long)wk[0]);
         atomicAdd(&P.counters[11], (unsigned long long)wk[1]);
@@ -1712,7 +1736,7 @@ __global__ __launch_bounds__(BLOCK) void tile_probe_kernel(KParams P, uint32_t* 
     const float om = fmaxf(fabsf(cam.x), fmaxf(fabsf(cam.y), fabsf(cam.z)));
     WStackLds stk{lv};
     WHit w;
-    uint32_t wk[3] = {0, 0, 0};
+    uint32_t wk[4] = {0, 0, 0, 0};
     wbvh_closest(P.wnodes, P.wtris, cam, rd, 0x1p-16f * (om + P.scene_scale), stk, w, wk, INFINITY, true,
                  TILE_PROBE_BUDGET);
     cost[tile] = wk[0] + wk[1];

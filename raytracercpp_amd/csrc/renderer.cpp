@@ -1338,6 +1338,7 @@ int Renderer::get_stats(rt_stats* out) const
     for (int i = 0; i < 6; i++) out->uncertified[i] = last_uncert_[i];
     out->deferred_pixels = last_deferred_;
     out->exact_pixels = last_exact_;
+    for (int i = 0; i < 6; i++) out->wave_steps[i] = last_wave_[i];
     return RT_OK;
 }
 
@@ -1480,6 +1481,7 @@ void Renderer::take_counters(const unsigned long long* cnt)
     for (int i = 0; i < 9; i++) last_work_[i] = (int64_t)cnt[4 + i];
     last_work_[9] = (int64_t)cnt[14];
     for (int i = 0; i < 6; i++) last_uncert_[i] = (int64_t)cnt[16 + i];
+    for (int i = 0; i < 6; i++) last_wave_[i] = (int64_t)cnt[22 + i];
     last_deferred_ = (int64_t)(cnt[3] & 0xffffffffull);
     last_exact_ = (int64_t)(cnt[13] & 0xffffffffull) + (split_last_ ? (int64_t)(cnt[3] & 0xffffffffull) : 0);
     if (split_last_)

@@ -194,6 +194,7 @@ private:
     int64_t last_work_[10] = {};  // RT_COUNT builds: counters[4..12], [14] of the last frame (executed k-DOP / MT
                                   // tests: whole-line, segment, abandoned; wide-BVH nodes, triangles, uncertified,
                                   // certificates)
+    int64_t last_wave_[6] = {};     // RT_COUNT builds: counters[22..27], wide-BVH loop iterations (rt_stats)
     int64_t last_uncert_[6] = {};   // RT_COUNT builds: uncertified wide-BVH queries by reason
     void take_counters(const unsigned long long* cnt);
     float kernel_ms_ = 0, post_ms_ = 0, build_ms_ = 0;

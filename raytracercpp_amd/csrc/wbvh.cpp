@@ -346,11 +346,13 @@ WNode quantise(const Box* cb, const uint32_t* link, int nc, const ChildGeom* cg,
     w.slo = slo;
     for (int j = 0; j < 4; j++) {
         if (j >= nc) {
-            w.nrm[j] = 128u | (128u << 8) | (128u << 16);
+            w.nrm[j] = 0;
             w.slab[j] = 0;
             continue;
         }
-        w.nrm[j] = (uint32_t)(nq[j][0] + 128) | ((uint32_t)(nq[j][1] + 128) << 8) | ((uint32_t)(nq[j][2] + 128) << 16);
+        // signed bytes (two's complement)
+        w.nrm[j] = (uint32_t)(uint8_t)(int8_t)nq[j][0] | ((uint32_t)(uint8_t)(int8_t)nq[j][1] << 8) |
+                   ((uint32_t)(uint8_t)(int8_t)nq[j][2] << 16);
         double q0 = std::floor((smin[j] - (double)slo) / st), q1 = std::ceil((smax[j] - (double)slo) / st);
         q0 = std::max(0.0, std::min(65535.0, q0));
         q1 = std::max(0.0, std::min(65535.0, q1));

@@ -71,8 +71,8 @@ struct alignas(16) WNode {
 #if RT_W_SLAB
     // Orientation slab of child j: every vertex v below it has
     //   slo + q0 s  <=  N_j . (v - origin)  <=  slo + q1 s,
-    // N_j = (nrm bytes 0..2) - 128 (the subtree's area-weighted normal, quantised; an
-    // integer vector), q0 / q1 the low / high 16 bits of slab[j].  A curved patch is thin
+    // N_j = nrm bytes 0..2 as signed 8-bit integers (the subtree's area-weighted normal,
+    // quantised to [-127, 127]), q0 / q1 the low / high 16 bits of slab[j].  A curved patch is thin
     // along its mean normal, so a ray that grazes the surface misses most patches' slabs
     // although it crosses their boxes (silhouette rays).
     float s, slo;
@@ -220,8 +220,8 @@ struct WStackLocal {   // host
 // Returns W_MISS (no triangle hits at t <= hi), W_HIT (h = the minimum-t hit, finite and
 // > 0, unique when ties: still to be certified by kdop_certifies on its octree leaf) or
 // W_UNCERT.  Shadow queries (hi = the segment end of kernels.hip is_shadowed, ties false)
-// read only the record's t.  work (optional, 3 entries): {nodes, triangles} added, [2] = the
-// reasons a query is not certified.  budget > 0: a query that
+// read only the record's t.  work (optional, 4 entries): {nodes, triangles} added, [2] = the
+// reasons a query is not certified, [3] = loop iterations added.  budget > 0: a query that
 // needs more loop iterations is abandoned (W_UNCERT).
 template <class Stack>
 RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m, Stack& stk, WHit& h,
@@ -239,6 +239,9 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
     const float ix = 1.0f / (fabsf(d.x) < DMIN ? copysignf(DMIN, d.x) : d.x);
     const float iy = 1.0f / (fabsf(d.y) < DMIN ? copysignf(DMIN, d.y) : d.y);
     const float iz = 1.0f / (fabsf(d.z) < DMIN ? copysignf(DMIN, d.z) : d.z);
+    // per axis, the byte row of the entry (near) planes: q_lo where the direction is positive,
+    // q_hi where it is negative; the near plane is widened by -m sign(d), the far one by +m sign(d)
+    const bool nx_lo = !(ix < 0.0f), ny_lo = !(iy < 0.0f), nz_lo = !(iz < 0.0f);
 
     constexpr float SL = 0x1p-20f;   // relative slack over the rounding of a slab parameter (<= 3 ulp)
     float best_s = hi + fabsf(hi) * SL;   // h.t (or hi) plus slack: a child entered at or below it may hold a hit
@@ -248,7 +251,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
     uint32_t nn = 0, nt = 0;
     uint32_t steps = 0;   // loop iterations (node or leaf visits): budget > 0 caps them
     while (cur != W_EMPTY) {
-        if (budget && ++steps > budget) {
+        if (++steps > budget && budget) {
             overflow = true;   // over budget: not certified here (the caller re-traces it)
             break;
         }
@@ -278,30 +281,37 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
             const float sx = bitsf((ex & 0xffu) << 23) * ix, sy = bitsf(((ex >> 8) & 0xffu) << 23) * iy,
                         sz = bitsf(((ex >> 16) & 0xffu) << 23) * iz;
             // origin - o per axis, then the planes widened by m on either side (no per-ray
-            // widened origins kept live: they would hold six registers through the loop)
+            // widened origins kept live: they would hold six registers through the loop).
+            // Near plane of axis a: t = q_near s_a / d_a + (origin_a - o_a -+ m) / d_a, with the
+            // byte row and the sign of m chosen by the direction's sign (the same products as
+            // testing both planes and ordering them by min / max)
             const float Dx = Q0.x - o.x, Dy = Q0.y - o.y, Dz = Q0.z - o.z;
-            const float ax = (Dx - m) * ix, ay = (Dy - m) * iy, az = (Dz - m) * iz;
-            const float bx = (Dx + m) * ix, by = (Dy + m) * iy, bz = (Dz + m) * iz;
+            const float mx = nx_lo ? m : -m, my = ny_lo ? m : -m, mz = nz_lo ? m : -m;
+            const float ax = (Dx - mx) * ix, ay = (Dy - my) * iy, az = (Dz - mz) * iz;
+            const float bx = (Dx + mx) * ix, by = (Dy + my) * iy, bz = (Dz + mz) * iz;
+            const uint32_t nqx = nx_lo ? Q1.x : Q1.w, fqx = nx_lo ? Q1.w : Q1.x;
+            const uint32_t nqy = ny_lo ? Q1.y : Q2.x, fqy = ny_lo ? Q2.x : Q1.y;
+            const uint32_t nqz = nz_lo ? Q1.z : Q2.y, fqz = nz_lo ? Q2.y : Q1.z;
             const uint32_t ch[4] = {CH.x, CH.y, CH.z, CH.w};
             float key[4];
             uint32_t ref[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const int sh = 8 * j;
-                float tlx = __builtin_fmaf((float)((Q1.x >> sh) & 0xffu), sx, ax);
-                float tly = __builtin_fmaf((float)((Q1.y >> sh) & 0xffu), sy, ay);
-                float tlz = __builtin_fmaf((float)((Q1.z >> sh) & 0xffu), sz, az);
-                float thx = __builtin_fmaf((float)((Q1.w >> sh) & 0xffu), sx, bx);
-                float thy = __builtin_fmaf((float)((Q2.x >> sh) & 0xffu), sy, by);
-                float thz = __builtin_fmaf((float)((Q2.y >> sh) & 0xffu), sz, bz);
-                float tmin = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fminf(tlz, thz));
-                float tmax = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fmaxf(tlz, thz));
+                const float tnx = __builtin_fmaf((float)((nqx >> sh) & 0xffu), sx, ax);
+                const float tny = __builtin_fmaf((float)((nqy >> sh) & 0xffu), sy, ay);
+                const float tnz = __builtin_fmaf((float)((nqz >> sh) & 0xffu), sz, az);
+                const float tfx = __builtin_fmaf((float)((fqx >> sh) & 0xffu), sx, bx);
+                const float tfy = __builtin_fmaf((float)((fqy >> sh) & 0xffu), sy, by);
+                const float tfz = __builtin_fmaf((float)((fqz >> sh) & 0xffu), sz, bz);
+                float tmin = fmaxf(fmaxf(tnx, tny), tnz);
+                float tmax = fminf(fminf(tfx, tfy), tfz);
 #if RT_W_SLAB
                 {
                     // N . (o + t d - origin) in [c0, c1] widened by m3 >= |N|_1 m: t between
                     // (c0 - m3 + b) / a and (c1 + m3 + b) / a, b = N . (origin - o), a = N . d
-                    const float nx = (float)(nr[j] & 0xffu) - 128.0f, ny = (float)((nr[j] >> 8) & 0xffu) - 128.0f,
-                                nz = (float)((nr[j] >> 16) & 0xffu) - 128.0f;
+                    const float nx = (float)(int8_t)(nr[j] & 0xffu), ny = (float)(int8_t)((nr[j] >> 8) & 0xffu),
+                                nz = (float)(int8_t)((nr[j] >> 16) & 0xffu);
                     const float a = nx * d.x + ny * d.y + nz * d.z;
                     const float b = nx * Dx + ny * Dy + nz * Dz;
                     // the hardware reciprocal (1 ulp): its error moves the slab's t by a relative
@@ -314,9 +324,12 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                     tmax = fminf(tmax, fmaxf(s0, s1));
                 }
 #endif
-                float tmax_s = tmax + fabsf(tmax) * SL;
-                bool ok = ch[j] != W_EMPTY && tmin <= tmax_s && tmin <= best_s && tmax_s >= 0.0f;
-                key[j] = ok ? fminf(tmin, 3.0e38f) : INFINITY;
+                // enter when max(tmin, 0) <= min(tmax (1 + SL), best_s); a NaN tmin (every
+                // slab NaN) enters too.  The key orders the children; misses get INFINITY.
+                const float lim = fminf(__builtin_fmaf(fabsf(tmax), SL, tmax), best_s);
+                const float k0 = fmaxf(tmin, 0.0f);
+                const bool ok = ch[j] != W_EMPTY && k0 <= lim;
+                key[j] = ok ? fminf(k0, 3.0e38f) : INFINITY;
                 ref[j] = ch[j];
 #if defined(__HIP_DEVICE_COMPILE__) && RT_W_SCHED_BARRIER
                 // one child at a time: the scheduler would interleave the four children's
@@ -408,6 +421,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
     if (work) {
         work[0] += nn;
         work[1] += nt;
+        work[3] += steps;
         // why a query is not certified (diagnostics): 1 stack overflow / budget, 2 NaN hit,
         // 4 only overflowed hits, 8 tie, 16 minimum t not in (0, inf)
         work[2] = (overflow ? 1u : 0u) | (nanhit ? 2u : 0u) | (h.k < 0 && infhit ? 4u : 0u) |

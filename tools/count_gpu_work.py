@@ -31,4 +31,7 @@ for mode in modes:
                       "wide_node_visits": s["work_wide"][0], "wide_tri_tests": s["work_wide"][1],
                       "wide_uncertified": s["work_wide"][2], "wide_certificates": s["work_wide"][3],
                       "exact_pixels": s["exact_pixels"], "uncertified_by_reason": s["uncertified"],
-                      "deferred_pixels": s["deferred_pixels"], "kernel_ms": s["kernel_ms"]}), flush=True)
+                      "deferred_pixels": s["deferred_pixels"], "kernel_ms": s["kernel_ms"],
+                      "wave_steps_primary": s["wave_steps"][:3], "wave_steps_shadow": s["wave_steps"][3:],
+                      "simd_efficiency": [round(s["wave_steps"][i + 1] / max(1, 64 * s["wave_steps"][i]), 4)
+                                          for i in (0, 3)]}), flush=True)
