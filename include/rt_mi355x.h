@@ -227,9 +227,11 @@ int rt_get_internal(rt_renderer *r, uint32_t *argb, float *rgba, int32_t *hit_id
 
 int rt_get_stats(rt_renderer *r, rt_stats *out);
 
-/* Diagnostic builds (-DRT_WAVE_STATS=1, with RT_DEBUG_WAVES set in the environment): the last
- * ray_trace's per-wave records {first dequeue tick, exit tick, tiles, busy ticks} (100 MHz
- * wall clock), n = 4 x waves values.  RT_EINVAL when no record buffer exists. */
+/* Diagnostic builds (with RT_DEBUG_WAVES set in the environment): the last ray_trace's
+ * per-wave records of 8 words, n = 8 x waves values -- -DRT_WAVE_STATS=1: {first dequeue tick,
+ * exit tick, tiles, busy ticks} (100 MHz wall clock); -DRT_PHASE_TIME=1: shader cycles per
+ * phase {dequeue, ray generation, primary query, shading, shadow query, framebuffer} (plain
+ * kernel).  RT_EINVAL when no record buffer exists. */
 int rt_debug_read(rt_renderer *r, uint64_t *out, int64_t n);
 
 /* Image-strip rendering for multi-GPU (one process per GPU): renders the bands of

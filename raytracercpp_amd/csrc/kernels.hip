@@ -18,6 +18,34 @@
 // 16-byte loads.  All arithmetic follows the reference expression trees with
 // no contraction (-ffp-contract=off) and IEEE division / sqrt, so results are
 // bit-identical to the reference compiled with -ffp-contract=off.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#if defined(RT_COUNT) && RT_COUNT
+// diagnostic builds: per wave iteration of the wide-BVH loop, the lanes in its node (leaf)
+// branch and whether they share one node (leaf) -- how often a scalar-cache path could
+// serve the step.  g_wsteps: [0] node steps, [1] of them uniform, [2] leaf steps, [3]
+// uniform, [4] / [5] lanes, [6] / [7] distinct nodes / leaves (tools/count_gpu_work.py)
+__device__ unsigned long long g_wsteps[8];
+__device__ __forceinline__ void w_step_hook(uint32_t cur, int leaf)
+{
+    const uint64_t act = __ballot(1);
+    uint64_t left = act;
+    unsigned distinct = 0;
+    while (left) {
+        const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)cur, __ffsll((unsigned long long)left) - 1);
+        left &= ~__ballot(cur == f);
+        distinct++;
+    }
+    if ((int)__lane_id() == __ffsll((unsigned long long)act) - 1) {
+        atomicAdd(&g_wsteps[2 * leaf], 1ull);
+        if (distinct == 1)
+            atomicAdd(&g_wsteps[2 * leaf + 1], 1ull);
+        atomicAdd(&g_wsteps[4 + leaf], (unsigned long long)__popcll(act));
+        atomicAdd(&g_wsteps[6 + leaf], (unsigned long long)distinct);
+    }
+}
+#define W_STEP_HOOK(cur, leaf) w_step_hook(cur, leaf)
+#endif
 #include "kparams.hpp"
 #include "rt_math.hpp"
 #include "wbvh.hpp"
@@ -44,6 +72,11 @@ constexpr int BLOCK = 64 * WAVES_PER_BLOCK;
 #endif
 #ifndef RT_WAVE_STATS
 #define RT_WAVE_STATS 0
+#endif
+// RT_PHASE_TIME=1 (diagnostic builds, tools/phase_time.py): shader cycles per wave spent in
+// each phase of the plain kernel's pixel loop (ph_mark), written to P.dbg
+#ifndef RT_PHASE_TIME
+#define RT_PHASE_TIME 0
 #endif
 #ifndef RT_OCC_PRIM
 #define RT_OCC_PRIM 5
@@ -962,6 +995,24 @@ __device__ void parallax_occlusion_mapping(const KParams& P, int tri, float u, f
     nv = (1 - w) * v2 + w * pv;
 }
 
+#if RT_PHASE_TIME
+// per wave: [0..5] cycles per phase, [7] the last mark (LDS; the wave's first active lane updates)
+__shared__ unsigned long long g_phase[WAVES_PER_BLOCK][8];
+__device__ __forceinline__ void ph_mark(int k)
+{
+    const unsigned long long now = __builtin_amdgcn_s_memtime();
+    const uint64_t act = __ballot(1);
+    if ((int)__lane_id() == __ffsll((unsigned long long)act) - 1) {
+        const int w = threadIdx.x >> 6;
+        g_phase[w][k] += now - g_phase[w][7];
+        g_phase[w][7] = now;
+    }
+}
+#define PH_MARK(k) ph_mark(k)
+#else
+#define PH_MARK(k)
+#endif
+
 // The lane's wide-BVH traversal stack: entry i at lv[i * BLOCK] (the LDS of the octree
 // level stack, which is not live during the wide-BVH query).
 struct WStackLds {
@@ -1389,7 +1440,9 @@ __device__ Direct shade_direct(const KParams& P, v3 ro, v3 rd, Rec& h, uint2* lv
         if (P.compute_shadows)
             nshadow++;
         v3 light = mk(P.light[0], P.light[1], P.light[2]);
+        if (PLAIN) PH_MARK(3);
         out.shadowed = is_shadowed<GRP, WIDE, PLAIN>(P, out.ip, h.normal, light, lv, defer);
+        if (PLAIN) PH_MARK(4);
         out.fc = shade_shadow_emit(P, fc, mat_of(P, h.mat), out.shadowed);
     } else
         out.fc = shade_debug(P, h);
@@ -1507,6 +1560,7 @@ __device__ PixelOut trace_pixel(const KParams& P, v3 cam, v3 rd0, uint2* lv, uin
     po.alpha = 1.0f;
     po.src = closest_hit<GRP, WIDE && !REFL, PLAIN && !REFL>(P, cam, rd0, po.fin, lv, REFL ? 0u : budget,
                                                              &po.deferred);
+    if (PLAIN) PH_MARK(2);
     if (!REFL) {
         if (po.deferred)
             return po;
@@ -1659,21 +1713,26 @@ __device__ __forceinline__ int global_row(const KParams& P, int lr)
     return (band * P.nranks + P.rank) * P.band_rows + (lr - band * P.band_rows);
 }
 
-// The persistent tile queue, sharded: shard s owns tiles [s T / 8, (s + 1) T / 8) (bands
-// of image rows) and its head counter sits on its own 128-B line.  A wave starts on the
+// The persistent tile queue, sharded: shard s owns the tile rows [s Y / 8, (s + 1) Y / 8)
+// (a band of the image) and its head counter sits on its own 128-B line.  A wave starts on the
 // shard of its block's XCD group (blockIdx % 8: blocks b and b + 8 share an XCD, so a
 // band's rays share that XCD's L2) and moves to the next shard when its own is empty;
 // it is done once it has found all eight empty.  One head word serves ~88 dequeues per
 // microsecond (MI355X_MICROARCH.md, dequeue row), under the frame's 130K tiles at ~2 ms.
-#ifndef RT_TILE_BATCH
-#define RT_TILE_BATCH 1   // tiles per dequeue (natural order)
-#endif
 struct TileQueue {
     int shard, empty;
-    int next, left;   // tiles of the last dequeue not yet handed out
 };
 
-__device__ __forceinline__ TileQueue tile_queue_begin() { return TileQueue{(int)(blockIdx.x & (TILE_SHARDS - 1)), 0, 0, 0}; }
+__device__ __forceinline__ TileQueue tile_queue_begin() { return TileQueue{(int)(blockIdx.x & (TILE_SHARDS - 1)), 0}; }
+
+// Ticket t of shard s -> tile index (row-major), or -1 past the shard's end.  Measured
+// against alternatives (r02): guided chunks of 2-4 adjacent tiles per dequeue, tickets taken
+// one tile ahead, and blocked orders (patches of 8x8 .. 32x16 tiles) were all slower.
+__device__ __forceinline__ int shard_tile(const KParams& P, int s, int t)
+{
+    const int r0 = (int)((long long)P.tiles_y * s / TILE_SHARDS), r1 = (int)((long long)P.tiles_y * (s + 1) / TILE_SHARDS);
+    return t < (r1 - r0) * P.tiles_x ? r0 * P.tiles_x + t : -1;
+}
 
 // next tile for the calling wave (wave-uniform), or -1 when every shard is empty.  With
 // P.tile_order (tiles sorted by estimated cost, heaviest first: tile_probe_kernel) shard s
@@ -1681,28 +1740,19 @@ __device__ __forceinline__ TileQueue tile_queue_begin() { return TileQueue{(int)
 __device__ __forceinline__ int tile_queue_next(const KParams& P, TileQueue& q, int ntiles)
 {
     const int lane = threadIdx.x & 63;
-    if (q.left > 0) {
-        q.left--;
-        return q.next++;
-    }
     while (q.empty < TILE_SHARDS) {
         int t = 0;
         if (lane == 0)
-            t = (int)atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[P.tq_base + 16 * q.shard]),
-                               P.tile_order ? 1u : (unsigned)RT_TILE_BATCH);
+            t = (int)atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[P.tq_base + 16 * q.shard]), 1u);
         t = __builtin_amdgcn_readfirstlane(t);
         if (P.tile_order) {
             const int pos = q.shard + TILE_SHARDS * t;
             if (pos < ntiles)
                 return (int)(ldg(P.tile_order + pos) & TILE_ID_MASK);
         } else {
-            const int b0 = (int)((long long)ntiles * q.shard / TILE_SHARDS);
-            const int b1 = (int)((long long)ntiles * (q.shard + 1) / TILE_SHARDS);
-            if (b0 + t < b1) {
-                q.next = b0 + t + 1;
-                q.left = min(RT_TILE_BATCH, b1 - (b0 + t)) - 1;
-                return b0 + t;
-            }
+            const int tile = shard_tile(P, q.shard, t);
+            if (tile >= 0)
+                return tile;
         }
         q.empty++;
         q.shard = (q.shard + 1) & (TILE_SHARDS - 1);
@@ -1781,6 +1831,13 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
     v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
     unsigned nshadow = 0, nrefl = 0;
     TileQueue q = tile_queue_begin();
+#if RT_PHASE_TIME
+    if (PLAIN && lane == 0) {
+        for (int k = 0; k < 7; k++)
+            g_phase[threadIdx.x >> 6][k] = 0;
+        g_phase[threadIdx.x >> 6][7] = __builtin_amdgcn_s_memtime();
+    }
+#endif
 #if RT_WAVE_STATS
     // diagnostic: per wave {first dequeue tick, exit tick, tiles, sum of tile ticks}
     const uint64_t w_begin = wall_clock64();
@@ -1798,6 +1855,7 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
         int px = tx * 8 + (lane & 7);
         int lr = ty * 8 + (lane >> 3);
         int py = lr < P.local_rows ? global_row(P, lr) : P.rh;
+        if (PLAIN) PH_MARK(0);
         if (px >= P.rw || py >= P.rh)
             continue;
 
@@ -1807,6 +1865,7 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
         v3 vs = xform_point(P.proj_inv, mk(x_world, y_world, -1));
         v3 ws = xform_point(P.cam_to_world, vs);
         v3 rd = normalize(ws - cam);
+        if (PLAIN) PH_MARK(1);
 
         uint32_t rng = REFL ? pixel_seed((uint32_t)(py * P.rw + px), P.rng_seed) : 0u;
 #if RT_TILE_TIME
@@ -1845,15 +1904,25 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
 #if RT_WAVE_STATS
         w_busy += wall_clock64() - w_t0;
 #endif
+        if (PLAIN) PH_MARK(5);
     }
+#if RT_PHASE_TIME
+    if (PLAIN) {
+        PH_MARK(0);   // the final (empty) dequeues
+        const int wid = (int)(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
+        if (P.dbg && lane == 0 && wid < DBG_WAVES)
+            for (int k = 0; k < 6; k++)
+                P.dbg[DBG_WORDS * wid + k] = g_phase[threadIdx.x >> 6][k];
+    }
+#endif
 #if RT_WAVE_STATS
     {
         const int wid = (int)(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
         if (P.dbg && lane == 0 && wid < DBG_WAVES) {
-            P.dbg[4 * wid + 0] = w_begin;
-            P.dbg[4 * wid + 1] = wall_clock64();
-            P.dbg[4 * wid + 2] = w_tiles;
-            P.dbg[4 * wid + 3] = w_busy;
+            P.dbg[DBG_WORDS * wid + 0] = w_begin;
+            P.dbg[DBG_WORDS * wid + 1] = wall_clock64();
+            P.dbg[DBG_WORDS * wid + 2] = w_tiles;
+            P.dbg[DBG_WORDS * wid + 3] = w_busy;
         }
     }
 #endif
@@ -3497,3 +3566,13 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ssao(const
                        dim3(rt::BLUR_X, rt::BLUR_Y), 0, stream, *A);
     return hipGetLastError();
 }
+
+#if defined(RT_COUNT) && RT_COUNT
+// diagnostic builds: read and clear g_wsteps (tools/count_gpu_work.py)
+extern "C" __attribute__((visibility("default"))) int rt_diag_wave_steps(unsigned long long* out)
+{
+    unsigned long long z[8] = {};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wsteps), sizeof(z)) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_wsteps), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif

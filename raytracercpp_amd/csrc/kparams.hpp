@@ -24,7 +24,8 @@ constexpr uint32_t TILE_ID_BITS = 20;
 constexpr uint32_t TILE_ID_MASK = (1u << TILE_ID_BITS) - 1;
 constexpr uint32_t TILE_COST_MAX = 2047;
 constexpr uint32_t TILE_PROBE_BUDGET = 96;
-constexpr int DBG_WAVES = 16384;   // per-wave diagnostic records (RT_WAVE_STATS builds)
+constexpr int DBG_WAVES = 16384;   // per-wave diagnostic records (RT_WAVE_STATS / RT_PHASE_TIME builds)
+constexpr int DBG_WORDS = 8;       // u64 words per record
 
 enum TexSlot { TEX_AO = 0, TEX_DIFFUSE = 1, TEX_NORMAL = 2, TEX_DISPLACEMENT = 3, TEX_ROUGHNESS = 4, TEX_SKYSPHERE = 5 };
 enum Shading { RT_SHADING = 0, ABS_NORMALS = 1, PASTEL_NORMALS = 2, BARYCENTRIC = 3, VISUALIZE_AO = 4 };
@@ -136,7 +137,7 @@ struct KParams {
                                     // tests, [16..21] uncertified queries by reason (RT_COUNT: overflow, NaN,
                                     // overflowed-only, tie, t outside (0, inf), certificate failed);
                                     // then the tile-queue heads, shard s at counters[NCOUNTERS + 16 s]
-    unsigned long long* dbg;        // diagnostic builds (RT_WAVE_STATS): per wave [DBG_WAVES][4], else nullptr
+    unsigned long long* dbg;        // diagnostic builds (RT_WAVE_STATS): per wave [DBG_WAVES][DBG_WORDS], else nullptr
     PrimRec* prim;            // split frame: one record per launch pixel (lr * rw + px), else nullptr
     int32_t tq_base;          // first counters[] word of this launch's tile-queue heads (NCOUNTERS or NCOUNTERS2)
     // SSAO inputs (enable_ssao): Renderer::_z_buffer / _normal_buffer, renderer.cpp:1107-1110, 975-979

@@ -1131,8 +1131,8 @@ int Renderer::trace_frame()
     P.counters = d_counters_.as<unsigned long long>();
     if ((e = hipMemsetAsync(d_counters_.p, 0, NCOUNTER_WORDS * 8, stream_)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
     if (getenv("RT_DEBUG_WAVES")) {   // diagnostic builds: per-wave records (rt_debug_read)
-        if ((e = d_dbg_.reserve((size_t)DBG_WAVES * 32)) != hipSuccess ||
-            (e = hipMemsetAsync(d_dbg_.p, 0, (size_t)DBG_WAVES * 32, stream_)) != hipSuccess)
+        if ((e = d_dbg_.reserve((size_t)DBG_WAVES * DBG_WORDS * 8)) != hipSuccess ||
+            (e = hipMemsetAsync(d_dbg_.p, 0, (size_t)DBG_WAVES * DBG_WORDS * 8, stream_)) != hipSuccess)
             return hip_fail(e, "debug buffer");
         P.dbg = d_dbg_.as<unsigned long long>();
     }
@@ -1308,7 +1308,7 @@ int Renderer::get_internal(uint32_t* argb, float* rgba, int32_t* hit_id, float* 
 
 int Renderer::debug_read(uint64_t* out, int64_t n)
 {
-    if (!d_dbg_.p || n < 0 || n > (int64_t)DBG_WAVES * 4)
+    if (!d_dbg_.p || n < 0 || n > (int64_t)DBG_WAVES * DBG_WORDS)
         return fail(RT_EINVAL, "debug_read: no debug buffer (RT_DEBUG_WAVES) or bad size");
     hipError_t e = hipMemcpy(out, d_dbg_.p, (size_t)n * 8, hipMemcpyDeviceToHost);
     return e == hipSuccess ? RT_OK : hip_fail(e, "debug_read");

@@ -59,6 +59,10 @@ constexpr int W_STACK = RT_W_STACK;
 #define RT_W_LOOP 2   // 1: while-while, 2: if-if, 3: if-if with one triangle per step (wbvh_closest)
 #endif   // traversal stack entries per lane (overflow: the query is not certified)
 
+#ifndef W_STEP_HOOK
+#define W_STEP_HOOK(cur, leaf)   // diagnostic builds (kernels.hip): per-step wave statistics
+#endif
+
 #ifndef RT_W_SLAB
 #define RT_W_SLAB 1   // per-child orientation slabs (below)
 #endif
@@ -264,17 +268,22 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
         while (cur != W_EMPTY && !(cur & W_LEAF)) {
 #endif
             nn++;
+            W_STEP_HOOK(cur, 0);
+            // (reading wave-uniform nodes, about half the steps of the C4 frame, through the
+            // scalar cache instead was measured no faster)
             const float4* p = reinterpret_cast<const float4*>(nodes + cur);
             const float4 Q0 = ldg(p);
             const uint4 Q1 = ldg(reinterpret_cast<const uint4*>(p) + 1), Q2 = ldg(reinterpret_cast<const uint4*>(p) + 2);
 #if RT_W_SLAB
             const uint4 NR = ldg(reinterpret_cast<const uint4*>(p) + 3), SB = ldg(reinterpret_cast<const uint4*>(p) + 4);
             const uint4 CH = ldg(reinterpret_cast<const uint4*>(p) + 5);
+#else
+            const uint4 CH = ldg(reinterpret_cast<const uint4*>(p) + 3);
+#endif
+#if RT_W_SLAB
             const float m3 = 384.0f * m;   // |N|_1 <= 3 * 128: the spatial margin in slab units
             const float ss = bitsf(Q2.z), slo_lo = bitsf(Q2.w) - m3, slo_hi = bitsf(Q2.w) + m3;
             const uint32_t nr[4] = {NR.x, NR.y, NR.z, NR.w}, sb[4] = {SB.x, SB.y, SB.z, SB.w};
-#else
-            const uint4 CH = ldg(reinterpret_cast<const uint4*>(p) + 3);
 #endif
             const uint32_t ex = fbits(Q0.w);
             // t of a plane origin + q s (widened by m) = q (s / d) + (origin -+ m - o) / d
@@ -374,6 +383,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
         {
 #endif
         // ---- a leaf: its triangles, closest hit kept; equal t from another triangle is a tie ----
+        W_STEP_HOOK(cur, 1);
         const uint32_t first = (cur >> 3) & 0x0FFFFFFFu, cnt = (cur & 7u) + 1u;
 #if RT_W_LOOP == 3
         // one triangle per step: the leaf link advances to the next triangle

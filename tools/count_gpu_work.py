@@ -16,12 +16,21 @@ modes = sys.argv[2:] or ["seg", "whole_line"]
 sc, st = scenes.CONFIGS[name]()
 r = Renderer(0)
 r.load_scene(sc, st)
+import ctypes
+from raytracercpp_amd import _lib
+_diag = getattr(_lib.lib(), "rt_diag_wave_steps", None) if hasattr(_lib, "lib") else None
 for mode in modes:
     if mode == "whole_line":
         os.environ["RT_SEG"] = "0"
         os.environ["RT_WBVH"] = "0"
+    steps = (ctypes.c_ulonglong * 8)()
+    if _diag:
+        _diag(steps)   # clear
     r.ray_trace()
     s = r.stats()
+    if _diag:
+        _diag(steps)
+    st8 = list(steps)
     w = s["work"]
     print(json.dumps({"config": name, "mode": mode, "seg_scale": s["seg_scale"], "primary_rays": s["primary_rays"],
                       "shadow_rays": s["shadow_rays"], "reflection_rays": s["reflection_rays"],
@@ -33,5 +42,8 @@ for mode in modes:
                       "exact_pixels": s["exact_pixels"], "uncertified_by_reason": s["uncertified"],
                       "deferred_pixels": s["deferred_pixels"], "kernel_ms": s["kernel_ms"],
                       "wave_steps_primary": s["wave_steps"][:3], "wave_steps_shadow": s["wave_steps"][3:],
+                      "wave_node_steps": st8[0], "uniform_node_steps": st8[1], "wave_leaf_steps": st8[2],
+                      "uniform_leaf_steps": st8[3], "node_step_lanes": st8[4], "leaf_step_lanes": st8[5],
+                      "distinct_nodes": st8[6], "distinct_leaves": st8[7],
                       "simd_efficiency": [round(s["wave_steps"][i + 1] / max(1, 64 * s["wave_steps"][i]), 4)
                                           for i in (0, 3)]}), flush=True)

@@ -18,7 +18,7 @@ r = Renderer(0)
 r.load_scene(sc, st)
 for _ in range(3):
     r.ray_trace()
-d = r.debug_read(16384 * 4).reshape(-1, 4).astype(np.int64)
+d = r.debug_read(16384 * 8).reshape(-1, 8)[:, :4].astype(np.int64)
 d = d[d[:, 1] > 0]
 t0 = d[:, 0].min()
 b, e, n, busy = (d[:, 0] - t0) / 100.0, (d[:, 1] - t0) / 100.0, d[:, 2], d[:, 3] / 100.0
