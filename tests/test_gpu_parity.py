@@ -539,6 +539,42 @@ def test_deferred_ray_groups_match_reference_golden(R, monkeypatch, budget, shif
     assert ran > 0 and deferred > 0
 
 
+FRAME_MODES = {
+    "split": {"RT_SPLIT": "1"},                                   # primary / shade passes
+    "lean": {"RT_WIDE_LEAN": "1"},                                # lean kernel + exact pass
+    "lean_budget": {"RT_WIDE_LEAN": "1", "RT_WIDE_BUDGET": "3"},  # + heavy-pixel pass
+    "generic": {"RT_PLAIN": "0"},                                 # the kernel without the plain specialisation
+    "tile_order": {"RT_TILE_ORDER": "1"},                         # probe-ordered tiles
+}
+
+
+@pytest.mark.parametrize("mode", sorted(FRAME_MODES))
+@pytest.mark.parametrize("scene_name", ["soup", "voxels", "bumpy_ssaa"])
+def test_frame_modes_match_oracle(R, monkeypatch, mode, scene_name):
+    """The wide-BVH frame's opt-in variants on the segment-query stress
+    scenes and a normal-mapped SSAA frame: the same framebuffers as the oracle."""
+    from raytracercpp_amd import scenes
+    from raytracercpp_amd.scene import empty_shapes
+    for k, v in FRAME_MODES[mode].items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(5)
+    if scene_name == "soup":
+        sc, st = _soup_scene(rng)
+        st = st.copy(image_width=200, image_height=120)
+        sc.light = np.asarray((60.0, -1.4999, -4.0), np.float32)
+    elif scene_name == "voxels":
+        sc = _voxel_scene(n=6)
+        sc.shape_kind, sc.shape, sc.shape_mat = empty_shapes()
+        _, st = scenes.bumpy70k(width=200, height=120)
+        st = st.copy(bvh_leaf_object_count=8)
+        sc.light = np.asarray((0.3, 0.0, 0.0), np.float32)
+    else:
+        sc, st = scenes.bumpy70k(width=160, height=90, enable_ssaa=True, ssaa_factor=2)
+    o = Oracle(sc, st).render_rows()
+    g = gpu_render(R, sc, st)
+    _check_vs_oracle(g, o, f"{scene_name} {mode}", R=R)
+
+
 @pytest.mark.parametrize("case", ["soup", "voxels", "huge", "ssao", "bands"])
 def test_forced_deferral_matches_oracle(R, monkeypatch, case):
     """Every primary query deferred (RT_DEFER_BUDGET=1) with the default 32-lane ray groups,
