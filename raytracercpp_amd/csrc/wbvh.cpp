@@ -261,6 +261,40 @@ struct ChildGeom {
     int32_t first, count;
 };
 
+// Backface cone code of a child (wbvh.hpp): theta = the largest angle between N and a triangle
+// normal n below (triangles with n = 0 never hit: Mdet = 0); a ray with angle(N, d) < psi =
+// acos(eps) - theta has angle(n, d) < acos(eps) for every n, i.e. exact n . d > eps |n| |d|,
+// and the float Mdet = n . (-d) is then negative (its rounding is below 2^-22 |n| |d| for |n|
+// in (1e-30, 1e27)).  cos(angle(N, d)) > cos psi  <=>  N . d > cos(psi) |N| |d|: the code is
+// the threshold cos(psi) |N| + 0.01 (the kernel's rounding margin) rounded up in steps of
+// W_CONE_STEP; 255 = no cone (psi <= 0, or a normal out of range).
+int cone_code(const int* nq, const ChildGeom& g, const std::vector<GTri, DefaultInitAlloc<GTri>>& tris)
+{
+#if RT_W_CONE
+    const double Nl = std::sqrt((double)nq[0] * nq[0] + (double)nq[1] * nq[1] + (double)nq[2] * nq[2]);
+    double theta = 0;
+    for (int32_t i = g.first; i < g.first + g.count; i++) {
+        const GTri& t = tris[(size_t)g.idx[i]];
+        const double n0 = t.n[0], n1 = t.n[1], n2 = t.n[2];
+        const double len = std::sqrt(n0 * n0 + n1 * n1 + n2 * n2);
+        if (len == 0)
+            continue;
+        if (!(len > 1e-30 && len < 1e27))
+            return 255;
+        const double c = (n0 * nq[0] + n1 * nq[1] + n2 * nq[2]) / (len * Nl);
+        theta = std::max(theta, std::acos(std::max(-1.0, std::min(1.0, c))));
+    }
+    const double psi = std::acos(W_CONE_EPS) - theta - 1e-9;
+    if (!(psi > 0))
+        return 255;
+    const double code = std::ceil((std::cos(psi) * Nl + 0.01) / ((double)W_CONE_STEP * (1 - 1e-9)));
+    return code <= 254 ? (int)code : 255;
+#else
+    (void)nq, (void)g, (void)tris;
+    return 255;
+#endif
+}
+
 WNode quantise(const Box* cb, const uint32_t* link, int nc, const ChildGeom* cg,
                const std::vector<GTri, DefaultInitAlloc<GTri>>* tris)
 {
@@ -350,9 +384,9 @@ WNode quantise(const Box* cb, const uint32_t* link, int nc, const ChildGeom* cg,
             w.slab[j] = 0;
             continue;
         }
-        // signed bytes (two's complement)
+        // signed bytes (two's complement), the cone code in byte 3
         w.nrm[j] = (uint32_t)(uint8_t)(int8_t)nq[j][0] | ((uint32_t)(uint8_t)(int8_t)nq[j][1] << 8) |
-                   ((uint32_t)(uint8_t)(int8_t)nq[j][2] << 16);
+                   ((uint32_t)(uint8_t)(int8_t)nq[j][2] << 16) | ((uint32_t)cone_code(nq[j], cg[j], *tris) << 24);
         double q0 = std::floor((smin[j] - (double)slo) / st), q1 = std::ceil((smax[j] - (double)slo) / st);
         q0 = std::max(0.0, std::min(65535.0, q0));
         q1 = std::max(0.0, std::min(65535.0, q1));
@@ -529,14 +563,23 @@ int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)
             s >= oct.nodes[L].a + (oct.nodes[L].b & ~LEAF_BIT))
             bad++;
     }
-    // every child box holds its subtree: node boxes and triangle vertices (a, a + ab, a + ac)
+    // every child box holds its subtree: node boxes and triangle vertices (a, a + ab, a + ac);
+    // every slab and cone on the path holds each triangle below (checked at the leaves)
+    constexpr int MAXP = 64;
     struct Item {
         uint32_t ref;
         Box box;
+        int np;
+        uint32_t path[MAXP];   // node << 2 | child of every inner node on the way
     };
     std::vector<Item> stack;
     Box all = {{-INFINITY, -INFINITY, -INFINITY}, {INFINITY, INFINITY, INFINITY}};
-    stack.push_back({0u, all});
+    {
+        Item root{};
+        root.ref = 0u;
+        root.box = all;
+        stack.push_back(root);
+    }
     auto inside = [](const Box& b, const Box& outer) {
         for (int a = 0; a < 3; a++)
             if (!(b.lo[a] >= outer.lo[a] && b.hi[a] <= outer.hi[a]))
@@ -558,6 +601,40 @@ int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)
                     bad++;
                 if (!inside(tri_box(w.tris[k]), it.box))
                     bad++;
+#if RT_W_SLAB
+                const GTri& T = w.tris[k];
+                for (int q = 0; q < it.np; q++) {
+                    const WNode& N = w.nodes[it.path[q] >> 2];
+                    const int j = (int)(it.path[q] & 3u);
+                    const double org[3] = {N.ox, N.oy, N.oz};
+                    const double nv[3] = {(double)(int8_t)(N.nrm[j] & 0xffu), (double)(int8_t)((N.nrm[j] >> 8) & 0xffu),
+                                          (double)(int8_t)((N.nrm[j] >> 16) & 0xffu)};
+                    const double lo = (double)N.slo + (double)(N.slab[j] & 0xffffu) * (double)N.s;
+                    const double hi = (double)N.slo + (double)(N.slab[j] >> 16) * (double)N.s;
+                    for (int v = 0; v < 3; v++) {
+                        double sp = 0;
+                        for (int a = 0; a < 3; a++)
+                            sp += nv[a] * ((double)T.a[a] + (v == 1 ? (double)T.ab[a] : v == 2 ? (double)T.ac[a] : 0.0) - org[a]);
+                        if (!(sp >= lo && sp <= hi))
+                            bad++;
+                    }
+#if RT_W_CONE
+                    const uint32_t code = N.nrm[j] >> 24;
+                    const double nn = std::sqrt((double)T.n[0] * T.n[0] + (double)T.n[1] * T.n[1] + (double)T.n[2] * T.n[2]);
+                    if (code < 255 && nn > 0) {
+                        // the kernel skips the child only for d with N . d > (code STEP - 0.01) |d|;
+                        // every such d must meet n at cos > eps
+                        const double Nl = std::sqrt(nv[0] * nv[0] + nv[1] * nv[1] + nv[2] * nv[2]);
+                        const double kap = (code * (double)W_CONE_STEP - 0.01) / Nl;
+                        const double c = (T.n[0] * nv[0] + T.n[1] * nv[1] + T.n[2] * nv[2]) / (nn * Nl);
+                        const double ang = std::acos(std::max(-1.0, std::min(1.0, c)));
+                        if (!(nn > 1e-30 && nn < 1e27) || !(kap > -1.0) ||
+                            !(std::acos(std::min(1.0, kap)) + ang < std::acos(W_CONE_EPS)))
+                            bad++;
+                    }
+#endif
+                }
+#endif
             }
             continue;
         }
@@ -574,12 +651,18 @@ int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)
             // the decoded box (outward-rounded to float) need not sit inside the parent's, but the
             // triangles below must sit inside every decoded box on their path: tested at the leaves
             // against the intersection of the path's boxes
-            Box path = cb;
+            Item ch = it;
+            ch.ref = N.child[j];
             for (int a = 0; a < 3; a++) {
-                path.lo[a] = std::max(cb.lo[a], it.box.lo[a]);
-                path.hi[a] = std::min(cb.hi[a], it.box.hi[a]);
+                ch.box.lo[a] = std::max(cb.lo[a], it.box.lo[a]);
+                ch.box.hi[a] = std::min(cb.hi[a], it.box.hi[a]);
             }
-            stack.push_back({N.child[j], path});
+            if (ch.np >= MAXP) {
+                bad++;
+                continue;
+            }
+            ch.path[ch.np++] = (it.ref << 2) | (uint32_t)j;
+            stack.push_back(ch);
         }
     }
     for (size_t k = 0; k < n; k++)

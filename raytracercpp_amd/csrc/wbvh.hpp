@@ -66,6 +66,13 @@ constexpr int W_STACK = RT_W_STACK;
 #ifndef RT_W_SLAB
 #define RT_W_SLAB 1   // per-child orientation slabs (below)
 #endif
+#ifndef RT_W_CONE
+#define RT_W_CONE 1   // per-child backface cones (below; needs RT_W_SLAB)
+#endif
+// cone threshold step: c in 0..254 encodes c * 224 / 254 >= |N| (|N| <= 127 sqrt 3 < 220), so 255
+// can never pass.  W_CONE_EPS: the triangles' minimum cos(normal, d) the build guarantees
+constexpr float W_CONE_STEP = 224.0f / 254.0f;
+constexpr double W_CONE_EPS = 1e-4;
 
 struct alignas(16) WNode {
     float ox, oy, oz;
@@ -79,6 +86,10 @@ struct alignas(16) WNode {
     // quantised to [-127, 127]), q0 / q1 the low / high 16 bits of slab[j].  A curved patch is thin
     // along its mean normal, so a ray that grazes the surface misses most patches' slabs
     // although it crosses their boxes (silhouette rays).
+    // Backface cone of child j (RT_W_CONE): nrm byte 3 = c, 255 = none.  Every triangle
+    // below j that Moller-Trumbore could ever hit faces away from a ray whose direction d has
+    //   N_j . d  >  c * W_CONE_STEP * |d|
+    // (the test rejects it on Mdet <= 0 before anything else), so such a ray skips j.
     float s, slo;
     uint32_t nrm[4];
     uint32_t slab[4];
@@ -248,6 +259,10 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
     const bool nx_lo = !(ix < 0.0f), ny_lo = !(iy < 0.0f), nz_lo = !(iz < 0.0f);
 
     constexpr float SL = 0x1p-20f;   // relative slack over the rounding of a slab parameter (<= 3 ulp)
+#if RT_W_SLAB && RT_W_CONE
+    // |d| rounded up (sqrt and dot within 2^-22), times the cone step: threshold = c * cstep
+    const float cstep = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z) * (1.0f + 0x1p-20f) * W_CONE_STEP;
+#endif
     float best_s = hi + fabsf(hi) * SL;   // h.t (or hi) plus slack: a child entered at or below it may hold a hit
     bool tie = false, nanhit = false, infhit = false, overflow = false;
     int sp = 0;
@@ -315,6 +330,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                 const float tfz = __builtin_fmaf((float)((fqz >> sh) & 0xffu), sz, bz);
                 float tmin = fmaxf(fmaxf(tnx, tny), tnz);
                 float tmax = fminf(fminf(tfx, tfy), tfz);
+                bool away = false;   // backface cone (RT_W_CONE)
 #if RT_W_SLAB
                 {
                     // N . (o + t d - origin) in [c0, c1] widened by m3 >= |N|_1 m: t between
@@ -331,13 +347,18 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                     const float s0 = c0 * ia, s1 = c1 * ia;
                     tmin = fmaxf(tmin, fminf(s0, s1));
                     tmax = fminf(tmax, fmaxf(s0, s1));
+#if RT_W_CONE
+                    // every triangle below faces away when a exceeds the threshold (rounding of
+                    // a and of the threshold: < 1e-4 |d|, inside the build's 0.01 |d|)
+                    away = a > (float)(nr[j] >> 24) * cstep;
+#endif
                 }
 #endif
                 // enter when max(tmin, 0) <= min(tmax (1 + SL), best_s); a NaN tmin (every
                 // slab NaN) enters too.  The key orders the children; misses get INFINITY.
                 const float lim = fminf(__builtin_fmaf(fabsf(tmax), SL, tmax), best_s);
                 const float k0 = fmaxf(tmin, 0.0f);
-                const bool ok = ch[j] != W_EMPTY && k0 <= lim;
+                const bool ok = ch[j] != W_EMPTY && k0 <= lim && !away;
                 key[j] = ok ? fminf(k0, 3.0e38f) : INFINITY;
                 ref[j] = ch[j];
 #if defined(__HIP_DEVICE_COMPILE__) && RT_W_SCHED_BARRIER

@@ -64,7 +64,8 @@ def _check(tri, o, d, depth=12, leaf=40, max_uncert=0.01):
     return status, stats
 
 
-@pytest.mark.parametrize("scene_name", ["robot", "voxels", "sphere1m_surface", "grazing", "soup", "bumpy_camera"])
+@pytest.mark.parametrize("scene_name", ["robot", "voxels", "sphere1m_surface", "grazing", "soup", "bumpy_camera",
+                                        "bumpy_shadow", "robot_shadow"])
 def test_certified_queries_match_oracle(scene_name):
     rng = np.random.default_rng(7)
     max_uncert = 0.01
@@ -87,6 +88,13 @@ def test_certified_queries_match_oracle(scene_name):
         # slivers (nearly collinear vertices) and degenerate triangles
         tri = _soup(rng)
         o, d = _rays(rng, 50000, np.array([0, 0, -1], np.float32), 1.0)
+    elif scene_name in ("bumpy_shadow", "robot_shadow"):
+        # is_shadowed's rays from the camera's hits toward the light: the backface cones
+        # (wbvh.hpp RT_W_CONE) skip most of the patches around each origin
+        import tools.shadow_probe as sp
+        sc, st = (scenes.bumpy70k if scene_name == "bumpy_shadow" else scenes.robot1080)(width=320, height=180)
+        o, d = sp.shadow_rays(sc, st, 1)
+        tri = sc.tri
     elif scene_name == "bumpy_camera":
         sc, st = scenes.bumpy70k(width=480, height=270)
         import tools.wbvh_probe as wp
