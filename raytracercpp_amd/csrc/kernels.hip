@@ -1719,20 +1719,121 @@ __device__ __forceinline__ int global_row(const KParams& P, int lr)
 // band's rays share that XCD's L2) and moves to the next shard when its own is empty;
 // it is done once it has found all eight empty.  One head word serves ~88 dequeues per
 // microsecond (MI355X_MICROARCH.md, dequeue row), under the frame's 130K tiles at ~2 ms.
+#ifndef RT_BLOCK_QUEUE
+#define RT_BLOCK_QUEUE 1   // the block's waves share one dequeue per 4 tiles (below)
+#endif
 struct TileQueue {
     int shard, empty;
 };
 
-__device__ __forceinline__ TileQueue tile_queue_begin() { return TileQueue{(int)(blockIdx.x & (TILE_SHARDS - 1)), 0}; }
-
 // Ticket t of shard s -> tile index (row-major), or -1 past the shard's end.  Measured
-// against alternatives (r02): guided chunks of 2-4 adjacent tiles per dequeue, tickets taken
-// one tile ahead, and blocked orders (patches of 8x8 .. 32x16 tiles) were all slower.
+// against alternatives (r02): guided chunks of 2-4 adjacent tiles per wave dequeue, tickets
+// taken one tile ahead, and blocked orders (patches of 8x8 .. 32x16 tiles) were all slower.
 __device__ __forceinline__ int shard_tile(const KParams& P, int s, int t)
 {
     const int r0 = (int)((long long)P.tiles_y * s / TILE_SHARDS), r1 = (int)((long long)P.tiles_y * (s + 1) / TILE_SHARDS);
     return t < (r1 - r0) * P.tiles_x ? r0 * P.tiles_x + t : -1;
 }
+
+// tile of ticket t on shard s (natural or probe order), or -1 past the shard's end
+__device__ __forceinline__ int ticket_tile(const KParams& P, int s, int t, int ntiles)
+{
+    if (P.tile_order) {
+        const int pos = s + TILE_SHARDS * t;
+        return pos < ntiles ? (int)(ldg(P.tile_order + pos) & TILE_ID_MASK) : -1;
+    }
+    return shard_tile(P, s, t);
+}
+
+#if RT_BLOCK_QUEUE
+// Block-shared dequeue.  One global atomic takes WAVES_PER_BLOCK consecutive tickets of the
+// block's shard, and the block's waves hand them out among themselves through one LDS word
+//   bit 31 done | bits 30..24 generation | bits 23..16 tickets in the batch | bits 15..0 next;
+// a wave's LDS add returns (generation g, count c, index i): i < c -> the batch's i-th ticket
+// (base and shard in slot g & 3); i == c -> this wave takes the next batch (the global atomic,
+// moving to the next shard when its own is empty) and publishes generation g + 1 with its own
+// ticket already taken; i > c -> it waits for generation g + 1.  The four waves of a block
+// then work on four adjacent tiles (one CU's L1), and the frame needs a quarter of the
+// global dequeues (a global round trip was ~7 % of a wave's time per tile, MI355X r02).
+struct BlockQueue {
+    unsigned int word;
+    int shard, empty;
+    int base[4], sh[4];
+};
+__shared__ BlockQueue g_bq;
+
+__device__ __forceinline__ void tile_queue_init()
+{
+    if (threadIdx.x == 0) {
+        g_bq.word = 0u;   // generation 0 with no tickets: the first wave refills
+        g_bq.shard = (int)(blockIdx.x & (TILE_SHARDS - 1));
+        g_bq.empty = 0;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ TileQueue tile_queue_begin() { return TileQueue{0, 0}; }
+
+__device__ __forceinline__ int tile_queue_next(const KParams& P, TileQueue&, int ntiles)
+{
+    const int lane = threadIdx.x & 63;
+    for (;;) {
+        unsigned int w = 0;
+        if (lane == 0)
+            w = __hip_atomic_fetch_add(&g_bq.word, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        w = __builtin_amdgcn_readfirstlane(w);
+        if (w & 0x80000000u)
+            return -1;
+        const unsigned int g = (w >> 24) & 0x7fu, c = (w >> 16) & 0xffu, i = w & 0xffffu;
+        if (i < c) {
+            const int slot = (int)(g & 3u);
+            return ticket_tile(P, g_bq.sh[slot], g_bq.base[slot] + (int)i, ntiles);
+        }
+        if (i == c) {
+            // this wave refills: WAVES_PER_BLOCK tickets of the first non-empty shard
+            int shard = g_bq.shard, empty = g_bq.empty, b = 0, n = 0;
+            while (empty < TILE_SHARDS) {
+                int t = 0;
+                if (lane == 0)
+                    t = (int)atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[P.tq_base + 16 * shard]),
+                                       (unsigned)WAVES_PER_BLOCK);
+                b = __builtin_amdgcn_readfirstlane(t);
+                n = 0;
+                while (n < WAVES_PER_BLOCK && ticket_tile(P, shard, b + n, ntiles) >= 0)
+                    n++;
+                if (n > 0)
+                    break;
+                empty++;
+                shard = (shard + 1) & (TILE_SHARDS - 1);
+            }
+            const unsigned int g1 = (g + 1u) & 0x7fu;
+            if (lane == 0) {
+                g_bq.shard = shard;
+                g_bq.empty = empty;
+                g_bq.base[g1 & 3u] = b;
+                g_bq.sh[g1 & 3u] = shard;
+                // publish: the batch's fields are visible before the word that names them
+                __hip_atomic_store(&g_bq.word, n > 0 ? (g1 << 24) | ((unsigned)n << 16) | 1u : 0x80000000u,
+                                   __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            return n > 0 ? ticket_tile(P, shard, b, ntiles) : -1;
+        }
+        // another wave is taking the next batch
+        for (;;) {
+            unsigned int v = 0;
+            if (lane == 0)
+                v = __hip_atomic_load(&g_bq.word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            v = __builtin_amdgcn_readfirstlane(v);
+            if ((v & 0x80000000u) || ((v >> 24) & 0x7fu) != g)
+                break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+}
+#else
+__device__ __forceinline__ void tile_queue_init() {}
+
+__device__ __forceinline__ TileQueue tile_queue_begin() { return TileQueue{(int)(blockIdx.x & (TILE_SHARDS - 1)), 0}; }
 
 // next tile for the calling wave (wave-uniform), or -1 when every shard is empty.  With
 // P.tile_order (tiles sorted by estimated cost, heaviest first: tile_probe_kernel) shard s
@@ -1745,20 +1846,15 @@ __device__ __forceinline__ int tile_queue_next(const KParams& P, TileQueue& q, i
         if (lane == 0)
             t = (int)atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[P.tq_base + 16 * q.shard]), 1u);
         t = __builtin_amdgcn_readfirstlane(t);
-        if (P.tile_order) {
-            const int pos = q.shard + TILE_SHARDS * t;
-            if (pos < ntiles)
-                return (int)(ldg(P.tile_order + pos) & TILE_ID_MASK);
-        } else {
-            const int tile = shard_tile(P, q.shard, t);
-            if (tile >= 0)
-                return tile;
-        }
+        const int tile = ticket_tile(P, q.shard, t, ntiles);
+        if (tile >= 0)
+            return tile;
         q.empty++;
         q.shard = (q.shard + 1) & (TILE_SHARDS - 1);
     }
     return -1;
 }
+#endif
 
 // Tile cost probe (the tile order above).  One ray per tile, through the tile's centre
 // pixel, is traced through the wide BVH with a small iteration budget; its node visits +
@@ -1830,6 +1926,7 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
     const int ntiles = P.tiles_x * P.tiles_y;
     v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
     unsigned nshadow = 0, nrefl = 0;
+    tile_queue_init();
     TileQueue q = tile_queue_begin();
 #if RT_PHASE_TIME
     if (PLAIN && lane == 0) {
@@ -1954,6 +2051,7 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_PRIM) void primary_kernel(KParams P)
     const int lane = threadIdx.x & 63;
     const int ntiles = P.tiles_x * P.tiles_y;
     const v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+    tile_queue_init();
     TileQueue q = tile_queue_begin();
     for (;;) {
         const int tile = tile_queue_next(P, q, ntiles);
@@ -2000,6 +2098,7 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_SHADE) void shade_kernel(KParams P)
     const int ntiles = P.tiles_x * P.tiles_y;
     const v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
     unsigned nshadow = 0;
+    tile_queue_init();
     TileQueue q = tile_queue_begin();
     for (;;) {
         const int tile = tile_queue_next(P, q, ntiles);
