@@ -1722,13 +1722,17 @@ __device__ __forceinline__ int global_row(const KParams& P, int lr)
 #ifndef RT_BLOCK_QUEUE
 #define RT_BLOCK_QUEUE 1   // the block's waves share one dequeue per 4 tiles (below)
 #endif
+#ifndef RT_BQ_BATCH
+#define RT_BQ_BATCH 4      // tickets per block dequeue (<= 255)
+#endif
 struct TileQueue {
     int shard, empty;
 };
 
 // Ticket t of shard s -> tile index (row-major), or -1 past the shard's end.  Measured
 // against alternatives (r02): guided chunks of 2-4 adjacent tiles per wave dequeue, tickets
-// taken one tile ahead, and blocked orders (patches of 8x8 .. 32x16 tiles) were all slower.
+// taken one tile ahead, blocked orders (patches of 8x8 .. 32x16 tiles), 2x2 tile quads per
+// block batch and 8-ticket block batches were all slower.
 __device__ __forceinline__ int shard_tile(const KParams& P, int s, int t)
 {
     const int r0 = (int)((long long)P.tiles_y * s / TILE_SHARDS), r1 = (int)((long long)P.tiles_y * (s + 1) / TILE_SHARDS);
@@ -1796,10 +1800,10 @@ __device__ __forceinline__ int tile_queue_next(const KParams& P, TileQueue&, int
                 int t = 0;
                 if (lane == 0)
                     t = (int)atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[P.tq_base + 16 * shard]),
-                                       (unsigned)WAVES_PER_BLOCK);
+                                       (unsigned)RT_BQ_BATCH);
                 b = __builtin_amdgcn_readfirstlane(t);
                 n = 0;
-                while (n < WAVES_PER_BLOCK && ticket_tile(P, shard, b + n, ntiles) >= 0)
+                while (n < RT_BQ_BATCH && ticket_tile(P, shard, b + n, ntiles) >= 0)
                     n++;
                 if (n > 0)
                     break;
