@@ -230,7 +230,7 @@ int rt_get_stats(rt_renderer *r, rt_stats *out);
 /* Diagnostic builds (with RT_DEBUG_WAVES set in the environment): the last ray_trace's
  * per-wave records of 8 words, n = 8 x waves values -- -DRT_WAVE_STATS=1: {first dequeue tick,
  * exit tick, tiles, busy ticks} (100 MHz wall clock); -DRT_PHASE_TIME=1: shader cycles per
- * phase {dequeue, ray generation, primary query, shading, shadow query, framebuffer} (plain
+ * phase {tile setup, ray generation, primary query, shading, shadow query, framebuffer, dequeue} (plain
  * kernel).  RT_EINVAL when no record buffer exists. */
 int rt_debug_read(rt_renderer *r, uint64_t *out, int64_t n);
 

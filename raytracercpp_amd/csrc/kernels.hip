@@ -931,7 +931,6 @@ __device__ c3 skybox_sample(const KParams& P, v3 dir, float* alpha)
 }
 
 __device__ __forceinline__ const float* mat_of(const KParams& P, int id) { return P.mats + (size_t)MAT_STRIDE * id; }
-__device__ __forceinline__ c3 mat_col(const float* m, int off) { return col(m[off], m[off + 1], m[off + 2]); }
 
 // Triangle::interpolate_texcoords (triangle.cpp:155-160) / get_tex_coords (renderer.cpp:436-445)
 __device__ __forceinline__ void get_tex_coords(const KParams& P, int tri, float u, float v, float& tu, float& tv)
@@ -996,7 +995,7 @@ __device__ void parallax_occlusion_mapping(const KParams& P, int tri, float u, f
 }
 
 #if RT_PHASE_TIME
-// per wave: [0..5] cycles per phase, [7] the last mark (LDS; the wave's first active lane updates)
+// per wave: [0..6] cycles per phase, [7] the last mark (LDS; the wave's first active lane updates)
 __shared__ unsigned long long g_phase[WAVES_PER_BLOCK][8];
 __device__ __forceinline__ void ph_mark(int k)
 {
@@ -1084,8 +1083,9 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
         atomicAdd(&P.counters[14], 1ull);   // the certificate's k-DOP test
 #endif
     if (st == W_HIT) {
+        // slot and octree leaf are independent loads: two round trips to the certificate
         const int32_t slot = ldg(P.wslot + w.k);
-        const GNode leaf = load_gnode(P.nodes + ldg(P.wleaf + slot));
+        const GNode leaf = load_gnode(P.nodes + ldg(P.wleaf + w.k));
         if (kdop_certifies(leaf, o, d, w.t)) {
             h.t = w.t;
             h.u = w.u;
@@ -1143,7 +1143,7 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
     if (st == W_HIT && P.counters)
         atomicAdd(&P.counters[14], 1ull);
 #endif
-    if (st == W_HIT && kdop_certifies(load_gnode(P.nodes + ldg(P.wleaf + ldg(P.wslot + w.k))), o, d, w.t)) {
+    if (st == W_HIT && kdop_certifies(load_gnode(P.nodes + ldg(P.wleaf + w.k)), o, d, w.t)) {
         v3 q = o + d * w.t;
         *sh = length2(p - q) < length2(p - lp);
         return true;
@@ -1946,6 +1946,7 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
 #endif
     for (;;) {
         const int tile = tile_queue_next(P, q, ntiles);
+        if (PLAIN) PH_MARK(6);
         if (tile < 0)
             break;
 #if RT_WAVE_STATS
@@ -2012,7 +2013,7 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
         PH_MARK(0);   // the final (empty) dequeues
         const int wid = (int)(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
         if (P.dbg && lane == 0 && wid < DBG_WAVES)
-            for (int k = 0; k < 6; k++)
+            for (int k = 0; k < 7; k++)
                 P.dbg[DBG_WORDS * wid + k] = g_phase[threadIdx.x >> 6][k];
     }
 #endif

@@ -60,7 +60,7 @@ struct KParams {
     const WNode* wnodes;
     const GTri* wtris;           // octree records in wide-BVH leaf order
     const int32_t* wslot;        // wide-BVH triangle -> octree GTri slot
-    const uint32_t* wleaf;       // octree GTri slot -> flattened octree leaf node
+    const uint32_t* wleaf;       // wide-BVH triangle -> flattened octree leaf node (its certificate's k-DOP)
     int32_t nnodes;
     int32_t ntri_slots;       // GTri count (brute-force loop bound when enable_bvh == 0)
     int32_t levels;           // flattened tree depth + 1 (LDS level-stack entries per lane)

@@ -534,13 +534,13 @@ int Renderer::ensure_device_scene()
             size_t wn = wb_.nodes.size() * sizeof(WNode), wt = wb_.tris.size() * sizeof(GTri);
             if ((e = d_wnodes_.reserve(wn)) != hipSuccess || (e = d_wtris_.reserve(wt)) != hipSuccess ||
                 (e = d_wslot_.reserve(wb_.slot.size() * 4)) != hipSuccess ||
-                (e = d_wleaf_.reserve(wb_.leaf_of_slot.size() * 4)) != hipSuccess)
+                (e = d_wleaf_.reserve(wb_.leaf_of_k.size() * 4)) != hipSuccess)
                 return hip_fail(e, "hipMalloc (wide BVH)");
             if ((e = hipMemcpyAsync(d_wnodes_.p, wb_.nodes.data(), wn, hipMemcpyHostToDevice, stream_)) != hipSuccess ||
                 (e = hipMemcpyAsync(d_wtris_.p, wb_.tris.data(), wt, hipMemcpyHostToDevice, stream_)) != hipSuccess ||
                 (e = hipMemcpyAsync(d_wslot_.p, wb_.slot.data(), wb_.slot.size() * 4, hipMemcpyHostToDevice,
                                     stream_)) != hipSuccess ||
-                (e = hipMemcpyAsync(d_wleaf_.p, wb_.leaf_of_slot.data(), wb_.leaf_of_slot.size() * 4,
+                (e = hipMemcpyAsync(d_wleaf_.p, wb_.leaf_of_k.data(), wb_.leaf_of_k.size() * 4,
                                     hipMemcpyHostToDevice, stream_)) != hipSuccess)
                 return hip_fail(e, "upload (wide BVH)");
         }

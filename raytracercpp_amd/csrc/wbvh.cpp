@@ -535,9 +535,11 @@ void build_wbvh(const FlatOctree& oct, WBvh& out)
     out.stats.tris = n;
     out.tris.resize((size_t)n);
     out.slot.resize((size_t)n);
+    out.leaf_of_k.resize((size_t)n);
     for (int64_t i = 0; i < n; i++) {
         out.tris[(size_t)i] = oct.tris[(size_t)idx[(size_t)i]];
         out.slot[(size_t)i] = idx[(size_t)i];
+        out.leaf_of_k[(size_t)i] = out.leaf_of_slot[(size_t)idx[(size_t)i]];
     }
 }
 
@@ -545,8 +547,11 @@ int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)
 {
     int64_t bad = 0;
     const size_t n = oct.tris.size();
-    if (w.tris.size() != n || w.slot.size() != n || w.leaf_of_slot.size() != n)
+    if (w.tris.size() != n || w.slot.size() != n || w.leaf_of_slot.size() != n || w.leaf_of_k.size() != n)
         return 1;
+    for (size_t k = 0; k < n; k++)
+        if (w.slot[k] >= 0 && (size_t)w.slot[k] < n && w.leaf_of_k[k] != w.leaf_of_slot[(size_t)w.slot[k]])
+            bad++;
     if (n == 0)
         return w.nodes.empty() ? 0 : 1;
     std::vector<uint8_t> seen(n, 0), used(w.tris.size(), 0);

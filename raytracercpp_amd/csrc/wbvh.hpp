@@ -110,6 +110,7 @@ struct WBvh {
     std::vector<GTri> tris;            // octree records in leaf order
     std::vector<int32_t> slot;         // wide-BVH triangle -> octree GTri slot
     std::vector<uint32_t> leaf_of_slot;   // octree GTri slot -> flattened octree leaf node
+    std::vector<uint32_t> leaf_of_k;      // wide-BVH triangle -> flattened octree leaf node (= leaf_of_slot[slot])
     WStats stats;
 };
 

@@ -12,7 +12,7 @@ import numpy as np
 from raytracercpp_amd import scenes
 from raytracercpp_amd.renderer import Renderer
 
-NAMES = ["dequeue + tile", "ray generation", "primary query", "shading", "shadow query", "framebuffer"]
+NAMES = ["tile setup", "ray generation", "primary query", "shading", "shadow query", "framebuffer", "dequeue"]
 sc, st = scenes.sphere1m()
 if "--miss" in sys.argv:   # every primary ray misses (the sphere moved behind the camera)
     import dataclasses
@@ -22,7 +22,7 @@ r.load_scene(sc, st)
 for _ in range(3):
     r.ray_trace()
 s = r.stats()
-d = r.debug_read(16384 * 8).reshape(-1, 8)[:, :6].astype(np.float64)
+d = r.debug_read(16384 * 8).reshape(-1, 8)[:, :7].astype(np.float64)
 d = d[d.sum(1) > 0]
 tot = d.sum()
 print(f"kernel ms {s['kernel_ms']:.3f}  waves {len(d)}  mean cycles per wave {d.sum(1).mean():.0f}")
