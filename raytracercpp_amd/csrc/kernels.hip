@@ -931,6 +931,7 @@ __device__ c3 skybox_sample(const KParams& P, v3 dir, float* alpha)
 }
 
 __device__ __forceinline__ const float* mat_of(const KParams& P, int id) { return P.mats + (size_t)MAT_STRIDE * id; }
+__device__ __forceinline__ c3 mat_col(const float* m, int off) { return col(m[off], m[off + 1], m[off + 2]); }
 
 // Triangle::interpolate_texcoords (triangle.cpp:155-160) / get_tex_coords (renderer.cpp:436-445)
 __device__ __forceinline__ void get_tex_coords(const KParams& P, int tri, float u, float v, float& tu, float& tv)
