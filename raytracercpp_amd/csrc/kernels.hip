@@ -146,6 +146,15 @@ __device__ __forceinline__ TRay make_ray(const KParams& P, v3 o, v3 d)
 }
 
 // make_ray's R.nan alone (the primary pass needs no plane products)
+// A copy of v the compiler cannot prove equal to v: the exact path's ray setup (make_ray) is
+// then computed inside that rarely taken branch instead of being merged with an earlier
+// one and held in registers across the wide-BVH query.
+__device__ __forceinline__ v3 opaque(v3 v)
+{
+    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z));
+    return v;
+}
+
 __device__ __forceinline__ bool ray_is_nan(v3 o, v3 d)
 {
     bool nan = false;
@@ -1190,33 +1199,49 @@ __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv, bool
         return false;
     v3 o = p + n * 1.0e-4f;
     v3 d = normalize(lp - p);
-    TRay R = make_ray(P, o, d);
     THit h;
     bool r;
-    if (P.enable_bvh) {
-        if (P.seg_scale > 0.0f) {
-            // segment [-m, past the light]: a hit beyond hi fails the distance test below
-            // (|p - q| >= t - |n| * 1e-4), one behind the origin does not exist (t >= 0)
-            float m = seg_margin(P, R);
-            float nl = fabsf(n.x) + fabsf(n.y) + fabsf(n.z);
-            R.lo = -m;
-            R.hi = (sqrtf(length2(p - lp)) + 1.0e-4f * nl) * (1.0f + 0x1p-10f) + m;
-            // (seg_scale > 0: no analytic shapes, so shapes_shadow below has nothing to add)
-            bool sh;
-            if (!GRP && P.wnodes && P.nnodes > 0 && !R.nan && wide_shadow(P, o, d, R.hi, p, lp, lv, &sh))
-                return sh;
-            if (WIDE) {
-                *defer = true;
-                return false;
-            }
-            r = bvh_closest_seg<GRP>(P, R, h, lv);
-        } else {
-            if (WIDE) {
-                *defer = true;
-                return false;
-            }
-            r = bvh_closest<false, GRP>(P, R, h, lv);
+    if (P.enable_bvh && P.seg_scale > 0.0f) {
+        // segment [-m, past the light]: a hit beyond hi fails the distance test below
+        // (|p - q| >= t - |n| * 1e-4), one behind the origin does not exist (t >= 0)
+        float m, hi;
+        bool nan;
+        {
+            const TRay R0 = make_ray(P, o, d);
+            m = seg_margin(P, R0);
+            nan = R0.nan;
+            const float nl = fabsf(n.x) + fabsf(n.y) + fabsf(n.z);
+            hi = (sqrtf(length2(p - lp)) + 1.0e-4f * nl) * (1.0f + 0x1p-10f) + m;
         }
+        // (seg_scale > 0: no analytic shapes, so shapes_shadow below has nothing to add)
+        bool sh;
+        if (!GRP && P.wnodes && P.nnodes > 0 && !nan && wide_shadow(P, o, d, hi, p, lp, lv, &sh))
+            return sh;
+        if (WIDE) {
+            *defer = true;
+            return false;
+        }
+        TRay R = make_ray(P, opaque(o), opaque(d));
+        R.lo = -m;
+        R.hi = hi;
+        r = bvh_closest_seg<GRP>(P, R, h, lv);
+        if (r) {
+            v3 q = o + d * h.t;
+            if (length2(p - q) < length2(p - lp))
+                return true;
+        }
+        if (PLAIN)
+            return false;
+        return shapes_shadow(P, o, d, h.t, p, lp);
+    }
+    TRay R = make_ray(P, o, d);
+    if (P.enable_bvh) {
+        // whole-line query (segment queries off)
+        if (WIDE) {
+            *defer = true;
+            return false;
+        }
+        r = bvh_closest<false, GRP>(P, R, h, lv);
         if (r) {
             v3 q = o + d * h.t;
             if (length2(p - q) < length2(p - lp))
@@ -1283,12 +1308,11 @@ __device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv, ui
                            bool* aborted = nullptr)
 {
     Rec local = rec_fresh();
-    TRay R = make_ray(P, o, d);
     int src = -1;
     if (WIDE) {
         THit h;
         bool r = false;
-        if (!(P.enable_bvh && P.nnodes > 0 && !R.nan && wide_closest(P, o, d, h, r, lv))) {
+        if (!(P.enable_bvh && P.nnodes > 0 && !ray_is_nan(o, d) && wide_closest(P, o, d, h, r, lv))) {
             *aborted = true;
             return -1;
         }
@@ -1296,18 +1320,20 @@ __device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv, ui
     } else if (P.enable_bvh) {
         THit h;
         bool r = false;
-        const bool wide = !GRP && P.wnodes && P.nnodes > 0 && !R.nan;
+        const bool wide = !GRP && P.wnodes && P.nnodes > 0 && !ray_is_nan(o, d);
         if (!(wide && wide_closest(P, o, d, h, r, lv))) {
             if (wide && budget) {
                 *aborted = true;   // not certified: the deferred pass traces it through the octree
                 return -1;
             }
+            TRay R = make_ray(P, opaque(o), opaque(d));
             r = bvh_closest<false, GRP>(P, R, h, lv, budget, aborted);
             if (budget && *aborted)
                 return -1;
         }
         bvh_record(P, h, r, local, fin, src);
     } else {
+        TRay R = make_ray(P, o, d);
         // brute-force loop, renderer.cpp:1021-1027: fin takes every hit nearer
         // than itself; local keeps the last triangle that was hit.
         THit best, last;
@@ -3526,7 +3552,10 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(
         if (P->wide_lean && P->defer && P->defer2 && P->defer_cap) {
             // lean kernel (list 1: over-budget or uncertified pixels, head counters[3]) -> heavy-pixel
             // pass (list 2: uncertified, head counters[13]) -> exact ray-group pass over list 2
-            hipLaunchKernelGGL((rt::ray_trace_kernel<false, true>), dim3(blocks), dim3(rt::BLOCK), lds, stream, A);
+            if (P->plain && !P->zbuf && !P->nbuf)
+                hipLaunchKernelGGL((rt::ray_trace_kernel<false, true, true>), dim3(blocks), dim3(rt::BLOCK), lds, stream, A);
+            else
+                hipLaunchKernelGGL((rt::ray_trace_kernel<false, true>), dim3(blocks), dim3(rt::BLOCK), lds, stream, A);
             rt::KParams B = *P;
             B.wide_budget = 0;
             B.defer_in = P->defer;
