@@ -58,6 +58,9 @@ constexpr int BLOCK = 64 * WAVES_PER_BLOCK;
 #ifndef RT_OCC
 #define RT_OCC 5
 #endif
+#ifndef RT_OCC_PLAIN
+#define RT_OCC_PLAIN 4   // the plain kernel: 128 VGPRs (measured r02: 0.67 ms vs 0.71 at 5 waves, 0.69 at 3)
+#endif
 #ifndef RT_WW
 #define RT_WW 1
 #endif
@@ -1949,7 +1952,7 @@ __global__ __launch_bounds__(BLOCK) void tile_key_kernel(KParams P, const uint32
 // PLAIN: no texture map, sky, analytic shape, debug shading or SSAO buffer (host-checked,
 // KParams::plain): those code paths are compiled out.
 template <bool REFL, bool WIDE = false, bool PLAIN = false>
-__global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_kernel(KParams P)
+__global__ __launch_bounds__(BLOCK, PLAIN ? RT_OCC_PLAIN : RT_OCC) void ray_trace_kernel(KParams P)
 {
     extern __shared__ uint2 lds_levels[];
     uint2* lv = lds_levels + threadIdx.x;
