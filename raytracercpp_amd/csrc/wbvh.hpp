@@ -413,10 +413,11 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
 #else
         const uint32_t kend = first + cnt;
 #endif
-        for (uint32_t k = first; k < kend; k++) {
+        // the leaf's triangles in order (loading two records at a time was measured slower)
+        auto fold = [&](const GTri& T, uint32_t k) {
             nt++;
             float t, u, v;
-            if (mt_record(load_gtri(tris + k), o, d, t, u, v)) {
+            if (mt_record(T, o, d, t, u, v)) {
                 if (t != t)
                     nanhit = true;
                 else if (!(t <= hi))
@@ -433,7 +434,9 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                 } else if (t == h.t)
                     tie = true;
             }
-        }
+        };
+        for (uint32_t k = first; k < kend; k++)
+            fold(load_gtri(tris + k), k);
 #if RT_W_LOOP == 3
         if (cnt > 1) {
             cur = W_LEAF | ((first + 1) << 3) | (cnt - 2);
