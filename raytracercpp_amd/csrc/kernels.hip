@@ -1736,9 +1736,34 @@ __device__ __forceinline__ void write_ssao_buffers(const KParams& P, size_t o, b
     P.nbuf[o] = found ? make_float4(fin.normal.x, fin.normal.y, fin.normal.z, 0.0f) : make_float4(0, 0, 0, 0);
 }
 
+// tile -> (tile column, tile row) without an integer division: the float quotient through
+// 1 / tiles_x is within one of the true one for tile < 2^24, then corrected
+__device__ __forceinline__ void tile_xy(const KParams& P, int tile, int& tx, int& ty)
+{
+    const int W = P.tiles_x;
+    if (tile >= (1 << 24)) {
+        tx = tile % W;
+        ty = tile / W;
+        return;
+    }
+    int q = (int)((float)tile * (1.0f / (float)W));
+    int r = tile - q * W;
+    if (r < 0) {
+        q--;
+        r += W;
+    } else if (r >= W) {
+        q++;
+        r -= W;
+    }
+    tx = r;
+    ty = q;
+}
+
 // Global internal row of a launch-local row (interleaved bands across ranks).
 __device__ __forceinline__ int global_row(const KParams& P, int lr)
 {
+    if (P.nranks == 1)
+        return lr;   // (band * 1 + 0) * band_rows + lr - band * band_rows
     int band = lr / P.band_rows;
     return (band * P.nranks + P.rank) * P.band_rows + (lr - band * P.band_rows);
 }
@@ -1983,7 +2008,8 @@ __global__ __launch_bounds__(BLOCK, PLAIN ? RT_OCC_PLAIN : RT_OCC) void ray_trac
         const uint64_t w_t0 = wall_clock64();
         w_tiles++;
 #endif
-        int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+        int tx, ty;
+        tile_xy(P, tile, tx, ty);
         int px = tx * 8 + (lane & 7);
         int lr = ty * 8 + (lane >> 3);
         int py = lr < P.local_rows ? global_row(P, lr) : P.rh;
@@ -2092,7 +2118,8 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_PRIM) void primary_kernel(KParams P)
         const int tile = tile_queue_next(P, q, ntiles);
         if (tile < 0)
             break;
-        const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+        int tx, ty;
+        tile_xy(P, tile, tx, ty);
         const int px = tx * 8 + (lane & 7);
         const int lr = ty * 8 + (lane >> 3);
         const int py = lr < P.local_rows ? global_row(P, lr) : P.rh;
@@ -2139,7 +2166,8 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_SHADE) void shade_kernel(KParams P)
         const int tile = tile_queue_next(P, q, ntiles);
         if (tile < 0)
             break;
-        const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+        int tx, ty;
+        tile_xy(P, tile, tx, ty);
         const int px = tx * 8 + (lane & 7);
         const int lr = ty * 8 + (lane >> 3);
         const int py = lr < P.local_rows ? global_row(P, lr) : P.rh;
@@ -2540,7 +2568,8 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void refl_level0_kernel(KParams P, F
         tile = __builtin_amdgcn_readfirstlane(tile);
         if (tile >= ntiles)
             break;
-        int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+        int tx, ty;
+        tile_xy(P, tile, tx, ty);
         int px = tx * 8 + (lane & 7);
         int lr = ty * 8 + (lane >> 3);
         int py = lr < P.local_rows ? global_row(P, lr) : P.rh;
@@ -3118,7 +3147,8 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void raster_shade_kernel(KParams P, 
         tile = __builtin_amdgcn_readfirstlane(tile);
         if (tile >= ntiles)
             break;
-        int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+        int tx, ty;
+        tile_xy(P, tile, tx, ty);
         int px = tx * 8 + (lane & 7);
         int lr = ty * 8 + (lane >> 3);
         int py = lr < P.local_rows ? global_row(P, lr) : P.rh;
