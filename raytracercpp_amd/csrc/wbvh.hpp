@@ -331,9 +331,14 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                 const float tfz = __builtin_fmaf((float)((fqz >> sh) & 0xffu), sz, bz);
                 float tmin = fmaxf(fmaxf(tnx, tny), tnz);
                 float tmax = fminf(fminf(tfx, tfy), tfz);
-                bool away = false;   // backface cone (RT_W_CONE)
+                // enter when max(tmin, 0) <= min(tmax (1 + SL), best_s); a NaN tmin (every
+                // slab NaN) enters too.  The key orders the children; misses get INFINITY.
+                bool ok = ch[j] != W_EMPTY &&
+                          fmaxf(tmin, 0.0f) <= fminf(__builtin_fmaf(fabsf(tmax), SL, tmax), best_s);
 #if RT_W_SLAB
-                {
+                // the slab (and cone) only narrow the box's interval, so a child whose box
+                // fails is out already: when no lane's box passes, the wave skips this part
+                if (ok) {
                     // N . (o + t d - origin) in [c0, c1] widened by m3 >= |N|_1 m: t between
                     // (c0 - m3 + b) / a and (c1 + m3 + b) / a, b = N . (origin - o), a = N . d
                     const float nx = (float)(int8_t)(nr[j] & 0xffu), ny = (float)(int8_t)((nr[j] >> 8) & 0xffu),
@@ -348,19 +353,15 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                     const float s0 = c0 * ia, s1 = c1 * ia;
                     tmin = fmaxf(tmin, fminf(s0, s1));
                     tmax = fminf(tmax, fmaxf(s0, s1));
+                    ok = fmaxf(tmin, 0.0f) <= fminf(__builtin_fmaf(fabsf(tmax), SL, tmax), best_s);
 #if RT_W_CONE
                     // every triangle below faces away when a exceeds the threshold (rounding of
                     // a and of the threshold: < 1e-4 |d|, inside the build's 0.01 |d|)
-                    away = a > (float)(nr[j] >> 24) * cstep;
+                    ok = ok && !(a > (float)(nr[j] >> 24) * cstep);
 #endif
                 }
 #endif
-                // enter when max(tmin, 0) <= min(tmax (1 + SL), best_s); a NaN tmin (every
-                // slab NaN) enters too.  The key orders the children; misses get INFINITY.
-                const float lim = fminf(__builtin_fmaf(fabsf(tmax), SL, tmax), best_s);
-                const float k0 = fmaxf(tmin, 0.0f);
-                const bool ok = ch[j] != W_EMPTY && k0 <= lim && !away;
-                key[j] = ok ? fminf(k0, 3.0e38f) : INFINITY;
+                key[j] = ok ? fminf(fmaxf(tmin, 0.0f), 3.0e38f) : INFINITY;
                 ref[j] = ch[j];
 #if defined(__HIP_DEVICE_COMPILE__) && RT_W_SCHED_BARRIER
                 // one child at a time: the scheduler would interleave the four children's
