@@ -799,20 +799,18 @@ __device__ __forceinline__ bool bvh_closest_seg(const KParams& P, TRay& R, THit&
 }
 
 // HitInfo filled by Triangle::intersect for slot k (triangle.cpp:81-88)
-__device__ __forceinline__ Rec tri_record(const KParams& P, const THit& h)
+// The record of a hit on triangle record T (caller index id, material mat).
+__device__ __forceinline__ Rec rec_of(const KParams& P, const GTri& T, int id, int mat, const THit& h)
 {
     Rec r;
-    int id = P.tri_id[h.k];
-    const float4* p = reinterpret_cast<const float4*>(P.tris + h.k);
-    float4 q0 = p[0], q1 = p[1], q2 = p[2];
-    v3 ab = mk(q0.w, q1.x, q1.y);
-    v3 ac = mk(q1.z, q1.w, q2.x);
-    v3 n = mk(q2.y, q2.z, q2.w);
+    v3 ab = mk(T.ab[0], T.ab[1], T.ab[2]);
+    v3 ac = mk(T.ac[0], T.ac[1], T.ac[2]);
+    v3 n = mk(T.n[0], T.n[1], T.n[2]);
     r.tri = id;
     r.t = h.t;
     r.u = h.u;
     r.v = h.v;
-    r.mat = P.tri_mat[id];
+    r.mat = mat;
     r.normal = normalize(n);
     // Triangle::get_tangent, triangle.cpp:134-153
     float u1 = -1, v1 = -1, u2 = -1, v2 = -1, u3 = -1, v3_ = -1;
@@ -827,6 +825,12 @@ __device__ __forceinline__ Rec tri_record(const KParams& P, const THit& h)
     r.tangent.y = f * (dV2 * ab.y - dV1 * ac.y);
     r.tangent.z = f * (dV2 * ab.z - dV1 * ac.z);
     return r;
+}
+
+__device__ __forceinline__ Rec tri_record(const KParams& P, const THit& h)
+{
+    const int id = P.tri_id[h.k];
+    return rec_of(P, load_gtri(P.tris + h.k), id, P.tri_mat[id], h);
 }
 
 // Sphere::intersect, analyticShape.cpp:9-60 (compute_uv forced true; reads a stale hit.t when delta>0 and t1>=t2)
@@ -1058,7 +1062,10 @@ __device__ void count_wave_steps(const KParams& P, int base, uint32_t steps)
 // BVH::intersect through the wide BVH and its certificate (wbvh.hpp).
 // Returns true with (h, r) = the reference's record and boolean when the query is
 // certified; false when it must be traced through the octree.
-__device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit& h, bool& r, uint2* lv)
+// rec (optional): on a certified hit, the record built from the wide BVH's own copies (the
+// triangle from wtris, index and material from wmeta), with no further dependent loads.
+__device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit& h, bool& r, uint2* lv,
+                                             Rec* rec = nullptr)
 {
     const float om = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
     WStackLds stk{lv};
@@ -1096,15 +1103,17 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
         atomicAdd(&P.counters[14], 1ull);   // the certificate's k-DOP test
 #endif
     if (st == W_HIT) {
-        // slot and octree leaf are independent loads: two round trips to the certificate
-        const int32_t slot = ldg(P.wslot + w.k);
-        const GNode leaf = load_gnode(P.nodes + ldg(P.wleaf + w.k));
+        // one 16-B load names the slot, the certificate's leaf, the index and the material
+        const uint4 M = ldg(P.wmeta + w.k);
+        const GNode leaf = load_gnode(P.nodes + M.y);
         if (kdop_certifies(leaf, o, d, w.t)) {
             h.t = w.t;
             h.u = w.u;
             h.v = w.v;
-            h.k = slot;
+            h.k = (int32_t)M.x;
             r = true;
+            if (rec)
+                *rec = rec_of(P, load_gtri(P.wtris + w.k), (int)M.z, (int)M.w, h);
             return true;
         }
     }
@@ -1156,7 +1165,7 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
     if (st == W_HIT && P.counters)
         atomicAdd(&P.counters[14], 1ull);
 #endif
-    if (st == W_HIT && kdop_certifies(load_gnode(P.nodes + ldg(P.wleaf + w.k)), o, d, w.t)) {
+    if (st == W_HIT && kdop_certifies(load_gnode(P.nodes + ldg(P.wmeta + w.k).y), o, d, w.t)) {
         v3 q = o + d * w.t;
         *sh = length2(p - q) < length2(p - lp);
         return true;
@@ -1324,7 +1333,13 @@ __device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv, ui
         THit h;
         bool r = false;
         const bool wide = !GRP && P.wnodes && P.nnodes > 0 && !ray_is_nan(o, d);
-        if (!(wide && wide_closest(P, o, d, h, r, lv))) {
+        if (wide && wide_closest(P, o, d, h, r, lv, &local)) {
+            // certified: a hit's record is already in local (a miss leaves it fresh)
+            if (r && (local.t < fin.t || fin.t == -1)) {
+                fin = local;
+                src = local.tri;
+            }
+        } else {
             if (wide && budget) {
                 *aborted = true;   // not certified: the deferred pass traces it through the octree
                 return -1;
@@ -1333,8 +1348,8 @@ __device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv, ui
             r = bvh_closest<false, GRP>(P, R, h, lv, budget, aborted);
             if (budget && *aborted)
                 return -1;
+            bvh_record(P, h, r, local, fin, src);
         }
-        bvh_record(P, h, r, local, fin, src);
     } else {
         TRay R = make_ray(P, o, d);
         // brute-force loop, renderer.cpp:1021-1027: fin takes every hit nearer

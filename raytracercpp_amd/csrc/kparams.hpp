@@ -59,8 +59,8 @@ struct KParams {
     // the wide BVH (wbvh.hpp; nullptr: off) -- closest-hit queries certified against the octree
     const WNode* wnodes;
     const GTri* wtris;           // octree records in wide-BVH leaf order
-    const int32_t* wslot;        // wide-BVH triangle -> octree GTri slot
-    const uint32_t* wleaf;       // wide-BVH triangle -> flattened octree leaf node (its certificate's k-DOP)
+    const uint4* wmeta;          // wide-BVH triangle k -> {octree GTri slot, flattened octree leaf node (its
+                                 // certificate's k-DOP), caller triangle index, material}
     int32_t nnodes;
     int32_t ntri_slots;       // GTri count (brute-force loop bound when enable_bvh == 0)
     int32_t levels;           // flattened tree depth + 1 (LDS level-stack entries per lane)

@@ -97,8 +97,8 @@ int Renderer::init(std::string& err)
     DevBuf* all[] = {&d_nodes_, &d_tris_,  &d_tri_id_, &d_tri_mat_, &d_tri_uv_, &d_mats_,   &d_internal_,
                      &d_image_, &d_rgba_,  &d_hit_id_, &d_hit_t_,   &d_shadow_, &d_counters_, &d_band_tmp_, &d_defer_,
                      &d_tri9_,  &d_rcount_, &d_roff_,  &d_pieces_,  &d_piece_uv_, &d_zkey_, &d_big_, &d_scan_tmp_,
-                     &d_zbuf_,  &d_nbuf_,   &d_ao_,     &d_cones_, &d_lslab_, &d_wnodes_, &d_wtris_, &d_wslot_,
-                     &d_wleaf_, &d_defer2_, &d_tile_sort_, &d_tile_sort_tmp_, &d_dbg_, &d_prim_};
+                     &d_zbuf_,  &d_nbuf_,   &d_ao_,     &d_cones_, &d_lslab_, &d_wnodes_, &d_wtris_, &d_wmeta_,
+                     &d_defer2_, &d_tile_sort_, &d_tile_sort_tmp_, &d_dbg_, &d_prim_};
     for (DevBuf* b : all) b->device = device_;
     for (auto& b : d_tex_) b.device = device_;
     for (auto& b : d_sky_) b.device = device_;
@@ -531,17 +531,27 @@ int Renderer::ensure_device_scene()
         else
             wb_ = WBvh();
         if (!wb_.nodes.empty()) {
+            // per wide-BVH triangle, everything a certified hit needs in one 16-B load: the
+            // octree slot (the record's triangle), the leaf of its certificate, the caller's
+            // triangle index and its material
+            const size_t nk = wb_.slot.size();
+            wmeta_.resize(4 * nk);
+            for (size_t k = 0; k < nk; k++) {
+                const int32_t slot = wb_.slot[k];
+                const int32_t id = oct_.tri_id[(size_t)slot];
+                wmeta_[4 * k + 0] = (uint32_t)slot;
+                wmeta_[4 * k + 1] = wb_.leaf_of_k[k];
+                wmeta_[4 * k + 2] = (uint32_t)id;
+                wmeta_[4 * k + 3] = (uint32_t)tri_mat_[(size_t)id];
+            }
             size_t wn = wb_.nodes.size() * sizeof(WNode), wt = wb_.tris.size() * sizeof(GTri);
             if ((e = d_wnodes_.reserve(wn)) != hipSuccess || (e = d_wtris_.reserve(wt)) != hipSuccess ||
-                (e = d_wslot_.reserve(wb_.slot.size() * 4)) != hipSuccess ||
-                (e = d_wleaf_.reserve(wb_.leaf_of_k.size() * 4)) != hipSuccess)
+                (e = d_wmeta_.reserve(wmeta_.size() * 4)) != hipSuccess)
                 return hip_fail(e, "hipMalloc (wide BVH)");
             if ((e = hipMemcpyAsync(d_wnodes_.p, wb_.nodes.data(), wn, hipMemcpyHostToDevice, stream_)) != hipSuccess ||
                 (e = hipMemcpyAsync(d_wtris_.p, wb_.tris.data(), wt, hipMemcpyHostToDevice, stream_)) != hipSuccess ||
-                (e = hipMemcpyAsync(d_wslot_.p, wb_.slot.data(), wb_.slot.size() * 4, hipMemcpyHostToDevice,
-                                    stream_)) != hipSuccess ||
-                (e = hipMemcpyAsync(d_wleaf_.p, wb_.leaf_of_k.data(), wb_.leaf_of_k.size() * 4,
-                                    hipMemcpyHostToDevice, stream_)) != hipSuccess)
+                (e = hipMemcpyAsync(d_wmeta_.p, wmeta_.data(), wmeta_.size() * 4, hipMemcpyHostToDevice, stream_)) !=
+                    hipSuccess)
                 return hip_fail(e, "upload (wide BVH)");
         }
         size_t nb = oct_.nodes.size() * sizeof(GNode), tb = oct_.tris.size() * sizeof(GTri);
@@ -667,8 +677,7 @@ void Renderer::fill_params(KParams& P) const
     if (!wb_.nodes.empty() && !(wenv && wenv[0] == '0') && P.scene_scale > 0x1p-20f && P.scene_scale < 0x1p20f) {
         P.wnodes = d_wnodes_.as<WNode>();
         P.wtris = d_wtris_.as<GTri>();
-        P.wslot = d_wslot_.as<int32_t>();
-        P.wleaf = d_wleaf_.as<uint32_t>();
+        P.wmeta = d_wmeta_.as<uint4>();
     }
     P.nnodes = (int32_t)oct_.nodes.size();
     P.ntri_slots = (int32_t)oct_.tris.size();

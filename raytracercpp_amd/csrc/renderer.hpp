@@ -158,7 +158,8 @@ private:
     DevBuf d_lslab_;
     // the wide BVH (wbvh.hpp): nodes, triangle records in its leaf order, slot maps
     WBvh wb_;
-    DevBuf d_wnodes_, d_wtris_, d_wslot_, d_wleaf_, d_defer2_;
+    DevBuf d_wnodes_, d_wtris_, d_wmeta_, d_defer2_;
+    std::vector<uint32_t> wmeta_;   // host copy of KParams::wmeta (4 words per wide-BVH triangle)
     DevBuf d_tile_sort_, d_tile_sort_tmp_;   // tile probe costs, sort keys, sorted order; radix-sort scratch
     DevBuf d_dbg_;                           // diagnostic per-wave records (RT_DEBUG_WAVES)
     DevBuf d_prim_;                          // split frame: the primary pass's records (PrimRec per pixel)
