@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--band-rows", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="frames in flight: consecutive steps alternate over this many streams (DESIGN.md 7)")
     return ap.parse_args()
 
 
@@ -53,7 +55,7 @@ def main():
     import torch.distributed as dist
     from raytracercpp_amd import scenes
     from raytracercpp_amd.renderer import Renderer
-    from raytracercpp_amd.strips import assemble_torch
+    from raytracercpp_amd.strips import FramePipeline, assemble_torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -72,30 +74,33 @@ def main():
     rw, rh = st.render_size()
     band = args.band_rows
     nloc = r.local_rows(band, rank, world)
-    out = torch.empty((nloc, W), dtype=torch.int32, device=dev)
-    parts = [torch.empty_like(out) for _ in range(world)] if world > 1 else [out]
-    stream = torch.cuda.current_stream(dev)
-
-    def step():
-        r.render_bands_device(band, rank, world, out.data_ptr(), stream.cuda_stream)
-        if world > 1:
-            dist.all_gather(parts, out)
+    # Frames in flight: step i renders on stream i % q into its own output
+    # buffer, and its all-gather is enqueued asynchronously behind it, so the next frame's
+    # kernel fills the CUs that this frame's tail leaves idle and the gather overlaps it.
+    # Before a slot is reused its previous gather has finished reading the buffer (wait).
+    q = max(1, args.inflight)
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(q - 1)]
+    outs = [torch.empty((nloc, W), dtype=torch.int32, device=dev) for _ in range(q)]
+    pipe = FramePipeline(lambda o, s: r.render_bands_device(band, rank, world, o.data_ptr(), s.cuda_stream),
+                         outs, world, streams, dist)
+    step, drain = pipe.step, pipe.drain
 
     t_build0 = time.perf_counter()
     step()   # first call builds + uploads the octree
-    torch.cuda.synchronize()
+    drain()
     t_first = time.perf_counter() - t_build0
     shadow_local, refl_local = r.band_counters()
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    drain()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    last = 0
     for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
+        last = step()
+    drain()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -116,7 +121,7 @@ def main():
     else:
         elapsed_max, shadow_total, k_mean_max, refl_total = elapsed, int(shadow_local), k_mean, int(refl_local)
     c5 = args.config == "sphere1m_refl"
-    frame = assemble_torch(parts, H, band) if rank == 0 else None
+    frame = assemble_torch(pipe.parts[last], H, band) if rank == 0 else None
 
     if rank == 0:
         primary = rw * rh
@@ -144,7 +149,8 @@ def main():
                                     "C4 sphere1m: 1,000,000 tris, 1920x1080, ssaa_factor 2 (3840x2160 rays), "
                                     "primary + shadow, octree 12/40"), "image": [W, H], "render": [rw, rh],
                        "rays_per_frame": rays, "primary_rays": primary, "shadow_rays": shadow_total,
-                       "reflection_rays": refl_total, "band_rows": band, "parallelism": f"image strips x{world}"},
+                       "reflection_rays": refl_total, "band_rows": band, "parallelism": f"image strips x{world}",
+                       "frames_in_flight": q},
             "kernel_ms": round(k_mean_max, 4),
             "first_call_s": round(t_first, 3),
         }

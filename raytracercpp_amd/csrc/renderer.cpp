@@ -95,7 +95,7 @@ int Renderer::init(std::string& err)
         return RT_EHIP;
     }
     DevBuf* all[] = {&d_nodes_, &d_tris_,  &d_tri_id_, &d_tri_mat_, &d_tri_uv_, &d_mats_,   &d_internal_,
-                     &d_image_, &d_rgba_,  &d_hit_id_, &d_hit_t_,   &d_shadow_, &d_counters_, &d_band_tmp_, &d_defer_,
+                     &d_image_, &d_rgba_,  &d_hit_id_, &d_hit_t_,   &d_shadow_, &d_counters_, &d_defer_,
                      &d_tri9_,  &d_rcount_, &d_roff_,  &d_pieces_,  &d_piece_uv_, &d_zkey_, &d_big_, &d_scan_tmp_,
                      &d_zbuf_,  &d_nbuf_,   &d_ao_,     &d_cones_, &d_lslab_, &d_wnodes_, &d_wtris_, &d_wmeta_,
                      &d_defer2_, &d_tile_sort_, &d_tile_sort_tmp_, &d_dbg_, &d_prim_};
@@ -184,6 +184,14 @@ int Renderer::set_triangles(const float* tri9, const int32_t* mat, const float* 
         return fail(RT_EUNSUPPORTED, "set_triangles: more than 2^30 triangles");
     tri_.assign(tri9, tri9 + 9 * n);
     tri_mat_.assign(mat, mat + n);
+    // the material range, checked by validate() before every launch without re-reading
+    // the per-triangle indices (a 1M-triangle scan per frame cost ~0.2 ms of host time)
+    tri_mat_lo_ = INT32_MAX;
+    tri_mat_hi_ = INT32_MIN;
+    for (int32_t m : tri_mat_) {
+        tri_mat_lo_ = std::min(tri_mat_lo_, m);
+        tri_mat_hi_ = std::max(tri_mat_hi_, m);
+    }
     if (uv6)
         tri_uv_.assign(uv6, uv6 + 6 * n);
     else
@@ -220,6 +228,8 @@ int Renderer::clear_geometry()
 {
     tri_.clear();
     tri_mat_.clear();
+    tri_mat_lo_ = INT32_MAX;
+    tri_mat_hi_ = INT32_MIN;
     tri_uv_.clear();
     shape_kind_.clear();
     shape_.clear();
@@ -619,9 +629,8 @@ int Renderer::validate() const
             return RT_EUNSUPPORTED;
     int nmat = material_count();
     if (s_.shading_method == RT_SHADING) {
-        for (int32_t m : tri_mat_)
-            if (m < 0 || m >= nmat)
-                return RT_EINVAL;
+        if (!tri_mat_.empty() && (tri_mat_lo_ < 0 || tri_mat_hi_ >= nmat))
+            return RT_EINVAL;
         for (int32_t m : shape_mat_)
             if (m < 0 || m >= nmat)
                 return RT_EINVAL;
@@ -1380,6 +1389,31 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
     KParams P;
     fill_params(P);
     last_seg_ = P.seg_scale;
+    hipError_t e;
+    // The stream's slot: its own tile-queue counters and SSAA band buffer, so that frames
+    // launched on different streams may run concurrently (the tail of one frame overlaps
+    // the next; same-stream launches are ordered by the stream).  Only the default trace
+    // path keeps all of its per-launch state in the slot: the reflection engine, the raster
+    // path and the opt-in modes (octree deferral, split / lean frames, tile order) share
+    // buffers across launches, so a launch on another stream first waits for the last one.
+    int si = -1;
+    for (int i = 0; i < band_nslots_; i++)
+        if (band_slot_[i].stream == stream) si = i;
+    if (si < 0) {
+        if (band_nslots_ == BAND_SLOTS)
+            return fail(RT_EINVAL, "render_bands_device: more than 8 distinct streams");
+        si = band_nslots_++;
+        band_slot_[si].stream = stream;
+        band_slot_[si].counters.device = band_slot_[si].tmp.device = device_;
+    }
+    auto env_on = [](const char* k) { const char* v = getenv(k); return v && v[0] == '1'; };
+    const bool slot_only = !P.has_reflection && !s_.hybrid_rasterization_tracing && P.wnodes && !P.pipeline &&
+                           !env_on("RT_SPLIT") && !env_on("RT_WIDE_LEAN") && !env_on("RT_TILE_ORDER");
+    if (!slot_only && band_last_ >= 0 && band_last_ != si &&
+        (e = hipStreamSynchronize(band_slot_[band_last_].stream)) != hipSuccess)
+        return hip_fail(e, "render_bands_device: previous launch");
+    BandSlot& S = band_slot_[si];
+    band_last_ = si;
     int f = s_.enable_ssaa ? s_.ssaa_factor : 1;
     P.band_rows = band_rows * f;
     P.nranks = nranks;
@@ -1387,22 +1421,21 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
     P.local_rows = lrows * f;
     P.tiles_x = (P.rw + 7) / 8;
     P.tiles_y = (P.local_rows + 7) / 8;
-    hipError_t e;
-    if ((e = d_counters_.reserve(NCOUNTER_WORDS * 8)) != hipSuccess) return hip_fail(e, "hipMalloc (counters)");
+    if ((e = S.counters.reserve(NCOUNTER_WORDS * 8)) != hipSuccess) return hip_fail(e, "hipMalloc (counters)");
     uint32_t* target = d_out;
     if (f > 1) {
-        if ((e = d_band_tmp_.reserve((size_t)P.rw * P.local_rows * 4)) != hipSuccess)
+        if ((e = S.tmp.reserve((size_t)P.rw * P.local_rows * 4)) != hipSuccess)
             return hip_fail(e, "hipMalloc (band)");
-        target = d_band_tmp_.as<uint32_t>();
+        target = S.tmp.as<uint32_t>();
     }
     P.argb = target;
-    P.counters = d_counters_.as<unsigned long long>();
+    P.counters = S.counters.as<unsigned long long>();
     if (ring_.empty()) {
         ring_.resize(2 * EV_RING, nullptr);
         for (auto& ev : ring_)
             if ((e = hipEventCreate(&ev)) != hipSuccess) return hip_fail(e, "hipEventCreate");
     }
-    if ((e = hipMemsetAsync(d_counters_.p, 0, NCOUNTER_WORDS * 8, stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+    if ((e = hipMemsetAsync(S.counters.p, 0, NCOUNTER_WORDS * 8, stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
     hipEventRecord(ring_[2 * ring_next_], stream);
     if ((rc = launch_frame(P, stream)) != RT_OK) return rc;
     hipEventRecord(ring_[2 * ring_next_ + 1], stream);
@@ -1474,8 +1507,11 @@ int Renderer::band_counters(unsigned long long out[2])
 {
     hipSetDevice(device_);
     unsigned long long cnt[NCOUNTERS] = {};
+    if (band_last_ < 0)
+        return fail(RT_ESTATE, "band_counters: no render_bands_device launch yet");
     hipError_t e = hipDeviceSynchronize();
-    if (e == hipSuccess) e = hipMemcpy(cnt, d_counters_.p, sizeof(cnt), hipMemcpyDeviceToHost);
+    if (e == hipSuccess)
+        e = hipMemcpy(cnt, band_slot_[band_last_].counters.p, sizeof(cnt), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return hip_fail(e, "band_counters");
     out[0] = cnt[0];
     out[1] = cnt[1];

@@ -128,6 +128,7 @@ private:
     // scene (host copies; the reference Renderer copies its inputs too)
     std::vector<float> tri_;
     std::vector<int32_t> tri_mat_;
+    int32_t tri_mat_lo_ = INT32_MAX, tri_mat_hi_ = INT32_MIN;   // range of tri_mat_
     std::vector<float> tri_uv_;
     std::vector<int32_t> shape_kind_;
     std::vector<float> shape_;
@@ -147,7 +148,7 @@ private:
     bool geom_dirty_ = true, mats_dirty_ = true, tex_dirty_ = true;
     DevBuf d_nodes_, d_tris_, d_tri_id_, d_tri_mat_, d_tri_uv_, d_mats_;
     DevBuf d_tex_[TEX_SLOTS], d_sky_[6];
-    DevBuf d_internal_, d_image_, d_rgba_, d_hit_id_, d_hit_t_, d_shadow_, d_counters_, d_band_tmp_, d_defer_;
+    DevBuf d_internal_, d_image_, d_rgba_, d_hit_id_, d_hit_t_, d_shadow_, d_counters_, d_defer_;
     // SSAO: _z_buffer, _normal_buffer (float4) and the occlusion counts of the internal image
     DevBuf d_zbuf_, d_nbuf_, d_ao_;
     // leaf normal cones, [4] per GTri slot (renderer.cpp leaf_cones)
@@ -182,6 +183,15 @@ private:
     static constexpr int REFL_LEVELS = 18;   // max_recursion_depth <= 15: frames at levels 1..16, +1 child slot
     ReflLevel refl_[REFL_LEVELS];
 
+    // render_bands_device: per-stream tile-queue counters and SSAA band buffers, so that
+    // frames launched on different streams can be in flight together
+    struct BandSlot {
+        hipStream_t stream = nullptr;
+        DevBuf counters, tmp;
+    };
+    static constexpr int BAND_SLOTS = 8;
+    BandSlot band_slot_[BAND_SLOTS];
+    int band_nslots_ = 0, band_last_ = -1;
     // event ring for render_bands_device kernel timing
     static constexpr int EV_RING = 256;
     std::vector<hipEvent_t> ring_;

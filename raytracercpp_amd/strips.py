@@ -54,3 +54,58 @@ def assemble_torch(parts, image_h: int, band_rows: int):
         keep = g >= 0
         out[g[keep]] = p[keep]
     return out
+
+
+class FramePipeline:
+    """Frames in flight over ``q`` slots.
+
+    Step i uses slot i % q: its stream, its output buffer and its gather buffers.  The
+    render is enqueued on the slot's stream and the all-gather of the slot's strips is
+    enqueued asynchronously behind it, so frame i's gather and tail overlap frame i+1's
+    render on the other stream.  A slot is reused only after its previous gather has
+    finished reading the buffer (``work.wait()``, which on a GPU makes the slot's stream
+    wait and on CPU blocks).  ``render(out, stream)`` writes one rank's strips into ``out``.
+    With ``streams=None`` (CPU / gloo) everything runs on the host in order.
+    """
+
+    def __init__(self, render, outs, world: int, streams=None, dist=None):
+        self.render = render
+        self.outs = outs
+        self.q = len(outs)
+        self.world = world
+        self.streams = streams
+        self.dist = dist
+        self.parts = [[o.new_empty(o.shape) for _ in range(world)] if world > 1 else [o] for o in outs]
+        self.works = [None] * self.q
+        self.count = 0
+
+    def _ctx(self, i):
+        import contextlib
+        if self.streams is None:
+            return contextlib.nullcontext()
+        import torch
+        return torch.cuda.stream(self.streams[i])
+
+    def step(self) -> int:
+        """Enqueue one frame; returns its slot."""
+        i = self.count % self.q
+        self.count += 1
+        with self._ctx(i):
+            if self.works[i] is not None:
+                self.works[i].wait()
+                self.works[i] = None
+            self.render(self.outs[i], None if self.streams is None else self.streams[i])
+            if self.world > 1:
+                self.works[i] = self.dist.all_gather(self.parts[i], self.outs[i], async_op=True)
+        return i
+
+    def drain(self):
+        """Wait for every enqueued frame and gather."""
+        for i in range(self.q):
+            if self.works[i] is not None:
+                with self._ctx(i):
+                    self.works[i].wait()
+                self.works[i] = None
+        if self.streams is not None:
+            import torch
+            torch.cuda.synchronize()

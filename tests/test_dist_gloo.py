@@ -69,3 +69,66 @@ def test_gloo_strips_equal_single_process(world, band):
     full = Oracle(sc, st).render_rows()
     ref = Oracle.downscale(full.argb, rw, rh, 2).reshape(st.image_height, st.image_width)
     assert np.array_equal(img, ref)
+
+
+def _pipe_worker(rank, world, port, nslots, nframes, q):
+    """FramePipeline over gloo: frame k's strips of rank r hold (k, r, local row); every
+    frame's gathered parts must be that frame's, in rank order, although the next
+    frames are enqueued before it is read (slots are reused only after their gather)."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import torch
+    import torch.distributed as dist
+    from raytracercpp_amd.strips import FramePipeline
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    frame = [0]
+
+    def render(out, stream):
+        assert stream is None
+        rows = torch.arange(out.shape[0], dtype=torch.int32).unsqueeze(1)
+        out.copy_((frame[0] * 1000 + rank * 100 + rows).expand_as(out))
+        frame[0] += 1
+
+    outs = [torch.zeros((5, 7), dtype=torch.int32) for _ in range(nslots)]
+    pipe = FramePipeline(render, outs, world, None, dist)
+    seen = []
+    for k in range(nframes):
+        slot = pipe.step()
+        if k >= nslots - 1:   # the frame enqueued nslots-1 steps ago has its gather in flight
+            old = (slot + 1) % nslots
+            if pipe.works[old] is not None:
+                pipe.works[old].wait()
+                pipe.works[old] = None
+            seen.append([p.clone() for p in pipe.parts[old]])
+    pipe.drain()
+    ok = len(seen) == nframes - (nslots - 1)
+    for k, parts in enumerate(seen):   # seen[k] was read at step k + nslots - 1: frame k
+        for r, p in enumerate(parts):
+            rows = torch.arange(5, dtype=torch.int32).unsqueeze(1)
+            ok &= bool(torch.equal(p, (k * 1000 + r * 100 + rows).expand(5, 7)))
+    last = (nframes - 1) % nslots
+    for r, p in enumerate(pipe.parts[last]):
+        rows = torch.arange(5, dtype=torch.int32).unsqueeze(1)
+        ok &= bool(torch.equal(p, ((nframes - 1) * 1000 + r * 100 + rows).expand(5, 7)))
+    q.put((rank, ok))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("nslots", [1, 2, 3])
+def test_gloo_frame_pipeline(nslots):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, nslots, 7, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    assert all(ok for _, ok in res), res

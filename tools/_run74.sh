@@ -1,0 +1,4 @@
+set -u
+mkdir -p gpurun_out
+timeout -k 10 300 python tools/strip_scaling.py --ranks 1 2 4 8 16 135 > gpurun_out/r02_strips74.log 2>&1 || { cat gpurun_out/r02_strips74.log; exit 1; }
+cat gpurun_out/r02_strips74.log

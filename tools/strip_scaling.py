@@ -1,0 +1,81 @@
+"""Strip-scaling probe on ONE GPU: per-step time of one rank's share of the C4 frame.
+
+For each N in --ranks, renders rank r's bands (render_bands_device(band, r, N)) K times
+back to back on one stream and reports the step time (wall clock over K async steps),
+the mean ray_trace_kernel time (HIP events) and the implied N-GPU throughput bound
+(frame rays / slowest rank's step time), i.e. the strip path without the gather.
+Usage (GPU box): python tools/strip_scaling.py [--ranks 1 2 4 8] [--steps 50]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ranks", type=int, nargs="+", default=[1, 2, 4, 8])
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--band-rows", type=int, default=8)
+    ap.add_argument("--config", default="sphere1m")
+    ap.add_argument("--all-ranks", action="store_true", help="time every rank of each N (default: rank 0 and N-1)")
+    ap.add_argument("--inflight", type=int, nargs="+", default=[1],
+                    help="frames in flight: consecutive steps alternate over this many streams")
+    args = ap.parse_args()
+    import torch
+    from raytracercpp_amd import scenes
+    from raytracercpp_amd.renderer import Renderer
+
+    sc, st = scenes.CONFIGS[args.config]()
+    r = Renderer(0)
+    r.load_scene(sc, st)
+    W = st.image_width
+    rw, rh = st.render_size()
+    band = args.band_rows
+    res = []
+    for q in args.inflight:
+        streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(q - 1)]
+        for n in args.ranks:
+            ranks = range(n) if args.all_ranks else sorted({0, n - 1})
+            for rank in ranks:
+                nloc = r.local_rows(band, rank, n)
+                outs = [torch.empty((nloc, W), dtype=torch.int32, device="cuda") for _ in range(q)]
+
+                def step(i):
+                    r.render_bands_device(band, rank, n, outs[i % q].data_ptr(), streams[i % q].cuda_stream)
+
+                for i in range(args.warmup):
+                    step(i)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for i in range(args.steps):
+                    step(i)
+                th = (time.perf_counter() - t0) / args.steps   # host time per enqueued step
+                torch.cuda.synchronize()
+                dt = (time.perf_counter() - t0) / args.steps
+                k = float(np.mean(r.kernel_times(args.steps)))
+                shadow, _ = r.band_counters()
+                rec = {"inflight": q, "N": n, "rank": rank, "step_ms": round(dt * 1e3, 4), "kernel_ms": round(k, 4),
+                       "overhead_ms": round(dt * 1e3 - k, 4), "host_ms": round(th * 1e3, 4), "local_rows": nloc,
+                       "shadow_rays": shadow}
+                res.append(rec)
+                print(json.dumps(rec), flush=True)
+    for q in args.inflight:
+        base = [x for x in res if x["N"] == 1 and x["inflight"] == 1]
+        if base:
+            b = base[0]["step_ms"]
+            for n in args.ranks:
+                worst = max(x["step_ms"] for x in res if x["N"] == n and x["inflight"] == q)
+                print(json.dumps({"inflight": q, "N": n, "bound_speedup_no_gather": round(b / worst, 3)}), flush=True)
+
+if __name__ == "__main__":
+    main()
