@@ -1982,6 +1982,32 @@ __global__ __launch_bounds__(BLOCK) void tile_key_kernel(KParams P, const uint32
     keys[tile] = ((TILE_COST_MAX - c) << TILE_ID_BITS) | (uint32_t)tile;
 }
 
+// ImageUtils::downscale_image_qt_ARGB32 (imageUtils.h:98-147) fused into the tile: the
+// wave holds its 8x8 tile's ARGB values one per lane (lane = 8 * row + column), every
+// lane active; the f x f blocks (f = 1 << P.ds_shift, f | 8, rows f-aligned in the band)
+// are summed per 8-bit channel across lanes, divided by f * f with truncation (the sums
+// are non-negative: a shift) and written by the block's first lane, as downscale_kernel.
+__device__ __forceinline__ void downscale_tile(const KParams& P, int lane, int lr, int px, uint32_t c)
+{
+    int r = (int)((c >> 16) & 0xffu), g = (int)((c >> 8) & 0xffu), b = (int)(c & 0xffu);
+    const int f = 1 << P.ds_shift;
+    for (int m = 1; m < f; m <<= 1) {   // columns, within the lane's row of 8
+        r += __shfl_xor(r, m);
+        g += __shfl_xor(g, m);
+        b += __shfl_xor(b, m);
+    }
+    for (int m = 8; m < 8 * f; m <<= 1) {   // rows
+        r += __shfl_xor(r, m);
+        g += __shfl_xor(g, m);
+        b += __shfl_xor(b, m);
+    }
+    if ((lane & (f - 1)) == 0 && ((lane >> 3) & (f - 1)) == 0) {
+        const int s2 = 2 * P.ds_shift;
+        P.ds_out[(size_t)(lr >> P.ds_shift) * (size_t)(P.rw >> P.ds_shift) + (size_t)(px >> P.ds_shift)] =
+            qrgb(r >> s2, g >> s2, b >> s2);
+    }
+}
+
 // Renderer::ray_trace (renderer.cpp:1068-1116): one lane per pixel, one wave
 // per 8x8 tile.  Waves are persistent and pull tiles from the sharded device-scope
 // queue (tile_queue_next): shadow-ray-heavy tiles cluster around the object, so
@@ -2059,6 +2085,7 @@ __global__ __launch_bounds__(BLOCK, PLAIN ? RT_OCC_PLAIN : RT_OCC) void ray_trac
         }
 
         if (P.argb) P.argb[o] = color_to_argb(po.color);
+        if (!REFL && P.ds_out) downscale_tile(P, lane, lr, px, color_to_argb(po.color));
         if (P.rgba) P.rgba[o] = make_float4(po.color.r, po.color.g, po.color.b, po.alpha);
         if (P.hit_id) P.hit_id[o] = po.found ? po.src : -1;
 #if RT_TILE_TIME

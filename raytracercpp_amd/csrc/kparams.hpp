@@ -143,6 +143,11 @@ struct KParams {
     // SSAO inputs (enable_ssao): Renderer::_z_buffer / _normal_buffer, renderer.cpp:1107-1110, 975-979
     float* zbuf;
     float4* nbuf;
+    // fused SSAA downscale (band launches, ssaa_factor 2 / 4 / 8): each wave box-filters its
+    // 8x8 tile's ARGB values across lanes and writes the (8 / f)^2 output pixels to ds_out
+    // (local output row lr / f, width rw / f); argb is then nullptr.  nullptr: off.
+    uint32_t* ds_out;
+    int32_t ds_shift;         // log2(ssaa_factor)
 };
 
 // ---- SSAO (kernels.hip "Renderer::post_process_ssao_SIMD") ----

@@ -1422,13 +1422,24 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
     P.tiles_x = (P.rw + 7) / 8;
     P.tiles_y = (P.local_rows + 7) / 8;
     if ((e = S.counters.reserve(NCOUNTER_WORDS * 8)) != hipSuccess) return hip_fail(e, "hipMalloc (counters)");
+    // SSAA fused into the trace kernel's tiles (kernels.hip downscale_tile) when every lane
+    // of every tile holds a pixel (no padding, no deferred pixels) and f divides the 8x8
+    // tile; otherwise the band is rendered at full size and downscale_kernel filters it.
+    // RT_FUSED_SSAA=0 keeps the separate pass.
+    const char* fz = getenv("RT_FUSED_SSAA");
+    const bool fused = (f == 2 || f == 4 || f == 8) && slot_only && !(fz && fz[0] == '0') && P.rw % 8 == 0 &&
+                       P.local_rows % 8 == 0;
     uint32_t* target = d_out;
-    if (f > 1) {
+    if (f > 1 && !fused) {
         if ((e = S.tmp.reserve((size_t)P.rw * P.local_rows * 4)) != hipSuccess)
             return hip_fail(e, "hipMalloc (band)");
         target = S.tmp.as<uint32_t>();
     }
-    P.argb = target;
+    P.argb = fused ? nullptr : target;
+    if (fused) {
+        P.ds_out = d_out;
+        P.ds_shift = f == 2 ? 1 : (f == 4 ? 2 : 3);
+    }
     P.counters = S.counters.as<unsigned long long>();
     if (ring_.empty()) {
         ring_.resize(2 * EV_RING, nullptr);
@@ -1441,7 +1452,7 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
     hipEventRecord(ring_[2 * ring_next_ + 1], stream);
     ring_next_ = (ring_next_ + 1) % EV_RING;
     if (ring_count_ < EV_RING) ring_count_++;
-    if (f > 1 && (e = rt_launch_downscale(target, P.rw, P.local_rows, f, d_out, stream)) != hipSuccess)
+    if (f > 1 && !fused && (e = rt_launch_downscale(target, P.rw, P.local_rows, f, d_out, stream)) != hipSuccess)
         return hip_fail(e, "downscale launch");
     return RT_OK;
 }

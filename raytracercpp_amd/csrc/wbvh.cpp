@@ -320,7 +320,7 @@ WNode quantise(const Box* cb, const uint32_t* link, int nc, const ChildGeom* cg,
         }
         w.exps |= (uint32_t)(127 + k) << (8 * a);
         const double st = std::ldexp(1.0, k);
-        for (int j = 0; j < 4; j++) {
+        for (int j = 0; j < W_WIDTH; j++) {
             if (j >= nc) {
                 w.qlo[a][j] = 0;
                 w.qhi[a][j] = 0;
@@ -332,13 +332,13 @@ WNode quantise(const Box* cb, const uint32_t* link, int nc, const ChildGeom* cg,
             w.qhi[a][j] = (uint8_t)std::max(0.0, std::min(255.0, hi));
         }
     }
-    for (int j = 0; j < 4; j++)
+    for (int j = 0; j < W_WIDTH; j++)
         w.child[j] = link[j];
 #if RT_W_SLAB
     // slabs: N_j = round(127 n / |n|) (integer), range of N_j . (v - origin) over the vertices
     // in double (exact: integer N, float vertices and origin), quantised outward on 16 bits
-    double smin[4], smax[4];
-    int nq[4][3];
+    double smin[W_WIDTH], smax[W_WIDTH];
+    int nq[W_WIDTH][3];
     double lo_all = INFINITY, hi_all = -INFINITY;
     for (int j = 0; j < nc; j++) {
         const ChildGeom& g = cg[j];
@@ -378,7 +378,7 @@ WNode quantise(const Box* cb, const uint32_t* link, int nc, const ChildGeom* cg,
     const double st = std::ldexp(1.0, k);
     w.s = (float)st;
     w.slo = slo;
-    for (int j = 0; j < 4; j++) {
+    for (int j = 0; j < W_WIDTH; j++) {
         if (j >= nc) {
             w.nrm[j] = 0;
             w.slab[j] = 0;
@@ -426,7 +426,7 @@ struct Collapser {
     uint32_t emit(int32_t bi, int depth)
     {
         max_depth = std::max<int64_t>(max_depth, depth);
-        int32_t c[4];
+        int32_t c[W_WIDTH];
         int nc = 0;
         const BNode& N = bn[(size_t)bi];
         if (N.left < 0)
@@ -434,7 +434,7 @@ struct Collapser {
         else {
             c[nc++] = N.left;
             c[nc++] = N.right;
-            while (nc < 4) {
+            while (nc < W_WIDTH) {
                 int pick = -1;
                 float pa = -1.0f;
                 for (int j = 0; j < nc; j++) {
@@ -453,9 +453,9 @@ struct Collapser {
         }
         const uint32_t me = (uint32_t)out.nodes.size();
         out.nodes.emplace_back();
-        Box cb[4];
-        uint32_t link[4];
-        for (int j = 0; j < 4; j++) {
+        Box cb[W_WIDTH];
+        uint32_t link[W_WIDTH];
+        for (int j = 0; j < W_WIDTH; j++) {
             cb[j] = empty_box();
             link[j] = W_EMPTY;
         }
@@ -469,7 +469,7 @@ struct Collapser {
             } else
                 link[j] = emit(c[j], depth + 1);
         }
-        ChildGeom cg[4];
+        ChildGeom cg[W_WIDTH];
         for (int j = 0; j < nc; j++) {
             const BNode& C = bn[(size_t)c[j]];
             cg[j].idx = idx.data();
@@ -575,7 +575,7 @@ int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)
         uint32_t ref;
         Box box;
         int np;
-        uint32_t path[MAXP];   // node << 2 | child of every inner node on the way
+        uint32_t path[MAXP];   // node << 3 | child of every inner node on the way
     };
     std::vector<Item> stack;
     Box all = {{-INFINITY, -INFINITY, -INFINITY}, {INFINITY, INFINITY, INFINITY}};
@@ -609,8 +609,8 @@ int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)
 #if RT_W_SLAB
                 const GTri& T = w.tris[k];
                 for (int q = 0; q < it.np; q++) {
-                    const WNode& N = w.nodes[it.path[q] >> 2];
-                    const int j = (int)(it.path[q] & 3u);
+                    const WNode& N = w.nodes[it.path[q] >> 3];
+                    const int j = (int)(it.path[q] & 7u);
                     const double org[3] = {N.ox, N.oy, N.oz};
                     const double nv[3] = {(double)(int8_t)(N.nrm[j] & 0xffu), (double)(int8_t)((N.nrm[j] >> 8) & 0xffu),
                                           (double)(int8_t)((N.nrm[j] >> 16) & 0xffu)};
@@ -648,7 +648,7 @@ int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)
             continue;
         }
         const WNode& N = w.nodes[it.ref];
-        for (int j = 0; j < 4; j++) {
+        for (int j = 0; j < W_WIDTH; j++) {
             if (N.child[j] == W_EMPTY)
                 continue;
             double lo[3], hi[3];
@@ -666,7 +666,7 @@ int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)
                 bad++;
                 continue;
             }
-            ch.path[ch.np++] = (it.ref << 2) | (uint32_t)j;
+            ch.path[ch.np++] = (it.ref << 3) | (uint32_t)j;
             stack.push_back(ch);
         }
     }

@@ -52,6 +52,11 @@ constexpr int W_MAX_LEAF = 8;
 #define RT_W_STACK 12
 #endif
 constexpr int W_STACK = RT_W_STACK;
+#ifndef RT_W_WIDTH
+#define RT_W_WIDTH 4   // children per node: 4 or 8
+#endif
+constexpr int W_WIDTH = RT_W_WIDTH;
+static_assert(W_WIDTH == 4 || W_WIDTH == 8, "W_WIDTH");
 #ifndef RT_W_SCHED_BARRIER
 #define RT_W_SCHED_BARRIER 1
 #endif
@@ -77,8 +82,8 @@ constexpr double W_CONE_EPS = 1e-4;
 struct alignas(16) WNode {
     float ox, oy, oz;
     uint32_t exps;        // byte a: biased exponent (127 + k) of the step 2^k along axis a
-    uint8_t qlo[3][4];    // [axis][child]
-    uint8_t qhi[3][4];
+    uint8_t qlo[3][W_WIDTH];    // [axis][child]
+    uint8_t qhi[3][W_WIDTH];
 #if RT_W_SLAB
     // Orientation slab of child j: every vertex v below it has
     //   slo + q0 s  <=  N_j . (v - origin)  <=  slo + q1 s,
@@ -91,14 +96,26 @@ struct alignas(16) WNode {
     //   N_j . d  >  c * W_CONE_STEP * |d|
     // (the test rejects it on Mdet <= 0 before anything else), so such a ray skips j.
     float s, slo;
-    uint32_t nrm[4];
-    uint32_t slab[4];
-#else
+#if RT_W_WIDTH == 8
     uint32_t pad[2];
 #endif
-    uint32_t child[4];
+    uint32_t nrm[W_WIDTH];
+    uint32_t slab[W_WIDTH];
+#elif RT_W_WIDTH == 4
+    uint32_t pad[2];
+#endif
+    uint32_t child[W_WIDTH];
 };
-static_assert(sizeof(WNode) == (RT_W_SLAB ? 96 : 64), "WNode size");
+// 4-wide: 96 B (64 B without slabs); 8-wide: 176 B (96 B)
+static_assert(sizeof(WNode) == (W_WIDTH == 4 ? (RT_W_SLAB ? 96 : 64) : (RT_W_SLAB ? 176 : 96)), "WNode size");
+// word offsets inside a node (the kernel loads it as 16-B rows and picks words)
+constexpr int WN_QLO = 4;                           // qlo[a] starts at word WN_QLO + a * W_WIDTH / 4
+constexpr int WN_QHI = 4 + 3 * W_WIDTH / 4;         // qhi[a] at WN_QHI + a * W_WIDTH / 4
+constexpr int WN_SS = 4 + 6 * W_WIDTH / 4;          // s, slo
+constexpr int WN_NRM = (RT_W_SLAB ? ((4 + 6 * W_WIDTH / 4 + 2 + 3) / 4) * 4 : 0);
+constexpr int WN_SLAB = WN_NRM + W_WIDTH;
+constexpr int WN_CHILD = RT_W_SLAB ? WN_SLAB + W_WIDTH : ((4 + 6 * W_WIDTH / 4 + 3) / 4) * 4;
+constexpr int WN_ROWS = (int)(sizeof(WNode) / 16);
 
 struct WStats {
     int64_t nodes = 0, leaves = 0, tris = 0, max_leaf = 0, depth = 0;
@@ -287,21 +304,21 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
             W_STEP_HOOK(cur, 0);
             // (reading wave-uniform nodes, about half the steps of the C4 frame, through the
             // scalar cache instead was measured no faster)
-            const float4* p = reinterpret_cast<const float4*>(nodes + cur);
-            const float4 Q0 = ldg(p);
-            const uint4 Q1 = ldg(reinterpret_cast<const uint4*>(p) + 1), Q2 = ldg(reinterpret_cast<const uint4*>(p) + 2);
-#if RT_W_SLAB
-            const uint4 NR = ldg(reinterpret_cast<const uint4*>(p) + 3), SB = ldg(reinterpret_cast<const uint4*>(p) + 4);
-            const uint4 CH = ldg(reinterpret_cast<const uint4*>(p) + 5);
-#else
-            const uint4 CH = ldg(reinterpret_cast<const uint4*>(p) + 3);
-#endif
+            const uint4* p = reinterpret_cast<const uint4*>(nodes + cur);
+            uint4 R[WN_ROWS];
+#pragma unroll
+            for (int i = 0; i < WN_ROWS; i++)
+                R[i] = ldg(p + i);
+            // word i of the node (compile-time i)
+            auto wd = [&](int i) -> uint32_t {
+                const uint4 r = R[i >> 2];
+                return (i & 3) == 0 ? r.x : (i & 3) == 1 ? r.y : (i & 3) == 2 ? r.z : r.w;
+            };
 #if RT_W_SLAB
             const float m3 = 384.0f * m;   // |N|_1 <= 3 * 128: the spatial margin in slab units
-            const float ss = bitsf(Q2.z), slo_lo = bitsf(Q2.w) - m3, slo_hi = bitsf(Q2.w) + m3;
-            const uint32_t nr[4] = {NR.x, NR.y, NR.z, NR.w}, sb[4] = {SB.x, SB.y, SB.z, SB.w};
+            const float ss = bitsf(wd(WN_SS)), slo_lo = bitsf(wd(WN_SS + 1)) - m3, slo_hi = bitsf(wd(WN_SS + 1)) + m3;
 #endif
-            const uint32_t ex = fbits(Q0.w);
+            const uint32_t ex = wd(3);
             // t of a plane origin + q s (widened by m) = q (s / d) + (origin -+ m - o) / d
             const float sx = bitsf((ex & 0xffu) << 23) * ix, sy = bitsf(((ex >> 8) & 0xffu) << 23) * iy,
                         sz = bitsf(((ex >> 16) & 0xffu) << 23) * iz;
@@ -310,19 +327,23 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
             // Near plane of axis a: t = q_near s_a / d_a + (origin_a - o_a -+ m) / d_a, with the
             // byte row and the sign of m chosen by the direction's sign (the same products as
             // testing both planes and ordering them by min / max)
-            const float Dx = Q0.x - o.x, Dy = Q0.y - o.y, Dz = Q0.z - o.z;
+            const float Dx = bitsf(wd(0)) - o.x, Dy = bitsf(wd(1)) - o.y, Dz = bitsf(wd(2)) - o.z;
             const float mx = nx_lo ? m : -m, my = ny_lo ? m : -m, mz = nz_lo ? m : -m;
             const float ax = (Dx - mx) * ix, ay = (Dy - my) * iy, az = (Dz - mz) * iz;
             const float bx = (Dx + mx) * ix, by = (Dy + my) * iy, bz = (Dz + mz) * iz;
-            const uint32_t nqx = nx_lo ? Q1.x : Q1.w, fqx = nx_lo ? Q1.w : Q1.x;
-            const uint32_t nqy = ny_lo ? Q1.y : Q2.x, fqy = ny_lo ? Q2.x : Q1.y;
-            const uint32_t nqz = nz_lo ? Q1.z : Q2.y, fqz = nz_lo ? Q2.y : Q1.z;
-            const uint32_t ch[4] = {CH.x, CH.y, CH.z, CH.w};
-            float key[4];
-            uint32_t ref[4];
+            constexpr int QW = W_WIDTH / 4;   // words per axis row of quantised planes
+            float key[W_WIDTH];
+            uint32_t ref[W_WIDTH];
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int sh = 8 * j;
+            for (int j = 0; j < W_WIDTH; j++) {
+                const int sh = 8 * (j & 3), jw = j >> 2;
+                const uint32_t lx = wd(WN_QLO + 0 * QW + jw), hx = wd(WN_QHI + 0 * QW + jw);
+                const uint32_t ly = wd(WN_QLO + 1 * QW + jw), hy = wd(WN_QHI + 1 * QW + jw);
+                const uint32_t lz = wd(WN_QLO + 2 * QW + jw), hz = wd(WN_QHI + 2 * QW + jw);
+                const uint32_t nqx = nx_lo ? lx : hx, fqx = nx_lo ? hx : lx;
+                const uint32_t nqy = ny_lo ? ly : hy, fqy = ny_lo ? hy : ly;
+                const uint32_t nqz = nz_lo ? lz : hz, fqz = nz_lo ? hz : lz;
+                const uint32_t chj = wd(WN_CHILD + j);
                 const float tnx = __builtin_fmaf((float)((nqx >> sh) & 0xffu), sx, ax);
                 const float tny = __builtin_fmaf((float)((nqy >> sh) & 0xffu), sy, ay);
                 const float tnz = __builtin_fmaf((float)((nqz >> sh) & 0xffu), sz, az);
@@ -333,7 +354,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                 float tmax = fminf(fminf(tfx, tfy), tfz);
                 // enter when max(tmin, 0) <= min(tmax (1 + SL), best_s); a NaN tmin (every
                 // slab NaN) enters too.  The key orders the children; misses get INFINITY.
-                bool ok = ch[j] != W_EMPTY &&
+                bool ok = chj != W_EMPTY &&
                           fmaxf(tmin, 0.0f) <= fminf(__builtin_fmaf(fabsf(tmax), SL, tmax), best_s);
 #if RT_W_SLAB
                 // the slab (and cone) only narrow the box's interval, so a child whose box
@@ -341,15 +362,16 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                 if (ok) {
                     // N . (o + t d - origin) in [c0, c1] widened by m3 >= |N|_1 m: t between
                     // (c0 - m3 + b) / a and (c1 + m3 + b) / a, b = N . (origin - o), a = N . d
-                    const float nx = (float)(int8_t)(nr[j] & 0xffu), ny = (float)(int8_t)((nr[j] >> 8) & 0xffu),
-                                nz = (float)(int8_t)((nr[j] >> 16) & 0xffu);
+                    const uint32_t nrj = wd(WN_NRM + j), sbj = wd(WN_SLAB + j);
+                    const float nx = (float)(int8_t)(nrj & 0xffu), ny = (float)(int8_t)((nrj >> 8) & 0xffu),
+                                nz = (float)(int8_t)((nrj >> 16) & 0xffu);
                     const float a = nx * d.x + ny * d.y + nz * d.z;
                     const float b = nx * Dx + ny * Dy + nz * Dz;
                     // the hardware reciprocal (1 ulp): its error moves the slab's t by a relative
                     // 2^-23, a distance far inside the margin m3 over the scene
                     const float ia = fast_rcp(a);
-                    const float c0 = __builtin_fmaf((float)(sb[j] & 0xffffu), ss, slo_lo) + b;
-                    const float c1 = __builtin_fmaf((float)(sb[j] >> 16), ss, slo_hi) + b;
+                    const float c0 = __builtin_fmaf((float)(sbj & 0xffffu), ss, slo_lo) + b;
+                    const float c1 = __builtin_fmaf((float)(sbj >> 16), ss, slo_hi) + b;
                     const float s0 = c0 * ia, s1 = c1 * ia;
                     tmin = fmaxf(tmin, fminf(s0, s1));
                     tmax = fminf(tmax, fmaxf(s0, s1));
@@ -357,30 +379,40 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
 #if RT_W_CONE
                     // every triangle below faces away when a exceeds the threshold (rounding of
                     // a and of the threshold: < 1e-4 |d|, inside the build's 0.01 |d|)
-                    ok = ok && !(a > (float)(nr[j] >> 24) * cstep);
+                    ok = ok && !(a > (float)(nrj >> 24) * cstep);
 #endif
                 }
 #endif
                 key[j] = ok ? fminf(fmaxf(tmin, 0.0f), 3.0e38f) : INFINITY;
-                ref[j] = ch[j];
+                ref[j] = chj;
 #if defined(__HIP_DEVICE_COMPILE__) && RT_W_SCHED_BARRIER
-                // one child at a time: the scheduler would interleave the four children's
+                // one child at a time: the scheduler would interleave the children's
                 // temporaries (VALU latency is hidden by the other waves anyway)
                 __builtin_amdgcn_sched_barrier(0);
 #endif
             }
-            // sort the four (key, ref) pairs ascending: misses (INFINITY) go last
+            // sort the (key, ref) pairs ascending: misses (INFINITY) go last
 #define W_CSWAP(a, b)                                                              \
     if (key[b] < key[a]) {                                                         \
         float tk = key[a]; key[a] = key[b]; key[b] = tk;                           \
         uint32_t tr = ref[a]; ref[a] = ref[b]; ref[b] = tr;                        \
     }
+#if RT_W_WIDTH == 4
             W_CSWAP(0, 1) W_CSWAP(2, 3) W_CSWAP(0, 2) W_CSWAP(1, 3) W_CSWAP(1, 2)
+#else
+            // 19 compare-exchanges (optimal 8-input network)
+            W_CSWAP(0, 2) W_CSWAP(1, 3) W_CSWAP(4, 6) W_CSWAP(5, 7)
+            W_CSWAP(0, 4) W_CSWAP(1, 5) W_CSWAP(2, 6) W_CSWAP(3, 7)
+            W_CSWAP(0, 1) W_CSWAP(2, 3) W_CSWAP(4, 5) W_CSWAP(6, 7)
+            W_CSWAP(2, 4) W_CSWAP(3, 5)
+            W_CSWAP(1, 4) W_CSWAP(3, 6)
+            W_CSWAP(1, 2) W_CSWAP(3, 4) W_CSWAP(5, 6)
+#endif
 #undef W_CSWAP
             if (key[0] < INFINITY) {
                 cur = ref[0];
 #pragma unroll
-                for (int j = 3; j >= 1; j--)
+                for (int j = W_WIDTH - 1; j >= 1; j--)
                     if (key[j] < INFINITY) {
                         if (sp < W_STACK)
                             stk.put(sp++, make_uint2(ref[j], fbits(key[j])));

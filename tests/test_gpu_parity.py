@@ -215,6 +215,33 @@ def test_bands_reassemble_to_full_frame(R, scene_name):
         assert np.array_equal(assemble(parts, st.image_height, band), full), (nranks, band)
 
 
+@pytest.mark.parametrize("f", [2, 3, 4])
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_band_streams_fused_ssaa(R, monkeypatch, f, fused):
+    """Band launches in flight on two streams (per-stream tile queues and band buffers), with
+    the SSAA box filter fused into the trace kernel's tiles (f = 2, 4; f = 3 and
+    RT_FUSED_SSAA=0 take the separate downscale pass): re-assembled == the full render."""
+    import torch
+    from raytracercpp_amd import scenes
+    from raytracercpp_amd.strips import assemble
+    monkeypatch.setenv("RT_FUSED_SSAA", fused)
+    sc, st = scenes.bumpy70k(width=160, height=96, enable_ssaa=True, ssaa_factor=f)
+    R.load_scene(sc, st)
+    R.ray_trace()
+    R.post_process()
+    full = R.get_image()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for nranks, band in ((1, 8), (4, 8), (3, 4)):
+        bufs = [torch.zeros((R.local_rows(band, rank, nranks), st.image_width), dtype=torch.int32, device="cuda:0")
+                for rank in range(nranks)]
+        torch.cuda.synchronize()   # the fills ran on the default stream
+        for rank in range(nranks):
+            R.render_bands_device(band, rank, nranks, bufs[rank].data_ptr(), streams[rank % 2].cuda_stream)
+        torch.cuda.synchronize()
+        parts = [b.cpu().numpy().view(np.uint32) for b in bufs]
+        assert np.array_equal(assemble(parts, st.image_height, band), full), (nranks, band)
+
+
 def test_render_api_and_errors(R):
     from raytracercpp_amd import scenes
     from raytracercpp_amd._lib import RtError

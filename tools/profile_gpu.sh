@@ -20,6 +20,6 @@ pass write WRITE_SIZE || exit 3
 pass tcc TCC_HIT_sum TCC_MISS_sum || exit 4
 pass sq SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES || exit 5
 pass sq2 SQ_WAIT_ANY SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS || exit 6
-pass sq3 SQ_THREAD_CYCLES_VALU SQ_INSTS_BRANCH GRBM_GUI_ACTIVE || exit 7
+pass sq3 SQ_THREAD_CYCLES_VALU SQ_INSTS_BRANCH SQ_INSTS_VALU GRBM_GUI_ACTIVE || exit 7
 pass mem TA_BUSY_avr TA_FLAT_READ_WAVEFRONTS_sum TD_TD_BUSY_sum TD_TC_STALL_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCP_LATENCY_sum GRBM_GUI_ACTIVE || exit 8
 find $OUT -name "*.csv" | sort

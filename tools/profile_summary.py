@@ -14,12 +14,14 @@ if stats:
         out["kernels"][r["Name"]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                                      "total_ns": float(r["TotalDurationNs"]), "pct": float(r["Percentage"])}
 for f in sorted(glob.glob(f"{src}/pmc_*/**/run_counter_collection.csv", recursive=True)):
-    agg = collections.defaultdict(list)
+    # per dispatch: the sum over the rows of one dispatch (instances / dimensions), then
+    # the mean over the ray_trace_kernel dispatches
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(f)):
         if "ray_trace_kernel" in r["Kernel_Name"]:
-            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+            agg[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
     for k, v in agg.items():
-        out["pmc_ray_trace_kernel"][k] = sum(v) / len(v)
+        out["pmc_ray_trace_kernel"][k] = sum(v.values()) / len(v)
     name = f.split(os.sep)[-3] if "pmc_" in f.split(os.sep)[-3] else os.path.basename(os.path.dirname(f))
     shutil.copy(f, os.path.join(dst, f"{name}_counters.csv"))
 p = out["pmc_ray_trace_kernel"]
@@ -31,6 +33,10 @@ if "TCC_HIT_sum" in p:
     out["l2_hit_rate"] = p["TCC_HIT_sum"] / max(1.0, p["TCC_HIT_sum"] + p["TCC_MISS_sum"])
 if "SQ_THREAD_CYCLES_VALU" in p and "SQ_ACTIVE_INST_VALU" in p:
     out["valu_lane_utilisation"] = p["SQ_THREAD_CYCLES_VALU"] / (64.0 * p["SQ_ACTIVE_INST_VALU"])
+if "SQ_INSTS_VALU" in p and "GRBM_GUI_ACTIVE" in p:
+    # VALU issue: a wave64 VALU instruction occupies its SIMD's issue for 2 cycles
+    # (MI355X_MICROARCH.md); 1024 SIMDs over the kernel's GPU-busy cycles
+    out["valu_issue_fraction"] = 2.0 * p["SQ_INSTS_VALU"] / (1024.0 * p["GRBM_GUI_ACTIVE"])
 if "SQ_WAIT_ANY" in p and "SQ_WAVE_CYCLES" in p:
     out["wave_wait_fraction"] = p["SQ_WAIT_ANY"] / p["SQ_WAVE_CYCLES"]
 json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1, sort_keys=True)
