@@ -2699,6 +2699,8 @@ __device__ __forceinline__ bool refl_gen(const KParams& P, const ReflArgs& A, in
     if (i >= F.nsamp) {
         S.kind = 2;
         S.ray = 0;
+        S.sh = 0;
+        S.child = -1;
         return false;
     }
     if (F.rough > 0) {
@@ -2719,6 +2721,8 @@ __device__ __forceinline__ bool refl_gen(const KParams& P, const ReflArgs& A, in
         S.kind = 0;
         st3(S.fc, col(0.0f, 0.0f, 0.0f));
         S.ray = 0;
+        S.sh = 0;
+        S.child = -1;
         return false;
     }
     S.kind = 1;
@@ -2758,6 +2762,18 @@ __global__ __launch_bounds__(BLOCK) void refl_trace_kernel(KParams P, ReflArgs A
     A.hit[slot] = H;
 }
 
+// append slot to the shadow list from (possibly divergent) lanes: one atomic per wave
+__device__ __forceinline__ void list_append(const ReflArgs& A, int slot)
+{
+    const uint64_t m = __ballot(1);   // the lanes appending now
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if ((int)(threadIdx.x & 63) == leader)
+        base = atomicAdd(A.list_count, (unsigned)__popcll(m));
+    base = __shfl(base, leader);
+    A.list[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = slot;
+}
+
 // pass1: per frame, the samples' trace_ray up to the shadow query, in sample order
 __global__ __launch_bounds__(BLOCK) void refl_pass1_kernel(KParams P, ReflArgs A)
 {
@@ -2783,9 +2799,15 @@ __global__ __launch_bounds__(BLOCK) void refl_pass1_kernel(KParams P, ReflArgs A
             int s = -1;
             bvh_record(P, h, H.r != 0, local, rhi, s);
             shapes_closest(P, ro, d, local, rhi, s);
+            if (A.fused) {
+                S.sh = 0;
+                S.child = -1;
+            }
             if (rhi.t > 0.1f) {
                 v3 ip;
                 c3 fc = shade_lit(P, ro, d, rhi, ip);   // may normal-map rhi.normal (persists)
+                if (A.fused)
+                    list_append(A, slot);   // a shaded sample: its shadow query (and spawn)
                 S.kind = 1;
                 st3(S.fc, fc);
                 st3(S.ip, ip);
@@ -2826,6 +2848,8 @@ __global__ __launch_bounds__(BLOCK) void refl_list_kernel(KParams P, ReflArgs A)
         A.list[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = slot;
 }
 
+__device__ __forceinline__ void spawn_sample(const KParams& P, const ReflArgs& A, int slot, SampleRec& S, bool sh);
+
 // shadow: is_shadowed (renderer.cpp:340-402) for every shaded sample (via the list)
 __global__ __launch_bounds__(BLOCK) void refl_shadow_kernel(KParams P, ReflArgs A)
 {
@@ -2834,12 +2858,32 @@ __global__ __launch_bounds__(BLOCK) void refl_shadow_kernel(KParams P, ReflArgs 
     unsigned t = blockIdx.x * BLOCK + threadIdx.x;
     if (t >= *A.list_count)
         return;
-    SampleRec& S = A.sm[A.list[t]];
+    const int slot = A.list[t];
+    SampleRec& S = A.sm[slot];
     v3 light = mk(P.light[0], P.light[1], P.light[2]);
-    S.sh = is_shadowed(P, ld3(S.ip), ld3(S.nrm), light, lv) ? 1 : 0;
+    const bool sh = is_shadowed(P, ld3(S.ip), ld3(S.nrm), light, lv);
+    S.sh = sh ? 1 : 0;
+    if (A.fused)
+        spawn_sample(P, A, slot, S, sh);
 }
 
-// spawn: reflective hits become frames of the next level
+// a shaded sample with a reflective material becomes a frame of the next level (its
+// compute_reflection call); the frame's index goes into S.child
+__device__ __forceinline__ void spawn_sample(const KParams& P, const ReflArgs& A, int slot, SampleRec& S, bool sh)
+{
+    const float* m = mat_of(P, S.mat);
+    if (!(m[12] > 0.0f))
+        return;
+    int f = A.order[A.c0 + slot / A.stride], i = slot % A.stride;
+    const FrameRec& F = A.fr[f];
+    unsigned idx = atomicAdd(A.child_count, 1u);
+    c3 dfc = shade_shadow_emit(P, ldc(S.fc), m, sh);
+    make_frame(P, A.child_fr[idx], ld3(S.ip), ld3(S.nrm), ld3(S.d), dfc, S.crough, S.mat,
+               child_key(F.key, (uint32_t)i), -1);
+    S.child = (int)idx;
+}
+
+// spawn: reflective hits become frames of the next level (A.fused == 0; else the shadow pass)
 __global__ __launch_bounds__(BLOCK) void refl_spawn_kernel(KParams P, ReflArgs A)
 {
     int slot = blockIdx.x * BLOCK + threadIdx.x;
@@ -2850,16 +2894,7 @@ __global__ __launch_bounds__(BLOCK) void refl_spawn_kernel(KParams P, ReflArgs A
     S.child = -1;
     if (!S.ray || S.kind != 1)
         return;
-    const float* m = mat_of(P, S.mat);
-    if (!(m[12] > 0.0f))
-        return;
-    int f = A.order[A.c0 + slot / A.stride], i = slot % A.stride;
-    const FrameRec& F = A.fr[f];
-    unsigned idx = atomicAdd(A.child_count, 1u);
-    c3 dfc = shade_shadow_emit(P, ldc(S.fc), m, S.sh != 0);
-    make_frame(P, A.child_fr[idx], ld3(S.ip), ld3(S.nrm), ld3(S.d), dfc, S.crough, S.mat,
-               child_key(F.key, (uint32_t)i), -1);
-    S.child = (int)idx;
+    spawn_sample(P, A, slot, S, S.sh != 0);
 }
 
 // resolve: compute_reflection's sum in sample order, then the frame's hit colour

@@ -215,6 +215,8 @@ struct ReflArgs {
     int32_t c0, c1;          // sorted positions [c0, c1) of this level
     int32_t level;           // samples trace at depth = level
     int32_t stride;          // max(N, 1)
+    int32_t fused;           // 1: pass1 builds the shadow list and the shadow pass spawns (no list /
+                             // spawn kernels); 0: the separate passes (RT_REFL_FUSE=0)
 };
 
 // ---- hybrid rasterisation (kernels.hip "Renderer::raster_trace") ----

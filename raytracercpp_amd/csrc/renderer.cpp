@@ -976,8 +976,15 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
         A.stride = stride;
         if ((e = hipMemsetAsync(L.cnt.p, 0, 8, stream)) != hipSuccess)
             return hip_fail(e, "hipMemsetAsync");
-        for (int stage : {1, 2, 6, 3, 4})
-            if ((e = rt_launch_refl_stage(stage, &P, &A, stream)) != hipSuccess)
+        // fused (default): trace, pass1 (+ shadow list), shadow (+ spawn); RT_REFL_FUSE=0: trace,
+        // pass1, list, shadow, spawn
+        const char* fz = getenv("RT_REFL_FUSE");
+        A.fused = !(fz && fz[0] == '0');
+        static const int fused_stages[] = {1, 2, 3}, split_stages[] = {1, 2, 6, 3, 4};
+        const int* st = A.fused ? fused_stages : split_stages;
+        const int nst = A.fused ? 3 : 5;
+        for (int k = 0; k < nst; k++)
+            if ((e = rt_launch_refl_stage(st[k], &P, &A, stream)) != hipSuccess)
                 return hip_fail(e, "reflection stage launch");
         unsigned nchild = 0;
         if ((e = hipMemcpyAsync(&nchild, L.cnt.p, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
@@ -1400,12 +1407,21 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
     for (int i = 0; i < band_nslots_; i++)
         if (band_slot_[i].stream == stream) si = i;
     if (si < 0) {
-        if (band_nslots_ == BAND_SLOTS)
-            return fail(RT_EINVAL, "render_bands_device: more than 8 distinct streams");
-        si = band_nslots_++;
+        if (band_nslots_ < BAND_SLOTS) {
+            si = band_nslots_++;
+            band_slot_[si].counters.device = band_slot_[si].tmp.device = device_;
+        } else {
+            // a ninth stream: the least recently used slot is recycled once the device is idle
+            // (its stream may no longer exist, so the wait is device-wide)
+            si = 0;
+            for (int i = 1; i < BAND_SLOTS; i++)
+                if (band_slot_[i].used < band_slot_[si].used) si = i;
+            if ((e = hipDeviceSynchronize()) != hipSuccess)
+                return hip_fail(e, "render_bands_device: recycling a stream slot");
+        }
         band_slot_[si].stream = stream;
-        band_slot_[si].counters.device = band_slot_[si].tmp.device = device_;
     }
+    band_slot_[si].used = ++band_uses_;
     auto env_on = [](const char* k) { const char* v = getenv(k); return v && v[0] == '1'; };
     const bool slot_only = !P.has_reflection && !s_.hybrid_rasterization_tracing && P.wnodes && !P.pipeline &&
                            !env_on("RT_SPLIT") && !env_on("RT_WIDE_LEAN") && !env_on("RT_TILE_ORDER");

@@ -188,10 +188,12 @@ private:
     struct BandSlot {
         hipStream_t stream = nullptr;
         DevBuf counters, tmp;
+        uint64_t used = 0;   // band_uses_ at the slot's last launch (least recently used is recycled)
     };
     static constexpr int BAND_SLOTS = 8;
     BandSlot band_slot_[BAND_SLOTS];
     int band_nslots_ = 0, band_last_ = -1;
+    uint64_t band_uses_ = 0;
     // event ring for render_bands_device kernel timing
     static constexpr int EV_RING = 256;
     std::vector<hipEvent_t> ring_;

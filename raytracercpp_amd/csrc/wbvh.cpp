@@ -86,6 +86,7 @@ struct Builder {
     std::vector<BNode>& nodes;       // preallocated, 2n - 1 nodes at most
     std::atomic<int32_t> next{1};
     std::atomic<int> spare;          // threads that may still be started
+    float ct = 1.0f;                 // SAH cost of a node visit, in triangle tests (RT_W_SAH_CT)
 
     struct Bins {
         int32_t cnt[3][NBINS];
@@ -204,7 +205,7 @@ struct Builder {
                     c += B.cnt[a][i];
                     if (c == 0 || rc[i + 1] == 0)
                         continue;
-                    float cost = 1.0f + (area(acc) * (float)c + ra[i + 1] * (float)rc[i + 1]) / (pa > 0 ? pa : 1.0f);
+                    float cost = ct + (area(acc) * (float)c + ra[i + 1] * (float)rc[i + 1]) / (pa > 0 ? pa : 1.0f);
                     if (cost < best_cost) {
                         best_cost = cost;
                         best_axis = a;
@@ -517,6 +518,13 @@ void build_wbvh(const FlatOctree& oct, WBvh& out)
     std::vector<BNode> bn((size_t)(2 * n));
     const int nt = wbvh_threads();
     Builder B(pb, pc, idx, bn, nt);
+    // RT_W_SAH_CT: the SAH's node-visit cost relative to one triangle test (default 1); larger
+    // values make larger leaves and a shallower tree.  Structure only: every tree is exact.
+    if (const char* e = std::getenv("RT_W_SAH_CT")) {
+        const float v = std::strtof(e, nullptr);
+        if (v > 0.0f && v < 100.0f)
+            B.ct = v;
+    }
     B.build(0, 0, (int32_t)n);
     bn.resize((size_t)B.next.load());
     // SAH cost of the binary tree (diagnostic)
