@@ -166,6 +166,7 @@ def main():
         # over the mean kernel time; "traffic" is the measured HBM bytes per launch (PMC, 2 x
         # FETCH_SIZE + WRITE_SIZE) -- the ~90 MB scene lives in L2 / Infinity Cache.
         ex = counts.get("gpu_executed") if counts else None
+        ms_per_step_local = 1e3 * elapsed_max / args.steps
         default_path = all(os.environ.get(k, "1") != "0" for k in ("RT_WBVH", "RT_SEG", "RT_CONES"))
         if ex and default_path:
             xb = (WIDE_NODE_BYTES * ex.get("wide_node_visits", 0) + TRI_BYTES * ex.get("wide_tri_tests", 0) +
@@ -181,7 +182,12 @@ def main():
                                "frac": round(xa / PEAK_HBM_GBS, 4), "traffic": int(traffic) if traffic else None,
                                "algorithmic_bytes_per_frame": xb,
                                "basis": "bytes read by the executed traversal (wide-BVH nodes 96 B, triangles 48 B, "
-                                        "certificates 72 B, octree k-DOPs 56 B) + 4 B/pixel; RT_COUNT counts"}
+                                        "certificates 72 B, octree k-DOPs 56 B) + 4 B/pixel; RT_COUNT counts",
+                               # with frames in flight a launch shares the GPU with the next frame's, so
+                               # its duration (above) is longer than the step; the same bytes over the
+                               # step interval (whole-job rate)
+                               "per_step": {"achieved": round(xb * share / (ms_per_step_local * 1e-3) / 1e9, 1),
+                                            "frac": round(xb * share / (ms_per_step_local * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}}
             if counts and "child_tests_primary" in counts:
                 # SURVEY.md 8(d)'s model priced on the REFERENCE's traversal (oracle count mode): the work
                 # the reference's octree walk would read, per second of this kernel

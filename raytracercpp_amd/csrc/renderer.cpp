@@ -925,7 +925,15 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
 {
     const int N = P.rough_reflections_sample_count;
     const int stride = N > 0 ? N : 1;
-    const int chunk = std::max(1024, (1 << 21) / stride);   // about 2M sample slots per chunk
+    // about 2^RT_REFL_CHUNK_LOG2 sample slots per chunk (default 2^23: C5 0.765 -> 0.714 s over 2^21; 18..25): a chunk's
+    // records (~170 B per slot with its child frames) and one host round trip per chunk
+    int clog = 23;
+    if (const char* ce = getenv("RT_REFL_CHUNK_LOG2")) {
+        const int v = atoi(ce);
+        if (v >= 18 && v <= 25)
+            clog = v;
+    }
+    const int chunk = std::max(1024, (1 << clog) / stride);
     if (level + 1 >= REFL_LEVELS)
         return fail(RT_EUNSUPPORTED, "reflection recursion deeper than the engine's levels");
     ReflLevel& L = refl_[level];
