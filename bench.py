@@ -32,7 +32,7 @@ CERT_BYTES = 72              # one certificate: the octree leaf's 64-B node + tw
 PIXEL_BYTES = 4              # ARGB32 write per internal pixel
 COUNTS_FILE = os.path.join(ROOT, "profiles", "work_counts.json")
 # rocprofv3 PMC summary of this kernel on the same command (tools/profile_gpu.sh + profile_summary.py)
-PROFILE_SUMMARY = os.path.join(ROOT, "profiles", "r02", "summary.json")
+PROFILE_SUMMARY = os.path.join(ROOT, "profiles", "r02c", "summary.json")
 
 
 def parse():
@@ -65,7 +65,11 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        # RCCL on a high-priority stream: with frames in flight the gather's blocks are
+        # dispatched ahead of the next frame's persistent grid instead of waiting for its tail
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        dist.init_process_group("nccl", device_id=dev, pg_options=opts)
 
     sc, st = scenes.CONFIGS[args.config]()
     r = Renderer(local)

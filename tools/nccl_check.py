@@ -1,0 +1,39 @@
+"""RCCL path of bench.py on one GPU (world size 1, torchrun): high-priority process group, two
+frames in flight with async all-gathers (strips.FramePipeline with the gather forced on);
+every gathered frame must equal the rendered strips.  Usage (GPU box):
+  python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 \\
+      --master-port 29511 tools/nccl_check.py"""
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+import torch.distributed as dist
+from raytracercpp_amd import scenes
+from raytracercpp_amd.renderer import Renderer
+from raytracercpp_amd.strips import FramePipeline
+
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+opts = dist.ProcessGroupNCCL.Options()
+opts.is_high_priority_stream = True
+dist.init_process_group("nccl", device_id=dev, pg_options=opts)
+sc, st = scenes.bumpy70k(width=320, height=184, enable_ssaa=True, ssaa_factor=2)
+r = Renderer(0)
+r.load_scene(sc, st)
+band = 8
+n = r.local_rows(band, 0, 1)
+streams = [torch.cuda.current_stream(dev), torch.cuda.Stream(dev)]
+outs = [torch.zeros((n, st.image_width), dtype=torch.int32, device=dev) for _ in range(2)]
+torch.cuda.synchronize()
+pipe = FramePipeline(lambda o, s: r.render_bands_device(band, 0, 1, o.data_ptr(), s.cuda_stream), outs, 1, streams, dist)
+pipe.world = 2   # force the gather path with one rank: parts[i] holds 2 slots, gather fills slot 0
+pipe.parts = [[torch.empty_like(o)] for o in outs]
+ok = True
+for k in range(12):
+    pipe.step()
+pipe.drain()
+ref = outs[0].clone()
+for i in range(2):
+    ok &= bool(torch.equal(pipe.parts[i][0], outs[i])) and bool(torch.equal(outs[i], ref))
+print("nccl pipeline ok" if ok else "nccl pipeline MISMATCH", flush=True)
+dist.destroy_process_group()
+sys.exit(0 if ok else 1)
