@@ -216,7 +216,10 @@ struct ReflArgs {
     int32_t level;           // samples trace at depth = level
     int32_t stride;          // max(N, 1)
     int32_t fused;           // 1: pass1 builds the shadow list and the shadow pass spawns (no list /
-                             // spawn kernels); 0: the separate passes (RT_REFL_FUSE=0)
+                             // spawn kernels), and every sample's result is in res; 0: the separate
+                             // passes (RT_REFL_FUSE=0), resolve reads the records
+    float4* res;             // fused: per sample slot, the colour it returns (xyz) or, in w as int bits,
+                             // the index of the child frame whose colour it returns (-1: xyz)
 };
 
 // ---- hybrid rasterisation (kernels.hip "Renderer::raster_trace") ----

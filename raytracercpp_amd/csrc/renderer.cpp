@@ -903,7 +903,7 @@ int Renderer::launch_trace(const KParams& P, hipStream_t stream)
     }
     for (auto& L : refl_)
         L.fr.device = L.ret.device = L.sm.device = L.hit.device = L.cnt.device = L.list.device = L.sort.device =
-            L.sort_tmp.device = device_;
+            L.sort_tmp.device = L.res.device = device_;
     size_t npx = (size_t)P.rw * P.local_rows;
     ReflLevel& L1 = refl_[1];
     if ((e = L1.fr.reserve(npx * sizeof(FrameRec))) != hipSuccess || (e = L1.cnt.reserve(64)) != hipSuccess)
@@ -942,7 +942,7 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
     hipError_t e;
     if ((e = L.ret.reserve((size_t)nframes * 12)) != hipSuccess || (e = L.sm.reserve(slots * sizeof(SampleRec))) != hipSuccess ||
         (e = L.hit.reserve(slots * sizeof(RawHit))) != hipSuccess || (e = L.cnt.reserve(64)) != hipSuccess ||
-        (e = L.list.reserve(slots * 4)) != hipSuccess ||
+        (e = L.list.reserve(slots * 4)) != hipSuccess || (e = L.res.reserve(slots * 16)) != hipSuccess ||
         (e = C.fr.reserve(slots * sizeof(FrameRec))) != hipSuccess || (e = C.ret.reserve(slots * 12)) != hipSuccess)
         return hip_fail(e, "hipMalloc (reflection level)");
     // the level's frames in Morton order of their origins (coherent sample and shadow rays)
@@ -977,6 +977,7 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
         A.child_fr = C.fr.as<FrameRec>();
         A.child_count = L.cnt.as<unsigned int>();
         A.list = L.list.as<int32_t>();
+        A.res = L.res.as<float4>();
         A.list_count = L.cnt.as<unsigned int>() + 1;
         A.c0 = c0;
         A.c1 = std::min(nframes, c0 + chunk);
@@ -1072,7 +1073,7 @@ int Renderer::launch_raster(const KParams& P, hipStream_t stream)
     PS.tri_uv = A.piece_uv;
     for (auto& L : refl_)
         L.fr.device = L.ret.device = L.sm.device = L.hit.device = L.cnt.device = L.list.device = L.sort.device =
-            L.sort_tmp.device = device_;
+            L.sort_tmp.device = L.res.device = device_;
     ReflLevel& L1 = refl_[1];
     const bool frames = P.has_reflection;
     if (frames) {

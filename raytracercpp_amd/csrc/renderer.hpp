@@ -178,7 +178,7 @@ private:
 
     // reflection engine buffers, per level (frames, results, chunk samples / hits, child counter)
     struct ReflLevel {
-        DevBuf fr, ret, sm, hit, cnt, list, sort, sort_tmp;
+        DevBuf fr, ret, sm, hit, cnt, list, sort, sort_tmp, res;
     };
     static constexpr int REFL_LEVELS = 18;   // max_recursion_depth <= 15: frames at levels 1..16, +1 child slot
     ReflLevel refl_[REFL_LEVELS];
