@@ -2696,11 +2696,15 @@ __device__ __forceinline__ bool refl_gen(const KParams& P, const ReflArgs& A, in
     int f = A.order[A.c0 + slot / A.stride], i = slot % A.stride;
     const FrameRec& F = A.fr[f];
     SampleRec& S = A.sm[slot];
+    // fused: a sample's direction and ray flag go to its 32-B RawHit (written by the trace
+    // kernel, coalesced) and nothing to the 72-B record, which only shaded samples fill
     if (i >= F.nsamp) {
-        S.kind = 2;
-        S.ray = 0;
-        S.sh = 0;
-        S.child = -1;
+        if (!A.fused) {
+            S.kind = 2;
+            S.ray = 0;
+            S.sh = 0;
+            S.child = -1;
+        }
         return false;
     }
     if (F.rough > 0) {
@@ -2714,21 +2718,26 @@ __device__ __forceinline__ bool refl_gen(const KParams& P, const ReflArgs& A, in
         dir = F.rough * rdir + (1 - F.rough) * ld3(F.perfect);
     } else
         dir = ld3(F.perfect);
-    st3(S.d, dir);
+    if (!A.fused)
+        st3(S.d, dir);
     if (i == 0)
         count = (unsigned)F.nsamp;   // reflection rays
     if (A.level > P.max_recursion_depth) {   // trace_ray's depth guard (renderer.cpp:1012-1013)
-        S.kind = 0;
-        st3(S.fc, col(0.0f, 0.0f, 0.0f));
-        S.ray = 0;
-        S.sh = 0;
-        S.child = -1;
-        if (A.fused)
+        if (A.fused) {
             A.res[slot] = make_float4(0.0f, 0.0f, 0.0f, __int_as_float(-1));
+        } else {
+            S.kind = 0;
+            st3(S.fc, col(0.0f, 0.0f, 0.0f));
+            S.ray = 0;
+            S.sh = 0;
+            S.child = -1;
+        }
         return false;
     }
-    S.kind = 1;
-    S.ray = 1;
+    if (!A.fused) {
+        S.kind = 1;
+        S.ray = 1;
+    }
     return true;
 }
 
@@ -2742,8 +2751,17 @@ __global__ __launch_bounds__(BLOCK) void refl_trace_kernel(KParams P, ReflArgs A
     v3 dir = mk(0, 0, 0);
     bool ray = slot < nslot && refl_gen(P, A, slot, dir, count);
     wave_count_add(&P.counters[1], count);
-    if (!ray)
+    if (!ray) {
+        if (A.fused && slot < nslot) {   // no ray (pass1 skips it: bit 1 clear)
+            RawHit H;
+            H.t = H.u = H.v = 0.0f;
+            H.k = -1;
+            st3(H.d, dir);
+            H.r = 0;
+            A.hit[slot] = H;
+        }
         return;
+    }
     const FrameRec& F = A.fr[A.order[A.c0 + slot / A.stride]];
     TRay R = make_ray(P, ld3(F.ro), dir);
     THit h;
@@ -2760,7 +2778,8 @@ __global__ __launch_bounds__(BLOCK) void refl_trace_kernel(KParams P, ReflArgs A
     H.u = h.u;
     H.v = h.v;
     H.k = h.k;
-    H.r = r ? 1 : 0;
+    st3(H.d, dir);
+    H.r = (r ? 1 : 0) | (A.fused ? 2 : 0);
     A.hit[slot] = H;
 }
 
@@ -2788,10 +2807,10 @@ __global__ __launch_bounds__(BLOCK) void refl_pass1_kernel(KParams P, ReflArgs A
         for (int i = 0; i < F.nsamp; i++) {
             int slot = (p - A.c0) * A.stride + i;
             SampleRec& S = A.sm[slot];
-            if (!S.ray)
+            const RawHit H = A.hit[slot];
+            if (A.fused ? !(H.r & 2) : !S.ray)
                 continue;   // depth limit: trace_ray returns before touching the record
-            v3 d = ld3(S.d);
-            RawHit H = A.hit[slot];
+            const v3 d = A.fused ? ld3(H.d) : ld3(S.d);
             THit h;
             h.t = H.t;
             h.u = H.u;
@@ -2799,9 +2818,9 @@ __global__ __launch_bounds__(BLOCK) void refl_pass1_kernel(KParams P, ReflArgs A
             h.k = H.k;
             Rec local = rec_fresh();
             int s = -1;
-            bvh_record(P, h, H.r != 0, local, rhi, s);
+            bvh_record(P, h, (H.r & 1) != 0, local, rhi, s);
             shapes_closest(P, ro, d, local, rhi, s);
-            if (A.fused) {
+            if (!A.fused) {
                 S.sh = 0;
                 S.child = -1;
             }
@@ -2821,11 +2840,13 @@ __global__ __launch_bounds__(BLOCK) void refl_pass1_kernel(KParams P, ReflArgs A
                     nshadow++;
             } else {
                 float a;
-                S.kind = 0;
                 const c3 mc = miss_color(P, d, a);
-                st3(S.fc, mc);
-                if (A.fused)
+                if (A.fused) {
                     A.res[slot] = make_float4(mc.r, mc.g, mc.b, __int_as_float(-1));
+                } else {
+                    S.kind = 0;
+                    st3(S.fc, mc);
+                }
             }
         }
     }
@@ -2891,7 +2912,7 @@ __device__ __forceinline__ int spawn_sample(const KParams& P, const ReflArgs& A,
     const FrameRec& F = A.fr[f];
     unsigned idx = atomicAdd(A.child_count, 1u);
     c3 dfc = shade_shadow_emit(P, ldc(S.fc), m, sh);
-    make_frame(P, A.child_fr[idx], ld3(S.ip), ld3(S.nrm), ld3(S.d), dfc, S.crough, S.mat,
+    make_frame(P, A.child_fr[idx], ld3(S.ip), ld3(S.nrm), A.fused ? ld3(A.hit[slot].d) : ld3(S.d), dfc, S.crough, S.mat,
                child_key(F.key, (uint32_t)i), -1);
     S.child = (int)idx;
     return (int)idx;

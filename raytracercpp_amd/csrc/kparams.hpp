@@ -198,7 +198,8 @@ struct SampleRec {
 struct RawHit {
     float t, u, v;
     int32_t k;          // GTri slot, -1 none
-    int32_t r;          // the query's return value
+    float d[3];         // the sample's direction (ReflArgs::fused; else in SampleRec::d)
+    int32_t r;          // bit 0: the query's return value; bit 1 (fused): the sample traced a ray
 };
 
 struct ReflArgs {

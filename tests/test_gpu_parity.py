@@ -309,13 +309,18 @@ def test_reflection_engine_matches_oracle_c5_small(R, monkeypatch):
     sc, st = scenes.sphere1m_refl(width=64, height=36, samples=4)
     st = st.copy(max_recursion_depth=3)
     o = Oracle(sc, st).render_rows()
-    for engine in ("1", "0"):
+    # (engine, fused passes, chunk log2): the default engine, its separate list / spawn passes,
+    # many small chunks per level (depth-first over chunks), and the recursive kernel
+    for engine, fuse, clog in (("1", "1", "24"), ("1", "0", "24"), ("1", "1", "10"), ("0", "1", "24")):
         monkeypatch.setenv("RT_REFL_ENGINE", engine)
+        monkeypatch.setenv("RT_REFL_FUSE", fuse)
+        monkeypatch.setenv("RT_REFL_CHUNK_LOG2", clog)
+        engine = f"engine {engine} fuse {fuse} chunk 2^{clog}"
         g = gpu_render(R, sc, st)
         assert np.array_equal(g["hit_id"], o.hit_id), engine
         assert np.array_equal(bits(g["hit_t"]), bits(o.hit_t)), engine
         assert np.array_equal(g["shadow"], o.shadow), engine
-        assert np.array_equal(g["argb"], o.argb), f"engine {engine}: {int((g['argb'] != o.argb).sum())} ARGB mismatches"
+        assert np.array_equal(g["argb"], o.argb), f"{engine}: {int((g['argb'] != o.argb).sum())} ARGB mismatches"
         assert float(np.abs(g["rgba"] - o.rgba).max()) <= RGBA_TOL
         stt = R.stats()
         assert stt["shadow_rays"] == o.counters["shadow_rays"], engine
