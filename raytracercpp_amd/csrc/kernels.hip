@@ -2741,7 +2741,10 @@ __device__ __forceinline__ bool refl_gen(const KParams& P, const ReflArgs& A, in
     return true;
 }
 
-__global__ __launch_bounds__(BLOCK) void refl_trace_kernel(KParams P, ReflArgs A)
+#ifndef RT_OCC_REFL
+#define RT_OCC_REFL 4   // waves per SIMD of the reflection trace / shadow / pass1 kernels
+#endif
+__global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_kernel(KParams P, ReflArgs A)
 {
     extern __shared__ uint2 lds_levels[];
     uint2* lv = lds_levels + threadIdx.x;
@@ -2796,7 +2799,7 @@ __device__ __forceinline__ void list_append(const ReflArgs& A, int slot)
 }
 
 // pass1: per frame, the samples' trace_ray up to the shadow query, in sample order
-__global__ __launch_bounds__(BLOCK) void refl_pass1_kernel(KParams P, ReflArgs A)
+__global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_pass1_kernel(KParams P, ReflArgs A)
 {
     int p = A.c0 + blockIdx.x * BLOCK + threadIdx.x;
     unsigned nshadow = 0;
@@ -2877,7 +2880,7 @@ __global__ __launch_bounds__(BLOCK) void refl_list_kernel(KParams P, ReflArgs A)
 __device__ __forceinline__ int spawn_sample(const KParams& P, const ReflArgs& A, int slot, SampleRec& S, bool sh);
 
 // shadow: is_shadowed (renderer.cpp:340-402) for every shaded sample (via the list)
-__global__ __launch_bounds__(BLOCK) void refl_shadow_kernel(KParams P, ReflArgs A)
+__global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_shadow_kernel(KParams P, ReflArgs A)
 {
     extern __shared__ uint2 lds_levels[];
     uint2* lv = lds_levels + threadIdx.x;
