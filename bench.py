@@ -38,8 +38,8 @@ PROFILE_SUMMARY = os.path.join(ROOT, "profiles", "r02c", "summary.json")
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)   # a step is ~0.55 ms: 50 keep the pipeline fill / drain small
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="sphere1m")
     ap.add_argument("--band-rows", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
