@@ -35,8 +35,16 @@ if "SQ_THREAD_CYCLES_VALU" in p and "SQ_ACTIVE_INST_VALU" in p:
     out["valu_lane_utilisation"] = p["SQ_THREAD_CYCLES_VALU"] / (64.0 * p["SQ_ACTIVE_INST_VALU"])
 if "SQ_INSTS_VALU" in p and "GRBM_GUI_ACTIVE" in p:
     # VALU issue: a wave64 VALU instruction occupies its SIMD's issue for 2 cycles
-    # (MI355X_MICROARCH.md); 1024 SIMDs over the kernel's GPU-busy cycles
-    out["valu_issue_fraction"] = 2.0 * p["SQ_INSTS_VALU"] / (1024.0 * p["GRBM_GUI_ACTIVE"])
+    # (MI355X_MICROARCH.md); 1024 SIMDs over the kernel's GPU-busy cycles.  GRBM_GUI_ACTIVE
+    # comes summed over the 8 XCDs (8x the kernel's duration in cycles)
+    out["grbm_cycles_per_xcd"] = p["GRBM_GUI_ACTIVE"] / 8.0
+    out["valu_issue_fraction"] = 2.0 * p["SQ_INSTS_VALU"] / (1024.0 * out["grbm_cycles_per_xcd"])
+if "TD_TD_BUSY_sum" in p and "GRBM_GUI_ACTIVE" in p:
+    # 256 TD / TA instances (one per CU)
+    out["td_busy_fraction"] = p["TD_TD_BUSY_sum"] / 256.0 / (p["GRBM_GUI_ACTIVE"] / 8.0)
+    out["td_stall_on_l1_fraction"] = p.get("TD_TC_STALL_sum", 0.0) / 256.0 / (p["GRBM_GUI_ACTIVE"] / 8.0)
+if "TA_BUSY_avr" in p and "GRBM_GUI_ACTIVE" in p:
+    out["ta_busy_fraction"] = p["TA_BUSY_avr"] / (p["GRBM_GUI_ACTIVE"] / 8.0)
 if "SQ_WAIT_ANY" in p and "SQ_WAVE_CYCLES" in p:
     out["wave_wait_fraction"] = p["SQ_WAIT_ANY"] / p["SQ_WAVE_CYCLES"]
 json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1, sort_keys=True)
