@@ -681,3 +681,25 @@ def test_forced_deferral_matches_oracle(R, monkeypatch, case):
     if case != "huge":
         assert R.stats()["seg_scale"] > 0
     _check_vs_oracle(g, ref, case, R=R)
+
+
+def test_rccl_frame_pipeline_world1():
+    """bench.py's N>1 path on one GPU: an RCCL process group (world size 1, torchrun) on a
+    high-priority stream, two frames in flight with asynchronous all-gathers
+    (strips.FramePipeline, gather forced on): every gathered frame equals the rendered strips
+    (tools/nccl_check.py).  Runs in its own process: the rendezvous and RCCL state stay out of
+    this one."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "1",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "tools/nccl_check.py"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0 and "nccl pipeline ok" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
