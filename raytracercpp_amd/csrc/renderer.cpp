@@ -925,9 +925,9 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
 {
     const int N = P.rough_reflections_sample_count;
     const int stride = N > 0 ? N : 1;
-    // about 2^RT_REFL_CHUNK_LOG2 sample slots per chunk (default 2^24: C5 0.765 / 0.714 / 0.695 s at 2^21 / 2^23 / 2^24; 10..25): a chunk's
+    // about 2^RT_REFL_CHUNK_LOG2 sample slots per chunk (default 2^25: C5 0.765 / 0.714 / 0.695 / 0.679 s at 2^21 / 2^23 / 2^24 / 2^25; 10..25): a chunk's
     // records (~170 B per slot with its child frames) and one host round trip per chunk
-    int clog = 24;
+    int clog = 25;
     if (const char* ce = getenv("RT_REFL_CHUNK_LOG2")) {
         const int v = atoi(ce);
         if (v >= 10 && v <= 25)   // small values (tests): many chunks per level
