@@ -3724,8 +3724,12 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(
             C.defer_in_head = 13;
             hipLaunchKernelGGL(rt::ray_trace_defer_kernel, dim3(db), dim3(rt::BLOCK), lds, stream, C);
         } else {
+            // the plain kernel's grid is exactly its residency (RT_OCC_PLAIN blocks of 4 waves per
+            // CU): with two frames in flight, surplus blocks of one frame would be dispatched ahead
+            // of the next frame's only to find the queue empty (C4 +1.3%: r02_bench98_*.log)
+            const int pblocks = P->max_blocks > 0 ? std::max(1, std::min(blocks, P->max_blocks / 8 * RT_OCC_PLAIN)) : blocks;
             if (P->plain && !P->zbuf && !P->nbuf)
-                hipLaunchKernelGGL((rt::ray_trace_kernel<false, false, true>), dim3(blocks), dim3(rt::BLOCK), lds, stream, A);
+                hipLaunchKernelGGL((rt::ray_trace_kernel<false, false, true>), dim3(pblocks), dim3(rt::BLOCK), lds, stream, A);
             else
                 hipLaunchKernelGGL((rt::ray_trace_kernel<false, false>), dim3(blocks), dim3(rt::BLOCK), lds, stream, A);
             if (P->defer && P->defer_cap) {

@@ -750,7 +750,7 @@ void Renderer::fill_params(KParams& P) const
         if (S > 0x1p-20f && S < 0x1p20f)
             P.seg_scale = S;
     }
-    P.max_blocks = num_cus_ * 8;
+    P.max_blocks = num_cus_ * 8;   // persistent grids: 8 blocks per CU (the plain kernel: its residency)
     P.tq_base = NCOUNTERS;
     // the plain specialisation (RT_PLAIN=0 turns it off); SSAO (zbuf) is checked at launch
     const char* plain_env = getenv("RT_PLAIN");
