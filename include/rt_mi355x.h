@@ -92,22 +92,17 @@ typedef struct rt_stats {
                                   0: shadow / reflection queries walked the whole line */
     int64_t work[4];           /* diagnostic builds (-DRT_COUNT=1) only, else 0: the last frame's k-DOP and
                                   Moller-Trumbore tests of whole-line queries, then of segment queries */
-    int64_t deferred_pixels;   /* pixels of the last ray_trace handed from the main kernel to a second pass: with
-                                  the wide BVH, queries over RT_WIDE_BUDGET or uncertified, else
-                                  primary queries over RT_DEFER_BUDGET (the ray-group pass, 5.5) */
-    int64_t work_abandoned[2]; /* diagnostic builds only: k-DOP and Moller-Trumbore tests of primary queries
-                                  abandoned over the budget (re-traced by the deferred pass, counted in work) */
     int64_t work_wide[4];      /* diagnostic builds only: wide-BVH node visits, triangle tests, the queries it could
                                   not certify (traced through the octree instead), and the
                                   certificates' octree k-DOP tests */
     int64_t uncertified[6];    /* diagnostic builds only: uncertified wide-BVH queries by reason -- stack overflow,
                                   NaN hit, only overflowed hits, tie, minimum t outside (0, inf), failed
                                   certificate */
-    int64_t exact_pixels;      /* pixels of the last frame whose queries the wide BVH could not certify, traced
-                                  through the octree by the exact pass */
     int64_t wave_steps[6];     /* diagnostic builds only: wide-BVH traversal loop iterations of primary queries --
                                   summed over waves (each wave's longest lane), summed over lanes, wave calls --
                                   then the same for shadow queries (SIMD efficiency = lanes / (64 waves)) */
+    float build_split_ms[4];   /* the last scene build (build_ms) split: octree build + flatten, leaf cones and
+                                  slabs, wide BVH, device upload (host milliseconds) */
 } rt_stats;
 
 typedef struct rt_renderer rt_renderer;
@@ -227,17 +222,27 @@ int rt_get_internal(rt_renderer *r, uint32_t *argb, float *rgba, int32_t *hit_id
 
 int rt_get_stats(rt_renderer *r, rt_stats *out);
 
-/* Diagnostic builds (with RT_DEBUG_WAVES set in the environment): the last ray_trace's
- * per-wave records of 8 words, n = 8 x waves values -- -DRT_WAVE_STATS=1: {first dequeue tick,
- * exit tick, tiles, busy ticks} (100 MHz wall clock); -DRT_PHASE_TIME=1: shader cycles per
- * phase {tile setup, ray generation, primary query, shading, shadow query, framebuffer, dequeue} (plain
- * kernel).  RT_EINVAL when no record buffer exists. */
+/* Diagnostic builds (-DRT_PHASE_TIME=1, with RT_DEBUG_WAVES set in the environment when the
+ * renderer is created): the last ray_trace's per-wave records of 8 words, n = 8 x waves values --
+ * shader cycles per phase {tile setup, ray generation, primary query, shading, shadow query,
+ * framebuffer, dequeue} of the plain kernel.  RT_EINVAL when no record buffer exists. */
 int rt_debug_read(rt_renderer *r, uint64_t *out, int64_t n);
 
 /* Image-strip rendering for multi-GPU (one process per GPU): renders the bands of
  * band_rows OUTPUT rows with band % nranks == rank into the device buffer d_out
  * (image_width x local_rows(...) ARGB32, final resolution, SSAA applied) on the
- * given HIP stream (NULL = the handle's stream).  Does not synchronise. */
+ * given HIP stream (NULL = the handle's stream).  Does not synchronise.
+ *
+ * Stream contract.  Every write to d_out is enqueued on hip_stream and ordered only by it:
+ *   - the caller orders any earlier work on d_out (fills, copies, reads of the previous frame)
+ *     before this call on hip_stream, e.g. with hipStreamWaitEvent; work that touches d_out
+ *     on another stream afterwards must wait for an event recorded on hip_stream after this call;
+ *   - launches on different streams may run concurrently (frames in flight); each stream has
+ *     its own tile-queue counters and band buffer (up to 8 streams, the least recently used is
+ *     recycled once its last launch is done);
+ *   - the library orders its own shared state: a launch that uses buffers shared across
+ *     launches (reflection engine, raster path) waits for every launch still in flight, and a
+ *     scene, material or texture change waits for them on the host before it is uploaded. */
 int rt_local_rows(rt_renderer *r, int32_t band_rows, int32_t rank, int32_t nranks, int32_t *rows_out);
 int rt_render_bands_device(rt_renderer *r, int32_t band_rows, int32_t rank, int32_t nranks, uint32_t *d_out,
                            void *hip_stream);
@@ -253,7 +258,8 @@ int rt_trace_rays(rt_renderer *r, const float *orig, const float *dir, int64_t n
 /* GPU durations (ms) of the ray-trace kernel of the last n rt_render_bands_device
  * calls, from HIP events recorded around each launch on its stream (waits for them). */
 int rt_kernel_times(rt_renderer *r, float *ms, int32_t n);
-/* shadow / reflection ray counts of the last rt_render_bands_device (synchronises the device) */
+/* shadow / reflection ray counts of the last rt_render_bands_device (waits for that launch);
+ * RT_ESTATE before the first rt_render_bands_device call */
 int rt_band_counters(rt_renderer *r, int64_t *shadow_rays, int64_t *reflection_rays);
 
 /* ---- tp2/src/mat.cpp restated (host) ---- */

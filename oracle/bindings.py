@@ -184,6 +184,8 @@ class Oracle:
             L.orc_destroy.argtypes = [C.c_void_p]
             L.orc_render_rows.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(OrcOutputs),
                                           C.POINTER(OrcCounters), C.c_int]
+            L.orc_render_row_set.argtypes = [C.c_void_p, _i32p, C.c_int, C.POINTER(OrcOutputs),
+                                             C.POINTER(OrcCounters), C.c_int]
             L.orc_raster.argtypes = [C.c_void_p, C.POINTER(OrcOutputs), C.POINTER(OrcCounters), C.c_int]
             L.orc_downscale_argb.argtypes = [_u32p, C.c_int, C.c_int, C.c_int, _u32p]
             L.orc_bvh_query.argtypes = [C.c_void_p, _f32p, _f32p, C.c_int64, _i32p, _f32p, _f32p, _f32p, _u8p, _i64p]
@@ -225,6 +227,22 @@ class Oracle:
         res.seconds = time.perf_counter() - t0
         if rc != 0:
             raise RuntimeError("orc_render_rows failed")
+        res.counters = cnt.as_dict()
+        return res
+
+    def render_row_set(self, rows, nthreads=0) -> RenderResult:
+        """render_rows on an arbitrary list of internal rows (output row i = rows[i]), with the
+        threads spread over the rows' pixels (a few rows of an expensive frame)."""
+        rows = np.ascontiguousarray(rows, np.int32)
+        rw, _ = self.settings.render_size()
+        res = RenderResult(rw, len(rows))
+        cnt = OrcCounters()
+        out = res.outputs()
+        t0 = time.perf_counter()
+        rc = self.lib().orc_render_row_set(self._h, _ptr(rows, _i32p), len(rows), C.byref(out), C.byref(cnt), nthreads)
+        res.seconds = time.perf_counter() - t0
+        if rc != 0:
+            raise RuntimeError("orc_render_row_set failed")
         res.counters = cnt.as_dict()
         return res
 

@@ -1487,6 +1487,44 @@ ORC_API int orc_raster(const struct orc_ctx *X, orc_outputs *out, orc_counters *
     return 0;
 }
 
+/* One pixel of Renderer::ray_trace (renderer.cpp:1086-1113) into output slot o */
+static void render_pixel(otracer *T, int px, int py, orc_outputs *out, size_t o)
+{
+    const struct orc_ctx *X = T->X;
+    int rw = X->rw, rh = X->rh;
+    v3 cam = V(X->sc.cam_pos[0], X->sc.cam_pos[1], X->sc.cam_pos[2]);
+    float y_world = ((float)py + 0.5f) / rh * 2 - 1;
+    float x_world = ((float)px + 0.5f) / rw * 2 - 1;
+    v3 vs = xform_point(X->sc.proj_inv, V(x_world, y_world, -1));
+    v3 ws = xform_point(X->sc.cam_to_world, vs);
+    v3 rd = vnormalize(vsub(ws, cam));
+    int found = 0, src = -1, shadowed = 0;
+    ohit hi = hit_fresh();
+    T->frame_key = pixel_seed((uint32_t)(py * rw + px), X->s.rng_seed);
+    T->ray_kind = 0;
+    T->cnt->primary_rays++;
+    c3 c = trace_ray(T, cam, rd, &hi, 0, &found, &src, &shadowed);
+    if (out->argb) out->argb[o] = qrgb(f2i(c.r * 255), f2i(c.g * 255), f2i(c.b * 255));
+    if (out->rgba) {
+        out->rgba[4 * o] = c.r;
+        out->rgba[4 * o + 1] = c.g;
+        out->rgba[4 * o + 2] = c.b;
+        out->rgba[4 * o + 3] = T->alpha;
+    }
+    if (out->hit_id) out->hit_id[o] = found ? src : -1;
+    if (out->hit_t) out->hit_t[o] = hi.t;
+    if (out->shadow) out->shadow[o] = (uint8_t)(found && shadowed);
+    /* renderer.cpp:1104-1110: hits write the z / normal buffers; the others keep
+     * the cleared values (the UI clears both before every render, mainwindow.cpp:184-185) */
+    if (out->zbuf) out->zbuf[o] = found ? -(cam.z + rd.z * hi.t) : INFINITY;
+    if (out->nbuf) {
+        v3 nn = found ? hi.normal : V(0, 0, 0);
+        out->nbuf[3 * o] = nn.x;
+        out->nbuf[3 * o + 1] = nn.y;
+        out->nbuf[3 * o + 2] = nn.z;
+    }
+}
+
 /* Renderer::ray_trace, renderer.cpp:1068-1116, rows [row_begin, row_begin+row_count) */
 ORC_API int orc_render_rows(const struct orc_ctx *X, int row_begin, int row_count, orc_outputs *out,
                             orc_counters *counters, int nthreads)
@@ -1494,7 +1532,6 @@ ORC_API int orc_render_rows(const struct orc_ctx *X, int row_begin, int row_coun
     int rw = X->rw, rh = X->rh;
     if (row_begin < 0 || row_count < 0 || row_begin + row_count > rh)
         return -1;
-    v3 cam = V(X->sc.cam_pos[0], X->sc.cam_pos[1], X->sc.cam_pos[2]);
     orc_counters total;
     memset(&total, 0, sizeof(total));
 #ifdef _OPENMP
@@ -1514,40 +1551,55 @@ ORC_API int orc_render_rows(const struct orc_ctx *X, int row_begin, int row_coun
 #ifdef _OPENMP
 #pragma omp for schedule(dynamic)
 #endif
-        for (int py = row_begin; py < row_begin + row_count; py++) {
-            float y_world = ((float)py + 0.5f) / rh * 2 - 1;
-            for (int px = 0; px < rw; px++) {
-                float x_world = ((float)px + 0.5f) / rw * 2 - 1;
-                v3 vs = xform_point(X->sc.proj_inv, V(x_world, y_world, -1));
-                v3 ws = xform_point(X->sc.cam_to_world, vs);
-                v3 rd = vnormalize(vsub(ws, cam));
-                int found = 0, src = -1, shadowed = 0;
-                ohit hi = hit_fresh();
-                T.frame_key = pixel_seed((uint32_t)(py * rw + px), X->s.rng_seed);
-                T.ray_kind = 0;
-                local.primary_rays++;
-                c3 c = trace_ray(&T, cam, rd, &hi, 0, &found, &src, &shadowed);
-                size_t o = (size_t)(py - row_begin) * rw + px;
-                if (out->argb) out->argb[o] = qrgb(f2i(c.r * 255), f2i(c.g * 255), f2i(c.b * 255));
-                if (out->rgba) {
-                    out->rgba[4 * o] = c.r;
-                    out->rgba[4 * o + 1] = c.g;
-                    out->rgba[4 * o + 2] = c.b;
-                    out->rgba[4 * o + 3] = T.alpha;
-                }
-                if (out->hit_id) out->hit_id[o] = found ? src : -1;
-                if (out->hit_t) out->hit_t[o] = hi.t;
-                if (out->shadow) out->shadow[o] = (uint8_t)(found && shadowed);
-                /* renderer.cpp:1104-1110: hits write the z / normal buffers; the others keep
-                 * the cleared values (the UI clears both before every render, mainwindow.cpp:184-185) */
-                if (out->zbuf) out->zbuf[o] = found ? -(cam.z + rd.z * hi.t) : INFINITY;
-                if (out->nbuf) {
-                    v3 nn = found ? hi.normal : V(0, 0, 0);
-                    out->nbuf[3 * o] = nn.x;
-                    out->nbuf[3 * o + 1] = nn.y;
-                    out->nbuf[3 * o + 2] = nn.z;
-                }
-            }
+        for (int py = row_begin; py < row_begin + row_count; py++)
+            for (int px = 0; px < rw; px++)
+                render_pixel(&T, px, py, out, (size_t)(py - row_begin) * rw + px);
+#ifdef _OPENMP
+#pragma omp critical
+#endif
+        add_counters(&total, &local);
+    }
+    if (counters)
+        *counters = total;
+    return 0;
+}
+
+/* The same pixels for an arbitrary set of rows (rows[i] -> output rows i), spread over the
+ * threads in runs of 16 pixels: a few rows of an expensive frame (rough reflections) keep
+ * every thread busy.  Pixels are independent (path-keyed RNG), so the result equals
+ * orc_render_rows on each row. */
+ORC_API int orc_render_row_set(const struct orc_ctx *X, const int *rows, int nrows, orc_outputs *out,
+                               orc_counters *counters, int nthreads)
+{
+    int rw = X->rw, rh = X->rh;
+    for (int i = 0; i < nrows; i++)
+        if (rows[i] < 0 || rows[i] >= rh)
+            return -1;
+    orc_counters total;
+    memset(&total, 0, sizeof(total));
+    const int64_t runs = ((int64_t)rw + 15) / 16;
+#ifdef _OPENMP
+    if (nthreads <= 0)
+        nthreads = omp_get_max_threads();
+#pragma omp parallel num_threads(nthreads)
+#endif
+    {
+        orc_counters local;
+        memset(&local, 0, sizeof(local));
+        otracer T;
+        T.X = X;
+        T.cnt = &local;
+        T.ray_kind = 0;
+        T.rng = 1;
+        T.frame_key = 0;
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic)
+#endif
+        for (int64_t k = 0; k < (int64_t)nrows * runs; k++) {
+            const int i = (int)(k / runs);
+            const int px0 = (int)(k % runs) * 16;
+            for (int px = px0; px < px0 + 16 && px < rw; px++)
+                render_pixel(&T, px, rows[i], out, (size_t)i * rw + px);
         }
 #ifdef _OPENMP
 #pragma omp critical

@@ -54,14 +54,19 @@ class RtStats(C.Structure):
         ("octree_max_leaf", C.c_int64), ("octree_max_depth", C.c_int64),
         ("gpu_nodes", C.c_int64), ("gpu_tris", C.c_int64),
         ("render_width", C.c_int32), ("render_height", C.c_int32), ("seg_scale", C.c_float),
-        ("work", C.c_int64 * 4), ("deferred_pixels", C.c_int64), ("work_abandoned", C.c_int64 * 2),
-        ("work_wide", C.c_int64 * 4), ("uncertified", C.c_int64 * 6), ("exact_pixels", C.c_int64),
-        ("wave_steps", C.c_int64 * 6),
+        ("work", C.c_int64 * 4), ("work_wide", C.c_int64 * 4), ("uncertified", C.c_int64 * 6),
+        ("wave_steps", C.c_int64 * 6), ("build_split_ms", C.c_float * 4),
     ]
 
     def as_dict(self):
-        return {n: (float(getattr(self, n)) if t is C.c_float else
-                    [int(x) for x in getattr(self, n)] if n.startswith(("work", "wave")) or n == "uncertified" else int(getattr(self, n))) for n, t in self._fields_}
+        def conv(n, t):
+            v = getattr(self, n)
+            if t is C.c_float:
+                return float(v)
+            if isinstance(v, C.Array):
+                return [float(x) if n == "build_split_ms" else int(x) for x in v]
+            return int(v)
+        return {n: conv(n, t) for n, t in self._fields_}
 
 
 # every exported symbol and its ctypes signature (restype, argtypes); tests check

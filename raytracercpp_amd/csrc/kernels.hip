@@ -61,43 +61,16 @@ constexpr int BLOCK = 64 * WAVES_PER_BLOCK;
 #ifndef RT_OCC_PLAIN
 #define RT_OCC_PLAIN 4   // the plain kernel: 128 VGPRs (measured r02: 0.67 ms vs 0.71 at 5 waves, 0.69 at 3)
 #endif
-#ifndef RT_WW
-#define RT_WW 1
-#endif
-#ifndef RT_MT_EARLY
-#define RT_MT_EARLY 2
-#endif
 // RT_COUNT=1 (diagnostic builds only, tools/count_gpu_work.py): every traversal adds
 // its k-DOP and Moller-Trumbore test counts to P.counters[4..7] (whole-line queries:
 // 4 / 5, segment queries: 6 / 7), the work the kernel actually did
 #ifndef RT_COUNT
 #define RT_COUNT 0
 #endif
-#ifndef RT_WAVE_STATS
-#define RT_WAVE_STATS 0
-#endif
 // RT_PHASE_TIME=1 (diagnostic builds, tools/phase_time.py): shader cycles per wave spent in
 // each phase of the plain kernel's pixel loop (ph_mark), written to P.dbg
 #ifndef RT_PHASE_TIME
 #define RT_PHASE_TIME 0
-#endif
-#ifndef RT_OCC_PRIM
-#define RT_OCC_PRIM 5
-#endif
-#ifndef RT_OCC_SHADE
-#define RT_OCC_SHADE 5
-#endif
-#if RT_COUNT == 2
-// RT_COUNT=2 (tools/pixel_work.py): per-thread k-DOP / MT counts of the pixel being traced
-__device__ uint2 g_pixel_work[1 << 20];
-__device__ __forceinline__ uint32_t pixel_work_slot() { return (blockIdx.x * blockDim.x + threadIdx.x) & ((1u << 20) - 1); }
-#endif
-// software prefetch of the next child node / the next leaf triangle (A/B knobs)
-#ifndef RT_CHILD_PF
-#define RT_CHILD_PF 0
-#endif
-#ifndef RT_TRI_PF
-#define RT_TRI_PF 1
 #endif
 
 struct TRay {
@@ -257,22 +230,16 @@ __device__ __forceinline__ bool tri_test_rec(const TriRec& T, const TRay& R, flo
     v3 nd = -R.d;
     v3 m = cross(nd, OA);
     float Mdet = dot(n, nd);
-#if RT_MT_EARLY
     // coherent waves often reject a back-facing triangle together: skip the rest
     if (Mdet <= 0)
         return false;
-#endif
     float inv = 1 / Mdet;
     float u = dot(m, ac) * inv;
-#if RT_MT_EARLY >= 2
     if (u < 0 || u > 1)
         return false;
-#endif
     float v = dot(m, -ab) * inv;
-#if RT_MT_EARLY >= 2
     if (v < 0 || u + v > 1)
         return false;
-#endif
     float t = dot(n, OA) * inv;
     t_out = t;
     u_out = u;
@@ -429,65 +396,7 @@ struct Trav {
 #endif
 };
 
-// Ray groups.  In the deferred pass the 1 << P.grp_shift lanes of a
-// group trace the same ray in lockstep (identical inputs, identical decisions) and split
-// each leaf's triangles: lane g tests slots a + g, a + g + G, ...  Every lane folds its
-// hits as bvh.h:237-243 does, the group then takes the smallest (t, slot), and that
-// replaces h under the reference's own rule.  This equals the sequential fold whenever no
-// hit has t = NaN (t < h.t is then a total order and the first of equal t is the lowest
-// slot); a NaN hit anywhere in the leaf sends the whole group through the sequential loop.
-__device__ __forceinline__ void leaf_group(const KParams& P, const TRay& R, THit& h, uint32_t a, uint32_t end)
-{
-    const uint32_t G = 1u << P.grp_shift;
-    const uint32_t g = __lane_id() & (G - 1);
-    float bt = -1.0f, bu = 1.0f, bv = 0.0f;
-    int bk = -1;
-    int nan_hit = 0;
-    for (uint32_t k = a + g; k < end; k += G) {
-        float t, u, v;
-        if (tri_test(P.tris, k, R, t, u, v)) {
-            nan_hit |= t != t;
-            if (t < bt || bk < 0) {
-                bt = t;
-                bu = u;
-                bv = v;
-                bk = (int)k;
-            }
-        }
-    }
-    for (uint32_t off = 1; off < G; off <<= 1) {
-        float ot = __shfl_xor(bt, off), ou = __shfl_xor(bu, off), ov = __shfl_xor(bv, off);
-        int ok = __shfl_xor(bk, off);
-        nan_hit |= __shfl_xor(nan_hit, off);
-        if (ok >= 0 && (bk < 0 || ot < bt || (ot == bt && ok < bk))) {
-            bt = ot;
-            bu = ou;
-            bv = ov;
-            bk = ok;
-        }
-    }
-    if (nan_hit) {
-        for (uint32_t k = a; k < end; k++) {
-            float t, u, v;
-            if (tri_test(P.tris, k, R, t, u, v))
-                if (t < h.t || h.t == -1) {
-                    h.t = t;
-                    h.u = u;
-                    h.v = v;
-                    h.k = (int)k;
-                }
-        }
-        return;
-    }
-    if (bk >= 0 && (bt < h.t || h.t == -1)) {
-        h.t = bt;
-        h.u = bu;
-        h.v = bv;
-        h.k = bk;
-    }
-}
-
-template <bool SEG = false, bool GRP = false>
+template <bool SEG = false>
 __device__ __forceinline__ void trav_begin(const KParams& P, const TRay& R, THit& h, Trav& T)
 {
     h.t = -1.0f;
@@ -520,7 +429,7 @@ __device__ __forceinline__ void trav_begin(const KParams& P, const TRay& R, THit
     T.live = true;
 }
 
-template <bool SEG = false, bool GRP = false>
+template <bool SEG = false>
 __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit& h, Trav& T, uint2* lv)
 {
     uint32_t a = T.a, b = T.b;
@@ -535,31 +444,7 @@ __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit&
 #if RT_COUNT
         T.ntri += end - a;
 #endif
-        if (GRP)
-            leaf_group(P, R, h, a, end);
-        else {
         // triangles in leaf order, h updated as in bvh.h:237-243
-#if RT_TRI_PF >= 2
-        // the next two triangles' records are in flight while this one is tested
-        TriRec cur, nx1;
-        if (a < end)
-            cur = load_tri(P.tris, a);
-        if (a + 1 < end)
-            nx1 = load_tri(P.tris, a + 1);
-        for (uint32_t k = a; k < end; k++) {
-            TriRec nx2 = load_tri(P.tris, k + 2 < end ? k + 2 : k);
-            float t, u, v;
-            if (tri_test_rec(cur, R, t, u, v))
-                if (t < h.t || h.t == -1) {
-                    h.t = t;
-                    h.u = u;
-                    h.v = v;
-                    h.k = (int)k;
-                }
-            cur = nx1;
-            nx1 = nx2;
-        }
-#elif RT_TRI_PF
         // the next triangle's record is loaded while this one is tested
         TriRec cur;
         if (a < end)
@@ -576,19 +461,6 @@ __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit&
                 }
             cur = nxt;
         }
-#else
-        for (uint32_t k = a; k < end; k++) {
-            float t, u, v;
-            if (tri_test(P.tris, k, R, t, u, v))
-                if (t < h.t || h.t == -1) {
-                    h.t = t;
-                    h.u = u;
-                    h.v = v;
-                    h.k = (int)k;
-                }
-        }
-#endif
-        }
         r = h.t > 0;
     } else {
         // the k non-empty children are nodes a .. a+k-1, in octant order; a
@@ -598,23 +470,6 @@ __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit&
         T.nvol += k;
 #endif
         float key[8];
-#if RT_CHILD_PF
-        // child j + 1's node is loaded while child j is tested (k >= 1 for an inner node)
-        NodeBox cur = load_node(P.nodes, a);
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            key[j] = __int_as_float(0x7fc00000);
-            if ((uint32_t)j < k) {
-                NodeBox nxt = cur;
-                if ((uint32_t)(j + 1) < k)
-                    nxt = load_node(P.nodes, a + j + 1);
-                float t;
-                if (vol_test<SEG>(cur, R, t))
-                    key[j] = t;
-                cur = nxt;
-            }
-        }
-#else
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             key[j] = __int_as_float(0x7fc00000);
@@ -625,7 +480,6 @@ __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit&
                     key[j] = t;
             }
         }
-#endif
         // pop position of child j = number of hit children before it in a
         // stable sort by t_near; equal keys need the heap's own order
         uint32_t pos[8];
@@ -718,49 +572,24 @@ __device__ __forceinline__ void trav_step(const KParams& P, const TRay& R, THit&
     T.any_true = any_true;
 }
 
-// budget > 0: the query is abandoned (*aborted = true, h and the result meaningless) once
-// its inner-node visits plus leaf triangle slots exceed budget (deferred pixels, section 5.5)
-template <bool SEG = false, bool GRP = false>
-__device__ bool bvh_closest(const KParams& P, const TRay& R, THit& h, uint2* lv, uint32_t budget = 0,
-                            bool* aborted = nullptr)
+template <bool SEG = false>
+__device__ bool bvh_closest(const KParams& P, const TRay& R, THit& h, uint2* lv)
 {
     Trav T;
-    trav_begin<SEG, GRP>(P, R, h, T);
-#if RT_WW
+    trav_begin<SEG>(P, R, h, T);
     // while-while: lanes at inner nodes keep expanding until every lane of the
     // wave sits on a leaf (or is done), then the leaves are tested together
-    uint32_t cost = 0;
     while (T.live) {
-        while (T.live && !(T.b & LEAF_BIT)) {
-            trav_step<SEG, GRP>(P, R, h, T, lv);
-            cost++;
-        }
-        if (T.live) {
-            cost += T.b & ~LEAF_BIT;
-            trav_step<SEG, GRP>(P, R, h, T, lv);
-        }
-        if (budget && cost > budget && T.live) {
-            T.live = false;
-            *aborted = true;
-        }
+        while (T.live && !(T.b & LEAF_BIT))
+            trav_step<SEG>(P, R, h, T, lv);
+        if (T.live)
+            trav_step<SEG>(P, R, h, T, lv);
     }
-#else
-    while (T.live)
-        trav_step<SEG, GRP>(P, R, h, T, lv);
-#endif
 #if RT_COUNT
-    // a ray group's lanes run one query in lockstep: its work is counted once, by the
-    // group's lane 0 (T.ntri holds the whole leaf, which the group tests between them).
-    // Abandoned (budget-exceeded) queries go to counters[8..9], not to the executed work.
-    if (P.counters && (!GRP || (__lane_id() & ((1u << P.grp_shift) - 1)) == 0)) {
-        const bool ab = budget && *aborted;
-        atomicAdd(&P.counters[ab ? 8 : (SEG ? 6 : 4)], (unsigned long long)T.nvol);
-        atomicAdd(&P.counters[ab ? 9 : (SEG ? 7 : 5)], (unsigned long long)T.ntri);
+    if (P.counters) {
+        atomicAdd(&P.counters[SEG ? 6 : 4], (unsigned long long)T.nvol);
+        atomicAdd(&P.counters[SEG ? 7 : 5], (unsigned long long)T.ntri);
     }
-#endif
-#if RT_COUNT == 2
-    g_pixel_work[pixel_work_slot()].x += T.nvol;
-    g_pixel_work[pixel_work_slot()].y += T.ntri;
 #endif
     return T.r;
 }
@@ -786,14 +615,13 @@ __device__ __forceinline__ float seg_margin(const KParams& P, const TRay& R)
     return 0x1p-8f * P.seg_scale + 0x1p-14f * (P.seg_scale + om) / dmin;
 }
 
-template <bool GRP = false>
 __device__ __forceinline__ bool bvh_closest_seg(const KParams& P, TRay& R, THit& h, uint2* lv)
 {
-    bool r = bvh_closest<true, GRP>(P, R, h, lv);
+    bool r = bvh_closest<true>(P, R, h, lv);
     if (h.k >= 0 && !(h.t > 0.0f && h.t < INFINITY)) {
         R.lo = -INFINITY;
         R.hi = INFINITY;
-        r = bvh_closest<true, GRP>(P, R, h, lv);
+        r = bvh_closest<true>(P, R, h, lv);
     }
     return r;
 }
@@ -1072,8 +900,7 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
     WHit w;
 #if RT_COUNT
     uint32_t wk[4] = {0, 0, 0, 0};
-    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, INFINITY, true,
-                                P.wide_budget);
+    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, INFINITY, true);
     count_wave_steps(P, 22, wk[3]);
     if (P.counters) {
         atomicAdd(&P.counters[10], (unsigned long long)wk[0]);
@@ -1082,13 +909,9 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
             if ((wk[2] >> c) & 1u)
                 atomicAdd(&P.counters[16 + c], 1ull);   // uncertified, by reason (wbvh_closest)
     }
-#if RT_COUNT == 2
-    g_pixel_work[pixel_work_slot()].x += wk[0];
-    g_pixel_work[pixel_work_slot()].y += wk[1];
-#endif
 #else
     const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, INFINITY,
-                                true, P.wide_budget);
+                                true);
 #endif
     if (st == W_MISS) {
         h.t = -1.0f;
@@ -1139,8 +962,7 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
     WHit w;
 #if RT_COUNT
     uint32_t wk[4] = {0, 0, 0, 0};
-    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, hi, false,
-                                P.wide_budget);
+    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, hi, false);
     count_wave_steps(P, 25, wk[3]);
     if (P.counters) {
         atomicAdd(&P.counters[10], (unsigned long long)wk[0]);
@@ -1149,13 +971,8 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
             if ((wk[2] >> c) & 1u)
                 atomicAdd(&P.counters[16 + c], 1ull);   // uncertified, by reason (wbvh_closest)
     }
-#if RT_COUNT == 2
-    g_pixel_work[pixel_work_slot()].x += wk[0];
-    g_pixel_work[pixel_work_slot()].y += wk[1];
-#endif
 #else
-    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, hi, false,
-                                P.wide_budget);
+    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, hi, false);
 #endif
     if (st == W_MISS) {
         *sh = false;
@@ -1201,11 +1018,8 @@ __device__ __forceinline__ bool shapes_shadow(const KParams& P, v3 o, v3 d, floa
 }
 
 // renderer.cpp:340-402
-// WIDE (the lean wide-BVH kernel; launched only with segment queries on, so the scene
-// has no analytic shapes): the decision comes from wide_shadow, or *defer is set and the
-// pixel goes to the exact pass -- no octree traversal is compiled in.
-template <bool GRP = false, bool WIDE = false, bool PLAIN = false>
-__device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv, bool* defer = nullptr)
+template <bool PLAIN = false>
+__device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
 {
     if (!P.compute_shadows)
         return false;
@@ -1227,16 +1041,12 @@ __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv, bool
         }
         // (seg_scale > 0: no analytic shapes, so shapes_shadow below has nothing to add)
         bool sh;
-        if (!GRP && P.wnodes && P.nnodes > 0 && !nan && wide_shadow(P, o, d, hi, p, lp, lv, &sh))
+        if (P.wnodes && P.nnodes > 0 && !nan && wide_shadow(P, o, d, hi, p, lp, lv, &sh))
             return sh;
-        if (WIDE) {
-            *defer = true;
-            return false;
-        }
         TRay R = make_ray(P, opaque(o), opaque(d));
         R.lo = -m;
         R.hi = hi;
-        r = bvh_closest_seg<GRP>(P, R, h, lv);
+        r = bvh_closest_seg(P, R, h, lv);
         if (r) {
             v3 q = o + d * h.t;
             if (length2(p - q) < length2(p - lp))
@@ -1249,21 +1059,13 @@ __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv, bool
     TRay R = make_ray(P, o, d);
     if (P.enable_bvh) {
         // whole-line query (segment queries off)
-        if (WIDE) {
-            *defer = true;
-            return false;
-        }
-        r = bvh_closest<false, GRP>(P, R, h, lv);
+        r = bvh_closest<false>(P, R, h, lv);
         if (r) {
             v3 q = o + d * h.t;
             if (length2(p - q) < length2(p - lp))
                 return true;
         }
     } else {
-        if (WIDE) {
-            *defer = true;
-            return false;
-        }
         h.t = -1.0f;
         for (int k = 0; k < P.ntri_slots; k++) {
             float t, u, v;
@@ -1313,26 +1115,16 @@ __device__ __forceinline__ void shapes_closest(const KParams& P, v3 o, v3 d, Rec
 // Closest hit over the BVH then the analytic shapes (renderer.cpp:1015-1037).
 // fin is the caller's HitInfo; returns the source (-1 none, >=0 triangle, -2-k shape k).
 // With the wide BVH (P.wnodes), a certified query takes its answer; one it cannot certify
-// is deferred to the ray-group pass (budget > 0) or traced through the octree here.
-// WIDE: only the wide BVH is compiled in; an uncertified query sets *aborted (deferred).
-template <bool GRP = false, bool WIDE = false, bool PLAIN = false>
-__device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv, uint32_t budget = 0,
-                           bool* aborted = nullptr)
+// is traced through the octree here.
+template <bool PLAIN = false>
+__device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv)
 {
     Rec local = rec_fresh();
     int src = -1;
-    if (WIDE) {
+    if (P.enable_bvh) {
         THit h;
         bool r = false;
-        if (!(P.enable_bvh && P.nnodes > 0 && !ray_is_nan(o, d) && wide_closest(P, o, d, h, r, lv))) {
-            *aborted = true;
-            return -1;
-        }
-        bvh_record(P, h, r, local, fin, src);
-    } else if (P.enable_bvh) {
-        THit h;
-        bool r = false;
-        const bool wide = !GRP && P.wnodes && P.nnodes > 0 && !ray_is_nan(o, d);
+        const bool wide = P.wnodes && P.nnodes > 0 && !ray_is_nan(o, d);
         if (wide && wide_closest(P, o, d, h, r, lv, &local)) {
             // certified: a hit's record is already in local (a miss leaves it fresh)
             if (r && (local.t < fin.t || fin.t == -1)) {
@@ -1340,14 +1132,8 @@ __device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv, ui
                 src = local.tri;
             }
         } else {
-            if (wide && budget) {
-                *aborted = true;   // not certified: the deferred pass traces it through the octree
-                return -1;
-            }
             TRay R = make_ray(P, opaque(o), opaque(d));
-            r = bvh_closest<false, GRP>(P, R, h, lv, budget, aborted);
-            if (budget && *aborted)
-                return -1;
+            r = bvh_closest<false>(P, R, h, lv);
             bvh_record(P, h, r, local, fin, src);
         }
     } else {
@@ -1473,9 +1259,8 @@ __device__ c3 shade_debug(const KParams& P, const Rec& h)
     return fc;
 }
 
-template <bool GRP = false, bool WIDE = false, bool PLAIN = false>
-__device__ Direct shade_direct(const KParams& P, v3 ro, v3 rd, Rec& h, uint2* lv, unsigned& nshadow,
-                               bool* defer = nullptr)
+template <bool PLAIN = false>
+__device__ Direct shade_direct(const KParams& P, v3 ro, v3 rd, Rec& h, uint2* lv, unsigned& nshadow)
 {
     Direct out;
     out.shadowed = false;
@@ -1486,7 +1271,7 @@ __device__ Direct shade_direct(const KParams& P, v3 ro, v3 rd, Rec& h, uint2* lv
             nshadow++;
         v3 light = mk(P.light[0], P.light[1], P.light[2]);
         if (PLAIN) PH_MARK(3);
-        out.shadowed = is_shadowed<GRP, WIDE, PLAIN>(P, out.ip, h.normal, light, lv, defer);
+        out.shadowed = is_shadowed<PLAIN>(P, out.ip, h.normal, light, lv);
         if (PLAIN) PH_MARK(4);
         out.fc = shade_shadow_emit(P, fc, mat_of(P, h.mat), out.shadowed);
     } else
@@ -1587,35 +1372,24 @@ struct PixelOut {
     Rec fin;
     int src;
     bool found, shadowed;
-    bool deferred;   // the primary query exceeded the budget: nothing else was computed
 };
 
 // Renderer::trace_ray (renderer.cpp:1008-1066) for one primary ray, with the
 // compute_reflection recursion (when REFL) unrolled onto an explicit stack.
-// WIDE (REFL false): the lean wide-BVH kernel; any query the wide BVH cannot certify sets
-// po.deferred and the pixel is re-done from scratch by the exact pass (its shadow ray is
-// counted there, not here).
-template <bool REFL, bool GRP = false, bool WIDE = false, bool PLAIN = false>
+template <bool REFL, bool PLAIN = false>
 __device__ PixelOut trace_pixel(const KParams& P, v3 cam, v3 rd0, uint2* lv, uint32_t pixel_key, unsigned& nshadow,
-                                unsigned& nrefl, uint32_t budget = 0)
+                                unsigned& nrefl)
 {
     PixelOut po;
     po.fin = rec_fresh();
-    po.found = po.shadowed = po.deferred = false;
+    po.found = po.shadowed = false;
     po.alpha = 1.0f;
-    po.src = closest_hit<GRP, WIDE && !REFL, PLAIN && !REFL>(P, cam, rd0, po.fin, lv, REFL ? 0u : budget,
-                                                             &po.deferred);
+    po.src = closest_hit<PLAIN && !REFL>(P, cam, rd0, po.fin, lv);
     if (PLAIN) PH_MARK(2);
     if (!REFL) {
-        if (po.deferred)
-            return po;
         if (po.fin.t > 0.1f) {
             po.found = true;
-            unsigned ns = 0;
-            Direct D = shade_direct<GRP, WIDE, PLAIN>(P, cam, rd0, po.fin, lv, ns, &po.deferred);
-            if (po.deferred)
-                return po;
-            nshadow += ns;
+            Direct D = shade_direct<PLAIN>(P, cam, rd0, po.fin, lv, nshadow);
             po.shadowed = D.shadowed;
             po.color = PLAIN || P.shading_method == RT_SHADING
                            ? shade_finish(P, D.fc, mat_of(P, po.fin.mat), col(0, 0, 0))
@@ -1789,15 +1563,7 @@ __device__ __forceinline__ int global_row(const KParams& P, int lr)
 // band's rays share that XCD's L2) and moves to the next shard when its own is empty;
 // it is done once it has found all eight empty.  One head word serves ~88 dequeues per
 // microsecond (MI355X_MICROARCH.md, dequeue row), under the frame's 130K tiles at ~2 ms.
-#ifndef RT_BLOCK_QUEUE
-#define RT_BLOCK_QUEUE 1   // the block's waves share one dequeue per 4 tiles (below)
-#endif
-#ifndef RT_BQ_BATCH
-#define RT_BQ_BATCH 4      // tickets per block dequeue (<= 255)
-#endif
-struct TileQueue {
-    int shard, empty;
-};
+constexpr int BQ_BATCH = 4;   // tickets per block dequeue (<= 255)
 
 // Ticket t of shard s -> tile index (row-major), or -1 past the shard's end.  Measured
 // against alternatives (r02): guided chunks of 2-4 adjacent tiles per wave dequeue, tickets
@@ -1809,17 +1575,7 @@ __device__ __forceinline__ int shard_tile(const KParams& P, int s, int t)
     return t < (r1 - r0) * P.tiles_x ? r0 * P.tiles_x + t : -1;
 }
 
-// tile of ticket t on shard s (natural or probe order), or -1 past the shard's end
-__device__ __forceinline__ int ticket_tile(const KParams& P, int s, int t, int ntiles)
-{
-    if (P.tile_order) {
-        const int pos = s + TILE_SHARDS * t;
-        return pos < ntiles ? (int)(ldg(P.tile_order + pos) & TILE_ID_MASK) : -1;
-    }
-    return shard_tile(P, s, t);
-}
 
-#if RT_BLOCK_QUEUE
 // Block-shared dequeue.  One global atomic takes WAVES_PER_BLOCK consecutive tickets of the
 // block's shard, and the block's waves hand them out among themselves through one LDS word
 //   bit 31 done | bits 30..24 generation | bits 23..16 tickets in the batch | bits 15..0 next;
@@ -1846,9 +1602,7 @@ __device__ __forceinline__ void tile_queue_init()
     __syncthreads();
 }
 
-__device__ __forceinline__ TileQueue tile_queue_begin() { return TileQueue{0, 0}; }
-
-__device__ __forceinline__ int tile_queue_next(const KParams& P, TileQueue&, int ntiles)
+__device__ __forceinline__ int tile_queue_next(const KParams& P)
 {
     const int lane = threadIdx.x & 63;
     for (;;) {
@@ -1861,7 +1615,7 @@ __device__ __forceinline__ int tile_queue_next(const KParams& P, TileQueue&, int
         const unsigned int g = (w >> 24) & 0x7fu, c = (w >> 16) & 0xffu, i = w & 0xffffu;
         if (i < c) {
             const int slot = (int)(g & 3u);
-            return ticket_tile(P, g_bq.sh[slot], g_bq.base[slot] + (int)i, ntiles);
+            return shard_tile(P, g_bq.sh[slot], g_bq.base[slot] + (int)i);
         }
         if (i == c) {
             // this wave refills: WAVES_PER_BLOCK tickets of the first non-empty shard
@@ -1869,11 +1623,11 @@ __device__ __forceinline__ int tile_queue_next(const KParams& P, TileQueue&, int
             while (empty < TILE_SHARDS) {
                 int t = 0;
                 if (lane == 0)
-                    t = (int)atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[P.tq_base + 16 * shard]),
-                                       (unsigned)RT_BQ_BATCH);
+                    t = (int)atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[NCOUNTERS + 16 * shard]),
+                                       (unsigned)BQ_BATCH);
                 b = __builtin_amdgcn_readfirstlane(t);
                 n = 0;
-                while (n < RT_BQ_BATCH && ticket_tile(P, shard, b + n, ntiles) >= 0)
+                while (n < BQ_BATCH && shard_tile(P, shard, b + n) >= 0)
                     n++;
                 if (n > 0)
                     break;
@@ -1890,7 +1644,7 @@ __device__ __forceinline__ int tile_queue_next(const KParams& P, TileQueue&, int
                 __hip_atomic_store(&g_bq.word, n > 0 ? (g1 << 24) | ((unsigned)n << 16) | 1u : 0x80000000u,
                                    __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-            return n > 0 ? ticket_tile(P, shard, b, ntiles) : -1;
+            return n > 0 ? shard_tile(P, shard, b) : -1;
         }
         // another wave is taking the next batch
         for (;;) {
@@ -1903,83 +1657,6 @@ __device__ __forceinline__ int tile_queue_next(const KParams& P, TileQueue&, int
             __builtin_amdgcn_s_sleep(2);
         }
     }
-}
-#else
-__device__ __forceinline__ void tile_queue_init() {}
-
-__device__ __forceinline__ TileQueue tile_queue_begin() { return TileQueue{(int)(blockIdx.x & (TILE_SHARDS - 1)), 0}; }
-
-// next tile for the calling wave (wave-uniform), or -1 when every shard is empty.  With
-// P.tile_order (tiles sorted by estimated cost, heaviest first: tile_probe_kernel) shard s
-// takes sorted positions s, s + 8, s + 16, ... so every shard starts on heavy tiles.
-__device__ __forceinline__ int tile_queue_next(const KParams& P, TileQueue& q, int ntiles)
-{
-    const int lane = threadIdx.x & 63;
-    while (q.empty < TILE_SHARDS) {
-        int t = 0;
-        if (lane == 0)
-            t = (int)atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[P.tq_base + 16 * q.shard]), 1u);
-        t = __builtin_amdgcn_readfirstlane(t);
-        const int tile = ticket_tile(P, q.shard, t, ntiles);
-        if (tile >= 0)
-            return tile;
-        q.empty++;
-        q.shard = (q.shard + 1) & (TILE_SHARDS - 1);
-    }
-    return -1;
-}
-#endif
-
-// Tile cost probe (the tile order above).  One ray per tile, through the tile's centre
-// pixel, is traced through the wide BVH with a small iteration budget; its node visits +
-// triangle tests (capped) estimate the tile's work.  Silhouette tiles, whose grazing rays
-// are the frame's longest, probe high.  The order changes only when tiles start, never
-// what they compute.
-__global__ __launch_bounds__(BLOCK) void tile_probe_kernel(KParams P, uint32_t* cost)
-{
-    extern __shared__ uint2 lds_levels[];
-    uint2* lv = lds_levels + threadIdx.x;
-    const int ntiles = P.tiles_x * P.tiles_y;
-    const int tile = blockIdx.x * BLOCK + threadIdx.x;
-    if (tile >= ntiles)
-        return;
-    const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
-    const int px = min(tx * 8 + 4, P.rw - 1);
-    const int lr = min(ty * 8 + 4, P.local_rows - 1);
-    const int py = min(global_row(P, lr), P.rh - 1);
-    const v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
-    float y_world = ((float)py + 0.5f) / P.rh * 2 - 1;
-    float x_world = ((float)px + 0.5f) / P.rw * 2 - 1;
-    v3 vs = xform_point(P.proj_inv, mk(x_world, y_world, -1));
-    v3 ws = xform_point(P.cam_to_world, vs);
-    v3 rd = normalize(ws - cam);
-    const float om = fmaxf(fabsf(cam.x), fmaxf(fabsf(cam.y), fabsf(cam.z)));
-    WStackLds stk{lv};
-    WHit w;
-    uint32_t wk[4] = {0, 0, 0, 0};
-    wbvh_closest(P.wnodes, P.wtris, cam, rd, 0x1p-16f * (om + P.scene_scale), stk, w, wk, INFINITY, true,
-                 TILE_PROBE_BUDGET);
-    cost[tile] = wk[0] + wk[1];
-}
-
-// sort keys: the largest probe cost among the tile and its 8 neighbours (a silhouette
-// crosses neighbouring tiles), descending, then the tile index
-__global__ __launch_bounds__(BLOCK) void tile_key_kernel(KParams P, const uint32_t* cost, uint32_t* keys)
-{
-    const int ntiles = P.tiles_x * P.tiles_y;
-    const int tile = blockIdx.x * BLOCK + threadIdx.x;
-    if (tile >= ntiles)
-        return;
-    const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
-    uint32_t c = 0;
-    for (int dy = -1; dy <= 1; dy++)
-        for (int dx = -1; dx <= 1; dx++) {
-            const int x = tx + dx, y = ty + dy;
-            if (x >= 0 && x < P.tiles_x && y >= 0 && y < P.tiles_y)
-                c = max(c, cost[y * P.tiles_x + x]);
-        }
-    c = min(c, TILE_COST_MAX);
-    keys[tile] = ((TILE_COST_MAX - c) << TILE_ID_BITS) | (uint32_t)tile;
 }
 
 // ImageUtils::downscale_image_qt_ARGB32 (imageUtils.h:98-147) fused into the tile: the
@@ -2013,21 +1690,17 @@ __device__ __forceinline__ void downscale_tile(const KParams& P, int lane, int l
 // queue (tile_queue_next): shadow-ray-heavy tiles cluster around the object, so
 // a static block -> tile (-> XCD) mapping leaves whole XCDs idle while others
 // still trace; dynamic pulling keeps every CU busy until the queue drains.
-// WIDE: the lean kernel (wide BVH only) -- pixels it cannot certify go to
-// the deferred list and the exact pass (ray_trace_defer_kernel).
 // PLAIN: no texture map, sky, analytic shape, debug shading or SSAO buffer (host-checked,
 // KParams::plain): those code paths are compiled out.
-template <bool REFL, bool WIDE = false, bool PLAIN = false>
+template <bool REFL, bool PLAIN = false>
 __global__ __launch_bounds__(BLOCK, PLAIN ? RT_OCC_PLAIN : RT_OCC) void ray_trace_kernel(KParams P)
 {
     extern __shared__ uint2 lds_levels[];
     uint2* lv = lds_levels + threadIdx.x;
     int lane = threadIdx.x & 63;
-    const int ntiles = P.tiles_x * P.tiles_y;
     v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
     unsigned nshadow = 0, nrefl = 0;
     tile_queue_init();
-    TileQueue q = tile_queue_begin();
 #if RT_PHASE_TIME
     if (PLAIN && lane == 0) {
         for (int k = 0; k < 7; k++)
@@ -2035,20 +1708,11 @@ __global__ __launch_bounds__(BLOCK, PLAIN ? RT_OCC_PLAIN : RT_OCC) void ray_trac
         g_phase[threadIdx.x >> 6][7] = __builtin_amdgcn_s_memtime();
     }
 #endif
-#if RT_WAVE_STATS
-    // diagnostic: per wave {first dequeue tick, exit tick, tiles, sum of tile ticks}
-    const uint64_t w_begin = wall_clock64();
-    uint64_t w_busy = 0, w_tiles = 0;
-#endif
     for (;;) {
-        const int tile = tile_queue_next(P, q, ntiles);
+        const int tile = tile_queue_next(P);
         if (PLAIN) PH_MARK(6);
         if (tile < 0)
             break;
-#if RT_WAVE_STATS
-        const uint64_t w_t0 = wall_clock64();
-        w_tiles++;
-#endif
         int tx, ty;
         tile_xy(P, tile, tx, ty);
         int px = tx * 8 + (lane & 7);
@@ -2067,43 +1731,15 @@ __global__ __launch_bounds__(BLOCK, PLAIN ? RT_OCC_PLAIN : RT_OCC) void ray_trac
         if (PLAIN) PH_MARK(1);
 
         uint32_t rng = REFL ? pixel_seed((uint32_t)(py * P.rw + px), P.rng_seed) : 0u;
-#if RT_TILE_TIME
-        const uint64_t t_start = wall_clock64();
-#endif
-#if RT_COUNT == 2
-        g_pixel_work[pixel_work_slot()] = make_uint2(0u, 0u);
-#endif
-        PixelOut po = trace_pixel<REFL, false, WIDE, PLAIN>(P, cam, rd, lv, rng, nshadow, nrefl,
-                                                            REFL ? 0u : P.trav_budget);
+        PixelOut po = trace_pixel<REFL, PLAIN>(P, cam, rd, lv, rng, nshadow, nrefl);
         size_t o = (size_t)lr * P.rw + px;
-        if (!REFL && po.deferred) {
-            // the deferred pass (ray_trace_defer_kernel) traces it with a ray group; the
-            // host sizes defer_cap >= the launch's pixels, and a pixel defers at most once
-            uint32_t idx = atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[P.defer_head]), 1u);
-            P.defer[idx] = (uint32_t)o;
-            continue;
-        }
-
         if (P.argb) P.argb[o] = color_to_argb(po.color);
         if (!REFL && P.ds_out) downscale_tile(P, lane, lr, px, color_to_argb(po.color));
         if (P.rgba) P.rgba[o] = make_float4(po.color.r, po.color.g, po.color.b, po.alpha);
         if (P.hit_id) P.hit_id[o] = po.found ? po.src : -1;
-#if RT_TILE_TIME
-        // diagnostic build: hit_t holds the pixel's trace time in wall-clock ticks, rgba.w its
-        // start tick (low 32 bits, as raw bits)
-        if (P.hit_t) P.hit_t[o] = (float)(wall_clock64() - t_start);
-        if (P.rgba) P.rgba[o].w = __uint_as_float((uint32_t)t_start);
-#elif RT_COUNT == 2
-        if (P.hit_t) P.hit_t[o] = (float)g_pixel_work[pixel_work_slot()].x;
-        if (P.argb) P.argb[o] = g_pixel_work[pixel_work_slot()].y;
-#else
         if (P.hit_t) P.hit_t[o] = po.fin.t;
-#endif
         if (P.shadow) P.shadow[o] = (uint8_t)(po.found && po.shadowed);
         if (!PLAIN && P.zbuf) write_ssao_buffers(P, o, po.found, cam, rd, po.fin);
-#if RT_WAVE_STATS
-        w_busy += wall_clock64() - w_t0;
-#endif
         if (PLAIN) PH_MARK(5);
     }
 #if RT_PHASE_TIME
@@ -2115,420 +1751,8 @@ __global__ __launch_bounds__(BLOCK, PLAIN ? RT_OCC_PLAIN : RT_OCC) void ray_trac
                 P.dbg[DBG_WORDS * wid + k] = g_phase[threadIdx.x >> 6][k];
     }
 #endif
-#if RT_WAVE_STATS
-    {
-        const int wid = (int)(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
-        if (P.dbg && lane == 0 && wid < DBG_WAVES) {
-            P.dbg[DBG_WORDS * wid + 0] = w_begin;
-            P.dbg[DBG_WORDS * wid + 1] = wall_clock64();
-            P.dbg[DBG_WORDS * wid + 2] = w_tiles;
-            P.dbg[DBG_WORDS * wid + 3] = w_busy;
-        }
-    }
-#endif
     if (nshadow) atomicAdd(&P.counters[0], (unsigned long long)nshadow);
     if (nrefl) atomicAdd(&P.counters[1], (unsigned long long)nrefl);
-}
-
-// ---- Split frame ----
-// Pass 1 (primary_kernel): per pixel, the primary ray's closest hit through the wide BVH
-// and its certificate, stored as a PrimRec.  Pass 2 (shade_kernel): the rest of trace_ray
-// from that record -- shading, the shadow ray through the wide BVH, the framebuffer.  The
-// pixels either pass cannot certify are rendered from scratch by the exact pass
-// (ray_trace_defer_kernel): pass 1's on a second stream while pass 2 runs, pass 2's after
-// it.  Each pass holds only its own state, so neither spills the traversal's registers.
-__device__ __forceinline__ v3 primary_dir(const KParams& P, int px, int py, v3 cam)
-{
-    // ray generation, renderer.cpp:1086-1098
-    float y_world = ((float)py + 0.5f) / P.rh * 2 - 1;
-    float x_world = ((float)px + 0.5f) / P.rw * 2 - 1;
-    v3 vs = xform_point(P.proj_inv, mk(x_world, y_world, -1));
-    v3 ws = xform_point(P.cam_to_world, vs);
-    return normalize(ws - cam);
-}
-
-__global__ __launch_bounds__(BLOCK, RT_OCC_PRIM) void primary_kernel(KParams P)
-{
-    extern __shared__ uint2 lds_levels[];
-    uint2* lv = lds_levels + threadIdx.x;
-    const int lane = threadIdx.x & 63;
-    const int ntiles = P.tiles_x * P.tiles_y;
-    const v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
-    tile_queue_init();
-    TileQueue q = tile_queue_begin();
-    for (;;) {
-        const int tile = tile_queue_next(P, q, ntiles);
-        if (tile < 0)
-            break;
-        int tx, ty;
-        tile_xy(P, tile, tx, ty);
-        const int px = tx * 8 + (lane & 7);
-        const int lr = ty * 8 + (lane >> 3);
-        const int py = lr < P.local_rows ? global_row(P, lr) : P.rh;
-        if (px >= P.rw || py >= P.rh)
-            continue;
-        const v3 rd = primary_dir(P, px, py, cam);
-        PrimRec rec;
-        rec.t = -1.0f;
-        rec.u = 1.0f;
-        rec.v = 0.0f;
-        rec.k = PRIM_MISS;
-        if (P.nnodes > 0) {
-            THit h;
-            bool r;
-            if (ray_is_nan(cam, rd)) {
-                rec.t = __int_as_float(0x7fc00000);
-                rec.k = PRIM_NAN;
-            } else if (wide_closest(P, cam, rd, h, r, lv)) {
-                rec.t = h.t;
-                rec.u = h.u;
-                rec.v = h.v;
-                rec.k = h.k >= 0 ? h.k : PRIM_MISS;
-            } else {
-                rec.k = PRIM_EXACT;
-                uint32_t idx = atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[P.defer_head]), 1u);
-                P.defer[idx] = (uint32_t)(lr * P.rw + px);
-            }
-        }
-        reinterpret_cast<float4*>(P.prim)[(size_t)lr * P.rw + px] = make_float4(rec.t, rec.u, rec.v, __int_as_float(rec.k));
-    }
-}
-
-__global__ __launch_bounds__(BLOCK, RT_OCC_SHADE) void shade_kernel(KParams P)
-{
-    extern __shared__ uint2 lds_levels[];
-    uint2* lv = lds_levels + threadIdx.x;
-    const int lane = threadIdx.x & 63;
-    const int ntiles = P.tiles_x * P.tiles_y;
-    const v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
-    unsigned nshadow = 0;
-    tile_queue_init();
-    TileQueue q = tile_queue_begin();
-    for (;;) {
-        const int tile = tile_queue_next(P, q, ntiles);
-        if (tile < 0)
-            break;
-        int tx, ty;
-        tile_xy(P, tile, tx, ty);
-        const int px = tx * 8 + (lane & 7);
-        const int lr = ty * 8 + (lane >> 3);
-        const int py = lr < P.local_rows ? global_row(P, lr) : P.rh;
-        if (px >= P.rw || py >= P.rh)
-            continue;
-        const size_t o = (size_t)lr * P.rw + px;
-        const float4 pr = ldg(reinterpret_cast<const float4*>(P.prim) + o);
-        const int32_t k = __float_as_int(pr.w);
-        if (k == PRIM_EXACT)
-            continue;   // the exact pass renders it
-        const v3 rd = primary_dir(P, px, py, cam);
-        // trace_ray's closest hit (renderer.cpp:1015-1020) from the record, as closest_hit
-        PixelOut po;
-        po.fin = rec_fresh();
-        po.found = po.shadowed = po.deferred = false;
-        po.alpha = 1.0f;
-        {
-            THit h;
-            h.t = pr.x;
-            h.u = pr.y;
-            h.v = pr.z;
-            h.k = k >= 0 ? k : -1;
-            Rec local = rec_fresh();
-            int src = -1;
-            bvh_record(P, h, k >= 0, local, po.fin, src);
-            shapes_closest(P, cam, rd, local, po.fin, src);
-            po.src = src;
-        }
-        // everything but the colour and the shadow flag is final before the shadow ray: write it
-        // now, so that only the shading colour stays live across the shadow traversal
-        po.found = po.fin.t > 0.1f;
-        if (P.hit_id) P.hit_id[o] = po.found ? po.src : -1;
-        if (!po.found) {
-            po.color = miss_color(P, rd, po.alpha);
-            if (P.hit_t) P.hit_t[o] = po.fin.t;
-            if (P.argb) P.argb[o] = color_to_argb(po.color);
-            if (P.rgba) P.rgba[o] = make_float4(po.color.r, po.color.g, po.color.b, po.alpha);
-            if (P.shadow) P.shadow[o] = 0;
-            if (P.zbuf) write_ssao_buffers(P, o, false, cam, rd, po.fin);
-            continue;
-        }
-        if (P.shading_method != RT_SHADING) {
-            po.color = clamp3(shade_debug(P, po.fin));
-            if (P.hit_t) P.hit_t[o] = po.fin.t;
-            if (P.argb) P.argb[o] = color_to_argb(po.color);
-            if (P.rgba) P.rgba[o] = make_float4(po.color.r, po.color.g, po.color.b, 1.0f);
-            if (P.shadow) P.shadow[o] = 0;
-            if (P.zbuf) write_ssao_buffers(P, o, true, cam, rd, po.fin);
-            continue;
-        }
-        // shade_direct (RT_SHADING), renderer.cpp:556-593
-        v3 ip;
-        const c3 lit = shade_lit(P, cam, rd, po.fin, ip);
-        if (P.hit_t) P.hit_t[o] = po.fin.t;
-        if (P.zbuf) write_ssao_buffers(P, o, true, cam, rd, po.fin);   // normal-mapped normal
-        const int mat = po.fin.mat;
-        const v3 nrm = po.fin.normal;
-        const v3 light = mk(P.light[0], P.light[1], P.light[2]);
-        bool defer = false;
-        const bool sh = is_shadowed<false, true>(P, ip, nrm, light, lv, &defer);
-        if (defer) {
-            uint32_t idx = atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[P.defer_head]), 1u);
-            P.defer[idx] = (uint32_t)o;
-            continue;
-        }
-        if (P.compute_shadows)
-            nshadow++;
-        const float* m = mat_of(P, mat);
-        const c3 color = shade_finish(P, shade_shadow_emit(P, lit, m, sh), m, col(0, 0, 0));
-        if (P.argb) P.argb[o] = color_to_argb(color);
-        if (P.rgba) P.rgba[o] = make_float4(color.r, color.g, color.b, 1.0f);
-        if (P.shadow) P.shadow[o] = (uint8_t)sh;
-    }
-    if (nshadow) atomicAdd(&P.counters[0], (unsigned long long)nshadow);
-}
-
-// The deferred pass: every pixel whose primary query exceeded
-// P.trav_budget in ray_trace_kernel is traced again from the start by a ray group of
-// 1 << P.grp_shift lanes (leaf_group); the group's lane 0 writes the pixel.
-__global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_defer_kernel(KParams P)
-{
-    extern __shared__ uint2 lds_levels[];
-    uint2* lv = lds_levels + threadIdx.x;
-    const uint32_t n = min(*reinterpret_cast<const unsigned int*>(&P.counters[P.defer_in_head]), P.defer_cap);
-    const int gs = P.grp_shift;
-    const uint32_t g = threadIdx.x & ((1u << gs) - 1);
-    const uint32_t stride = (gridDim.x * (uint32_t)BLOCK) >> gs;
-    v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
-    unsigned nshadow = 0, nrefl = 0;
-    for (uint32_t i = (blockIdx.x * (uint32_t)BLOCK + threadIdx.x) >> gs; i < n; i += stride) {
-        const uint32_t o = P.defer_in[i];
-        const int lr = (int)(o / (uint32_t)P.rw), px = (int)(o % (uint32_t)P.rw);
-        const int py = global_row(P, lr);
-        // ray generation, renderer.cpp:1086-1098 (as ray_trace_kernel)
-        float y_world = ((float)py + 0.5f) / P.rh * 2 - 1;
-        float x_world = ((float)px + 0.5f) / P.rw * 2 - 1;
-        v3 vs = xform_point(P.proj_inv, mk(x_world, y_world, -1));
-        v3 ws = xform_point(P.cam_to_world, vs);
-        v3 rd = normalize(ws - cam);
-        unsigned ns = 0;
-        PixelOut po = trace_pixel<false, true>(P, cam, rd, lv, 0u, ns, nrefl, 0u);
-        if (g != 0)
-            continue;
-        nshadow += ns;
-        if (P.argb) P.argb[o] = color_to_argb(po.color);
-        if (P.rgba) P.rgba[o] = make_float4(po.color.r, po.color.g, po.color.b, po.alpha);
-        if (P.hit_id) P.hit_id[o] = po.found ? po.src : -1;
-        if (P.hit_t) P.hit_t[o] = po.fin.t;
-        if (P.shadow) P.shadow[o] = (uint8_t)(po.found && po.shadowed);
-        if (P.zbuf) write_ssao_buffers(P, o, po.found, cam, rd, po.fin);
-    }
-    if (nshadow) atomicAdd(&P.counters[0], (unsigned long long)nshadow);
-}
-
-// The heavy-pixel pass of the lean kernel: pixels whose wide-BVH queries
-// exceeded P.wide_budget there (silhouette rays that graze many boxes) are traced again,
-// one lane per pixel and without a budget, so that a wave holds 64 heavy rays instead of
-// one heavy ray among 63 finished lanes; what the wide BVH cannot certify goes on to the
-// exact pass (ray_trace_defer_kernel) through P.defer.
-__global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_retry_kernel(KParams P)
-{
-    extern __shared__ uint2 lds_levels[];
-    uint2* lv = lds_levels + threadIdx.x;
-    const uint32_t n = min(*reinterpret_cast<const unsigned int*>(&P.counters[P.defer_in_head]), P.defer_cap);
-    v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
-    unsigned nshadow = 0, nrefl = 0;
-    for (uint32_t i = blockIdx.x * (uint32_t)BLOCK + threadIdx.x; i < n; i += gridDim.x * (uint32_t)BLOCK) {
-        const uint32_t o = P.defer_in[i];
-        const int lr = (int)(o / (uint32_t)P.rw), px = (int)(o % (uint32_t)P.rw);
-        const int py = global_row(P, lr);
-        float y_world = ((float)py + 0.5f) / P.rh * 2 - 1;
-        float x_world = ((float)px + 0.5f) / P.rw * 2 - 1;
-        v3 vs = xform_point(P.proj_inv, mk(x_world, y_world, -1));
-        v3 ws = xform_point(P.cam_to_world, vs);
-        v3 rd = normalize(ws - cam);
-        PixelOut po = trace_pixel<false, false, true>(P, cam, rd, lv, 0u, nshadow, nrefl, 0u);
-        if (po.deferred) {
-            uint32_t idx = atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[P.defer_head]), 1u);
-            P.defer[idx] = o;
-            continue;
-        }
-        if (P.argb) P.argb[o] = color_to_argb(po.color);
-        if (P.rgba) P.rgba[o] = make_float4(po.color.r, po.color.g, po.color.b, po.alpha);
-        if (P.hit_id) P.hit_id[o] = po.found ? po.src : -1;
-        if (P.hit_t) P.hit_t[o] = po.fin.t;
-        if (P.shadow) P.shadow[o] = (uint8_t)(po.found && po.shadowed);
-        if (P.zbuf) write_ssao_buffers(P, o, po.found, cam, rd, po.fin);
-    }
-    if (nshadow) atomicAdd(&P.counters[0], (unsigned long long)nshadow);
-}
-
-// Pixel q of the launch (tile-major: q = tile * 64 + 8 * y + x inside the 8x8
-// tile) -> column and launch-local row.
-__device__ __forceinline__ void tile_pixel(const KParams& P, uint32_t q, int& px, int& lr)
-{
-    uint32_t tile = q >> 6, w = q & 63u;
-    px = (int)(tile % (uint32_t)P.tiles_x) * 8 + (int)(w & 7u);
-    lr = (int)(tile / (uint32_t)P.tiles_x) * 8 + (int)(w >> 3);
-}
-
-__device__ __forceinline__ void write_pixel(const KParams& P, uint32_t q, c3 c, float alpha, int id, float t, bool sh)
-{
-    int px, lr;
-    tile_pixel(P, q, px, lr);
-    size_t o = (size_t)lr * P.rw + px;
-    if (P.argb) P.argb[o] = color_to_argb(c);
-    if (P.rgba) P.rgba[o] = make_float4(c.r, c.g, c.b, alpha);
-    if (P.hit_id) P.hit_id[o] = id;
-    if (P.hit_t) P.hit_t[o] = t;
-    if (P.shadow) P.shadow[o] = (uint8_t)sh;
-}
-
-#ifndef RT_REFILL
-#define RT_REFILL 1
-#endif
-
-// Renderer::ray_trace for scenes without reflections (BVH on), as a per-lane
-// pipeline.  Every lane owns one pixel at a time and walks it through
-//   PRIM: primary-ray traversal -> trace_ray's closest hit + shade_lit
-//   SHAD: shadow-ray traversal  -> is_shadowed + emission + ambient -> framebuffer
-// and takes the next pixel as soon as its own pixel is written.  Both ray kinds
-// advance through the same trav_step, one octree node per lane per iteration,
-// so a wave never idles while one lane's ray is still deep in the octree (the
-// tile-per-wave kernel runs every tile for as long as its slowest ray).  Pixels
-// are handed out in tile order from the device-scope queue, 64 per atomic, so
-// the rays in flight in one wave stay spatially coherent.  Per pixel the
-// results are those of trace_pixel<false>: the same functions in the same order.
-enum : int { ST_IDLE = 0, ST_PRIM = 1, ST_SHAD = 2, ST_NEW = 3, ST_EXIT = 4 };
-
-__global__ __launch_bounds__(BLOCK, RT_OCC) void ray_trace_pipe_kernel(KParams P)
-{
-    extern __shared__ uint2 lds_levels[];
-    uint2* lv = lds_levels + threadIdx.x;
-    const int lane = threadIdx.x & 63;
-    const uint32_t ntiles = (uint32_t)(P.tiles_x * P.tiles_y);
-    const v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
-    const v3 light = mk(P.light[0], P.light[1], P.light[2]);
-    unsigned nshadow = 0;
-
-    int stage = ST_IDLE;
-    bool drained = false;        // wave-uniform: the pixel queue is empty
-    uint32_t cur = 0, end = 0;   // wave-uniform: unassigned pixels [cur, end) of the wave's tile
-    uint32_t q = 0;              // this lane's pixel
-    TRay R;
-    THit h;
-    Trav T;
-    T.live = false;
-    // state carried from the primary hit to the end of its shadow ray
-    v3 ip = mk(0, 0, 0);
-    c3 fc = col(0, 0, 0);
-    int mat = 0, src = -1;
-    float fin_t = 0.0f;
-
-    for (;;) {
-        // ---- a traversal has returned ----
-        if (stage == ST_PRIM && !T.live) {
-            Rec fin = rec_fresh(), local = rec_fresh();
-            int s = -1;
-            bvh_record(P, h, T.r, local, fin, s);
-            shapes_closest(P, cam, R.d, local, fin, s);
-            if (fin.t > 0.1f) {
-                if (P.shading_method == RT_SHADING) {
-                    fc = shade_lit(P, cam, R.d, fin, ip);
-                    mat = fin.mat;
-                    src = s;
-                    fin_t = fin.t;
-                    if (P.compute_shadows) {
-                        // is_shadowed (renderer.cpp:340-345): the shadow ray's query
-                        nshadow++;
-                        R = make_ray(P, ip + fin.normal * 1.0e-4f, normalize(light - ip));
-                        trav_begin(P, R, h, T);
-                        stage = ST_SHAD;
-                    } else {
-                        const float* m = mat_of(P, mat);
-                        write_pixel(P, q, shade_finish(P, shade_shadow_emit(P, fc, m, false), m, col(0, 0, 0)), 1.0f,
-                                    src, fin_t, false);
-                        stage = ST_IDLE;
-                    }
-                } else {
-                    write_pixel(P, q, clamp3(shade_debug(P, fin)), 1.0f, s, fin.t, false);
-                    stage = ST_IDLE;
-                }
-            } else {
-                float alpha;
-                c3 c = miss_color(P, R.d, alpha);
-                write_pixel(P, q, c, alpha, -1, fin.t, false);
-                stage = ST_IDLE;
-            }
-        } else if (stage == ST_SHAD && !T.live) {
-            // is_shadowed (renderer.cpp:346-401) on the finished query
-            bool sh = false;
-            if (T.r) {
-                v3 qq = R.o + R.d * h.t;
-                sh = length2(ip - qq) < length2(ip - light);
-            }
-            if (!sh)
-                sh = shapes_shadow(P, R.o, R.d, h.t, ip, light);
-            const float* m = mat_of(P, mat);
-            write_pixel(P, q, shade_finish(P, shade_shadow_emit(P, fc, m, sh), m, col(0, 0, 0)), 1.0f, src, fin_t, sh);
-            stage = ST_IDLE;
-        }
-
-        // ---- hand out pixels to idle lanes (wave-uniform control flow) ----
-        uint64_t idle = __ballot(stage == ST_IDLE);
-        if (idle && !drained && (__popcll(idle) >= RT_REFILL || __ballot(T.live) == 0)) {
-            for (;;) {
-                if (cur >= end) {
-                    uint32_t t = 0;
-                    if (lane == 0)
-                        t = atomicAdd(reinterpret_cast<unsigned int*>(&P.counters[2]), 1u);
-                    t = __builtin_amdgcn_readfirstlane(t);
-                    if (t >= ntiles) {
-                        drained = true;
-                        break;
-                    }
-                    cur = t * 64u;
-                    end = cur + 64u;
-                }
-                uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
-                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                uint32_t avail = end - cur;
-                if (stage == ST_IDLE && rank < avail) {
-                    q = cur + rank;
-                    stage = ST_NEW;
-                }
-                uint32_t n = (uint32_t)__popcll(idle);
-                cur += n < avail ? n : avail;
-                idle = __ballot(stage == ST_IDLE);
-                if (!idle)
-                    break;
-            }
-        }
-        if (drained && stage == ST_IDLE)
-            stage = ST_EXIT;
-        if (stage == ST_NEW) {
-            int px, lr;
-            tile_pixel(P, q, px, lr);
-            int py = lr < P.local_rows ? global_row(P, lr) : P.rh;
-            if (px < P.rw && py < P.rh) {
-                // ray generation, renderer.cpp:1086-1098
-                float y_world = ((float)py + 0.5f) / P.rh * 2 - 1;
-                float x_world = ((float)px + 0.5f) / P.rw * 2 - 1;
-                v3 vs = xform_point(P.proj_inv, mk(x_world, y_world, -1));
-                v3 ws = xform_point(P.cam_to_world, vs);
-                R = make_ray(P, cam, normalize(ws - cam));
-                trav_begin(P, R, h, T);
-                stage = ST_PRIM;
-            } else
-                stage = drained ? ST_EXIT : ST_IDLE;   // tile padding
-        }
-        if (__ballot(stage != ST_EXIT) == 0)
-            break;
-
-        // ---- one octree node for every lane with a ray in flight ----
-        if (T.live)
-            trav_step(P, R, h, T, lv);
-    }
-    if (nshadow)
-        atomicAdd(&P.counters[0], (unsigned long long)nshadow);
 }
 
 // ===========================================================================
@@ -3642,50 +2866,6 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_trace_rays
     return hipGetLastError();
 }
 
-extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_tile_probe(const rt::KParams* P, uint32_t* cost,
-                                                                                uint32_t* keys, hipStream_t stream)
-{
-    int ntiles = P->tiles_x * P->tiles_y;
-    if (ntiles <= 0)
-        return hipSuccess;
-    dim3 g((ntiles + rt::BLOCK - 1) / rt::BLOCK);
-    hipLaunchKernelGGL(rt::tile_probe_kernel, g, dim3(rt::BLOCK), rt::lds_bytes(*P), stream, *P, cost);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess)
-        return e;
-    hipLaunchKernelGGL(rt::tile_key_kernel, g, dim3(rt::BLOCK), 0, stream, *P, cost, keys);
-    return hipGetLastError();
-}
-
-// split frame: pass 1 (stage 0), pass 2 (stage 1), the exact pass over a list (stage 2:
-// list P->defer_in, count counters[P->defer_in_head])
-extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_split(int stage, const rt::KParams* P,
-                                                                           hipStream_t stream)
-{
-    const int tiles = P->tiles_x * P->tiles_y;
-    int blocks = (tiles + rt::WAVES_PER_BLOCK - 1) / rt::WAVES_PER_BLOCK;
-    if (blocks > P->max_blocks && P->max_blocks > 0)
-        blocks = P->max_blocks;
-    if (blocks < 1)
-        return hipSuccess;
-    const size_t lds = rt::lds_bytes(*P);
-    rt::KParams A = *P;
-    if (stage == 0) {
-        A.tq_base = rt::NCOUNTERS;
-        A.grp_shift = 0;
-        hipLaunchKernelGGL(rt::primary_kernel, dim3(blocks), dim3(rt::BLOCK), lds, stream, A);
-    } else if (stage == 1) {
-        A.tq_base = rt::NCOUNTERS2;
-        A.grp_shift = 0;
-        hipLaunchKernelGGL(rt::shade_kernel, dim3(blocks), dim3(rt::BLOCK), lds, stream, A);
-    } else {
-        // few pixels (ties, stack overflows): a small grid, so that it fits beside the shade pass
-        const int db = 256;
-        hipLaunchKernelGGL(rt::ray_trace_defer_kernel, dim3(db), dim3(rt::BLOCK), lds, stream, A);
-    }
-    return hipGetLastError();
-}
-
 // ---- host-side launch wrappers (called from renderer.cpp) ----
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(const rt::KParams* P, hipStream_t stream)
 {
@@ -3694,53 +2874,19 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(
     // persistent waves: enough blocks to fill every CU (surplus blocks find the queue empty)
     if (blocks > P->max_blocks && P->max_blocks > 0)
         blocks = P->max_blocks;
+    if (blocks < 1)
+        return hipSuccess;
     size_t lds = rt::lds_bytes(*P);
     if (P->has_reflection)
         hipLaunchKernelGGL((rt::ray_trace_kernel<true, false>), dim3(blocks), dim3(rt::BLOCK), lds, stream, *P);
-    else if (P->enable_bvh && P->pipeline)
-        hipLaunchKernelGGL(rt::ray_trace_pipe_kernel, dim3(blocks), dim3(rt::BLOCK), lds, stream, *P);
-    else {
-        rt::KParams A = *P;
-        A.grp_shift = 0;   // one lane per pixel; the groups are the deferred pass's
-        A.defer_head = 3;
-        A.tq_base = rt::NCOUNTERS;
-        const int db = P->max_blocks > 0 ? P->max_blocks : 1024;
-        if (P->wide_lean && P->defer && P->defer2 && P->defer_cap) {
-            // lean kernel (list 1: over-budget or uncertified pixels, head counters[3]) -> heavy-pixel
-            // pass (list 2: uncertified, head counters[13]) -> exact ray-group pass over list 2
-            if (P->plain && !P->zbuf && !P->nbuf)
-                hipLaunchKernelGGL((rt::ray_trace_kernel<false, true, true>), dim3(blocks), dim3(rt::BLOCK), lds, stream, A);
-            else
-                hipLaunchKernelGGL((rt::ray_trace_kernel<false, true>), dim3(blocks), dim3(rt::BLOCK), lds, stream, A);
-            rt::KParams B = *P;
-            B.wide_budget = 0;
-            B.defer_in = P->defer;
-            B.defer_in_head = 3;
-            B.defer = P->defer2;
-            B.defer_head = 13;
-            hipLaunchKernelGGL(rt::ray_trace_retry_kernel, dim3(db), dim3(rt::BLOCK), lds, stream, B);
-            rt::KParams C = *P;
-            C.defer_in = P->defer2;
-            C.defer_in_head = 13;
-            hipLaunchKernelGGL(rt::ray_trace_defer_kernel, dim3(db), dim3(rt::BLOCK), lds, stream, C);
-        } else {
-            // the plain kernel's grid is exactly its residency (RT_OCC_PLAIN blocks of 4 waves per
-            // CU): with two frames in flight, surplus blocks of one frame would be dispatched ahead
-            // of the next frame's only to find the queue empty (C4 +1.3%: r02_bench98_*.log)
-            const int pblocks = P->max_blocks > 0 ? std::max(1, std::min(blocks, P->max_blocks / 8 * RT_OCC_PLAIN)) : blocks;
-            if (P->plain && !P->zbuf && !P->nbuf)
-                hipLaunchKernelGGL((rt::ray_trace_kernel<false, false, true>), dim3(pblocks), dim3(rt::BLOCK), lds, stream, A);
-            else
-                hipLaunchKernelGGL((rt::ray_trace_kernel<false, false>), dim3(blocks), dim3(rt::BLOCK), lds, stream, A);
-            if (P->defer && P->defer_cap) {
-                // deferred pixels: a persistent grid of ray groups over the list ray_trace_kernel left
-                rt::KParams C = *P;
-                C.defer_in = P->defer;
-                C.defer_in_head = 3;
-                hipLaunchKernelGGL(rt::ray_trace_defer_kernel, dim3(db), dim3(rt::BLOCK), lds, stream, C);
-            }
-        }
-    }
+    else if (P->plain && !P->zbuf && !P->nbuf) {
+        // the plain kernel's grid is exactly its residency (RT_OCC_PLAIN blocks of 4 waves per
+        // CU): with two frames in flight, surplus blocks of one frame would be dispatched ahead
+        // of the next frame's only to find the queue empty (C4 +1.3%: r02_bench98_*.log)
+        const int pblocks = P->max_blocks > 0 ? std::max(1, std::min(blocks, P->max_blocks / 8 * RT_OCC_PLAIN)) : blocks;
+        hipLaunchKernelGGL((rt::ray_trace_kernel<false, true>), dim3(pblocks), dim3(rt::BLOCK), lds, stream, *P);
+    } else
+        hipLaunchKernelGGL((rt::ray_trace_kernel<false, false>), dim3(blocks), dim3(rt::BLOCK), lds, stream, *P);
     return hipGetLastError();
 }
 

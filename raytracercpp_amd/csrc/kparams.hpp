@@ -13,18 +13,9 @@ constexpr int TEX_SLOTS = 6;   // ao, diffuse, normal, displacement, roughness, 
 constexpr int MAT_STRIDE = 16; // see include/rt_mi355x.h
 constexpr int MAX_SHAPES = 64;
 constexpr int NCOUNTERS = 32;  // KParams::counters entries (u64) before the tile-queue heads
-#ifndef RT_TILE_SHARDS
-#define RT_TILE_SHARDS 8
-#endif
-constexpr int TILE_SHARDS = RT_TILE_SHARDS;   // tile-queue shards (blockIdx % TILE_SHARDS; a power of 2)
-constexpr int NCOUNTERS2 = NCOUNTERS + 16 * TILE_SHARDS;      // a second set of heads (split frame's shade pass)
-constexpr int NCOUNTER_WORDS = NCOUNTERS2 + 16 * TILE_SHARDS;  // one 128-B line per shard head
-// tile order (kernels.hip tile_probe_kernel): key = (TILE_COST_MAX - cost) << TILE_ID_BITS | tile
-constexpr uint32_t TILE_ID_BITS = 20;
-constexpr uint32_t TILE_ID_MASK = (1u << TILE_ID_BITS) - 1;
-constexpr uint32_t TILE_COST_MAX = 2047;
-constexpr uint32_t TILE_PROBE_BUDGET = 96;
-constexpr int DBG_WAVES = 16384;   // per-wave diagnostic records (RT_WAVE_STATS / RT_PHASE_TIME builds)
+constexpr int TILE_SHARDS = 8;  // tile-queue shards (blockIdx % TILE_SHARDS; a power of 2; r02: 16 was slower)
+constexpr int NCOUNTER_WORDS = NCOUNTERS + 16 * TILE_SHARDS;  // one 128-B line per shard head
+constexpr int DBG_WAVES = 16384;   // per-wave diagnostic records (RT_PHASE_TIME builds)
 constexpr int DBG_WORDS = 8;       // u64 words per record
 
 enum TexSlot { TEX_AO = 0, TEX_DIFFUSE = 1, TEX_NORMAL = 2, TEX_DISPLACEMENT = 3, TEX_ROUGHNESS = 4, TEX_SKYSPHERE = 5 };
@@ -34,15 +25,6 @@ struct KTex {
     const float4* px;   // row-major texels (Image, tp2/src/image.h:20-135), nullptr when absent
     int w, h;
 };
-
-// Split frame: the primary pass's record of one pixel
-struct PrimRec {
-    float t, u, v;
-    int32_t k;   // >= 0: the certified hit's GTri slot; PRIM_MISS / PRIM_NAN / PRIM_EXACT
-};
-constexpr int32_t PRIM_MISS = -1;    // certified: no triangle hit (BVH::intersect returns false)
-constexpr int32_t PRIM_EXACT = -2;   // not certified: the exact pass renders the pixel
-constexpr int32_t PRIM_NAN = -3;     // NaN ray: NaN record, returns false (trav_begin)
 
 struct KParams {
     // geometry (flattened octree, octree.hpp)
@@ -93,8 +75,7 @@ struct KParams {
     int32_t parallax_mapping_steps;
     int32_t enable_roughness_mapping, enable_skysphere, enable_skybox;
     uint32_t rng_seed;
-    int32_t has_reflection;   // RT_SHADING with a material whose reflection > 0: recursive kernel
-    int32_t pipeline;         // per-lane pipelined kernel for the non-recursive case (RT_PIPELINE=1; default 0)
+    int32_t has_reflection;   // RT_SHADING with a material whose reflection > 0: the reflection engine
     float seg_scale;          // > 0: shadow / reflection queries are segment queries (kernels.hip seg_margin),
                               // the scene's largest |coordinate|; 0: every query walks the whole line
 
@@ -105,23 +86,8 @@ struct KParams {
     int32_t local_rows;       // rows in this launch's (padded) local buffers
     int32_t tiles_x, tiles_y; // 8x8 tiles over (rw, local_rows)
     int32_t max_blocks;       // persistent grid size (CUs x resident blocks per CU)
-    const uint32_t* tile_order;   // tiles in descending estimated cost (low TILE_ID_BITS bits), or nullptr
-    // Deferred pixels (kernels.hip "Ray groups").  trav_budget > 0: a primary query whose
-    // traversal work exceeds it is abandoned and its pixel appended to defer[] (count in
-    // counters[3]); the deferred pass then traces each such pixel with 1 << grp_shift lanes
-    // that split every leaf's triangles between them.  0 / 0: off.
-    uint32_t trav_budget;
-    int32_t grp_shift;
-    int32_t wide_lean;        // 1: the lean wide-BVH kernel, everything it cannot certify deferred (needs defer[])
     int32_t plain;            // 1: no texture map, sky, analytic shape, debug shading or SSAO buffers
                               // (ray_trace_kernel's plain specialisation)
-    uint32_t* defer;          // output list of deferred pixels, head counters[defer_head]
-    uint32_t defer_cap;
-    int32_t defer_head;
-    const uint32_t* defer_in; // input list of a deferred pass, count counters[defer_in_head]
-    int32_t defer_in_head;
-    uint32_t* defer2;         // lean mode: the second list (pixels the wide BVH cannot certify)
-    uint32_t wide_budget;     // lean kernel: wide-BVH loop iterations per query before it is deferred (0: none)
 
     // outputs, indexed by local_row * rw + px (nullptr = not requested)
     uint32_t* argb;
@@ -129,17 +95,15 @@ struct KParams {
     int32_t* hit_id;
     float* hit_t;
     uint8_t* shadow;
-    unsigned long long* counters;   // [NCOUNTERS]: [0] shadow rays, [1] reflection rays, [2] tile queue head,
-                                    // [3] deferred-pixel list head, [4..7] executed k-DOP / MT tests of
-                                    // whole-line / segment queries and [8..9] of abandoned queries, [10..11]
-                                    // wide-BVH node visits / triangle tests, [12] uncertified queries (RT_COUNT),
-                                    // [13] head of the lean mode's second deferred list, [14] certificate k-DOP
-                                    // tests, [16..21] uncertified queries by reason (RT_COUNT: overflow, NaN,
-                                    // overflowed-only, tie, t outside (0, inf), certificate failed);
-                                    // then the tile-queue heads, shard s at counters[NCOUNTERS + 16 s]
-    unsigned long long* dbg;        // diagnostic builds (RT_WAVE_STATS): per wave [DBG_WAVES][DBG_WORDS], else nullptr
-    PrimRec* prim;            // split frame: one record per launch pixel (lr * rw + px), else nullptr
-    int32_t tq_base;          // first counters[] word of this launch's tile-queue heads (NCOUNTERS or NCOUNTERS2)
+    unsigned long long* counters;   // [NCOUNTERS]: [0] shadow rays, [1] reflection rays, [2] tile queue head
+                                    // (reflection / raster kernels), [4..7] executed k-DOP / MT tests of
+                                    // whole-line / segment queries, [10..11] wide-BVH node visits / triangle
+                                    // tests, [12] uncertified queries, [14] certificate k-DOP tests, [16..21]
+                                    // uncertified queries by reason (overflow, NaN, overflowed-only, tie, t
+                                    // outside (0, inf), certificate failed), [22..27] wide-BVH loop iterations
+                                    // (all but [0..2]: RT_COUNT builds only); then the tile-queue heads,
+                                    // shard s at counters[NCOUNTERS + 16 s]
+    unsigned long long* dbg;        // diagnostic builds (RT_PHASE_TIME): per wave [DBG_WAVES][DBG_WORDS], else nullptr
     // SSAO inputs (enable_ssao): Renderer::_z_buffer / _normal_buffer, renderer.cpp:1107-1110, 975-979
     float* zbuf;
     float4* nbuf;

@@ -13,10 +13,6 @@
 #include "host_scene.hpp"
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(const rt::KParams* P, hipStream_t stream);
-extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_split(int stage, const rt::KParams* P,
-                                                                           hipStream_t stream);
-extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_tile_probe(const rt::KParams* P, uint32_t* cost,
-                                                                                uint32_t* keys, hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_level0(const rt::KParams* P, rt::FrameRec* fr1,
                                                                            unsigned int* nfr1, hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_stage(int stage, const rt::KParams* P,
@@ -67,7 +63,33 @@ hipError_t DevBuf::reserve(size_t n)
     return hipSuccess;
 }
 
-Renderer::Renderer(int device) : device_(device)
+// each switch is on unless its variable is set to 0 (RT_DEBUG_WAVES: on when set)
+Knobs Knobs::from_env()
+{
+    Knobs k;
+    auto on = [](const char* name, bool dflt) {
+        const char* v = getenv(name);
+        return v ? v[0] != '0' : dflt;
+    };
+    k.wbvh = on("RT_WBVH", true);
+    k.seg = on("RT_SEG", true);
+    k.cones = on("RT_CONES", true);
+    k.lslab = on("RT_LSLAB", true);
+    k.plain = on("RT_PLAIN", true);
+    k.fused_ssaa = on("RT_FUSED_SSAA", true);
+    k.refl_engine = on("RT_REFL_ENGINE", true);
+    k.refl_sort = on("RT_REFL_SORT", true);
+    k.refl_fuse = on("RT_REFL_FUSE", true);
+    k.debug_waves = getenv("RT_DEBUG_WAVES") != nullptr;
+    if (const char* ce = getenv("RT_REFL_CHUNK_LOG2")) {
+        const int v = atoi(ce);
+        if (v >= 10 && v <= 25)   // small values (tests): many chunks per level
+            k.refl_chunk_log2 = v;
+    }
+    return k;
+}
+
+Renderer::Renderer(int device) : knobs_(Knobs::from_env()), device_(device)
 {
     rt_default_settings(&s_);
     mat::identity(c2w_);
@@ -95,10 +117,10 @@ int Renderer::init(std::string& err)
         return RT_EHIP;
     }
     DevBuf* all[] = {&d_nodes_, &d_tris_,  &d_tri_id_, &d_tri_mat_, &d_tri_uv_, &d_mats_,   &d_internal_,
-                     &d_image_, &d_rgba_,  &d_hit_id_, &d_hit_t_,   &d_shadow_, &d_counters_, &d_defer_,
+                     &d_image_, &d_rgba_,  &d_hit_id_, &d_hit_t_,   &d_shadow_, &d_counters_,
                      &d_tri9_,  &d_rcount_, &d_roff_,  &d_pieces_,  &d_piece_uv_, &d_zkey_, &d_big_, &d_scan_tmp_,
                      &d_zbuf_,  &d_nbuf_,   &d_ao_,     &d_cones_, &d_lslab_, &d_wnodes_, &d_wtris_, &d_wmeta_,
-                     &d_defer2_, &d_tile_sort_, &d_tile_sort_tmp_, &d_dbg_, &d_prim_};
+                     &d_dbg_};
     for (DevBuf* b : all) b->device = device_;
     for (auto& b : d_tex_) b.device = device_;
     for (auto& b : d_sky_) b.device = device_;
@@ -112,9 +134,8 @@ Renderer::~Renderer()
         if (e) hipEventDestroy(e);
     for (auto& e : ring_)
         if (e) hipEventDestroy(e);
-    if (fork_) hipEventDestroy(fork_);
-    if (join_) hipEventDestroy(join_);
-    if (stream2_) hipStreamDestroy(stream2_);
+    for (auto& b : band_slot_)
+        if (b.done) hipEventDestroy(b.done);
     if (stream_) hipStreamDestroy(stream_);
 }
 
@@ -499,8 +520,13 @@ int Renderer::ensure_device_scene()
     hipError_t e = hipSetDevice(device_);
     if (e != hipSuccess)
         return hip_fail(e, "hipSetDevice");
+    // frames still in flight on other streams read the buffers replaced below
+    if ((geom_dirty_ || mats_dirty_ || tex_dirty_) && sync_slots() != RT_OK)
+        return RT_EHIP;
     if (geom_dirty_) {
-        auto t0 = std::chrono::steady_clock::now();
+        using clk = std::chrono::steady_clock;
+        auto ms_since = [](clk::time_point t) { return std::chrono::duration<float, std::milli>(clk::now() - t).count(); };
+        auto t0 = clk::now();
         int64_t n = (int64_t)tri_mat_.size();
         for (float c : tri_)
             if (!std::isfinite(c))
@@ -528,18 +554,23 @@ int Renderer::ensure_device_scene()
                 oct_.tri_id[(size_t)i] = (int32_t)i;
             }
         }
+        build_split_ms_[0] = ms_since(t0);
+        auto t1 = clk::now();
         if (s_.enable_bvh)
             leaf_cones(oct_, cones_, lslab_);
         else {
             cones_.clear();
             lslab_.clear();
         }
-        // the wide BVH (wbvh.hpp): RT_WBVH=0 (at build time) skips it
-        const char* wenv = getenv("RT_WBVH");
-        if (s_.enable_bvh && !(wenv && wenv[0] == '0'))
+        build_split_ms_[1] = ms_since(t1);
+        // the wide BVH (wbvh.hpp): RT_WBVH=0 skips it
+        auto t2 = clk::now();
+        if (s_.enable_bvh && knobs_.wbvh)
             build_wbvh(oct_, wb_);
         else
             wb_ = WBvh();
+        build_split_ms_[2] = ms_since(t2);
+        auto t3 = clk::now();
         if (!wb_.nodes.empty()) {
             // per wide-BVH triangle, everything a certified hit needs in one 16-B load: the
             // octree slot (the record's triangle), the leaf of its certificate, the caller's
@@ -592,7 +623,8 @@ int Renderer::ensure_device_scene()
             return hip_fail(e, "upload (scene)");
         geom_dirty_ = false;
         tri9_dirty_ = true;
-        build_ms_ = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        build_split_ms_[3] = ms_since(t3);
+        build_ms_ = ms_since(t0);
     }
     if (mats_dirty_) {
         if ((e = d_mats_.reserve(mats_.size() * 4)) != hipSuccess)
@@ -671,10 +703,9 @@ void Renderer::fill_params(KParams& P) const
     P.tri_id = d_tri_id_.as<int32_t>();
     P.tri_mat = d_tri_mat_.as<int32_t>();
     P.tri_uv = tri_uv_.empty() ? nullptr : d_tri_uv_.as<float>();
-    const char* cone_env = getenv("RT_CONES");   // RT_CONES=0: every leaf's triangles are tested
-    P.cones = (cones_.empty() || (cone_env && cone_env[0] == '0')) ? nullptr : d_cones_.as<float>();
-    const char* slab_env = getenv("RT_LSLAB");   // RT_LSLAB=0: no leaf slabs (they read the cone axis)
-    P.lslab = (!P.cones || lslab_.empty() || (slab_env && slab_env[0] == '0')) ? nullptr : d_lslab_.as<float>();
+    P.cones = (cones_.empty() || !knobs_.cones) ? nullptr : d_cones_.as<float>();
+    // (the leaf slabs read the cone axis)
+    P.lslab = (!P.cones || lslab_.empty() || !knobs_.lslab) ? nullptr : d_lslab_.as<float>();
     P.scene_scale = 0.0f;
     if (!oct_.nodes.empty())
         for (int c = 0; c < 3; c++)
@@ -682,8 +713,7 @@ void Renderer::fill_params(KParams& P) const
     // wide BVH: closest-hit queries certified against the octree, when it
     // was built, the scene's scale keeps the certificate's rounding margins (as for the
     // segment queries), and RT_WBVH is not 0
-    const char* wenv = getenv("RT_WBVH");
-    if (!wb_.nodes.empty() && !(wenv && wenv[0] == '0') && P.scene_scale > 0x1p-20f && P.scene_scale < 0x1p20f) {
+    if (!wb_.nodes.empty() && knobs_.wbvh && P.scene_scale > 0x1p-20f && P.scene_scale < 0x1p20f) {
         P.wnodes = d_wnodes_.as<WNode>();
         P.wtris = d_wtris_.as<GTri>();
         P.wmeta = d_wmeta_.as<uint4>();
@@ -733,16 +763,12 @@ void Renderer::fill_params(KParams& P) const
     P.enable_skybox = s_.enable_skybox;
     P.rng_seed = s_.rng_seed;
     P.has_reflection = s_.shading_method == RT_SHADING && any_reflection(mats_);
-    // RT_PIPELINE=1 selects the per-lane pipelined kernel instead of the tile-per-wave one (A/B runs)
-    const char* pipe_env = getenv("RT_PIPELINE");
-    P.pipeline = pipe_env && pipe_env[0] == '1' && !s_.enable_ssao;
     // segment queries (RT_SEG=0 turns them off): only when the
     // queries' results depend on the triangles alone (analytic shapes read the stale
     // record) and the scene's scale keeps Moller-Trumbore's products far from overflow
     // and underflow, so that the rounding bound of seg_margin holds
     P.seg_scale = 0.0f;
-    const char* seg_env = getenv("RT_SEG");
-    if (!(seg_env && seg_env[0] == '0') && P.nshape == 0 && !oct_.nodes.empty()) {
+    if (knobs_.seg && P.nshape == 0 && !oct_.nodes.empty()) {
         const GNode& root = oct_.nodes[0];
         float S = 0.0f;
         for (int a = 0; a < 3; a++)   // the axis slabs are the vertices' coordinate range
@@ -751,10 +777,8 @@ void Renderer::fill_params(KParams& P) const
             P.seg_scale = S;
     }
     P.max_blocks = num_cus_ * 8;   // persistent grids: 8 blocks per CU (the plain kernel: its residency)
-    P.tq_base = NCOUNTERS;
     // the plain specialisation (RT_PLAIN=0 turns it off); SSAO (zbuf) is checked at launch
-    const char* plain_env = getenv("RT_PLAIN");
-    P.plain = !(plain_env && plain_env[0] == '0') && P.shading_method == RT_SHADING && P.nshape == 0 &&
+    P.plain = knobs_.plain && P.shading_method == RT_SHADING && P.nshape == 0 &&
               !P.enable_ao_mapping && !P.enable_diffuse_mapping && !P.enable_normal_mapping &&
               !P.enable_displacement_mapping && !P.enable_skysphere && !P.enable_skybox && !P.has_reflection;
     render_size(P.rw, P.rh);
@@ -769,135 +793,9 @@ void Renderer::fill_params(KParams& P) const
 int Renderer::launch_trace(const KParams& P, hipStream_t stream)
 {
     hipError_t e;
-    const char* env = getenv("RT_REFL_ENGINE");
-    bool engine = P.has_reflection && P.enable_bvh && !(env && env[0] == '0');
-    split_last_ = false;
-    const char* split_env = getenv("RT_SPLIT");
-    const size_t npx_split = (size_t)P.rw * P.local_rows;
-    if (!engine && P.wnodes && P.seg_scale > 0.0f && P.enable_bvh && !P.has_reflection && !P.pipeline &&
-        (split_env && split_env[0] == '1') && npx_split > 0 && npx_split < (1ull << 32)) {
-        // RT_SPLIT=1, split frame: primary pass -> records; the exact pass over the
-        // pixels it could not certify runs on stream2_ while the shade pass runs on 'stream'; then
-        // the exact pass over the shade pass's uncertified shadow queries; join.  Measured slower
-        // than the fused kernel (each pass pays the per-pixel and queue costs): off by default.
-        if ((e = d_prim_.reserve(npx_split * sizeof(PrimRec))) != hipSuccess ||
-            (e = d_defer_.reserve(npx_split * 4)) != hipSuccess || (e = d_defer2_.reserve(npx_split * 4)) != hipSuccess)
-            return hip_fail(e, "hipMalloc (split frame)");
-        if (!stream2_) {
-            // high priority: its few blocks are dispatched ahead of the shade pass's persistent grid
-            int lo = 0, hi = 0;
-            if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess)
-                hi = 0;
-            if ((e = hipStreamCreateWithPriority(&stream2_, hipStreamNonBlocking, hi)) != hipSuccess)
-                return hip_fail(e, "hipStreamCreate");
-        }
-        if (!fork_ && ((e = hipEventCreateWithFlags(&fork_, hipEventDisableTiming)) != hipSuccess ||
-                       (e = hipEventCreateWithFlags(&join_, hipEventDisableTiming)) != hipSuccess))
-            return hip_fail(e, "hipEventCreate");
-        const char* gs = getenv("RT_GROUP_SHIFT");
-        long shift = gs ? atol(gs) : 5;
-        KParams Q = P;
-        Q.prim = d_prim_.as<PrimRec>();
-        Q.grp_shift = (shift >= 1 && shift <= 6) ? (int32_t)shift : 5;
-        Q.defer_cap = (uint32_t)npx_split;
-        Q.trav_budget = 0;
-        Q.defer = d_defer_.as<uint32_t>();
-        Q.defer_head = 3;
-        if ((e = rt_launch_split(0, &Q, stream)) != hipSuccess) return hip_fail(e, "primary_kernel launch");
-        if ((e = hipEventRecord(fork_, stream)) != hipSuccess || (e = hipStreamWaitEvent(stream2_, fork_, 0)) != hipSuccess)
-            return hip_fail(e, "split fork");
-        KParams C = Q;
-        C.defer_in = d_defer_.as<uint32_t>();
-        C.defer_in_head = 3;
-        if ((e = rt_launch_split(2, &C, stream2_)) != hipSuccess) return hip_fail(e, "exact pass launch");
-        if ((e = hipEventRecord(join_, stream2_)) != hipSuccess) return hip_fail(e, "split join");
-        KParams B = Q;
-        B.defer = d_defer2_.as<uint32_t>();
-        B.defer_head = 13;
-        if ((e = rt_launch_split(1, &B, stream)) != hipSuccess) return hip_fail(e, "shade_kernel launch");
-        KParams D = Q;
-        D.defer_in = d_defer2_.as<uint32_t>();
-        D.defer_in_head = 13;
-        if ((e = rt_launch_split(2, &D, stream)) != hipSuccess) return hip_fail(e, "exact pass launch");
-        if ((e = hipStreamWaitEvent(stream, join_, 0)) != hipSuccess) return hip_fail(e, "split join");
-        split_last_ = true;
-        return RT_OK;
-    }
+    const bool engine = P.has_reflection && P.enable_bvh && knobs_.refl_engine;
     if (!engine) {
-        // deferred pixels (kernels.hip ray_trace_defer_kernel):
-        // RT_DEFER_BUDGET (default 1000; 0 = off) and RT_GROUP_SHIFT (default 5: 32 lanes per ray)
-        KParams Q = P;
-        // RT_WIDE_LEAN=1, with the wide BVH and segment queries (no analytic shapes, scene scale
-        // in range): the lean kernel (no octree code) -- pixels over RT_WIDE_BUDGET
-        // go to a heavy-pixel pass and those the wide BVH cannot certify to the exact ray-group
-        // pass.  Measured slower than the default full kernel, which traces the few uncertified
-        // queries through the octree in place (each extra pass waits on its slowest ray).
-        const char* lean_env = getenv("RT_WIDE_LEAN");
-        size_t npx_all = (size_t)P.rw * P.local_rows;
-        if (P.wnodes && P.seg_scale > 0.0f && P.enable_bvh && !P.has_reflection && !P.pipeline &&
-            (lean_env && lean_env[0] == '1') && npx_all > 0 && npx_all < (1ull << 32)) {
-            if ((e = d_defer_.reserve(npx_all * 4)) != hipSuccess || (e = d_defer2_.reserve(npx_all * 4)) != hipSuccess)
-                return hip_fail(e, "hipMalloc (deferred pixels)");
-            const char* gs = getenv("RT_GROUP_SHIFT");
-            long shift = gs ? atol(gs) : 5;
-            // RT_WIDE_BUDGET: wide-BVH loop iterations per query in the lean kernel before the
-            // pixel moves to the heavy-pixel pass (default 64; 0: no budget)
-            const char* wb = getenv("RT_WIDE_BUDGET");
-            long wbud = wb ? atol(wb) : 0;
-            Q.wide_budget = (uint32_t)std::max(0L, std::min(wbud, 1L << 30));
-            Q.defer2 = d_defer2_.as<uint32_t>();
-            Q.wide_lean = 1;
-            Q.trav_budget = 0;
-            Q.grp_shift = (shift >= 1 && shift <= 6) ? (int32_t)shift : 5;
-            Q.defer = d_defer_.as<uint32_t>();
-            Q.defer_cap = (uint32_t)npx_all;
-        } else if (P.enable_bvh && !P.has_reflection && !P.pipeline && !P.wnodes) {
-            const char* bs = getenv("RT_DEFER_BUDGET");
-            const char* gs = getenv("RT_GROUP_SHIFT");
-            // out-of-range values (negative, above 2^32 - 1, not a number) turn deferral off
-            char* end = nullptr;
-            long long budget = 1000, shift = 5;
-            if (bs) {
-                budget = strtoll(bs, &end, 10);
-                if (end == bs || *end != '\0' || budget < 0 || budget > (long long)UINT32_MAX) budget = 0;
-            }
-            if (gs) {
-                shift = strtoll(gs, &end, 10);
-                if (end == gs || *end != '\0') shift = 0;
-            }
-            size_t npx = (size_t)P.rw * P.local_rows;
-            if (budget > 0 && shift >= 1 && shift <= 6 && npx > 0 && npx < (1ull << 32)) {
-                if ((e = d_defer_.reserve(npx * 4)) != hipSuccess)
-                    return hip_fail(e, "hipMalloc (deferred pixels)");
-                Q.trav_budget = (uint32_t)budget;
-                Q.grp_shift = (int32_t)shift;
-                Q.defer = d_defer_.as<uint32_t>();
-                Q.defer_cap = (uint32_t)npx;   // >= the launch's pixels: the list cannot overflow
-            }
-        }
-        // RT_TILE_ORDER=1: tiles in descending estimated cost (kernels.hip tile_probe_kernel), so
-        // that the silhouette tiles, whose grazing rays are the frame's longest, start first.
-        // Measured no faster than the natural order: off by default.
-        const char* to_env = getenv("RT_TILE_ORDER");
-        const int ntiles = P.tiles_x * P.tiles_y;
-        if (P.wnodes && !P.pipeline && !P.has_reflection && (to_env && to_env[0] == '1') && ntiles > 0 &&
-            ntiles <= (int)TILE_ID_MASK) {
-            const size_t nt = (size_t)ntiles;
-            if ((e = d_tile_sort_.reserve(nt * 12)) != hipSuccess)
-                return hip_fail(e, "hipMalloc (tile order)");
-            uint32_t* cost = d_tile_sort_.as<uint32_t>();
-            uint32_t* keys = cost + nt;
-            uint32_t* sorted = keys + nt;
-            size_t tb = 0;
-            if ((e = rt_launch_tile_probe(&Q, cost, keys, stream)) != hipSuccess ||
-                (e = hipcub::DeviceRadixSort::SortKeys(nullptr, tb, keys, sorted, ntiles, 0, 31, stream)) != hipSuccess ||
-                (e = d_tile_sort_tmp_.reserve(tb)) != hipSuccess ||
-                (e = hipcub::DeviceRadixSort::SortKeys(d_tile_sort_tmp_.p, tb, keys, sorted, ntiles, 0, 31, stream)) !=
-                    hipSuccess)
-                return hip_fail(e, "tile order");
-            Q.tile_order = sorted;
-        }
-        if ((e = rt_launch_ray_trace(&Q, stream)) != hipSuccess)
+        if ((e = rt_launch_ray_trace(&P, stream)) != hipSuccess)
             return hip_fail(e, "ray_trace_kernel launch");
         return RT_OK;
     }
@@ -925,26 +823,41 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
 {
     const int N = P.rough_reflections_sample_count;
     const int stride = N > 0 ? N : 1;
-    // about 2^RT_REFL_CHUNK_LOG2 sample slots per chunk (default 2^25: C5 0.765 / 0.714 / 0.695 / 0.679 s at 2^21 / 2^23 / 2^24 / 2^25; 10..25): a chunk's
-    // records (~170 B per slot with its child frames) and one host round trip per chunk
-    int clog = 25;
-    if (const char* ce = getenv("RT_REFL_CHUNK_LOG2")) {
-        const int v = atoi(ce);
-        if (v >= 10 && v <= 25)   // small values (tests): many chunks per level
-            clog = v;
-    }
-    const int chunk = std::max(1024, (1 << clog) / stride);
     if (level + 1 >= REFL_LEVELS)
         return fail(RT_EUNSUPPORTED, "reflection recursion deeper than the engine's levels");
     ReflLevel& L = refl_[level];
     ReflLevel& C = refl_[level + 1];
-    size_t slots = (size_t)std::min(nframes, chunk) * stride;
     hipError_t e;
-    if ((e = L.ret.reserve((size_t)nframes * 12)) != hipSuccess || (e = L.sm.reserve(slots * sizeof(SampleRec))) != hipSuccess ||
-        (e = L.hit.reserve(slots * sizeof(RawHit))) != hipSuccess || (e = L.cnt.reserve(64)) != hipSuccess ||
-        (e = L.list.reserve(slots * 4)) != hipSuccess || (e = L.res.reserve(slots * 16)) != hipSuccess ||
-        (e = C.fr.reserve(slots * sizeof(FrameRec))) != hipSuccess || (e = C.ret.reserve(slots * 12)) != hipSuccess)
+    // about 2^RT_REFL_CHUNK_LOG2 sample slots per chunk (default 2^25: C5 0.765 / 0.714 / 0.695 /
+    // 0.679 s at 2^21 / 2^23 / 2^24 / 2^25): one host round trip per chunk, ~204 B of records per
+    // slot (72-B SampleRec, 32-B RawHit, 16-B result, list entry, child frame and its colour).
+    // A level may take at most a quarter of the memory still free (what it already holds
+    // counts as free), so that the deeper levels, each bounded the same way, fit behind it;
+    // an allocation that fails anyway halves the chunk and retries.
+    constexpr size_t SLOT_BYTES = sizeof(SampleRec) + sizeof(RawHit) + 4 + 16 + sizeof(FrameRec) + 12;
+    size_t chunk = (size_t)std::max(1024, (1 << knobs_.refl_chunk_log2) / stride);
+    {
+        size_t freeb = 0, totalb = 0;
+        if (hipMemGetInfo(&freeb, &totalb) == hipSuccess) {
+            const size_t held = L.sm.bytes + L.hit.bytes + L.list.bytes + L.res.bytes + C.fr.bytes + C.ret.bytes;
+            const size_t cap = (freeb + held) / 4 / (SLOT_BYTES * (size_t)stride);
+            chunk = std::max<size_t>(1024, std::min(chunk, cap));
+        }
+    }
+    if ((e = L.ret.reserve((size_t)nframes * 12)) != hipSuccess || (e = L.cnt.reserve(64)) != hipSuccess)
         return hip_fail(e, "hipMalloc (reflection level)");
+    for (;;) {
+        const size_t slots = std::min((size_t)nframes, chunk) * stride;
+        if ((e = L.sm.reserve(slots * sizeof(SampleRec))) == hipSuccess &&
+            (e = L.hit.reserve(slots * sizeof(RawHit))) == hipSuccess && (e = L.list.reserve(slots * 4)) == hipSuccess &&
+            (e = L.res.reserve(slots * 16)) == hipSuccess && (e = C.fr.reserve(slots * sizeof(FrameRec))) == hipSuccess &&
+            (e = C.ret.reserve(slots * 12)) == hipSuccess)
+            break;
+        if (e != hipErrorOutOfMemory || chunk <= 1024)
+            return hip_fail(e, "hipMalloc (reflection level)");
+        (void)hipGetLastError();   // clear the sticky out-of-memory status
+        chunk /= 2;
+    }
     // the level's frames in Morton order of their origins (coherent sample and shadow rays)
     if ((e = L.sort.reserve((size_t)nframes * 16)) != hipSuccess)
         return hip_fail(e, "hipMalloc (frame sort)");
@@ -955,8 +868,7 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
     if ((e = rt_launch_refl_keys(&P, L.fr.as<FrameRec>(), nframes, keys_in, idx_in, stream)) != hipSuccess)
         return hip_fail(e, "refl_keys_kernel launch");
     const int32_t* order = idx_in;
-    const char* sort_env = getenv("RT_REFL_SORT");
-    if (!(sort_env && sort_env[0] == '0')) {
+    if (knobs_.refl_sort) {
         size_t tb = 0;
         if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys_in, keys_out, idx_in, idx_out, nframes, 0, 30,
                                                     stream)) != hipSuccess ||
@@ -966,7 +878,7 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
             return hip_fail(e, "frame sort");
         order = idx_out;
     }
-    for (int c0 = 0; c0 < nframes; c0 += chunk) {
+    for (int c0 = 0; c0 < nframes; c0 += (int)chunk) {
         ReflArgs A;
         A.order = order;
         A.fr = L.fr.as<FrameRec>();
@@ -980,15 +892,14 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
         A.res = L.res.as<float4>();
         A.list_count = L.cnt.as<unsigned int>() + 1;
         A.c0 = c0;
-        A.c1 = std::min(nframes, c0 + chunk);
+        A.c1 = (int)std::min<size_t>((size_t)nframes, (size_t)c0 + chunk);
         A.level = level;
         A.stride = stride;
         if ((e = hipMemsetAsync(L.cnt.p, 0, 8, stream)) != hipSuccess)
             return hip_fail(e, "hipMemsetAsync");
         // fused (default): trace, pass1 (+ shadow list), shadow (+ spawn); RT_REFL_FUSE=0: trace,
         // pass1, list, shadow, spawn
-        const char* fz = getenv("RT_REFL_FUSE");
-        A.fused = !(fz && fz[0] == '0');
+        A.fused = knobs_.refl_fuse;
         static const int fused_stages[] = {1, 2, 3}, split_stages[] = {1, 2, 6, 3, 4};
         const int* st = A.fused ? fused_stages : split_stages;
         const int nst = A.fused ? 3 : 5;
@@ -1164,12 +1075,14 @@ int Renderer::trace_frame()
     P.shadow = want_shadow_ ? d_shadow_.as<uint8_t>() : nullptr;
     P.counters = d_counters_.as<unsigned long long>();
     if ((e = hipMemsetAsync(d_counters_.p, 0, NCOUNTER_WORDS * 8, stream_)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
-    if (getenv("RT_DEBUG_WAVES")) {   // diagnostic builds: per-wave records (rt_debug_read)
+    if (knobs_.debug_waves) {   // diagnostic builds: per-wave records (rt_debug_read)
         if ((e = d_dbg_.reserve((size_t)DBG_WAVES * DBG_WORDS * 8)) != hipSuccess ||
             (e = hipMemsetAsync(d_dbg_.p, 0, (size_t)DBG_WAVES * DBG_WORDS * 8, stream_)) != hipSuccess)
             return hip_fail(e, "debug buffer");
         P.dbg = d_dbg_.as<unsigned long long>();
     }
+    if (wait_slots(stream_) != RT_OK)   // band launches in flight share the engine / raster buffers
+        return RT_EHIP;
     hipEventRecord(ev_[0], stream_);
     if ((rc = launch_frame(P, stream_)) != RT_OK) return rc;
     hipEventRecord(ev_[1], stream_);
@@ -1367,12 +1280,10 @@ int Renderer::get_stats(rt_stats* out) const
     render_size(out->render_width, out->render_height);
     out->seg_scale = last_seg_;
     for (int i = 0; i < 4; i++) out->work[i] = last_work_[i];
-    for (int i = 0; i < 2; i++) out->work_abandoned[i] = last_work_[4 + i];
-    for (int i = 0; i < 4; i++) out->work_wide[i] = last_work_[6 + i];
+    for (int i = 0; i < 4; i++) out->work_wide[i] = last_work_[4 + i];
     for (int i = 0; i < 6; i++) out->uncertified[i] = last_uncert_[i];
-    out->deferred_pixels = last_deferred_;
-    out->exact_pixels = last_exact_;
     for (int i = 0; i < 6; i++) out->wave_steps[i] = last_wave_[i];
+    for (int i = 0; i < 4; i++) out->build_split_ms[i] = build_split_ms_[i];
     return RT_OK;
 }
 
@@ -1419,24 +1330,26 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
         if (band_nslots_ < BAND_SLOTS) {
             si = band_nslots_++;
             band_slot_[si].counters.device = band_slot_[si].tmp.device = device_;
+            if ((e = hipEventCreateWithFlags(&band_slot_[si].done, hipEventDisableTiming)) != hipSuccess)
+                return hip_fail(e, "hipEventCreate");
         } else {
-            // a ninth stream: the least recently used slot is recycled once the device is idle
-            // (its stream may no longer exist, so the wait is device-wide)
+            // a ninth stream: the least recently used slot is recycled once its last launch is
+            // done (its own event; the stream it ran on may no longer exist)
             si = 0;
             for (int i = 1; i < BAND_SLOTS; i++)
                 if (band_slot_[i].used < band_slot_[si].used) si = i;
-            if ((e = hipDeviceSynchronize()) != hipSuccess)
+            if (band_slot_[si].live && (e = hipEventSynchronize(band_slot_[si].done)) != hipSuccess)
                 return hip_fail(e, "render_bands_device: recycling a stream slot");
         }
         band_slot_[si].stream = stream;
     }
     band_slot_[si].used = ++band_uses_;
-    auto env_on = [](const char* k) { const char* v = getenv(k); return v && v[0] == '1'; };
-    const bool slot_only = !P.has_reflection && !s_.hybrid_rasterization_tracing && P.wnodes && !P.pipeline &&
-                           !env_on("RT_SPLIT") && !env_on("RT_WIDE_LEAN") && !env_on("RT_TILE_ORDER");
-    if (!slot_only && band_last_ >= 0 && band_last_ != si &&
-        (e = hipStreamSynchronize(band_slot_[band_last_].stream)) != hipSuccess)
-        return hip_fail(e, "render_bands_device: previous launch");
+    // Only the default trace path keeps all of its per-launch state in the slot; the
+    // reflection engine and the raster path use buffers shared across launches, so such a
+    // launch first waits for every launch still in flight on any stream.
+    const bool slot_only = !P.has_reflection && !s_.hybrid_rasterization_tracing;
+    if (!slot_only && wait_slots(stream) != RT_OK)
+        return RT_EHIP;
     BandSlot& S = band_slot_[si];
     band_last_ = si;
     int f = s_.enable_ssaa ? s_.ssaa_factor : 1;
@@ -1448,11 +1361,10 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
     P.tiles_y = (P.local_rows + 7) / 8;
     if ((e = S.counters.reserve(NCOUNTER_WORDS * 8)) != hipSuccess) return hip_fail(e, "hipMalloc (counters)");
     // SSAA fused into the trace kernel's tiles (kernels.hip downscale_tile) when every lane
-    // of every tile holds a pixel (no padding, no deferred pixels) and f divides the 8x8
+    // of every tile holds a pixel (no padding) and f divides the 8x8
     // tile; otherwise the band is rendered at full size and downscale_kernel filters it.
     // RT_FUSED_SSAA=0 keeps the separate pass.
-    const char* fz = getenv("RT_FUSED_SSAA");
-    const bool fused = (f == 2 || f == 4 || f == 8) && slot_only && !(fz && fz[0] == '0') && P.rw % 8 == 0 &&
+    const bool fused = (f == 2 || f == 4 || f == 8) && slot_only && knobs_.fused_ssaa && P.rw % 8 == 0 &&
                        P.local_rows % 8 == 0;
     uint32_t* target = d_out;
     if (f > 1 && !fused) {
@@ -1479,6 +1391,35 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
     if (ring_count_ < EV_RING) ring_count_++;
     if (f > 1 && !fused && (e = rt_launch_downscale(target, P.rw, P.local_rows, f, d_out, stream)) != hipSuccess)
         return hip_fail(e, "downscale launch");
+    if ((e = hipEventRecord(S.done, stream)) != hipSuccess)
+        return hip_fail(e, "hipEventRecord");
+    S.live = true;
+    return RT_OK;
+}
+
+int Renderer::wait_slots(hipStream_t stream)
+{
+    for (int i = 0; i < band_nslots_; i++) {
+        BandSlot& b = band_slot_[i];
+        if (!b.live || b.stream == stream)
+            continue;
+        hipError_t e = hipStreamWaitEvent(stream, b.done, 0);
+        if (e != hipSuccess)
+            return hip_fail(e, "hipStreamWaitEvent (frames in flight)");
+    }
+    return RT_OK;
+}
+
+int Renderer::sync_slots()
+{
+    for (int i = 0; i < band_nslots_; i++) {
+        BandSlot& b = band_slot_[i];
+        if (!b.live)
+            continue;
+        hipError_t e = hipEventSynchronize(b.done);
+        if (e != hipSuccess)
+            return hip_fail(e, "hipEventSynchronize (frames in flight)");
+    }
     return RT_OK;
 }
 
@@ -1538,14 +1479,14 @@ int Renderer::kernel_times(float* ms, int n)
 }
 
 // the counters of the last band launch; they also become the stats of the last frame
-// (deferred pixels, RT_COUNT work), as after ray_trace
+// (RT_COUNT work), as after ray_trace
 int Renderer::band_counters(unsigned long long out[2])
 {
     hipSetDevice(device_);
     unsigned long long cnt[NCOUNTERS] = {};
     if (band_last_ < 0)
         return fail(RT_ESTATE, "band_counters: no render_bands_device launch yet");
-    hipError_t e = hipDeviceSynchronize();
+    hipError_t e = hipEventSynchronize(band_slot_[band_last_].done);
     if (e == hipSuccess)
         e = hipMemcpy(cnt, band_slot_[band_last_].counters.p, sizeof(cnt), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return hip_fail(e, "band_counters");
@@ -1559,14 +1500,11 @@ void Renderer::take_counters(const unsigned long long* cnt)
 {
     last_shadow_ = (int64_t)cnt[0];
     last_refl_ = (int64_t)cnt[1];
-    for (int i = 0; i < 9; i++) last_work_[i] = (int64_t)cnt[4 + i];
-    last_work_[9] = (int64_t)cnt[14];
+    for (int i = 0; i < 4; i++) last_work_[i] = (int64_t)cnt[4 + i];
+    for (int i = 0; i < 3; i++) last_work_[4 + i] = (int64_t)cnt[10 + i];
+    last_work_[7] = (int64_t)cnt[14];
     for (int i = 0; i < 6; i++) last_uncert_[i] = (int64_t)cnt[16 + i];
     for (int i = 0; i < 6; i++) last_wave_[i] = (int64_t)cnt[22 + i];
-    last_deferred_ = (int64_t)(cnt[3] & 0xffffffffull);
-    last_exact_ = (int64_t)(cnt[13] & 0xffffffffull) + (split_last_ ? (int64_t)(cnt[3] & 0xffffffffull) : 0);
-    if (split_last_)
-        last_deferred_ = 0;
 }
 
 float render(Renderer& renderer, int* rc)

@@ -32,6 +32,23 @@ struct HostTex {
     std::vector<float> rgba;
 };
 
+// Diagnostic switches, read once from the environment when the renderer is created
+// (rt_create); each selects an equivalent path (same framebuffer) for A/B runs and tests.
+struct Knobs {
+    bool wbvh = true;         // RT_WBVH=0: no wide BVH, every query walks the octree
+    bool seg = true;          // RT_SEG=0: shadow / reflection queries walk the whole line (5.2)
+    bool cones = true;        // RT_CONES=0: no leaf normal cones (5.3; also turns the leaf slabs off)
+    bool lslab = true;        // RT_LSLAB=0: no leaf slabs (5.4)
+    bool plain = true;        // RT_PLAIN=0: no plain specialisation of ray_trace_kernel (5.6)
+    bool fused_ssaa = true;   // RT_FUSED_SSAA=0: band launches downscale in a separate pass (7)
+    bool refl_engine = true;  // RT_REFL_ENGINE=0: the one-lane-per-pixel recursive kernel (9)
+    bool refl_sort = true;    // RT_REFL_SORT=0: reflection frames in spawn order, not Morton order
+    bool refl_fuse = true;    // RT_REFL_FUSE=0: the engine's separate list / spawn passes
+    int refl_chunk_log2 = 25; // RT_REFL_CHUNK_LOG2 (10..25): sample slots per engine chunk
+    bool debug_waves = false; // RT_DEBUG_WAVES: per-wave records of diagnostic builds (rt_debug_read)
+    static Knobs from_env();
+};
+
 class Renderer {
 public:
     explicit Renderer(int device);
@@ -112,15 +129,16 @@ private:
     int launch_ssao();
     int trace_frame();
     int refl_level(const KParams& P, int level, int nframes, hipStream_t stream);
+    // frames in flight (render_bands_device): make 'stream' wait for every live slot's last
+    // launch, or the host for all of them (before buffers that launches read are replaced)
+    int wait_slots(hipStream_t stream);
+    int sync_slots();
 
+    Knobs knobs_;
     int device_;
     int num_cus_ = 256;
     hipStream_t stream_ = nullptr;
     hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};
-    // split frame: the exact pass's stream and the fork / join events
-    hipStream_t stream2_ = nullptr;
-    hipEvent_t fork_ = nullptr, join_ = nullptr;
-    bool split_last_ = false;   // the last frame ran split (exact_pixels = both lists)
     std::string err_;
 
     rt_settings s_;
@@ -148,7 +166,7 @@ private:
     bool geom_dirty_ = true, mats_dirty_ = true, tex_dirty_ = true;
     DevBuf d_nodes_, d_tris_, d_tri_id_, d_tri_mat_, d_tri_uv_, d_mats_;
     DevBuf d_tex_[TEX_SLOTS], d_sky_[6];
-    DevBuf d_internal_, d_image_, d_rgba_, d_hit_id_, d_hit_t_, d_shadow_, d_counters_, d_defer_;
+    DevBuf d_internal_, d_image_, d_rgba_, d_hit_id_, d_hit_t_, d_shadow_, d_counters_;
     // SSAO: _z_buffer, _normal_buffer (float4) and the occlusion counts of the internal image
     DevBuf d_zbuf_, d_nbuf_, d_ao_;
     // leaf normal cones, [4] per GTri slot (renderer.cpp leaf_cones)
@@ -159,11 +177,9 @@ private:
     DevBuf d_lslab_;
     // the wide BVH (wbvh.hpp): nodes, triangle records in its leaf order, slot maps
     WBvh wb_;
-    DevBuf d_wnodes_, d_wtris_, d_wmeta_, d_defer2_;
+    DevBuf d_wnodes_, d_wtris_, d_wmeta_;
     std::vector<uint32_t> wmeta_;   // host copy of KParams::wmeta (4 words per wide-BVH triangle)
-    DevBuf d_tile_sort_, d_tile_sort_tmp_;   // tile probe costs, sort keys, sorted order; radix-sort scratch
     DevBuf d_dbg_;                           // diagnostic per-wave records (RT_DEBUG_WAVES)
-    DevBuf d_prim_;                          // split frame: the primary pass's records (PrimRec per pixel)
     bool ssao_ready_ = false;   // the buffers hold the last frame's z / normals
     // raster path: caller-order triangles, per-triangle piece counts / offsets, the piece
     // table and its texcoords, the z-key buffer, the big-piece list, scan scratch
@@ -184,10 +200,15 @@ private:
     ReflLevel refl_[REFL_LEVELS];
 
     // render_bands_device: per-stream tile-queue counters and SSAA band buffers, so that
-    // frames launched on different streams can be in flight together
+    // frames launched on different streams can be in flight together.  Each
+    // slot owns an event recorded after its last launch: launches that use buffers shared
+    // across launches (reflection engine, raster path) and scene uploads wait on every live
+    // slot's event, never on a stored stream handle (the caller may have destroyed it).
     struct BandSlot {
         hipStream_t stream = nullptr;
         DevBuf counters, tmp;
+        hipEvent_t done = nullptr;   // recorded on 'stream' after the slot's last launch
+        bool live = false;           // 'done' has been recorded
         uint64_t used = 0;   // band_uses_ at the slot's last launch (least recently used is recycled)
     };
     static constexpr int BAND_SLOTS = 8;
@@ -202,15 +223,14 @@ private:
     // stats
     int64_t last_primary_ = 0, last_shadow_ = 0, last_refl_ = 0;
     float last_seg_ = 0;   // KParams::seg_scale of the last frame
-    int64_t last_deferred_ = 0;               // pixels the last frame handed to the ray-group pass
-    int64_t last_exact_ = 0;                  // lean mode: pixels traced through the octree (exact pass)
-    int64_t last_work_[10] = {};  // RT_COUNT builds: counters[4..12], [14] of the last frame (executed k-DOP / MT
-                                  // tests: whole-line, segment, abandoned; wide-BVH nodes, triangles, uncertified,
+    int64_t last_work_[8] = {};   // RT_COUNT builds: counters[4..7], [10..12], [14] of the last frame (executed
+                                  // k-DOP / MT tests: whole-line, segment; wide-BVH nodes, triangles, uncertified,
                                   // certificates)
     int64_t last_wave_[6] = {};     // RT_COUNT builds: counters[22..27], wide-BVH loop iterations (rt_stats)
     int64_t last_uncert_[6] = {};   // RT_COUNT builds: uncertified wide-BVH queries by reason
     void take_counters(const unsigned long long* cnt);
     float kernel_ms_ = 0, post_ms_ = 0, build_ms_ = 0;
+    float build_split_ms_[4] = {};   // octree, leaf cones + slabs, wide BVH, upload
 };
 
 // render(Renderer&) (tp2/projets/utils/mainUtils.cpp:6-21): ray_trace then post_process;

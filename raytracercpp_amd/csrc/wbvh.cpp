@@ -86,7 +86,7 @@ struct Builder {
     std::vector<BNode>& nodes;       // preallocated, 2n - 1 nodes at most
     std::atomic<int32_t> next{1};
     std::atomic<int> spare;          // threads that may still be started
-    float ct = 1.0f;                 // SAH cost of a node visit, in triangle tests (RT_W_SAH_CT)
+    float ct = 1.0f;                 // SAH cost of a node visit, in triangle tests (r02: 2 and 3 were slower)
 
     struct Bins {
         int32_t cnt[3][NBINS];
@@ -271,7 +271,6 @@ struct ChildGeom {
 // W_CONE_STEP; 255 = no cone (psi <= 0, or a normal out of range).
 int cone_code(const int* nq, const ChildGeom& g, const std::vector<GTri, DefaultInitAlloc<GTri>>& tris)
 {
-#if RT_W_CONE
     const double Nl = std::sqrt((double)nq[0] * nq[0] + (double)nq[1] * nq[1] + (double)nq[2] * nq[2]);
     double theta = 0;
     for (int32_t i = g.first; i < g.first + g.count; i++) {
@@ -290,10 +289,6 @@ int cone_code(const int* nq, const ChildGeom& g, const std::vector<GTri, Default
         return 255;
     const double code = std::ceil((std::cos(psi) * Nl + 0.01) / ((double)W_CONE_STEP * (1 - 1e-9)));
     return code <= 254 ? (int)code : 255;
-#else
-    (void)nq, (void)g, (void)tris;
-    return 255;
-#endif
 }
 
 WNode quantise(const Box* cb, const uint32_t* link, int nc, const ChildGeom* cg,
@@ -335,7 +330,6 @@ WNode quantise(const Box* cb, const uint32_t* link, int nc, const ChildGeom* cg,
     }
     for (int j = 0; j < W_WIDTH; j++)
         w.child[j] = link[j];
-#if RT_W_SLAB
     // slabs: N_j = round(127 n / |n|) (integer), range of N_j . (v - origin) over the vertices
     // in double (exact: integer N, float vertices and origin), quantised outward on 16 bits
     double smin[W_WIDTH], smax[W_WIDTH];
@@ -393,7 +387,6 @@ WNode quantise(const Box* cb, const uint32_t* link, int nc, const ChildGeom* cg,
         q1 = std::max(0.0, std::min(65535.0, q1));
         w.slab[j] = (uint32_t)q0 | ((uint32_t)q1 << 16);
     }
-#endif
     return w;
 }
 
@@ -477,13 +470,11 @@ struct Collapser {
             cg[j].first = C.first;
             cg[j].count = C.count;
             cg[j].n[0] = cg[j].n[1] = cg[j].n[2] = 0;
-#if RT_W_SLAB
             for (int32_t i = C.first; i < C.first + C.count; i++) {
                 const GTri& t = tris[(size_t)idx[(size_t)i]];
                 for (int a = 0; a < 3; a++)
                     cg[j].n[a] += t.n[a];
             }
-#endif
         }
         WNode w = quantise(cb, link, nc, cg, &tris);
         out.nodes[me] = w;
@@ -518,13 +509,6 @@ void build_wbvh(const FlatOctree& oct, WBvh& out)
     std::vector<BNode> bn((size_t)(2 * n));
     const int nt = wbvh_threads();
     Builder B(pb, pc, idx, bn, nt);
-    // RT_W_SAH_CT: the SAH's node-visit cost relative to one triangle test (default 1); larger
-    // values make larger leaves and a shallower tree.  Structure only: every tree is exact.
-    if (const char* e = std::getenv("RT_W_SAH_CT")) {
-        const float v = std::strtof(e, nullptr);
-        if (v > 0.0f && v < 100.0f)
-            B.ct = v;
-    }
     B.build(0, 0, (int32_t)n);
     bn.resize((size_t)B.next.load());
     // SAH cost of the binary tree (diagnostic)
@@ -614,7 +598,6 @@ int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)
                     bad++;
                 if (!inside(tri_box(w.tris[k]), it.box))
                     bad++;
-#if RT_W_SLAB
                 const GTri& T = w.tris[k];
                 for (int q = 0; q < it.np; q++) {
                     const WNode& N = w.nodes[it.path[q] >> 3];
@@ -631,7 +614,6 @@ int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)
                         if (!(sp >= lo && sp <= hi))
                             bad++;
                     }
-#if RT_W_CONE
                     const uint32_t code = N.nrm[j] >> 24;
                     const double nn = std::sqrt((double)T.n[0] * T.n[0] + (double)T.n[1] * T.n[1] + (double)T.n[2] * T.n[2]);
                     if (code < 255 && nn > 0) {
@@ -645,9 +627,7 @@ int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)
                             !(std::acos(std::min(1.0, kap)) + ang < std::acos(W_CONE_EPS)))
                             bad++;
                     }
-#endif
                 }
-#endif
             }
             continue;
         }

@@ -48,32 +48,13 @@ namespace rt {
 constexpr uint32_t W_LEAF = 0x80000000u;
 constexpr uint32_t W_EMPTY = 0xFFFFFFFFu;
 constexpr int W_MAX_LEAF = 8;
-#ifndef RT_W_STACK
-#define RT_W_STACK 12
-#endif
-constexpr int W_STACK = RT_W_STACK;
-#ifndef RT_W_WIDTH
-#define RT_W_WIDTH 4   // children per node: 4 or 8
-#endif
-constexpr int W_WIDTH = RT_W_WIDTH;
-static_assert(W_WIDTH == 4 || W_WIDTH == 8, "W_WIDTH");
-#ifndef RT_W_SCHED_BARRIER
-#define RT_W_SCHED_BARRIER 1
-#endif
-#ifndef RT_W_LOOP
-#define RT_W_LOOP 2   // 1: while-while, 2: if-if, 3: if-if with one triangle per step (wbvh_closest)
-#endif   // traversal stack entries per lane (overflow: the query is not certified)
+constexpr int W_STACK = 12;   // traversal stack entries per lane (overflow: the query is not certified)
+constexpr int W_WIDTH = 4;    // children per node
 
 #ifndef W_STEP_HOOK
 #define W_STEP_HOOK(cur, leaf)   // diagnostic builds (kernels.hip): per-step wave statistics
 #endif
 
-#ifndef RT_W_SLAB
-#define RT_W_SLAB 1   // per-child orientation slabs (below)
-#endif
-#ifndef RT_W_CONE
-#define RT_W_CONE 1   // per-child backface cones (below; needs RT_W_SLAB)
-#endif
 // cone threshold step: c in 0..254 encodes c * 224 / 254 >= |N| (|N| <= 127 sqrt 3 < 220), so 255
 // can never pass.  W_CONE_EPS: the triangles' minimum cos(normal, d) the build guarantees
 constexpr float W_CONE_STEP = 224.0f / 254.0f;
@@ -84,37 +65,29 @@ struct alignas(16) WNode {
     uint32_t exps;        // byte a: biased exponent (127 + k) of the step 2^k along axis a
     uint8_t qlo[3][W_WIDTH];    // [axis][child]
     uint8_t qhi[3][W_WIDTH];
-#if RT_W_SLAB
     // Orientation slab of child j: every vertex v below it has
     //   slo + q0 s  <=  N_j . (v - origin)  <=  slo + q1 s,
     // N_j = nrm bytes 0..2 as signed 8-bit integers (the subtree's area-weighted normal,
     // quantised to [-127, 127]), q0 / q1 the low / high 16 bits of slab[j].  A curved patch is thin
     // along its mean normal, so a ray that grazes the surface misses most patches' slabs
     // although it crosses their boxes (silhouette rays).
-    // Backface cone of child j (RT_W_CONE): nrm byte 3 = c, 255 = none.  Every triangle
+    // Backface cone of child j: nrm byte 3 = c, 255 = none.  Every triangle
     // below j that Moller-Trumbore could ever hit faces away from a ray whose direction d has
     //   N_j . d  >  c * W_CONE_STEP * |d|
     // (the test rejects it on Mdet <= 0 before anything else), so such a ray skips j.
     float s, slo;
-#if RT_W_WIDTH == 8
-    uint32_t pad[2];
-#endif
     uint32_t nrm[W_WIDTH];
     uint32_t slab[W_WIDTH];
-#elif RT_W_WIDTH == 4
-    uint32_t pad[2];
-#endif
     uint32_t child[W_WIDTH];
 };
-// 4-wide: 96 B (64 B without slabs); 8-wide: 176 B (96 B)
-static_assert(sizeof(WNode) == (W_WIDTH == 4 ? (RT_W_SLAB ? 96 : 64) : (RT_W_SLAB ? 176 : 96)), "WNode size");
+static_assert(sizeof(WNode) == 96, "WNode size");
 // word offsets inside a node (the kernel loads it as 16-B rows and picks words)
 constexpr int WN_QLO = 4;                           // qlo[a] starts at word WN_QLO + a * W_WIDTH / 4
 constexpr int WN_QHI = 4 + 3 * W_WIDTH / 4;         // qhi[a] at WN_QHI + a * W_WIDTH / 4
 constexpr int WN_SS = 4 + 6 * W_WIDTH / 4;          // s, slo
-constexpr int WN_NRM = (RT_W_SLAB ? ((4 + 6 * W_WIDTH / 4 + 2 + 3) / 4) * 4 : 0);
+constexpr int WN_NRM = ((4 + 6 * W_WIDTH / 4 + 2 + 3) / 4) * 4;
 constexpr int WN_SLAB = WN_NRM + W_WIDTH;
-constexpr int WN_CHILD = RT_W_SLAB ? WN_SLAB + W_WIDTH : ((4 + 6 * W_WIDTH / 4 + 3) / 4) * 4;
+constexpr int WN_CHILD = WN_SLAB + W_WIDTH;
 constexpr int WN_ROWS = (int)(sizeof(WNode) / 16);
 
 struct WStats {
@@ -254,11 +227,10 @@ struct WStackLocal {   // host
 // > 0, unique when ties: still to be certified by kdop_certifies on its octree leaf) or
 // W_UNCERT.  Shadow queries (hi = the segment end of kernels.hip is_shadowed, ties false)
 // read only the record's t.  work (optional, 4 entries): {nodes, triangles} added, [2] = the
-// reasons a query is not certified, [3] = loop iterations added.  budget > 0: a query that
-// needs more loop iterations is abandoned (W_UNCERT).
+// reasons a query is not certified, [3] = loop iterations added.
 template <class Stack>
 RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m, Stack& stk, WHit& h,
-                       uint32_t* work = nullptr, float hi = INFINITY, bool ties = true, uint32_t budget = 0)
+                       uint32_t* work = nullptr, float hi = INFINITY, bool ties = true)
 {
     h.t = INFINITY;
     h.u = 1.0f;
@@ -277,29 +249,19 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
     const bool nx_lo = !(ix < 0.0f), ny_lo = !(iy < 0.0f), nz_lo = !(iz < 0.0f);
 
     constexpr float SL = 0x1p-20f;   // relative slack over the rounding of a slab parameter (<= 3 ulp)
-#if RT_W_SLAB && RT_W_CONE
     // |d| rounded up (sqrt and dot within 2^-22), times the cone step: threshold = c * cstep
     const float cstep = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z) * (1.0f + 0x1p-20f) * W_CONE_STEP;
-#endif
     float best_s = hi + fabsf(hi) * SL;   // h.t (or hi) plus slack: a child entered at or below it may hold a hit
     bool tie = false, nanhit = false, infhit = false, overflow = false;
     int sp = 0;
     uint32_t cur = 0;   // root node
     uint32_t nn = 0, nt = 0;
-    uint32_t steps = 0;   // loop iterations (node or leaf visits): budget > 0 caps them
+    uint32_t steps = 0;   // loop iterations (node or leaf visits)
     while (cur != W_EMPTY) {
-        if (++steps > budget && budget) {
-            overflow = true;   // over budget: not certified here (the caller re-traces it)
-            break;
-        }
+        ++steps;
         // ---- inner nodes: test the four child boxes, go to the nearest, push the others ----
-#if RT_W_LOOP >= 2
         // if-if: every lane takes one step (inner node or leaf) per iteration
         if (!(cur & W_LEAF)) {
-#else
-        // while-while: lanes at inner nodes expand until every lane sits on a leaf (or is done)
-        while (cur != W_EMPTY && !(cur & W_LEAF)) {
-#endif
             nn++;
             W_STEP_HOOK(cur, 0);
             // (reading wave-uniform nodes, about half the steps of the C4 frame, through the
@@ -314,10 +276,8 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                 const uint4 r = R[i >> 2];
                 return (i & 3) == 0 ? r.x : (i & 3) == 1 ? r.y : (i & 3) == 2 ? r.z : r.w;
             };
-#if RT_W_SLAB
             const float m3 = 384.0f * m;   // |N|_1 <= 3 * 128: the spatial margin in slab units
             const float ss = bitsf(wd(WN_SS)), slo_lo = bitsf(wd(WN_SS + 1)) - m3, slo_hi = bitsf(wd(WN_SS + 1)) + m3;
-#endif
             const uint32_t ex = wd(3);
             // t of a plane origin + q s (widened by m) = q (s / d) + (origin -+ m - o) / d
             const float sx = bitsf((ex & 0xffu) << 23) * ix, sy = bitsf(((ex >> 8) & 0xffu) << 23) * iy,
@@ -356,7 +316,6 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                 // slab NaN) enters too.  The key orders the children; misses get INFINITY.
                 bool ok = chj != W_EMPTY &&
                           fmaxf(tmin, 0.0f) <= fminf(__builtin_fmaf(fabsf(tmax), SL, tmax), best_s);
-#if RT_W_SLAB
                 // the slab (and cone) only narrow the box's interval, so a child whose box
                 // fails is out already: when no lane's box passes, the wave skips this part
                 if (ok) {
@@ -376,16 +335,13 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                     tmin = fmaxf(tmin, fminf(s0, s1));
                     tmax = fminf(tmax, fmaxf(s0, s1));
                     ok = fmaxf(tmin, 0.0f) <= fminf(__builtin_fmaf(fabsf(tmax), SL, tmax), best_s);
-#if RT_W_CONE
                     // every triangle below faces away when a exceeds the threshold (rounding of
                     // a and of the threshold: < 1e-4 |d|, inside the build's 0.01 |d|)
                     ok = ok && !(a > (float)(nrj >> 24) * cstep);
-#endif
                 }
-#endif
                 key[j] = ok ? fminf(fmaxf(tmin, 0.0f), 3.0e38f) : INFINITY;
                 ref[j] = chj;
-#if defined(__HIP_DEVICE_COMPILE__) && RT_W_SCHED_BARRIER
+#if defined(__HIP_DEVICE_COMPILE__)
                 // one child at a time: the scheduler would interleave the children's
                 // temporaries (VALU latency is hidden by the other waves anyway)
                 __builtin_amdgcn_sched_barrier(0);
@@ -397,17 +353,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
         float tk = key[a]; key[a] = key[b]; key[b] = tk;                           \
         uint32_t tr = ref[a]; ref[a] = ref[b]; ref[b] = tr;                        \
     }
-#if RT_W_WIDTH == 4
             W_CSWAP(0, 1) W_CSWAP(2, 3) W_CSWAP(0, 2) W_CSWAP(1, 3) W_CSWAP(1, 2)
-#else
-            // 19 compare-exchanges (optimal 8-input network)
-            W_CSWAP(0, 2) W_CSWAP(1, 3) W_CSWAP(4, 6) W_CSWAP(5, 7)
-            W_CSWAP(0, 4) W_CSWAP(1, 5) W_CSWAP(2, 6) W_CSWAP(3, 7)
-            W_CSWAP(0, 1) W_CSWAP(2, 3) W_CSWAP(4, 5) W_CSWAP(6, 7)
-            W_CSWAP(2, 4) W_CSWAP(3, 5)
-            W_CSWAP(1, 4) W_CSWAP(3, 6)
-            W_CSWAP(1, 2) W_CSWAP(3, 4) W_CSWAP(5, 6)
-#endif
 #undef W_CSWAP
             if (key[0] < INFINITY) {
                 cur = ref[0];
@@ -430,22 +376,11 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                 }
             }
         }
-#if RT_W_LOOP >= 2
         else {
-#else
-        if (cur == W_EMPTY)
-            break;
-        {
-#endif
         // ---- a leaf: its triangles, closest hit kept; equal t from another triangle is a tie ----
         W_STEP_HOOK(cur, 1);
         const uint32_t first = (cur >> 3) & 0x0FFFFFFFu, cnt = (cur & 7u) + 1u;
-#if RT_W_LOOP == 3
-        // one triangle per step: the leaf link advances to the next triangle
-        const uint32_t kend = first + 1;
-#else
         const uint32_t kend = first + cnt;
-#endif
         // the leaf's triangles in order (loading two records at a time was measured slower)
         auto fold = [&](const GTri& T, uint32_t k) {
             nt++;
@@ -470,12 +405,6 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
         };
         for (uint32_t k = first; k < kend; k++)
             fold(load_gtri(tris + k), k);
-#if RT_W_LOOP == 3
-        if (cnt > 1) {
-            cur = W_LEAF | ((first + 1) << 3) | (cnt - 2);
-            continue;
-        }
-#endif
         cur = W_EMPTY;
         while (sp > 0) {
             uint2 e = stk.get(--sp);
@@ -490,7 +419,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
         work[0] += nn;
         work[1] += nt;
         work[3] += steps;
-        // why a query is not certified (diagnostics): 1 stack overflow / budget, 2 NaN hit,
+        // why a query is not certified (diagnostics): 1 stack overflow, 2 NaN hit,
         // 4 only overflowed hits, 8 tie, 16 minimum t not in (0, inf)
         work[2] = (overflow ? 1u : 0u) | (nanhit ? 2u : 0u) | (h.k < 0 && infhit ? 4u : 0u) |
                   (h.k >= 0 && ties && tie ? 8u : 0u) | (h.k >= 0 && !(h.t > 0.0f && h.t < INFINITY) ? 16u : 0u);
