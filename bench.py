@@ -8,14 +8,19 @@ renders the whole frame: ray generation, octree traversal, Moller-Trumbore,
 shadow rays, RT shading, quantisation and the SSAA downscale, as image strips on
 N GPUs (one process per GPU) followed by the RCCL all-gather of the strips.
 
-Run: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* from the env).
+Run: python bench.py [--gpus N --steps K --warmup W].  For N > 1 the driver launches it
+under torch.distributed.run (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* from the env); when
+WORLD_SIZE is unset and N > 1, bench.py starts that launcher itself as a child process
+before anything touches a GPU.  --dry-run exercises the launch / strip / gather / check
+plumbing on CPU ranks over gloo with synthetic pattern strips (no GPU, no renderer).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -24,7 +29,14 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-PEAK_HBM_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md)
+# Roofline.  The kernel is bound by dependent gathers through L1 / L2, not by
+# HBM: its ~130 MB working set stays in L2 and the Infinity Cache (profiles/r02d: 104 MB of
+# HBM traffic per launch against 4.2 GB read by the traversal).  The executed bytes are
+# priced against the L2 ceiling; the HBM rate and the guide's random-row gather rate are
+# reported beside it.  Peaks: /opt/skills/guides/MI355X_MICROARCH.md.
+PEAK_L2_GBS = 34500.0        # L2 aggregate, 8 XCDs (MI355X_MICROARCH.md, L2 per XCD)
+PEAK_HBM_GBS = 8000.0        # HBM3E spec peak
+GATHER_151MB_GBS = 7650.0    # uniformly random 1,152-B rows of a 151 MB table (Indexed rows: 7.4-7.9 TB/s)
 NODE_BYTES = 56              # one octree k-DOP test reads 14 floats
 TRI_BYTES = 48               # one Moller-Trumbore test reads a, b-a, c-a, n
 WIDE_NODE_BYTES = 96         # one wide-BVH node visit reads the 96-B node (6 x 16-B loads)
@@ -33,6 +45,7 @@ PIXEL_BYTES = 4              # ARGB32 write per internal pixel
 COUNTS_FILE = os.path.join(ROOT, "profiles", "work_counts.json")
 # rocprofv3 PMC summary of this kernel on the same command (tools/profile_gpu.sh + profile_summary.py)
 PROFILE_SUMMARY = os.path.join(ROOT, "profiles", "r02d", "summary.json")
+C5_CHECK_ROWS = (172, 400, 540, 907)   # output rows whose internal row pairs bench's C5 mode checks
 
 
 def parse():
@@ -43,25 +56,67 @@ def parse():
     ap.add_argument("--config", default="sphere1m")
     ap.add_argument("--band-rows", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-check", action="store_true", help="skip max_abs_dpixel (the oracle frame)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--inflight", type=int, default=2,
                     help="frames in flight: consecutive steps alternate over this many streams (DESIGN.md 7)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU ranks over gloo, synthetic pattern strips: the launch / gather / check plumbing only")
     return ap.parse_args()
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int) -> int:
+    """--gpus N > 1 without a launcher: run N ranks under torch.distributed.run as a child
+    process (this process has not touched a GPU) and return its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def pattern_strip(rows: np.ndarray, width: int) -> np.ndarray:
+    """Dry run: a deterministic ARGB value per (global row, column); padding rows stay 0."""
+    col = np.arange(width, dtype=np.uint64)
+    v = (rows.astype(np.int64)[:, None].astype(np.uint64) * np.uint64(0x9E3779B1) + col[None, :] * np.uint64(0x85EBCA77))
+    v = (v ^ (v >> np.uint64(15))) & np.uint64(0x00FFFFFF)
+    out = (v | np.uint64(0xFF000000)).astype(np.uint32)
+    out[rows < 0] = 0
+    return out.view(np.int32)
+
+
+def max_abs_dpixel(a: np.ndarray, b: np.ndarray) -> int:
+    a = np.asarray(a).ravel().view(np.uint32)
+    b = np.asarray(b).ravel().view(np.uint32)
+    d = 0
+    for sh in (16, 8, 0):
+        d = max(d, int(np.max(np.abs(((a >> sh) & 0xFF).astype(np.int32) - ((b >> sh) & 0xFF).astype(np.int32)))))
+    return d
 
 
 def main():
     args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "0"))
+    if world == 0 and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    world = max(world, 1)
+    if args.dry_run:
+        return dry_run(args, world)
     import torch
     import torch.distributed as dist
     from raytracercpp_amd import scenes
     from raytracercpp_amd.renderer import Renderer
     from raytracercpp_amd.strips import FramePipeline, assemble_torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -70,6 +125,7 @@ def main():
         opts = dist.ProcessGroupNCCL.Options()
         opts.is_high_priority_stream = True
         dist.init_process_group("nccl", device_id=dev, pg_options=opts)
+        world = dist.get_world_size()
 
     sc, st = scenes.CONFIGS[args.config]()
     r = Renderer(local)
@@ -90,9 +146,10 @@ def main():
     step, drain = pipe.step, pipe.drain
 
     t_build0 = time.perf_counter()
-    step()   # first call builds + uploads the octree
+    step()   # first call builds + uploads the octree and the wide BVH
     drain()
     t_first = time.perf_counter() - t_build0
+    build = r.stats()
     shadow_local, refl_local = r.band_counters()
     for _ in range(args.warmup):
         step()
@@ -114,16 +171,15 @@ def main():
 
     t = torch.tensor([elapsed, float(shadow_local), k_mean, float(refl_local)], dtype=torch.float64, device=dev)
     if world > 1:
-        tm = t.clone()
-        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
-        ts = t.clone()
-        dist.all_reduce(ts, op=dist.ReduceOp.SUM)
-        elapsed_max = float(tm[0])
-        shadow_total = int(ts[1])
-        k_mean_max = float(tm[2])
-        refl_total = int(ts[3])
+        allt = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(allt, t)
+        per_rank = torch.stack(allt).cpu().numpy()
     else:
-        elapsed_max, shadow_total, k_mean_max, refl_total = elapsed, int(shadow_local), k_mean, int(refl_local)
+        per_rank = t.cpu().numpy()[None, :]
+    elapsed_max = float(per_rank[:, 0].max())
+    shadow_total = int(per_rank[:, 1].sum())
+    k_max, k_min = float(per_rank[:, 2].max()), float(per_rank[:, 2].min())
+    refl_total = int(per_rank[:, 3].sum())
     c5 = args.config == "sphere1m_refl"
     frame = assemble_torch(pipe.parts[last], H, band) if rank == 0 else None
 
@@ -154,114 +210,218 @@ def main():
                                     "primary + shadow, octree 12/40"), "image": [W, H], "render": [rw, rh],
                        "rays_per_frame": rays, "primary_rays": primary, "shadow_rays": shadow_total,
                        "reflection_rays": refl_total, "band_rows": band, "parallelism": f"image strips x{world}",
-                       "frames_in_flight": q},
-            "kernel_ms": round(k_mean_max, 4),
+                       "frames_in_flight": q, "world_size": world},
+            "kernel_ms": round(k_max, 4),
+            "kernel_ms_per_rank": {"max": round(k_max, 4), "min": round(k_min, 4)},
             "first_call_s": round(t_first, 3),
+            "build_ms": {"total": round(build["build_ms"], 1),
+                         **{k: round(v, 1) for k, v in zip(("octree", "cones_slabs", "wide_bvh", "upload"),
+                                                            build["build_split_ms"])}},
         }
-        counts = None
-        if os.path.exists(COUNTS_FILE):
-            with open(COUNTS_FILE) as f:
-                counts = json.load(f).get(args.config)
-        share = 1.0 / world
-        # Roofline: the bytes the launch's traversal reads, per the counted units of
-        # the RT_COUNT build (tools/count_gpu_work.py -> profiles/work_counts.json "gpu_executed"):
-        # WIDE_NODE_BYTES per wide-BVH node visit, TRI_BYTES per Moller-Trumbore test, CERT_BYTES per
-        # certificate, NODE_BYTES per octree k-DOP test (uncertified queries), PIXEL_BYTES per pixel,
-        # over the mean kernel time; "traffic" is the measured HBM bytes per launch (PMC, 2 x
-        # FETCH_SIZE + WRITE_SIZE) -- the ~90 MB scene lives in L2 / Infinity Cache.
-        ex = counts.get("gpu_executed") if counts else None
-        ms_per_step_local = 1e3 * elapsed_max / args.steps
-        default_path = all(os.environ.get(k, "1") != "0" for k in ("RT_WBVH", "RT_SEG", "RT_CONES"))
-        if ex and default_path:
-            xb = (WIDE_NODE_BYTES * ex.get("wide_node_visits", 0) + TRI_BYTES * ex.get("wide_tri_tests", 0) +
-                  CERT_BYTES * ex.get("wide_certificates", 0) +
-                  NODE_BYTES * (ex["vol_tests_whole_line"] + ex["vol_tests_segment"]) +
-                  TRI_BYTES * (ex["tri_tests_whole_line"] + ex["tri_tests_segment"]) + PIXEL_BYTES * primary)
-            xa = xb * share / (k_mean_max * 1e-3) / 1e9
-            traffic = None
-            if world == 1 and args.config == "sphere1m" and os.path.exists(PROFILE_SUMMARY):
-                with open(PROFILE_SUMMARY) as f:
-                    traffic = json.load(f).get("hbm_traffic_bytes_per_launch")
-            res["roofline"] = {"bound": "hbm", "achieved": round(xa, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                               "frac": round(xa / PEAK_HBM_GBS, 4), "traffic": int(traffic) if traffic else None,
-                               "algorithmic_bytes_per_frame": xb,
-                               "basis": "bytes read by the executed traversal (wide-BVH nodes 96 B, triangles 48 B, "
-                                        "certificates 72 B, octree k-DOPs 56 B) + 4 B/pixel; RT_COUNT counts",
-                               # with frames in flight a launch shares the GPU with the next frame's, so
-                               # its duration (above) is longer than the step; the same bytes over the
-                               # step interval (whole-job rate)
-                               "per_step": {"achieved": round(xb * share / (ms_per_step_local * 1e-3) / 1e9, 1),
-                                            "frac": round(xb * share / (ms_per_step_local * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}}
-            if counts and "child_tests_primary" in counts:
-                # SURVEY.md 8(d)'s model priced on the REFERENCE's traversal (oracle count mode): the work
-                # the reference's octree walk would read, per second of this kernel
-                tests = counts["child_tests_primary"] + counts["child_tests_shadow"]
-                tris = counts["tri_tests_primary"] + counts["tri_tests_shadow"]
-                nbytes = NODE_BYTES * tests + TRI_BYTES * tris + PIXEL_BYTES * primary
-                res["roofline"]["reference_traversal_equivalent"] = {
-                    "bytes_per_frame": nbytes, "achieved": round(nbytes * share / (k_mean_max * 1e-3) / 1e9, 1)}
-        if world == 1 and not args.no_cpu_baseline:
-            if c5:
-                res["cpu_baseline"] = cpu_baseline_c5(sc, st, args.cpu_threads)
-            else:
-                res["cpu_baseline"], res["max_abs_dpixel"] = cpu_baseline(sc, st, img, args.cpu_threads)
+        rl = roofline(args.config, world, k_max, ms_per_step, primary)
+        if rl:
+            res["roofline"] = rl
+        if not args.no_check or (world == 1 and not args.no_cpu_baseline):
+            base, dpx, check = cpu_leg(sc, st, img, args.cpu_threads, c5, check=not args.no_check,
+                                       baseline=world == 1 and not args.no_cpu_baseline)
+            if base:
+                res["cpu_baseline"] = base
+            if dpx is not None:
+                res["max_abs_dpixel"] = dpx
+                res["dpixel_check"] = check
         print(json.dumps(res), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 
-def cpu_baseline(sc, st, gpu_img, threads):
-    """CPU baseline on the box's host cores, and max |dpixel| of the GPU frame.
-    * the reference itself (oracle/_ref/libref_harness.so: the reference's own compiled
-      BVH / triangle / vector code driven by the harness's restated pixel loop, OpenMP
-      schedule(dynamic) over rows as renderer.cpp:1082) timed on a bounded sample of row
-      bands spread over the frame (octree build excluded), when that library was built;
-    * the oracle's C restatement (oracle/liboracle.so, OpenMP) on the full frame, which
-      also gives the pixel comparison (and the baseline when the reference is absent)."""
-    from oracle.bindings import Oracle, RefHarness
-    threads = threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    o = Oracle(sc, st)
-    res = o.render_rows(nthreads=threads)
-    rw, rh = st.render_size()
-    ref = Oracle.downscale(res.argb, rw, rh, st.ssaa_factor) if st.enable_ssaa else res.argb
-    g = gpu_img.ravel()
-    d = 0
-    for sh in (16, 8, 0):
-        d = max(d, int(np.max(np.abs(((g >> sh) & 0xFF).astype(np.int32) - ((ref >> sh) & 0xFF).astype(np.int32)))))
-    port_rays = res.counters["primary_rays"] + res.counters["shadow_rays"]
-    port = {"value": round(port_rays / res.seconds / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"full C4 frame ({rw}x{rh} primary + {res.counters['shadow_rays']} shadow rays) "
-                      f"in {res.seconds:.2f} s, oracle.c OpenMP x{threads}"}
-    if not RefHarness.available():
-        return port, d
-    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
-    stride = 2
-    rr = RefHarness.render_row_sample(sc, st, stride // 2, rh // stride, stride)
-    rays = rr.counters["primary_rays"] + rr.counters["shadow_rays"]
-    base = {"value": round(rays / rr.seconds / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "reference",
-            "sample": f"every {stride}th internal row of the C4 frame ({rh // stride} rows x {rw}: {rr.counters['primary_rays']}"
-                      f" primary + {rr.counters['shadow_rays']} shadow rays in {rr.seconds:.2f} s, octree build "
-                      f"excluded), reference TUs + OpenMP x{threads}",
-            "port_value": port["value"]}
-    return base, d
-
-
-def cpu_baseline_c5(sc, st, threads):
-    """C5: the reference harness on every 128th internal row (primary + shadow + reflection rays)."""
-    from oracle.bindings import RefHarness
-    threads = threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    if not RefHarness.available():
+def roofline(config, world, kernel_ms, ms_per_step, primary):
+    """The roofline object, recomputable from the files it names: unit counts of
+    the RT_COUNT build (profiles/work_counts.json "gpu_executed") times bytes per unit, per
+    launch (this rank's share of the frame), over the launch's HIP-event duration."""
+    if not os.path.exists(COUNTS_FILE):
         return None
+    with open(COUNTS_FILE) as f:
+        counts = json.load(f).get(config)
+    ex = counts.get("gpu_executed") if counts else None
+    if not ex:
+        return None
+    units = {"wide_node_visits": ex.get("wide_node_visits", 0), "wide_tri_tests": ex.get("wide_tri_tests", 0),
+             "certificates": ex.get("wide_certificates", 0),
+             "octree_kdop_tests": ex["vol_tests_whole_line"] + ex["vol_tests_segment"],
+             "octree_tri_tests": ex["tri_tests_whole_line"] + ex["tri_tests_segment"], "pixels": primary}
+    per = {"wide_node_visits": WIDE_NODE_BYTES, "wide_tri_tests": TRI_BYTES, "certificates": CERT_BYTES,
+           "octree_kdop_tests": NODE_BYTES, "octree_tri_tests": TRI_BYTES, "pixels": PIXEL_BYTES}
+    frame_bytes = sum(units[k] * per[k] for k in units)
+    share = 1.0 / world
+    launch_bytes = frame_bytes * share
+    achieved = launch_bytes / (kernel_ms * 1e-3) / 1e9
+    out = {"bound": "l1_l2_gather", "achieved": round(achieved, 1), "peak": PEAK_L2_GBS, "unit": "GB/s",
+           "frac": round(achieved / PEAK_L2_GBS, 4), "traffic": None,
+           "basis": "bytes the launch's traversal reads (units x bytes_per_unit, RT_COUNT build counts for the "
+                    "whole frame, x 1/world) / kernel_ms (HIP events on the launch stream); peak = L2 aggregate",
+           "units_per_frame": units, "bytes_per_unit": per, "bytes_per_launch": int(launch_bytes),
+           "kernel_ms": round(kernel_ms, 4),
+           "counts_source": "profiles/work_counts.json [%s].gpu_executed" % config,
+           "gather_ceiling": {"peak": GATHER_151MB_GBS, "unit": "GB/s", "frac": round(achieved / GATHER_151MB_GBS, 4),
+                              "what": "uniformly random 1,152-B rows of a 151 MB table (MI355X_MICROARCH.md, "
+                                      "Indexed rows), the guide's rate for a working set like this one's ~130 MB"},
+           "per_step": {"achieved": round(launch_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+                        "frac": round(launch_bytes / (ms_per_step * 1e-3) / 1e9 / PEAK_L2_GBS, 4)}}
+    if world == 1 and config == "sphere1m" and os.path.exists(PROFILE_SUMMARY):
+        with open(PROFILE_SUMMARY) as f:
+            traffic = json.load(f).get("hbm_traffic_bytes_per_launch")
+        if traffic:
+            out["traffic"] = int(traffic)
+            hbm = traffic / (kernel_ms * 1e-3) / 1e9
+            out["hbm"] = {"bytes_per_launch": int(traffic), "achieved": round(hbm, 1), "peak": PEAK_HBM_GBS,
+                          "frac": round(hbm / PEAK_HBM_GBS, 4),
+                          "source": os.path.relpath(PROFILE_SUMMARY, ROOT) + " (2 x FETCH_SIZE + WRITE_SIZE)"}
+    if "child_tests_primary" in counts:
+        # SURVEY.md 8(d)'s model priced on the REFERENCE's traversal (oracle count mode): the work
+        # the reference's octree walk would read, per second of this kernel -- a rate of retiring
+        # the reference's work, not a bandwidth
+        tests = counts["child_tests_primary"] + counts["child_tests_shadow"]
+        tris = counts["tri_tests_primary"] + counts["tri_tests_shadow"]
+        nbytes = NODE_BYTES * tests + TRI_BYTES * tris + PIXEL_BYTES * primary
+        out["reference_traversal_equivalent"] = {
+            "bytes_per_frame": nbytes, "rate_GBs": round(nbytes * share / (kernel_ms * 1e-3) / 1e9, 1)}
+    return out
+
+
+def cpu_info(threads):
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = None
+    return {"cpu_model": model, "os_cpu_count": os.cpu_count(), "affinity_cpus": affinity, "threads": threads}
+
+
+def cpu_leg(sc, st, gpu_img, threads, c5, check=True, baseline=True):
+    """The CPU leg (rank 0, outside the timed region): the only place bench.py uses oracle/.
+    * check: max |dpixel| of the GPU frame against the oracle's C restatement -- the full C4
+      frame, or for C5 the row pairs of C5_CHECK_ROWS (oracle.render_row_set, downscaled);
+    * baseline (N = 1): the reference itself (oracle/_ref/libref_harness.so: the reference's
+      own compiled BVH / triangle / vector code under the harness's OpenMP schedule(dynamic)
+      row loop, renderer.cpp:1082) on a bounded row sample, one warm-up pass then the median of
+      5; the port's rate (oracle.c) beside it, or as the baseline when the
+      reference library was not built."""
+    from oracle.bindings import Oracle, RefHarness
+    if not threads:
+        try:
+            aff = len(os.sched_getaffinity(0))
+        except AttributeError:
+            aff = os.cpu_count() or 1
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or aff
     os.environ.setdefault("OMP_NUM_THREADS", str(threads))
     rw, rh = st.render_size()
-    stride = 128
-    rr = RefHarness.render_row_sample(sc, st, stride // 2, rh // stride, stride)
+    W = st.image_width
+    dpx, check_desc, port = None, None, None
+    o = Oracle(sc, st)
+    if check or baseline:
+        if c5:
+            rows = [2 * r + k for r in C5_CHECK_ROWS for k in (0, 1)]
+            res = o.render_row_set(rows, nthreads=threads)
+            ref = Oracle.downscale(res.argb, rw, len(rows), 2).reshape(len(C5_CHECK_ROWS), W)
+            gpu = np.asarray(gpu_img).reshape(-1, W)[list(C5_CHECK_ROWS)]
+            check_desc = f"output rows {list(C5_CHECK_ROWS)} (internal rows {rows}) vs oracle.c, SSAA applied"
+            port_rays = res.counters["primary_rays"] + res.counters["shadow_rays"] + res.counters["reflection_rays"]
+        else:
+            res = o.render_rows(nthreads=threads)
+            ref = Oracle.downscale(res.argb, rw, rh, st.ssaa_factor) if st.enable_ssaa else res.argb
+            gpu = gpu_img
+            check_desc = "whole frame vs oracle.c (the C restatement), SSAA applied"
+            port_rays = res.counters["primary_rays"] + res.counters["shadow_rays"]
+        if check:
+            dpx = max_abs_dpixel(gpu, ref)
+        port = {"value": round(port_rays / res.seconds / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+                "sample": ("the C5 check rows" if c5 else f"full C4 frame ({rw}x{rh} primary + "
+                           f"{res.counters['shadow_rays']} shadow rays)") + f" in {res.seconds:.2f} s, oracle.c OpenMP x{threads}"}
+    if not baseline:
+        return None, dpx, check_desc
+    if not RefHarness.available():
+        port.update(cpu_info(threads))
+        return port, dpx, check_desc
+    stride = 128 if c5 else 2
+    passes = []
+    rr = None
+    for i in range(6):   # one warm-up pass, then 5 timed
+        rr = RefHarness.render_row_sample(sc, st, stride // 2, rh // stride, stride)
+        if i:
+            passes.append(rr.seconds)
+    sec = float(np.median(passes))
     c = rr.counters
-    rays = c["primary_rays"] + c["shadow_rays"] + c["reflection_rays"]
-    return {"value": round(rays / rr.seconds / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "reference",
-            "sample": f"every {stride}th internal row ({rh // stride} rows x {rw}: {c['primary_rays']} primary + "
-                      f"{c['shadow_rays']} shadow + {c['reflection_rays']} reflection rays in {rr.seconds:.2f} s), "
-                      f"reference TUs + OpenMP x{threads}"}
+    rays = c["primary_rays"] + c["shadow_rays"] + (c["reflection_rays"] if c5 else 0)
+    base = {"value": round(rays / sec / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "reference",
+            "sample": f"every {stride}th internal row of the {'C5' if c5 else 'C4'} frame ({rh // stride} rows x {rw}: "
+                      f"{c['primary_rays']} primary + {c['shadow_rays']} shadow"
+                      + (f" + {c['reflection_rays']} reflection" if c5 else "") +
+                      f" rays, octree build excluded), reference TUs + OpenMP x{threads}; median of 5 passes "
+                      f"after one warm-up ({', '.join(f'{p:.3f}' for p in passes)} s)",
+            "port_value": port["value"] if port else None}
+    base.update(cpu_info(threads))
+    return base, dpx, check_desc
+
+
+def dry_run(args, world):
+    """--dry-run: gloo ranks, each 'renders' its bands as a pattern keyed by the global row
+    (strips.rank_rows), frames in flight through strips.FramePipeline, the same all-gather and
+    re-assembly as the GPU path; rank 0 checks the frame against the pattern computed whole."""
+    import torch
+    import torch.distributed as dist
+    from raytracercpp_amd import scenes
+    from raytracercpp_amd.strips import FramePipeline, assemble, local_rows, rank_rows
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+        world = dist.get_world_size()
+    _, st = scenes.CONFIGS[args.config]()
+    W, H = st.image_width, st.image_height
+    band = args.band_rows
+    nloc = local_rows(H, band, world)
+    rows = rank_rows(H, band, rank, world)
+    outs = [torch.zeros((nloc, W), dtype=torch.int32) for _ in range(max(1, args.inflight))]
+
+    def render(o, _stream):
+        o.copy_(torch.from_numpy(pattern_strip(rows, W)))
+    pipe = FramePipeline(render, outs, world, None, dist if world > 1 else None)
+    for _ in range(args.warmup):
+        pipe.step()
+    pipe.drain()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    last = 0
+    for _ in range(args.steps):
+        last = pipe.step()
+    pipe.drain()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if rank == 0:
+        parts = [p.numpy() for p in pipe.parts[last]]
+        frame = assemble(parts, H, band)
+        expect = pattern_strip(np.arange(H), W)
+        ms = 1e3 * elapsed / max(1, args.steps)
+        print(json.dumps({"metric": "dry run: strip layout + gloo all-gather + re-assembly (no rendering)",
+                          "value": 0.0, "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+                          "scaling": "strong", "vs_baseline": None, "dtype": "u32", "data": "synthetic pattern strips",
+                          "config": {"workload": "dry run", "image": [W, H], "band_rows": band,
+                                     "parallelism": f"image strips x{world}", "world_size": world},
+                          "dry_run": True, "max_abs_dpixel": max_abs_dpixel(frame, expect)}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":
