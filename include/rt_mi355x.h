@@ -101,8 +101,9 @@ typedef struct rt_stats {
     int64_t wave_steps[6];     /* diagnostic builds only: wide-BVH traversal loop iterations of primary queries --
                                   summed over waves (each wave's longest lane), summed over lanes, wave calls --
                                   then the same for shadow queries (SIMD efficiency = lanes / (64 waves)) */
-    float build_split_ms[4];   /* the last scene build (build_ms) split: octree build + flatten, leaf cones and
-                                  slabs, wide BVH, device upload (host milliseconds) */
+    float build_split_ms[4];   /* the last scene build (build_ms) split, host milliseconds: octree build +
+                                  flatten; leaf cones and slabs and wide BVH (these two run concurrently, the
+                                  octree's upload behind the cones); what the uploads add after the wide BVH */
 } rt_stats;
 
 typedef struct rt_renderer rt_renderer;

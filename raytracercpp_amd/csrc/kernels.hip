@@ -2843,6 +2843,28 @@ __global__ __launch_bounds__(BLOCK) void trace_rays_kernel(KParams P, const floa
     out_ret[i] = r ? 1 : 0;
 }
 
+// The wide BVH's triangle records and their metadata, gathered on the device from the octree's
+// (already uploaded) instead of uploading 64 B per triangle again: wide-BVH triangle k is octree
+// slot s = slot[k]; wmeta[k] = {s, its octree leaf, its caller index, that triangle's material}.
+__global__ __launch_bounds__(256) void wide_gather_kernel(const GTri* __restrict__ tris, const int32_t* __restrict__ slot,
+                                                          const uint32_t* __restrict__ leaf_of_slot,
+                                                          const int32_t* __restrict__ tri_id,
+                                                          const int32_t* __restrict__ tri_mat, int n, GTri* wtris,
+                                                          uint4* wmeta)
+{
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= n)
+        return;
+    const int32_t s = slot[k];
+    const float4* src = reinterpret_cast<const float4*>(tris + s);
+    float4* dst = reinterpret_cast<float4*>(wtris + k);
+    dst[0] = src[0];
+    dst[1] = src[1];
+    dst[2] = src[2];
+    const int32_t id = tri_id[s];
+    wmeta[k] = make_uint4((uint32_t)s, leaf_of_slot[s], (uint32_t)id, (uint32_t)tri_mat[id]);
+}
+
 // dynamic LDS of the traversal kernels: the octree level stack, or the wide-BVH stack
 // (the same memory; a lane uses one at a time)
 size_t lds_bytes(const KParams& P)
@@ -2887,6 +2909,17 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(
         hipLaunchKernelGGL((rt::ray_trace_kernel<false, true>), dim3(pblocks), dim3(rt::BLOCK), lds, stream, *P);
     } else
         hipLaunchKernelGGL((rt::ray_trace_kernel<false, false>), dim3(blocks), dim3(rt::BLOCK), lds, stream, *P);
+    return hipGetLastError();
+}
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_wide_gather(
+    const rt::GTri* tris, const int32_t* slot, const uint32_t* leaf_of_slot, const int32_t* tri_id,
+    const int32_t* tri_mat, int n, rt::GTri* wtris, uint4* wmeta, hipStream_t stream)
+{
+    if (n <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(rt::wide_gather_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, tris, slot, leaf_of_slot,
+                       tri_id, tri_mat, n, wtris, wmeta);
     return hipGetLastError();
 }
 

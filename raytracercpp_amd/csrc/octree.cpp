@@ -3,6 +3,7 @@
 // slab distances, the octant assignment and the leaf triangle order are
 // bit-identical to BVH(&triangles, max_depth, leaf_max_obj_count).
 #include "octree.hpp"
+#include "pool.hpp"
 
 #include <algorithm>
 #include <array>
@@ -327,72 +328,6 @@ void build_flat_octree_serial(const float* tri9, int64_t n, int max_depth, int l
 // ---------------------------------------------------------------------------
 namespace {
 
-class Pool {
-public:
-    explicit Pool(int n) : n_(n)
-    {
-        for (int w = 1; w < n; w++)
-            th_.emplace_back([this, w] { loop(w); });
-    }
-    ~Pool()
-    {
-        {
-            std::lock_guard<std::mutex> g(m_);
-            stop_ = true;
-            gen_++;
-        }
-        cv_.notify_all();
-        for (auto& t : th_)
-            t.join();
-    }
-    int size() const { return n_; }
-    // runs f(worker) on every worker (the caller is worker 0) and waits for all
-    void run(const std::function<void(int)>& f)
-    {
-        {
-            std::lock_guard<std::mutex> g(m_);
-            job_ = &f;
-            pending_ = n_ - 1;
-            gen_++;
-        }
-        cv_.notify_all();
-        f(0);
-        std::unique_lock<std::mutex> l(m_);
-        done_.wait(l, [this] { return pending_ == 0; });
-    }
-
-private:
-    void loop(int w)
-    {
-        uint64_t seen = 0;
-        for (;;) {
-            const std::function<void(int)>* f;
-            {
-                std::unique_lock<std::mutex> l(m_);
-                cv_.wait(l, [&] { return gen_ != seen; });
-                seen = gen_;
-                if (stop_)
-                    return;
-                f = job_;
-            }
-            (*f)(w);
-            {
-                std::lock_guard<std::mutex> g(m_);
-                if (--pending_ == 0)
-                    done_.notify_one();
-            }
-        }
-    }
-    int n_;
-    std::vector<std::thread> th_;
-    std::mutex m_;
-    std::condition_variable cv_, done_;
-    const std::function<void(int)>* job_ = nullptr;
-    int pending_ = 0;
-    uint64_t gen_ = 0;
-    bool stop_ = false;
-};
-
 struct Item {
     v3 c;        // Triangle::bbox_centroid
     int32_t t;   // caller triangle index
@@ -405,34 +340,6 @@ struct LNode {
     bool leaf = true;
     float dn[NPLANES], df[NPLANES];
 };
-
-// dynamic work split: calls body(i) for i in [0, n) in chunks
-template <class F>
-void parallel_for(Pool& pool, int64_t n, int64_t chunk, F&& body)
-{
-    std::atomic<int64_t> next{0};
-    pool.run([&](int) {
-        for (;;) {
-            int64_t b = next.fetch_add(chunk);
-            if (b >= n)
-                return;
-            int64_t e = std::min(n, b + chunk);
-            for (int64_t i = b; i < e; i++)
-                body(i);
-        }
-    });
-}
-
-int build_threads()
-{
-    if (const char* e = std::getenv("RT_BUILD_THREADS")) {
-        int v = std::atoi(e);
-        if (v >= 1)
-            return v;
-    }
-    unsigned hc = std::thread::hardware_concurrency();
-    return (int)std::max(1u, std::min(hc, 16u));
-}
 
 }  // namespace
 
@@ -451,6 +358,10 @@ void build_flat_octree(const float* tri9, int64_t n, int max_depth, int leaf_max
         fprintf(stderr, "[octree] %-10s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(now - tick).count());
         tick = now;
     };
+    struct ExitPhase {   // the locals' destructors, reported after them
+        decltype(phase)& ph;
+        ~ExitPhase() { ph("exit"); }
+    } exit_phase{phase};
     Pool pool(nt);
     phase("pool");
 

@@ -9,6 +9,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstring>
+#include <thread>
 
 #include "host_scene.hpp"
 
@@ -30,6 +31,9 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_raster_sha
                                                                             rt::FrameRec* fr1, unsigned int* nfr1,
                                                                             hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ssao(const rt::SsaoArgs* A, hipStream_t stream);
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_wide_gather(
+    const rt::GTri* tris, const int32_t* slot, const uint32_t* leaf_of_slot, const int32_t* tri_id,
+    const int32_t* tri_mat, int n, rt::GTri* wtris, uint4* wmeta, hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_downscale(const uint32_t* in, int w, int h_rows, int f, uint32_t* out,
                                           hipStream_t stream);
 
@@ -119,7 +123,7 @@ int Renderer::init(std::string& err)
     DevBuf* all[] = {&d_nodes_, &d_tris_,  &d_tri_id_, &d_tri_mat_, &d_tri_uv_, &d_mats_,   &d_internal_,
                      &d_image_, &d_rgba_,  &d_hit_id_, &d_hit_t_,   &d_shadow_, &d_counters_,
                      &d_tri9_,  &d_rcount_, &d_roff_,  &d_pieces_,  &d_piece_uv_, &d_zkey_, &d_big_, &d_scan_tmp_,
-                     &d_zbuf_,  &d_nbuf_,   &d_ao_,     &d_cones_, &d_lslab_, &d_wnodes_, &d_wtris_, &d_wmeta_,
+                     &d_zbuf_,  &d_nbuf_,   &d_ao_,     &d_cones_, &d_lslab_, &d_wnodes_, &d_wtris_, &d_wmeta_, &d_wtmp_,
                      &d_dbg_};
     for (DevBuf* b : all) b->device = device_;
     for (auto& b : d_tex_) b.device = device_;
@@ -555,14 +559,54 @@ int Renderer::ensure_device_scene()
             }
         }
         build_split_ms_[0] = ms_since(t0);
-        auto t1 = clk::now();
-        if (s_.enable_bvh)
-            leaf_cones(oct_, cones_, lslab_);
-        else {
-            cones_.clear();
-            lslab_.clear();
-        }
-        build_split_ms_[1] = ms_since(t1);
+        // A helper thread computes the leaf cones and slabs and uploads the octree while this
+        // thread builds the wide BVH (both only read oct_); the wide BVH is uploaded after.
+        std::string up_err;
+        hipError_t up_e = hipSuccess;
+        float cones_ms = 0;
+        std::thread helper([&] {
+            auto t1 = clk::now();
+            if (s_.enable_bvh)
+                leaf_cones(oct_, cones_, lslab_);
+            else {
+                cones_.clear();
+                lslab_.clear();
+            }
+            cones_ms = ms_since(t1);
+            hipError_t e2 = hipSetDevice(device_);
+            size_t nb = oct_.nodes.size() * sizeof(GNode), tb = oct_.tris.size() * sizeof(GTri);
+            if (e2 == hipSuccess &&
+                ((e2 = d_nodes_.reserve(nb)) != hipSuccess || (e2 = d_tris_.reserve(tb)) != hipSuccess ||
+                 (e2 = d_tri_id_.reserve(oct_.tri_id.size() * 4)) != hipSuccess ||
+                 (e2 = d_tri_mat_.reserve(tri_mat_.size() * 4)) != hipSuccess ||
+                 (e2 = d_tri_uv_.reserve(tri_uv_.size() * 4)) != hipSuccess)) {
+                up_e = e2;
+                up_err = "hipMalloc (scene)";
+                return;
+            }
+            if (e2 == hipSuccess && nb) e2 = hipMemcpyAsync(d_nodes_.p, oct_.nodes.data(), nb, hipMemcpyHostToDevice, stream_);
+            if (e2 == hipSuccess && tb) e2 = hipMemcpyAsync(d_tris_.p, oct_.tris.data(), tb, hipMemcpyHostToDevice, stream_);
+            if (e2 == hipSuccess && !lslab_.empty()) {
+                if ((e2 = d_lslab_.reserve(lslab_.size() * 4)) == hipSuccess)
+                    e2 = hipMemcpyAsync(d_lslab_.p, lslab_.data(), lslab_.size() * 4, hipMemcpyHostToDevice, stream_);
+            }
+            if (e2 == hipSuccess && !cones_.empty()) {
+                if ((e2 = d_cones_.reserve(cones_.size() * 4)) == hipSuccess)
+                    e2 = hipMemcpyAsync(d_cones_.p, cones_.data(), cones_.size() * 4, hipMemcpyHostToDevice, stream_);
+            }
+            if (e2 == hipSuccess && !oct_.tri_id.empty())
+                e2 = hipMemcpyAsync(d_tri_id_.p, oct_.tri_id.data(), oct_.tri_id.size() * 4, hipMemcpyHostToDevice, stream_);
+            if (e2 == hipSuccess && !tri_mat_.empty())
+                e2 = hipMemcpyAsync(d_tri_mat_.p, tri_mat_.data(), tri_mat_.size() * 4, hipMemcpyHostToDevice, stream_);
+            if (e2 == hipSuccess && !tri_uv_.empty())
+                e2 = hipMemcpyAsync(d_tri_uv_.p, tri_uv_.data(), tri_uv_.size() * 4, hipMemcpyHostToDevice, stream_);
+            if (e2 == hipSuccess)
+                e2 = hipStreamSynchronize(stream_);
+            if (e2 != hipSuccess) {
+                up_e = e2;
+                up_err = "upload (scene)";
+            }
+        });
         // the wide BVH (wbvh.hpp): RT_WBVH=0 skips it
         auto t2 = clk::now();
         if (s_.enable_bvh && knobs_.wbvh)
@@ -571,59 +615,35 @@ int Renderer::ensure_device_scene()
             wb_ = WBvh();
         build_split_ms_[2] = ms_since(t2);
         auto t3 = clk::now();
+        helper.join();
+        build_split_ms_[1] = cones_ms;
+        if (up_e != hipSuccess)
+            return hip_fail(up_e, up_err.c_str());
         if (!wb_.nodes.empty()) {
-            // per wide-BVH triangle, everything a certified hit needs in one 16-B load: the
+            // the nodes, and the permutation from which the device gathers the wide BVH's triangle
+            // records and, per triangle, everything a certified hit needs in one 16-B load: the
             // octree slot (the record's triangle), the leaf of its certificate, the caller's
-            // triangle index and its material
+            // triangle index and its material (kernels.hip wide_gather_kernel)
             const size_t nk = wb_.slot.size();
-            wmeta_.resize(4 * nk);
-            for (size_t k = 0; k < nk; k++) {
-                const int32_t slot = wb_.slot[k];
-                const int32_t id = oct_.tri_id[(size_t)slot];
-                wmeta_[4 * k + 0] = (uint32_t)slot;
-                wmeta_[4 * k + 1] = wb_.leaf_of_k[k];
-                wmeta_[4 * k + 2] = (uint32_t)id;
-                wmeta_[4 * k + 3] = (uint32_t)tri_mat_[(size_t)id];
-            }
-            size_t wn = wb_.nodes.size() * sizeof(WNode), wt = wb_.tris.size() * sizeof(GTri);
-            if ((e = d_wnodes_.reserve(wn)) != hipSuccess || (e = d_wtris_.reserve(wt)) != hipSuccess ||
-                (e = d_wmeta_.reserve(wmeta_.size() * 4)) != hipSuccess)
+            size_t wn = wb_.nodes.size() * sizeof(WNode);
+            if ((e = d_wnodes_.reserve(wn)) != hipSuccess || (e = d_wtris_.reserve(nk * sizeof(GTri))) != hipSuccess ||
+                (e = d_wmeta_.reserve(nk * 16)) != hipSuccess || (e = d_wtmp_.reserve(nk * 8)) != hipSuccess)
                 return hip_fail(e, "hipMalloc (wide BVH)");
+            int32_t* d_slot = d_wtmp_.as<int32_t>();
+            uint32_t* d_leaf = reinterpret_cast<uint32_t*>(d_slot + nk);
             if ((e = hipMemcpyAsync(d_wnodes_.p, wb_.nodes.data(), wn, hipMemcpyHostToDevice, stream_)) != hipSuccess ||
-                (e = hipMemcpyAsync(d_wtris_.p, wb_.tris.data(), wt, hipMemcpyHostToDevice, stream_)) != hipSuccess ||
-                (e = hipMemcpyAsync(d_wmeta_.p, wmeta_.data(), wmeta_.size() * 4, hipMemcpyHostToDevice, stream_)) !=
-                    hipSuccess)
+                (e = hipMemcpyAsync(d_slot, wb_.slot.data(), nk * 4, hipMemcpyHostToDevice, stream_)) != hipSuccess ||
+                (e = hipMemcpyAsync(d_leaf, wb_.leaf_of_slot.data(), nk * 4, hipMemcpyHostToDevice, stream_)) !=
+                    hipSuccess ||
+                (e = rt_launch_wide_gather(d_tris_.as<GTri>(), d_slot, d_leaf, d_tri_id_.as<int32_t>(),
+                                           d_tri_mat_.as<int32_t>(), (int)nk, d_wtris_.as<GTri>(), d_wmeta_.as<uint4>(),
+                                           stream_)) != hipSuccess ||
+                (e = hipStreamSynchronize(stream_)) != hipSuccess)
                 return hip_fail(e, "upload (wide BVH)");
         }
-        size_t nb = oct_.nodes.size() * sizeof(GNode), tb = oct_.tris.size() * sizeof(GTri);
-        if ((e = d_nodes_.reserve(nb)) != hipSuccess || (e = d_tris_.reserve(tb)) != hipSuccess ||
-            (e = d_tri_id_.reserve(oct_.tri_id.size() * 4)) != hipSuccess ||
-            (e = d_tri_mat_.reserve(tri_mat_.size() * 4)) != hipSuccess ||
-            (e = d_tri_uv_.reserve(tri_uv_.size() * 4)) != hipSuccess)
-            return hip_fail(e, "hipMalloc (scene)");
-        if (nb) e = hipMemcpyAsync(d_nodes_.p, oct_.nodes.data(), nb, hipMemcpyHostToDevice, stream_);
-        if (e == hipSuccess && tb) e = hipMemcpyAsync(d_tris_.p, oct_.tris.data(), tb, hipMemcpyHostToDevice, stream_);
-        if (e == hipSuccess && !lslab_.empty()) {
-            if ((e = d_lslab_.reserve(lslab_.size() * 4)) == hipSuccess)
-                e = hipMemcpyAsync(d_lslab_.p, lslab_.data(), lslab_.size() * 4, hipMemcpyHostToDevice, stream_);
-        }
-        if (e == hipSuccess && !cones_.empty()) {
-            if ((e = d_cones_.reserve(cones_.size() * 4)) == hipSuccess)
-                e = hipMemcpyAsync(d_cones_.p, cones_.data(), cones_.size() * 4, hipMemcpyHostToDevice, stream_);
-        }
-        if (e == hipSuccess && !oct_.tri_id.empty())
-            e = hipMemcpyAsync(d_tri_id_.p, oct_.tri_id.data(), oct_.tri_id.size() * 4, hipMemcpyHostToDevice, stream_);
-        if (e == hipSuccess && !tri_mat_.empty())
-            e = hipMemcpyAsync(d_tri_mat_.p, tri_mat_.data(), tri_mat_.size() * 4, hipMemcpyHostToDevice, stream_);
-        if (e == hipSuccess && !tri_uv_.empty())
-            e = hipMemcpyAsync(d_tri_uv_.p, tri_uv_.data(), tri_uv_.size() * 4, hipMemcpyHostToDevice, stream_);
-        if (e == hipSuccess)
-            e = hipStreamSynchronize(stream_);
-        if (e != hipSuccess)
-            return hip_fail(e, "upload (scene)");
         geom_dirty_ = false;
         tri9_dirty_ = true;
-        build_split_ms_[3] = ms_since(t3);
+        build_split_ms_[3] = ms_since(t3);   // what the uploads added after the wide BVH build
         build_ms_ = ms_since(t0);
     }
     if (mats_dirty_) {

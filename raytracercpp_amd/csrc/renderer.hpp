@@ -178,7 +178,7 @@ private:
     // the wide BVH (wbvh.hpp): nodes, triangle records in its leaf order, slot maps
     WBvh wb_;
     DevBuf d_wnodes_, d_wtris_, d_wmeta_;
-    std::vector<uint32_t> wmeta_;   // host copy of KParams::wmeta (4 words per wide-BVH triangle)
+    DevBuf d_wtmp_;   // the wide BVH's slot map and the octree's slot -> leaf map, for wide_gather_kernel
     DevBuf d_dbg_;                           // diagnostic per-wave records (RT_DEBUG_WAVES)
     bool ssao_ready_ = false;   // the buffers hold the last frame's z / normals
     // raster path: caller-order triangles, per-triangle piece counts / offsets, the piece

@@ -2,13 +2,18 @@
 // records: binned SAH binary tree (16 bins per axis, parallel over subtrees), collapsed
 // to 4-wide nodes by repeatedly opening the child with the largest surface area.
 #include "wbvh.hpp"
+#include "pool.hpp"
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <thread>
+
+#include <emmintrin.h>   // SSE2 (x86-64 baseline): the builder's box min / max four lanes at a time
 
 namespace rt {
 
@@ -61,191 +66,449 @@ Box tri_box(const GTri& g)
 struct BNode {
     Box box;
     int32_t left, right;   // left < 0: leaf
-    int32_t first, count;
+    int32_t first, count;  // primitives [first, first + count) of the final order
+    double ns[3];          // sum of the subtree's stored triangle normals (the slab normal, wbvh.hpp)
+};
+
+// A primitive during the build: its box (a record's vertices, rounded outward) and the
+// octree slot it came from; its centroid is 0.5 lo + 0.5 hi.  The builder partitions these
+// 32-B records in place, so every level of the build reads them sequentially, and keeps
+// boxes in SSE registers (lane 3 unused).
+struct alignas(16) Prim {
+    float lo[3];
+    int32_t id;
+    float hi[3];
+    float pad;
+};
+inline __m128 plo(const Prim& p) { return _mm_load_ps(p.lo); }
+inline __m128 phi(const Prim& p) { return _mm_load_ps(p.hi); }
+// (lane 3 of lo holds the id's bits -- a denormal as a float, slow in arithmetic: masked out)
+inline __m128 pcen(const Prim& p)
+{
+    const __m128 xyz = _mm_castsi128_ps(_mm_setr_epi32(-1, -1, -1, 0));
+    return _mm_add_ps(_mm_mul_ps(_mm_and_ps(plo(p), xyz), _mm_set1_ps(0.5f)), _mm_mul_ps(phi(p), _mm_set1_ps(0.5f)));
+}
+
+// a box as two SSE registers (lane 3 ignored)
+struct VBox {
+    __m128 lo, hi;
+    static VBox empty() { return VBox{_mm_set1_ps(INFINITY), _mm_set1_ps(-INFINITY)}; }
+    void grow(__m128 l, __m128 h)
+    {
+        lo = _mm_min_ps(lo, l);
+        hi = _mm_max_ps(hi, h);
+    }
+    void grow(const VBox& o) { grow(o.lo, o.hi); }
+    Box box() const
+    {
+        alignas(16) float l[4], h[4];
+        _mm_store_ps(l, lo);
+        _mm_store_ps(h, hi);
+        return Box{{l[0], l[1], l[2]}, {h[0], h[1], h[2]}};
+    }
+    static VBox of(const Box& b)
+    {
+        return VBox{_mm_setr_ps(b.lo[0], b.lo[1], b.lo[2], 0.0f), _mm_setr_ps(b.hi[0], b.hi[1], b.hi[2], 0.0f)};
+    }
 };
 
 constexpr int NBINS = 16;
-constexpr int64_t PAR_BIN = 1 << 17;     // nodes with more primitives bin with all threads
-constexpr int64_t PAR_TASK = 1 << 14;    // subtrees at least this large run on their own thread
+constexpr int32_t PAR_BIN = 1 << 14;   // nodes with more primitives are binned and partitioned by every thread
+constexpr int32_t PAR_CHUNK = 1 << 13; // primitives per chunk of a cooperative pass
 
-int wbvh_threads()
-{
-    if (const char* e = std::getenv("RT_BUILD_THREADS")) {
-        int v = std::atoi(e);
-        if (v >= 1)
-            return v;
+struct Bins {
+    int32_t cnt[3][NBINS];
+    VBox box[3][NBINS];
+    void clear()
+    {
+        for (int a = 0; a < 3; a++)
+            for (int i = 0; i < NBINS; i++) {
+                cnt[a][i] = 0;
+                box[a][i] = VBox::empty();
+            }
     }
-    unsigned hc = std::thread::hardware_concurrency();
-    return (int)std::max(1u, std::min(hc, 16u));
+    void add(const Bins& o)
+    {
+        for (int a = 0; a < 3; a++)
+            for (int i = 0; i < NBINS; i++) {
+                cnt[a][i] += o.cnt[a][i];
+                box[a][i].grow(o.box[a][i]);
+            }
+    }
+};
+
+inline int bin_of(float c, float lo, float scale)
+{
+    int k = (int)((c - lo) * scale);
+    return k < 0 ? 0 : (k >= NBINS ? NBINS - 1 : k);
+}
+// the three axes' bins of a centroid at once: trunc(clamp((c - lo) scale, 0, NBINS - 1)), the
+// same integers as bin_of (no NaN: the triangles are finite)
+inline __m128i bins_of(__m128 c, __m128 lo, __m128 scale)
+{
+    __m128 k = _mm_mul_ps(_mm_sub_ps(c, lo), scale);
+    k = _mm_min_ps(_mm_max_ps(k, _mm_setzero_ps()), _mm_set1_ps((float)(NBINS - 1)));
+    return _mm_cvttps_epi32(k);
+}
+inline float lane(__m128 v, int a)
+{
+    alignas(16) float f[4];
+    _mm_store_ps(f, v);
+    return f[a];
 }
 
+// Binned SAH (16 bins per axis) over the primitive records; the children's boxes and centroid
+// boxes come out of the partition pass, so no node re-reads its primitives for its bounds.
 struct Builder {
-    const std::vector<Box>& pb;      // primitive boxes
-    const std::vector<float>& pc;    // primitive centroids [3 * i]
-    std::vector<int32_t>& idx;
-    std::vector<BNode>& nodes;       // preallocated, 2n - 1 nodes at most
-    std::atomic<int32_t> next{1};
-    std::atomic<int> spare;          // threads that may still be started
-    float ct = 1.0f;                 // SAH cost of a node visit, in triangle tests (r02: 2 and 3 were slower)
+    std::vector<Prim, DefaultInitAlloc<Prim>>& P;
+    std::vector<Prim, DefaultInitAlloc<Prim>>& tmp;
+    std::vector<BNode, DefaultInitAlloc<BNode>>& nodes;    // preallocated, 2n - 1 nodes at most
+    const GTri* tris;             // octree records by slot (leaf normal sums)
+    Pool& pool;
+    int32_t next = 1;             // the cooperative phase's node counter (one thread)
+    float ct = 1.0f;              // SAH cost of a node visit, in triangle tests (r02: 2 and 3 were slower)
+    struct Task {
+        int32_t ni, b, e;
+        Box box, cbox;
+        double sah;      // sum of (leaf ? count : 1) x area over the subtree's nodes
+    };
+    double sah_big = 0;
+    std::vector<Task> tasks;      // subtrees below PAR_BIN, built one per thread
+    std::vector<int32_t> big;     // nodes built cooperatively (their normal sums are filled last)
 
-    struct Bins {
-        int32_t cnt[3][NBINS];
-        Box box[3][NBINS];
-        void clear()
-        {
-            for (int a = 0; a < 3; a++)
-                for (int i = 0; i < NBINS; i++) {
-                    cnt[a][i] = 0;
-                    box[a][i] = empty_box();
+    Builder(std::vector<Prim, DefaultInitAlloc<Prim>>& p, std::vector<Prim, DefaultInitAlloc<Prim>>& t,
+            std::vector<BNode, DefaultInitAlloc<BNode>>& n, const GTri* tr, Pool& pl)
+        : P(p), tmp(t), nodes(n), tris(tr), pool(pl)
+    {
+    }
+
+    // best split of a node from its bins: axis (-1: none), bin, cost
+    void best_split(const Bins& B, const float* scale, const Box& box, int& axis, int& split, float& cost) const
+    {
+        axis = split = -1;
+        cost = INFINITY;
+        const float pa = area(box);
+        for (int a = 0; a < 3; a++) {
+            if (scale[a] == 0.0f)
+                continue;
+            float ra[NBINS];
+            int32_t rc[NBINS];
+            Box acc = empty_box();
+            int32_t c = 0;
+            for (int i = NBINS - 1; i >= 1; i--) {
+                grow(acc, B.box[a][i].box());
+                c += B.cnt[a][i];
+                ra[i] = area(acc);
+                rc[i] = c;
+            }
+            acc = empty_box();
+            c = 0;
+            for (int i = 0; i < NBINS - 1; i++) {
+                grow(acc, B.box[a][i].box());
+                c += B.cnt[a][i];
+                if (c == 0 || rc[i + 1] == 0)
+                    continue;
+                float k = ct + (area(acc) * (float)c + ra[i + 1] * (float)rc[i + 1]) / (pa > 0 ? pa : 1.0f);
+                if (k < cost) {
+                    cost = k;
+                    axis = a;
+                    split = i;
                 }
+            }
         }
-        void add(const Bins& o)
-        {
-            for (int a = 0; a < 3; a++)
-                for (int i = 0; i < NBINS; i++) {
-                    cnt[a][i] += o.cnt[a][i];
-                    grow(box[a][i], o.box[a][i]);
-                }
+    }
+
+    static void bin_range(const Prim* p, int32_t n, const float* clo, const float* scale, Bins& B)
+    {
+        const __m128 lo = _mm_setr_ps(clo[0], clo[1], clo[2], 0.0f), sc = _mm_setr_ps(scale[0], scale[1], scale[2], 0.0f);
+        for (int32_t i = 0; i < n; i++) {
+            const Prim& q = p[i];
+            const __m128 l = plo(q), h = phi(q);
+            alignas(16) int32_t k[4];
+            _mm_store_si128(reinterpret_cast<__m128i*>(k), bins_of(pcen(q), lo, sc));
+            for (int a = 0; a < 3; a++) {
+                B.cnt[a][k[a]]++;
+                B.box[a][k[a]].grow(l, h);
+            }
         }
+    }
+
+    // is primitive i left of the split (axis >= 0), or in the first half (axis < 0)
+    struct Pred {
+        int axis, split;
+        float lo, sc;
+        bool operator()(const Prim& q) const { return bin_of(lane(pcen(q), axis), lo, sc) <= split; }
     };
 
-    Builder(const std::vector<Box>& b, const std::vector<float>& c, std::vector<int32_t>& i, std::vector<BNode>& n,
-            int threads)
-        : pb(b), pc(c), idx(i), nodes(n), spare(threads - 1)
+    void make_leaf(BNode& N) const
     {
-    }
-
-    static int bin_of(float c, float lo, float scale)
-    {
-        int k = (int)((c - lo) * scale);
-        return k < 0 ? 0 : (k >= NBINS ? NBINS - 1 : k);
-    }
-
-    void bin_range(int32_t b, int32_t e, const float* clo, const float* scale, Bins& B) const
-    {
-        B.clear();
-        for (int32_t i = b; i < e; i++) {
-            const int32_t p = idx[(size_t)i];
-            for (int a = 0; a < 3; a++) {
-                int k = bin_of(pc[3 * (size_t)p + a], clo[a], scale[a]);
-                B.cnt[a][k]++;
-                grow(B.box[a][k], pb[(size_t)p]);
-            }
-        }
-    }
-
-    void build(int32_t ni, int32_t b, int32_t e)
-    {
-        BNode& N = nodes[(size_t)ni];
-        const int32_t n = e - b;
-        Box box = empty_box(), cb = empty_box();
-        for (int32_t i = b; i < e; i++) {
-            const int32_t p = idx[(size_t)i];
-            grow(box, pb[(size_t)p]);
-            for (int a = 0; a < 3; a++) {
-                cb.lo[a] = std::min(cb.lo[a], pc[3 * (size_t)p + a]);
-                cb.hi[a] = std::max(cb.hi[a], pc[3 * (size_t)p + a]);
-            }
-        }
-        N.box = box;
-        N.first = b;
-        N.count = n;
         N.left = N.right = -1;
-        if (n <= 1)
-            return;
-        float scale[3];
+        N.ns[0] = N.ns[1] = N.ns[2] = 0.0;
+        for (int32_t i = N.first; i < N.first + N.count; i++) {
+            const GTri& t = tris[(size_t)P[(size_t)i].id];
+            for (int a = 0; a < 3; a++)
+                N.ns[a] += t.n[a];
+        }
+    }
+
+    // the split decision shared by both build paths: false -> the node is a leaf; else the
+    // predicate's axis / bin (axis -1: halves in order)
+    bool decide(int32_t n, const Box& box, const Box& cb, float* scale, Bins* B, int& axis, int& split)
+    {
         bool any = false;
         for (int a = 0; a < 3; a++) {
-            float ext = cb.hi[a] - cb.lo[a];
+            const float ext = cb.hi[a] - cb.lo[a];
             scale[a] = ext > 0 ? (float)NBINS / ext : 0.0f;
             any |= ext > 0;
         }
-        int best_axis = -1, best_split = -1;
-        float best_cost = INFINITY;
-        if (any) {
-            Bins B;
-            if (n >= PAR_BIN) {
-                const int nt = wbvh_threads();
-                std::vector<Bins> part((size_t)nt);
-                std::vector<std::thread> th;
-                const int32_t chunk = (n + nt - 1) / nt;
-                for (int t = 0; t < nt; t++)
-                    th.emplace_back([&, t] {
-                        int32_t cb0 = b + t * chunk, ce = std::min(e, cb0 + chunk);
-                        if (cb0 < ce)
-                            bin_range(cb0, ce, cb.lo, scale, part[(size_t)t]);
-                        else
-                            part[(size_t)t].clear();
-                    });
-                for (auto& t : th)
-                    t.join();
-                B = part[0];
-                for (int t = 1; t < nt; t++)
-                    B.add(part[(size_t)t]);
-            } else
-                bin_range(b, e, cb.lo, scale, B);
-            const float pa = area(box);
+        axis = split = -1;
+        if (n <= 1)
+            return false;
+        if (!any)
+            return n > W_MAX_LEAF;   // every centroid equal: halves in order
+        float cost;
+        best_split(*B, scale, box, axis, split, cost);
+        if (axis >= 0 && n <= W_MAX_LEAF && (float)n <= cost)
+            return false;   // a leaf is no more expensive than the best split
+        if (axis < 0)
+            return n > W_MAX_LEAF;
+        return true;
+    }
+
+    // serial subtree build (a task); its nodes' normal sums post-order.  Node indices come from
+    // the task's own counter (a region of its own: no shared atomic per node).
+    void build_serial(int32_t ni, int32_t b, int32_t e, const Box& box, const Box& cb, int32_t& alloc, double& sah)
+    {
+        BNode& N = nodes[(size_t)ni];
+        const int32_t n = e - b;
+        N.box = box;
+        N.first = b;
+        N.count = n;
+        float scale[3];
+        Bins B;
+        bool anyext = false;
+        for (int a = 0; a < 3; a++)
+            anyext |= cb.hi[a] - cb.lo[a] > 0;
+        if (n > 1 && anyext) {
             for (int a = 0; a < 3; a++) {
-                if (scale[a] == 0.0f)
-                    continue;
-                float ra[NBINS];
-                int32_t rc[NBINS];
-                Box acc = empty_box();
-                int32_t c = 0;
-                for (int i = NBINS - 1; i >= 1; i--) {
-                    grow(acc, B.box[a][i]);
-                    c += B.cnt[a][i];
-                    ra[i] = area(acc);
-                    rc[i] = c;
+                const float ext = cb.hi[a] - cb.lo[a];
+                scale[a] = ext > 0 ? (float)NBINS / ext : 0.0f;
+            }
+            B.clear();
+            bin_range(&P[(size_t)b], n, cb.lo, scale, B);
+        }
+        int axis, split;
+        if (!decide(n, box, cb, scale, &B, axis, split)) {
+            make_leaf(N);
+            sah += (double)n * area(box);
+            return;
+        }
+        sah += area(box);
+        // partition (two-sided, every primitive visited once) with the children's bounds
+        VBox lb = VBox::empty(), lc = VBox::empty(), rb = VBox::empty(), rc = VBox::empty();
+        int32_t mid;
+        if (axis >= 0) {
+            const Pred left{axis, split, cb.lo[axis], scale[axis]};
+            int32_t i = b, j = e - 1;
+            for (;;) {
+                while (i <= j && left(P[(size_t)i])) {
+                    lb.grow(plo(P[(size_t)i]), phi(P[(size_t)i]));
+                    const __m128 c = pcen(P[(size_t)i]);
+                    lc.grow(c, c);
+                    i++;
                 }
-                acc = empty_box();
-                c = 0;
-                for (int i = 0; i < NBINS - 1; i++) {
-                    grow(acc, B.box[a][i]);
-                    c += B.cnt[a][i];
-                    if (c == 0 || rc[i + 1] == 0)
-                        continue;
-                    float cost = ct + (area(acc) * (float)c + ra[i + 1] * (float)rc[i + 1]) / (pa > 0 ? pa : 1.0f);
-                    if (cost < best_cost) {
-                        best_cost = cost;
-                        best_axis = a;
-                        best_split = i;
-                    }
+                while (i <= j && !left(P[(size_t)j])) {
+                    rb.grow(plo(P[(size_t)j]), phi(P[(size_t)j]));
+                    const __m128 c = pcen(P[(size_t)j]);
+                    rc.grow(c, c);
+                    j--;
                 }
+                if (i >= j)
+                    break;
+                std::swap(P[(size_t)i], P[(size_t)j]);
+            }
+            mid = i;
+        } else
+            mid = b + n / 2;
+        if (mid == b || mid == e || axis < 0) {
+            mid = b + n / 2;
+            lb = lc = rb = rc = VBox::empty();
+            for (int32_t i = b; i < e; i++) {
+                VBox& bb = i < mid ? lb : rb;
+                VBox& cc = i < mid ? lc : rc;
+                bb.grow(plo(P[(size_t)i]), phi(P[(size_t)i]));
+                const __m128 c = pcen(P[(size_t)i]);
+                cc.grow(c, c);
             }
         }
-        int32_t mid;
-        if (best_axis >= 0) {
-            if (n <= W_MAX_LEAF && (float)n <= best_cost)
-                return;   // a leaf is no more expensive than the best split
-            const int a = best_axis;
-            const float lo = cb.lo[a], sc = scale[a];
-            auto it = std::partition(idx.begin() + b, idx.begin() + e,
-                                     [&](int32_t p) { return bin_of(pc[3 * (size_t)p + a], lo, sc) <= best_split; });
-            mid = (int32_t)(it - idx.begin());
-        } else {
-            // every centroid equal: a leaf if it fits, else halves in index order
-            if (n <= W_MAX_LEAF)
-                return;
-            mid = b + n / 2;
-        }
-        if (mid == b || mid == e)
-            mid = b + n / 2;
-        const int32_t l = next.fetch_add(2);
+        const int32_t l = alloc;
+        alloc += 2;
         N.left = l;
         N.right = l + 1;
-        const bool big = (mid - b) >= PAR_TASK && (e - mid) >= PAR_TASK;
-        const bool par = big && spare.fetch_sub(1) > 0;
-        if (big && !par)
-            spare.fetch_add(1);   // no thread left: give the claim back
-        if (par) {
-            std::thread t([&, l, b, mid] { build(l, b, mid); });
-            build(l + 1, mid, e);
-            t.join();
-            spare.fetch_add(1);
+        build_serial(l, b, mid, lb.box(), lc.box(), alloc, sah);
+        build_serial(l + 1, mid, e, rb.box(), rc.box(), alloc, sah);
+        const BNode &L = nodes[(size_t)l], &R = nodes[(size_t)l + 1];
+        for (int a = 0; a < 3; a++)
+            nodes[(size_t)ni].ns[a] = L.ns[a] + R.ns[a];
+    }
+
+    // cooperative build of the large nodes: binning and a stable partition (through tmp) by
+    // every thread; subtrees below PAR_BIN become tasks
+    void build_big(int32_t ni, int32_t b, int32_t e, const Box& box, const Box& cb)
+    {
+        const int32_t n = e - b;
+        if (n < PAR_BIN) {
+            tasks.push_back(Task{ni, b, e, box, cb, 0.0});
+            return;
+        }
+        big.push_back(ni);
+        sah_big += area(box);
+        BNode& N = nodes[(size_t)ni];
+        N.box = box;
+        N.first = b;
+        N.count = n;
+        float scale[3];
+        for (int a = 0; a < 3; a++) {
+            const float ext = cb.hi[a] - cb.lo[a];
+            scale[a] = ext > 0 ? (float)NBINS / ext : 0.0f;
+        }
+        const int32_t nch = (n + PAR_CHUNK - 1) / PAR_CHUNK;
+        std::vector<Bins> part((size_t)nch);
+        parallel_for(pool, nch, 1, [&](int64_t k) {
+            const int32_t cb0 = b + (int32_t)k * PAR_CHUNK, ce = std::min(e, cb0 + PAR_CHUNK);
+            part[(size_t)k].clear();
+            bin_range(&P[(size_t)cb0], ce - cb0, cb.lo, scale, part[(size_t)k]);
+        });
+        Bins B = part[0];
+        for (int32_t k = 1; k < nch; k++)
+            B.add(part[(size_t)k]);
+        int axis, split;
+        if (!decide(n, box, cb, scale, &B, axis, split)) {
+            make_leaf(N);   // (never for n >= PAR_BIN > W_MAX_LEAF)
+            return;
+        }
+        // stable partition: per chunk, the count going left and both sides' bounds
+        struct Side {
+            int32_t nl;
+            VBox lb, lc, rb, rc;
+        };
+        std::vector<Side> side((size_t)nch);
+        const Pred pred{axis, split, axis >= 0 ? cb.lo[axis] : 0.0f, axis >= 0 ? scale[axis] : 0.0f};
+        const int32_t half = b + n / 2;
+        auto left_of = [&](int32_t i) { return axis >= 0 ? pred(P[(size_t)i]) : i < half; };
+        auto sides = [&](bool halves) {
+            parallel_for(pool, nch, 1, [&](int64_t k) {
+                const int32_t c0 = b + (int32_t)k * PAR_CHUNK, c1 = std::min(e, c0 + PAR_CHUNK);
+                Side& S = side[(size_t)k];
+                S.nl = 0;
+                S.lb = S.lc = S.rb = S.rc = VBox::empty();
+                for (int32_t i = c0; i < c1; i++) {
+                    const bool l = halves ? i < half : left_of(i);
+                    S.nl += l;
+                    const __m128 c = pcen(P[(size_t)i]);
+                    (l ? S.lb : S.rb).grow(plo(P[(size_t)i]), phi(P[(size_t)i]));
+                    (l ? S.lc : S.rc).grow(c, c);
+                }
+            });
+        };
+        sides(false);
+        std::vector<int32_t> loff((size_t)nch), roff((size_t)nch);
+        int32_t nl = 0;
+        for (int32_t k = 0; k < nch; k++) {
+            loff[(size_t)k] = nl;
+            nl += side[(size_t)k].nl;
+        }
+        if (nl == 0 || nl == n) {
+            sides(true);   // a degenerate split: halves in order
+            nl = n / 2;
         } else {
-            build(l, b, mid);
-            build(l + 1, mid, e);
+            int32_t nr = 0;
+            for (int32_t k = 0; k < nch; k++) {
+                roff[(size_t)k] = nl + nr;
+                nr += std::min(e, b + (k + 1) * PAR_CHUNK) - (b + k * PAR_CHUNK) - side[(size_t)k].nl;
+            }
+            parallel_for(pool, nch, 1, [&](int64_t k) {
+                const int32_t c0 = b + (int32_t)k * PAR_CHUNK, c1 = std::min(e, c0 + PAR_CHUNK);
+                int32_t li = b + loff[(size_t)k], ri = b + roff[(size_t)k];
+                for (int32_t i = c0; i < c1; i++)
+                    tmp[(size_t)(left_of(i) ? li++ : ri++)] = P[(size_t)i];
+            });
+            parallel_for(pool, nch, 1, [&](int64_t k) {
+                const int32_t c0 = b + (int32_t)k * PAR_CHUNK, c1 = std::min(e, c0 + PAR_CHUNK);
+                std::copy(tmp.begin() + c0, tmp.begin() + c1, P.begin() + c0);
+            });
+        }
+        VBox lb = VBox::empty(), lc = VBox::empty(), rb = VBox::empty(), rc = VBox::empty();
+        for (const Side& S : side) {
+            lb.grow(S.lb);
+            lc.grow(S.lc);
+            rb.grow(S.rb);
+            rc.grow(S.rc);
+        }
+        const int32_t mid = b + nl;
+        const int32_t l = next;
+        next += 2;
+        N.left = l;
+        N.right = l + 1;
+        build_big(l, b, mid, lb.box(), lc.box());
+        build_big(l + 1, mid, e, rb.box(), rc.box());
+    }
+
+    void run(int32_t n)
+    {
+        VBox vb = VBox::empty(), vc = VBox::empty();
+        {
+            const int32_t nch = (n + PAR_CHUNK - 1) / PAR_CHUNK;
+            std::vector<VBox> pb((size_t)nch), pc((size_t)nch);
+            parallel_for(pool, nch, 1, [&](int64_t k) {
+                const int32_t c0 = (int32_t)k * PAR_CHUNK, c1 = std::min(n, c0 + PAR_CHUNK);
+                VBox a = VBox::empty(), c = VBox::empty();
+                for (int32_t i = c0; i < c1; i++) {
+                    a.grow(plo(P[(size_t)i]), phi(P[(size_t)i]));
+                    const __m128 q = pcen(P[(size_t)i]);
+                    c.grow(q, q);
+                }
+                pb[(size_t)k] = a;
+                pc[(size_t)k] = c;
+            });
+            for (int32_t k = 0; k < nch; k++) {
+                vb.grow(pb[(size_t)k]);
+                vc.grow(pc[(size_t)k]);
+            }
+        }
+        const Box box = vb.box(), cb = vc.box();
+        build_big(0, 0, n, box, cb);
+        if (std::getenv("RT_BUILD_PROFILE"))
+            fprintf(stderr, "[wbvh]   cooperative part done: %zu big nodes, %zu tasks\n", big.size(), tasks.size());
+        auto tt0 = std::chrono::steady_clock::now();
+        // the subtrees, largest first, one per thread at a time; the task over primitives [b, e)
+        // allocates its nodes from [next + 2 b, next + 2 e) (a subtree of m primitives has 2 m - 1
+        // nodes at most, its root allocated above)
+        if (nodes.size() < (size_t)next + 2 * (size_t)n)   // (only after many uneven cooperative splits)
+            nodes.resize((size_t)next + 2 * (size_t)n);
+        std::sort(tasks.begin(), tasks.end(), [](const Task& x, const Task& y) { return x.e - x.b > y.e - y.b; });
+        std::atomic<size_t> ti{0};
+        const int32_t base = next;
+        pool.run([&](int) {
+            for (;;) {
+                const size_t k = ti.fetch_add(1);
+                if (k >= tasks.size())
+                    return;
+                Task& T = tasks[k];
+                int32_t alloc = base + 2 * T.b;
+                build_serial(T.ni, T.b, T.e, T.box, T.cbox, alloc, T.sah);
+            }
+        });
+        if (std::getenv("RT_BUILD_PROFILE"))
+            fprintf(stderr, "[wbvh]   tasks %.2f ms\n",
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tt0).count());
+        // the cooperative nodes' normal sums, children before parents (they were pushed top-down)
+        for (size_t k = big.size(); k-- > 0;) {
+            BNode& N = nodes[(size_t)big[k]];
+            if (N.left < 0)
+                continue;
+            for (int a = 0; a < 3; a++)
+                N.ns[a] = nodes[(size_t)N.left].ns[a] + nodes[(size_t)N.right].ns[a];
         }
     }
 };
@@ -254,12 +517,17 @@ struct Builder {
 // node box's low corner, low planes rounded down and high planes up (exact in double:
 // origin, q and the power-of-two step are all representable), so each decoded box holds
 // its float box.
-// Per child: the area-weighted normal of its subtree's triangles and its vertices (for the
-// orientation slabs, wbvh.hpp)
+// Per child: the sum of its subtree's stored triangle normals (for the orientation slab's
+// normal, wbvh.hpp) and its triangles [first, first + count) of the final order.
 struct ChildGeom {
     double n[3];
-    const int32_t* idx;   // the subtree's triangles: idx[first .. first + count)
     int32_t first, count;
+};
+
+// Per triangle of the final order, for the cone codes: the unit normal in double, or a flag.
+struct UnitN {
+    double u[3];
+    int state;   // 0: |n| in (1e-30, 1e27); 1: n = 0 (never hit: Mdet = 0); 2: out of range (no cone)
 };
 
 // Backface cone code of a child (wbvh.hpp): theta = the largest angle between N and a triangle
@@ -268,22 +536,21 @@ struct ChildGeom {
 // and the float Mdet = n . (-d) is then negative (its rounding is below 2^-22 |n| |d| for |n|
 // in (1e-30, 1e27)).  cos(angle(N, d)) > cos psi  <=>  N . d > cos(psi) |N| |d|: the code is
 // the threshold cos(psi) |N| + 0.01 (the kernel's rounding margin) rounded up in steps of
-// W_CONE_STEP; 255 = no cone (psi <= 0, or a normal out of range).
-int cone_code(const int* nq, const ChildGeom& g, const std::vector<GTri, DefaultInitAlloc<GTri>>& tris)
+// W_CONE_STEP; 255 = no cone (psi <= 0, or a normal out of range).  The largest angle is the
+// arccosine of the smallest cosine.
+int cone_code(const int* nq, const ChildGeom& g, const UnitN* un)
 {
     const double Nl = std::sqrt((double)nq[0] * nq[0] + (double)nq[1] * nq[1] + (double)nq[2] * nq[2]);
-    double theta = 0;
+    double cmin = 1.0;
     for (int32_t i = g.first; i < g.first + g.count; i++) {
-        const GTri& t = tris[(size_t)g.idx[i]];
-        const double n0 = t.n[0], n1 = t.n[1], n2 = t.n[2];
-        const double len = std::sqrt(n0 * n0 + n1 * n1 + n2 * n2);
-        if (len == 0)
+        const UnitN& t = un[i];
+        if (t.state == 1)
             continue;
-        if (!(len > 1e-30 && len < 1e27))
+        if (t.state == 2)
             return 255;
-        const double c = (n0 * nq[0] + n1 * nq[1] + n2 * nq[2]) / (len * Nl);
-        theta = std::max(theta, std::acos(std::max(-1.0, std::min(1.0, c))));
+        cmin = std::min(cmin, (t.u[0] * nq[0] + t.u[1] * nq[1] + t.u[2] * nq[2]) / Nl);
     }
+    const double theta = std::acos(std::max(-1.0, std::min(1.0, cmin)));
     const double psi = std::acos(W_CONE_EPS) - theta - 1e-9;
     if (!(psi > 0))
         return 255;
@@ -291,8 +558,7 @@ int cone_code(const int* nq, const ChildGeom& g, const std::vector<GTri, Default
     return code <= 254 ? (int)code : 255;
 }
 
-WNode quantise(const Box* cb, const uint32_t* link, int nc, const ChildGeom* cg,
-               const std::vector<GTri, DefaultInitAlloc<GTri>>* tris)
+WNode quantise(const Box* cb, const uint32_t* link, int nc, const ChildGeom* cg, const GTri* tris, const UnitN* un)
 {
     WNode w;
     std::memset(&w, 0, sizeof(w));
@@ -342,20 +608,22 @@ WNode quantise(const Box* cb, const uint32_t* link, int nc, const ChildGeom* cg,
             nq[j][a] = len > 0 ? (int)std::lround(127.0 * g.n[a] / len) : (a == 0 ? 1 : 0);
         if (nq[j][0] == 0 && nq[j][1] == 0 && nq[j][2] == 0)
             nq[j][0] = 1;
-        smin[j] = INFINITY;
-        smax[j] = -INFINITY;
+        const double n0 = nq[j][0], n1 = nq[j][1], n2 = nq[j][2];
+        const double o0 = org[0], o1 = org[1], o2 = org[2];
+        double mn = INFINITY, mx = -INFINITY;
         for (int32_t i = g.first; i < g.first + g.count; i++) {
-            const GTri& t = (*tris)[(size_t)g.idx[i]];
-            for (int v = 0; v < 3; v++) {
-                double s = 0;
-                for (int a = 0; a < 3; a++) {
-                    double x = (double)t.a[a] + (v == 1 ? (double)t.ab[a] : v == 2 ? (double)t.ac[a] : 0.0);
-                    s += nq[j][a] * (x - (double)org[a]);
-                }
-                smin[j] = std::min(smin[j], s);
-                smax[j] = std::max(smax[j], s);
-            }
+            const GTri& t = tris[(size_t)i];
+            const double a0 = t.a[0], a1 = t.a[1], a2 = t.a[2];
+            const double s0 = n0 * (a0 - o0) + n1 * (a1 - o1) + n2 * (a2 - o2);
+            const double s1 = n0 * ((a0 + (double)t.ab[0]) - o0) + n1 * ((a1 + (double)t.ab[1]) - o1) +
+                              n2 * ((a2 + (double)t.ab[2]) - o2);
+            const double s2 = n0 * ((a0 + (double)t.ac[0]) - o0) + n1 * ((a1 + (double)t.ac[1]) - o1) +
+                              n2 * ((a2 + (double)t.ac[2]) - o2);
+            mn = std::min(mn, std::min(s0, std::min(s1, s2)));
+            mx = std::max(mx, std::max(s0, std::max(s1, s2)));
         }
+        smin[j] = mn;
+        smax[j] = mx;
         lo_all = std::min(lo_all, smin[j]);
         hi_all = std::max(hi_all, smax[j]);
     }
@@ -381,7 +649,7 @@ WNode quantise(const Box* cb, const uint32_t* link, int nc, const ChildGeom* cg,
         }
         // signed bytes (two's complement), the cone code in byte 3
         w.nrm[j] = (uint32_t)(uint8_t)(int8_t)nq[j][0] | ((uint32_t)(uint8_t)(int8_t)nq[j][1] << 8) |
-                   ((uint32_t)(uint8_t)(int8_t)nq[j][2] << 16) | ((uint32_t)cone_code(nq[j], cg[j], *tris) << 24);
+                   ((uint32_t)(uint8_t)(int8_t)nq[j][2] << 16) | ((uint32_t)cone_code(nq[j], cg[j], un) << 24);
         double q0 = std::floor((smin[j] - (double)slo) / st), q1 = std::ceil((smax[j] - (double)slo) / st);
         q0 = std::max(0.0, std::min(65535.0, q0));
         q1 = std::max(0.0, std::min(65535.0, q1));
@@ -405,80 +673,125 @@ Box decode(const WNode& w, int j, double lo[3], double hi[3])
     return b;
 }
 
-struct Collapser {
-    const std::vector<BNode>& bn;
-    WBvh& out;
-    const std::vector<int32_t>& idx;
-    const std::vector<GTri, DefaultInitAlloc<GTri>>& tris;
-    int64_t max_depth = 0;
+// The 4-wide topology: each wide node opens the binary child with the largest surface area
+// until it has four children (leaves stay leaves).  The top of the tree is planned on one
+// thread; subtrees of at most PLAN_CUT triangles are planned in parallel, each in depth-first
+// preorder into a contiguous range of wide nodes after the top ones.  The geometry (quantise)
+// of every wide node is computed afterwards, in parallel.
+constexpr int32_t PLAN_CUT = 1 << 12;
 
-    uint32_t leaf_ref(const BNode& L) const
+struct Planner {
+    const std::vector<BNode, DefaultInitAlloc<BNode>>& bn;
+    struct Plan {
+        int32_t c[W_WIDTH];   // binary nodes of the children
+        uint32_t link[W_WIDTH];
+        int nc;
+    };
+    struct Stats {
+        int64_t leaves = 0, max_leaf = 0, max_depth = 0;
+        void add(const Stats& o)
+        {
+            leaves += o.leaves;
+            max_leaf = std::max(max_leaf, o.max_leaf);
+            max_depth = std::max(max_depth, o.max_depth);
+        }
+    };
+    struct Cut {
+        int32_t bi;       // the subtree's binary root
+        uint32_t node;    // the top wide node linking to it ...
+        int j;            // ... through its child j
+        int depth;
+        std::vector<Plan> local;
+        Stats st;
+    };
+    std::vector<Plan> plans;
+    std::vector<Cut> cuts;
+    Stats st;
+
+    // the children of the wide node for binary node bi
+    void open(int32_t bi, Plan& p) const
     {
-        return W_LEAF | ((uint32_t)L.first << 3) | (uint32_t)(L.count - 1);
+        p.nc = 0;
+        const BNode& N = bn[(size_t)bi];
+        if (N.left < 0) {
+            p.c[p.nc++] = bi;   // a leaf root: one child
+            return;
+        }
+        p.c[p.nc++] = N.left;
+        p.c[p.nc++] = N.right;
+        while (p.nc < W_WIDTH) {
+            int pick = -1;
+            float pa = -1.0f;
+            for (int j = 0; j < p.nc; j++) {
+                const BNode& C = bn[(size_t)p.c[j]];
+                if (C.left >= 0 && area(C.box) > pa) {
+                    pa = area(C.box);
+                    pick = j;
+                }
+            }
+            if (pick < 0)
+                break;
+            const BNode& C = bn[(size_t)p.c[pick]];
+            p.c[pick] = C.left;
+            p.c[p.nc++] = C.right;
+        }
     }
 
-    uint32_t emit(int32_t bi, int depth)
+    // plan the subtree of binary node bi into 'out' (indices local to it); top: children of at
+    // most PLAN_CUT triangles become cuts instead of being planned here
+    uint32_t plan(int32_t bi, int depth, std::vector<Plan>& out, Stats& s, bool top)
     {
-        max_depth = std::max<int64_t>(max_depth, depth);
-        int32_t c[W_WIDTH];
-        int nc = 0;
-        const BNode& N = bn[(size_t)bi];
-        if (N.left < 0)
-            c[nc++] = bi;   // a leaf root: one child
-        else {
-            c[nc++] = N.left;
-            c[nc++] = N.right;
-            while (nc < W_WIDTH) {
-                int pick = -1;
-                float pa = -1.0f;
-                for (int j = 0; j < nc; j++) {
-                    const BNode& C = bn[(size_t)c[j]];
-                    if (C.left >= 0 && area(C.box) > pa) {
-                        pa = area(C.box);
-                        pick = j;
-                    }
-                }
-                if (pick < 0)
-                    break;
-                const BNode& C = bn[(size_t)c[pick]];
-                c[pick] = C.left;
-                c[nc++] = C.right;
-            }
-        }
-        const uint32_t me = (uint32_t)out.nodes.size();
-        out.nodes.emplace_back();
-        Box cb[W_WIDTH];
+        s.max_depth = std::max<int64_t>(s.max_depth, depth);
+        Plan p;
+        open(bi, p);
+        const uint32_t me = (uint32_t)out.size();
+        out.push_back(p);
         uint32_t link[W_WIDTH];
-        for (int j = 0; j < W_WIDTH; j++) {
-            cb[j] = empty_box();
+        for (int j = 0; j < W_WIDTH; j++)
             link[j] = W_EMPTY;
-        }
-        for (int j = 0; j < nc; j++) {
-            const BNode& C = bn[(size_t)c[j]];
-            cb[j] = C.box;
+        for (int j = 0; j < p.nc; j++) {
+            const BNode& C = bn[(size_t)p.c[j]];
             if (C.left < 0) {
-                link[j] = leaf_ref(C);
-                out.stats.leaves++;
-                out.stats.max_leaf = std::max<int64_t>(out.stats.max_leaf, C.count);
+                link[j] = W_LEAF | ((uint32_t)C.first << 3) | (uint32_t)(C.count - 1);
+                s.leaves++;
+                s.max_leaf = std::max<int64_t>(s.max_leaf, C.count);
+            } else if (top && C.count <= PLAN_CUT) {
+                cuts.push_back(Cut{p.c[j], me, j, depth + 1, {}, {}});
+                link[j] = W_EMPTY;   // patched once the cut has its place
             } else
-                link[j] = emit(c[j], depth + 1);
+                link[j] = plan(p.c[j], depth + 1, out, s, top);
         }
-        ChildGeom cg[W_WIDTH];
-        for (int j = 0; j < nc; j++) {
-            const BNode& C = bn[(size_t)c[j]];
-            cg[j].idx = idx.data();
-            cg[j].first = C.first;
-            cg[j].count = C.count;
-            cg[j].n[0] = cg[j].n[1] = cg[j].n[2] = 0;
-            for (int32_t i = C.first; i < C.first + C.count; i++) {
-                const GTri& t = tris[(size_t)idx[(size_t)i]];
-                for (int a = 0; a < 3; a++)
-                    cg[j].n[a] += t.n[a];
-            }
-        }
-        WNode w = quantise(cb, link, nc, cg, &tris);
-        out.nodes[me] = w;
+        for (int j = 0; j < W_WIDTH; j++)
+            out[me].link[j] = link[j];
         return me;
+    }
+
+    void run(Pool& pool)
+    {
+        plan(0, 1, plans, st, true);
+        parallel_for(pool, (int64_t)cuts.size(), 1, [&](int64_t k) {
+            Cut& c = cuts[(size_t)k];
+            plan(c.bi, c.depth, c.local, c.st, false);
+        });
+        size_t total = plans.size();
+        std::vector<size_t> base(cuts.size());
+        for (size_t k = 0; k < cuts.size(); k++) {
+            base[k] = total;
+            total += cuts[k].local.size();
+            plans[cuts[k].node].link[cuts[k].j] = (uint32_t)base[k];
+            st.add(cuts[k].st);
+        }
+        plans.resize(total);
+        parallel_for(pool, (int64_t)cuts.size(), 1, [&](int64_t k) {
+            const Cut& c = cuts[(size_t)k];
+            for (size_t i = 0; i < c.local.size(); i++) {
+                Plan p = c.local[i];
+                for (int j = 0; j < W_WIDTH; j++)
+                    if (p.link[j] != W_EMPTY && !(p.link[j] & W_LEAF))
+                        p.link[j] += (uint32_t)base[(size_t)k];
+                plans[base[(size_t)k] + i] = p;
+            }
+        });
     }
 };
 
@@ -486,53 +799,99 @@ struct Collapser {
 
 void build_wbvh(const FlatOctree& oct, WBvh& out)
 {
+    const bool prof = std::getenv("RT_BUILD_PROFILE") != nullptr;
+    auto tick = std::chrono::steady_clock::now();
+    auto phase = [&](const char* what) {
+        if (!prof)
+            return;
+        auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[wbvh] %-10s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(now - tick).count());
+        tick = now;
+    };
     out = WBvh();
     const int64_t n = (int64_t)oct.tris.size();
+    Pool pool(build_threads());
     out.leaf_of_slot.assign((size_t)n, 0u);
-    for (size_t i = 0; i < oct.nodes.size(); i++) {
-        const GNode& g = oct.nodes[i];
+    parallel_for(pool, (int64_t)oct.nodes.size(), 4096, [&](int64_t i) {
+        const GNode& g = oct.nodes[(size_t)i];
         if (g.b & LEAF_BIT)
             for (uint32_t s = g.a; s < g.a + (g.b & ~LEAF_BIT); s++)
                 out.leaf_of_slot[s] = (uint32_t)i;
-    }
+    });
     if (n == 0 || n >= ((int64_t)1 << 28))
         return;
-    std::vector<Box> pb((size_t)n);
-    std::vector<float> pc(3 * (size_t)n);
-    std::vector<int32_t> idx((size_t)n);
-    for (int64_t i = 0; i < n; i++) {
-        pb[(size_t)i] = tri_box(oct.tris[(size_t)i]);
-        for (int a = 0; a < 3; a++)
-            pc[3 * (size_t)i + a] = 0.5f * pb[(size_t)i].lo[a] + 0.5f * pb[(size_t)i].hi[a];
-        idx[(size_t)i] = (int32_t)i;
-    }
-    std::vector<BNode> bn((size_t)(2 * n));
-    const int nt = wbvh_threads();
-    Builder B(pb, pc, idx, bn, nt);
-    B.build(0, 0, (int32_t)n);
-    bn.resize((size_t)B.next.load());
+    std::vector<Prim, DefaultInitAlloc<Prim>> P((size_t)n), tmp((size_t)n);
+    parallel_for(pool, n, 8192, [&](int64_t i) {
+        const Box b = tri_box(oct.tris[(size_t)i]);
+        Prim& q = P[(size_t)i];
+        for (int a = 0; a < 3; a++) {
+            q.lo[a] = b.lo[a];
+            q.hi[a] = b.hi[a];
+        }
+        q.pad = 0.0f;
+        q.id = (int32_t)i;
+    });
+    // 2n for the tasks' regions plus room for the cooperative phase's nodes
+    std::vector<BNode, DefaultInitAlloc<BNode>> bn((size_t)(2 * n + 4 * (n / PAR_BIN) + 64));
+    phase("prep");
+    Builder B(P, tmp, bn, oct.tris.data(), pool);
+    B.run((int32_t)n);
+    phase("binary");
     // SAH cost of the binary tree (diagnostic)
     {
         const float ra = area(bn[0].box) > 0 ? area(bn[0].box) : 1.0f;
-        double s = 0;
-        for (const BNode& N : bn)
-            s += (N.left < 0 ? (double)N.count : 1.0) * area(N.box) / ra;
-        out.stats.sah = (float)s;
+        double s = B.sah_big;
+        for (const auto& T : B.tasks)
+            s += T.sah;
+        out.stats.sah = (float)(s / ra);
     }
-    Collapser C{bn, out, idx, oct.tris};
-    out.nodes.reserve(bn.size() / 2 + 1);
-    C.emit(0, 1);
-    out.stats.nodes = (int64_t)out.nodes.size();
-    out.stats.depth = C.max_depth;
-    out.stats.tris = n;
+    // the triangles in the final (leaf) order, and the cone codes' unit normals
     out.tris.resize((size_t)n);
     out.slot.resize((size_t)n);
     out.leaf_of_k.resize((size_t)n);
-    for (int64_t i = 0; i < n; i++) {
-        out.tris[(size_t)i] = oct.tris[(size_t)idx[(size_t)i]];
-        out.slot[(size_t)i] = idx[(size_t)i];
-        out.leaf_of_k[(size_t)i] = out.leaf_of_slot[(size_t)idx[(size_t)i]];
-    }
+    std::vector<UnitN, DefaultInitAlloc<UnitN>> un((size_t)n);
+    parallel_for(pool, n, 8192, [&](int64_t i) {
+        const int32_t s = P[(size_t)i].id;
+        const GTri& t = oct.tris[(size_t)s];
+        out.tris[(size_t)i] = t;
+        out.slot[(size_t)i] = s;
+        out.leaf_of_k[(size_t)i] = out.leaf_of_slot[(size_t)s];
+        const double n0 = t.n[0], n1 = t.n[1], n2 = t.n[2];
+        const double len = std::sqrt(n0 * n0 + n1 * n1 + n2 * n2);
+        UnitN& u = un[(size_t)i];
+        u.state = len == 0 ? 1 : (len > 1e-30 && len < 1e27 ? 0 : 2);
+        u.u[0] = u.state == 0 ? n0 / len : 0.0;
+        u.u[1] = u.state == 0 ? n1 / len : 0.0;
+        u.u[2] = u.state == 0 ? n2 / len : 0.0;
+    });
+    phase("order");
+    Planner pl{bn};
+    pl.plans.reserve(1024);
+    pl.run(pool);
+    phase("plan");
+    out.nodes.resize(pl.plans.size());
+    parallel_for(pool, (int64_t)pl.plans.size(), 64, [&](int64_t w) {
+        const Planner::Plan& p = pl.plans[(size_t)w];
+        Box cb[W_WIDTH];
+        ChildGeom cg[W_WIDTH];
+        for (int j = 0; j < W_WIDTH; j++)
+            cb[j] = empty_box();
+        for (int j = 0; j < p.nc; j++) {
+            const BNode& C = bn[(size_t)p.c[j]];
+            cb[j] = C.box;
+            cg[j].first = C.first;
+            cg[j].count = C.count;
+            for (int a = 0; a < 3; a++)
+                cg[j].n[a] = C.ns[a];
+        }
+        out.nodes[(size_t)w] = quantise(cb, p.link, p.nc, cg, out.tris.data(), un.data());
+    });
+    phase("geometry");
+    out.stats.nodes = (int64_t)out.nodes.size();
+    out.stats.leaves = pl.st.leaves;
+    out.stats.max_leaf = pl.st.max_leaf;
+    out.stats.depth = pl.st.max_depth;
+    out.stats.tris = n;
 }
 
 int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)
