@@ -124,6 +124,14 @@ const char *rt_last_error(void);
 int rt_get_settings(rt_renderer *r, rt_settings *out);
 int rt_set_settings(rt_renderer *r, const rt_settings *s);
 
+/* Exact mode (no reference counterpart).  on != 0: every BVH query walks
+ * the octree over the whole ray line as BVH::intersect does (bvh.h:212-287), so every
+ * result is the reference's by construction, rays grazing a triangle within rounding
+ * included.  Off (default): closest hits come from the certified wide BVH, exact except
+ * for rays whose line is nearly coplanar with a triangle's plane (DESIGN.md 5.6 bounds
+ * that set).  Also RT_EXACT=1 at rt_create. */
+int rt_set_exact(rt_renderer *r, int on);
+
 /* Renderer::change_render_size (renderer.cpp:250-261) */
 int rt_change_render_size(rt_renderer *r, int32_t width, int32_t height);
 

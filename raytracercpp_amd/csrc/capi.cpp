@@ -111,6 +111,10 @@ int rt_set_settings(rt_renderer* r, const rt_settings* s)
 {
     return guarded(R(r), [&] { return s ? R(r)->set_settings(*s) : RT_EINVAL; });
 }
+int rt_set_exact(rt_renderer* r, int on)
+{
+    return guarded(R(r), [&] { return R(r)->set_exact(on != 0); });
+}
 int rt_change_render_size(rt_renderer* r, int32_t w, int32_t h)
 {
     return guarded(R(r), [&] { return R(r)->change_render_size(w, h); });

@@ -263,16 +263,30 @@ struct THit {
 // on the leaf's cone axis (P.cones[a].xyz).  A curved-surface patch is thin along its mean
 // normal, so a line that grazes the surface (a silhouette ray) passes above most patches
 // near it: if the line's parameter intervals inside the box and inside the slab, both
-// widened by a margin far above their rounding, do not overlap (within the query segment),
-// no triangle of the leaf lies on the line and none can be hit.
+// widened by a margin, do not overlap (within the query segment), no triangle of the leaf
+// can be hit.  The margin holds every point Moller-Trumbore can report: it lies within
+// 2^-17 (|o|_inf + S) / Q of its triangle, Q = sin(angle at a) |cos(n, d)|,
+// bounded below by P.lsin[a] and the leaf's cone; a leaf without a Q bound >= 2^-16 (no
+// cone, or a ray within a few degrees of grazing it) is never skipped.
 __device__ __forceinline__ bool leaf_missed(const KParams& P, uint32_t a, const TRay& R)
 {
     if (!P.lslab)
         return false;
+    const float4 c = ldg(reinterpret_cast<const float4*>(P.cones) + a);
+    const float om = fmaxf(fabsf(R.o.x), fmaxf(fabsf(R.o.y), fabsf(R.o.z)));
+    const float dd = R.d.x * R.d.x + R.d.y * R.d.y + R.d.z * R.d.z;
+    if (!(c.w > 0.0f && om <= 0x1p30f && dd >= 0x1p-60f && dd <= 0x1p60f))
+        return false;
+    // cos(n, -d) >= cos(phi + theta): phi = angle(axis, -d), theta the cone's half-angle
+    const float cb = -(c.x * R.d.x + c.y * R.d.y + c.z * R.d.z) / sqrtf(dd);
+    const float lb = c.w * cb - sqrtf(fmaxf(0.0f, 1.0f - c.w * c.w)) * sqrtf(fmaxf(0.0f, 1.0f - cb * cb)) - 0x1p-18f;
+    const float Q = ldg(P.lsin + a) * lb;
+    if (!(Q >= 0x1p-16f))
+        return false;
     const float4* L = reinterpret_cast<const float4*>(P.lslab) + 2 * (size_t)a;
     const float4 lo = ldg(L), hi = ldg(L + 1);
-    const float4 c = ldg(reinterpret_cast<const float4*>(P.cones) + a);
-    const float m = 0x1p-16f * (fmaxf(fabsf(R.o.x), fmaxf(fabsf(R.o.y), fabsf(R.o.z))) + P.scene_scale);
+    const float Sc = om + P.scene_scale;
+    const float m = 0x1p-16f * Sc + 0x1p-17f * Sc / Q * (1.0f + 0x1p-20f);
     const float ix = 1.0f / R.d.x, iy = 1.0f / R.d.y, iz = 1.0f / R.d.z;
     float tx0 = (lo.x - m - R.o.x) * ix, tx1 = (hi.x + m - R.o.x) * ix;
     float ty0 = (lo.y - m - R.o.y) * iy, ty1 = (hi.y + m - R.o.y) * iy;

@@ -38,6 +38,7 @@ struct KParams {
     const float* lslab;       // [8] per GTri slot, at each leaf's first slot: box lo xyz, smin, hi xyz, smax
                               // along the cone axis; nullptr: none (kernels.hip leaf_missed)
     float scene_scale;        // largest |vertex coordinate| (leaf_missed's margin)
+    const float* lsin;        // per GTri slot, at each leaf's first slot: <= sin(angle at a) of its triangles
     // the wide BVH (wbvh.hpp; nullptr: off) -- closest-hit queries certified against the octree
     const WNode* wnodes;
     const GTri* wtris;           // octree records in wide-BVH leaf order

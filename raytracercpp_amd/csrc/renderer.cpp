@@ -75,7 +75,7 @@ Knobs Knobs::from_env()
         const char* v = getenv(name);
         return v ? v[0] != '0' : dflt;
     };
-    k.wbvh = on("RT_WBVH", true);
+    k.wbvh = on("RT_WBVH", true);   // (exact mode overrides: Renderer::fill_params)
     k.seg = on("RT_SEG", true);
     k.cones = on("RT_CONES", true);
     k.lslab = on("RT_LSLAB", true);
@@ -85,6 +85,7 @@ Knobs Knobs::from_env()
     k.refl_sort = on("RT_REFL_SORT", true);
     k.refl_fuse = on("RT_REFL_FUSE", true);
     k.debug_waves = getenv("RT_DEBUG_WAVES") != nullptr;
+    k.exact = on("RT_EXACT", false);
     if (const char* ce = getenv("RT_REFL_CHUNK_LOG2")) {
         const int v = atoi(ce);
         if (v >= 10 && v <= 25)   // small values (tests): many chunks per level
@@ -123,7 +124,7 @@ int Renderer::init(std::string& err)
     DevBuf* all[] = {&d_nodes_, &d_tris_,  &d_tri_id_, &d_tri_mat_, &d_tri_uv_, &d_mats_,   &d_internal_,
                      &d_image_, &d_rgba_,  &d_hit_id_, &d_hit_t_,   &d_shadow_, &d_counters_,
                      &d_tri9_,  &d_rcount_, &d_roff_,  &d_pieces_,  &d_piece_uv_, &d_zkey_, &d_big_, &d_scan_tmp_,
-                     &d_zbuf_,  &d_nbuf_,   &d_ao_,     &d_cones_, &d_lslab_, &d_wnodes_, &d_wtris_, &d_wmeta_, &d_wtmp_,
+                     &d_zbuf_,  &d_nbuf_,   &d_ao_,     &d_cones_, &d_lslab_, &d_lsin_, &d_wnodes_, &d_wtris_, &d_wmeta_, &d_wtmp_,
                      &d_dbg_};
     for (DevBuf* b : all) b->device = device_;
     for (auto& b : d_tex_) b.device = device_;
@@ -295,6 +296,16 @@ int Renderer::set_light_position(float x, float y, float z)
 }
 
 // renderer.cpp:226-233
+// Exact mode: every query walks the octree over the whole line, the
+// reference's own traversal; leaving it rebuilds the wide BVH if it was never built.
+int Renderer::set_exact(bool on)
+{
+    if (knobs_.exact && !on && knobs_.wbvh && wb_.nodes.empty() && s_.enable_bvh)
+        geom_dirty_ = true;
+    knobs_.exact = on;
+    return RT_OK;
+}
+
 int Renderer::set_camera_transform(const float m[16])
 {
     std::memcpy(c2w_, m, sizeof(c2w_));
@@ -468,16 +479,23 @@ static void leaf_slab_axis(const FlatOctree& o, uint32_t a, uint32_t cnt, double
 // cosine between it and any of them, less 1e-6.  Triangles with n == 0 never hit (Mdet ==
 // 0) and are left out; a leaf with a normal too small or too large for the kernel's
 // rounding argument, or a cone of 90 degrees or more, gets no cone (cos = -2).
-static void leaf_cones(const FlatOctree& o, std::vector<float>& out, std::vector<float>& slab)
+static void leaf_cones(const FlatOctree& o, std::vector<float>& out, std::vector<float>& slab, std::vector<float>& lsin)
 {
     out.assign(4 * o.tris.size(), 0.0f);
     slab.assign(8 * o.tris.size(), 0.0f);
+    lsin.assign(o.tris.size(), 0.0f);
     for (const GNode& g : o.nodes) {
         if (!(g.b & LEAF_BIT))
             continue;
         const uint32_t a = g.a, cnt = g.b & ~LEAF_BIT;
         float* c = &out[4 * (size_t)a];
         c[3] = -2.0f;
+        if (cnt > 0) {
+            float sm = 1.0f;
+            for (uint32_t k = a; k < a + cnt; k++)
+                sm = std::min(sm, sin_at_a_f(o.tris[k]));
+            lsin[a] = sm;   // leaf_missed's grazing margin
+        }
         leaf_slab(o, a, cnt, &slab[8 * (size_t)a]);
         double sx = 0, sy = 0, sz = 0;
         bool ok = cnt > 0;
@@ -567,10 +585,11 @@ int Renderer::ensure_device_scene()
         std::thread helper([&] {
             auto t1 = clk::now();
             if (s_.enable_bvh)
-                leaf_cones(oct_, cones_, lslab_);
+                leaf_cones(oct_, cones_, lslab_, lsin_);
             else {
                 cones_.clear();
                 lslab_.clear();
+                lsin_.clear();
             }
             cones_ms = ms_since(t1);
             hipError_t e2 = hipSetDevice(device_);
@@ -589,6 +608,8 @@ int Renderer::ensure_device_scene()
             if (e2 == hipSuccess && !lslab_.empty()) {
                 if ((e2 = d_lslab_.reserve(lslab_.size() * 4)) == hipSuccess)
                     e2 = hipMemcpyAsync(d_lslab_.p, lslab_.data(), lslab_.size() * 4, hipMemcpyHostToDevice, stream_);
+                if (e2 == hipSuccess && (e2 = d_lsin_.reserve(lsin_.size() * 4)) == hipSuccess)
+                    e2 = hipMemcpyAsync(d_lsin_.p, lsin_.data(), lsin_.size() * 4, hipMemcpyHostToDevice, stream_);
             }
             if (e2 == hipSuccess && !cones_.empty()) {
                 if ((e2 = d_cones_.reserve(cones_.size() * 4)) == hipSuccess)
@@ -609,7 +630,7 @@ int Renderer::ensure_device_scene()
         });
         // the wide BVH (wbvh.hpp): RT_WBVH=0 skips it
         auto t2 = clk::now();
-        if (s_.enable_bvh && knobs_.wbvh)
+        if (s_.enable_bvh && knobs_.wbvh && !knobs_.exact)
             build_wbvh(oct_, wb_);
         else
             wb_ = WBvh();
@@ -726,6 +747,7 @@ void Renderer::fill_params(KParams& P) const
     P.cones = (cones_.empty() || !knobs_.cones) ? nullptr : d_cones_.as<float>();
     // (the leaf slabs read the cone axis)
     P.lslab = (!P.cones || lslab_.empty() || !knobs_.lslab) ? nullptr : d_lslab_.as<float>();
+    P.lsin = P.lslab ? d_lsin_.as<float>() : nullptr;
     P.scene_scale = 0.0f;
     if (!oct_.nodes.empty())
         for (int c = 0; c < 3; c++)
@@ -733,7 +755,7 @@ void Renderer::fill_params(KParams& P) const
     // wide BVH: closest-hit queries certified against the octree, when it
     // was built, the scene's scale keeps the certificate's rounding margins (as for the
     // segment queries), and RT_WBVH is not 0
-    if (!wb_.nodes.empty() && knobs_.wbvh && P.scene_scale > 0x1p-20f && P.scene_scale < 0x1p20f) {
+    if (!wb_.nodes.empty() && knobs_.wbvh && !knobs_.exact && P.scene_scale > 0x1p-20f && P.scene_scale < 0x1p20f) {
         P.wnodes = d_wnodes_.as<WNode>();
         P.wtris = d_wtris_.as<GTri>();
         P.wmeta = d_wmeta_.as<uint4>();
@@ -788,7 +810,7 @@ void Renderer::fill_params(KParams& P) const
     // record) and the scene's scale keeps Moller-Trumbore's products far from overflow
     // and underflow, so that the rounding bound of seg_margin holds
     P.seg_scale = 0.0f;
-    if (knobs_.seg && P.nshape == 0 && !oct_.nodes.empty()) {
+    if (knobs_.seg && !knobs_.exact && P.nshape == 0 && !oct_.nodes.empty()) {
         const GNode& root = oct_.nodes[0];
         float S = 0.0f;
         for (int a = 0; a < 3; a++)   // the axis slabs are the vertices' coordinate range

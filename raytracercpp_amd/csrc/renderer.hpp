@@ -46,6 +46,7 @@ struct Knobs {
     bool refl_fuse = true;    // RT_REFL_FUSE=0: the engine's separate list / spawn passes
     int refl_chunk_log2 = 25; // RT_REFL_CHUNK_LOG2 (10..25): sample slots per engine chunk
     bool debug_waves = false; // RT_DEBUG_WAVES: per-wave records of diagnostic builds (rt_debug_read)
+    bool exact = false;       // RT_EXACT=1 / rt_set_exact: wbvh and seg off
     static Knobs from_env();
 };
 
@@ -58,6 +59,8 @@ public:
     // ---- reference API (renderer.h) ----
     const rt_settings& render_settings() const { return s_; }
     int set_settings(const rt_settings& s);
+    int set_exact(bool on);
+    bool exact() const { return knobs_.exact; }
     int change_render_size(int w, int h);
     int set_triangles(const float* tri9, const int32_t* mat, const float* uv6, int64_t n);
     int add_sphere(float cx, float cy, float cz, float r, int mat);
@@ -175,6 +178,8 @@ private:
     // leaf slabs, [8] per GTri slot (renderer.cpp leaf_slab)
     std::vector<float> lslab_;
     DevBuf d_lslab_;
+    std::vector<float> lsin_;   // per leaf (at its first slot): <= sin(angle at a) of its triangles
+    DevBuf d_lsin_;
     // the wide BVH (wbvh.hpp): nodes, triangle records in its leaf order, slot maps
     WBvh wb_;
     DevBuf d_wnodes_, d_wtris_, d_wmeta_;

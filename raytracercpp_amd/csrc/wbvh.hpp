@@ -39,6 +39,8 @@
 
 #include <stdint.h>
 
+#include <algorithm>
+#include <cmath>
 #include <vector>
 
 #include "octree.hpp"
@@ -103,6 +105,25 @@ struct WBvh {
     std::vector<uint32_t> leaf_of_k;      // wide-BVH triangle -> flattened octree leaf node (= leaf_of_slot[slot])
     WStats stats;
 };
+
+// sin of the triangle's angle at a (Moller-Trumbore's vertex): |n| / (|ab| |ac|) with the stored
+// normal, as a float rounded down; 1 for n = 0 (never hit: Mdet = 0); 0 where the rounding
+// analysis of DESIGN.md 5.6 does not apply (|n| outside [2^-60, 2^60] or |ab| |ac| below 2^-60).
+// Host only (kernels.hip leaf_missed's margin).
+inline float sin_at_a_f(const GTri& t)
+{
+    const double n = std::sqrt((double)t.n[0] * t.n[0] + (double)t.n[1] * t.n[1] + (double)t.n[2] * t.n[2]);
+    if (n == 0)
+        return 1.0f;
+    const double ab = std::sqrt((double)t.ab[0] * t.ab[0] + (double)t.ab[1] * t.ab[1] + (double)t.ab[2] * t.ab[2]);
+    const double ac = std::sqrt((double)t.ac[0] * t.ac[0] + (double)t.ac[1] * t.ac[1] + (double)t.ac[2] * t.ac[2]);
+    const double lam = ab * ac;
+    if (!(lam >= 0x1p-60) || !(n >= 0x1p-60 && n <= 0x1p60))
+        return 0.0f;
+    const double s = std::min(1.0, n / lam) * (1 - 1e-9);
+    const float f = (float)s;
+    return (double)f > s ? std::nextafter(f, 0.0f) : f;
+}
 
 // Binned-SAH binary build over the octree's triangle records, collapsed to 4-wide nodes
 // (RT_BUILD_THREADS threads, as the octree build).  Boxes are the records' vertices a,

@@ -83,6 +83,11 @@ class Renderer:
     def change_render_size(self, width: int, height: int):
         self._call("rt_change_render_size", int(width), int(height))
 
+    def set_exact(self, on: bool = True):
+        """Exact mode: every query walks the octree over the whole line, as
+        the reference does, instead of the certified wide BVH."""
+        self._call("rt_set_exact", 1 if on else 0)
+
     # -- geometry (renderer.h:57-62) ------------------------------------------------
     def set_triangles(self, tri9, mat, uv6=None):
         tri9 = f32(tri9).reshape(-1, 9)

@@ -149,7 +149,8 @@ def _voxel_scene(n=8, size=0.2, gap=0.05):
     return base
 
 
-@pytest.mark.parametrize("scene_name", ["robot", "voxels", "sphere1m_surface", "grazing", "tiny", "huge"])
+@pytest.mark.parametrize("scene_name", ["robot", "voxels", "sphere1m_surface", "grazing", "tiny", "huge",
+                                        "grazing_plane"])
 def test_trace_rays_match_oracle(R, scene_name):
     """BVH::intersect on arbitrary rays (rt_trace_rays) vs the oracle: ids, t, u, v, return value."""
     from raytracercpp_amd import scenes
@@ -171,6 +172,15 @@ def test_trace_rays_match_oracle(R, scene_name):
         tiny = rng.choice(np.array([0.0, 1e-13, -1e-13, 1e-30, -1e-41], np.float32), (50000,))
         axis = rng.integers(0, 3, 50000)
         d[np.arange(50000), axis] = tiny
+    elif scene_name == "grazing_plane":
+        # rays meeting a rotated tessellated plane at sin 1e-7..1e-3: Moller-Trumbore reports
+        # hits outside the triangles' boxes; the octree walk tests what the
+        # reference tests and returns its record
+        import dataclasses
+        from test_wbvh import grazing_plane_case
+        tri, o, d = grazing_plane_case()
+        sc, st = scenes.robot1080(width=64, height=36)
+        sc = dataclasses.replace(sc, tri=tri, tri_mat=np.zeros(len(tri), np.int32), tri_uv=None)
     elif scene_name in ("tiny", "huge"):
         # every slab value outside [2^-38, 2^39): the whole scene takes the exact-division path
         f = np.float32(1e-13 if scene_name == "tiny" else 1e13)
@@ -604,7 +614,8 @@ def test_segment_queries_match_oracle(R, scene_name, light):
 
 FRAME_MODES = {
     "generic": {"RT_PLAIN": "0"},   # the kernel without the plain specialisation
-    "octree": {"RT_WBVH": "0"},     # no wide BVH: every query walks the octree (the exact path)
+    "octree": {"RT_WBVH": "0"},     # no wide BVH: every query walks the octree
+    "exact": {"RT_EXACT": "1"},     # exact mode: the octree over the whole line
 }
 
 
@@ -779,3 +790,40 @@ def test_rccl_frame_pipeline_world1():
                         "--master-addr", "127.0.0.1", "--master-port", str(port), "tools/nccl_check.py"],
                        cwd=root, env=env, capture_output=True, text=True, timeout=180)
     assert r.returncode == 0 and "nccl pipeline ok" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
+
+
+def _telephoto_plane_scene(h0=1e-3, roll=0.2, yaw=17.0, fov=0.5, size=20.0, n=400, width=320, height=180):
+    """A 40 x 40 plane of 320,000 triangles, h0 below a telephoto camera (fov 0.5 degrees): the
+    lower part of the frame meets it at grazing angles between 5e-5 and 5e-3."""
+    import dataclasses
+    from raytracercpp_amd import scenes
+    from test_wbvh import _grid
+
+    def rot(ax, deg):
+        a = np.deg2rad(deg)
+        c, s_ = np.cos(a), np.sin(a)
+        return np.array([[c, -s_, 0], [s_, c, 0], [0, 0, 1]]) if ax == "z" else np.array([[c, 0, s_], [0, 1, 0], [-s_, 0, c]])
+    sc, st = scenes.robot1080(width=width, height=height)
+    T = scenes.default_transforms()
+    rw, rh = st.render_size()
+    proj, pinv = T.camera_matrices(fov, np.float32(rw) / np.float32(rh))
+    Rm = rot("z", roll) @ rot("y", yaw)
+    g = _grid(n, size).reshape(-1, 3, 3) + np.array([0, 0, -size - 0.5])
+    tri = (g @ Rm.T + np.array([0, -h0, 0])).reshape(-1, 9).astype(np.float32)
+    sc = dataclasses.replace(sc, tri=tri, tri_mat=np.zeros(len(tri), np.int32), tri_uv=None, proj_inv=pinv, proj=proj,
+                             cam_fov=fov)
+    return sc, st
+
+
+@pytest.mark.parametrize("mode", ["exact", "default"])
+def test_grazing_plane_frame_matches_oracle(make_renderer, mode):
+    """A frame whose rays graze a tessellated plane: exact mode (rt_set_exact)
+    walks the octree as the reference does; the default certificate is exact here too (the
+    adversarial rays of tests/test_wbvh.py are steeper than a frame's pixels reach)."""
+    R = make_renderer()
+    R.set_exact(mode == "exact")
+    sc, st = _telephoto_plane_scene()
+    o = Oracle(sc, st).render_rows()
+    g = gpu_render(R, sc, st)
+    assert int((o.hit_id >= 0).sum()) > 10000
+    _check_vs_oracle(g, o, f"grazing plane {mode}", R=R)
