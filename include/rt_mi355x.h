@@ -132,6 +132,19 @@ int rt_set_settings(rt_renderer *r, const rt_settings *s);
  * that set).  Also RT_EXACT=1 at rt_create. */
 int rt_set_exact(rt_renderer *r, int on);
 
+/* Single-process multi-device rendering (no reference counterpart: the reference renders on
+ * one host, RenderThread::run, QT/mainWindowThreads.cpp:39-65).  ids[0] must be the handle's
+ * device; n = 0 (or ids NULL) returns to one device.  rt_render then renders on every device
+ * the interleaved bands of 8 output rows with band % n == its index in ids (the kernels of
+ * rt_render_bands_device), sends them to ids[0] with RCCL (librccl, loaded at the first call
+ * with n > 1) and re-assembles the frame there: rt_get_image returns the same image as on one
+ * device.  Scene and settings changes on the handle reach the other devices before each
+ * frame.  ids may instead repeat the handle's device n times (n renderers on one device, the
+ * bands copied instead of sent: the same path without RCCL, for one-device machines).
+ * Frames with enable_ssao render on ids[0] alone (SSAO reads across bands);
+ * rt_ray_trace / rt_post_process / rt_get_internal are single-device as before. */
+int rt_set_devices(rt_renderer *r, const int32_t *ids, int32_t n);
+
 /* Renderer::change_render_size (renderer.cpp:250-261) */
 int rt_change_render_size(rt_renderer *r, int32_t width, int32_t height);
 

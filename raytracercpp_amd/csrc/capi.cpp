@@ -111,6 +111,10 @@ int rt_set_settings(rt_renderer* r, const rt_settings* s)
 {
     return guarded(R(r), [&] { return s ? R(r)->set_settings(*s) : RT_EINVAL; });
 }
+int rt_set_devices(rt_renderer* r, const int32_t* ids, int32_t n)
+{
+    return guarded(R(r), [&] { return R(r)->set_devices(ids, n); });
+}
 int rt_set_exact(rt_renderer* r, int on)
 {
     return guarded(R(r), [&] { return R(r)->set_exact(on != 0); });

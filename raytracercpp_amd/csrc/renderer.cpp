@@ -1,5 +1,6 @@
 // renderer.cpp -- rt::Renderer (see renderer.hpp).
 #include "renderer.hpp"
+#include "multidev.hpp"
 
 #include <hipcub/hipcub.hpp>
 
@@ -180,7 +181,7 @@ int Renderer::set_settings(const rt_settings& s)
                        s.bvh_leaf_object_count != s_.bvh_leaf_object_count;
     s_ = s;
     if (bvh_changed)
-        geom_dirty_ = true;
+        geom_dirty_ = true, ++geom_ver_;
     return RT_OK;
 }
 
@@ -223,7 +224,7 @@ int Renderer::set_triangles(const float* tri9, const int32_t* mat, const float* 
     else
         tri_uv_.clear();
     has_bvh_ = s_.enable_bvh;
-    geom_dirty_ = true;
+    geom_dirty_ = true, ++geom_ver_;
     return RT_OK;
 }
 
@@ -260,7 +261,7 @@ int Renderer::clear_geometry()
     shape_kind_.clear();
     shape_.clear();
     shape_mat_.clear();
-    geom_dirty_ = true;
+    geom_dirty_ = true, ++geom_ver_;
     return RT_OK;
 }
 
@@ -269,7 +270,7 @@ int Renderer::set_materials(const float* mats16, int n)
     if (n < 0 || (n > 0 && !mats16))
         return fail(RT_EINVAL, "set_materials: null array");
     mats_.assign(mats16, mats16 + (size_t)MAT_STRIDE * n);
-    mats_dirty_ = true;
+    mats_dirty_ = true, ++mats_ver_;
     return RT_OK;
 }
 
@@ -301,7 +302,7 @@ int Renderer::set_light_position(float x, float y, float z)
 int Renderer::set_exact(bool on)
 {
     if (knobs_.exact && !on && knobs_.wbvh && wb_.nodes.empty() && s_.enable_bvh)
-        geom_dirty_ = true;
+        geom_dirty_ = true, ++geom_ver_;
     knobs_.exact = on;
     return RT_OK;
 }
@@ -372,7 +373,7 @@ int Renderer::set_object_transform(const float m[16])
     mat::transform_points(t, tri_.data(), (int64_t)n, out.data());
     tri_.swap(out);
     has_bvh_ = true;
-    geom_dirty_ = true;
+    geom_dirty_ = true, ++geom_ver_;
     std::memcpy(prev_object_, m, sizeof(prev_object_));
     return RT_OK;
 }
@@ -396,7 +397,7 @@ int Renderer::set_texture(int slot, int w, int h, const float* rgba)
         tex_[slot].h = h;
         tex_[slot].rgba.assign(rgba, rgba + (size_t)w * h * 4);
     }
-    tex_dirty_ = true;
+    tex_dirty_ = true, ++tex_ver_;
     return RT_OK;
 }
 
@@ -413,21 +414,21 @@ int Renderer::set_skybox(const int32_t w[6], const int32_t h[6], const float* co
         sky_[i].h = h[i];
         sky_[i].rgba.assign(faces[i], faces[i] + (size_t)w[i] * h[i] * 4);
     }
-    tex_dirty_ = true;
+    tex_dirty_ = true, ++tex_ver_;
     return RT_OK;
 }
 
 int Renderer::reconstruct_bvh_new()
 {
     has_bvh_ = true;
-    geom_dirty_ = true;
+    geom_dirty_ = true, ++geom_ver_;
     return RT_OK;
 }
 
 int Renderer::destroy_bvh()
 {
     has_bvh_ = false;
-    geom_dirty_ = true;
+    geom_dirty_ = true, ++geom_ver_;
     return RT_OK;
 }
 
@@ -1552,10 +1553,16 @@ void Renderer::take_counters(const unsigned long long* cnt)
 float render(Renderer& renderer, int* rc)
 {
     auto t0 = std::chrono::steady_clock::now();
-    // mainUtils.cpp:10-13: raster_trace or ray_trace by the settings
-    int r = renderer.render_settings().hybrid_rasterization_tracing ? renderer.raster_trace() : renderer.ray_trace();
-    if (r == RT_OK)
-        r = renderer.post_process();
+    int r;
+    if (renderer.multi_active() && !renderer.render_settings().enable_ssao) {
+        // rt_set_devices: bands on every device, gathered to the lead (SSAO frames stay whole)
+        r = renderer.render_multi();
+    } else {
+        // mainUtils.cpp:10-13: raster_trace or ray_trace by the settings
+        r = renderer.render_settings().hybrid_rasterization_tracing ? renderer.raster_trace() : renderer.ray_trace();
+        if (r == RT_OK)
+            r = renderer.post_process();
+    }
     if (rc)
         *rc = r;
     return std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();

@@ -7,6 +7,7 @@
 
 #include <stdint.h>
 
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -105,6 +106,12 @@ public:
     int kernel_times(float* ms, int n);
     int band_counters(unsigned long long out[2]);
     int debug_read(uint64_t* out, int64_t n);   // diagnostic builds: the per-wave records of the last frame
+    // single-process multi-device rendering (rt_set_devices, multidev.hpp): render(Renderer&)
+    // renders interleaved bands on every device and gathers them here with RCCL
+    int set_devices(const int* ids, int n);
+    bool multi_active() const { return multi_ != nullptr; }
+    int render_multi();
+
     // BVH::intersect over n host rays (closest hit, reference semantics)
     int trace_rays(const float* orig, const float* dir, int64_t n, int32_t* id, float* t, float* u, float* v,
                    uint8_t* ret);
@@ -139,6 +146,12 @@ private:
 
     Knobs knobs_;
     int device_;
+    // scene versions (bumped with the dirty flags): what a multi-device helper has mirrored
+    uint64_t geom_ver_ = 0, mats_ver_ = 0, tex_ver_ = 0;
+    uint64_t mir_geom_ = ~0ull, mir_mats_ = ~0ull, mir_tex_ = ~0ull;   // a helper: the lead's versions copied
+    void mirror_from(const Renderer& lead);
+    struct MultiDev;
+    std::unique_ptr<MultiDev> multi_;
     int num_cus_ = 256;
     hipStream_t stream_ = nullptr;
     hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};

@@ -83,6 +83,12 @@ class Renderer:
     def change_render_size(self, width: int, height: int):
         self._call("rt_change_render_size", int(width), int(height))
 
+    def set_devices(self, ids):
+        """rt_set_devices: render() uses every device in ids (ids[0] = this renderer's device),
+        bands gathered to ids[0] with RCCL; an empty list returns to one device."""
+        a = np.ascontiguousarray(list(ids), np.int32)
+        self._call("rt_set_devices", ptr(a, _i32p) if len(a) else None, len(a))
+
     def set_exact(self, on: bool = True):
         """Exact mode: every query walks the octree over the whole line, as
         the reference does, instead of the certified wide BVH."""

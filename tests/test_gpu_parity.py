@@ -827,3 +827,34 @@ def test_grazing_plane_frame_matches_oracle(make_renderer, mode):
     g = gpu_render(R, sc, st)
     assert int((o.hit_id >= 0).sum()) > 10000
     _check_vs_oracle(g, o, f"grazing plane {mode}", R=R)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_set_devices_bands_match_one_device(make_renderer, n):
+    """rt_set_devices with the device repeated n times (n renderers on one device; the band
+    copy replaces the RCCL send): every frame equals the one-device frame and the oracle, also
+    after light, material and geometry changes that the helpers must mirror."""
+    from raytracercpp_amd import scenes
+    from raytracercpp_amd.renderer import render
+    R = make_renderer()
+    sc, st = scenes.bumpy70k(width=200, height=117, enable_ssaa=True, ssaa_factor=2)
+    R.load_scene(sc, st)
+    R.set_devices([0] * n)
+    rw, rh = st.render_size()
+    for step in range(3):
+        if step == 1:
+            R.set_light_position((1.0, 4.0, 3.0))
+            sc.light = np.asarray((1.0, 4.0, 3.0), np.float32)
+        if step == 2:
+            sc.tri = (sc.tri * np.float32(0.9)).astype(np.float32)
+            sc.materials = sc.materials.copy()
+            sc.materials[0, 0] = 0.2
+            R.set_materials(sc.materials)
+            R.set_triangles(sc.tri, sc.tri_mat, sc.tri_uv)
+        render(R)
+        multi = R.get_image().ravel().copy()
+        o = Oracle(sc, st).render_rows()
+        assert np.array_equal(multi, Oracle.downscale(o.argb, rw, rh, 2)), f"step {step}"
+    R.set_devices([])
+    render(R)
+    assert np.array_equal(R.get_image().ravel(), multi)
