@@ -67,7 +67,7 @@ int Renderer::set_devices(const int* ids, int n)
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess)
         return hip_fail(e, "hipGetDeviceCount");
-    if (n < 0 || n > ndev)
+    if (n < 0 || n > 64)
         return fail(RT_EINVAL, "rt_set_devices: n out of range");
     if (ids[0] != device_)
         return fail(RT_EINVAL, "rt_set_devices: ids[0] must be the handle's device");
@@ -76,6 +76,8 @@ int Renderer::set_devices(const int* ids, int n)
     bool one_device = true;
     for (int i = 0; i < n; i++)
         one_device = one_device && ids[i] == device_;
+    if (!one_device && n > ndev)
+        return fail(RT_EINVAL, "rt_set_devices: more devices than the machine has");
     std::set<int> seen;
     for (int i = 0; i < n && !one_device; i++)
         if (ids[i] < 0 || ids[i] >= ndev || !seen.insert(ids[i]).second)
