@@ -344,8 +344,15 @@ class RefHarness:
             L.ref_downscale_argb.argtypes = [_u32p, C.c_int, C.c_int, C.c_int, _u32p]
             L.ref_heap_order.argtypes = [_f32p, C.c_int, _i32p]
             L.ref_ssao.argtypes = [C.POINTER(OrcScene), C.POINTER(OrcSettings), _f32p, _f32p, _u32p, _i32p]
+            L.ref_set_rng_sequential.argtypes = [C.c_int, C.c_uint32]
             cls._lib = L
         return cls._lib
+
+    @classmethod
+    def set_rng_sequential(cls, on, seed=0):
+        """The reference's own XorShiftGenerator stream at OMP_NUM_THREADS=1 (one thread, row
+        order) instead of the path-keyed one; see ref_harness.cpp g_seq."""
+        cls.lib().ref_set_rng_sequential(1 if on else 0, int(seed) & 0xFFFFFFFF)
 
     # --- transforms (mat.cpp) -------------------------------------------------
     @classmethod

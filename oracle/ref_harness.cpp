@@ -38,6 +38,8 @@
 
 #include <omp.h>
 
+#include "xorshift.h"   // the reference's XorShiftGenerator (sequential RNG mode)
+
 #include "analyticShape.h"
 #include "bvh.h"
 #include "camera.h"
@@ -144,6 +146,15 @@ uint32_t h_sample_state(uint32_t key, uint32_t i)
 }
 
 uint32_t h_child_key(uint32_t key, uint32_t i) { return h_mix32(key ^ (0x85EBCA6Bu * (2u * i + 2u))); }
+
+/* Sequential mode (ref_set_rng_sequential): the reference's own stream at OMP_NUM_THREADS=1.
+ * One XorShiftGenerator (the reference's struct, xorshift.h:37-65) seeded as
+ * init_xorshift_generators seeds thread 0's (renderer.cpp:51-59: std::rand()), consumed in
+ * the reference's order: pixels row by row (renderer.cpp:1082-1088, one thread), the three
+ * draws of each rough sample, depth first through the recursion (renderer.cpp:294-313).
+ * Used only to make the statistical fixtures of tests/golden/make_rng_stats.py. */
+static bool g_seq = false;
+static XorShiftGenerator g_seq_gen(1u);
 
 struct HScene {
     std::vector<Triangle> tris;
@@ -376,9 +387,16 @@ struct Tracer {
             } else
                 roughness = m.roughness;
             if (roughness > 0) {
-                float rx = rng.bilateral();
-                float ry = rng.bilateral();
-                float rz = rng.bilateral();
+                float rx, ry, rz;
+                if (g_seq) {
+                    rx = g_seq_gen.get_rand_bilateral();
+                    ry = g_seq_gen.get_rand_bilateral();
+                    rz = g_seq_gen.get_rand_bilateral();
+                } else {
+                    rx = rng.bilateral();
+                    ry = rng.bilateral();
+                    rz = rng.bilateral();
+                }
                 Vector rd = normalize(Vector(rx, ry, rz));
                 if (dot(rd, hi.normal_at_intersection) < 0)
                     rd = -rd;
@@ -668,6 +686,14 @@ void ref_bvh_query(const float* tri9, int64_t ntri, int max_depth, int leaf, con
  * [row_begin, row_begin + row_count), restated on reference primitives. */
 static double g_last_render_seconds = 0.0;
 
+/* Sequential RNG mode (see g_seq): on != 0 renders on one thread in the reference's pixel
+ * order with XorShiftGenerator(seed); 0 returns to the path-keyed stream. */
+void ref_set_rng_sequential(int on, uint32_t seed)
+{
+    g_seq = on != 0;
+    g_seq_gen = XorShiftGenerator(seed);
+}
+
 /* Wall time of the last ref_render_rows pixel loop (the octree build excluded). */
 double ref_last_render_seconds(void) { return g_last_render_seconds; }
 
@@ -700,7 +726,7 @@ static int render_rows_strided(const orc_scene* sc, const orc_settings* st, int 
         return -1;
     orc_counters total = {};
     const double t_start = omp_get_wtime();
-#pragma omp parallel
+#pragma omp parallel if (!g_seq)
     {
         orc_counters local = {};
 #pragma omp for schedule(dynamic)
