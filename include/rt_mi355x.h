@@ -84,7 +84,7 @@ typedef struct rt_stats {
     int64_t reflection_rays;
     float kernel_ms;           /* GPU time of the last ray_trace kernel (HIP events) */
     float post_ms;             /* GPU time of the last post_process */
-    float build_ms;            /* host octree build + flatten + upload */
+    float build_ms;            /* the last geometry change's blocking part: octree build + flatten + upload */
     int64_t octree_inner, octree_leaves, octree_empty_leaves, octree_max_leaf, octree_max_depth;
     int64_t gpu_nodes, gpu_tris;
     int32_t render_width, render_height;
@@ -101,9 +101,9 @@ typedef struct rt_stats {
     int64_t wave_steps[6];     /* diagnostic builds only: wide-BVH traversal loop iterations of primary queries --
                                   summed over waves (each wave's longest lane), summed over lanes, wave calls --
                                   then the same for shadow queries (SIMD efficiency = lanes / (64 waves)) */
-    float build_split_ms[4];   /* the last scene build (build_ms) split, host milliseconds: octree build +
-                                  flatten; leaf cones and slabs and wide BVH (these two run concurrently, the
-                                  octree's upload behind the cones); what the uploads add after the wide BVH */
+    float build_split_ms[4];   /* the last scene build, host milliseconds: octree build + flatten; leaf cones and
+                                  slabs, and the wide BVH with its upload (both on the background thread,
+                                  rt_finish_accel; 0 until adopted); the octree's upload */
 } rt_stats;
 
 typedef struct rt_renderer rt_renderer;
@@ -131,6 +131,14 @@ int rt_set_settings(rt_renderer *r, const rt_settings *s);
  * for rays whose line is nearly coplanar with a triangle's plane (DESIGN.md 5.6 bounds
  * that set).  Also RT_EXACT=1 at rt_create. */
 int rt_set_exact(rt_renderer *r, int on);
+
+/* Acceleration structures beside the octree (no reference counterpart): after a
+ * geometry change the octree (the reference's BVH, renderer.cpp:214-224) is built and uploaded
+ * before the next frame, and the leaf cones / slabs and the wide BVH are built on a background
+ * thread; frames that start before they are resident take the exact octree traversal (the same
+ * images).  rt_finish_accel waits for that build (RT_ASYNC_ACCEL=0 at rt_create: every geometry
+ * change waits for it). */
+int rt_finish_accel(rt_renderer *r);
 
 /* Single-process multi-device rendering (no reference counterpart: the reference renders on
  * one host, RenderThread::run, QT/mainWindowThreads.cpp:39-65).  ids[0] must be the handle's

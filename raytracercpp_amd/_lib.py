@@ -81,6 +81,7 @@ SIGNATURES = {
     "rt_set_settings": (C.c_int, [_H, C.POINTER(RtSettings)]),
     "rt_change_render_size": (C.c_int, [_H, C.c_int32, C.c_int32]),
     "rt_set_exact": (C.c_int, [_H, C.c_int]),
+    "rt_finish_accel": (C.c_int, [_H]),
     "rt_set_devices": (C.c_int, [_H, _i32p, C.c_int32]),
     "rt_set_triangles": (C.c_int, [_H, _f32p, _i32p, _f32p, C.c_int64]),
     "rt_add_sphere": (C.c_int, [_H, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int32]),

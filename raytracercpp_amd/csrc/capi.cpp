@@ -115,6 +115,10 @@ int rt_set_devices(rt_renderer* r, const int32_t* ids, int32_t n)
 {
     return guarded(R(r), [&] { return R(r)->set_devices(ids, n); });
 }
+int rt_finish_accel(rt_renderer* r)
+{
+    return guarded(R(r), [&] { return R(r)->finish_accel(); });
+}
 int rt_set_exact(rt_renderer* r, int on)
 {
     return guarded(R(r), [&] { return R(r)->set_exact(on != 0); });

@@ -362,7 +362,7 @@ void build_flat_octree(const float* tri9, int64_t n, int max_depth, int leaf_max
         decltype(phase)& ph;
         ~ExitPhase() { ph("exit"); }
     } exit_phase{phase};
-    Pool pool(nt);
+    Pool& pool = build_pool();
     phase("pool");
 
     // ---- triangle prep + root box ----
@@ -651,6 +651,7 @@ void build_flat_octree(const float* tri9, int64_t n, int max_depth, int leaf_max
     out.levels = maxd + 1;
     finish_checks(out);
     phase("checks");
+    free_later(std::move(T), std::move(idx), std::move(L), std::move(scratch), std::move(flat), std::move(slot));
 }
 
 }  // namespace rt

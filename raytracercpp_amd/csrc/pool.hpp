@@ -9,7 +9,9 @@
 #include <condition_variable>
 #include <cstdlib>
 #include <functional>
+#include <memory>
 #include <mutex>
+#include <type_traits>
 #include <thread>
 #include <vector>
 
@@ -106,6 +108,14 @@ void parallel_for(Pool& pool, int64_t n, int64_t chunk, F&& body)
     });
 }
 
+// Large temporaries released on a detached thread, off the caller's critical path (freeing
+// hundreds of MB of build scratch takes milliseconds).
+template <class... T>
+void free_later(T&&... v)
+{
+    std::thread([](std::decay_t<T>...) {}, std::move(v)...).detach();
+}
+
 inline int build_threads()
 {
     if (const char* e = std::getenv("RT_BUILD_THREADS")) {
@@ -115,6 +125,18 @@ inline int build_threads()
     }
     unsigned hc = std::thread::hardware_concurrency();
     return (int)std::max(1u, std::min(hc, 16u));
+}
+
+// The calling thread's build pool, created at its first build and kept (joining 16 workers
+// after every build cost more than the build's last phase): builds on different threads
+// (a renderer's background wide-BVH build, another renderer) each have their own.
+inline Pool& build_pool()
+{
+    thread_local std::unique_ptr<Pool> pool;
+    const int nt = build_threads();
+    if (!pool || pool->size() != nt)
+        pool = std::make_unique<Pool>(nt);
+    return *pool;
 }
 
 }  // namespace rt

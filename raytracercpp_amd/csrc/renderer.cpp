@@ -87,6 +87,7 @@ Knobs Knobs::from_env()
     k.refl_fuse = on("RT_REFL_FUSE", true);
     k.debug_waves = getenv("RT_DEBUG_WAVES") != nullptr;
     k.exact = on("RT_EXACT", false);
+    k.async_accel = on("RT_ASYNC_ACCEL", true);
     if (const char* ce = getenv("RT_REFL_CHUNK_LOG2")) {
         const int v = atoi(ce);
         if (v >= 10 && v <= 25)   // small values (tests): many chunks per level
@@ -115,6 +116,8 @@ int Renderer::init(std::string& err)
     if (e == hipSuccess)
         e = hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking);
     if (e == hipSuccess)
+        e = hipStreamCreateWithFlags(&accel_stream_, hipStreamNonBlocking);
+    if (e == hipSuccess)
         e = hipDeviceGetAttribute(&num_cus_, hipDeviceAttributeMultiprocessorCount, device_);
     for (int i = 0; i < 4 && e == hipSuccess; i++)
         e = hipEventCreate(&ev_[i]);
@@ -135,7 +138,10 @@ int Renderer::init(std::string& err)
 
 Renderer::~Renderer()
 {
+    if (accel_thread_.joinable())
+        accel_thread_.join();
     hipSetDevice(device_);
+    if (accel_stream_) hipStreamDestroy(accel_stream_);
     for (auto& e : ev_)
         if (e) hipEventDestroy(e);
     for (auto& e : ring_)
@@ -301,6 +307,7 @@ int Renderer::set_light_position(float x, float y, float z)
 // reference's own traversal; leaving it rebuilds the wide BVH if it was never built.
 int Renderer::set_exact(bool on)
 {
+    poll_accel(true);   // (reads wb_)
     if (knobs_.exact && !on && knobs_.wbvh && wb_.nodes.empty() && s_.enable_bvh)
         geom_dirty_ = true, ++geom_ver_;
     knobs_.exact = on;
@@ -538,6 +545,96 @@ static void leaf_cones(const FlatOctree& o, std::vector<float>& out, std::vector
     }
 }
 
+// The leaf cones / slabs and the wide BVH of the current octree, on accel_thread_ (DESIGN.md
+// 5.8).  Reads oct_ and the uploaded triangle tables; writes only cones_, lslab_, lsin_, wb_, their
+// device buffers and accel_ms_, none of which a frame reads before poll_accel adopts them.
+void Renderer::start_accel()
+{
+    accel_state_.store(1);
+    accel_err_.clear();
+    accel_thread_ = std::thread([this] {
+        using clk = std::chrono::steady_clock;
+        auto ms_since = [](clk::time_point t) { return std::chrono::duration<float, std::milli>(clk::now() - t).count(); };
+        hipError_t e = hipSetDevice(device_);
+        auto t0 = clk::now();
+        leaf_cones(oct_, cones_, lslab_, lsin_);
+        if (e == hipSuccess && !lslab_.empty()) {
+            if ((e = d_lslab_.reserve(lslab_.size() * 4)) == hipSuccess)
+                e = hipMemcpyAsync(d_lslab_.p, lslab_.data(), lslab_.size() * 4, hipMemcpyHostToDevice, accel_stream_);
+            if (e == hipSuccess && (e = d_lsin_.reserve(lsin_.size() * 4)) == hipSuccess)
+                e = hipMemcpyAsync(d_lsin_.p, lsin_.data(), lsin_.size() * 4, hipMemcpyHostToDevice, accel_stream_);
+        }
+        if (e == hipSuccess && !cones_.empty() && (e = d_cones_.reserve(cones_.size() * 4)) == hipSuccess)
+            e = hipMemcpyAsync(d_cones_.p, cones_.data(), cones_.size() * 4, hipMemcpyHostToDevice, accel_stream_);
+        accel_ms_[0] = ms_since(t0);
+        auto t1 = clk::now();
+        if (knobs_.wbvh && !knobs_.exact)
+            build_wbvh(oct_, wb_);
+        else
+            wb_ = WBvh();
+        accel_ms_[1] = ms_since(t1);
+        auto t2 = clk::now();
+        hipSetDevice(device_);
+        if (e == hipSuccess && !wb_.nodes.empty()) {
+            // the nodes, and the permutation from which the device gathers the wide BVH's triangle
+            // records and, per triangle, everything a certified hit needs in one 16-B load: the
+            // octree slot (the record's triangle), the leaf of its certificate, the caller's
+            // triangle index and its material (kernels.hip wide_gather_kernel)
+            const size_t nk = wb_.slot.size(), wn = wb_.nodes.size() * sizeof(WNode);
+            if ((e = d_wnodes_.reserve(wn)) == hipSuccess && (e = d_wtris_.reserve(nk * sizeof(GTri))) == hipSuccess &&
+                (e = d_wmeta_.reserve(nk * 16)) == hipSuccess && (e = d_wtmp_.reserve(nk * 8)) == hipSuccess) {
+                hipSetDevice(device_);
+                int32_t* d_slot = d_wtmp_.as<int32_t>();
+                uint32_t* d_leaf = reinterpret_cast<uint32_t*>(d_slot + nk);
+                if ((e = hipMemcpyAsync(d_wnodes_.p, wb_.nodes.data(), wn, hipMemcpyHostToDevice, accel_stream_)) ==
+                        hipSuccess &&
+                    (e = hipMemcpyAsync(d_slot, wb_.slot.data(), nk * 4, hipMemcpyHostToDevice, accel_stream_)) ==
+                        hipSuccess &&
+                    (e = hipMemcpyAsync(d_leaf, wb_.leaf_of_slot.data(), nk * 4, hipMemcpyHostToDevice, accel_stream_)) ==
+                        hipSuccess)
+                    e = rt_launch_wide_gather(d_tris_.as<GTri>(), d_slot, d_leaf, d_tri_id_.as<int32_t>(),
+                                              d_tri_mat_.as<int32_t>(), (int)nk, d_wtris_.as<GTri>(), d_wmeta_.as<uint4>(),
+                                              accel_stream_);
+            }
+        }
+        if (e == hipSuccess)
+            e = hipStreamSynchronize(accel_stream_);
+        accel_ms_[2] = ms_since(t2);
+        if (e != hipSuccess)
+            accel_err_ = std::string("acceleration structures (upload): ") + hipGetErrorString(e);
+        accel_state_.store(e == hipSuccess ? 2 : 3);
+    });
+}
+
+// Adopts a finished background build (wait: blocks until it is); its structures are resident.
+int Renderer::poll_accel(bool wait)
+{
+    if (!accel_thread_.joinable())
+        return RT_OK;
+    if (!wait && accel_state_.load() == 1)
+        return RT_OK;
+    accel_thread_.join();
+    hipSetDevice(device_);
+    if (accel_state_.load() == 3) {
+        accel_state_.store(0);
+        return fail(RT_EHIP, accel_err_);
+    }
+    accel_state_.store(0);
+    cones_ready_ = !cones_.empty();
+    wide_ready_ = !wb_.nodes.empty();
+    build_split_ms_[1] = accel_ms_[0];
+    build_split_ms_[2] = accel_ms_[1] + accel_ms_[2];
+    return RT_OK;
+}
+
+int Renderer::finish_accel()
+{
+    hipError_t e = hipSetDevice(device_);
+    if (e != hipSuccess)
+        return hip_fail(e, "hipSetDevice");
+    return poll_accel(true);
+}
+
 int Renderer::ensure_device_scene()
 {
     hipError_t e = hipSetDevice(device_);
@@ -547,6 +644,9 @@ int Renderer::ensure_device_scene()
     if ((geom_dirty_ || mats_dirty_ || tex_dirty_) && sync_slots() != RT_OK)
         return RT_EHIP;
     if (geom_dirty_) {
+        // a build of the previous geometry reads oct_: let it finish (its result is dropped)
+        poll_accel(true);
+        cones_ready_ = wide_ready_ = false;
         using clk = std::chrono::steady_clock;
         auto ms_since = [](clk::time_point t) { return std::chrono::duration<float, std::milli>(clk::now() - t).count(); };
         auto t0 = clk::now();
@@ -578,95 +678,50 @@ int Renderer::ensure_device_scene()
             }
         }
         build_split_ms_[0] = ms_since(t0);
-        // A helper thread computes the leaf cones and slabs and uploads the octree while this
-        // thread builds the wide BVH (both only read oct_); the wide BVH is uploaded after.
-        std::string up_err;
-        hipError_t up_e = hipSuccess;
-        float cones_ms = 0;
-        std::thread helper([&] {
-            auto t1 = clk::now();
-            if (s_.enable_bvh)
-                leaf_cones(oct_, cones_, lslab_, lsin_);
-            else {
-                cones_.clear();
-                lslab_.clear();
-                lsin_.clear();
-            }
-            cones_ms = ms_since(t1);
-            hipError_t e2 = hipSetDevice(device_);
-            size_t nb = oct_.nodes.size() * sizeof(GNode), tb = oct_.tris.size() * sizeof(GTri);
-            if (e2 == hipSuccess &&
-                ((e2 = d_nodes_.reserve(nb)) != hipSuccess || (e2 = d_tris_.reserve(tb)) != hipSuccess ||
-                 (e2 = d_tri_id_.reserve(oct_.tri_id.size() * 4)) != hipSuccess ||
-                 (e2 = d_tri_mat_.reserve(tri_mat_.size() * 4)) != hipSuccess ||
-                 (e2 = d_tri_uv_.reserve(tri_uv_.size() * 4)) != hipSuccess)) {
-                up_e = e2;
-                up_err = "hipMalloc (scene)";
-                return;
-            }
-            if (e2 == hipSuccess && nb) e2 = hipMemcpyAsync(d_nodes_.p, oct_.nodes.data(), nb, hipMemcpyHostToDevice, stream_);
-            if (e2 == hipSuccess && tb) e2 = hipMemcpyAsync(d_tris_.p, oct_.tris.data(), tb, hipMemcpyHostToDevice, stream_);
-            if (e2 == hipSuccess && !lslab_.empty()) {
-                if ((e2 = d_lslab_.reserve(lslab_.size() * 4)) == hipSuccess)
-                    e2 = hipMemcpyAsync(d_lslab_.p, lslab_.data(), lslab_.size() * 4, hipMemcpyHostToDevice, stream_);
-                if (e2 == hipSuccess && (e2 = d_lsin_.reserve(lsin_.size() * 4)) == hipSuccess)
-                    e2 = hipMemcpyAsync(d_lsin_.p, lsin_.data(), lsin_.size() * 4, hipMemcpyHostToDevice, stream_);
-            }
-            if (e2 == hipSuccess && !cones_.empty()) {
-                if ((e2 = d_cones_.reserve(cones_.size() * 4)) == hipSuccess)
-                    e2 = hipMemcpyAsync(d_cones_.p, cones_.data(), cones_.size() * 4, hipMemcpyHostToDevice, stream_);
-            }
-            if (e2 == hipSuccess && !oct_.tri_id.empty())
-                e2 = hipMemcpyAsync(d_tri_id_.p, oct_.tri_id.data(), oct_.tri_id.size() * 4, hipMemcpyHostToDevice, stream_);
-            if (e2 == hipSuccess && !tri_mat_.empty())
-                e2 = hipMemcpyAsync(d_tri_mat_.p, tri_mat_.data(), tri_mat_.size() * 4, hipMemcpyHostToDevice, stream_);
-            if (e2 == hipSuccess && !tri_uv_.empty())
-                e2 = hipMemcpyAsync(d_tri_uv_.p, tri_uv_.data(), tri_uv_.size() * 4, hipMemcpyHostToDevice, stream_);
-            if (e2 == hipSuccess)
-                e2 = hipStreamSynchronize(stream_);
-            if (e2 != hipSuccess) {
-                up_e = e2;
-                up_err = "upload (scene)";
-            }
-        });
-        // the wide BVH (wbvh.hpp): RT_WBVH=0 skips it
-        auto t2 = clk::now();
-        if (s_.enable_bvh && knobs_.wbvh && !knobs_.exact)
-            build_wbvh(oct_, wb_);
-        else
-            wb_ = WBvh();
-        build_split_ms_[2] = ms_since(t2);
-        auto t3 = clk::now();
-        helper.join();
-        build_split_ms_[1] = cones_ms;
-        if (up_e != hipSuccess)
-            return hip_fail(up_e, up_err.c_str());
-        if (!wb_.nodes.empty()) {
-            // the nodes, and the permutation from which the device gathers the wide BVH's triangle
-            // records and, per triangle, everything a certified hit needs in one 16-B load: the
-            // octree slot (the record's triangle), the leaf of its certificate, the caller's
-            // triangle index and its material (kernels.hip wide_gather_kernel)
-            const size_t nk = wb_.slot.size();
-            size_t wn = wb_.nodes.size() * sizeof(WNode);
-            if ((e = d_wnodes_.reserve(wn)) != hipSuccess || (e = d_wtris_.reserve(nk * sizeof(GTri))) != hipSuccess ||
-                (e = d_wmeta_.reserve(nk * 16)) != hipSuccess || (e = d_wtmp_.reserve(nk * 8)) != hipSuccess)
-                return hip_fail(e, "hipMalloc (wide BVH)");
-            int32_t* d_slot = d_wtmp_.as<int32_t>();
-            uint32_t* d_leaf = reinterpret_cast<uint32_t*>(d_slot + nk);
-            if ((e = hipMemcpyAsync(d_wnodes_.p, wb_.nodes.data(), wn, hipMemcpyHostToDevice, stream_)) != hipSuccess ||
-                (e = hipMemcpyAsync(d_slot, wb_.slot.data(), nk * 4, hipMemcpyHostToDevice, stream_)) != hipSuccess ||
-                (e = hipMemcpyAsync(d_leaf, wb_.leaf_of_slot.data(), nk * 4, hipMemcpyHostToDevice, stream_)) !=
-                    hipSuccess ||
-                (e = rt_launch_wide_gather(d_tris_.as<GTri>(), d_slot, d_leaf, d_tri_id_.as<int32_t>(),
-                                           d_tri_mat_.as<int32_t>(), (int)nk, d_wtris_.as<GTri>(), d_wmeta_.as<uint4>(),
-                                           stream_)) != hipSuccess ||
-                (e = hipStreamSynchronize(stream_)) != hipSuccess)
-                return hip_fail(e, "upload (wide BVH)");
-        }
+        // the octree and the triangle tables (everything the exact path reads), synchronously
+        auto t1 = clk::now();
+        size_t nb = oct_.nodes.size() * sizeof(GNode), tb = oct_.tris.size() * sizeof(GTri);
+        if ((e = d_nodes_.reserve(nb)) != hipSuccess || (e = d_tris_.reserve(tb)) != hipSuccess ||
+            (e = d_tri_id_.reserve(oct_.tri_id.size() * 4)) != hipSuccess ||
+            (e = d_tri_mat_.reserve(tri_mat_.size() * 4)) != hipSuccess ||
+            (e = d_tri_uv_.reserve(tri_uv_.size() * 4)) != hipSuccess)
+            return hip_fail(e, "hipMalloc (scene)");
+        hipSetDevice(device_);
+        if (nb) e = hipMemcpyAsync(d_nodes_.p, oct_.nodes.data(), nb, hipMemcpyHostToDevice, stream_);
+        if (e == hipSuccess && tb) e = hipMemcpyAsync(d_tris_.p, oct_.tris.data(), tb, hipMemcpyHostToDevice, stream_);
+        if (e == hipSuccess && !oct_.tri_id.empty())
+            e = hipMemcpyAsync(d_tri_id_.p, oct_.tri_id.data(), oct_.tri_id.size() * 4, hipMemcpyHostToDevice, stream_);
+        if (e == hipSuccess && !tri_mat_.empty())
+            e = hipMemcpyAsync(d_tri_mat_.p, tri_mat_.data(), tri_mat_.size() * 4, hipMemcpyHostToDevice, stream_);
+        if (e == hipSuccess && !tri_uv_.empty())
+            e = hipMemcpyAsync(d_tri_uv_.p, tri_uv_.data(), tri_uv_.size() * 4, hipMemcpyHostToDevice, stream_);
+        if (e == hipSuccess)
+            e = hipStreamSynchronize(stream_);
+        if (e != hipSuccess)
+            return hip_fail(e, "upload (scene)");
+        build_split_ms_[3] = ms_since(t1);
         geom_dirty_ = false;
         tri9_dirty_ = true;
-        build_split_ms_[3] = ms_since(t3);   // what the uploads added after the wide BVH build
         build_ms_ = ms_since(t0);
+        build_split_ms_[1] = build_split_ms_[2] = 0.0f;
+        // the leaf cones / slabs and the wide BVH: beside the next frames (RT_ASYNC_ACCEL=0: now)
+        if (s_.enable_bvh) {
+            start_accel();
+            if (!knobs_.async_accel) {
+                int rc = poll_accel(true);
+                if (rc != RT_OK)
+                    return rc;
+            }
+        } else {
+            cones_.clear();
+            lslab_.clear();
+            lsin_.clear();
+            wb_ = WBvh();
+        }
+    } else {
+        int rc = poll_accel(false);
+        if (rc != RT_OK)
+            return rc;
     }
     if (mats_dirty_) {
         if ((e = d_mats_.reserve(mats_.size() * 4)) != hipSuccess)
@@ -745,7 +800,7 @@ void Renderer::fill_params(KParams& P) const
     P.tri_id = d_tri_id_.as<int32_t>();
     P.tri_mat = d_tri_mat_.as<int32_t>();
     P.tri_uv = tri_uv_.empty() ? nullptr : d_tri_uv_.as<float>();
-    P.cones = (cones_.empty() || !knobs_.cones) ? nullptr : d_cones_.as<float>();
+    P.cones = (!cones_ready_ || !knobs_.cones) ? nullptr : d_cones_.as<float>();
     // (the leaf slabs read the cone axis)
     P.lslab = (!P.cones || lslab_.empty() || !knobs_.lslab) ? nullptr : d_lslab_.as<float>();
     P.lsin = P.lslab ? d_lsin_.as<float>() : nullptr;
@@ -756,7 +811,7 @@ void Renderer::fill_params(KParams& P) const
     // wide BVH: closest-hit queries certified against the octree, when it
     // was built, the scene's scale keeps the certificate's rounding margins (as for the
     // segment queries), and RT_WBVH is not 0
-    if (!wb_.nodes.empty() && knobs_.wbvh && !knobs_.exact && P.scene_scale > 0x1p-20f && P.scene_scale < 0x1p20f) {
+    if (wide_ready_ && knobs_.wbvh && !knobs_.exact && P.scene_scale > 0x1p-20f && P.scene_scale < 0x1p20f) {
         P.wnodes = d_wnodes_.as<WNode>();
         P.wtris = d_wtris_.as<GTri>();
         P.wmeta = d_wmeta_.as<uint4>();

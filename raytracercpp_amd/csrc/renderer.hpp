@@ -7,8 +7,10 @@
 
 #include <stdint.h>
 
+#include <atomic>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rt_mi355x.h"
@@ -48,6 +50,8 @@ struct Knobs {
     int refl_chunk_log2 = 25; // RT_REFL_CHUNK_LOG2 (10..25): sample slots per engine chunk
     bool debug_waves = false; // RT_DEBUG_WAVES: per-wave records of diagnostic builds (rt_debug_read)
     bool exact = false;       // RT_EXACT=1 / rt_set_exact: wbvh and seg off
+    bool async_accel = true;  // RT_ASYNC_ACCEL=0: the leaf cones / slabs and the wide BVH are built
+                              // before the first frame instead of beside it
     static Knobs from_env();
 };
 
@@ -61,6 +65,8 @@ public:
     const rt_settings& render_settings() const { return s_; }
     int set_settings(const rt_settings& s);
     int set_exact(bool on);
+    // waits for the background build of the leaf cones / slabs and the wide BVH
+    int finish_accel();
     bool exact() const { return knobs_.exact; }
     int change_render_size(int w, int h);
     int set_triangles(const float* tri9, const int32_t* mat, const float* uv6, int64_t n);
@@ -149,6 +155,17 @@ private:
     // scene versions (bumped with the dirty flags): what a multi-device helper has mirrored
     uint64_t geom_ver_ = 0, mats_ver_ = 0, tex_ver_ = 0;
     uint64_t mir_geom_ = ~0ull, mir_mats_ = ~0ull, mir_tex_ = ~0ull;   // a helper: the lead's versions copied
+    // The acceleration structures beside the octree: built on accel_thread_ after
+    // the octree is uploaded, adopted by the first frame that starts after they are resident;
+    // until then frames take the exact octree path (same results).
+    std::thread accel_thread_;
+    std::atomic<int> accel_state_{0};   // 0 idle, 1 building, 2 built, 3 failed
+    std::string accel_err_;
+    hipStream_t accel_stream_ = nullptr;
+    float accel_ms_[3] = {};            // cones + slabs, wide BVH, wide-BVH upload (background)
+    bool cones_ready_ = false, wide_ready_ = false;
+    void start_accel();
+    int poll_accel(bool wait);
     void mirror_from(const Renderer& lead);
     struct MultiDev;
     std::unique_ptr<MultiDev> multi_;

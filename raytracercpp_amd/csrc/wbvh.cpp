@@ -810,7 +810,7 @@ void build_wbvh(const FlatOctree& oct, WBvh& out)
     };
     out = WBvh();
     const int64_t n = (int64_t)oct.tris.size();
-    Pool pool(build_threads());
+    Pool& pool = build_pool();
     out.leaf_of_slot.assign((size_t)n, 0u);
     parallel_for(pool, (int64_t)oct.nodes.size(), 4096, [&](int64_t i) {
         const GNode& g = oct.nodes[(size_t)i];
@@ -892,6 +892,8 @@ void build_wbvh(const FlatOctree& oct, WBvh& out)
     out.stats.max_leaf = pl.st.max_leaf;
     out.stats.depth = pl.st.max_depth;
     out.stats.tris = n;
+    free_later(std::move(P), std::move(tmp), std::move(bn), std::move(un), std::move(pl.plans));
+    phase("exit");
 }
 
 int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)

@@ -89,6 +89,11 @@ class Renderer:
         a = np.ascontiguousarray(list(ids), np.int32)
         self._call("rt_set_devices", ptr(a, _i32p) if len(a) else None, len(a))
 
+    def finish_accel(self):
+        """rt_finish_accel: wait for the background build of the leaf cones / slabs and the wide
+        BVH (frames before it take the exact octree path)."""
+        self._call("rt_finish_accel")
+
     def set_exact(self, on: bool = True):
         """Exact mode: every query walks the octree over the whole line, as
         the reference does, instead of the certified wide BVH."""

@@ -23,6 +23,8 @@ for mode in modes:
         os.environ["RT_WBVH"] = "0"
     r = Renderer(0)
     r.load_scene(sc, st)
+    r.ray_trace()        # builds the octree; the wide BVH and leaf cones build beside it
+    r.finish_accel()     # counted frame on the adopted structures
     steps = (ctypes.c_ulonglong * 8)()
     if _diag:
         _diag(steps)   # clear
