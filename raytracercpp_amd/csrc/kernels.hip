@@ -1031,6 +1031,37 @@ __device__ __forceinline__ bool shapes_shadow(const KParams& P, v3 o, v3 d, floa
     return false;
 }
 
+// The exact octree traversal (BVH::intersect) as a function of its own: the wide BVH's
+// fallback and the path of every query when the wide BVH is off.  Not inlined, so that its large
+// state (the ray's k-DOP products, the traversal record, the heap) stays out of the register
+// allocation of the kernels' hot loop (which otherwise spills on every tile); the result comes
+// back in registers.  seg: the segment query [lo, hi] (bvh_closest_seg), else the whole line.
+struct OctQ {
+    THit h;
+    bool r;
+};
+
+// The launch's KParams where the kernel received it (every kernel that reaches octree_query takes
+// KParams as its first argument, at offset 0 of the kernel-argument segment): passing the
+// kernel's by-value copy to a call would copy all of it into scratch first.
+__device__ __forceinline__ const KParams& kernel_params()
+{
+    return *reinterpret_cast<const KParams*>((const void*)__builtin_amdgcn_kernarg_segment_ptr());
+}
+
+__device__ __noinline__ OctQ octree_query(const KParams& P, v3 o, v3 d, float lo, float hi, bool seg, uint2* lv)
+{
+    TRay R = make_ray(P, opaque(o), opaque(d));
+    OctQ q;
+    if (seg) {
+        R.lo = lo;
+        R.hi = hi;
+        q.r = bvh_closest_seg(P, R, q.h, lv);
+    } else
+        q.r = bvh_closest<false>(P, R, q.h, lv);
+    return q;
+}
+
 // renderer.cpp:340-402
 template <bool PLAIN = false>
 __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
@@ -1041,7 +1072,7 @@ __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
     v3 d = normalize(lp - p);
     THit h;
     bool r;
-    if (P.enable_bvh && P.seg_scale > 0.0f) {
+    if ((PLAIN || P.enable_bvh) && P.seg_scale > 0.0f) {
         // segment [-m, past the light]: a hit beyond hi fails the distance test below
         // (|p - q| >= t - |n| * 1e-4), one behind the origin does not exist (t >= 0)
         float m, hi;
@@ -1057,10 +1088,9 @@ __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
         bool sh;
         if (P.wnodes && P.nnodes > 0 && !nan && wide_shadow(P, o, d, hi, p, lp, lv, &sh))
             return sh;
-        TRay R = make_ray(P, opaque(o), opaque(d));
-        R.lo = -m;
-        R.hi = hi;
-        r = bvh_closest_seg(P, R, h, lv);
+        const OctQ q = octree_query(kernel_params(), o, d, -m, hi, true, lv);
+        h = q.h;
+        r = q.r;
         if (r) {
             v3 q = o + d * h.t;
             if (length2(p - q) < length2(p - lp))
@@ -1070,16 +1100,18 @@ __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
             return false;
         return shapes_shadow(P, o, d, h.t, p, lp);
     }
-    TRay R = make_ray(P, o, d);
-    if (P.enable_bvh) {
+    if (PLAIN || P.enable_bvh) {
         // whole-line query (segment queries off)
-        r = bvh_closest<false>(P, R, h, lv);
+        const OctQ oq = octree_query(kernel_params(), o, d, 0.0f, 0.0f, false, lv);
+        h = oq.h;
+        r = oq.r;
         if (r) {
             v3 q = o + d * h.t;
             if (length2(p - q) < length2(p - lp))
                 return true;
         }
     } else {
+        TRay R = make_ray(P, o, d);
         h.t = -1.0f;
         for (int k = 0; k < P.ntri_slots; k++) {
             float t, u, v;
@@ -1135,7 +1167,7 @@ __device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv)
 {
     Rec local = rec_fresh();
     int src = -1;
-    if (P.enable_bvh) {
+    if (PLAIN || P.enable_bvh) {
         THit h;
         bool r = false;
         const bool wide = P.wnodes && P.nnodes > 0 && !ray_is_nan(o, d);
@@ -1146,9 +1178,8 @@ __device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv)
                 src = local.tri;
             }
         } else {
-            TRay R = make_ray(P, opaque(o), opaque(d));
-            r = bvh_closest<false>(P, R, h, lv);
-            bvh_record(P, h, r, local, fin, src);
+            const OctQ q = octree_query(kernel_params(), o, d, 0.0f, 0.0f, false, lv);
+            bvh_record(P, q.h, q.r, local, fin, src);
         }
     } else {
         TRay R = make_ray(P, o, d);
