@@ -1031,25 +1031,19 @@ __device__ __forceinline__ bool shapes_shadow(const KParams& P, v3 o, v3 d, floa
     return false;
 }
 
-// The exact octree traversal (BVH::intersect) as a function of its own: the wide BVH's
-// fallback and the path of every query when the wide BVH is off.  Not inlined, so that its large
-// state (the ray's k-DOP products, the traversal record, the heap) stays out of the register
-// allocation of the kernels' hot loop (which otherwise spills on every tile); the result comes
-// back in registers.  seg: the segment query [lo, hi] (bvh_closest_seg), else the whole line.
+// The exact octree traversal (BVH::intersect): the wide BVH's rare fallback, and the path of
+// every query when the wide BVH is off (exact mode, frames before it is adopted).  The plain
+// kernel calls it as a function of its own, so that its large state (the ray's k-DOP products,
+// the traversal record, the heap) stays out of the register allocation of the hot loop (inlined
+// there it made the loop spill on every tile); the result comes back in registers.  Every other
+// kernel inlines it (their queries may all take it).  seg: the segment query [lo, hi]
+// (bvh_closest_seg), else the whole line.
 struct OctQ {
     THit h;
     bool r;
 };
 
-// The launch's KParams where the kernel received it (every kernel that reaches octree_query takes
-// KParams as its first argument, at offset 0 of the kernel-argument segment): passing the
-// kernel's by-value copy to a call would copy all of it into scratch first.
-__device__ __forceinline__ const KParams& kernel_params()
-{
-    return *reinterpret_cast<const KParams*>((const void*)__builtin_amdgcn_kernarg_segment_ptr());
-}
-
-__device__ __noinline__ OctQ octree_query(const KParams& P, v3 o, v3 d, float lo, float hi, bool seg, uint2* lv)
+__device__ __forceinline__ OctQ octree_query_inl(const KParams& P, v3 o, v3 d, float lo, float hi, bool seg, uint2* lv)
 {
     TRay R = make_ray(P, opaque(o), opaque(d));
     OctQ q;
@@ -1060,6 +1054,27 @@ __device__ __noinline__ OctQ octree_query(const KParams& P, v3 o, v3 d, float lo
     } else
         q.r = bvh_closest<false>(P, R, q.h, lv);
     return q;
+}
+
+__device__ __noinline__ OctQ octree_query_call(const KParams& P, v3 o, v3 d, float lo, float hi, bool seg, uint2* lv)
+{
+    return octree_query_inl(P, o, d, lo, hi, seg, lv);
+}
+
+// The launch's KParams where the kernel received it (the plain kernel takes KParams as its first
+// argument, at offset 0 of the kernel-argument segment): passing the kernel's by-value copy to a
+// call would copy all of it into scratch first.
+__device__ __forceinline__ const KParams& kernel_params()
+{
+    return *reinterpret_cast<const KParams*>((const void*)__builtin_amdgcn_kernarg_segment_ptr());
+}
+
+template <bool CALL>
+__device__ __forceinline__ OctQ octree_query(const KParams& P, v3 o, v3 d, float lo, float hi, bool seg, uint2* lv)
+{
+    if (CALL)
+        return octree_query_call(kernel_params(), o, d, lo, hi, seg, lv);
+    return octree_query_inl(P, o, d, lo, hi, seg, lv);
 }
 
 // renderer.cpp:340-402
@@ -1088,7 +1103,7 @@ __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
         bool sh;
         if (P.wnodes && P.nnodes > 0 && !nan && wide_shadow(P, o, d, hi, p, lp, lv, &sh))
             return sh;
-        const OctQ q = octree_query(kernel_params(), o, d, -m, hi, true, lv);
+        const OctQ q = octree_query<PLAIN>(P, o, d, -m, hi, true, lv);
         h = q.h;
         r = q.r;
         if (r) {
@@ -1102,7 +1117,7 @@ __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
     }
     if (PLAIN || P.enable_bvh) {
         // whole-line query (segment queries off)
-        const OctQ oq = octree_query(kernel_params(), o, d, 0.0f, 0.0f, false, lv);
+        const OctQ oq = octree_query<PLAIN>(P, o, d, 0.0f, 0.0f, false, lv);
         h = oq.h;
         r = oq.r;
         if (r) {
@@ -1137,8 +1152,9 @@ __device__ __forceinline__ void bvh_record(const KParams& P, const THit& h, bool
 {
     if (h.k >= 0)
         local = tri_record(P, h);
-    else if (h.t != h.t)
-        local.t = h.t;   // NaN ray: stale NaN record
+    else
+        local.t = h.t != h.t ? h.t : local.t;   // NaN ray: stale NaN record (a select: a conditional
+                                                // partial store kept the record in scratch)
     if (r && (local.t < fin.t || fin.t == -1)) {
         fin = local;
         src = local.tri;
@@ -1178,7 +1194,7 @@ __device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv)
                 src = local.tri;
             }
         } else {
-            const OctQ q = octree_query(kernel_params(), o, d, 0.0f, 0.0f, false, lv);
+            const OctQ q = octree_query<PLAIN>(P, o, d, 0.0f, 0.0f, false, lv);
             bvh_record(P, q.h, q.r, local, fin, src);
         }
     } else {
@@ -1738,8 +1754,14 @@ __device__ __forceinline__ void downscale_tile(const KParams& P, int lane, int l
 // PLAIN: no texture map, sky, analytic shape, debug shading or SSAO buffer (host-checked,
 // KParams::plain): those code paths are compiled out.
 template <bool REFL, bool PLAIN = false>
-__global__ __launch_bounds__(BLOCK, PLAIN ? RT_OCC_PLAIN : RT_OCC) void ray_trace_kernel(KParams P)
+__global__ __launch_bounds__(BLOCK, PLAIN ? RT_OCC_PLAIN : RT_OCC) void ray_trace_kernel(KParams P_arg)
 {
+    // The plain kernel reads its parameters where the kernel received them, through a pointer
+    // the compiler cannot hoist out of the tile loop: each field is loaded (scalar cache) where
+    // a tile uses it instead of ~100 of them being held in registers across the loop, which
+    // spilled (register budget).
+    auto kp = __builtin_amdgcn_kernarg_segment_ptr();
+    const KParams& P = PLAIN ? *reinterpret_cast<const KParams*>((const void*)kp) : P_arg;
     extern __shared__ uint2 lds_levels[];
     uint2* lv = lds_levels + threadIdx.x;
     int lane = threadIdx.x & 63;
@@ -1754,6 +1776,9 @@ __global__ __launch_bounds__(BLOCK, PLAIN ? RT_OCC_PLAIN : RT_OCC) void ray_trac
     }
 #endif
     for (;;) {
+        if (PLAIN)
+            asm volatile("" : "+s"(kp));   // (the loop's loads depend on it: not hoisted)
+        const KParams& P = PLAIN ? *reinterpret_cast<const KParams*>((const void*)kp) : P_arg;
         const int tile = tile_queue_next(P);
         if (PLAIN) PH_MARK(6);
         if (tile < 0)

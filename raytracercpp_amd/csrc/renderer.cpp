@@ -876,7 +876,7 @@ void Renderer::fill_params(KParams& P) const
     }
     P.max_blocks = num_cus_ * 8;   // persistent grids: 8 blocks per CU (the plain kernel: its residency)
     // the plain specialisation (RT_PLAIN=0 turns it off); SSAO (zbuf) is checked at launch
-    P.plain = knobs_.plain && P.enable_bvh && P.shading_method == RT_SHADING && P.nshape == 0 &&
+    P.plain = knobs_.plain && P.enable_bvh && P.wnodes && P.shading_method == RT_SHADING && P.nshape == 0 &&
               !P.enable_ao_mapping && !P.enable_diffuse_mapping && !P.enable_normal_mapping &&
               !P.enable_displacement_mapping && !P.enable_skysphere && !P.enable_skybox && !P.has_reflection;
     render_size(P.rw, P.rh);
