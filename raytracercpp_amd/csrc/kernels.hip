@@ -1756,16 +1756,16 @@ __device__ __forceinline__ void downscale_tile(const KParams& P, int lane, int l
 template <bool REFL, bool PLAIN = false>
 __global__ __launch_bounds__(BLOCK, PLAIN ? RT_OCC_PLAIN : RT_OCC) void ray_trace_kernel(KParams P_arg)
 {
-    // The plain kernel reads its parameters where the kernel received them, through a pointer
+    // The kernel reads its parameters where the kernel received them, through a pointer
     // the compiler cannot hoist out of the tile loop: each field is loaded (scalar cache) where
     // a tile uses it instead of ~100 of them being held in registers across the loop, which
     // spilled (register budget).
     auto kp = __builtin_amdgcn_kernarg_segment_ptr();
-    const KParams& P = PLAIN ? *reinterpret_cast<const KParams*>((const void*)kp) : P_arg;
+    (void)P_arg;
+    const KParams& P = *reinterpret_cast<const KParams*>((const void*)kp);
     extern __shared__ uint2 lds_levels[];
     uint2* lv = lds_levels + threadIdx.x;
     int lane = threadIdx.x & 63;
-    v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
     unsigned nshadow = 0, nrefl = 0;
     tile_queue_init();
 #if RT_PHASE_TIME
@@ -1776,9 +1776,10 @@ __global__ __launch_bounds__(BLOCK, PLAIN ? RT_OCC_PLAIN : RT_OCC) void ray_trac
     }
 #endif
     for (;;) {
-        if (PLAIN)
-            asm volatile("" : "+s"(kp));   // (the loop's loads depend on it: not hoisted)
-        const KParams& P = PLAIN ? *reinterpret_cast<const KParams*>((const void*)kp) : P_arg;
+        auto kpl = kp;
+        asm volatile("" : "+s"(kpl));   // (the loop's loads depend on it: not hoisted)
+        const KParams& P = *reinterpret_cast<const KParams*>((const void*)kpl);
+        const v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
         const int tile = tile_queue_next(P);
         if (PLAIN) PH_MARK(6);
         if (tile < 0)
