@@ -15,13 +15,18 @@ if stats:
                                      "total_ns": float(r["TotalDurationNs"]), "pct": float(r["Percentage"])}
 for f in sorted(glob.glob(f"{src}/pmc_*/**/run_counter_collection.csv", recursive=True)):
     # per dispatch: the sum over the rows of one dispatch (instances / dimensions), then
-    # the mean over the ray_trace_kernel dispatches
-    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    # the mean over the dispatches of the ray_trace_kernel instance launched most often (the
+    # steady-state frame; the first frame of a scene may take the exact octree instance while
+    # the wide BVH is built in the background)
+    agg = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(float)))
     for r in csv.DictReader(open(f)):
         if "ray_trace_kernel" in r["Kernel_Name"]:
-            agg[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
-    for k, v in agg.items():
-        out["pmc_ray_trace_kernel"][k] = sum(v.values()) / len(v)
+            agg[r["Kernel_Name"]][r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
+    if agg:
+        main = max(agg, key=lambda n: max(len(v) for v in agg[n].values()))
+        out["pmc_kernel_name"] = main
+        for k, v in agg[main].items():
+            out["pmc_ray_trace_kernel"][k] = sum(v.values()) / len(v)
     name = f.split(os.sep)[-3] if "pmc_" in f.split(os.sep)[-3] else os.path.basename(os.path.dirname(f))
     shutil.copy(f, os.path.join(dst, f"{name}_counters.csv"))
 p = out["pmc_ray_trace_kernel"]
@@ -47,5 +52,14 @@ if "TA_BUSY_avr" in p and "GRBM_GUI_ACTIVE" in p:
     out["ta_busy_fraction"] = p["TA_BUSY_avr"] / (p["GRBM_GUI_ACTIVE"] / 8.0)
 if "SQ_WAIT_ANY" in p and "SQ_WAVE_CYCLES" in p:
     out["wave_wait_fraction"] = p["SQ_WAIT_ANY"] / p["SQ_WAVE_CYCLES"]
+traces = glob.glob(f"{src}/trace/**/run_kernel_trace.csv", recursive=True)
+if traces:
+    # per-instance resources as dispatched (scratch bytes per lane, VGPRs)
+    res = {}
+    for r in csv.DictReader(open(traces[0])):
+        if "ray_trace_kernel" in r["Kernel_Name"] and r["Kernel_Name"] not in res:
+            res[r["Kernel_Name"]] = {"scratch_bytes_per_lane": int(r["Scratch_Size"]), "vgprs": int(r["VGPR_Count"]),
+                                     "sgprs": int(r["SGPR_Count"]), "grid": int(r["Grid_Size_X"])}
+    out["ray_trace_resources"] = res
 json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1, sort_keys=True)
 print(json.dumps({k: v for k, v in out.items() if k != "kernels"}, indent=1))
