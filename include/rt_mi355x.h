@@ -19,7 +19,9 @@
  *     cross this boundary.  The reference has no error reporting (asserts / UB):
  *     invalid material indices, absent textures and renders without geometry
  *     are rejected here up front with RT_EINVAL.
- *   - a handle belongs to one thread at a time (as Renderer does).
+ *   - a handle belongs to one thread at a time (as Renderer does), except that rt_get_image,
+ *     rt_lock_image and rt_unlock_image may be called from a second (display) thread while the
+ *     owning thread renders (DisplayThread / RenderThread, QT/mainWindowThreads.cpp:6-65).
  */
 #ifndef RT_MI355X_H
 #define RT_MI355X_H
@@ -236,8 +238,21 @@ int rt_get_ssao_buffers(rt_renderer *r, float *z, float *n4, int32_t *ao);
 int rt_post_process(rt_renderer *r);
 
 /* Renderer::get_image (renderer.cpp:106-109): copies the current image
- * (image_width x image_height after post_process) to argb; w/h receive its size. */
+ * (image_width x image_height after post_process) to argb; w/h receive its size.
+ * Progressive readback: from the start of a ray_trace / raster_trace the image is the frame's
+ * internal (render_w x render_h) buffer, which the GPU fills tile by tile, as the reference's
+ * ray_trace fills _image pixel by pixel.  Called from a display thread while the owning thread
+ * renders, rt_get_image returns the image as it stands (finished tiles of the frame in progress,
+ * elsewhere the previous frame or, for a re-created image -- size change, SSAA frame -- the
+ * BACKGROUND_COLOR fill); it does not wait for the frame.  Frames rendered with rt_set_devices
+ * appear whole, after their gather. */
 int rt_get_image(rt_renderer *r, uint32_t *argb, int32_t *w, int32_t *h);
+
+/* Renderer::lock_image_mutex / unlock_image_mutex (renderer.h:41-42, renderer.cpp:96-104): while a
+ * thread holds the image lock, no frame of the handle switches or re-creates the image (the start
+ * of a frame and post_process's SSAA swap wait for it); rt_get_image takes it too (recursive). */
+int rt_lock_image(rt_renderer *r);
+int rt_unlock_image(rt_renderer *r);
 
 /* render(Renderer&) (utils/mainUtils.cpp:6-21): raster_trace (hybrid_rasterization_tracing)
  * or ray_trace, then post_process;
@@ -284,6 +299,18 @@ int rt_render_bands_device(rt_renderer *r, int32_t band_rows, int32_t rank, int3
  * Uses the brute-force loop when enable_bvh is 0. */
 int rt_trace_rays(rt_renderer *r, const float *orig, const float *dir, int64_t n, int32_t *tri_id, float *t,
                   float *u, float *v, uint8_t *ret);
+
+/* Renderer::trace_ray(ray, hit_info, current_recursion_depth, intersection_found)
+ * (renderer.h:144, renderer.cpp:1008-1066) for n arbitrary rays (origins / directions [n][3]),
+ * each with a fresh HitInfo: rgba [n][4] = the Color trace_ray returns (shading, shadow ray,
+ * compute_reflection recursion down to max_recursion_depth, sky / background on a miss);
+ * hit_src = the record's source when intersection_found (triangle index, -2 - k for analytic
+ * shape k), else -1; t = the record's t; intersection_found; shadowed = the hit's shadow ray was
+ * blocked.  Ray i's rough-reflection samples draw from the stream of pixel i of a frame (the
+ * counter-based RNG of rt_settings::rng_seed).  rt_get_stats reports the call's shadow and
+ * reflection ray counts. */
+int rt_trace_ray(rt_renderer *r, const float *orig, const float *dir, int64_t n, int32_t current_recursion_depth,
+                 float *rgba, int32_t *hit_src, float *t, uint8_t *intersection_found, uint8_t *shadowed);
 
 /* GPU durations (ms) of the ray-trace kernel of the last n rt_render_bands_device
  * calls, from HIP events recorded around each launch on its stream (waits for them). */

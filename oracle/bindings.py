@@ -190,6 +190,8 @@ class Oracle:
             L.orc_downscale_argb.argtypes = [_u32p, C.c_int, C.c_int, C.c_int, _u32p]
             L.orc_bvh_query.argtypes = [C.c_void_p, _f32p, _f32p, C.c_int64, _i32p, _f32p, _f32p, _f32p, _u8p, _i64p]
             L.orc_bvh_stats.argtypes = [C.c_void_p, _i64p]
+            L.orc_trace_rays_shaded.argtypes = [C.c_void_p, _f32p, _f32p, C.c_int64, C.c_int, _f32p, _i32p, _f32p,
+                                                _u8p, _u8p, C.POINTER(OrcCounters)]
             L.orc_bvh_node.argtypes = [C.c_void_p, C.c_int, _f32p, _f32p, _i32p, _i32p, _i32p]
             L.orc_heap_order.argtypes = [_f32p, C.c_int, _i32p]
             L.orc_ssao.argtypes = [C.c_void_p, _f32p, _f32p, _u32p, _i32p, C.c_int]
@@ -284,6 +286,22 @@ class Oracle:
         self.lib().orc_bvh_query(self._h, _ptr(orig, _f32p), _ptr(dirs, _f32p), n, _ptr(ids, _i32p), _ptr(t, _f32p),
                                  _ptr(u, _f32p), _ptr(v, _f32p), _ptr(ret, _u8p), _ptr(counts, _i64p))
         return ids, t, u, v, ret, counts
+
+    def trace_ray(self, orig, dirs, depth=0):
+        """Renderer::trace_ray (shaded), fresh HitInfo per ray -> (rgba, src, t, found, shadowed, counters)."""
+        orig = np.ascontiguousarray(orig, np.float32).reshape(-1, 3)
+        dirs = np.ascontiguousarray(dirs, np.float32).reshape(-1, 3)
+        n = orig.shape[0]
+        rgba = np.zeros((n, 4), np.float32)
+        src = np.zeros(n, np.int32)
+        t = np.zeros(n, np.float32)
+        found = np.zeros(n, np.uint8)
+        shadowed = np.zeros(n, np.uint8)
+        cnt = OrcCounters()
+        self.lib().orc_trace_rays_shaded(self._h, _ptr(orig, _f32p), _ptr(dirs, _f32p), n, int(depth),
+                                         _ptr(rgba, _f32p), _ptr(src, _i32p), _ptr(t, _f32p), _ptr(found, _u8p),
+                                         _ptr(shadowed, _u8p), C.byref(cnt))
+        return rgba, src, t, found, shadowed, cnt.as_dict()
 
     def bvh_stats(self):
         st = np.zeros(6, np.int64)

@@ -1859,6 +1859,52 @@ ORC_API void orc_bvh_query(const struct orc_ctx *X, const float *orig, const flo
     }
 }
 
+/* Renderer::trace_ray(ray, hit_info, current_recursion_depth, intersection_found)
+ * (renderer.cpp:1008-1066) for n arbitrary rays, each with a fresh HitInfo: colour
+ * (rgba), the record's source (triangle index, -2-k for analytic shape k, -1 when
+ * intersection_found stays false), its t, intersection_found and the depth-0 shadow
+ * flag.  Ray i's rough-reflection stream is keyed pixel_seed(i, rng_seed), as pixel i
+ * of a frame. */
+ORC_API void orc_trace_rays_shaded(const struct orc_ctx *X, const float *orig, const float *dir, int64_t n, int depth,
+                                   float *rgba, int32_t *out_src, float *out_t, uint8_t *out_found,
+                                   uint8_t *out_shadow, orc_counters *counters)
+{
+    orc_counters total;
+    memset(&total, 0, sizeof(total));
+#pragma omp parallel
+    {
+        orc_counters local;
+        memset(&local, 0, sizeof(local));
+        otracer T;
+        T.X = X;
+        T.cnt = &local;
+        T.ray_kind = 0;
+        T.rng = 1;
+        T.frame_key = 0;
+#pragma omp for schedule(dynamic, 16)
+        for (int64_t i = 0; i < n; i++) {
+            int found = 0, src = -1, shadowed = 0;
+            ohit hi = hit_fresh();
+            T.frame_key = pixel_seed((uint32_t)i, X->s.rng_seed);
+            T.alpha = 1.0f;
+            c3 c = trace_ray(&T, V(orig[3 * i], orig[3 * i + 1], orig[3 * i + 2]),
+                             V(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]), &hi, depth, &found, &src, &shadowed);
+            rgba[4 * i] = c.r;
+            rgba[4 * i + 1] = c.g;
+            rgba[4 * i + 2] = c.b;
+            rgba[4 * i + 3] = T.alpha;
+            out_src[i] = found ? src : -1;
+            out_t[i] = hi.t;
+            out_found[i] = (uint8_t)found;
+            out_shadow[i] = (uint8_t)(found && shadowed);
+        }
+#pragma omp critical
+        add_counters(&total, &local);
+    }
+    if (counters)
+        *counters = total;
+}
+
 /* Octree statistics: [inner, leaves, empty_leaves, max_leaf_size, max_depth, node_count] */
 static void stats_rec(const obvh *B, int ni, int depth, int64_t *st)
 {

@@ -110,12 +110,15 @@ SIGNATURES = {
     "rt_post_process": (C.c_int, [_H]),
     "rt_get_image": (C.c_int, [_H, _u32p, _i32p, _i32p]),
     "rt_render": (C.c_int, [_H, _f32p]),
+    "rt_lock_image": (C.c_int, [_H]),
+    "rt_unlock_image": (C.c_int, [_H]),
     "rt_request_aux": (C.c_int, [_H, C.c_int32, C.c_int32, C.c_int32]),
     "rt_get_internal": (C.c_int, [_H, _u32p, _f32p, _i32p, _f32p, _u8p]),
     "rt_get_stats": (C.c_int, [_H, C.POINTER(RtStats)]),
     "rt_local_rows": (C.c_int, [_H, C.c_int32, C.c_int32, C.c_int32, _i32p]),
     "rt_render_bands_device": (C.c_int, [_H, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]),
     "rt_trace_rays": (C.c_int, [_H, _f32p, _f32p, C.c_int64, _i32p, _f32p, _f32p, _f32p, _u8p]),
+    "rt_trace_ray": (C.c_int, [_H, _f32p, _f32p, C.c_int64, C.c_int32, _f32p, _i32p, _f32p, _u8p, _u8p]),
     "rt_kernel_times": (C.c_int, [_H, _f32p, C.c_int32]),
     "rt_band_counters": (C.c_int, [_H, _i64p, _i64p]),
     "rt_make_transform": (None, [C.c_int32, C.c_float, C.c_float, C.c_float, _f32p]),

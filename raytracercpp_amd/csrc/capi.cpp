@@ -233,9 +233,35 @@ int rt_post_process(rt_renderer* r)
 {
     return guarded(R(r), [&] { return R(r)->post_process(); });
 }
+// rt_get_image / rt_lock_image / rt_unlock_image may run on a display thread while the owning
+// thread renders: they touch only the image state (under the image mutex), never err_
 int rt_get_image(rt_renderer* r, uint32_t* argb, int32_t* w, int32_t* h)
 {
-    return guarded(R(r), [&] { return R(r)->get_image(argb, w, h); });
+    if (!r)
+        return bad("null renderer handle");
+    try {
+        int rc = R(r)->get_image(argb, w, h);
+        if (rc != RT_OK)
+            g_err = R(r)->display_error();
+        return rc;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return RT_EINVAL;
+    }
+}
+int rt_lock_image(rt_renderer* r)
+{
+    if (!r)
+        return bad("null renderer handle");
+    R(r)->lock_image();
+    return RT_OK;
+}
+int rt_unlock_image(rt_renderer* r)
+{
+    if (!r)
+        return bad("null renderer handle");
+    R(r)->unlock_image();
+    return RT_OK;
 }
 int rt_render(rt_renderer* r, float* ms)
 {
@@ -285,6 +311,14 @@ int rt_trace_rays(rt_renderer* r, const float* orig, const float* dir, int64_t n
                   float* u, float* v, uint8_t* ret)
 {
     return guarded(R(r), [&] { return R(r)->trace_rays(orig, dir, n, tri_id, t, u, v, ret); });
+}
+int rt_trace_ray(rt_renderer* r, const float* orig, const float* dir, int64_t n, int32_t current_recursion_depth,
+                 float* rgba, int32_t* hit_src, float* t, uint8_t* intersection_found, uint8_t* shadowed)
+{
+    return guarded(R(r), [&] {
+        return R(r)->trace_ray_colors(orig, dir, n, current_recursion_depth, rgba, hit_src, t, intersection_found,
+                                      shadowed);
+    });
 }
 int rt_kernel_times(rt_renderer* r, float* ms, int32_t n)
 {

@@ -2914,6 +2914,39 @@ __global__ __launch_bounds__(BLOCK) void trace_rays_kernel(KParams P, const floa
     out_ret[i] = r ? 1 : 0;
 }
 
+// Renderer::trace_ray (renderer.cpp:1008-1066) for a batch of arbitrary rays, one lane per
+// ray, each with a fresh HitInfo: the colour trace_ray returns (shading, shadow ray, the
+// compute_reflection recursion when REFL), and the record it leaves.  The host folds
+// current_recursion_depth into P.max_recursion_depth (only their difference is read).  Ray
+// i's rough-reflection stream is keyed as pixel i of a frame.
+template <bool REFL>
+__global__ __launch_bounds__(BLOCK, RT_OCC) void trace_colors_kernel(KParams P, const float* __restrict__ orig,
+                                                                     const float* __restrict__ dir, int n,
+                                                                     float4* __restrict__ out_rgba,
+                                                                     int32_t* __restrict__ out_src,
+                                                                     float* __restrict__ out_t,
+                                                                     uint8_t* __restrict__ out_found,
+                                                                     uint8_t* __restrict__ out_shadow)
+{
+    extern __shared__ uint2 lds_levels[];
+    uint2* lv = lds_levels + threadIdx.x;
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    unsigned nshadow = 0, nrefl = 0;
+    if (i < n) {
+        const v3 o = mk(orig[3 * i], orig[3 * i + 1], orig[3 * i + 2]);
+        const v3 d = mk(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]);
+        const uint32_t key = REFL ? pixel_seed((uint32_t)i, P.rng_seed) : 0u;
+        PixelOut po = trace_pixel<REFL>(P, o, d, lv, key, nshadow, nrefl);
+        out_rgba[i] = make_float4(po.color.r, po.color.g, po.color.b, po.alpha);
+        out_src[i] = po.found ? po.src : -1;
+        out_t[i] = po.fin.t;
+        out_found[i] = po.found ? 1 : 0;
+        out_shadow[i] = (uint8_t)(po.found && po.shadowed);
+    }
+    if (nshadow) atomicAdd(&P.counters[0], (unsigned long long)nshadow);
+    if (nrefl) atomicAdd(&P.counters[1], (unsigned long long)nrefl);
+}
+
 // The wide BVH's triangle records and their metadata, gathered on the device from the octree's
 // (already uploaded) instead of uploading 64 B per triangle again: wide-BVH triangle k is octree
 // slot s = slot[k]; wmeta[k] = {s, its octree leaf, its caller index, that triangle's material}.
@@ -2956,6 +2989,25 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_trace_rays
     size_t lds = rt::lds_bytes(*P);
     hipLaunchKernelGGL(rt::trace_rays_kernel, dim3((n + rt::BLOCK - 1) / rt::BLOCK), dim3(rt::BLOCK), lds, stream, *P,
                        o, d, n, id, t, u, v, ret);
+    return hipGetLastError();
+}
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_trace_colors(const rt::KParams* P, bool refl,
+                                                                                   const float* o, const float* d,
+                                                                                   int n, float4* rgba, int32_t* src,
+                                                                                   float* t, uint8_t* found,
+                                                                                   uint8_t* shadow, hipStream_t stream)
+{
+    if (n <= 0)
+        return hipSuccess;
+    size_t lds = rt::lds_bytes(*P);
+    dim3 grid((n + rt::BLOCK - 1) / rt::BLOCK), block(rt::BLOCK);
+    if (refl)
+        hipLaunchKernelGGL(rt::trace_colors_kernel<true>, grid, block, lds, stream, *P, o, d, n, rgba, src, t, found,
+                           shadow);
+    else
+        hipLaunchKernelGGL(rt::trace_colors_kernel<false>, grid, block, lds, stream, *P, o, d, n, rgba, src, t, found,
+                           shadow);
     return hipGetLastError();
 }
 

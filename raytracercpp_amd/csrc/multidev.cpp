@@ -219,7 +219,10 @@ int Renderer::render_multi()
             return fail(RT_EHIP, std::string("RCCL band gather: ") + api->error_string(r != 0 ? r : r2));
     }
     // band b is local band b / n of rank b % n
-    if ((e = d_image_.reserve((size_t)W * H * 4)) != hipSuccess) return hip_fail(e, "hipMalloc (image)");
+    {
+        std::lock_guard<std::recursive_mutex> g(image_mu_);
+        if ((e = d_image_.reserve((size_t)W * H * 4)) != hipSuccess) return hip_fail(e, "hipMalloc (image)");
+    }
     const int nb = (H + band - 1) / band;
     for (int b = 0; b < nb && e == hipSuccess; b++) {
         const int rows = std::min(band, H - b * band);
@@ -236,6 +239,7 @@ int Renderer::render_multi()
     hipSetDevice(device_);
     if (e != hipSuccess)
         return hip_fail(e, "render_multi");
+    std::lock_guard<std::recursive_mutex> g(image_mu_);
     img_w_ = W;
     img_h_ = H;
     img_is_internal_ = false;

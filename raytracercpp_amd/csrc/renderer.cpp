@@ -24,6 +24,11 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_keys(
                                                                          hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_trace_rays(const rt::KParams* P, const float* o, const float* d, int n, int32_t* id,
                                            float* t, float* u, float* v, uint8_t* ret, hipStream_t stream);
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_trace_colors(const rt::KParams* P, bool refl,
+                                                                                   const float* o, const float* d,
+                                                                                   int n, float4* rgba, int32_t* src,
+                                                                                   float* t, uint8_t* found,
+                                                                                   uint8_t* shadow, hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_raster_stage(int stage, const rt::KParams* P,
                                                                             const rt::RasterArgs* A, int npieces,
                                                                             hipStream_t stream);
@@ -149,6 +154,8 @@ Renderer::~Renderer()
     for (auto& b : band_slot_)
         if (b.done) hipEventDestroy(b.done);
     if (stream_) hipStreamDestroy(stream_);
+    if (display_stream_) hipStreamDestroy(display_stream_);
+    if (display_host_) hipHostFree(display_host_);
 }
 
 int Renderer::fail(int code, const std::string& msg)
@@ -200,9 +207,12 @@ int Renderer::change_render_size(int w, int h)
     s_.image_height = h;
     int rw, rh;
     render_size(rw, rh);
-    img_w_ = rw;
-    img_h_ = rh;
-    rendered_ = false;
+    {
+        std::lock_guard<std::recursive_mutex> g(image_mu_);
+        img_w_ = rw;
+        img_h_ = rh;
+        rendered_ = false;
+    }
     aspect_ = (float)rw / rh;
     update_camera_projection();
     return RT_OK;
@@ -1150,8 +1160,10 @@ int Renderer::trace_frame()
     last_seg_ = P.seg_scale;
     size_t npx = (size_t)P.rw * P.rh;
     hipError_t e;
-    if ((e = d_internal_.reserve(npx * 4)) != hipSuccess || (e = d_counters_.reserve(NCOUNTER_WORDS * 8)) != hipSuccess)
-        return hip_fail(e, "hipMalloc (image)");
+    if ((e = d_counters_.reserve(NCOUNTER_WORDS * 8)) != hipSuccess)
+        return hip_fail(e, "hipMalloc (counters)");
+    if ((rc = begin_internal_image(P.rw, P.rh)) != RT_OK)
+        return rc;
     if (want_rgba_ && (e = d_rgba_.reserve(npx * 16)) != hipSuccess) return hip_fail(e, "hipMalloc (rgba)");
     if (want_hit_ && ((e = d_hit_id_.reserve(npx * 4)) != hipSuccess || (e = d_hit_t_.reserve(npx * 4)) != hipSuccess))
         return hip_fail(e, "hipMalloc (hit)");
@@ -1191,10 +1203,6 @@ int Renderer::trace_frame()
     hipEventElapsedTime(&kernel_ms_, ev_[0], ev_[1]);
     last_primary_ = (int64_t)npx;
     take_counters(cnt);
-    img_w_ = P.rw;
-    img_h_ = P.rh;
-    img_is_internal_ = true;
-    rendered_ = true;
     aux_valid_ = true;
     ssao_ready_ = s_.enable_ssao;
     post_ms_ = 0;
@@ -1224,7 +1232,10 @@ int Renderer::post_process()
     if (img_w_ % f != 0 || img_h_ % f != 0)
         return RT_OK;   // downscale_image_qt_ARGB32 prints and leaves the output untouched
     int dw = img_w_ / f, dh = img_h_ / f;
-    if ((e = d_image_.reserve((size_t)dw * dh * 4)) != hipSuccess) return hip_fail(e, "hipMalloc (ssaa)");
+    {
+        std::lock_guard<std::recursive_mutex> g(image_mu_);
+        if ((e = d_image_.reserve((size_t)dw * dh * 4)) != hipSuccess) return hip_fail(e, "hipMalloc (ssaa)");
+    }
     hipEventRecord(ev_[2], stream_);
     if ((e = rt_launch_downscale(d_internal_.as<uint32_t>(), img_w_, img_h_, f, d_image_.as<uint32_t>(), stream_)) !=
         hipSuccess)
@@ -1234,6 +1245,7 @@ int Renderer::post_process()
     float ms = 0;
     hipEventElapsedTime(&ms, ev_[2], ev_[3]);
     post_ms_ += ms;
+    std::lock_guard<std::recursive_mutex> g(image_mu_);   // apply_ssaa's swap under _image_mutex (:1132-1134)
     img_w_ = dw;
     img_h_ = dh;
     img_is_internal_ = false;
@@ -1298,20 +1310,65 @@ int Renderer::get_ssao_buffers(float* z, float* n4, int32_t* ao)
 
 int Renderer::get_image(uint32_t* argb, int32_t* w, int32_t* h)
 {
+    std::lock_guard<std::recursive_mutex> g(image_mu_);
     if (w) *w = img_w_;
     if (h) *h = img_h_;
     if (!argb)
         return RT_OK;
+    const size_t n = (size_t)img_w_ * img_h_;
     if (!rendered_) {
         // init_buffers / clear_image fill with BACKGROUND_COLOR (renderer.cpp:131-134)
         uint32_t bg = color_to_argb(col(135.0f / 255.0f, 206.0f / 255.0f, 235.0f / 255.0f));
-        for (size_t i = 0; i < (size_t)img_w_ * img_h_; i++) argb[i] = bg;
+        for (size_t i = 0; i < n; i++) argb[i] = bg;
         return RT_OK;
     }
-    hipSetDevice(device_);
+    // the image as it stands in HBM: a frame still rendering on stream_ (another thread) is
+    // neither waited for nor blocked -- the copy runs on a non-blocking stream of its own
+    hipError_t e = hipSetDevice(device_);
+    if (e == hipSuccess && !display_stream_)
+        e = hipStreamCreateWithFlags(&display_stream_, hipStreamNonBlocking);
+    if (e == hipSuccess && display_bytes_ < n * 4) {
+        if (display_host_) hipHostFree(display_host_);
+        display_host_ = nullptr;
+        display_bytes_ = 0;
+        e = hipHostMalloc(&display_host_, n * 4, hipHostMallocDefault);
+        if (e == hipSuccess) display_bytes_ = n * 4;
+    }
     const DevBuf& src = img_is_internal_ ? d_internal_ : d_image_;
-    hipError_t e = hipMemcpy(argb, src.p, (size_t)img_w_ * img_h_ * 4, hipMemcpyDeviceToHost);
-    if (e != hipSuccess) return hip_fail(e, "get_image");
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(display_host_, src.p, n * 4, hipMemcpyDeviceToHost, display_stream_);
+    if (e == hipSuccess)
+        e = hipStreamSynchronize(display_stream_);
+    if (e != hipSuccess) {
+        // (not err_: the owning thread may be writing it)
+        display_err_ = std::string("get_image: ") + hipGetErrorString(e);
+        return RT_EHIP;
+    }
+    std::memcpy(argb, display_host_, n * 4);
+    return RT_OK;
+}
+
+// The frame about to launch renders into the internal buffer, which becomes the image
+// (Renderer::_image, written pixel by pixel by ray_trace, renderer.cpp:1080-1112).  The
+// reference re-creates _image (uninitialised) each SSAA frame (:1079-1080) and keeps the
+// previous one otherwise; here a fresh or re-created image starts as BACKGROUND_COLOR
+// (init_buffers, :131-134), so a display sees the frame's finished tiles over a defined fill.
+int Renderer::begin_internal_image(int rw, int rh)
+{
+    std::lock_guard<std::recursive_mutex> g(image_mu_);
+    const size_t n = (size_t)rw * rh;
+    const bool grown = d_internal_.bytes < n * 4 || !d_internal_.p;
+    hipError_t e = d_internal_.reserve(n * 4);
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc (image)");
+    if (grown || s_.enable_ssaa || !img_is_internal_ || !rendered_ || img_w_ != rw || img_h_ != rh) {
+        const uint32_t bg = color_to_argb(col(135.0f / 255.0f, 206.0f / 255.0f, 235.0f / 255.0f));
+        if ((e = hipMemsetD32Async((hipDeviceptr_t)d_internal_.p, (int)bg, n, stream_)) != hipSuccess)
+            return hip_fail(e, "hipMemsetD32Async (image)");
+    }
+    img_w_ = rw;
+    img_h_ = rh;
+    img_is_internal_ = true;
+    rendered_ = true;
     return RT_OK;
 }
 
@@ -1559,6 +1616,77 @@ int Renderer::trace_rays(const float* orig, const float* dir, int64_t n, int32_t
         return hip_fail(e, "download (rays)");
     if ((e = hipStreamSynchronize(stream_)) != hipSuccess)
         return hip_fail(e, "trace_rays_kernel");
+    return RT_OK;
+}
+
+// Renderer::trace_ray (renderer.cpp:1008-1066) over n host rays at current_recursion_depth
+// 'depth', each with a fresh HitInfo (trace_colors_kernel)
+int Renderer::trace_ray_colors(const float* orig, const float* dir, int64_t n, int depth, float* rgba, int32_t* src,
+                               float* t, uint8_t* found, uint8_t* shadow)
+{
+    if (n < 0 || n > (1 << 30) || depth < 0 ||
+        (n > 0 && (!orig || !dir || !rgba || !src || !t || !found || !shadow)))
+        return fail(RT_EINVAL, "trace_ray: bad arguments");
+    if (validate() != RT_OK)
+        return fail(RT_EINVAL, "invalid scene: material index out of range or enabled texture map missing");
+    if (check_frame() != RT_OK)
+        return fail(RT_EUNSUPPORTED, "reflective materials with max_recursion_depth > 15");
+    int rc = ensure_device_scene();
+    if (rc != RT_OK)
+        return rc;
+    if (n == 0)
+        return RT_OK;
+    if (depth > s_.max_recursion_depth) {
+        // renderer.cpp:1012-1013: Color(0.0f), the record untouched, intersection_found false
+        for (int64_t i = 0; i < n; i++) {
+            rgba[4 * i] = rgba[4 * i + 1] = rgba[4 * i + 2] = 0.0f;
+            rgba[4 * i + 3] = 1.0f;
+            src[i] = -1;
+            t[i] = -1.0f;
+            found[i] = shadow[i] = 0;
+        }
+        last_shadow_ = last_refl_ = 0;
+        return RT_OK;
+    }
+    KParams P;
+    fill_params(P);
+    P.max_recursion_depth = s_.max_recursion_depth - depth;   // only the difference is read
+    DevBuf din, dout;
+    din.device = dout.device = device_;
+    size_t nb = (size_t)n;
+    hipError_t e;
+    if ((e = din.reserve(nb * 24)) != hipSuccess || (e = dout.reserve(nb * 26)) != hipSuccess ||
+        (e = d_counters_.reserve(NCOUNTER_WORDS * 8)) != hipSuccess)
+        return hip_fail(e, "hipMalloc (rays)");
+    float* d_o = din.as<float>();
+    float* d_d = d_o + 3 * nb;
+    float4* d_rgba = dout.as<float4>();
+    int32_t* d_src = reinterpret_cast<int32_t*>(d_rgba + nb);
+    float* d_t = reinterpret_cast<float*>(d_src + nb);
+    uint8_t* d_found = reinterpret_cast<uint8_t*>(d_t + nb);
+    uint8_t* d_sh = d_found + nb;
+    P.counters = d_counters_.as<unsigned long long>();
+    if (wait_slots(stream_) != RT_OK)   // band launches in flight share the counters' buffer
+        return RT_EHIP;
+    if ((e = hipMemsetAsync(d_counters_.p, 0, NCOUNTER_WORDS * 8, stream_)) != hipSuccess ||
+        (e = hipMemcpyAsync(d_o, orig, nb * 12, hipMemcpyHostToDevice, stream_)) != hipSuccess ||
+        (e = hipMemcpyAsync(d_d, dir, nb * 12, hipMemcpyHostToDevice, stream_)) != hipSuccess)
+        return hip_fail(e, "upload (rays)");
+    if ((e = rt_launch_trace_colors(&P, P.has_reflection, d_o, d_d, (int)n, d_rgba, d_src, d_t, d_found, d_sh,
+                                    stream_)) != hipSuccess)
+        return hip_fail(e, "trace_colors_kernel launch");
+    unsigned long long cnt[NCOUNTERS] = {};
+    if ((e = hipMemcpyAsync(rgba, d_rgba, nb * 16, hipMemcpyDeviceToHost, stream_)) != hipSuccess ||
+        (e = hipMemcpyAsync(src, d_src, nb * 4, hipMemcpyDeviceToHost, stream_)) != hipSuccess ||
+        (e = hipMemcpyAsync(t, d_t, nb * 4, hipMemcpyDeviceToHost, stream_)) != hipSuccess ||
+        (e = hipMemcpyAsync(found, d_found, nb, hipMemcpyDeviceToHost, stream_)) != hipSuccess ||
+        (e = hipMemcpyAsync(shadow, d_sh, nb, hipMemcpyDeviceToHost, stream_)) != hipSuccess ||
+        (e = hipMemcpyAsync(cnt, d_counters_.p, sizeof(cnt), hipMemcpyDeviceToHost, stream_)) != hipSuccess)
+        return hip_fail(e, "download (rays)");
+    if ((e = hipStreamSynchronize(stream_)) != hipSuccess)
+        return hip_fail(e, "trace_colors_kernel");
+    last_shadow_ = (int64_t)cnt[0];
+    last_refl_ = (int64_t)cnt[1];
     return RT_OK;
 }
 

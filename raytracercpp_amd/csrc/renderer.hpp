@@ -9,6 +9,7 @@
 
 #include <atomic>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -97,7 +98,19 @@ public:
     // trace_triangle shading (shadows / reflections through the octree)
     int raster_trace();
     int post_process();
+    // Renderer::get_image (renderer.cpp:106-109); callable from another thread while this
+    // handle renders (the display thread, QT/mainWindowThreads.cpp:6-23): it copies the image as
+    // it stands in HBM on its own stream, so a frame in progress shows its finished tiles
     int get_image(uint32_t* argb, int32_t* w, int32_t* h);
+    // Renderer::lock_image_mutex / unlock_image_mutex (renderer.h:41-42, renderer.cpp:96-104):
+    // while held, no frame switches or reallocates the image (get_image takes it too)
+    void lock_image() { image_mu_.lock(); }
+    void unlock_image() { image_mu_.unlock(); }
+    std::string display_error()
+    {
+        std::lock_guard<std::recursive_mutex> g(image_mu_);
+        return display_err_;
+    }
     // diagnostics: _z_buffer, _normal_buffer (xyz + pad) and the last SSAO pass's counts
     int get_ssao_buffers(float* z, float* n4, int32_t* ao);
     int request_aux(bool rgba, bool hit, bool shadow);
@@ -121,6 +134,9 @@ public:
     // BVH::intersect over n host rays (closest hit, reference semantics)
     int trace_rays(const float* orig, const float* dir, int64_t n, int32_t* id, float* t, float* u, float* v,
                    uint8_t* ret);
+    // Renderer::trace_ray (shaded) over n host rays at current_recursion_depth 'depth'
+    int trace_ray_colors(const float* orig, const float* dir, int64_t n, int depth, float* rgba, int32_t* src,
+                         float* t, uint8_t* found, uint8_t* shadow);
 
     const std::string& error() const { return err_; }
 
@@ -222,7 +238,17 @@ private:
     bool tri9_dirty_ = true;
     bool want_rgba_ = false, want_hit_ = false, want_shadow_ = false;
     bool aux_valid_ = false;
-    // current image (Renderer::_image): internal after ray_trace, downscaled after post_process
+    // current image (Renderer::_image): internal from the start of ray_trace, downscaled after
+    // post_process.  image_mu_ (Renderer::_image_mutex) guards these fields and the image
+    // buffers' (re)allocation against get_image on a display thread, which copies on its own
+    // non-blocking stream through a pinned staging buffer.
+    std::recursive_mutex image_mu_;
+    hipStream_t display_stream_ = nullptr;
+    void* display_host_ = nullptr;
+    size_t display_bytes_ = 0;
+    std::string display_err_;   // get_image's last failure (err_ belongs to the owning thread)
+    // the image becomes the internal buffer of a frame about to launch (trace_frame)
+    int begin_internal_image(int rw, int rh);
     int img_w_ = 0, img_h_ = 0;
     bool img_is_internal_ = false;
     bool rendered_ = false;

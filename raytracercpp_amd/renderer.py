@@ -216,12 +216,26 @@ class Renderer:
         self._call("rt_post_process")
 
     def get_image(self) -> np.ndarray:
-        """Renderer::get_image: the current ARGB32 image as (h, w) uint32 (row 0 = bottom)."""
+        """Renderer::get_image: the current ARGB32 image as (h, w) uint32 (row 0 = bottom).
+        Safe from a display thread while another thread renders (progressive readback): the
+        size query and the copy run under the image lock."""
         w, h = C.c_int32(), C.c_int32()
-        self._call("rt_get_image", ptr(None, _u32p), C.byref(w), C.byref(h))
-        out = np.zeros((h.value, w.value), np.uint32)
-        self._call("rt_get_image", ptr(out, _u32p), C.byref(w), C.byref(h))
+        self.lock_image()
+        try:
+            self._call("rt_get_image", ptr(None, _u32p), C.byref(w), C.byref(h))
+            out = np.zeros((h.value, w.value), np.uint32)
+            self._call("rt_get_image", ptr(out, _u32p), C.byref(w), C.byref(h))
+        finally:
+            self.unlock_image()
         return out
+
+    def lock_image(self):
+        """Renderer::lock_image_mutex (renderer.h:41)."""
+        self._call("rt_lock_image")
+
+    def unlock_image(self):
+        """Renderer::unlock_image_mutex (renderer.h:42)."""
+        self._call("rt_unlock_image")
 
     def request_aux(self, rgba=False, hit=False, shadow=False):
         self._call("rt_request_aux", int(rgba), int(hit), int(shadow))
@@ -283,6 +297,21 @@ class Renderer:
         self._call("rt_trace_rays", ptr(o, _f32p), ptr(d, _f32p), n, ptr(ids, _i32p), ptr(t, _f32p), ptr(u, _f32p),
                    ptr(v, _f32p), ptr(ret, _u8p))
         return ids, t, u, v, ret
+
+    def trace_ray(self, orig, dirs, current_recursion_depth=0):
+        """Renderer::trace_ray (shaded) for a batch of rays, each with a fresh HitInfo
+        -> (rgba [n,4], hit_src, t, intersection_found, shadowed)."""
+        o = f32(orig).reshape(-1, 3)
+        d = f32(dirs).reshape(-1, 3)
+        n = o.shape[0]
+        rgba = np.zeros((n, 4), np.float32)
+        src = np.zeros(n, np.int32)
+        t = np.zeros(n, np.float32)
+        found = np.zeros(n, np.uint8)
+        shadowed = np.zeros(n, np.uint8)
+        self._call("rt_trace_ray", ptr(o, _f32p), ptr(d, _f32p), n, int(current_recursion_depth), ptr(rgba, _f32p),
+                   ptr(src, _i32p), ptr(t, _f32p), ptr(found, _u8p), ptr(shadowed, _u8p))
+        return rgba, src, t, found, shadowed
 
     def kernel_times(self, n):
         ms = np.zeros(n, np.float32)
