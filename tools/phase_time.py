@@ -9,6 +9,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import numpy as np
 
+os.environ.setdefault("RT_ASYNC_ACCEL", "0")   # every frame on the wide BVH
+
 from raytracercpp_amd import scenes
 from raytracercpp_amd.renderer import Renderer
 
