@@ -1746,6 +1746,34 @@ __device__ __forceinline__ void downscale_tile(const KParams& P, int lane, int l
     }
 }
 
+// Renderer::ray_trace's ray generation (renderer.cpp:1086-1098) for pixel (px, py): the two
+// Transform::operator()(Point) (mat.cpp:83-100) skip their division when the host found w
+// constant (KParams::proj_mode, c2w_affine); the direction is bit for bit the general path's.
+__device__ __forceinline__ v3 camera_dir(const KParams& P, int px, int py, v3 cam)
+{
+    const float y_world = ((float)py + 0.5f) / P.rh * 2 - 1;
+    const float x_world = ((float)px + 0.5f) / P.rw * 2 - 1;
+    v3 vs;
+    if (P.proj_mode != 0) {
+        const float* m = P.proj_inv;
+        const float x = x_world, y = y_world, z = -1.0f;
+        const float xt = m[0] * x + m[1] * y + m[2] * z + m[3];
+        const float yt = m[4] * x + m[5] * y + m[6] * z + m[7];
+        const float zt = m[8] * x + m[9] * y + m[10] * z + m[11];
+        const float w = P.proj_w;
+        vs = P.proj_mode == 1 ? mk(xt, yt, zt) : mk(xt * w, yt * w, zt * w);
+    } else
+        vs = xform_point(P.proj_inv, mk(x_world, y_world, -1));
+    v3 ws;
+    if (P.c2w_affine && fabsf(vs.x) < INFINITY && fabsf(vs.y) < INFINITY && fabsf(vs.z) < INFINITY) {
+        const float* m = P.cam_to_world;
+        ws = mk(m[0] * vs.x + m[1] * vs.y + m[2] * vs.z + m[3], m[4] * vs.x + m[5] * vs.y + m[6] * vs.z + m[7],
+                m[8] * vs.x + m[9] * vs.y + m[10] * vs.z + m[11]);
+    } else
+        ws = xform_point(P.cam_to_world, vs);
+    return normalize(ws - cam);
+}
+
 // Renderer::ray_trace (renderer.cpp:1068-1116): one lane per pixel, one wave
 // per 8x8 tile.  Waves are persistent and pull tiles from the sharded device-scope
 // queue (tile_queue_next): shadow-ray-heavy tiles cluster around the object, so
@@ -1792,13 +1820,8 @@ __global__ __launch_bounds__(BLOCK, PLAIN ? RT_OCC_PLAIN : RT_OCC) void ray_trac
         if (PLAIN) PH_MARK(0);
         if (px >= P.rw || py >= P.rh)
             continue;
-
         // ray generation, renderer.cpp:1086-1098
-        float y_world = ((float)py + 0.5f) / P.rh * 2 - 1;
-        float x_world = ((float)px + 0.5f) / P.rw * 2 - 1;
-        v3 vs = xform_point(P.proj_inv, mk(x_world, y_world, -1));
-        v3 ws = xform_point(P.cam_to_world, vs);
-        v3 rd = normalize(ws - cam);
+        const v3 rd = camera_dir(P, px, py, cam);
         if (PLAIN) PH_MARK(1);
 
         uint32_t rng = REFL ? pixel_seed((uint32_t)(py * P.rw + px), P.rng_seed) : 0u;
@@ -1913,11 +1936,7 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void refl_level0_kernel(KParams P, F
         if (px >= P.rw || py >= P.rh)
             continue;
         // ray generation, renderer.cpp:1086-1098
-        float y_world = ((float)py + 0.5f) / P.rh * 2 - 1;
-        float x_world = ((float)px + 0.5f) / P.rw * 2 - 1;
-        v3 vs = xform_point(P.proj_inv, mk(x_world, y_world, -1));
-        v3 ws = xform_point(P.cam_to_world, vs);
-        v3 rd = normalize(ws - cam);
+        const v3 rd = camera_dir(P, px, py, cam);
 
         Rec fin = rec_fresh();
         int src = closest_hit(P, cam, rd, fin, lv);

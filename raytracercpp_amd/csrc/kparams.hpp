@@ -60,6 +60,14 @@ struct KParams {
     float proj_inv[16];
     float cam_to_world[16];
     float light[3];
+    // Ray generation shortcuts (kernels.hip camera_dir), set on the host when they give the same
+    // bits as Transform::operator()(Point) (mat.cpp:83-100) for every pixel:
+    //   proj_mode 1: proj_inv's w row makes w == 1 for every image-plane point; 2: w is the same
+    //   value 1 / proj_w_den for every one (row 3 = (0, 0, c, d)), proj_w = that reciprocal;
+    //   0: per pixel.  c2w_affine: cam_to_world's row 3 is (0, 0, 0, 1) (w == 1 for finite points).
+    int32_t proj_mode;
+    float proj_w;
+    int32_t c2w_affine;
 
     KTex tex[TEX_SLOTS];
     KTex sky[6];

@@ -841,6 +841,27 @@ void Renderer::fill_params(KParams& P) const
     std::memcpy(P.proj_inv, proj_inv_, sizeof(P.proj_inv));
     std::memcpy(P.cam_to_world, c2w_, sizeof(P.cam_to_world));
     std::memcpy(P.light, light_, sizeof(P.light));
+    {
+        // ray generation shortcuts (kparams.hpp): for an image-plane point (x, y, -1) with finite x, y
+        // the w row evaluates ((m12 x + m13 y) + m14 (-1)) + m15; with m12 = m13 = 0 that is the
+        // constant (-m14) + m15 (the two signed zeros add to a zero that leaves -m14 unchanged when
+        // it is nonzero; a zero or non-finite constant keeps the per-pixel path)
+        const float* m = proj_inv_;
+        bool fin = true;
+        for (int i = 0; i < 16; i++) fin = fin && std::isfinite(m[i]);
+        P.proj_mode = 0;
+        P.proj_w = 1.0f;
+        if (fin && m[12] == 0.0f && m[13] == 0.0f && m[14] != 0.0f) {
+            volatile float mz = m[14] * -1.0f;   // (volatile: evaluated as the kernel does, in float)
+            const float wt = mz + m[15];
+            if (std::isfinite(wt) && wt != 0.0f) {
+                P.proj_mode = wt == 1.0f ? 1 : 2;
+                P.proj_w = 1.0f / wt;
+            }
+        }
+        const float* c = c2w_;
+        P.c2w_affine = c[12] == 0.0f && c[13] == 0.0f && c[14] == 0.0f && c[15] == 1.0f;
+    }
     for (int i = 0; i < TEX_SLOTS; i++) {
         P.tex[i].px = tex_[i].rgba.empty() ? nullptr : d_tex_[i].as<float4>();
         P.tex[i].w = tex_[i].w;

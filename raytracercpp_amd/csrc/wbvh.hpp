@@ -193,10 +193,21 @@ RT_HD GNode load_gnode(const GNode* p)
     return g;
 }
 
+RT_HD float fast_rcp(float a)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcpf(a);
+#else
+    // host emulation: the correctly rounded reciprocal (the device's is within 1 ulp of it;
+    // both stay inside the slab margin)
+    return 1.0f / a;
+#endif
+}
+
 // BoundingVolume::intersect (bvh.h:79-105) with the ray's plane products as
 // OctreeNode::intersect computes them (bvh.h:216-223), branch-free as kernels.hip
 // vol_test: returns pass && t_near <= t.
-RT_HD bool kdop_certifies(const GNode& nd, v3 o, v3 d, float t)
+RT_HD bool kdop_certifies_exact(const GNode& nd, v3 o, v3 d, float t)
 {
     float t_near = -INFINITY, t_far = INFINITY;
 #pragma unroll
@@ -214,15 +225,37 @@ RT_HD bool kdop_certifies(const GNode& nd, v3 o, v3 d, float t)
     return !(t_far < t_near) && t_near <= t;
 }
 
-RT_HD float fast_rcp(float a)
+// The same decision, first from quotients through the hardware reciprocal (1 ulp): each is
+// within 2^-21 of the correctly rounded one (relative), a max / min of them within 2^-21 of its
+// exact counterpart's magnitude, so a comparison won by more than 2^-19 (|t_near| + |t_far| + |t|)
+// is the exact comparison's.  Closer calls, a denominator below 2^-100 (reciprocal range) and
+// infinite bounds take the correctly rounded divisions.  The numerators are the reference's.
+RT_HD bool kdop_certifies(const GNode& nd, v3 o, v3 d, float t)
 {
-#if defined(__HIP_DEVICE_COMPILE__)
-    return __builtin_amdgcn_rcpf(a);
-#else
-    // host emulation: the correctly rounded reciprocal (the device's is within 1 ulp of it;
-    // both stay inside the slab margin)
-    return 1.0f / a;
-#endif
+    float t_near = -INFINITY, t_far = INFINITY;
+    bool tiny = false;
+#pragma unroll
+    for (int i = 0; i < NPLANES; i++) {
+        v3 n = mk(PLANE_N[i][0], PLANE_N[i][1], PLANE_N[i][2]);
+        float den = dot(n, d);
+        float num = dot(n, o);
+        if (den == 0.0f)
+            num = __builtin_nanf("");
+        tiny |= den != 0.0f && !(fabsf(den) >= 0x1p-100f);
+        const float r = fast_rcp(den);
+        float d0 = (nd.dn[i] - num) * r;
+        float d1 = (nd.df[i] - num) * r;
+        t_near = fmaxf(t_near, fminf(d0, d1));
+        t_far = fminf(t_far, fmaxf(d0, d1));
+    }
+    const float e = (fabsf(t_near) + fabsf(t_far) + fabsf(t)) * 0x1p-19f;
+    if (!tiny && fabsf(t_near) < INFINITY && fabsf(t_far) < INFINITY && e < INFINITY) {
+        if (t_far - t_near > e && t - t_near > e)
+            return true;
+        if (t_near - t_far > e || t_near - t > e)
+            return false;
+    }
+    return kdop_certifies_exact(nd, o, d, t);
 }
 
 RT_HD uint32_t fbits(float f) { return __builtin_bit_cast(uint32_t, f); }
