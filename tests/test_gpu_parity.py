@@ -903,7 +903,9 @@ def test_camera_matrix_forms_match_oracle(R, cam):
     elif cam == "projective_c2w":
         c2w[12:16] = np.float32([0.002, -0.001, 0.003, 1.0])
     elif cam == "w_one":
-        pinv[14], pinv[15] = np.float32(0.0), np.float32(1.0)           # w == 1: no scaling at all
+        # (-m14) + m15 == 1: w == 1 for every pixel, the point is not scaled (proj_mode 1)
+        pinv[15] = np.float32(1.0) + pinv[14]
+        assert np.float32(-pinv[14]) + pinv[15] == np.float32(1.0)
     sc = dataclasses.replace(sc, proj_inv=pinv, cam_to_world=c2w)
     o = Oracle(sc, st).render_rows()
     g = gpu_render(R, sc, st)
