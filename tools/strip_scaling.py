@@ -38,6 +38,8 @@ def main():
     sc, st = scenes.CONFIGS[args.config]()
     r = Renderer(0)
     r.load_scene(sc, st)
+    r.ray_trace()
+    r.finish_accel()   # every timed step on the wide BVH
     W = st.image_width
     rw, rh = st.render_size()
     band = args.band_rows
