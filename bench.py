@@ -30,7 +30,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 # Roofline.  The kernel is bound by dependent gathers through L1 / L2, not by
-# HBM: its ~130 MB working set stays in L2 and the Infinity Cache (profiles/r03f: 45 MB of
+# HBM: its ~130 MB working set stays in L2 and the Infinity Cache (profiles/r03g: 41 MB of
 # HBM traffic per launch against 4.2 GB read by the traversal).  The executed bytes are
 # priced against the L2 ceiling; the HBM rate and the guide's random-row gather rate are
 # reported beside it.  Peaks: /opt/skills/guides/MI355X_MICROARCH.md.
@@ -44,7 +44,7 @@ CERT_BYTES = 72              # one certificate: the octree leaf's 64-B node + tw
 PIXEL_BYTES = 4              # ARGB32 write per internal pixel
 COUNTS_FILE = os.path.join(ROOT, "profiles", "work_counts.json")
 # rocprofv3 PMC summary of this kernel on the same command (tools/profile_gpu.sh + profile_summary.py)
-PROFILE_SUMMARY = os.path.join(ROOT, "profiles", "r03f", "summary.json")
+PROFILE_SUMMARY = os.path.join(ROOT, "profiles", "r03g", "summary.json")
 C5_CHECK_ROWS = (172, 400, 540, 907)   # output rows whose internal row pairs bench's C5 mode checks
 
 
