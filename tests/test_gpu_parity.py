@@ -911,3 +911,29 @@ def test_camera_matrix_forms_match_oracle(R, cam):
     g = gpu_render(R, sc, st)
     assert int((o.hit_id >= 0).sum()) > 500, cam
     _check_vs_oracle(g, o, cam, R=R)
+
+
+def test_band_counters_across_self_resetting_launches(R):
+    """Band launches of the default trace path reset their slot's counters themselves (no memset
+    between frames, KParams::self_reset): repeated launches on one stream and on alternating
+    streams each report the frame's shadow-ray count and produce the same strips."""
+    import torch
+    from raytracercpp_amd import scenes
+    sc, st = scenes.bumpy70k(width=160, height=96, enable_ssaa=True, ssaa_factor=2)
+    R.load_scene(sc, st)
+    R.ray_trace()
+    full_shadow = R.stats()["shadow_rays"]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    nloc = R.local_rows(8, 0, 1)
+    outs = [torch.zeros((nloc, st.image_width), dtype=torch.int32, device="cuda:0") for _ in range(2)]
+    torch.cuda.synchronize()
+    first = None
+    for i in range(6):
+        s = streams[0] if i < 3 else streams[i % 2]
+        R.render_bands_device(8, 0, 1, outs[i % 2].data_ptr(), s.cuda_stream)
+        sh, rf = R.band_counters()
+        assert (sh, rf) == (full_shadow, 0), (i, sh, full_shadow)
+        img = outs[i % 2].cpu().numpy()
+        if first is None:
+            first = img.copy()
+        assert np.array_equal(img, first), i
