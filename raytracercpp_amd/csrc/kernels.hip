@@ -1995,9 +1995,19 @@ __global__ __launch_bounds__(BLOCK) void refl_keys_kernel(KParams P, const Frame
         float lo = P.nodes[0].dn[a], hi = P.nodes[0].df[a];
         float t = (fr[f].ro[a] - lo) / (hi - lo);
         t = t == t ? fminf(fmaxf(t, 0.0f), 1.0f) : 0.0f;
+#if defined(RT_REFL_KEY_DIR)
+        q[a] = (uint32_t)(t * 511.0f);
+#else
         q[a] = (uint32_t)(t * 1023.0f);
+#endif
     }
+#if defined(RT_REFL_KEY_DIR)
+    const uint32_t oct = (fr[f].perfect[0] < 0.0f ? 1u : 0u) | (fr[f].perfect[1] < 0.0f ? 2u : 0u) |
+                         (fr[f].perfect[2] < 0.0f ? 4u : 0u);
+    keys[f] = (oct << 27) | spread10(q[0]) | (spread10(q[1]) << 1) | (spread10(q[2]) << 2);
+#else
     keys[f] = spread10(q[0]) | (spread10(q[1]) << 1) | (spread10(q[2]) << 2);
+#endif
     idx[f] = f;
 }
 
