@@ -292,6 +292,39 @@ def roofline(config, world, kernel_ms, ms_per_step, primary):
     return out
 
 
+def cgroup_cpus():
+    """CPUs the job's cgroup may use (cpu.max quota / period, cgroup v2; v1 cfs files), or None."""
+    for q, per in (("/sys/fs/cgroup/cpu.max", None), ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us",
+                                                         "/sys/fs/cgroup/cpu/cpu.cfs_period_us")):
+        try:
+            with open(q) as f:
+                txt = f.read().split()
+            if per is None:
+                if txt[0] == "max":
+                    return None
+                return max(1, int(int(txt[0]) / int(txt[1])))
+            quota = int(txt[0])
+            if quota <= 0:
+                return None
+            with open(per) as f:
+                return max(1, int(quota / int(f.read().split()[0])))
+        except (OSError, ValueError, IndexError, ZeroDivisionError):
+            continue
+    return None
+
+
+def all_cores():
+    """Every core this process may run on (OMP_NUM_THREADS=$(nproc), as the
+    reference's OpenMP loop forks, renderer.cpp:1082): the affinity mask, capped by the cgroup's
+    CPU quota when one is set (threads beyond it only time-share the quota)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    q = cgroup_cpus()
+    return min(aff, q) if q else aff
+
+
 def cpu_info(threads):
     model = None
     try:
@@ -306,7 +339,8 @@ def cpu_info(threads):
         affinity = len(os.sched_getaffinity(0))
     except AttributeError:
         affinity = None
-    return {"cpu_model": model, "os_cpu_count": os.cpu_count(), "affinity_cpus": affinity, "threads": threads}
+    return {"cpu_model": model, "os_cpu_count": os.cpu_count(), "affinity_cpus": affinity,
+            "cgroup_cpu_quota": cgroup_cpus(), "threads": threads}
 
 
 def cpu_leg(sc, st, gpu_img, threads, c5, check=True, baseline=True):
@@ -320,12 +354,8 @@ def cpu_leg(sc, st, gpu_img, threads, c5, check=True, baseline=True):
       reference library was not built."""
     from oracle.bindings import Oracle, RefHarness
     if not threads:
-        try:
-            aff = len(os.sched_getaffinity(0))
-        except AttributeError:
-            aff = os.cpu_count() or 1
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or aff
-    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+        threads = all_cores()
+    env_threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     rw, rh = st.render_size()
     W = st.image_width
     dpx, check_desc, port = None, None, None
@@ -355,22 +385,35 @@ def cpu_leg(sc, st, gpu_img, threads, c5, check=True, baseline=True):
         port.update(cpu_info(threads))
         return port, dpx, check_desc
     stride = 128 if c5 else 2
-    passes = []
-    rr = None
-    for i in range(6):   # one warm-up pass, then 5 timed
-        rr = RefHarness.render_row_sample(sc, st, stride // 2, rh // stride, stride)
-        if i:
-            passes.append(rr.seconds)
-    sec = float(np.median(passes))
-    c = rr.counters
-    rays = c["primary_rays"] + c["shadow_rays"] + (c["reflection_rays"] if c5 else 0)
-    base = {"value": round(rays / sec / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "reference",
+
+    def ref_rate(nthr):
+        RefHarness.set_threads(nthr)
+        passes = []
+        rr = None
+        for i in range(6):   # one warm-up pass, then 5 timed
+            rr = RefHarness.render_row_sample(sc, st, stride // 2, rh // stride, stride)
+            if i:
+                passes.append(rr.seconds)
+        sec = float(np.median(passes))
+        c = rr.counters
+        rays = c["primary_rays"] + c["shadow_rays"] + (c["reflection_rays"] if c5 else 0)
+        return rays / sec / 1e6, passes, c
+
+    rate, passes, c = ref_rate(threads)
+    # the box's default team (OMP_NUM_THREADS, 16 on the GPU pool) beside it, when it differs
+    alt = None
+    if env_threads and env_threads != threads:
+        alt = {"threads": env_threads, "value": round(ref_rate(env_threads)[0], 3)}
+    RefHarness.set_threads(threads)
+    base = {"value": round(rate, 3), "unit": "Mrays/s", "cores": threads, "kind": "reference",
             "sample": f"every {stride}th internal row of the {'C5' if c5 else 'C4'} frame ({rh // stride} rows x {rw}: "
                       f"{c['primary_rays']} primary + {c['shadow_rays']} shadow"
                       + (f" + {c['reflection_rays']} reflection" if c5 else "") +
                       f" rays, octree build excluded), reference TUs + OpenMP x{threads}; median of 5 passes "
                       f"after one warm-up ({', '.join(f'{p:.3f}' for p in passes)} s)",
             "port_value": port["value"] if port else None}
+    if alt:
+        base["omp_num_threads_env"] = alt
     base.update(cpu_info(threads))
     return base, dpx, check_desc
 

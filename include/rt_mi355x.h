@@ -106,6 +106,8 @@ typedef struct rt_stats {
     float build_split_ms[4];   /* the last scene build, host milliseconds: octree build + flatten; leaf cones and
                                   slabs, and the wide BVH with its upload (both on the background thread,
                                   rt_finish_accel; 0 until adopted); the octree's upload */
+    int64_t host_builds;       /* host octree builds since rt_create, over every device of rt_set_devices (its
+                                  helpers copy the lead's build: one per geometry change, renderer.cpp:214-224) */
 } rt_stats;
 
 typedef struct rt_renderer rt_renderer;
@@ -152,7 +154,13 @@ int rt_finish_accel(rt_renderer *r);
  * frame.  ids may instead repeat the handle's device n times (n renderers on one device, the
  * bands copied instead of sent: the same path without RCCL, for one-device machines).
  * Frames with enable_ssao render on ids[0] alone (SSAO reads across bands);
- * rt_ray_trace / rt_post_process / rt_get_internal are single-device as before. */
+ * rt_ray_trace / rt_post_process / rt_get_internal are single-device as before.
+ * The geometry is built once, on ids[0]; the other devices copy its device tables (rt_stats
+ * host_builds).
+ * EXPERIMENTAL: distinct device ids (the RCCL send / receive path) have not run on a multi-GPU
+ * machine yet; they are refused with RT_EUNSUPPORTED unless RT_MULTIDEV_RCCL=1 is set in the
+ * environment (tests/test_gpu_parity.py test_set_devices_distinct_rccl runs them where two or
+ * more devices exist).  The repeated-device form is tested on every GPU run. */
 int rt_set_devices(rt_renderer *r, const int32_t *ids, int32_t n);
 
 /* Renderer::change_render_size (renderer.cpp:250-261) */

@@ -363,8 +363,14 @@ class RefHarness:
             L.ref_heap_order.argtypes = [_f32p, C.c_int, _i32p]
             L.ref_ssao.argtypes = [C.POINTER(OrcScene), C.POINTER(OrcSettings), _f32p, _f32p, _u32p, _i32p]
             L.ref_set_rng_sequential.argtypes = [C.c_int, C.c_uint32]
+            L.ref_set_threads.argtypes = [C.c_int]
             cls._lib = L
         return cls._lib
+
+    @classmethod
+    def set_threads(cls, n):
+        """OpenMP team size of the harness's row loops (omp_set_num_threads)."""
+        cls.lib().ref_set_threads(int(n))
 
     @classmethod
     def set_rng_sequential(cls, on, seed=0):

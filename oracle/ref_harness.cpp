@@ -697,6 +697,14 @@ void ref_set_rng_sequential(int on, uint32_t seed)
 /* Wall time of the last ref_render_rows pixel loop (the octree build excluded). */
 double ref_last_render_seconds(void) { return g_last_render_seconds; }
 
+/* the OpenMP team size of the row loops (the reference forks omp_get_max_threads(), i.e.
+   OMP_NUM_THREADS or every CPU, renderer.cpp:1082); n <= 0 leaves it unchanged */
+void ref_set_threads(int n)
+{
+    if (n > 0)
+        omp_set_num_threads(n);
+}
+
 static int render_rows_strided(const orc_scene* sc, const orc_settings* st, int row_begin, int row_count,
                                int row_stride, orc_outputs* out, orc_counters* counters);
 

@@ -55,7 +55,7 @@ class RtStats(C.Structure):
         ("gpu_nodes", C.c_int64), ("gpu_tris", C.c_int64),
         ("render_width", C.c_int32), ("render_height", C.c_int32), ("seg_scale", C.c_float),
         ("work", C.c_int64 * 4), ("work_wide", C.c_int64 * 4), ("uncertified", C.c_int64 * 6),
-        ("wave_steps", C.c_int64 * 6), ("build_split_ms", C.c_float * 4),
+        ("wave_steps", C.c_int64 * 6), ("build_split_ms", C.c_float * 4), ("host_builds", C.c_int64),
     ]
 
     def as_dict(self):

@@ -901,6 +901,14 @@ __device__ void count_wave_steps(const KParams& P, int base, uint32_t steps)
 }
 #endif
 
+// The grazing split of the wide query's child test (wbvh.hpp wbvh_closest QS) per query kind
+#ifndef W_QS_CLOSEST
+#define W_QS_CLOSEST 0x1p-8f
+#endif
+#ifndef W_QS_SHADOW
+#define W_QS_SHADOW 0x1p-8f
+#endif
+
 // BVH::intersect through the wide BVH and its certificate (wbvh.hpp).
 // Returns true with (h, r) = the reference's record and boolean when the query is
 // certified; false when it must be traced through the octree.
@@ -914,7 +922,8 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
     WHit w;
 #if RT_COUNT
     uint32_t wk[4] = {0, 0, 0, 0};
-    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, INFINITY, true);
+    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, INFINITY, true,
+                                W_QS_CLOSEST);
     count_wave_steps(P, 22, wk[3]);
     if (P.counters) {
         atomicAdd(&P.counters[10], (unsigned long long)wk[0]);
@@ -925,7 +934,7 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
     }
 #else
     const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, INFINITY,
-                                true);
+                                true, W_QS_CLOSEST);
 #endif
     if (st == W_MISS) {
         h.t = -1.0f;
@@ -976,7 +985,8 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
     WHit w;
 #if RT_COUNT
     uint32_t wk[4] = {0, 0, 0, 0};
-    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, hi, false);
+    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, hi, false,
+                                W_QS_SHADOW);
     count_wave_steps(P, 25, wk[3]);
     if (P.counters) {
         atomicAdd(&P.counters[10], (unsigned long long)wk[0]);
@@ -986,7 +996,8 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
                 atomicAdd(&P.counters[16 + c], 1ull);   // uncertified, by reason (wbvh_closest)
     }
 #else
-    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, hi, false);
+    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, hi, false,
+                                W_QS_SHADOW);
 #endif
     if (st == W_MISS) {
         *sh = false;
@@ -1103,7 +1114,7 @@ __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
         bool sh;
         if (P.wnodes && P.nnodes > 0 && !nan && wide_shadow(P, o, d, hi, p, lp, lv, &sh))
             return sh;
-        const OctQ q = octree_query<PLAIN>(P, o, d, -m, hi, true, lv);
+        const OctQ q = octree_query<PLAIN>(P, o, d, -m, hi, P.seg_oct != 0, lv);
         h = q.h;
         r = q.r;
         if (r) {
@@ -2095,7 +2106,7 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_kernel(KParams 
     bool r;
     if (P.wnodes && P.nnodes > 0 && !R.nan && wide_closest(P, ld3(F.ro), dir, h, r, lv))
         ;   // certified by the wide BVH
-    else if (P.seg_scale > 0.0f) {
+    else if (P.seg_scale > 0.0f && P.seg_oct) {
         R.lo = -seg_margin(P, R);   // nothing behind the origin can be hit (t >= 0)
         r = bvh_closest_seg(P, R, h, lv);
     } else

@@ -85,8 +85,11 @@ struct KParams {
     int32_t enable_roughness_mapping, enable_skysphere, enable_skybox;
     uint32_t rng_seed;
     int32_t has_reflection;   // RT_SHADING with a material whose reflection > 0: the reflection engine
-    float seg_scale;          // > 0: shadow / reflection queries are segment queries (kernels.hip seg_margin),
-                              // the scene's largest |coordinate|; 0: every query walks the whole line
+    float seg_scale;          // > 0: shadow queries end at the light (kernels.hip is_shadowed's hi, with
+                              // seg_margin's rounding bound), the scene's largest |coordinate|; 0: none
+    int32_t seg_oct;          // 1: the octree walks only the volumes overlapping a shadow / reflection
+                              // query's segment (assumes no grazing report falls outside its
+                              // volumes, RT_SEG_OCTREE=1); 0 (default): the octree walks the whole line
 
     // image: render size (internal, after the SSAA factor) and this launch's rows
     int32_t rw, rh;

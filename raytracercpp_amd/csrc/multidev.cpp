@@ -6,6 +6,7 @@
 #include <rccl/rccl.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <set>
@@ -78,6 +79,12 @@ int Renderer::set_devices(const int* ids, int n)
         one_device = one_device && ids[i] == device_;
     if (!one_device && n > ndev)
         return fail(RT_EINVAL, "rt_set_devices: more devices than the machine has");
+    if (!one_device) {
+        const char* v = getenv("RT_MULTIDEV_RCCL");
+        if (!v || v[0] == '0')
+            return fail(RT_EUNSUPPORTED, "rt_set_devices: distinct devices (RCCL) are experimental, not yet run on a "
+                                         "multi-GPU machine; set RT_MULTIDEV_RCCL=1 to use them");
+    }
     std::set<int> seen;
     for (int i = 0; i < n && !one_device; i++)
         if (ids[i] < 0 || ids[i] >= ndev || !seen.insert(ids[i]).second)
@@ -91,6 +98,7 @@ int Renderer::set_devices(const int* ids, int n)
         std::string err;
         if (h->init(err) != RT_OK)
             return fail(RT_EHIP, "rt_set_devices: device " + std::to_string(ids[i]) + ": " + err);
+        h->lead_ = this;   // its scene comes from this renderer's build (adopt_from_lead)
         M->helpers.push_back(std::move(h));
         auto b = std::make_unique<DevBuf>();
         b->device = ids[i];
@@ -175,6 +183,12 @@ int Renderer::render_multi()
     auto t0 = std::chrono::steady_clock::now();
     hipError_t e = hipSetDevice(device_);
     if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    // the lead's scene first: the helpers copy its build (one host build per geometry change)
+    {
+        int rc0 = ensure_device_scene();
+        if (rc0 != RT_OK)
+            return rc0;
+    }
     if ((e = M.gather.reserve(chunk * n)) != hipSuccess) return hip_fail(e, "hipMalloc (gather)");
     for (int i = 1; i < n; i++) {
         Renderer& h = *M.helpers[i - 1];

@@ -83,6 +83,7 @@ Knobs Knobs::from_env()
     };
     k.wbvh = on("RT_WBVH", true);   // (exact mode overrides: Renderer::fill_params)
     k.seg = on("RT_SEG", true);
+    k.seg_oct = on("RT_SEG_OCTREE", false);
     k.cones = on("RT_CONES", true);
     k.lslab = on("RT_LSLAB", true);
     k.plain = on("RT_PLAIN", true);
@@ -92,6 +93,10 @@ Knobs Knobs::from_env()
     k.refl_fuse = on("RT_REFL_FUSE", true);
     k.debug_waves = getenv("RT_DEBUG_WAVES") != nullptr;
     k.exact = on("RT_EXACT", false);
+    {
+        const char* v = getenv("RT_INJECT_FRAME_FAIL");   // tests: the k-th ray_trace fails after its image start
+        k.inject_fail = v ? std::atoi(v) : 0;
+    }
     k.async_accel = on("RT_ASYNC_ACCEL", true);
     if (const char* ce = getenv("RT_REFL_CHUNK_LOG2")) {
         const int v = atoi(ce);
@@ -156,6 +161,8 @@ Renderer::~Renderer()
     if (stream_) hipStreamDestroy(stream_);
     if (display_stream_) hipStreamDestroy(display_stream_);
     if (display_host_) hipHostFree(display_host_);
+    for (void* q : display_old_)
+        hipHostFree(q);
 }
 
 int Renderer::fail(int code, const std::string& msg)
@@ -632,6 +639,8 @@ int Renderer::poll_accel(bool wait)
     accel_state_.store(0);
     cones_ready_ = !cones_.empty();
     wide_ready_ = !wb_.nodes.empty();
+    lslab_ready_ = !lslab_.empty();
+    ++accel_ver_;
     build_split_ms_[1] = accel_ms_[0];
     build_split_ms_[2] = accel_ms_[1] + accel_ms_[2];
     return RT_OK;
@@ -645,6 +654,74 @@ int Renderer::finish_accel()
     return poll_accel(true);
 }
 
+// A multi-device helper's scene (rt_set_devices): the lead has built and uploaded the octree
+// (render_multi ensures its scene first); the helper copies the lead's device tables to its own
+// device instead of building them again, and later the lead's leaf cones / slabs and wide BVH
+// once the lead has adopted them.  One host build per geometry change for any number of devices
+// (the reference rebuilds once, renderer.cpp:214-224).
+int Renderer::adopt_from_lead()
+{
+    const Renderer& L = *lead_;
+    hipError_t e = hipSuccess;
+    auto copy = [&](DevBuf& dst, const DevBuf& src, size_t n) {
+        if (e != hipSuccess || n == 0)
+            return;
+        if ((e = dst.reserve(n)) == hipSuccess)
+            e = hipMemcpyPeerAsync(dst.p, device_, src.p, L.device_, n, stream_);
+    };
+    if (geom_dirty_) {
+        poll_accel(true);
+        cones_ready_ = wide_ready_ = lslab_ready_ = false;
+        auto t0 = std::chrono::steady_clock::now();
+        oct_ = FlatOctree();   // (never built here)
+        oct_nn_ = L.oct_nn_;
+        oct_nt_ = L.oct_nt_;
+        oct_levels_ = L.oct_levels_;
+        oct_root_ = L.oct_root_;
+        oct_stats_ = L.oct_stats_;
+        has_uv_dev_ = L.has_uv_dev_;
+        copy(d_nodes_, L.d_nodes_, (size_t)L.oct_nn_ * sizeof(GNode));
+        copy(d_tris_, L.d_tris_, (size_t)L.oct_nt_ * sizeof(GTri));
+        copy(d_tri_id_, L.d_tri_id_, (size_t)L.oct_nt_ * 4);
+        copy(d_tri_mat_, L.d_tri_mat_, tri_mat_.size() * 4);
+        copy(d_tri_uv_, L.d_tri_uv_, L.has_uv_dev_ ? tri_uv_.size() * 4 : 0);
+        if (e == hipSuccess)
+            e = hipStreamSynchronize(stream_);
+        if (e != hipSuccess)
+            return hip_fail(e, "rt_set_devices: scene copy from the lead device");
+        geom_dirty_ = false;
+        tri9_dirty_ = true;
+        mir_accel_ = ~0ull;
+        build_ms_ = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        build_split_ms_[0] = build_split_ms_[1] = build_split_ms_[2] = 0.0f;
+        build_split_ms_[3] = build_ms_;
+    }
+    if (mir_accel_ != L.accel_ver_ && mir_geom_ == L.geom_ver_ && !L.geom_dirty_ && (L.cones_ready_ || L.wide_ready_)) {
+        const size_t ns = (size_t)L.oct_nt_;
+        if (L.cones_ready_) {
+            copy(d_cones_, L.d_cones_, 4 * ns * 4);
+            if (L.lslab_ready_) {
+                copy(d_lslab_, L.d_lslab_, 8 * ns * 4);
+                copy(d_lsin_, L.d_lsin_, ns * 4);
+            }
+        }
+        if (L.wide_ready_) {
+            copy(d_wnodes_, L.d_wnodes_, L.wb_.nodes.size() * sizeof(WNode));
+            copy(d_wtris_, L.d_wtris_, L.wb_.slot.size() * sizeof(GTri));
+            copy(d_wmeta_, L.d_wmeta_, L.wb_.slot.size() * 16);
+        }
+        if (e == hipSuccess)
+            e = hipStreamSynchronize(stream_);
+        if (e != hipSuccess)
+            return hip_fail(e, "rt_set_devices: acceleration structures from the lead device");
+        cones_ready_ = L.cones_ready_;
+        lslab_ready_ = L.cones_ready_ && L.lslab_ready_;
+        wide_ready_ = L.wide_ready_;
+        mir_accel_ = L.accel_ver_;
+    }
+    return RT_OK;
+}
+
 int Renderer::ensure_device_scene()
 {
     hipError_t e = hipSetDevice(device_);
@@ -653,10 +730,14 @@ int Renderer::ensure_device_scene()
     // frames still in flight on other streams read the buffers replaced below
     if ((geom_dirty_ || mats_dirty_ || tex_dirty_) && sync_slots() != RT_OK)
         return RT_EHIP;
-    if (geom_dirty_) {
+    if (lead_) {
+        int rc = adopt_from_lead();
+        if (rc != RT_OK)
+            return rc;
+    } else if (geom_dirty_) {
         // a build of the previous geometry reads oct_: let it finish (its result is dropped)
         poll_accel(true);
-        cones_ready_ = wide_ready_ = false;
+        cones_ready_ = wide_ready_ = lslab_ready_ = false;
         using clk = std::chrono::steady_clock;
         auto ms_since = [](clk::time_point t) { return std::chrono::duration<float, std::milli>(clk::now() - t).count(); };
         auto t0 = clk::now();
@@ -688,6 +769,13 @@ int Renderer::ensure_device_scene()
             }
         }
         build_split_ms_[0] = ms_since(t0);
+        ++host_builds_;
+        oct_nn_ = (int64_t)oct_.nodes.size();
+        oct_nt_ = (int64_t)oct_.tris.size();
+        oct_levels_ = oct_.levels;
+        oct_root_ = oct_nn_ > 0 ? oct_.nodes[0] : GNode{};
+        oct_stats_ = oct_.stats;
+        has_uv_dev_ = !tri_uv_.empty();
         // the octree and the triangle tables (everything the exact path reads), synchronously
         auto t1 = clk::now();
         size_t nb = oct_.nodes.size() * sizeof(GNode), tb = oct_.tris.size() * sizeof(GTri);
@@ -809,15 +897,15 @@ void Renderer::fill_params(KParams& P) const
     P.tris = d_tris_.as<GTri>();
     P.tri_id = d_tri_id_.as<int32_t>();
     P.tri_mat = d_tri_mat_.as<int32_t>();
-    P.tri_uv = tri_uv_.empty() ? nullptr : d_tri_uv_.as<float>();
+    P.tri_uv = has_uv_dev_ ? d_tri_uv_.as<float>() : nullptr;
     P.cones = (!cones_ready_ || !knobs_.cones) ? nullptr : d_cones_.as<float>();
     // (the leaf slabs read the cone axis)
-    P.lslab = (!P.cones || lslab_.empty() || !knobs_.lslab) ? nullptr : d_lslab_.as<float>();
+    P.lslab = (!P.cones || !lslab_ready_ || !knobs_.lslab) ? nullptr : d_lslab_.as<float>();
     P.lsin = P.lslab ? d_lsin_.as<float>() : nullptr;
     P.scene_scale = 0.0f;
-    if (!oct_.nodes.empty())
+    if (oct_nn_ > 0)
         for (int c = 0; c < 3; c++)
-            P.scene_scale = std::max(P.scene_scale, std::max(std::fabs(oct_.nodes[0].dn[c]), std::fabs(oct_.nodes[0].df[c])));
+            P.scene_scale = std::max(P.scene_scale, std::max(std::fabs(oct_root_.dn[c]), std::fabs(oct_root_.df[c])));
     // wide BVH: closest-hit queries certified against the octree, when it
     // was built, the scene's scale keeps the certificate's rounding margins (as for the
     // segment queries), and RT_WBVH is not 0
@@ -826,9 +914,9 @@ void Renderer::fill_params(KParams& P) const
         P.wtris = d_wtris_.as<GTri>();
         P.wmeta = d_wmeta_.as<uint4>();
     }
-    P.nnodes = (int32_t)oct_.nodes.size();
-    P.ntri_slots = (int32_t)oct_.tris.size();
-    P.levels = oct_.levels > 0 ? oct_.levels : 1;
+    P.nnodes = (int32_t)oct_nn_;
+    P.ntri_slots = (int32_t)oct_nt_;
+    P.levels = oct_levels_ > 0 ? oct_levels_ : 1;
     P.nshape = (int32_t)shape_kind_.size();
     for (int k = 0; k < P.nshape; k++) {
         P.shape_kind[k] = shape_kind_[k];
@@ -897,8 +985,9 @@ void Renderer::fill_params(KParams& P) const
     // record) and the scene's scale keeps Moller-Trumbore's products far from overflow
     // and underflow, so that the rounding bound of seg_margin holds
     P.seg_scale = 0.0f;
-    if (knobs_.seg && !knobs_.exact && P.nshape == 0 && !oct_.nodes.empty()) {
-        const GNode& root = oct_.nodes[0];
+    P.seg_oct = knobs_.seg_oct ? 1 : 0;
+    if (knobs_.seg && !knobs_.exact && P.nshape == 0 && oct_nn_ > 0) {
+        const GNode& root = oct_root_;
         float S = 0.0f;
         for (int a = 0; a < 3; a++)   // the axis slabs are the vertices' coordinate range
             S = std::max(S, std::max(std::fabs(root.dn[a]), std::fabs(root.df[a])));
@@ -1183,8 +1272,30 @@ int Renderer::trace_frame()
     hipError_t e;
     if ((e = d_counters_.reserve(NCOUNTER_WORDS * 8)) != hipSuccess)
         return hip_fail(e, "hipMalloc (counters)");
+    // the image state before this frame: restored if the frame fails after the image became its
+    // internal buffer (a partly written frame is never presented; when the previous image was that
+    // same buffer, its content is gone and the image reads as not rendered)
+    const int prev_w = img_w_, prev_h = img_h_;
+    const bool prev_internal = img_is_internal_, prev_rendered = rendered_;
     if ((rc = begin_internal_image(P.rw, P.rh)) != RT_OK)
         return rc;
+    struct Restore {
+        Renderer* r;
+        int w, h;
+        bool internal, rendered, armed = true;
+        ~Restore()
+        {
+            if (!armed)
+                return;
+            std::lock_guard<std::recursive_mutex> g(r->image_mu_);
+            r->img_w_ = w;
+            r->img_h_ = h;
+            r->img_is_internal_ = internal;
+            r->rendered_ = rendered && !internal;
+        }
+    } restore{this, prev_w, prev_h, prev_internal, prev_rendered};
+    if (knobs_.inject_fail > 0 && ++frames_started_ == knobs_.inject_fail)
+        return fail(RT_EHIP, "injected frame failure (RT_INJECT_FRAME_FAIL)");
     if (want_rgba_ && (e = d_rgba_.reserve(npx * 16)) != hipSuccess) return hip_fail(e, "hipMalloc (rgba)");
     if (want_hit_ && ((e = d_hit_id_.reserve(npx * 4)) != hipSuccess || (e = d_hit_t_.reserve(npx * 4)) != hipSuccess))
         return hip_fail(e, "hipMalloc (hit)");
@@ -1227,6 +1338,7 @@ int Renderer::trace_frame()
     aux_valid_ = true;
     ssao_ready_ = s_.enable_ssao;
     post_ms_ = 0;
+    restore.armed = false;
     return RT_OK;
 }
 
@@ -1349,11 +1461,16 @@ int Renderer::get_image(uint32_t* argb, int32_t* w, int32_t* h)
     if (e == hipSuccess && !display_stream_)
         e = hipStreamCreateWithFlags(&display_stream_, hipStreamNonBlocking);
     if (e == hipSuccess && display_bytes_ < n * 4) {
-        if (display_host_) hipHostFree(display_host_);
-        display_host_ = nullptr;
-        display_bytes_ = 0;
-        e = hipHostMalloc(&display_host_, n * 4, hipHostMallocDefault);
-        if (e == hipSuccess) display_bytes_ = n * 4;
+        // a larger staging buffer: the old one is freed only when the renderer is destroyed
+        // (hipHostFree synchronises the device, i.e. it would wait for the frame in flight)
+        void* q = nullptr;
+        e = hipHostMalloc(&q, n * 4, hipHostMallocDefault);
+        if (e == hipSuccess) {
+            if (display_host_)
+                display_old_.push_back(display_host_);
+            display_host_ = q;
+            display_bytes_ = n * 4;
+        }
     }
     const DevBuf& src = img_is_internal_ ? d_internal_ : d_image_;
     if (e == hipSuccess)
@@ -1446,13 +1563,17 @@ int Renderer::get_stats(rt_stats* out) const
     out->kernel_ms = kernel_ms_;
     out->post_ms = post_ms_;
     out->build_ms = build_ms_;
-    out->octree_inner = oct_.stats.inner;
-    out->octree_leaves = oct_.stats.leaves;
-    out->octree_empty_leaves = oct_.stats.empty_leaves;
-    out->octree_max_leaf = oct_.stats.max_leaf;
-    out->octree_max_depth = oct_.stats.max_depth;
-    out->gpu_nodes = (int64_t)oct_.nodes.size();
-    out->gpu_tris = (int64_t)oct_.tris.size();
+    out->octree_inner = oct_stats_.inner;
+    out->octree_leaves = oct_stats_.leaves;
+    out->octree_empty_leaves = oct_stats_.empty_leaves;
+    out->octree_max_leaf = oct_stats_.max_leaf;
+    out->octree_max_depth = oct_stats_.max_depth;
+    out->gpu_nodes = oct_nn_;
+    out->gpu_tris = oct_nt_;
+    out->host_builds = host_builds_;
+    if (multi_)
+        for (const auto& h : multi_->helpers)
+            out->host_builds += h->host_builds_;
     render_size(out->render_width, out->render_height);
     out->seg_scale = last_seg_;
     for (int i = 0; i < 4; i++) out->work[i] = last_work_[i];

@@ -40,7 +40,9 @@ struct HostTex {
 // (rt_create); each selects an equivalent path (same framebuffer) for A/B runs and tests.
 struct Knobs {
     bool wbvh = true;         // RT_WBVH=0: no wide BVH, every query walks the octree
-    bool seg = true;          // RT_SEG=0: shadow / reflection queries walk the whole line (5.2)
+    bool seg = true;          // RT_SEG=0: shadow queries have no segment end (5.2)
+    bool seg_oct = false;     // RT_SEG_OCTREE=1: the octree walks only a shadow / reflection query's segment
+                              // (5.2; off by default: it assumes no grazing report falls outside its volumes)
     bool cones = true;        // RT_CONES=0: no leaf normal cones (5.3; also turns the leaf slabs off)
     bool lslab = true;        // RT_LSLAB=0: no leaf slabs (5.4)
     bool plain = true;        // RT_PLAIN=0: no plain specialisation of ray_trace_kernel (5.6)
@@ -51,6 +53,7 @@ struct Knobs {
     int refl_chunk_log2 = 25; // RT_REFL_CHUNK_LOG2 (10..25): sample slots per engine chunk
     bool debug_waves = false; // RT_DEBUG_WAVES: per-wave records of diagnostic builds (rt_debug_read)
     bool exact = false;       // RT_EXACT=1 / rt_set_exact: wbvh and seg off
+    int inject_fail = 0;      // RT_INJECT_FRAME_FAIL=k (tests): the k-th ray_trace fails after its image start
     bool async_accel = true;  // RT_ASYNC_ACCEL=0: the leaf cones / slabs and the wide BVH are built
                               // before the first frame instead of beside it
     static Knobs from_env();
@@ -179,10 +182,17 @@ private:
     std::string accel_err_;
     hipStream_t accel_stream_ = nullptr;
     float accel_ms_[3] = {};            // cones + slabs, wide BVH, wide-BVH upload (background)
-    bool cones_ready_ = false, wide_ready_ = false;
+    bool cones_ready_ = false, wide_ready_ = false, lslab_ready_ = false;
+    uint64_t accel_ver_ = 0;   // bumped when poll_accel adopts a build
     void start_accel();
     int poll_accel(bool wait);
     void mirror_from(const Renderer& lead);
+    // a multi-device helper (rt_set_devices): the lead builds the octree, the leaf cones / slabs
+    // and the wide BVH once; a helper copies the lead's device buffers to its own device
+    const Renderer* lead_ = nullptr;
+    uint64_t mir_accel_ = ~0ull;   // the lead's accel_ver_ copied
+    int adopt_from_lead();
+    int64_t host_builds_ = 0;      // host octree builds (rt_stats host_builds, helpers included)
     struct MultiDev;
     std::unique_ptr<MultiDev> multi_;
     int num_cus_ = 256;
@@ -212,6 +222,12 @@ private:
 
     // device state
     FlatOctree oct_;
+    // what the frames read of the octree on the host (a helper gets the lead's)
+    int64_t oct_nn_ = 0, oct_nt_ = 0;
+    int oct_levels_ = 0;
+    GNode oct_root_{};
+    OctreeStats oct_stats_{};
+    bool has_uv_dev_ = false;   // d_tri_uv_ holds texcoords
     bool geom_dirty_ = true, mats_dirty_ = true, tex_dirty_ = true;
     DevBuf d_nodes_, d_tris_, d_tri_id_, d_tri_mat_, d_tri_uv_, d_mats_;
     DevBuf d_tex_[TEX_SLOTS], d_sky_[6];
@@ -246,6 +262,8 @@ private:
     hipStream_t display_stream_ = nullptr;
     void* display_host_ = nullptr;
     size_t display_bytes_ = 0;
+    std::vector<void*> display_old_;   // outgrown staging buffers (freed with the renderer)
+    int frames_started_ = 0;           // (RT_INJECT_FRAME_FAIL)
     std::string display_err_;   // get_image's last failure (err_ belongs to the owning thread)
     // the image becomes the internal buffer of a frame about to launch (trace_frame)
     int begin_internal_image(int rw, int rh);

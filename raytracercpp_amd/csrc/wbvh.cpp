@@ -167,6 +167,7 @@ struct Builder {
     Pool& pool;
     int32_t next = 1;             // the cooperative phase's node counter (one thread)
     float ct = 1.0f;              // SAH cost of a node visit, in triangle tests (r02: 2 and 3 were slower)
+    int32_t maxleaf = W_MAX_LEAF; // primitives per leaf at most
     struct Task {
         int32_t ni, b, e;
         Box box, cbox;
@@ -265,13 +266,13 @@ struct Builder {
         if (n <= 1)
             return false;
         if (!any)
-            return n > W_MAX_LEAF;   // every centroid equal: halves in order
+            return n > maxleaf;   // every centroid equal: halves in order
         float cost;
         best_split(*B, scale, box, axis, split, cost);
-        if (axis >= 0 && n <= W_MAX_LEAF && (float)n <= cost)
+        if (axis >= 0 && n <= maxleaf && (float)n <= cost)
             return false;   // a leaf is no more expensive than the best split
         if (axis < 0)
-            return n > W_MAX_LEAF;
+            return n > maxleaf;
         return true;
     }
 
@@ -512,6 +513,43 @@ struct Builder {
         }
     }
 };
+
+// The conditioning bytes (wbvh.hpp wq_val): the largest code whose value is <= x (a lower
+// bound on a sine in [0, 1]), and the smallest code whose value is >= x (an upper bound; for
+// lengths 255 = no bound).
+uint32_t wq_code_lb(double x)
+{
+    if (!(x > 0))
+        return 0u;
+    if (x >= 1)
+        return 255u;
+    float f = (float)x;
+    if ((double)f > x)
+        f = std::nextafter(f, 0.0f);
+    uint32_t bits;
+    std::memcpy(&bits, &f, 4);
+    if (bits < WQ_UNIT + (1u << 20))
+        return 0u;
+    const uint32_t k = (bits - WQ_UNIT) >> 20;
+    return k > 255u ? 255u : k;
+}
+
+uint32_t wq_code_ub(double x, uint32_t base)
+{
+    if (!(x > 0))
+        return x == 0 ? 0u : 255u;   // (NaN: no bound)
+    float f = (float)x;
+    if ((double)f < x)
+        f = std::nextafter(f, INFINITY);
+    uint32_t bits;
+    std::memcpy(&bits, &f, 4);
+    if (bits <= base + (1u << 20))
+        return 1u;
+    const uint32_t k = (bits - base + (1u << 20) - 1u) >> 20;
+    if (base == WQ_UNIT)
+        return k > 255u ? 255u : k;
+    return k > 254u ? 255u : k;
+}
 
 // One 4-wide node: the children's float boxes quantised to 8 bits per plane against the
 // node box's low corner, low planes rounded down and high planes up (exact in double:
@@ -795,6 +833,123 @@ struct Planner {
     }
 };
 
+// Two-level build: a binary SAH tree over the octree's non-empty leaves (one leaf per top
+// leaf, boxes = the leaf's triangles' boxes and its k-DOP's axis planes), then under each top
+// leaf a binary SAH tree over that octree leaf's triangles.  Every node above the octree
+// leaves then holds the k-DOP boxes of the octree leaves of all its triangles.
+void build_two_level(const FlatOctree& oct, std::vector<Prim, DefaultInitAlloc<Prim>>& P,
+                     std::vector<Prim, DefaultInitAlloc<Prim>>& tmp, std::vector<BNode, DefaultInitAlloc<BNode>>& bn,
+                     Pool& pool)
+{
+    std::vector<uint32_t> leaves;
+    for (size_t i = 0; i < oct.nodes.size(); i++)
+        if ((oct.nodes[i].b & LEAF_BIT) && (oct.nodes[i].b & ~LEAF_BIT) > 0)
+            leaves.push_back((uint32_t)i);
+    const int32_t nl = (int32_t)leaves.size();
+    std::vector<Prim, DefaultInitAlloc<Prim>> LP((size_t)nl), Ltmp((size_t)nl);
+    parallel_for(pool, nl, 256, [&](int64_t k) {
+        const GNode& g = oct.nodes[leaves[(size_t)k]];
+        Box b = empty_box();
+        for (int a = 0; a < 3; a++) {
+            b.lo[a] = g.dn[a];
+            b.hi[a] = g.df[a];
+        }
+        for (uint32_t s = g.a; s < g.a + (g.b & ~LEAF_BIT); s++)
+            grow(b, Box{{P[s].lo[0], P[s].lo[1], P[s].lo[2]}, {P[s].hi[0], P[s].hi[1], P[s].hi[2]}});
+        Prim& q = LP[(size_t)k];
+        for (int a = 0; a < 3; a++) {
+            q.lo[a] = b.lo[a];
+            q.hi[a] = b.hi[a];
+        }
+        q.pad = 0.0f;
+        q.id = (int32_t)k;
+    });
+    std::vector<BNode, DefaultInitAlloc<BNode>> tn((size_t)(2 * nl + 4 * (nl / PAR_BIN) + 64));
+    std::vector<GTri> dummy((size_t)std::max<int32_t>(nl, 1));   // make_leaf's normal sums: recomputed below
+    for (auto& t : dummy)
+        std::memset(&t, 0, sizeof(t));
+    {
+        Builder T(LP, Ltmp, tn, dummy.data(), pool);
+        T.maxleaf = 1;
+        T.run(nl);
+    }
+    // the top tree's nodes: those reachable from the root
+    std::vector<int32_t> order;   // top nodes, preorder
+    std::vector<int32_t> st{0};
+    while (!st.empty()) {
+        int32_t k = st.back();
+        st.pop_back();
+        order.push_back(k);
+        if (tn[(size_t)k].left >= 0) {
+            st.push_back(tn[(size_t)k].right);
+            st.push_back(tn[(size_t)k].left);
+        }
+    }
+    const int32_t ntop = (int32_t)tn.size();
+    // the triangles in top-leaf order
+    std::vector<int32_t> tb((size_t)nl), te((size_t)nl);
+    {
+        int32_t pos = 0;
+        for (int32_t k : order) {
+            const BNode& N = tn[(size_t)k];
+            if (N.left >= 0)
+                continue;
+            for (int32_t i = N.first; i < N.first + N.count; i++) {
+                const int32_t lk = LP[(size_t)i].id;
+                const GNode& g = oct.nodes[leaves[(size_t)lk]];
+                tb[(size_t)lk] = pos;
+                for (uint32_t s = g.a; s < g.a + (g.b & ~LEAF_BIT); s++)
+                    tmp[(size_t)pos++] = P[s];
+                te[(size_t)lk] = pos;
+            }
+        }
+        std::copy(tmp.begin(), tmp.begin() + pos, P.begin());
+    }
+    const size_t need = (size_t)ntop + 2 * P.size() + 64;
+    if (bn.size() < need)
+        bn.resize(need);
+    for (int32_t k : order)
+        bn[(size_t)k] = tn[(size_t)k];
+    // bottom trees: each top leaf (one octree leaf) becomes the root of its triangles' tree, with
+    // the top leaf's box (it holds the octree leaf's k-DOP box)
+    std::vector<int32_t> top_leaves;
+    for (int32_t k : order)
+        if (tn[(size_t)k].left < 0)
+            top_leaves.push_back(k);
+    std::vector<GTri> none;
+    Builder Bt(P, tmp, bn, oct.tris.data(), pool);
+    parallel_for(pool, (int64_t)top_leaves.size(), 16, [&](int64_t q) {
+        const int32_t k = top_leaves[(size_t)q];
+        const BNode N0 = tn[(size_t)k];
+        int32_t b = INT32_MAX, e = 0;
+        for (int32_t i = N0.first; i < N0.first + N0.count; i++) {
+            b = std::min(b, tb[(size_t)LP[(size_t)i].id]);
+            e = std::max(e, te[(size_t)LP[(size_t)i].id]);
+        }
+        VBox vb = VBox::empty(), vc = VBox::empty();
+        for (int32_t i = b; i < e; i++) {
+            vb.grow(plo(P[(size_t)i]), phi(P[(size_t)i]));
+            const __m128 c = pcen(P[(size_t)i]);
+            vc.grow(c, c);
+        }
+        int32_t alloc = ntop + 2 * b;
+        double sah = 0;
+        Bt.build_serial(k, b, e, vb.box(), vc.box(), alloc, sah);
+        bn[(size_t)k].box = N0.box;
+    });
+    // top inner nodes: triangle ranges and normal sums, children first
+    for (size_t q = order.size(); q-- > 0;) {
+        BNode& N = bn[(size_t)order[q]];
+        if (tn[(size_t)order[q]].left < 0)
+            continue;
+        const BNode &L = bn[(size_t)N.left], &R = bn[(size_t)N.right];
+        N.first = L.first;
+        N.count = L.count + R.count;
+        for (int a = 0; a < 3; a++)
+            N.ns[a] = L.ns[a] + R.ns[a];
+    }
+}
+
 }  // namespace
 
 void build_wbvh(const FlatOctree& oct, WBvh& out)
@@ -834,17 +989,21 @@ void build_wbvh(const FlatOctree& oct, WBvh& out)
     // 2n for the tasks' regions plus room for the cooperative phase's nodes
     std::vector<BNode, DefaultInitAlloc<BNode>> bn((size_t)(2 * n + 4 * (n / PAR_BIN) + 64));
     phase("prep");
-    Builder B(P, tmp, bn, oct.tris.data(), pool);
-    B.run((int32_t)n);
-    phase("binary");
-    // SAH cost of the binary tree (diagnostic)
-    {
+    // two levels (the default): every node above the octree's leaves holds the k-DOP boxes of the
+    // octree leaves of all its triangles (the grazing-sound query's rho = 0 there)
+    const bool two = !(std::getenv("RT_WBVH_TWOLEVEL") && std::atoi(std::getenv("RT_WBVH_TWOLEVEL")) == 0);
+    if (!two) {
+        Builder B(P, tmp, bn, oct.tris.data(), pool);
+        B.run((int32_t)n);
+        // SAH cost of the binary tree (diagnostic)
         const float ra = area(bn[0].box) > 0 ? area(bn[0].box) : 1.0f;
         double s = B.sah_big;
         for (const auto& T : B.tasks)
             s += T.sah;
         out.stats.sah = (float)(s / ra);
-    }
+    } else
+        build_two_level(oct, P, tmp, bn, pool);
+    phase("binary");
     // the triangles in the final (leaf) order, and the cone codes' unit normals
     out.tris.resize((size_t)n);
     out.slot.resize((size_t)n);
@@ -885,6 +1044,54 @@ void build_wbvh(const FlatOctree& oct, WBvh& out)
                 cg[j].n[a] = C.ns[a];
         }
         out.nodes[(size_t)w] = quantise(cb, p.link, p.nc, cg, out.tris.data(), un.data());
+        // the conditioning bytes of the grazing-sound query (wbvh.hpp WNode::ext): per child the
+        // triangles' shape and orientation bounds, and the octree leaves' reach
+        WNode& WN = out.nodes[(size_t)w];
+        for (int j = 0; j < W_WIDTH; j++) {
+            WN.ext[j] = 0u;
+            WN.ext2[j] = 0u;
+            if (j >= p.nc)
+                continue;
+            double lo[3], hi[3];
+            decode(WN, j, lo, hi);
+            const double N0 = (int8_t)(WN.nrm[j] & 0xffu), N1 = (int8_t)((WN.nrm[j] >> 8) & 0xffu),
+                         N2 = (int8_t)((WN.nrm[j] >> 16) & 0xffu);
+            const double NLd = std::sqrt(N0 * N0 + N1 * N1 + N2 * N2);
+            double smin = 1.0, s2 = 1.0, cmin = 1.0, lmax = 0.0;
+            double ulo[3] = {lo[0], lo[1], lo[2]}, uhi[3] = {hi[0], hi[1], hi[2]};
+            for (int32_t i = cg[j].first; i < cg[j].first + cg[j].count; i++) {
+                const GTri& t = out.tris[(size_t)i];
+                const GNode& L = oct.nodes[out.leaf_of_k[(size_t)i]];
+                for (int a = 0; a < 3; a++) {
+                    ulo[a] = std::min(ulo[a], (double)L.dn[a]);
+                    uhi[a] = std::max(uhi[a], (double)L.df[a]);
+                }
+                if (t.n[0] == 0.0f && t.n[1] == 0.0f && t.n[2] == 0.0f)
+                    continue;   // Mdet = 0: never a hit
+                const double x0 = t.ab[0], x1 = t.ab[1], x2 = t.ab[2], y0 = t.ac[0], y1 = t.ac[1], y2 = t.ac[2];
+                const double c0 = x1 * y2 - x2 * y1, c1 = x2 * y0 - x0 * y2, c2 = x0 * y1 - x1 * y0;
+                const double la = std::sqrt(x0 * x0 + x1 * x1 + x2 * x2), lc = std::sqrt(y0 * y0 + y1 * y1 + y2 * y2);
+                const double cl = std::sqrt(c0 * c0 + c1 * c1 + c2 * c2);
+                lmax = std::max(lmax, std::max(la, lc) * (1 + 1e-12));
+                smin = std::min(smin, sin_at_a_lb(t));
+                if (!(la * lc > 0x1p-100) || !(cl > 0x1p-50 * la * lc) || !(NLd > 0)) {
+                    s2 = 0.0;   // no bound: a zero-area record with Mdet != 0
+                    cmin = -1.0;
+                    continue;
+                }
+                const double ca = std::fabs(x0 * y0 + x1 * y1 + x2 * y2) / (la * lc);
+                s2 = std::min(s2, std::sqrt(std::max(0.0, (1.0 - std::min(1.0, ca + 1e-12)) / 2.0)) * (1 - 1e-9));
+                cmin = std::min(cmin, (c0 * N0 + c1 * N1 + c2 * N2) / (cl * NLd) - 1e-12);
+            }
+            double rho = 0.0;
+            for (int a = 0; a < 3; a++)
+                rho = std::max(rho, std::max(lo[a] - ulo[a], uhi[a] - hi[a]));
+            cmin = std::max(-1.0, std::min(1.0, cmin));
+            const double sth = cmin > 0 ? std::min(1.0, std::sqrt(1.0 - cmin * cmin) + 1e-12) : 1.0;
+            WN.ext[j] = wq_code_lb(smin) | (wq_code_lb(s2) << 8) | (wq_code_ub(sth, WQ_UNIT) << 16) |
+                        (wq_code_ub(lmax, WQ_LEN) << 24);
+            WN.ext2[j] = wq_code_ub(rho, WQ_LEN);
+        }
     });
     phase("geometry");
     out.stats.nodes = (int64_t)out.nodes.size();

@@ -50,7 +50,7 @@ namespace rt {
 constexpr uint32_t W_LEAF = 0x80000000u;
 constexpr uint32_t W_EMPTY = 0xFFFFFFFFu;
 constexpr int W_MAX_LEAF = 8;
-constexpr int W_STACK = 12;   // traversal stack entries per lane (overflow: the query is not certified)
+constexpr int W_STACK = 16;   // traversal stack entries per lane (overflow: the query is not certified)
 constexpr int W_WIDTH = 4;    // children per node
 
 #ifndef W_STEP_HOOK
@@ -81,8 +81,18 @@ struct alignas(16) WNode {
     uint32_t nrm[W_WIDTH];
     uint32_t slab[W_WIDTH];
     uint32_t child[W_WIDTH];
+    // Conditioning of child j's triangles (the grazing-sound query), one byte each,
+    // as 8-bit minifloats (wn_code / wn_decode):
+    //   ext[j]  byte 0: smin, a lower bound on sin(alpha) (alpha: the triangle's angle at a);
+    //           byte 1: s2, a lower bound on sin(alpha' / 2), alpha' = min(alpha, pi - alpha);
+    //           byte 2: sth, an upper bound on sin(angle(N_j, n)) over the triangles' exact normals;
+    //           byte 3: lmax, an upper bound on their edges |ab|, |ac|;
+    //   ext2[j] byte 0: rho, how far the k-DOP boxes of the octree leaves holding them reach past
+    //           the child's box (0 when the child holds whole octree leaves); bytes 1-3 unused.
+    uint32_t ext[W_WIDTH];
+    uint32_t ext2[W_WIDTH];
 };
-static_assert(sizeof(WNode) == 96, "WNode size");
+static_assert(sizeof(WNode) == 128, "WNode size");
 // word offsets inside a node (the kernel loads it as 16-B rows and picks words)
 constexpr int WN_QLO = 4;                           // qlo[a] starts at word WN_QLO + a * W_WIDTH / 4
 constexpr int WN_QHI = 4 + 3 * W_WIDTH / 4;         // qhi[a] at WN_QHI + a * W_WIDTH / 4
@@ -90,7 +100,23 @@ constexpr int WN_SS = 4 + 6 * W_WIDTH / 4;          // s, slo
 constexpr int WN_NRM = ((4 + 6 * W_WIDTH / 4 + 2 + 3) / 4) * 4;
 constexpr int WN_SLAB = WN_NRM + W_WIDTH;
 constexpr int WN_CHILD = WN_SLAB + W_WIDTH;
+constexpr int WN_EXT = WN_CHILD + W_WIDTH;
+constexpr int WN_EXT2 = WN_EXT + W_WIDTH;
 constexpr int WN_ROWS = (int)(sizeof(WNode) / 16);
+
+// The conditioning bytes: value(k) = float with bits (k << 20) + base for k > 0 (three mantissa
+// bits, an octave per 8 codes); k = 0 is 0.  Unit quantities (sines) use WQ_UNIT (k = 255 is
+// 1.0), lengths WQ_LEN (2^-16 .. 2^16; k = 255 stands for "no bound", infinity).
+constexpr uint32_t WQ_UNIT = 0x3F800000u - (255u << 20);
+constexpr uint32_t WQ_LEN = 111u << 23;
+RT_HD float wq_val(uint32_t k, uint32_t base)
+{
+    return k == 0u ? 0.0f : __builtin_bit_cast(float, (k << 20) + base);
+}
+RT_HD float wq_len(uint32_t k)
+{
+    return k == 255u ? INFINITY : wq_val(k, WQ_LEN);
+}
 
 struct WStats {
     int64_t nodes = 0, leaves = 0, tris = 0, max_leaf = 0, depth = 0;
@@ -106,23 +132,37 @@ struct WBvh {
     WStats stats;
 };
 
-// sin of the triangle's angle at a (Moller-Trumbore's vertex): |n| / (|ab| |ac|) with the stored
-// normal, as a float rounded down; 1 for n = 0 (never hit: Mdet = 0); 0 where the rounding
-// analysis of DESIGN.md 5.6 does not apply (|n| outside [2^-60, 2^60] or |ab| |ac| below 2^-60).
-// Host only (kernels.hip leaf_missed's margin).
+// A lower bound on sin(angle at a) of the record's edges ab, ac (floats) from the exact cross
+// product: the double products of floats are exact, each difference rounds once (2^-53 of the
+// larger term), so |ab x ac| >= |cross_double| - 2^-51 |ab| |ac|.  1 for a zero cross product
+// of non-zero edges is not claimed: 0 then (never skipped by the query's margins).
+inline double sin_at_a_lb(const GTri& t)
+{
+    const double x0 = t.ab[0], x1 = t.ab[1], x2 = t.ab[2], y0 = t.ac[0], y1 = t.ac[1], y2 = t.ac[2];
+    const double c0 = x1 * y2 - x2 * y1, c1 = x2 * y0 - x0 * y2, c2 = x0 * y1 - x1 * y0;
+    const double ab = std::sqrt(x0 * x0 + x1 * x1 + x2 * x2), ac = std::sqrt(y0 * y0 + y1 * y1 + y2 * y2);
+    const double lam = ab * ac;
+    if (!(lam > 0x1p-100) || !(lam < 0x1p100))
+        return 0.0;
+    const double c = std::sqrt(c0 * c0 + c1 * c1 + c2 * c2);
+    return std::max(0.0, (c - 0x1p-50 * lam) / lam * (1 - 1e-12));
+}
+
+// sin of the triangle's angle at a (Moller-Trumbore's vertex) as a float rounded down, from the
+// exact cross product of the record's edges (sin_at_a_lb; the stored normal's own rounding could
+// make |n| / (|ab| |ac|) overestimate it); 1 for n = 0 (never hit: Mdet = 0); 0 where the
+// rounding analysis of DESIGN.md 5.6 does not apply (|n| outside [2^-60, 2^60], |ab| |ac|
+// outside (2^-100, 2^100)).  Host only (kernels.hip leaf_missed's margin).
 inline float sin_at_a_f(const GTri& t)
 {
     const double n = std::sqrt((double)t.n[0] * t.n[0] + (double)t.n[1] * t.n[1] + (double)t.n[2] * t.n[2]);
     if (n == 0)
         return 1.0f;
-    const double ab = std::sqrt((double)t.ab[0] * t.ab[0] + (double)t.ab[1] * t.ab[1] + (double)t.ab[2] * t.ab[2]);
-    const double ac = std::sqrt((double)t.ac[0] * t.ac[0] + (double)t.ac[1] * t.ac[1] + (double)t.ac[2] * t.ac[2]);
-    const double lam = ab * ac;
-    if (!(lam >= 0x1p-60) || !(n >= 0x1p-60 && n <= 0x1p60))
+    if (!(n >= 0x1p-60 && n <= 0x1p60))
         return 0.0f;
-    const double s = std::min(1.0, n / lam) * (1 - 1e-9);
-    const float f = (float)s;
-    return (double)f > s ? std::nextafter(f, 0.0f) : f;
+    const double sl = sin_at_a_lb(t);
+    const float f = (float)sl;
+    return (double)f > sl ? std::nextafter(f, 0.0f) : f;
 }
 
 // Binned-SAH binary build over the octree's triangle records, collapsed to 4-wide nodes
@@ -277,22 +317,149 @@ struct WStackLocal {   // host
     RT_HD uint2 get(int i) const { return e[i]; }
 };
 
+// Case (b) of wbvh_closest's child test (the triangles with q < QS), out of line: its state stays
+// out of the traversal loop's registers; it re-reads the node (in cache).  Returns the child's key
+// (the smallest t of a reported point it allows), or INFINITY.
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__
+#else
+inline
+#endif
+float wq_case_b(const WNode* node, int j, v3 o, v3 d, float ix, float iy, float iz, float m, float QS, float dl,
+                float best_s, float a, float qa, float iq)
+{
+    constexpr float SL = 0x1p-20f;
+    constexpr float U = 0x1p-24f;
+    constexpr float NLH = 127.9f;
+    // the node's words straight from memory (in cache: the traversal just read them)
+    const uint32_t* Wp = reinterpret_cast<const uint32_t*>(node);
+    auto W = [&](int i) -> uint32_t { return ldg(Wp + i); };
+    const bool nx_lo = !(ix < 0.0f), ny_lo = !(iy < 0.0f), nz_lo = !(iz < 0.0f);
+    const float ss = bitsf(W(WN_SS)), slo = bitsf(W(WN_SS + 1));
+    const uint32_t ex = W(3);
+    const float stx = bitsf((ex & 0xffu) << 23), sty = bitsf(((ex >> 8) & 0xffu) << 23),
+                stz = bitsf(((ex >> 16) & 0xffu) << 23);
+    const float sx = stx * ix, sy = sty * iy, sz = stz * iz;
+    const float Dx = bitsf(W(0)) - o.x, Dy = bitsf(W(1)) - o.y, Dz = bitsf(W(2)) - o.z;
+    const int sh = 8 * (j & 3);
+    const float qlx = (float)((W(WN_QLO + 0) >> sh) & 0xffu), qhx = (float)((W(WN_QHI + 0) >> sh) & 0xffu);
+    const float qly = (float)((W(WN_QLO + 1) >> sh) & 0xffu), qhy = (float)((W(WN_QHI + 1) >> sh) & 0xffu);
+    const float qlz = (float)((W(WN_QLO + 2) >> sh) & 0xffu), qhz = (float)((W(WN_QHI + 2) >> sh) & 0xffu);
+    const uint32_t nrj = W(WN_NRM + j);
+    const float nx = (float)(int8_t)(nrj & 0xffu), ny = (float)(int8_t)((nrj >> 8) & 0xffu),
+                nz = (float)(int8_t)((nrj >> 16) & 0xffu);
+    const uint32_t e = W(WN_EXT + j), e2 = W(WN_EXT2 + j), sbj = W(WN_SLAB + j);
+    const float sth = wq_val((e >> 16) & 0xffu, WQ_UNIT);
+    const float L = wq_len(e >> 24);
+    const float C0 = __builtin_fmaf((float)(sbj & 0xffffu), ss, slo);
+    const float C1 = __builtin_fmaf((float)(sbj >> 16), ss, slo);
+    const float b = nx * Dx + ny * Dy + nz * Dz;   // N . (origin - o)
+    auto box = [&](float M, float& tmin, float& tmax) {
+        const float mx = nx_lo ? M : -M, my = ny_lo ? M : -M, mz = nz_lo ? M : -M;
+        const float tnx = __builtin_fmaf(nx_lo ? qlx : qhx, sx, (Dx - mx) * ix);
+        const float tny = __builtin_fmaf(ny_lo ? qly : qhy, sy, (Dy - my) * iy);
+        const float tnz = __builtin_fmaf(nz_lo ? qlz : qhz, sz, (Dz - mz) * iz);
+        const float tfx = __builtin_fmaf(nx_lo ? qhx : qlx, sx, (Dx + mx) * ix);
+        const float tfy = __builtin_fmaf(ny_lo ? qhy : qly, sy, (Dy + my) * iy);
+        const float tfz = __builtin_fmaf(nz_lo ? qhz : qlz, sz, (Dz + mz) * iz);
+        tmin = fmaxf(fmaxf(tnx, tny), tnz);
+        tmax = fminf(fminf(tfx, tfy), tfz);
+    };
+    float key = INFINITY;
+    const float s2 = wq_val((e >> 8) & 0xffu, WQ_UNIT);
+    const float rho = wq_len(e2 & 0xffu);
+    const float M = m + rho;
+    float umin, umax;
+    box(M, umin, umax);   // the octree leaves' reach, any t
+    bool okb = !(umin > __builtin_fmaf(fabsf(umax), SL, umax));
+    // distances from o: the child box's farthest corner (>= |o - a|), and the
+    // widened box's (>= |x - o|) and diameter
+    const float ax0 = __builtin_fmaf(qlx, stx, Dx), ax1 = __builtin_fmaf(qhx, stx, Dx);
+    const float ay0 = __builtin_fmaf(qly, sty, Dy), ay1 = __builtin_fmaf(qhy, sty, Dy);
+    const float az0 = __builtin_fmaf(qlz, stz, Dz), az1 = __builtin_fmaf(qhz, stz, Dz);
+    const float ex0 = fmaxf(fabsf(ax0), fabsf(ax1)), ey0 = fmaxf(fabsf(ay0), fabsf(ay1)),
+                ez0 = fmaxf(fabsf(az0), fabsf(az1));
+    const float Dm = sqrtf(ex0 * ex0 + ey0 * ey0 + ez0 * ez0) * (1.0f + 0x1p-16f) + m;
+    const float H0 = 1.01f * (QS + 8.0f * U) * (L + Dm) / s2;
+    if (okb) {
+        // the origin: N . (o - origin) = -b within the slab widened by H0 + Dm sin(theta)
+        const float w = NLH * (H0 + __builtin_fmaf(Dm, sth, m)) * (1.0f + 0x1p-16f) + 384.0f * m;
+        okb = !(-b < C0 - w || -b > C1 + w);
+    }
+    if (okb) {
+        // the line where it crosses the widened box: within H0 + QS |x - o| of the
+        // triangle's plane, which lies within diam sin(theta) of the slab there
+        const float Dr = Dm + 1.733f * M, dg = sqrtf((ax1 - ax0) * (ax1 - ax0) + (ay1 - ay0) * (ay1 - ay0) +
+                                                      (az1 - az0) * (az1 - az0)) + 3.47f * M;
+        const float Hl = H0 + QS * Dr + dg * sth * 1.01f + m;
+        const float w = NLH * Hl * (1.0f + 0x1p-16f) + 384.0f * m;
+        const float ia = fast_rcp(a);
+        const float s0 = (C0 - w + b) * ia, s1 = (C1 + w + b) * ia;
+        umin = fmaxf(umin, fminf(s0, s1));
+        umax = fminf(umax, fmaxf(s0, s1));
+        okb = !(umin > __builtin_fmaf(fabsf(umax), SL, umax));
+    }
+    if (okb) {
+        // the reported point p' = o + t d, 0 <= t <= best: N . (p' - origin) in
+        // [C0, C1] widened by w0 + w1 t (eta and the tilt over |p' - a| <= Dm + t |d|)
+        const float ke = U * __builtin_fmaf(8.0f * qa, iq, 5.0f) + 1.01f * sth;
+        const float w0 = NLH * __builtin_fmaf(ke, Dm, m) * (1.0f + 0x1p-16f) + 384.0f * m;
+        const float w1 = NLH * ke * dl * (1.0f + 0x1p-16f);
+        const float al = C1 + w0 + b, be = C0 - w0 + b;   // S0 = -b
+        float lo = 0.0f, up = best_s;
+        const float pa = a - w1, pb = a + w1;
+        if (pa > 0.0f)
+            up = fminf(up, al / pa * (1.0f + 0x1p-20f));
+        else if (pa < 0.0f)
+            lo = fmaxf(lo, al / pa * (1.0f - 0x1p-20f));
+        else if (al < 0.0f)
+            lo = INFINITY;
+        if (pb > 0.0f)
+            lo = fmaxf(lo, be / pb * (1.0f - 0x1p-20f));
+        else if (pb < 0.0f)
+            up = fminf(up, be / pb * (1.0f + 0x1p-20f));
+        else if (be > 0.0f)
+            lo = INFINITY;
+        if (!(lo > up))
+            key = fminf(key, lo == lo ? fminf(lo, 3.0e38f) : 0.0f);
+    }
+    return key;
+}
+
 // Closest hit over the wide BVH for the ray (o, d) among hits with t <= hi.  m: box margin
 // (2^-16 (max|o| + scene scale), the leaf-slab margin of kernels.hip leaf_missed).
-// Returns W_MISS (no triangle hits at t <= hi), W_HIT (h = the minimum-t hit, finite and
-// > 0, unique when ties: still to be certified by kdop_certifies on its octree leaf) or
-// W_UNCERT.  Shadow queries (hi = the segment end of kernels.hip is_shadowed, ties false)
-// read only the record's t.  work (optional, 4 entries): {nodes, triangles} added, [2] = the
-// reasons a query is not certified, [3] = loop iterations added.
+// Returns W_MISS (no triangle reports a hit at t <= hi), W_HIT (h = the minimum-t hit, finite
+// and > 0, unique when ties: still to be certified by kdop_certifies on its octree leaf) or
+// W_UNCERT.  Shadow queries (hi = the segment end of kernels.hip is_shadowed, ties false) read
+// only the record's t.  work (optional, 4 entries): {nodes, triangles} added, [2] = the reasons
+// a query is not certified, [3] = loop iterations added.
+//
+// The query is sound for every ray: a child is skipped only when no triangle
+// below it can REPORT a hit (Moller-Trumbore's rounded t, u, v; triangle.cpp:25-91) that the
+// reference could record at t <= the best hit so far.  With q = |cos(n, d)| of a triangle, s =
+// sin(alpha), u = 2^-24 and D >= |o - a| (the node frame's farthest corner):
+//   (a) every reported point p' lies within R = (A + B D) / (1 - B) of its triangle, A = u (30.4 D +
+//       14.4 L) / (q s) + u (4.02 L + 2.01 D), B = 7.21 u / (q s) + 2.01 u (L: the longest edge),
+//       and within eta = u (5 + 8 / s) (2 D + R) of its plane,
+//       which is tilted by theta from the child's slab normal: the child's box widened by R and
+//       its slab widened by eta + R sin(theta) hold p' (q is bounded below by the cone: q >=
+//       cos(phi) - sin(theta) (1 + sin(theta)), phi the angle between N and -d);
+//   (b) for the triangles with q < QS that bound is not used: their reported points can lie
+//       anywhere on their plane, but the origin is then within H0 = 1.01 (QS + 8u) (L + D) / s2 of
+//       that plane (the barycentric numerators must be small), the reference tests such a
+//       triangle only where the line crosses its octree leaf's k-DOP (inside the child box
+//       widened by rho), and p' = o + t d (0 <= t <= best) lies within eta + sin(theta) |p' - a|
+//       of the child's slab.  A child passing all three is entered, keyed by the smallest such t.
+// Robustly back-facing children (the cone) report nothing and are skipped as before.
 template <class Stack>
 RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m, Stack& stk, WHit& h,
-                       uint32_t* work = nullptr, float hi = INFINITY, bool ties = true)
+                       uint32_t* work = nullptr, float hi = INFINITY, bool ties = true, float QS = 0x1p-8f)
 {
     h.t = INFINITY;
     h.u = 1.0f;
     h.v = 0.0f;
     h.k = -1;
-    // slab parameters: t = (lo - (o + m)) / d and (hi - (o - m)) / d over the box widened by m.
+    // slab parameters: t = (lo - (o + M)) / d and (hi - (o - M)) / d over the box widened by M.
     // A direction component below 2^-100 in magnitude (or 0) is treated as +-2^-100: the
     // slab's t range then exceeds 2^70 m / |d| on the far side, far beyond the scene's, so
     // it constrains only as much as the true one does (the margin covers the origin's side).
@@ -301,12 +468,16 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
     const float iy = 1.0f / (fabsf(d.y) < DMIN ? copysignf(DMIN, d.y) : d.y);
     const float iz = 1.0f / (fabsf(d.z) < DMIN ? copysignf(DMIN, d.z) : d.z);
     // per axis, the byte row of the entry (near) planes: q_lo where the direction is positive,
-    // q_hi where it is negative; the near plane is widened by -m sign(d), the far one by +m sign(d)
+    // q_hi where it is negative; the near plane is widened by -M sign(d), the far one by +M sign(d)
     const bool nx_lo = !(ix < 0.0f), ny_lo = !(iy < 0.0f), nz_lo = !(iz < 0.0f);
 
     constexpr float SL = 0x1p-20f;   // relative slack over the rounding of a slab parameter (<= 3 ulp)
+    constexpr float U = 0x1p-24f;
+    constexpr float NLH = 127.9f;    // |N| of a quantised slab normal: 127 +- sqrt(3) / 2 (wbvh.cpp quantise)
     // |d| rounded up (sqrt and dot within 2^-22), times the cone step: threshold = c * cstep
-    const float cstep = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z) * (1.0f + 0x1p-20f) * W_CONE_STEP;
+    const float dl = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z) * (1.0f + 0x1p-20f);
+    const float cstep = dl * W_CONE_STEP;
+    const float icp = (1.0f - 0x1p-18f) / (NLH * dl);   // cos(angle(N, -d)) >= -a icp
     float best_s = hi + fabsf(hi) * SL;   // h.t (or hi) plus slack: a child entered at or below it may hold a hit
     bool tie = false, nanhit = false, infhit = false, overflow = false;
     int sp = 0;
@@ -320,83 +491,108 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
         if (!(cur & W_LEAF)) {
             nn++;
             W_STEP_HOOK(cur, 0);
-            // (reading wave-uniform nodes, about half the steps of the C4 frame, through the
-            // scalar cache instead was measured no faster)
             const uint4* p = reinterpret_cast<const uint4*>(nodes + cur);
-            uint4 R[WN_ROWS];
+            uint4 Rw[WN_ROWS];
 #pragma unroll
             for (int i = 0; i < WN_ROWS; i++)
-                R[i] = ldg(p + i);
+                Rw[i] = ldg(p + i);
             // word i of the node (compile-time i)
             auto wd = [&](int i) -> uint32_t {
-                const uint4 r = R[i >> 2];
+                const uint4 r = Rw[i >> 2];
                 return (i & 3) == 0 ? r.x : (i & 3) == 1 ? r.y : (i & 3) == 2 ? r.z : r.w;
             };
-            const float m3 = 384.0f * m;   // |N|_1 <= 3 * 128: the spatial margin in slab units
-            const float ss = bitsf(wd(WN_SS)), slo_lo = bitsf(wd(WN_SS + 1)) - m3, slo_hi = bitsf(wd(WN_SS + 1)) + m3;
+            const float ss = bitsf(wd(WN_SS)), slo = bitsf(wd(WN_SS + 1));
             const uint32_t ex = wd(3);
-            // t of a plane origin + q s (widened by m) = q (s / d) + (origin -+ m - o) / d
-            const float sx = bitsf((ex & 0xffu) << 23) * ix, sy = bitsf(((ex >> 8) & 0xffu) << 23) * iy,
-                        sz = bitsf(((ex >> 16) & 0xffu) << 23) * iz;
-            // origin - o per axis, then the planes widened by m on either side (no per-ray
-            // widened origins kept live: they would hold six registers through the loop).
-            // Near plane of axis a: t = q_near s_a / d_a + (origin_a - o_a -+ m) / d_a, with the
-            // byte row and the sign of m chosen by the direction's sign (the same products as
-            // testing both planes and ordering them by min / max)
+            const float stx = bitsf((ex & 0xffu) << 23), sty = bitsf(((ex >> 8) & 0xffu) << 23),
+                        stz = bitsf(((ex >> 16) & 0xffu) << 23);
+            // t of a plane origin + q s (widened by M) = q (s / d) + (origin - o -+ M) / d
+            const float sx = stx * ix, sy = sty * iy, sz = stz * iz;
             const float Dx = bitsf(wd(0)) - o.x, Dy = bitsf(wd(1)) - o.y, Dz = bitsf(wd(2)) - o.z;
-            const float mx = nx_lo ? m : -m, my = ny_lo ? m : -m, mz = nz_lo ? m : -m;
-            const float ax = (Dx - mx) * ix, ay = (Dy - my) * iy, az = (Dz - mz) * iz;
-            const float bx = (Dx + mx) * ix, by = (Dy + my) * iy, bz = (Dz + mz) * iz;
+            // D: o to the farthest corner of the node's frame [origin, origin + 255 step]
+            float Dn;
+            {
+                const float fx = fmaxf(fabsf(Dx), fabsf(__builtin_fmaf(255.0f, stx, Dx)));
+                const float fy = fmaxf(fabsf(Dy), fabsf(__builtin_fmaf(255.0f, sty, Dy)));
+                const float fz = fmaxf(fabsf(Dz), fabsf(__builtin_fmaf(255.0f, stz, Dz)));
+                Dn = sqrtf(fx * fx + fy * fy + fz * fz) * (1.0f + 0x1p-16f) + m;
+            }
+            const float RA = U * 30.4f * Dn, RB = U * 2.01f * Dn;
             constexpr int QW = W_WIDTH / 4;   // words per axis row of quantised planes
             float key[W_WIDTH];
             uint32_t ref[W_WIDTH];
 #pragma unroll
             for (int j = 0; j < W_WIDTH; j++) {
                 const int sh = 8 * (j & 3), jw = j >> 2;
-                const uint32_t lx = wd(WN_QLO + 0 * QW + jw), hx = wd(WN_QHI + 0 * QW + jw);
-                const uint32_t ly = wd(WN_QLO + 1 * QW + jw), hy = wd(WN_QHI + 1 * QW + jw);
-                const uint32_t lz = wd(WN_QLO + 2 * QW + jw), hz = wd(WN_QHI + 2 * QW + jw);
-                const uint32_t nqx = nx_lo ? lx : hx, fqx = nx_lo ? hx : lx;
-                const uint32_t nqy = ny_lo ? ly : hy, fqy = ny_lo ? hy : ly;
-                const uint32_t nqz = nz_lo ? lz : hz, fqz = nz_lo ? hz : lz;
                 const uint32_t chj = wd(WN_CHILD + j);
-                const float tnx = __builtin_fmaf((float)((nqx >> sh) & 0xffu), sx, ax);
-                const float tny = __builtin_fmaf((float)((nqy >> sh) & 0xffu), sy, ay);
-                const float tnz = __builtin_fmaf((float)((nqz >> sh) & 0xffu), sz, az);
-                const float tfx = __builtin_fmaf((float)((fqx >> sh) & 0xffu), sx, bx);
-                const float tfy = __builtin_fmaf((float)((fqy >> sh) & 0xffu), sy, by);
-                const float tfz = __builtin_fmaf((float)((fqz >> sh) & 0xffu), sz, bz);
-                float tmin = fmaxf(fmaxf(tnx, tny), tnz);
-                float tmax = fminf(fminf(tfx, tfy), tfz);
-                // enter when max(tmin, 0) <= min(tmax (1 + SL), best_s); a NaN tmin (every
-                // slab NaN) enters too.  The key orders the children; misses get INFINITY.
-                bool ok = chj != W_EMPTY &&
-                          fmaxf(tmin, 0.0f) <= fminf(__builtin_fmaf(fabsf(tmax), SL, tmax), best_s);
-                // the slab (and cone) only narrow the box's interval, so a child whose box
-                // fails is out already: when no lane's box passes, the wave skips this part
-                if (ok) {
-                    // N . (o + t d - origin) in [c0, c1] widened by m3 >= |N|_1 m: t between
-                    // (c0 - m3 + b) / a and (c1 + m3 + b) / a, b = N . (origin - o), a = N . d
-                    const uint32_t nrj = wd(WN_NRM + j), sbj = wd(WN_SLAB + j);
-                    const float nx = (float)(int8_t)(nrj & 0xffu), ny = (float)(int8_t)((nrj >> 8) & 0xffu),
-                                nz = (float)(int8_t)((nrj >> 16) & 0xffu);
-                    const float a = nx * d.x + ny * d.y + nz * d.z;
-                    const float b = nx * Dx + ny * Dy + nz * Dz;
-                    // the hardware reciprocal (1 ulp): its error moves the slab's t by a relative
-                    // 2^-23, a distance far inside the margin m3 over the scene
-                    const float ia = fast_rcp(a);
-                    const float c0 = __builtin_fmaf((float)(sbj & 0xffffu), ss, slo_lo) + b;
-                    const float c1 = __builtin_fmaf((float)(sbj >> 16), ss, slo_hi) + b;
-                    const float s0 = c0 * ia, s1 = c1 * ia;
-                    tmin = fmaxf(tmin, fminf(s0, s1));
-                    tmax = fminf(tmax, fmaxf(s0, s1));
-                    ok = fmaxf(tmin, 0.0f) <= fminf(__builtin_fmaf(fabsf(tmax), SL, tmax), best_s);
-                    // every triangle below faces away when a exceeds the threshold (rounding of
-                    // a and of the threshold: < 1e-4 |d|, inside the build's 0.01 |d|)
-                    ok = ok && !(a > (float)(nrj >> 24) * cstep);
-                }
-                key[j] = ok ? fminf(fmaxf(tmin, 0.0f), 3.0e38f) : INFINITY;
                 ref[j] = chj;
+                key[j] = INFINITY;
+                const uint32_t nrj = wd(WN_NRM + j);
+                const float nx = (float)(int8_t)(nrj & 0xffu), ny = (float)(int8_t)((nrj >> 8) & 0xffu),
+                            nz = (float)(int8_t)((nrj >> 16) & 0xffu);
+                const float a = nx * d.x + ny * d.y + nz * d.z;
+                // every triangle below faces away when a exceeds the cone threshold (rounding of
+                // a and of the threshold: < 1e-4 |d|, inside the build's 0.01 |d|): none reports a hit
+                if (chj != W_EMPTY && !(a > (float)(nrj >> 24) * cstep)) {
+                    const uint32_t e = wd(WN_EXT + j);
+                    const float smin = wq_val(e & 0xffu, WQ_UNIT);
+                    const float sth = wq_val((e >> 16) & 0xffu, WQ_UNIT);
+                    const float L = wq_len(e >> 24);
+                    const float qlb = __builtin_fmaf(-sth, 1.0f + sth, -a * icp) - 0x1p-20f;
+                    const float qa = fmaxf(qlb, QS);
+                    // (a): the box widened by R, the slab by eta + R sin(theta)
+                    // R = (A + B D) / (1 - B) with |p' - o| <= D + R folded in: A = u (30.4 D + 14.4 L) /
+                    // (q s) + u (4.02 L + 2.01 D), B = 7.21 u / (q s) + 2.01 u; 1 / (1 - B) <= 1 + 2 B for
+                    // B <= 1/2 (beyond: no bound)
+                    const float iq = fast_rcp(qa * smin) * (1.0f + 0x1p-18f);
+                    const float Bq = __builtin_fmaf(7.21f * U, iq, 2.01f * U);
+                    const float Aq = __builtin_fmaf(__builtin_fmaf(14.4f * U, L, RA), iq, __builtin_fmaf(4.02f * U, L, RB));
+                    const float R = !(Bq <= 0.5f) ? INFINITY
+                                                  : __builtin_fmaf(Bq, Dn, Aq) * __builtin_fmaf(2.0f, Bq, 1.0f) * (1.0f + 0x1p-16f) + m;
+                    const uint32_t lx = wd(WN_QLO + 0 * QW + jw), hx = wd(WN_QHI + 0 * QW + jw);
+                    const uint32_t ly = wd(WN_QLO + 1 * QW + jw), hy = wd(WN_QHI + 1 * QW + jw);
+                    const uint32_t lz = wd(WN_QLO + 2 * QW + jw), hz = wd(WN_QHI + 2 * QW + jw);
+                    const float qlx = (float)((lx >> sh) & 0xffu), qhx = (float)((hx >> sh) & 0xffu);
+                    const float qly = (float)((ly >> sh) & 0xffu), qhy = (float)((hy >> sh) & 0xffu);
+                    const float qlz = (float)((lz >> sh) & 0xffu), qhz = (float)((hz >> sh) & 0xffu);
+                    auto box = [&](float M, float& tmin, float& tmax) {
+                        const float mx = nx_lo ? M : -M, my = ny_lo ? M : -M, mz = nz_lo ? M : -M;
+                        const float tnx = __builtin_fmaf(nx_lo ? qlx : qhx, sx, (Dx - mx) * ix);
+                        const float tny = __builtin_fmaf(ny_lo ? qly : qhy, sy, (Dy - my) * iy);
+                        const float tnz = __builtin_fmaf(nz_lo ? qlz : qhz, sz, (Dz - mz) * iz);
+                        const float tfx = __builtin_fmaf(nx_lo ? qhx : qlx, sx, (Dx + mx) * ix);
+                        const float tfy = __builtin_fmaf(ny_lo ? qhy : qly, sy, (Dy + my) * iy);
+                        const float tfz = __builtin_fmaf(nz_lo ? qhz : qlz, sz, (Dz + mz) * iz);
+                        tmin = fmaxf(fmaxf(tnx, tny), tnz);
+                        tmax = fminf(fminf(tfx, tfy), tfz);
+                    };
+                    const uint32_t sbj = wd(WN_SLAB + j);
+                    const float C0 = __builtin_fmaf((float)(sbj & 0xffffu), ss, slo);
+                    const float C1 = __builtin_fmaf((float)(sbj >> 16), ss, slo);
+                    const float b = nx * Dx + ny * Dy + nz * Dz;   // N . (origin - o)
+                    float tmin, tmax;
+                    box(R, tmin, tmax);
+                    // enter when max(tmin, 0) <= min(tmax (1 + SL), best_s); a NaN tmin (every
+                    // slab NaN) enters too.  The key orders the children; misses get INFINITY.
+                    bool ok = fmaxf(tmin, 0.0f) <= fminf(__builtin_fmaf(fabsf(tmax), SL, tmax), best_s);
+                    // the slab only narrows the box's interval: skipped when no lane's box passes
+                    if (ok && R < INFINITY) {
+                        // N . (o + t d - origin) in [C0, C1] widened by w: t between
+                        // (C0 - w + b) / a and (C1 + w + b) / a
+                        const float eta = U * __builtin_fmaf(8.0f * qa, iq, 5.0f) * __builtin_fmaf(2.0f, Dn, R);
+                        const float w = NLH * __builtin_fmaf(R, sth, eta) * (1.0f + 0x1p-16f) + 384.0f * m;
+                        // the hardware reciprocal (1 ulp): its error moves the slab's t by a relative
+                        // 2^-23, a distance far inside the margin over the scene
+                        const float ia = fast_rcp(a);
+                        const float s0 = (C0 - w + b) * ia, s1 = (C1 + w + b) * ia;
+                        tmin = fmaxf(tmin, fminf(s0, s1));
+                        tmax = fminf(tmax, fmaxf(s0, s1));
+                        ok = fmaxf(tmin, 0.0f) <= fminf(__builtin_fmaf(fabsf(tmax), SL, tmax), best_s);
+                    }
+                    if (ok)
+                        key[j] = fminf(fmaxf(tmin, 0.0f), 3.0e38f);
+                    if (qlb < QS)   // (b): triangles that may lie nearly parallel to d
+                        key[j] = fminf(key[j], wq_case_b(nodes + cur, j, o, d, ix, iy, iz, m, QS, dl, best_s, a, qa, iq));
+                }
 #if defined(__HIP_DEVICE_COMPILE__)
                 // one child at a time: the scheduler would interleave the children's
                 // temporaries (VALU latency is hidden by the other waves anyway)

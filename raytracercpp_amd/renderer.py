@@ -290,6 +290,8 @@ class Renderer:
         """BVH::intersect for a batch of rays -> (tri_id, t, u, v, ret)."""
         o = f32(orig).reshape(-1, 3)
         d = f32(dirs).reshape(-1, 3)
+        if d.shape != o.shape:
+            raise ValueError(f"trace_rays: {o.shape[0]} origins but {d.shape[0]} directions")
         n = o.shape[0]
         ids = np.zeros(n, np.int32)
         t, u, v = np.zeros(n, np.float32), np.zeros(n, np.float32), np.zeros(n, np.float32)
@@ -303,6 +305,8 @@ class Renderer:
         -> (rgba [n,4], hit_src, t, intersection_found, shadowed)."""
         o = f32(orig).reshape(-1, 3)
         d = f32(dirs).reshape(-1, 3)
+        if d.shape != o.shape:
+            raise ValueError(f"trace_ray: {o.shape[0]} origins but {d.shape[0]} directions")
         n = o.shape[0]
         rgba = np.zeros((n, 4), np.float32)
         src = np.zeros(n, np.int32)

@@ -841,7 +841,7 @@ def test_set_devices_bands_match_one_device(make_renderer, n):
     R.load_scene(sc, st)
     R.set_devices([0] * n)
     rw, rh = st.render_size()
-    for step in range(3):
+    for step in range(4):
         if step == 1:
             R.set_light_position((1.0, 4.0, 3.0))
             sc.light = np.asarray((1.0, 4.0, 3.0), np.float32)
@@ -851,13 +851,45 @@ def test_set_devices_bands_match_one_device(make_renderer, n):
             sc.materials[0, 0] = 0.2
             R.set_materials(sc.materials)
             R.set_triangles(sc.tri, sc.tri_mat, sc.tri_uv)
+        if step == 3:
+            R.finish_accel()   # the helpers then copy the lead's cones / slabs and wide BVH
         render(R)
         multi = R.get_image().ravel().copy()
         o = Oracle(sc, st).render_rows()
         assert np.array_equal(multi, Oracle.downscale(o.argb, rw, rh, 2)), f"step {step}"
+        # one host octree build per geometry change for all n devices (the helpers copy the
+        # lead's device tables; reference renderer.cpp:214-224 rebuilds once)
+        assert R.stats()["host_builds"] == (1 if step < 2 else 2), (step, R.stats()["host_builds"])
     R.set_devices([])
     render(R)
     assert np.array_equal(R.get_image().ravel(), multi)
+
+
+@pytest.mark.gpu
+def test_set_devices_first_frame_after_geometry_change(make_renderer):
+    """rt_set_devices with 3 renderers: the frame right after set_triangles costs about the
+    one-device first frame (one build; the helpers copy the lead's tables), not three builds."""
+    import time
+    from raytracercpp_amd import scenes
+    from raytracercpp_amd.renderer import render
+    sc, st = scenes.sphere1m(width=320, height=180)
+    times = {}
+    for n in (1, 3):
+        R = make_renderer()
+        R.load_scene(sc, st)
+        if n > 1:
+            R.set_devices([0] * n)
+        render(R)
+        R.finish_accel()
+        render(R)
+        tri = (sc.tri * np.float32(1.01)).astype(np.float32)
+        R.set_triangles(tri, sc.tri_mat, sc.tri_uv)
+        t0 = time.perf_counter()
+        render(R)
+        times[n] = time.perf_counter() - t0
+        assert R.stats()["host_builds"] == 2
+    print("first frame after a geometry change:", times)
+    assert times[3] < 1.6 * times[1] + 0.02, times
 
 
 def test_async_accel_frames(make_renderer):
@@ -937,3 +969,57 @@ def test_band_counters_across_self_resetting_launches(R):
         if first is None:
             first = img.copy()
         assert np.array_equal(img, first), i
+
+
+@pytest.mark.parametrize("ssaa", [False, True])
+def test_failed_frame_keeps_the_previous_image(make_renderer, ssaa):
+    """A frame that fails after its image became the internal buffer (RT_INJECT_FRAME_FAIL: the
+    2nd ray_trace) is never presented: with SSAA the previous (downscaled) image stays; without,
+    the internal buffer was reused, so the image reads as not rendered (background)."""
+    from raytracercpp_amd import scenes
+    from raytracercpp_amd._lib import RtError
+    R = make_renderer(RT_INJECT_FRAME_FAIL="2")
+    sc, st = scenes.bumpy70k(width=96, height=54, enable_ssaa=ssaa, ssaa_factor=2)
+    R.load_scene(sc, st)
+    R.ray_trace()
+    R.post_process()
+    first = R.get_image().copy()
+    with pytest.raises(RtError):
+        R.ray_trace()
+    after = R.get_image()
+    if ssaa:
+        assert after.shape == first.shape and np.array_equal(after, first)
+    else:
+        bg = np.uint32(0xFF87CEEB)
+        assert (after.ravel().view(np.uint32) == bg).all()
+    R.ray_trace()   # the next frame renders normally
+    R.post_process()
+    assert np.array_equal(R.get_image(), first)
+
+
+def test_set_devices_distinct_rccl(make_renderer):
+    """The RCCL send / receive path of rt_set_devices (distinct devices, RT_MULTIDEV_RCCL=1):
+    frames equal the one-device frame.  Needs two or more devices (skipped on one-GPU boxes);
+    without the switch distinct devices are refused (experimental, include/rt_mi355x.h)."""
+    import os
+    import torch
+    from raytracercpp_amd import scenes
+    from raytracercpp_amd.renderer import render
+    from raytracercpp_amd._lib import RtError
+    n = torch.cuda.device_count()
+    sc, st = scenes.bumpy70k(width=200, height=117, enable_ssaa=True, ssaa_factor=2)
+    if n < 2:
+        R = make_renderer()
+        R.load_scene(sc, st)
+        with pytest.raises(RtError):
+            R.set_devices([0, 0, 0][:1] + [1])   # a second device id that does not exist here
+        pytest.skip("one device: the RCCL path needs two or more")
+    R1 = make_renderer()
+    R1.load_scene(sc, st)
+    render(R1)
+    one = R1.get_image().copy()
+    R = make_renderer(RT_MULTIDEV_RCCL="1")
+    R.load_scene(sc, st)
+    R.set_devices(list(range(min(n, 4))))
+    render(R)
+    assert np.array_equal(R.get_image(), one)

@@ -99,3 +99,15 @@ def test_strip_assemble_roundtrip():
             p[g >= 0] = img[g[g >= 0]]
             parts.append(p)
         assert np.array_equal(strips.assemble(parts, 37, band), img)
+
+
+def test_trace_ray_rejects_mismatched_rays():
+    """Renderer.trace_ray / trace_rays refuse origin and direction arrays of different lengths
+    before the C call (rt_trace_ray copies n rays from each buffer)."""
+    import pytest as _pt
+    from raytracercpp_amd.renderer import Renderer
+    o = np.zeros((4, 3), np.float32)
+    d = np.zeros((3, 3), np.float32)
+    for f in (Renderer.trace_ray, Renderer.trace_rays):
+        with _pt.raises(ValueError):
+            f(None, o, d)

@@ -182,28 +182,82 @@ def grazing_q(tri, ids, d):
     return np.abs((n * dd).sum(1)) / (np.linalg.norm(ab, axis=1) * np.linalg.norm(ac, axis=1) * np.linalg.norm(dd, axis=1))
 
 
-def test_grazing_residual_is_confined_to_grazing_triangles():
-    """The default certificate's residual, measured on the adversarial case:
-    Moller-Trumbore can report a hit far outside its triangle's box when the ray nearly lies in
-    the triangle's plane, which the wide BVH's box margin does not cover.  Certified answers that
-    differ from the oracle occur only there: the reference's recorded triangle then has
-    Q < 0.2 (the margin covers every hit of a triangle with Q >= 0.2).  Exact mode
-    (rt_set_exact; rt_trace_rays) walks the octree like the reference and has no residual
-    (tests/test_gpu_parity.py test_exact_mode_on_grazing_plane)."""
+def _grazing_differences(tri, o, d):
+    """(certified fraction, number of certified answers that differ from the oracle's BVH::intersect)"""
     from raytracercpp_amd.scene import RenderSettings
     import dataclasses
-    tri, o, d = grazing_plane_case()
     status, ids, t, u, v, stats, _ = _lib.wbvh_query(tri, o, d, 12, 40)
     assert stats["violations"] == 0
     base, _ = scenes.robot1080(width=8, height=8)
-    sc = dataclasses.replace(base, tri=tri, tri_mat=np.zeros(len(tri), np.int32), tri_uv=None)
+    sc = dataclasses.replace(base, tri=np.ascontiguousarray(tri, np.float32), tri_mat=np.zeros(len(tri), np.int32),
+                             tri_uv=None)
     oi, ot, ou, ov, orr, _ = Oracle(sc, RenderSettings(bvh_max_depth=12, bvh_leaf_object_count=40)).bvh_query(o, d)
     cert = status != 2
     bad = cert & ((status == 1) != (orr != 0))
     hit = (status == 1) & (orr != 0)
-    bad |= hit & ((ids != oi) | (bits(t) != bits(ot)))
-    print(f"grazing plane: {cert.mean():.4f} certified, {int(bad.sum())} of {len(o)} certified answers differ")
-    # the reference recorded a hit on a grazing triangle in every differing case
-    assert (orr[bad] != 0).all()
-    q = grazing_q(tri, oi[bad], d[bad])
-    assert (q < 0.2).all(), q.max()
+    bad |= hit & ((ids != oi) | (bits(t) != bits(ot)) | (bits(u) != bits(ou)) | (bits(v) != bits(ov)))
+    return float(cert.mean()), int(bad.sum())
+
+
+@pytest.mark.parametrize("seed,sin_lo,sin_hi", [(99, 1e-7, 1e-3), (5, 1e-9, 1e-5), (17, 1e-5, 1e-1)])
+def test_grazing_plane_certified_answers_match_oracle(seed, sin_lo, sin_hi):
+    """The adversarial input of DESIGN.md 5.6: a tessellated plane and rays that meet it at
+    grazing angles, where Moller-Trumbore reports hits far outside a triangle's box (r03 measured
+    131 of 20,000 certified answers differing with the r02 query).  The query's child test bounds
+    every point Moller-Trumbore can report (wbvh.hpp wbvh_closest), so every certified answer is
+    the reference's; what it cannot bound it leaves uncertified (the exact octree traversal)."""
+    tri, o, d = grazing_plane_case(seed=seed, sin_lo=sin_lo, sin_hi=sin_hi)
+    cert, bad = _grazing_differences(tri, o, d)
+    print(f"grazing plane seed {seed}: {cert:.4f} certified, {bad} certified answers differ")
+    assert bad == 0
+
+
+def grazing_sphere_case(seed=3, n_rays=20000):
+    """Rays nearly tangent to a 1M-triangle-class tessellated sphere (a smaller UV sphere here):
+    silhouette rays at 1e-8 .. 1e-2 of the radius from tangency, from inside and outside the
+    scene box."""
+    rng = np.random.default_rng(seed)
+    sc, _ = scenes.bumpy70k(width=8, height=8)
+    tri = sc.tri
+    T = tri.reshape(-1, 3, 3).astype(np.float64)
+    c = T.reshape(-1, 3).mean(0)
+    k = rng.integers(0, len(T), n_rays)
+    p = T[k].mean(1)
+    n = np.cross(T[k, 1] - T[k, 0], T[k, 2] - T[k, 0])
+    n /= np.linalg.norm(n, axis=1, keepdims=True)
+    t1 = np.cross(n, rng.standard_normal((n_rays, 3)))
+    t1 /= np.linalg.norm(t1, axis=1, keepdims=True)
+    eps = np.exp(rng.uniform(np.log(1e-8), np.log(1e-2), n_rays))
+    d = t1 + n * (eps * rng.choice([-1, 1], n_rays))[:, None]
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    o = p - d * rng.uniform(0.5, 4.0, n_rays)[:, None] + n * (eps * rng.uniform(0, 1, n_rays))[:, None]
+    return tri, o.astype(np.float32), d.astype(np.float32)
+
+
+def test_grazing_sphere_certified_answers_match_oracle():
+    tri, o, d = grazing_sphere_case()
+    cert, bad = _grazing_differences(tri, o, d)
+    print(f"grazing sphere: {cert:.4f} certified, {bad} certified answers differ")
+    assert bad == 0
+    assert cert > 0.5
+
+
+def test_grazing_sliver_soup_certified_answers_match_oracle():
+    """Slivers and degenerate triangles (the soup scene) hit at grazing angles: rays in the plane
+    of a random sliver, offset by 1e-7 .. 1e-3."""
+    rng = np.random.default_rng(11)
+    tri = _soup(rng)
+    T = tri.reshape(-1, 3, 3).astype(np.float64)
+    k = rng.integers(0, len(T), 20000)
+    n = np.cross(T[k, 1] - T[k, 0], T[k, 2] - T[k, 0])
+    ok = np.linalg.norm(n, axis=1) > 1e-12
+    k, n = k[ok], n[ok] / np.linalg.norm(n[ok], axis=1, keepdims=True)
+    e = T[k, 1] - T[k, 0]
+    e /= np.maximum(np.linalg.norm(e, axis=1, keepdims=True), 1e-30)
+    eps = np.exp(rng.uniform(np.log(1e-7), np.log(1e-3), len(k)))
+    d = e + n * eps[:, None]
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    o = T[k].mean(1) - d * rng.uniform(0.2, 2.0, len(k))[:, None] + n * (eps * rng.uniform(-1, 1, len(k)))[:, None]
+    cert, bad = _grazing_differences(tri, o.astype(np.float32), d.astype(np.float32))
+    print(f"grazing slivers: {cert:.4f} certified, {bad} certified answers differ")
+    assert bad == 0

@@ -1,19 +1,21 @@
 #!/bin/bash
 # Runs on the GPU box: kernel-trace stats + PMC passes (one rocprofv3 run per pass,
 # counters never combined with sys/runtime traces) of bench.py.
-# Usage: bash tools/profile_gpu.sh <tag>   -> gpurun_out/prof_<tag>/...
+# Usage: bash tools/profile_gpu.sh <tag> [bench args...]   -> gpurun_out/prof_<tag>/...
+#   e.g. bash tools/profile_gpu.sh r04c5 --config sphere1m_refl
 set -u
 TAG=${1:-r01}
+shift || true
+EXTRA="$*"
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-B="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
-    $B > $OUT/trace.log 2>&1 || exit 1
+    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-check $EXTRA > $OUT/trace.log 2>&1 || exit 1
 pass() {   # pass <name> <counters...>
     local name=$1; shift
     timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d $OUT/pmc_$name -o run -- \
-        python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/pmc_$name.log 2>&1
+        python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-check $EXTRA > $OUT/pmc_$name.log 2>&1
 }
 pass fetch FETCH_SIZE || exit 2
 pass write WRITE_SIZE || exit 3
