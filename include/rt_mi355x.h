@@ -364,6 +364,16 @@ int rt_octree_digest(const float *tri9, int64_t n, int32_t max_depth, int32_t le
 int rt_wbvh_query(const float *tri9, int64_t n, int32_t max_depth, int32_t leaf_max_obj_count, const float *orig,
                   const float *dir, int64_t nrays, int32_t *status, int32_t *id, float *t, float *u, float *v,
                   int64_t stats[8], float *ms);
+/* The same with the frame's grazing-risk bits of a camera and / or a light point:
+ * rays whose origin equals cam (bitwise) read the camera's bits; with shadow_rays = 1 (light
+ * required) each ray is given as (hit point p in orig, normal n in dir) and becomes is_shadowed's
+ * ray o = p + 1e-4 n, d = normalize(light - p) (renderer.cpp:340-402), reading the light's bits when
+ * its segment bound allows, and is answered as a closest-hit query over the whole line.  o_out /
+ * d_out (optional, 3 floats per ray) receive the rays queried. */
+int rt_wbvh_query_ex(const float *tri9, int64_t n, int32_t max_depth, int32_t leaf_max_obj_count, const float *orig,
+                     const float *dir, int64_t nrays, const float *cam, const float *light, int32_t shadow_rays,
+                     float *o_out, float *d_out, int32_t *status, int32_t *id, float *t, float *u, float *v,
+                     int64_t stats[8], float *ms);
 
 #ifdef __cplusplus
 }

@@ -135,6 +135,8 @@ SIGNATURES = {
     "rt_debug_read": (C.c_int, [_H, C.POINTER(C.c_uint64), C.c_int64]),
     "rt_wbvh_query": (C.c_int, [_f32p, C.c_int64, C.c_int32, C.c_int32, _f32p, _f32p, C.c_int64, _i32p, _i32p, _f32p,
                                 _f32p, _f32p, _i64p, _f32p]),
+    "rt_wbvh_query_ex": (C.c_int, [_f32p, C.c_int64, C.c_int32, C.c_int32, _f32p, _f32p, C.c_int64, _f32p, _f32p,
+                                   C.c_int32, _f32p, _f32p, _i32p, _i32p, _f32p, _f32p, _f32p, _i64p, _f32p]),
 }
 
 _lib = None
@@ -251,10 +253,12 @@ def load_obj(path, xform, mat_offset=0):
         L.rt_obj_close(h)
 
 
-def wbvh_query(tri9, orig, dirs, max_depth=12, leaf=40):
-    """rt_wbvh_query: the wide-BVH certified closest hit on the host (no GPU).  Returns
+def wbvh_query(tri9, orig, dirs, max_depth=12, leaf=40, cam=None, light=None, shadow_rays=False, rays_out=False):
+    """rt_wbvh_query(_ex): the wide-BVH certified closest hit on the host (no GPU).  Returns
     (status, id, t, u, v, stats dict, (octree ms, wide-BVH ms)); status 0 certified miss,
-    1 certified hit, 2 not certified."""
+    1 certified hit, 2 not certified.  cam / light: the frame's grazing-risk points (rays from cam
+    read the camera's bits); shadow_rays: orig / dirs are hit points and normals, traced as
+    is_shadowed's rays towards light.  rays_out: (o, d) of the queried rays are appended."""
     tri9 = f32(tri9).reshape(-1, 9)
     o = f32(orig).reshape(-1, 3)
     d = f32(dirs).reshape(-1, 3)
@@ -264,11 +268,18 @@ def wbvh_query(tri9, orig, dirs, max_depth=12, leaf=40):
     t, u, v = (np.zeros(n, np.float32) for _ in range(3))
     stats = np.zeros(8, np.int64)
     ms = np.zeros(2, np.float32)
-    check(lib().rt_wbvh_query(ptr(tri9, _f32p), tri9.shape[0], max_depth, leaf, ptr(o, _f32p), ptr(d, _f32p), n,
-                              ptr(st, _i32p), ptr(ids, _i32p), ptr(t, _f32p), ptr(u, _f32p), ptr(v, _f32p),
-                              ptr(stats, _i64p), ptr(ms, _f32p)), "rt_wbvh_query")
+    oo = np.zeros((n, 3), np.float32)
+    do = np.zeros((n, 3), np.float32)
+    c = None if cam is None else f32(cam).reshape(3)
+    li = None if light is None else f32(light).reshape(3)
+    check(lib().rt_wbvh_query_ex(ptr(tri9, _f32p), tri9.shape[0], max_depth, leaf, ptr(o, _f32p), ptr(d, _f32p), n,
+                                 None if c is None else ptr(c, _f32p), None if li is None else ptr(li, _f32p),
+                                 1 if shadow_rays else 0, ptr(oo, _f32p), ptr(do, _f32p),
+                                 ptr(st, _i32p), ptr(ids, _i32p), ptr(t, _f32p), ptr(u, _f32p), ptr(v, _f32p),
+                                 ptr(stats, _i64p), ptr(ms, _f32p)), "rt_wbvh_query")
     keys = ("nodes", "leaves", "max_leaf", "depth", "node_visits", "tri_tests", "violations", "sah_x1000")
-    return st, ids, t, u, v, dict(zip(keys, map(int, stats))), (float(ms[0]), float(ms[1]))
+    out = (st, ids, t, u, v, dict(zip(keys, map(int, stats))), (float(ms[0]), float(ms[1])))
+    return out + (oo, do) if rays_out else out
 
 
 def octree_digest(tri9, max_depth=12, leaf=40, builder=0):

@@ -466,7 +466,17 @@ int rt_wbvh_query(const float* tri9, int64_t n, int32_t max_depth, int32_t leaf_
                   const float* dir, int64_t nrays, int32_t* status, int32_t* id, float* t, float* u, float* v,
                   int64_t stats[8], float* ms)
 {
-    if (n < 0 || (n > 0 && !tri9) || nrays < 0 || (nrays > 0 && (!orig || !dir || !status || !id || !t || !u || !v)))
+    return rt_wbvh_query_ex(tri9, n, max_depth, leaf_max_obj_count, orig, dir, nrays, nullptr, nullptr, 0, nullptr,
+                            nullptr, status, id, t, u, v, stats, ms);
+}
+
+int rt_wbvh_query_ex(const float* tri9, int64_t n, int32_t max_depth, int32_t leaf_max_obj_count, const float* orig,
+                     const float* dir, int64_t nrays, const float* cam, const float* light, int32_t shadow_rays,
+                     float* o_out, float* d_out, int32_t* status, int32_t* id, float* t, float* u, float* v,
+                     int64_t stats[8], float* ms)
+{
+    if (n < 0 || (n > 0 && !tri9) || nrays < 0 || (nrays > 0 && (!orig || !dir || !status || !id || !t || !u || !v)) ||
+        (shadow_rays && !light))
         return bad("rt_wbvh_query: bad arguments");
     try {
         rt::FlatOctree f;
@@ -484,6 +494,20 @@ int rt_wbvh_query(const float* tri9, int64_t n, int32_t max_depth, int32_t leaf_
             for (int a = 0; a < 3; a++)
                 S = std::max(S, std::max(std::fabs(f.nodes[0].dn[a]), std::fabs(f.nodes[0].df[a])));
         const bool usable = !w.nodes.empty() && S > 0x1p-20f && S < 0x1p20f;
+        // the risk bits of the camera / light (renderer.cpp prepare_risk, kernels.hip wide_risk_kernel)
+        std::vector<uint32_t> risk;
+        rt::WRiskArgs RA{};
+        if (usable && (cam || light)) {
+            const float lo[3] = {f.nodes[0].dn[0], f.nodes[0].dn[1], f.nodes[0].dn[2]};
+            const float hi[3] = {f.nodes[0].df[0], f.nodes[0].df[1], f.nodes[0].df[2]};
+            const float zero[3] = {0, 0, 0};
+            RA = rt::wbvh_risk_args(lo, hi, S, cam ? cam : zero, light ? light : zero, W_QS_CLOSEST, W_QS_SHADOW);
+            risk.assign(w.nodes.size(), 0u);
+            if (cam)
+                rt::wbvh_risk_host(w, RA, 0, risk);
+            if (light)
+                rt::wbvh_risk_host(w, RA, 1, risk);
+        }
         std::atomic<int64_t> work_n{0}, work_t{0};
         auto body = [&](int64_t b, int64_t e) {
             rt::WStackLocal stk;
@@ -491,6 +515,31 @@ int rt_wbvh_query(const float* tri9, int64_t n, int32_t max_depth, int32_t leaf_
             for (int64_t i = b; i < e; i++) {
                 rt::v3 o = rt::mk(orig[3 * i], orig[3 * i + 1], orig[3 * i + 2]);
                 rt::v3 d = rt::mk(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]);
+                const uint32_t* rk = nullptr;
+                int rsel = 0;
+                if (shadow_rays) {
+                    // is_shadowed's ray (kernels.hip): orig = the hit point p, dir = its normal n
+                    const rt::v3 p = o, nrm = d, lp = rt::mk(light[0], light[1], light[2]);
+                    o = p + nrm * 1.0e-4f;
+                    d = rt::normalize(lp - p);
+                    const float nl = std::fabs(nrm.x) + std::fabs(nrm.y) + std::fabs(nrm.z);
+                    const float hi = (std::sqrt(rt::length2(p - lp)) + 1.0e-4f * nl) * (1.0f + 0x1p-10f);
+                    if (!risk.empty() && hi <= RA.ray_G && nl <= RA.ray_nl) {
+                        rk = risk.data();
+                        rsel = 1;
+                    }
+                } else if (!risk.empty() && cam && o.x == cam[0] && o.y == cam[1] && o.z == cam[2])
+                    rk = risk.data();
+                if (o_out) {
+                    o_out[3 * i] = o.x;
+                    o_out[3 * i + 1] = o.y;
+                    o_out[3 * i + 2] = o.z;
+                }
+                if (d_out) {
+                    d_out[3 * i] = d.x;
+                    d_out[3 * i + 1] = d.y;
+                    d_out[3 * i + 2] = d.z;
+                }
                 bool nan = false;
                 for (int p = 0; p < rt::NPLANES; p++) {
                     rt::v3 pn = rt::mk(rt::PLANE_N[p][0], rt::PLANE_N[p][1], rt::PLANE_N[p][2]);
@@ -512,7 +561,8 @@ int rt_wbvh_query(const float* tri9, int64_t n, int32_t max_depth, int32_t leaf_
                 float om = std::max(std::fabs(o.x), std::max(std::fabs(o.y), std::fabs(o.z)));
                 float m = 0x1p-16f * (om + S);
                 rt::WHit h;
-                int st = rt::wbvh_closest(w.nodes.data(), w.tris.data(), o, d, m, stk, h, wk);
+                int st = rt::wbvh_closest(w.nodes.data(), w.tris.data(), o, d, m, stk, h, wk, INFINITY, true,
+                                          shadow_rays ? W_QS_SHADOW : W_QS_CLOSEST, rk, rsel);
                 if (st == rt::W_HIT) {
                     int32_t slot = w.slot[(size_t)h.k];
                     if (rt::kdop_certifies(f.nodes[w.leaf_of_slot[(size_t)slot]], o, d, h.t)) {

@@ -920,10 +920,12 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
     const float om = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
     WStackLds stk{lv};
     WHit w;
+    // a ray from the camera position reads the frame's camera risk bits
+    const uint32_t* rk = P.wrisk && o.x == P.cam_pos[0] && o.y == P.cam_pos[1] && o.z == P.cam_pos[2] ? P.wrisk : nullptr;
 #if RT_COUNT
     uint32_t wk[4] = {0, 0, 0, 0};
     const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, INFINITY, true,
-                                W_QS_CLOSEST);
+                                W_QS_CLOSEST, rk, 0);
     count_wave_steps(P, 22, wk[3]);
     if (P.counters) {
         atomicAdd(&P.counters[10], (unsigned long long)wk[0]);
@@ -934,7 +936,7 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
     }
 #else
     const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, INFINITY,
-                                true, W_QS_CLOSEST);
+                                true, W_QS_CLOSEST, rk, 0);
 #endif
     if (st == W_MISS) {
         h.t = -1.0f;
@@ -978,15 +980,19 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
 // end, which fails the distance test, so the point is lit whatever the record is.  A
 // minimum hit t* <= hi whose octree leaf certifies it is the reference's record t.
 // Returns true when decided (shadowed in *sh); false: take the octree segment query.
-__device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float hi, v3 p, v3 lp, uint2* lv, bool* sh)
+// light: the ray is one of the frame's shadow rays towards P.light that may read its risk bits
+// (KParams::wrisk)
+__device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float hi, v3 p, v3 lp, uint2* lv, bool* sh,
+                                            bool light)
 {
     const float om = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
     WStackLds stk{lv};
     WHit w;
+    const uint32_t* rk = light ? P.wrisk : nullptr;
 #if RT_COUNT
     uint32_t wk[4] = {0, 0, 0, 0};
     const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, hi, false,
-                                W_QS_SHADOW);
+                                W_QS_SHADOW, rk, 1);
     count_wave_steps(P, 25, wk[3]);
     if (P.counters) {
         atomicAdd(&P.counters[10], (unsigned long long)wk[0]);
@@ -997,7 +1003,7 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
     }
 #else
     const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, hi, false,
-                                W_QS_SHADOW);
+                                W_QS_SHADOW, rk, 1);
 #endif
     if (st == W_MISS) {
         *sh = false;
@@ -1102,17 +1108,20 @@ __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
         // segment [-m, past the light]: a hit beyond hi fails the distance test below
         // (|p - q| >= t - |n| * 1e-4), one behind the origin does not exist (t >= 0)
         float m, hi;
-        bool nan;
+        bool nan, light;
         {
             const TRay R0 = make_ray(P, o, d);
             m = seg_margin(P, R0);
             nan = R0.nan;
             const float nl = fabsf(n.x) + fabsf(n.y) + fabsf(n.z);
             hi = (sqrtf(length2(p - lp)) + 1.0e-4f * nl) * (1.0f + 0x1p-10f) + m;
+            // the frame's light risk bits hold for this ray (wbvh.hpp WRiskArgs)
+            light = P.wrisk && lp.x == P.light[0] && lp.y == P.light[1] && lp.z == P.light[2] && hi <= P.risk_G &&
+                    nl <= P.risk_nl;
         }
         // (seg_scale > 0: no analytic shapes, so shapes_shadow below has nothing to add)
         bool sh;
-        if (P.wnodes && P.nnodes > 0 && !nan && wide_shadow(P, o, d, hi, p, lp, lv, &sh))
+        if (P.wnodes && P.nnodes > 0 && !nan && wide_shadow(P, o, d, hi, p, lp, lv, &sh, light))
             return sh;
         const OctQ q = octree_query<PLAIN>(P, o, d, -m, hi, P.seg_oct != 0, lv);
         h = q.h;
@@ -2990,6 +2999,39 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void trace_colors_kernel(KParams P, 
 // The wide BVH's triangle records and their metadata, gathered on the device from the octree's
 // (already uploaded) instead of uploading 64 B per triangle again: wide-BVH triangle k is octree
 // slot s = slot[k]; wmeta[k] = {s, its octree leaf, its caller index, that triangle's material}.
+// The frame's grazing-risk bits (wbvh.hpp wbvh_risk_tri / WRiskArgs): one thread per
+// wide-BVH triangle; a triangle at risk for point sel sets bit (slot + 4 sel) of its leaf child's
+// node and walks up the parent entries, stopping at the first bit another walk has already set (that
+// walk goes on to the root).  A point with no bound (A.on 0) marks every child.  risk[] is cleared
+// before the launch.  Vector atomics on global memory.
+__global__ __launch_bounds__(256) void wide_risk_kernel(const GTri* __restrict__ wtris,
+                                                        const uint32_t* __restrict__ tri_leaf,
+                                                        const uint32_t* __restrict__ parent, uint32_t* risk, int n,
+                                                        int nnodes, WRiskArgs A)
+{
+    const int k = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (k < nnodes) {
+        const uint32_t all = (A.on[0] ? 0u : 0xFu) | (A.on[1] ? 0u : 0xF0u);
+        if (all)
+            atomicOr(risk + k, all);
+    }
+    if (k >= n)
+        return;
+    const GTri t = load_gtri(wtris + k);
+    for (int sel = 0; sel < 2; sel++) {
+        if (!A.on[sel] || !wbvh_risk_tri(t, A.p[sel][0], A.p[sel][1], A.p[sel][2], A.G[sel], A.nu[sel], A.slack[sel],
+                                         A.QS[sel]))
+            continue;
+        uint32_t e = tri_leaf[k];
+        for (int it = 0; it < 1024 && e != W_EMPTY; it++) {   // (a walk ends at the root)
+            const uint32_t bit = 1u << ((e & 3u) + 4u * (uint32_t)sel);
+            if (atomicOr(risk + (e >> 2), bit) & bit)
+                break;
+            e = parent[e >> 2];
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void wide_gather_kernel(const GTri* __restrict__ tris, const int32_t* __restrict__ slot,
                                                           const uint32_t* __restrict__ leaf_of_slot,
                                                           const int32_t* __restrict__ tri_id,
@@ -3072,6 +3114,21 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(
         hipLaunchKernelGGL((rt::ray_trace_kernel<false, true>), dim3(pblocks), dim3(rt::BLOCK), lds, stream, *P);
     } else
         hipLaunchKernelGGL((rt::ray_trace_kernel<false, false>), dim3(blocks), dim3(rt::BLOCK), lds, stream, *P);
+    return hipGetLastError();
+}
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_wide_risk(const rt::GTri* wtris,
+                                                                                const uint32_t* tri_leaf,
+                                                                                const uint32_t* parent, uint32_t* risk,
+                                                                                int n, int nnodes,
+                                                                                const rt::WRiskArgs* A,
+                                                                                hipStream_t stream)
+{
+    const int m = n > nnodes ? n : nnodes;
+    if (m <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(rt::wide_risk_kernel, dim3((m + 255) / 256), dim3(256), 0, stream, wtris, tri_leaf, parent, risk,
+                       n, nnodes, *A);
     return hipGetLastError();
 }
 

@@ -40,6 +40,12 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ssao(const
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_wide_gather(
     const rt::GTri* tris, const int32_t* slot, const uint32_t* leaf_of_slot, const int32_t* tri_id,
     const int32_t* tri_mat, int n, rt::GTri* wtris, uint4* wmeta, hipStream_t stream);
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_wide_risk(const rt::GTri* wtris,
+                                                                                const uint32_t* tri_leaf,
+                                                                                const uint32_t* parent, uint32_t* risk,
+                                                                                int n, int nnodes,
+                                                                                const rt::WRiskArgs* A,
+                                                                                hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_downscale(const uint32_t* in, int w, int h_rows, int f, uint32_t* out,
                                           hipStream_t stream);
 
@@ -93,6 +99,7 @@ Knobs Knobs::from_env()
     k.refl_fuse = on("RT_REFL_FUSE", true);
     k.debug_waves = getenv("RT_DEBUG_WAVES") != nullptr;
     k.exact = on("RT_EXACT", false);
+    k.risk = on("RT_WBVH_RISK", true);
     {
         const char* v = getenv("RT_INJECT_FRAME_FAIL");   // tests: the k-th ray_trace fails after its image start
         k.inject_fail = v ? std::atoi(v) : 0;
@@ -131,6 +138,8 @@ int Renderer::init(std::string& err)
         e = hipDeviceGetAttribute(&num_cus_, hipDeviceAttributeMultiprocessorCount, device_);
     for (int i = 0; i < 4 && e == hipSuccess; i++)
         e = hipEventCreate(&ev_[i]);
+    if (e == hipSuccess)
+        e = hipEventCreateWithFlags(&risk_ev_, hipEventDisableTiming);
     if (e != hipSuccess) {
         err = std::string("HIP init failed: ") + hipGetErrorString(e);
         return RT_EHIP;
@@ -139,7 +148,7 @@ int Renderer::init(std::string& err)
                      &d_image_, &d_rgba_,  &d_hit_id_, &d_hit_t_,   &d_shadow_, &d_counters_,
                      &d_tri9_,  &d_rcount_, &d_roff_,  &d_pieces_,  &d_piece_uv_, &d_zkey_, &d_big_, &d_scan_tmp_,
                      &d_zbuf_,  &d_nbuf_,   &d_ao_,     &d_cones_, &d_lslab_, &d_lsin_, &d_wnodes_, &d_wtris_, &d_wmeta_, &d_wtmp_,
-                     &d_dbg_};
+                     &d_wlinks_, &d_wrisk_, &d_dbg_};
     for (DevBuf* b : all) b->device = device_;
     for (auto& b : d_tex_) b.device = device_;
     for (auto& b : d_sky_) b.device = device_;
@@ -154,6 +163,7 @@ Renderer::~Renderer()
     if (accel_stream_) hipStreamDestroy(accel_stream_);
     for (auto& e : ev_)
         if (e) hipEventDestroy(e);
+    if (risk_ev_) hipEventDestroy(risk_ev_);
     for (auto& e : ring_)
         if (e) hipEventDestroy(e);
     for (auto& b : band_slot_)
@@ -598,8 +608,15 @@ void Renderer::start_accel()
             // octree slot (the record's triangle), the leaf of its certificate, the caller's
             // triangle index and its material (kernels.hip wide_gather_kernel)
             const size_t nk = wb_.slot.size(), wn = wb_.nodes.size() * sizeof(WNode);
+            const size_t nl = wb_.tri_leaf.size() + wb_.parent.size();
             if ((e = d_wnodes_.reserve(wn)) == hipSuccess && (e = d_wtris_.reserve(nk * sizeof(GTri))) == hipSuccess &&
-                (e = d_wmeta_.reserve(nk * 16)) == hipSuccess && (e = d_wtmp_.reserve(nk * 8)) == hipSuccess) {
+                (e = d_wmeta_.reserve(nk * 16)) == hipSuccess && (e = d_wtmp_.reserve(nk * 8)) == hipSuccess &&
+                (e = d_wlinks_.reserve(nl * 4)) == hipSuccess &&
+                (e = d_wrisk_.reserve(wb_.nodes.size() * 4)) == hipSuccess &&
+                (e = hipMemcpyAsync(d_wlinks_.p, wb_.tri_leaf.data(), wb_.tri_leaf.size() * 4, hipMemcpyHostToDevice,
+                                    accel_stream_)) == hipSuccess &&
+                (e = hipMemcpyAsync(d_wlinks_.as<uint32_t>() + wb_.tri_leaf.size(), wb_.parent.data(),
+                                    wb_.parent.size() * 4, hipMemcpyHostToDevice, accel_stream_)) == hipSuccess) {
                 hipSetDevice(device_);
                 int32_t* d_slot = d_wtmp_.as<int32_t>();
                 uint32_t* d_leaf = reinterpret_cast<uint32_t*>(d_slot + nk);
@@ -640,6 +657,9 @@ int Renderer::poll_accel(bool wait)
     cones_ready_ = !cones_.empty();
     wide_ready_ = !wb_.nodes.empty();
     lslab_ready_ = !lslab_.empty();
+    risk_valid_ = false;
+    risk_nodes_ = (int64_t)wb_.nodes.size();
+    risk_tris_ = (int64_t)wb_.tri_leaf.size();
     ++accel_ver_;
     build_split_ms_[1] = accel_ms_[0];
     build_split_ms_[2] = accel_ms_[1] + accel_ms_[2];
@@ -709,6 +729,9 @@ int Renderer::adopt_from_lead()
             copy(d_wnodes_, L.d_wnodes_, L.wb_.nodes.size() * sizeof(WNode));
             copy(d_wtris_, L.d_wtris_, L.wb_.slot.size() * sizeof(GTri));
             copy(d_wmeta_, L.d_wmeta_, L.wb_.slot.size() * 16);
+            copy(d_wlinks_, L.d_wlinks_, (L.wb_.tri_leaf.size() + L.wb_.parent.size()) * 4);
+            if (e == hipSuccess)
+                e = d_wrisk_.reserve(L.wb_.nodes.size() * 4);
         }
         if (e == hipSuccess)
             e = hipStreamSynchronize(stream_);
@@ -717,6 +740,9 @@ int Renderer::adopt_from_lead()
         cones_ready_ = L.cones_ready_;
         lslab_ready_ = L.cones_ready_ && L.lslab_ready_;
         wide_ready_ = L.wide_ready_;
+        risk_valid_ = false;
+        risk_nodes_ = L.risk_nodes_;
+        risk_tris_ = L.risk_tris_;
         mir_accel_ = L.accel_ver_;
     }
     return RT_OK;
@@ -1325,6 +1351,8 @@ int Renderer::trace_frame()
     }
     if (wait_slots(stream_) != RT_OK)   // band launches in flight share the engine / raster buffers
         return RT_EHIP;
+    if ((rc = prepare_risk(P, stream_)) != RT_OK)
+        return rc;
     hipEventRecord(ev_[0], stream_);
     if ((rc = launch_frame(P, stream_)) != RT_OK) return rc;
     hipEventRecord(ev_[1], stream_);
@@ -1681,6 +1709,8 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
             if ((e = hipEventCreate(&ev)) != hipSuccess) return hip_fail(e, "hipEventCreate");
     }
     if ((e = hipMemsetAsync(S.counters.p, 0, NCOUNTER_WORDS * 8, stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+    if ((rc = prepare_risk(P, stream)) != RT_OK)
+        return rc;
     hipEventRecord(ring_[2 * ring_next_], stream);
     if ((rc = launch_frame(P, stream)) != RT_OK) return rc;
     hipEventRecord(ring_[2 * ring_next_ + 1], stream);
@@ -1691,6 +1721,46 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
     if ((e = hipEventRecord(S.done, stream)) != hipSuccess)
         return hip_fail(e, "hipEventRecord");
     S.live = true;
+    return RT_OK;
+}
+
+// The frame's grazing-risk bits (KParams::wrisk, wbvh.hpp WRiskArgs): computed on
+// 'stream' when the camera, the light or the resident wide BVH changed since the last computation
+// (launches in flight on other streams read the bits: the stream first waits for them); every
+// launch waits for the computation (risk_ev_).  RT_WBVH_RISK=0: none (every child runs case (b)).
+int Renderer::prepare_risk(KParams& P, hipStream_t stream)
+{
+    P.wrisk = nullptr;
+    P.risk_G = 0.0f;
+    P.risk_nl = 0.0f;
+    if (!P.wnodes || !knobs_.risk || risk_nodes_ <= 0 || !d_wrisk_.p || !d_wlinks_.p)
+        return RT_OK;
+    hipError_t e;
+    if (!risk_valid_ || std::memcmp(risk_cam_, P.cam_pos, sizeof risk_cam_) ||
+        std::memcmp(risk_light_, P.light, sizeof risk_light_)) {
+        if (wait_slots(stream) != RT_OK)
+            return RT_EHIP;
+        const float lo[3] = {oct_root_.dn[0], oct_root_.dn[1], oct_root_.dn[2]};
+        const float hi[3] = {oct_root_.df[0], oct_root_.df[1], oct_root_.df[2]};
+        const WRiskArgs A = wbvh_risk_args(lo, hi, P.scene_scale, P.cam_pos, P.light, W_QS_CLOSEST, W_QS_SHADOW);
+        risk_valid_ = false;
+        const uint32_t* links = d_wlinks_.as<uint32_t>();
+        if ((e = hipMemsetAsync(d_wrisk_.p, 0, (size_t)risk_nodes_ * 4, stream)) != hipSuccess ||
+            (e = rt_launch_wide_risk(P.wtris, links, links + risk_tris_, d_wrisk_.as<uint32_t>(), (int)risk_tris_,
+                                     (int)risk_nodes_, &A, stream)) != hipSuccess ||
+            (e = hipEventRecord(risk_ev_, stream)) != hipSuccess)
+            return hip_fail(e, "wide_risk_kernel");
+        risk_ev_live_ = true;
+        risk_valid_ = true;
+        std::memcpy(risk_cam_, P.cam_pos, sizeof risk_cam_);
+        std::memcpy(risk_light_, P.light, sizeof risk_light_);
+        risk_G_ = A.ray_G;
+        risk_nl_ = A.ray_nl;
+    } else if (risk_ev_live_ && (e = hipStreamWaitEvent(stream, risk_ev_, 0)) != hipSuccess)
+        return hip_fail(e, "hipStreamWaitEvent (risk bits)");
+    P.wrisk = d_wrisk_.as<uint32_t>();
+    P.risk_G = risk_G_;
+    P.risk_nl = risk_nl_;
     return RT_OK;
 }
 
@@ -1810,6 +1880,8 @@ int Renderer::trace_ray_colors(const float* orig, const float* dir, int64_t n, i
     P.counters = d_counters_.as<unsigned long long>();
     if (wait_slots(stream_) != RT_OK)   // band launches in flight share the counters' buffer
         return RT_EHIP;
+    if ((rc = prepare_risk(P, stream_)) != RT_OK)
+        return rc;
     if ((e = hipMemsetAsync(d_counters_.p, 0, NCOUNTER_WORDS * 8, stream_)) != hipSuccess ||
         (e = hipMemcpyAsync(d_o, orig, nb * 12, hipMemcpyHostToDevice, stream_)) != hipSuccess ||
         (e = hipMemcpyAsync(d_d, dir, nb * 12, hipMemcpyHostToDevice, stream_)) != hipSuccess)

@@ -53,6 +53,7 @@ struct Knobs {
     int refl_chunk_log2 = 25; // RT_REFL_CHUNK_LOG2 (10..25): sample slots per engine chunk
     bool debug_waves = false; // RT_DEBUG_WAVES: per-wave records of diagnostic builds (rt_debug_read)
     bool exact = false;       // RT_EXACT=1 / rt_set_exact: wbvh and seg off
+    bool risk = true;         // RT_WBVH_RISK=0: no per-frame grazing-risk bits (every child runs case (b), 5.6)
     int inject_fail = 0;      // RT_INJECT_FRAME_FAIL=k (tests): the k-th ray_trace fails after its image start
     bool async_accel = true;  // RT_ASYNC_ACCEL=0: the leaf cones / slabs and the wide BVH are built
                               // before the first frame instead of beside it
@@ -246,6 +247,18 @@ private:
     WBvh wb_;
     DevBuf d_wnodes_, d_wtris_, d_wmeta_;
     DevBuf d_wtmp_;   // the wide BVH's slot map and the octree's slot -> leaf map, for wide_gather_kernel
+    // the grazing-risk bits (KParams::wrisk): the walk's links (WBvh::tri_leaf then parent), the bits,
+    // and the camera / light / structure they were computed for; risk_ev_ follows their launch
+    DevBuf d_wlinks_, d_wrisk_;
+    bool risk_valid_ = false;
+    int64_t risk_nodes_ = 0, risk_tris_ = 0;   // the resident wide BVH's node and triangle counts
+    float risk_cam_[3] = {0, 0, 0}, risk_light_[3] = {0, 0, 0};
+    float risk_G_ = 0.0f, risk_nl_ = 0.0f;
+    hipEvent_t risk_ev_ = nullptr;
+    bool risk_ev_live_ = false;
+    // sets P.wrisk (and risk_G / risk_nl) for the frame's camera and light, recomputing the bits on
+    // 'stream' when they changed; every launch that reads them waits for their computation
+    int prepare_risk(KParams& P, hipStream_t stream);
     DevBuf d_dbg_;                           // diagnostic per-wave records (RT_DEBUG_WAVES)
     bool ssao_ready_ = false;   // the buffers hold the last frame's z / normals
     // raster path: caller-order triangles, per-triangle piece counts / offsets, the piece

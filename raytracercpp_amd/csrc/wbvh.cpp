@@ -1094,6 +1094,25 @@ void build_wbvh(const FlatOctree& oct, WBvh& out)
         }
     });
     phase("geometry");
+    // the risk walk's links (wbvh.hpp WBvh::tri_leaf / parent)
+    out.tri_leaf.assign((size_t)n, W_EMPTY);
+    out.parent.assign(out.nodes.size(), W_EMPTY);
+    parallel_for(pool, (int64_t)out.nodes.size(), 256, [&](int64_t w) {
+        const WNode& WN = out.nodes[(size_t)w];
+        for (int j = 0; j < W_WIDTH; j++) {
+            const uint32_t c = WN.child[j];
+            const uint32_t e = (uint32_t)w << 2 | (uint32_t)j;
+            if (c == W_EMPTY)
+                continue;
+            if (c & W_LEAF) {
+                const uint32_t first = (c >> 3) & 0x0FFFFFFFu, cnt = (c & 7u) + 1u;
+                for (uint32_t k = first; k < first + cnt; k++)
+                    out.tri_leaf[k] = e;
+            } else
+                out.parent[c] = e;
+        }
+    });
+    phase("links");
     out.stats.nodes = (int64_t)out.nodes.size();
     out.stats.leaves = pl.st.leaves;
     out.stats.max_leaf = pl.st.max_leaf;
@@ -1126,6 +1145,26 @@ int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)
         uint32_t L = w.leaf_of_slot[s];
         if (L >= oct.nodes.size() || !(oct.nodes[L].b & LEAF_BIT) || s < oct.nodes[L].a ||
             s >= oct.nodes[L].a + (oct.nodes[L].b & ~LEAF_BIT))
+            bad++;
+    }
+    // the risk walk's links: each triangle's leaf entry names it, each node's parent entry names it,
+    // and every walk reaches the root
+    if (w.tri_leaf.size() != n || w.parent.size() != w.nodes.size() || w.parent[0] != W_EMPTY)
+        return bad + 1;
+    for (size_t k = 0; k < n; k++) {
+        const uint32_t e = w.tri_leaf[k];
+        if (e == W_EMPTY || (e >> 2) >= w.nodes.size()) {
+            bad++;
+            continue;
+        }
+        const uint32_t c = w.nodes[e >> 2].child[e & 3u];
+        const uint32_t first = (c >> 3) & 0x0FFFFFFFu, cnt = (c & 7u) + 1u;
+        if (c == W_EMPTY || !(c & W_LEAF) || k < first || k >= first + cnt)
+            bad++;
+    }
+    for (size_t v = 1; v < w.nodes.size(); v++) {
+        const uint32_t e = w.parent[v];
+        if (e == W_EMPTY || (e >> 2) >= w.nodes.size() || w.nodes[e >> 2].child[e & 3u] != (uint32_t)v)
             bad++;
     }
     // every child box holds its subtree: node boxes and triangle vertices (a, a + ab, a + ac);

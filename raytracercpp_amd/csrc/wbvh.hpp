@@ -53,6 +53,22 @@ constexpr int W_MAX_LEAF = 8;
 constexpr int W_STACK = 16;   // traversal stack entries per lane (overflow: the query is not certified)
 constexpr int W_WIDTH = 4;    // children per node
 
+// the grazing split QS of the wide query's child test per query kind (wbvh_closest, wbvh_risk_tri)
+#ifndef W_QS_CLOSEST
+#define W_QS_CLOSEST 0x1p-8f
+#endif
+#ifndef W_QS_SHADOW
+#define W_QS_SHADOW 0x1p-8f
+#endif
+
+// timing-only switches (tools/variants.py; never sound when off)
+#ifndef W_CASE_B
+#define W_CASE_B 1
+#endif
+#ifndef W_SOUND_A
+#define W_SOUND_A 1
+#endif
+
 #ifndef W_STEP_HOOK
 #define W_STEP_HOOK(cur, leaf)   // diagnostic builds (kernels.hip): per-step wave statistics
 #endif
@@ -129,6 +145,9 @@ struct WBvh {
     std::vector<int32_t> slot;         // wide-BVH triangle -> octree GTri slot
     std::vector<uint32_t> leaf_of_slot;   // octree GTri slot -> flattened octree leaf node
     std::vector<uint32_t> leaf_of_k;      // wide-BVH triangle -> flattened octree leaf node (= leaf_of_slot[slot])
+    // the grazing-risk walk (wbvh_risk_tri): wide-BVH triangle -> its leaf child (node << 2 | slot),
+    // node -> its parent's child entry (parent << 2 | slot; W_EMPTY for the root)
+    std::vector<uint32_t> tri_leaf, parent;
     WStats stats;
 };
 
@@ -303,6 +322,111 @@ RT_HD bool kdop_certifies(const GNode& nd, v3 o, v3 d, float t)
 RT_HD uint32_t fbits(float f) { return __builtin_bit_cast(uint32_t, f); }
 RT_HD float bitsf(uint32_t u) { return __builtin_bit_cast(float, u); }
 
+// Grazing risk of a triangle for a point X ("risk bits"): false only when no ray
+// of the kind X stands for can make the triangle report a hit in case (b) of wbvh_closest (|cos(n,
+// d)| < QS).  Case (b) puts the ray's origin o within H0 = 1.01 (QS + 8u) (L + |o - a|) / s2 of the
+// triangle's plane (s2 = sin(alpha' / 2) as the build's ext byte 1, L = the longer edge).
+//   camera (G = 0, nu = 0): the rays start at X itself;
+//   light: the rays start at o with |X - o| <= G and pass within nu of X with their direction within
+//          QS of the plane's, so X lies within H0(|X - a| + G) + QS G + nu of the plane.
+// slack >= the query's box margin m for those rays.  In double from the record's float edges (the
+// products exact, each difference rounded once); a degenerate record (no s2 bound) is always at
+// risk, one whose stored normal is zero never (Mdet = 0: never a hit).
+RT_HD bool wbvh_risk_tri(const GTri& t, double px, double py, double pz, double G, double nu, double slack, double QS)
+{
+    if (t.n[0] == 0.0f && t.n[1] == 0.0f && t.n[2] == 0.0f)
+        return false;
+    const double x0 = t.ab[0], x1 = t.ab[1], x2 = t.ab[2], y0 = t.ac[0], y1 = t.ac[1], y2 = t.ac[2];
+    const double c0 = x1 * y2 - x2 * y1, c1 = x2 * y0 - x0 * y2, c2 = x0 * y1 - x1 * y0;
+    const double la = sqrt(x0 * x0 + x1 * x1 + x2 * x2), lc = sqrt(y0 * y0 + y1 * y1 + y2 * y2);
+    const double cl = sqrt(c0 * c0 + c1 * c1 + c2 * c2);
+    if (!(la * lc > 0x1p-100) || !(cl > 0x1p-50 * la * lc))
+        return true;
+    const double ca = fabs(x0 * y0 + x1 * y1 + x2 * y2) / (la * lc);
+    const double s2 = sqrt(fmax(0.0, (1.0 - fmin(1.0, ca + 1e-12)) / 2.0)) * (1 - 1e-9);
+    if (!(s2 > 0.0))
+        return true;
+    const double ax = px - (double)t.a[0], ay = py - (double)t.a[1], az = pz - (double)t.a[2];
+    const double Da = sqrt(ax * ax + ay * ay + az * az);
+    const double dist = fabs(c0 * ax + c1 * ay + c2 * az) / cl;
+    const double L = fmax(la, lc) * (1 + 1e-12);
+    const double rhs = (1.01 * (QS + 8.0 * 0x1p-24) * (L + Da + G + slack) / s2 + QS * G + nu) * (1 + 1e-6);
+    return !(dist > rhs);
+}
+
+// A frame's two risk points (kernels.hip wide_risk_kernel): sel 0 the camera (rays start at it), sel
+// 1 the light (shadow rays: o = p + 1e-4 n, d = normalize(light - p), renderer.cpp:340-402, for hit
+// points p in the scene box [lo, hi]).  The shadow rays that may use the light's bits are the ones
+// whose segment bound hi (kernels.hip is_shadowed, >= |light - o|) is <= ray_G and whose normal has
+// |n|_1 <= ray_nl: their lines pass within nu = 1.001e-4 ray_nl + 16u G of the light (the offset
+// and normalize's rounding).  slack >= the query's margin m for the kind's origins.
+struct WRiskArgs {
+    double p[2][3];
+    double G[2], nu[2], slack[2], QS[2];
+    int32_t on[2];
+    float ray_G, ray_nl;
+};
+
+inline WRiskArgs wbvh_risk_args(const float lo[3], const float hi[3], float S, const float cam[3], const float light[3],
+                                float qs_cam, float qs_light)
+{
+    WRiskArgs A{};
+    double cm = 0, lm = 0, gc = 0;
+    for (int a = 0; a < 3; a++) {
+        A.p[0][a] = cam[a];
+        A.p[1][a] = light[a];
+        cm = std::max(cm, std::fabs((double)cam[a]));
+        lm = std::max(lm, std::fabs((double)light[a]));
+    }
+    for (int c = 0; c < 8; c++) {
+        double g = 0;
+        for (int a = 0; a < 3; a++) {
+            const double x = ((c >> a) & 1) ? hi[a] : lo[a];
+            g += (x - light[a]) * (x - light[a]);
+        }
+        gc = std::max(gc, std::sqrt(g));
+    }
+    A.ray_nl = 2.0f;
+    const double G = 1.01 * (gc + 1e-4 * A.ray_nl) + 0x1p-10 * (S + lm);
+    A.ray_G = std::nextafter((float)G, 0.0f);
+    A.G[0] = 0.0;
+    A.nu[0] = 0.0;
+    A.slack[0] = 1.01 * 0x1p-16 * (cm + S);
+    A.QS[0] = qs_cam;
+    A.G[1] = G;
+    A.nu[1] = 1.001e-4 * A.ray_nl + 16.0 * 0x1p-24 * G;
+    A.slack[1] = 1.01 * 0x1p-16 * (lm + G + S);
+    A.QS[1] = qs_light;
+    const bool fin = std::isfinite(cm) && std::isfinite(lm) && std::isfinite(G);
+    A.on[0] = A.on[1] = fin ? 1 : 0;
+    return A;
+}
+
+// The per-point risk bits of the wide BVH: bit (j + 4 sel) of risk[node] is set when child j holds a
+// triangle at risk for point sel.  Host version of kernels.hip wide_risk_kernel (tests, rt_wbvh_query_ex).
+inline void wbvh_risk_host(const WBvh& w, const WRiskArgs& A, int sel, std::vector<uint32_t>& risk)
+{
+    risk.resize(w.nodes.size(), 0u);
+    if (!A.on[sel]) {   // no bound: every child at risk
+        for (auto& r : risk)
+            r |= 0xFu << (4 * sel);
+        return;
+    }
+    for (size_t k = 0; k < w.tris.size(); k++) {
+        if (!wbvh_risk_tri(w.tris[k], A.p[sel][0], A.p[sel][1], A.p[sel][2], A.G[sel], A.nu[sel], A.slack[sel], A.QS[sel]))
+            continue;
+        uint32_t e = w.tri_leaf[k];
+        while (e != W_EMPTY) {
+            const uint32_t bit = 1u << ((e & 3u) + 4 * sel);
+            uint32_t& r = risk[e >> 2];
+            if (r & bit)
+                break;
+            r |= bit;
+            e = w.parent[e >> 2];
+        }
+    }
+}
+
 enum WStatus : int { W_MISS = 0, W_HIT = 1, W_UNCERT = 2 };
 
 struct WHit {
@@ -451,9 +575,13 @@ float wq_case_b(const WNode* node, int j, v3 o, v3 d, float ix, float iy, float 
 //       widened by rho), and p' = o + t d (0 <= t <= best) lies within eta + sin(theta) |p' - a|
 //       of the child's slab.  A child passing all three is entered, keyed by the smallest such t.
 // Robustly back-facing children (the cone) report nothing and are skipped as before.
+// risk (optional): the risk bits of the ray's kind rsel (wbvh_risk_host / kernels.hip
+// wide_risk_kernel); a child whose bit is clear holds no triangle that can report a hit in case (b)
+// for this ray, so (b) is skipped for it.  The caller guarantees the ray is of that kind.
 template <class Stack>
 RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m, Stack& stk, WHit& h,
-                       uint32_t* work = nullptr, float hi = INFINITY, bool ties = true, float QS = 0x1p-8f)
+                       uint32_t* work = nullptr, float hi = INFINITY, bool ties = true, float QS = 0x1p-8f,
+                       const uint32_t* risk = nullptr, int rsel = 0)
 {
     h.t = INFINITY;
     h.u = 1.0f;
@@ -517,6 +645,9 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                 Dn = sqrtf(fx * fx + fy * fy + fz * fz) * (1.0f + 0x1p-16f) + m;
             }
             const float RA = U * 30.4f * Dn, RB = U * 2.01f * Dn;
+            // the children that may hold a triangle at risk for this ray's kind (wbvh_risk_tri): the
+            // others skip case (b)
+            const uint32_t rbits = risk ? ldg(risk + cur) >> (4 * rsel) : 0xFu;
             constexpr int QW = W_WIDTH / 4;   // words per axis row of quantised planes
             float key[W_WIDTH];
             uint32_t ref[W_WIDTH];
@@ -546,8 +677,12 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                     const float iq = fast_rcp(qa * smin) * (1.0f + 0x1p-18f);
                     const float Bq = __builtin_fmaf(7.21f * U, iq, 2.01f * U);
                     const float Aq = __builtin_fmaf(__builtin_fmaf(14.4f * U, L, RA), iq, __builtin_fmaf(4.02f * U, L, RB));
+#if W_SOUND_A
                     const float R = !(Bq <= 0.5f) ? INFINITY
                                                   : __builtin_fmaf(Bq, Dn, Aq) * __builtin_fmaf(2.0f, Bq, 1.0f) * (1.0f + 0x1p-16f) + m;
+#else
+                    const float R = m + 0.0f * Bq * Aq;
+#endif
                     const uint32_t lx = wd(WN_QLO + 0 * QW + jw), hx = wd(WN_QHI + 0 * QW + jw);
                     const uint32_t ly = wd(WN_QLO + 1 * QW + jw), hy = wd(WN_QHI + 1 * QW + jw);
                     const uint32_t lz = wd(WN_QLO + 2 * QW + jw), hz = wd(WN_QHI + 2 * QW + jw);
@@ -590,7 +725,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                     }
                     if (ok)
                         key[j] = fminf(fmaxf(tmin, 0.0f), 3.0e38f);
-                    if (qlb < QS)   // (b): triangles that may lie nearly parallel to d
+                    if (W_CASE_B && qlb < QS && ((rbits >> j) & 1u))   // (b): triangles that may lie nearly parallel to d
                         key[j] = fminf(key[j], wq_case_b(nodes + cur, j, o, d, ix, iy, iz, m, QS, dl, best_s, a, qa, iq));
                 }
 #if defined(__HIP_DEVICE_COMPILE__)

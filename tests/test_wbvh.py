@@ -182,11 +182,12 @@ def grazing_q(tri, ids, d):
     return np.abs((n * dd).sum(1)) / (np.linalg.norm(ab, axis=1) * np.linalg.norm(ac, axis=1) * np.linalg.norm(dd, axis=1))
 
 
-def _grazing_differences(tri, o, d):
-    """(certified fraction, number of certified answers that differ from the oracle's BVH::intersect)"""
-    from raytracercpp_amd.scene import RenderSettings
+def _grazing_differences(tri, o, d, **risk):
+    """(certified fraction, number of certified answers that differ from the oracle's BVH::intersect);
+    risk: the frame's risk points (cam / light / shadow_rays, _lib.wbvh_query), the oracle answering
+    the rays the query built"""
     import dataclasses
-    status, ids, t, u, v, stats, _ = _lib.wbvh_query(tri, o, d, 12, 40)
+    status, ids, t, u, v, stats, _, o, d = _lib.wbvh_query(tri, o, d, 12, 40, rays_out=True, **risk)
     assert stats["violations"] == 0
     base, _ = scenes.robot1080(width=8, height=8)
     sc = dataclasses.replace(base, tri=np.ascontiguousarray(tri, np.float32), tri_mat=np.zeros(len(tri), np.int32),
@@ -260,4 +261,99 @@ def test_grazing_sliver_soup_certified_answers_match_oracle():
     o = T[k].mean(1) - d * rng.uniform(0.2, 2.0, len(k))[:, None] + n * (eps * rng.uniform(-1, 1, len(k)))[:, None]
     cert, bad = _grazing_differences(tri, o.astype(np.float32), d.astype(np.float32))
     print(f"grazing slivers: {cert:.4f} certified, {bad} certified answers differ")
+    assert bad == 0
+
+
+# ---- the frame's grazing-risk bits (wbvh.hpp wbvh_risk_tri) ----
+# Rays from the camera position read the camera's bits, shadow rays the light's: a child whose bit
+# is clear skips case (b).  Adversarial placements: the camera / light at 0 .. 1e-1 from the plane of
+# a tessellated plane (every ray grazes it), on a tangent of the sphere.
+
+def _plane_frame(seed, h, n_rays=20000):
+    """The grazing plane of grazing_plane_case and a camera at height h above it, looking at points
+    of the plane (ray sines ~ h / distance) and along it (a third of the rays just above / below)."""
+    rng = np.random.default_rng(seed)
+    R = _rotation(rng)
+    off = rng.uniform(-5, 5, 3)
+    tri = (_grid(400, 4.0).reshape(-1, 3, 3) @ R.T + off).reshape(-1, 9).astype(np.float32)
+    C = np.array([rng.uniform(-5, 5), h, rng.uniform(-5, 5)])
+    p = np.stack([rng.uniform(-4, 4, n_rays), np.zeros(n_rays), rng.uniform(-4, 4, n_rays)], 1)
+    d = p - C
+    k = n_rays // 3
+    d[:k, 1] = rng.choice([-1, 1], k) * np.exp(rng.uniform(np.log(1e-9), np.log(1e-3), k)) * np.linalg.norm(d[:k], axis=1)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    cam = (C @ R.T + off).astype(np.float32)
+    return tri, np.repeat(cam[None], n_rays, 0), (d @ R.T).astype(np.float32), cam
+
+
+@pytest.mark.parametrize("h", [0.0, 1e-7, 1e-4, 1e-1])
+def test_risk_bits_camera_grazing_plane(h):
+    tri, o, d, cam = _plane_frame(23, h)
+    cert, bad = _grazing_differences(tri, o, d, cam=cam)
+    print(f"camera at {h} from the plane: {cert:.4f} certified, {bad} differ")
+    assert bad == 0
+
+
+def test_risk_bits_camera_sphere_silhouette():
+    """Camera rays tangent to the bumpy sphere from one camera point (its silhouette)."""
+    rng = np.random.default_rng(4)
+    sc, _ = scenes.bumpy70k(width=8, height=8)
+    tri = sc.tri
+    T = tri.reshape(-1, 3, 3).astype(np.float64)
+    cam = np.array([0.3, 0.2, 6.0])
+    k = rng.integers(0, len(T), 20000)
+    p = T[k].mean(1) + (T[k, 1] - T[k, 0]) * rng.uniform(-0.3, 0.3, (20000, 1))
+    d = p - cam
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    o = np.repeat(cam[None].astype(np.float32), 20000, 0)
+    cert, bad = _grazing_differences(tri, o, d.astype(np.float32), cam=cam.astype(np.float32))
+    print(f"sphere silhouette from the camera: {cert:.4f} certified, {bad} differ")
+    assert bad == 0
+
+
+@pytest.mark.parametrize("h", [0.0, 1e-6, 1e-3])
+def test_risk_bits_light_grazing_plane(h):
+    """Shadow rays from hit points on the plane towards a light at height h above it: every ray
+    grazes the plane."""
+    rng = np.random.default_rng(31)
+    R = _rotation(rng)
+    off = rng.uniform(-5, 5, 3)
+    tri = (_grid(400, 4.0).reshape(-1, 3, 3) @ R.T + off).reshape(-1, 9).astype(np.float32)
+    L = (np.array([rng.uniform(-6, 6), h, rng.uniform(-6, 6)]) @ R.T + off).astype(np.float32)
+    n = 20000
+    # hit points on the plane (normal up) and, for half the rays, on surfaces standing on it (normals
+    # in the plane) at heights up to +-1e-3: their rays start next to the plane
+    hp = np.zeros(n)
+    hp[n // 2:] = rng.choice([-1, 1], n - n // 2) * np.exp(rng.uniform(np.log(1e-9), np.log(1e-3), n - n // 2))
+    p = (np.stack([rng.uniform(-4, 4, n), hp, rng.uniform(-4, 4, n)], 1) @ R.T + off).astype(np.float32)
+    az = rng.uniform(0, 2 * np.pi, n)
+    nl = np.stack([np.cos(az), np.zeros(n), np.sin(az)], 1)
+    nl[: n // 2] = [0.0, 1.0, 0.0]
+    nrm = (nl @ R.T).astype(np.float32)
+    cert, bad = _grazing_differences(tri, p, nrm, light=L, shadow_rays=True)
+    print(f"light at {h} from the plane: {cert:.4f} certified, {bad} differ")
+    assert bad == 0
+
+
+def test_risk_bits_light_sphere_terminator():
+    """Shadow rays from points on the bumpy sphere near its terminator (normal nearly perpendicular
+    to the light) and a camera in the same frame."""
+    rng = np.random.default_rng(8)
+    sc, _ = scenes.bumpy70k(width=8, height=8)
+    tri = sc.tri
+    T = tri.reshape(-1, 3, 3).astype(np.float64)
+    L = np.array([5.0, 0.5, 1.0], np.float32)
+    nn = np.cross(T[:, 1] - T[:, 0], T[:, 2] - T[:, 0])
+    nn /= np.maximum(np.linalg.norm(nn, axis=1, keepdims=True), 1e-30)
+    c = T.mean(1)
+    toL = L - c
+    toL /= np.linalg.norm(toL, axis=1, keepdims=True)
+    cosl = np.abs((nn * toL).sum(1))
+    k = np.argsort(cosl)[:20000]   # the triangles closest to grazing the light
+    uv = rng.uniform(0, 1, (len(k), 2))
+    uv[uv.sum(1) > 1] = 1 - uv[uv.sum(1) > 1]
+    p = T[k, 0] + (T[k, 1] - T[k, 0]) * uv[:, :1] + (T[k, 2] - T[k, 0]) * uv[:, 1:]
+    cert, bad = _grazing_differences(tri, p.astype(np.float32), nn[k].astype(np.float32), light=L,
+                                     cam=np.array([0.0, 0.0, 6.0], np.float32), shadow_rays=True)
+    print(f"sphere terminator: {cert:.4f} certified, {bad} differ")
     assert bad == 0
