@@ -462,6 +462,15 @@ int rt_octree_digest(const float* tri9, int64_t n, int32_t max_depth, int32_t le
     }
 }
 
+#if defined(W_DIAG) && !defined(__HIP_DEVICE_COMPILE__)
+// host diagnostic counters of wbvh_closest (W_DIAG builds): read and reset
+__attribute__((visibility("default"))) void rt_diag_read(long long* out)
+{
+    for (int i = 0; i < 8; i++)
+        out[i] = rt::g_wdiag[i].exchange(0);
+}
+#endif
+
 int rt_wbvh_query(const float* tri9, int64_t n, int32_t max_depth, int32_t leaf_max_obj_count, const float* orig,
                   const float* dir, int64_t nrays, int32_t* status, int32_t* id, float* t, float* u, float* v,
                   int64_t stats[8], float* ms)
@@ -495,14 +504,14 @@ int rt_wbvh_query_ex(const float* tri9, int64_t n, int32_t max_depth, int32_t le
                 S = std::max(S, std::max(std::fabs(f.nodes[0].dn[a]), std::fabs(f.nodes[0].df[a])));
         const bool usable = !w.nodes.empty() && S > 0x1p-20f && S < 0x1p20f;
         // the risk bits of the camera / light (renderer.cpp prepare_risk, kernels.hip wide_risk_kernel)
-        std::vector<uint32_t> risk;
+        std::vector<float> risk;
         rt::WRiskArgs RA{};
         if (usable && (cam || light)) {
             const float lo[3] = {f.nodes[0].dn[0], f.nodes[0].dn[1], f.nodes[0].dn[2]};
             const float hi[3] = {f.nodes[0].df[0], f.nodes[0].df[1], f.nodes[0].df[2]};
             const float zero[3] = {0, 0, 0};
             RA = rt::wbvh_risk_args(lo, hi, S, cam ? cam : zero, light ? light : zero, W_QS_CLOSEST, W_QS_SHADOW);
-            risk.assign(w.nodes.size(), 0u);
+            risk.assign(w.nodes.size() * 8, INFINITY);
             if (cam)
                 rt::wbvh_risk_host(w, RA, 0, risk);
             if (light)
@@ -515,8 +524,9 @@ int rt_wbvh_query_ex(const float* tri9, int64_t n, int32_t max_depth, int32_t le
             for (int64_t i = b; i < e; i++) {
                 rt::v3 o = rt::mk(orig[3 * i], orig[3 * i + 1], orig[3 * i + 2]);
                 rt::v3 d = rt::mk(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]);
-                const uint32_t* rk = nullptr;
+                const float* rk = nullptr;
                 int rsel = 0;
+                float rsub = 0.0f;
                 if (shadow_rays) {
                     // is_shadowed's ray (kernels.hip): orig = the hit point p, dir = its normal n
                     const rt::v3 p = o, nrm = d, lp = rt::mk(light[0], light[1], light[2]);
@@ -527,6 +537,7 @@ int rt_wbvh_query_ex(const float* tri9, int64_t n, int32_t max_depth, int32_t le
                     if (!risk.empty() && hi <= RA.ray_G && nl <= RA.ray_nl) {
                         rk = risk.data();
                         rsel = 1;
+                        rsub = rt::wrisk_sub(W_QS_SHADOW, hi, RA.ray_nu);
                     }
                 } else if (!risk.empty() && cam && o.x == cam[0] && o.y == cam[1] && o.z == cam[2])
                     rk = risk.data();
@@ -562,7 +573,7 @@ int rt_wbvh_query_ex(const float* tri9, int64_t n, int32_t max_depth, int32_t le
                 float m = 0x1p-16f * (om + S);
                 rt::WHit h;
                 int st = rt::wbvh_closest(w.nodes.data(), w.tris.data(), o, d, m, stk, h, wk, INFINITY, true,
-                                          shadow_rays ? W_QS_SHADOW : W_QS_CLOSEST, rk, rsel);
+                                          shadow_rays ? W_QS_SHADOW : W_QS_CLOSEST, rk, rsel, rsub);
                 if (st == rt::W_HIT) {
                     int32_t slot = w.slot[(size_t)h.k];
                     if (rt::kdop_certifies(f.nodes[w.leaf_of_slot[(size_t)slot]], o, d, h.t)) {

@@ -920,12 +920,12 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
     const float om = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
     WStackLds stk{lv};
     WHit w;
-    // a ray from the camera position reads the frame's camera risk bits
-    const uint32_t* rk = P.wrisk && o.x == P.cam_pos[0] && o.y == P.cam_pos[1] && o.z == P.cam_pos[2] ? P.wrisk : nullptr;
+    // a ray from the camera position reads the frame's camera risk keys
+    const float* rk = P.wrisk && o.x == P.cam_pos[0] && o.y == P.cam_pos[1] && o.z == P.cam_pos[2] ? P.wrisk : nullptr;
 #if RT_COUNT
     uint32_t wk[4] = {0, 0, 0, 0};
     const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, INFINITY, true,
-                                W_QS_CLOSEST, rk, 0);
+                                W_QS_CLOSEST, rk, 0, 0.0f);
     count_wave_steps(P, 22, wk[3]);
     if (P.counters) {
         atomicAdd(&P.counters[10], (unsigned long long)wk[0]);
@@ -936,7 +936,7 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
     }
 #else
     const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, INFINITY,
-                                true, W_QS_CLOSEST, rk, 0);
+                                true, W_QS_CLOSEST, rk, 0, 0.0f);
 #endif
     if (st == W_MISS) {
         h.t = -1.0f;
@@ -980,19 +980,20 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
 // end, which fails the distance test, so the point is lit whatever the record is.  A
 // minimum hit t* <= hi whose octree leaf certifies it is the reference's record t.
 // Returns true when decided (shadowed in *sh); false: take the octree segment query.
-// light: the ray is one of the frame's shadow rays towards P.light that may read its risk bits
-// (KParams::wrisk)
+// light: the ray is one of the frame's shadow rays towards P.light that may read its risk keys
+// (KParams::wrisk; hi >= |light - o|)
 __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float hi, v3 p, v3 lp, uint2* lv, bool* sh,
                                             bool light)
 {
     const float om = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
     WStackLds stk{lv};
     WHit w;
-    const uint32_t* rk = light ? P.wrisk : nullptr;
+    const float* rk = light ? P.wrisk : nullptr;
+    const float rsub = light ? wrisk_sub(W_QS_SHADOW, hi, P.risk_nu) : 0.0f;
 #if RT_COUNT
     uint32_t wk[4] = {0, 0, 0, 0};
     const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, hi, false,
-                                W_QS_SHADOW, rk, 1);
+                                W_QS_SHADOW, rk, 1, rsub);
     count_wave_steps(P, 25, wk[3]);
     if (P.counters) {
         atomicAdd(&P.counters[10], (unsigned long long)wk[0]);
@@ -1003,7 +1004,7 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
     }
 #else
     const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, hi, false,
-                                W_QS_SHADOW, rk, 1);
+                                W_QS_SHADOW, rk, 1, rsub);
 #endif
     if (st == W_MISS) {
         *sh = false;
@@ -1115,7 +1116,7 @@ __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
             nan = R0.nan;
             const float nl = fabsf(n.x) + fabsf(n.y) + fabsf(n.z);
             hi = (sqrtf(length2(p - lp)) + 1.0e-4f * nl) * (1.0f + 0x1p-10f) + m;
-            // the frame's light risk bits hold for this ray (wbvh.hpp WRiskArgs)
+            // the frame's light risk keys hold for this ray (wbvh.hpp WRiskArgs)
             light = P.wrisk && lp.x == P.light[0] && lp.y == P.light[1] && lp.z == P.light[2] && hi <= P.risk_G &&
                     nl <= P.risk_nl;
         }
@@ -2015,19 +2016,9 @@ __global__ __launch_bounds__(BLOCK) void refl_keys_kernel(KParams P, const Frame
         float lo = P.nodes[0].dn[a], hi = P.nodes[0].df[a];
         float t = (fr[f].ro[a] - lo) / (hi - lo);
         t = t == t ? fminf(fmaxf(t, 0.0f), 1.0f) : 0.0f;
-#if defined(RT_REFL_KEY_DIR)
-        q[a] = (uint32_t)(t * 511.0f);
-#else
         q[a] = (uint32_t)(t * 1023.0f);
-#endif
     }
-#if defined(RT_REFL_KEY_DIR)
-    const uint32_t oct = (fr[f].perfect[0] < 0.0f ? 1u : 0u) | (fr[f].perfect[1] < 0.0f ? 2u : 0u) |
-                         (fr[f].perfect[2] < 0.0f ? 4u : 0u);
-    keys[f] = (oct << 27) | spread10(q[0]) | (spread10(q[1]) << 1) | (spread10(q[2]) << 2);
-#else
     keys[f] = spread10(q[0]) | (spread10(q[1]) << 1) | (spread10(q[2]) << 2);
-#endif
     idx[f] = f;
 }
 
@@ -2999,33 +2990,37 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void trace_colors_kernel(KParams P, 
 // The wide BVH's triangle records and their metadata, gathered on the device from the octree's
 // (already uploaded) instead of uploading 64 B per triangle again: wide-BVH triangle k is octree
 // slot s = slot[k]; wmeta[k] = {s, its octree leaf, its caller index, that triangle's material}.
-// The frame's grazing-risk bits (wbvh.hpp wbvh_risk_tri / WRiskArgs): one thread per
-// wide-BVH triangle; a triangle at risk for point sel sets bit (slot + 4 sel) of its leaf child's
-// node and walks up the parent entries, stopping at the first bit another walk has already set (that
-// walk goes on to the root).  A point with no bound (A.on 0) marks every child.  risk[] is cleared
-// before the launch.  Vector atomics on global memory.
+// The frame's grazing-risk keys (wbvh.hpp wbvh_risk_key / wbvh_risk_host / WRiskArgs):
+// one thread per wide-BVH triangle; a triangle at risk for point sel takes the minimum of its key
+// and its leaf child's, then of its parent entries', stopping where the stored key is already no
+// larger (the walk that stored it goes on to the root).  A point with no bound (A.on 0) gives every
+// child key 0.  risk[] is filled with INFINITY before the launch; non-negative float keys compare
+// as their bit patterns (vector atomics on global memory).
 __global__ __launch_bounds__(256) void wide_risk_kernel(const GTri* __restrict__ wtris,
                                                         const uint32_t* __restrict__ tri_leaf,
                                                         const uint32_t* __restrict__ parent, uint32_t* risk, int n,
                                                         int nnodes, WRiskArgs A)
 {
     const int k = (int)(blockIdx.x * 256 + threadIdx.x);
-    if (k < nnodes) {
-        const uint32_t all = (A.on[0] ? 0u : 0xFu) | (A.on[1] ? 0u : 0xF0u);
-        if (all)
-            atomicOr(risk + k, all);
-    }
+    if (k < nnodes)
+        for (int sel = 0; sel < 2; sel++)
+            if (!A.on[sel])
+                for (int j = 0; j < 4; j++)
+                    atomicMin(risk + (2 * (size_t)k + sel) * 4 + j, 0u);
     if (k >= n)
         return;
     const GTri t = load_gtri(wtris + k);
     for (int sel = 0; sel < 2; sel++) {
-        if (!A.on[sel] || !wbvh_risk_tri(t, A.p[sel][0], A.p[sel][1], A.p[sel][2], A.G[sel], A.nu[sel], A.slack[sel],
-                                         A.QS[sel]))
+        if (!A.on[sel])
             continue;
+        const float K = wbvh_risk_key(t, A.p[sel][0], A.p[sel][1], A.p[sel][2], A.G[sel], A.nu[sel], A.slack[sel],
+                                      A.QS[sel]);
+        if (!(K < INFINITY))
+            continue;
+        const uint32_t kb = __builtin_bit_cast(uint32_t, K);
         uint32_t e = tri_leaf[k];
         for (int it = 0; it < 1024 && e != W_EMPTY; it++) {   // (a walk ends at the root)
-            const uint32_t bit = 1u << ((e & 3u) + 4u * (uint32_t)sel);
-            if (atomicOr(risk + (e >> 2), bit) & bit)
+            if (atomicMin(risk + (2 * (size_t)(e >> 2) + sel) * 4 + (e & 3u), kb) <= kb)
                 break;
             e = parent[e >> 2];
         }

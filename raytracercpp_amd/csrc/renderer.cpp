@@ -612,7 +612,7 @@ void Renderer::start_accel()
             if ((e = d_wnodes_.reserve(wn)) == hipSuccess && (e = d_wtris_.reserve(nk * sizeof(GTri))) == hipSuccess &&
                 (e = d_wmeta_.reserve(nk * 16)) == hipSuccess && (e = d_wtmp_.reserve(nk * 8)) == hipSuccess &&
                 (e = d_wlinks_.reserve(nl * 4)) == hipSuccess &&
-                (e = d_wrisk_.reserve(wb_.nodes.size() * 4)) == hipSuccess &&
+                (e = d_wrisk_.reserve(wb_.nodes.size() * 32)) == hipSuccess &&
                 (e = hipMemcpyAsync(d_wlinks_.p, wb_.tri_leaf.data(), wb_.tri_leaf.size() * 4, hipMemcpyHostToDevice,
                                     accel_stream_)) == hipSuccess &&
                 (e = hipMemcpyAsync(d_wlinks_.as<uint32_t>() + wb_.tri_leaf.size(), wb_.parent.data(),
@@ -731,7 +731,7 @@ int Renderer::adopt_from_lead()
             copy(d_wmeta_, L.d_wmeta_, L.wb_.slot.size() * 16);
             copy(d_wlinks_, L.d_wlinks_, (L.wb_.tri_leaf.size() + L.wb_.parent.size()) * 4);
             if (e == hipSuccess)
-                e = d_wrisk_.reserve(L.wb_.nodes.size() * 4);
+                e = d_wrisk_.reserve(L.wb_.nodes.size() * 32);
         }
         if (e == hipSuccess)
             e = hipStreamSynchronize(stream_);
@@ -1724,15 +1724,16 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
     return RT_OK;
 }
 
-// The frame's grazing-risk bits (KParams::wrisk, wbvh.hpp WRiskArgs): computed on
+// The frame's grazing-risk keys (KParams::wrisk, wbvh.hpp WRiskArgs): computed on
 // 'stream' when the camera, the light or the resident wide BVH changed since the last computation
-// (launches in flight on other streams read the bits: the stream first waits for them); every
+// (launches in flight on other streams read the keys: the stream first waits for them); every
 // launch waits for the computation (risk_ev_).  RT_WBVH_RISK=0: none (every child runs case (b)).
 int Renderer::prepare_risk(KParams& P, hipStream_t stream)
 {
     P.wrisk = nullptr;
     P.risk_G = 0.0f;
     P.risk_nl = 0.0f;
+    P.risk_nu = 0.0f;
     if (!P.wnodes || !knobs_.risk || risk_nodes_ <= 0 || !d_wrisk_.p || !d_wlinks_.p)
         return RT_OK;
     hipError_t e;
@@ -1745,7 +1746,8 @@ int Renderer::prepare_risk(KParams& P, hipStream_t stream)
         const WRiskArgs A = wbvh_risk_args(lo, hi, P.scene_scale, P.cam_pos, P.light, W_QS_CLOSEST, W_QS_SHADOW);
         risk_valid_ = false;
         const uint32_t* links = d_wlinks_.as<uint32_t>();
-        if ((e = hipMemsetAsync(d_wrisk_.p, 0, (size_t)risk_nodes_ * 4, stream)) != hipSuccess ||
+        if ((e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_wrisk_.p), 0x7F800000, (size_t)risk_nodes_ * 8,
+                                   stream)) != hipSuccess ||
             (e = rt_launch_wide_risk(P.wtris, links, links + risk_tris_, d_wrisk_.as<uint32_t>(), (int)risk_tris_,
                                      (int)risk_nodes_, &A, stream)) != hipSuccess ||
             (e = hipEventRecord(risk_ev_, stream)) != hipSuccess)
@@ -1756,11 +1758,13 @@ int Renderer::prepare_risk(KParams& P, hipStream_t stream)
         std::memcpy(risk_light_, P.light, sizeof risk_light_);
         risk_G_ = A.ray_G;
         risk_nl_ = A.ray_nl;
+        risk_nu_ = A.ray_nu;
     } else if (risk_ev_live_ && (e = hipStreamWaitEvent(stream, risk_ev_, 0)) != hipSuccess)
         return hip_fail(e, "hipStreamWaitEvent (risk bits)");
-    P.wrisk = d_wrisk_.as<uint32_t>();
+    P.wrisk = d_wrisk_.as<float>();
     P.risk_G = risk_G_;
     P.risk_nl = risk_nl_;
+    P.risk_nu = risk_nu_;
     return RT_OK;
 }
 

@@ -247,13 +247,13 @@ private:
     WBvh wb_;
     DevBuf d_wnodes_, d_wtris_, d_wmeta_;
     DevBuf d_wtmp_;   // the wide BVH's slot map and the octree's slot -> leaf map, for wide_gather_kernel
-    // the grazing-risk bits (KParams::wrisk): the walk's links (WBvh::tri_leaf then parent), the bits,
+    // the grazing-risk keys (KParams::wrisk): the walk's links (WBvh::tri_leaf then parent), the keys,
     // and the camera / light / structure they were computed for; risk_ev_ follows their launch
     DevBuf d_wlinks_, d_wrisk_;
     bool risk_valid_ = false;
     int64_t risk_nodes_ = 0, risk_tris_ = 0;   // the resident wide BVH's node and triangle counts
     float risk_cam_[3] = {0, 0, 0}, risk_light_[3] = {0, 0, 0};
-    float risk_G_ = 0.0f, risk_nl_ = 0.0f;
+    float risk_G_ = 0.0f, risk_nl_ = 0.0f, risk_nu_ = 0.0f;
     hipEvent_t risk_ev_ = nullptr;
     bool risk_ev_live_ = false;
     // sets P.wrisk (and risk_G / risk_nl) for the frame's camera and light, recomputing the bits on

@@ -40,6 +40,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <vector>
 
@@ -67,6 +68,14 @@ constexpr int W_WIDTH = 4;    // children per node
 #endif
 #ifndef W_SOUND_A
 #define W_SOUND_A 1
+#endif
+
+// host diagnostic counters (tools/variants.py build diag="-DW_DIAG=1"; rt_diag_read)
+#if defined(W_DIAG) && !defined(__HIP_DEVICE_COMPILE__)
+inline std::atomic<long long> g_wdiag[8];
+#define W_DIAG_ADD(i, v) rt::g_wdiag[i].fetch_add((long long)(v), std::memory_order_relaxed)
+#else
+#define W_DIAG_ADD(i, v) ((void)0)
 #endif
 
 #ifndef W_STEP_HOOK
@@ -322,49 +331,67 @@ RT_HD bool kdop_certifies(const GNode& nd, v3 o, v3 d, float t)
 RT_HD uint32_t fbits(float f) { return __builtin_bit_cast(uint32_t, f); }
 RT_HD float bitsf(uint32_t u) { return __builtin_bit_cast(float, u); }
 
-// Grazing risk of a triangle for a point X ("risk bits"): false only when no ray
-// of the kind X stands for can make the triangle report a hit in case (b) of wbvh_closest (|cos(n,
-// d)| < QS).  Case (b) puts the ray's origin o within H0 = 1.01 (QS + 8u) (L + |o - a|) / s2 of the
-// triangle's plane (s2 = sin(alpha' / 2) as the build's ext byte 1, L = the longer edge).
-//   camera (G = 0, nu = 0): the rays start at X itself;
-//   light: the rays start at o with |X - o| <= G and pass within nu of X with their direction within
-//          QS of the plane's, so X lies within H0(|X - a| + G) + QS G + nu of the plane.
+// Grazing risk of a triangle for a point X ("risk keys"): INFINITY when no ray of the
+// kind X stands for can make the triangle report a hit in case (b) of wbvh_closest (|cos(n, d)| = q <
+// QS); otherwise a key K >= 0 such that every hit it reports in case (b) has
+//   t' >= (K - QS hi - nu) / (QS |d|)      (camera: t' >= K / (QS |d|)).
+// Case (b) puts the ray's origin o within H0 = 1.01 (QS + 8u) (L + |o - a|) / s2 of the triangle's
+// plane (s2 = sin(alpha' / 2) as the build's ext byte 1, L = the longer edge).  And with s = sin(alpha)
+// and u = 2^-24, Moller-Trumbore's float quantities (triangle.cpp:25-91; stored normal n within
+// 2.83u |ab||ac| of the exact one) satisfy |Mdet| <= (q + 6u/s) |n~||d| and |n . OA| >= |n~| (dist(o) -
+// cN |o - a|), cN = (6/s + 1.2)u, so a reported t' >= (dist(o) - cN |o - a|) / ((QS + 6u/s) |d|) (1 - 2.01u).
+//   camera (G = 0, nu = 0): the rays start at X itself: K = (dist(X) - cN |X - a|) / f, f = 1 + 6u/(s QS);
+//   light: the rays start at o with |X - o| <= hi <= G and their lines pass within nu of X, so
+//          dist(o) >= dist(X) - QS hi - nu and |o - a| <= |X - a| + G: K = (dist(X) - cN (|X - a| + G)) / f;
+//          X lies within H0(|X - a| + G) + QS G + nu of the plane when it is at risk at all.
 // slack >= the query's box margin m for those rays.  In double from the record's float edges (the
-// products exact, each difference rounded once); a degenerate record (no s2 bound) is always at
-// risk, one whose stored normal is zero never (Mdet = 0: never a hit).
-RT_HD bool wbvh_risk_tri(const GTri& t, double px, double py, double pz, double G, double nu, double slack, double QS)
+// products exact, each difference rounded once); the key is rounded down to float (0 when negative).
+// A degenerate record (no s2 bound) is always at risk with key 0, one whose stored normal is zero
+// never (Mdet = 0: never a hit).
+RT_HD float wbvh_risk_key(const GTri& t, double px, double py, double pz, double G, double nu, double slack, double QS)
 {
     if (t.n[0] == 0.0f && t.n[1] == 0.0f && t.n[2] == 0.0f)
-        return false;
+        return INFINITY;
     const double x0 = t.ab[0], x1 = t.ab[1], x2 = t.ab[2], y0 = t.ac[0], y1 = t.ac[1], y2 = t.ac[2];
     const double c0 = x1 * y2 - x2 * y1, c1 = x2 * y0 - x0 * y2, c2 = x0 * y1 - x1 * y0;
     const double la = sqrt(x0 * x0 + x1 * x1 + x2 * x2), lc = sqrt(y0 * y0 + y1 * y1 + y2 * y2);
     const double cl = sqrt(c0 * c0 + c1 * c1 + c2 * c2);
     if (!(la * lc > 0x1p-100) || !(cl > 0x1p-50 * la * lc))
-        return true;
+        return 0.0f;
     const double ca = fabs(x0 * y0 + x1 * y1 + x2 * y2) / (la * lc);
     const double s2 = sqrt(fmax(0.0, (1.0 - fmin(1.0, ca + 1e-12)) / 2.0)) * (1 - 1e-9);
-    if (!(s2 > 0.0))
-        return true;
+    const double sa = cl / (la * lc) * (1 - 1e-9);
+    if (!(s2 > 0.0) || !(sa > 0.0))
+        return 0.0f;
     const double ax = px - (double)t.a[0], ay = py - (double)t.a[1], az = pz - (double)t.a[2];
     const double Da = sqrt(ax * ax + ay * ay + az * az);
     const double dist = fabs(c0 * ax + c1 * ay + c2 * az) / cl;
     const double L = fmax(la, lc) * (1 + 1e-12);
     const double rhs = (1.01 * (QS + 8.0 * 0x1p-24) * (L + Da + G + slack) / s2 + QS * G + nu) * (1 + 1e-6);
-    return !(dist > rhs);
+    if (dist > rhs)
+        return INFINITY;
+    if (!(dist <= rhs))
+        return 0.0f;   // NaN
+    const double cN = (6.0 / sa + 1.2) * 0x1p-24 * 1.01;
+    const double K = (dist * (1 - 1e-9) - cN * (Da + G + slack)) / (1.0 + 6.0 * 0x1p-24 / (sa * QS)) * (1 - 1e-6);
+    if (!(K > 0.0))
+        return 0.0f;
+    const float f = (float)K;
+    return (double)f > K ? nextafterf(f, 0.0f) : f;
 }
 
 // A frame's two risk points (kernels.hip wide_risk_kernel): sel 0 the camera (rays start at it), sel
 // 1 the light (shadow rays: o = p + 1e-4 n, d = normalize(light - p), renderer.cpp:340-402, for hit
-// points p in the scene box [lo, hi]).  The shadow rays that may use the light's bits are the ones
+// points p in the scene box [lo, hi]).  The shadow rays that may use the light's keys are the ones
 // whose segment bound hi (kernels.hip is_shadowed, >= |light - o|) is <= ray_G and whose normal has
 // |n|_1 <= ray_nl: their lines pass within nu = 1.001e-4 ray_nl + 16u G of the light (the offset
-// and normalize's rounding).  slack >= the query's margin m for the kind's origins.
+// and normalize's rounding; ray_nu: nu rounded up).  slack >= the query's margin m for the kind's
+// origins.
 struct WRiskArgs {
     double p[2][3];
     double G[2], nu[2], slack[2], QS[2];
     int32_t on[2];
-    float ray_G, ray_nl;
+    float ray_G, ray_nl, ray_nu;
 };
 
 inline WRiskArgs wbvh_risk_args(const float lo[3], const float hi[3], float S, const float cam[3], const float light[3],
@@ -395,6 +422,7 @@ inline WRiskArgs wbvh_risk_args(const float lo[3], const float hi[3], float S, c
     A.QS[0] = qs_cam;
     A.G[1] = G;
     A.nu[1] = 1.001e-4 * A.ray_nl + 16.0 * 0x1p-24 * G;
+    A.ray_nu = std::nextafter((float)(A.nu[1] * (1 + 1e-6)), INFINITY);
     A.slack[1] = 1.01 * 0x1p-16 * (lm + G + S);
     A.QS[1] = qs_light;
     const bool fin = std::isfinite(cm) && std::isfinite(lm) && std::isfinite(G);
@@ -402,26 +430,36 @@ inline WRiskArgs wbvh_risk_args(const float lo[3], const float hi[3], float S, c
     return A;
 }
 
-// The per-point risk bits of the wide BVH: bit (j + 4 sel) of risk[node] is set when child j holds a
-// triangle at risk for point sel.  Host version of kernels.hip wide_risk_kernel (tests, rt_wbvh_query_ex).
-inline void wbvh_risk_host(const WBvh& w, const WRiskArgs& A, int sel, std::vector<uint32_t>& risk)
+// rsub of wbvh_closest for a shadow ray with |light - o| <= h (rounded up)
+RT_HD float wrisk_sub(float QS, float h, float nu)
 {
-    risk.resize(w.nodes.size(), 0u);
-    if (!A.on[sel]) {   // no bound: every child at risk
-        for (auto& r : risk)
-            r |= 0xFu << (4 * sel);
+    return __builtin_fmaf(QS, h, nu) * (1.0f + 0x1p-20f);
+}
+
+// The per-point risk keys of the wide BVH: risk[(2 node + sel) 4 + j] = the smallest key
+// (wbvh_risk_key) of child j's triangles for point sel, INFINITY when none is at risk.  The keys of a
+// triangle go up its leaf entry's parent chain with a minimum, stopping where the stored key is already
+// no larger.  Host version of kernels.hip wide_risk_kernel (tests, rt_wbvh_query_ex).
+inline void wbvh_risk_host(const WBvh& w, const WRiskArgs& A, int sel, std::vector<float>& risk)
+{
+    risk.resize(w.nodes.size() * 8, INFINITY);
+    if (!A.on[sel]) {   // no bound: every child at risk, key 0
+        for (size_t v = 0; v < w.nodes.size(); v++)
+            for (int j = 0; j < 4; j++)
+                risk[(2 * v + sel) * 4 + j] = 0.0f;
         return;
     }
     for (size_t k = 0; k < w.tris.size(); k++) {
-        if (!wbvh_risk_tri(w.tris[k], A.p[sel][0], A.p[sel][1], A.p[sel][2], A.G[sel], A.nu[sel], A.slack[sel], A.QS[sel]))
+        const float K = wbvh_risk_key(w.tris[k], A.p[sel][0], A.p[sel][1], A.p[sel][2], A.G[sel], A.nu[sel],
+                                      A.slack[sel], A.QS[sel]);
+        if (!(K < INFINITY))
             continue;
         uint32_t e = w.tri_leaf[k];
         while (e != W_EMPTY) {
-            const uint32_t bit = 1u << ((e & 3u) + 4 * sel);
-            uint32_t& r = risk[e >> 2];
-            if (r & bit)
+            float& r = risk[(2 * (size_t)(e >> 2) + sel) * 4 + (e & 3u)];
+            if (r <= K)
                 break;
-            r |= bit;
+            r = K;
             e = w.parent[e >> 2];
         }
     }
@@ -440,115 +478,6 @@ struct WStackLocal {   // host
     RT_HD void put(int i, uint2 v) { e[i] = v; }
     RT_HD uint2 get(int i) const { return e[i]; }
 };
-
-// Case (b) of wbvh_closest's child test (the triangles with q < QS), out of line: its state stays
-// out of the traversal loop's registers; it re-reads the node (in cache).  Returns the child's key
-// (the smallest t of a reported point it allows), or INFINITY.
-#if defined(__HIP_DEVICE_COMPILE__)
-__device__ __forceinline__
-#else
-inline
-#endif
-float wq_case_b(const WNode* node, int j, v3 o, v3 d, float ix, float iy, float iz, float m, float QS, float dl,
-                float best_s, float a, float qa, float iq)
-{
-    constexpr float SL = 0x1p-20f;
-    constexpr float U = 0x1p-24f;
-    constexpr float NLH = 127.9f;
-    // the node's words straight from memory (in cache: the traversal just read them)
-    const uint32_t* Wp = reinterpret_cast<const uint32_t*>(node);
-    auto W = [&](int i) -> uint32_t { return ldg(Wp + i); };
-    const bool nx_lo = !(ix < 0.0f), ny_lo = !(iy < 0.0f), nz_lo = !(iz < 0.0f);
-    const float ss = bitsf(W(WN_SS)), slo = bitsf(W(WN_SS + 1));
-    const uint32_t ex = W(3);
-    const float stx = bitsf((ex & 0xffu) << 23), sty = bitsf(((ex >> 8) & 0xffu) << 23),
-                stz = bitsf(((ex >> 16) & 0xffu) << 23);
-    const float sx = stx * ix, sy = sty * iy, sz = stz * iz;
-    const float Dx = bitsf(W(0)) - o.x, Dy = bitsf(W(1)) - o.y, Dz = bitsf(W(2)) - o.z;
-    const int sh = 8 * (j & 3);
-    const float qlx = (float)((W(WN_QLO + 0) >> sh) & 0xffu), qhx = (float)((W(WN_QHI + 0) >> sh) & 0xffu);
-    const float qly = (float)((W(WN_QLO + 1) >> sh) & 0xffu), qhy = (float)((W(WN_QHI + 1) >> sh) & 0xffu);
-    const float qlz = (float)((W(WN_QLO + 2) >> sh) & 0xffu), qhz = (float)((W(WN_QHI + 2) >> sh) & 0xffu);
-    const uint32_t nrj = W(WN_NRM + j);
-    const float nx = (float)(int8_t)(nrj & 0xffu), ny = (float)(int8_t)((nrj >> 8) & 0xffu),
-                nz = (float)(int8_t)((nrj >> 16) & 0xffu);
-    const uint32_t e = W(WN_EXT + j), e2 = W(WN_EXT2 + j), sbj = W(WN_SLAB + j);
-    const float sth = wq_val((e >> 16) & 0xffu, WQ_UNIT);
-    const float L = wq_len(e >> 24);
-    const float C0 = __builtin_fmaf((float)(sbj & 0xffffu), ss, slo);
-    const float C1 = __builtin_fmaf((float)(sbj >> 16), ss, slo);
-    const float b = nx * Dx + ny * Dy + nz * Dz;   // N . (origin - o)
-    auto box = [&](float M, float& tmin, float& tmax) {
-        const float mx = nx_lo ? M : -M, my = ny_lo ? M : -M, mz = nz_lo ? M : -M;
-        const float tnx = __builtin_fmaf(nx_lo ? qlx : qhx, sx, (Dx - mx) * ix);
-        const float tny = __builtin_fmaf(ny_lo ? qly : qhy, sy, (Dy - my) * iy);
-        const float tnz = __builtin_fmaf(nz_lo ? qlz : qhz, sz, (Dz - mz) * iz);
-        const float tfx = __builtin_fmaf(nx_lo ? qhx : qlx, sx, (Dx + mx) * ix);
-        const float tfy = __builtin_fmaf(ny_lo ? qhy : qly, sy, (Dy + my) * iy);
-        const float tfz = __builtin_fmaf(nz_lo ? qhz : qlz, sz, (Dz + mz) * iz);
-        tmin = fmaxf(fmaxf(tnx, tny), tnz);
-        tmax = fminf(fminf(tfx, tfy), tfz);
-    };
-    float key = INFINITY;
-    const float s2 = wq_val((e >> 8) & 0xffu, WQ_UNIT);
-    const float rho = wq_len(e2 & 0xffu);
-    const float M = m + rho;
-    float umin, umax;
-    box(M, umin, umax);   // the octree leaves' reach, any t
-    bool okb = !(umin > __builtin_fmaf(fabsf(umax), SL, umax));
-    // distances from o: the child box's farthest corner (>= |o - a|), and the
-    // widened box's (>= |x - o|) and diameter
-    const float ax0 = __builtin_fmaf(qlx, stx, Dx), ax1 = __builtin_fmaf(qhx, stx, Dx);
-    const float ay0 = __builtin_fmaf(qly, sty, Dy), ay1 = __builtin_fmaf(qhy, sty, Dy);
-    const float az0 = __builtin_fmaf(qlz, stz, Dz), az1 = __builtin_fmaf(qhz, stz, Dz);
-    const float ex0 = fmaxf(fabsf(ax0), fabsf(ax1)), ey0 = fmaxf(fabsf(ay0), fabsf(ay1)),
-                ez0 = fmaxf(fabsf(az0), fabsf(az1));
-    const float Dm = sqrtf(ex0 * ex0 + ey0 * ey0 + ez0 * ez0) * (1.0f + 0x1p-16f) + m;
-    const float H0 = 1.01f * (QS + 8.0f * U) * (L + Dm) / s2;
-    if (okb) {
-        // the origin: N . (o - origin) = -b within the slab widened by H0 + Dm sin(theta)
-        const float w = NLH * (H0 + __builtin_fmaf(Dm, sth, m)) * (1.0f + 0x1p-16f) + 384.0f * m;
-        okb = !(-b < C0 - w || -b > C1 + w);
-    }
-    if (okb) {
-        // the line where it crosses the widened box: within H0 + QS |x - o| of the
-        // triangle's plane, which lies within diam sin(theta) of the slab there
-        const float Dr = Dm + 1.733f * M, dg = sqrtf((ax1 - ax0) * (ax1 - ax0) + (ay1 - ay0) * (ay1 - ay0) +
-                                                      (az1 - az0) * (az1 - az0)) + 3.47f * M;
-        const float Hl = H0 + QS * Dr + dg * sth * 1.01f + m;
-        const float w = NLH * Hl * (1.0f + 0x1p-16f) + 384.0f * m;
-        const float ia = fast_rcp(a);
-        const float s0 = (C0 - w + b) * ia, s1 = (C1 + w + b) * ia;
-        umin = fmaxf(umin, fminf(s0, s1));
-        umax = fminf(umax, fmaxf(s0, s1));
-        okb = !(umin > __builtin_fmaf(fabsf(umax), SL, umax));
-    }
-    if (okb) {
-        // the reported point p' = o + t d, 0 <= t <= best: N . (p' - origin) in
-        // [C0, C1] widened by w0 + w1 t (eta and the tilt over |p' - a| <= Dm + t |d|)
-        const float ke = U * __builtin_fmaf(8.0f * qa, iq, 5.0f) + 1.01f * sth;
-        const float w0 = NLH * __builtin_fmaf(ke, Dm, m) * (1.0f + 0x1p-16f) + 384.0f * m;
-        const float w1 = NLH * ke * dl * (1.0f + 0x1p-16f);
-        const float al = C1 + w0 + b, be = C0 - w0 + b;   // S0 = -b
-        float lo = 0.0f, up = best_s;
-        const float pa = a - w1, pb = a + w1;
-        if (pa > 0.0f)
-            up = fminf(up, al / pa * (1.0f + 0x1p-20f));
-        else if (pa < 0.0f)
-            lo = fmaxf(lo, al / pa * (1.0f - 0x1p-20f));
-        else if (al < 0.0f)
-            lo = INFINITY;
-        if (pb > 0.0f)
-            lo = fmaxf(lo, be / pb * (1.0f - 0x1p-20f));
-        else if (pb < 0.0f)
-            up = fminf(up, be / pb * (1.0f + 0x1p-20f));
-        else if (be > 0.0f)
-            lo = INFINITY;
-        if (!(lo > up))
-            key = fminf(key, lo == lo ? fminf(lo, 3.0e38f) : 0.0f);
-    }
-    return key;
-}
 
 // Closest hit over the wide BVH for the ray (o, d) among hits with t <= hi.  m: box margin
 // (2^-16 (max|o| + scene scale), the leaf-slab margin of kernels.hip leaf_missed).
@@ -575,13 +504,16 @@ float wq_case_b(const WNode* node, int j, v3 o, v3 d, float ix, float iy, float 
 //       widened by rho), and p' = o + t d (0 <= t <= best) lies within eta + sin(theta) |p' - a|
 //       of the child's slab.  A child passing all three is entered, keyed by the smallest such t.
 // Robustly back-facing children (the cone) report nothing and are skipped as before.
-// risk (optional): the risk bits of the ray's kind rsel (wbvh_risk_host / kernels.hip
-// wide_risk_kernel); a child whose bit is clear holds no triangle that can report a hit in case (b)
-// for this ray, so (b) is skipped for it.  The caller guarantees the ray is of that kind.
+// risk (optional): the risk keys of the ray's kind rsel (wbvh_risk_key / wbvh_risk_host / kernels.hip
+// wide_risk_kernel): a child whose key is INFINITY holds no triangle that can report a hit in case (b)
+// for this ray, and none of its (b) reports has t' below (key - rsub) / (QS |d|), so (b) is skipped for
+// it when that exceeds the best hit.  rsub: 0 for the camera (rsel 0); for the light (rsel 1), at least
+// QS h + nu with h >= |light - o| and nu the frame's (WRiskArgs::ray_nu; wrisk_sub).  The caller
+// guarantees the ray is of that kind.
 template <class Stack>
 RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m, Stack& stk, WHit& h,
                        uint32_t* work = nullptr, float hi = INFINITY, bool ties = true, float QS = 0x1p-8f,
-                       const uint32_t* risk = nullptr, int rsel = 0)
+                       const float* risk = nullptr, int rsel = 0, float rsub = 0.0f)
 {
     h.t = INFINITY;
     h.u = 1.0f;
@@ -598,6 +530,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
     // per axis, the byte row of the entry (near) planes: q_lo where the direction is positive,
     // q_hi where it is negative; the near plane is widened by -M sign(d), the far one by +M sign(d)
     const bool nx_lo = !(ix < 0.0f), ny_lo = !(iy < 0.0f), nz_lo = !(iz < 0.0f);
+    const float aix = fabsf(ix), aiy = fabsf(iy), aiz = fabsf(iz);
 
     constexpr float SL = 0x1p-20f;   // relative slack over the rounding of a slab parameter (<= 3 ulp)
     constexpr float U = 0x1p-24f;
@@ -606,6 +539,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
     const float dl = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z) * (1.0f + 0x1p-20f);
     const float cstep = dl * W_CONE_STEP;
     const float icp = (1.0f - 0x1p-18f) / (NLH * dl);   // cos(angle(N, -d)) >= -a icp
+    const float iqd = (1.0f - 0x1p-20f) / (QS * dl);        // a risk key's t bound: key / (QS |d|)
     float best_s = hi + fabsf(hi) * SL;   // h.t (or hi) plus slack: a child entered at or below it may hold a hit
     bool tie = false, nanhit = false, infhit = false, overflow = false;
     int sp = 0;
@@ -618,11 +552,15 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
         // if-if: every lane takes one step (inner node or leaf) per iteration
         if (!(cur & W_LEAF)) {
             nn++;
+            W_DIAG_ADD(0, 1);
             W_STEP_HOOK(cur, 0);
             const uint4* p = reinterpret_cast<const uint4*>(nodes + cur);
-            uint4 Rw[WN_ROWS];
+            // every row but the last (ext2: rho, read by case (b) alone, per lane when it runs)
+            constexpr int NR = WN_EXT2 / 4;
+            static_assert(WN_EXT2 % 4 == 0 && NR == WN_ROWS - 1, "ext2 is the node's last row");
+            uint4 Rw[NR];
 #pragma unroll
-            for (int i = 0; i < WN_ROWS; i++)
+            for (int i = 0; i < NR; i++)
                 Rw[i] = ldg(p + i);
             // word i of the node (compile-time i)
             auto wd = [&](int i) -> uint32_t {
@@ -636,6 +574,23 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
             // t of a plane origin + q s (widened by M) = q (s / d) + (origin - o -+ M) / d
             const float sx = stx * ix, sy = sty * iy, sz = stz * iz;
             const float Dx = bitsf(wd(0)) - o.x, Dy = bitsf(wd(1)) - o.y, Dz = bitsf(wd(2)) - o.z;
+            const float bx = Dx * ix, by = Dy * iy, bz = Dz * iz;
+            // per axis, the byte rows of the entry (near) and exit (far) planes: q_lo where the direction
+            // is positive, q_hi where it is negative (one select per node and row)
+            constexpr int QW = W_WIDTH / 4;   // words per axis row of quantised planes
+            uint32_t nwx[QW], fwx[QW], nwy[QW], fwy[QW], nwz[QW], fwz[QW];
+#pragma unroll
+            for (int jw = 0; jw < QW; jw++) {
+                const uint32_t lx = wd(WN_QLO + 0 * QW + jw), hx = wd(WN_QHI + 0 * QW + jw);
+                const uint32_t ly = wd(WN_QLO + 1 * QW + jw), hy = wd(WN_QHI + 1 * QW + jw);
+                const uint32_t lz = wd(WN_QLO + 2 * QW + jw), hz = wd(WN_QHI + 2 * QW + jw);
+                nwx[jw] = nx_lo ? lx : hx;
+                fwx[jw] = nx_lo ? hx : lx;
+                nwy[jw] = ny_lo ? ly : hy;
+                fwy[jw] = ny_lo ? hy : ly;
+                nwz[jw] = nz_lo ? lz : hz;
+                fwz[jw] = nz_lo ? hz : lz;
+            }
             // D: o to the farthest corner of the node's frame [origin, origin + 255 step]
             float Dn;
             {
@@ -645,10 +600,15 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                 Dn = sqrtf(fx * fx + fy * fy + fz * fz) * (1.0f + 0x1p-16f) + m;
             }
             const float RA = U * 30.4f * Dn, RB = U * 2.01f * Dn;
-            // the children that may hold a triangle at risk for this ray's kind (wbvh_risk_tri): the
-            // others skip case (b)
-            const uint32_t rbits = risk ? ldg(risk + cur) >> (4 * rsel) : 0xFu;
-            constexpr int QW = W_WIDTH / 4;   // words per axis row of quantised planes
+            // the children's risk keys for this ray's kind (wbvh_risk_key): INFINITY skips case (b)
+            float rk[W_WIDTH] = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (risk) {
+                const float4 r4 = ldg(reinterpret_cast<const float4*>(risk) + (2 * (size_t)cur + rsel));
+                rk[0] = r4.x;
+                rk[1] = r4.y;
+                rk[2] = r4.z;
+                rk[3] = r4.w;
+            }
             float key[W_WIDTH];
             uint32_t ref[W_WIDTH];
 #pragma unroll
@@ -683,20 +643,18 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
 #else
                     const float R = m + 0.0f * Bq * Aq;
 #endif
-                    const uint32_t lx = wd(WN_QLO + 0 * QW + jw), hx = wd(WN_QHI + 0 * QW + jw);
-                    const uint32_t ly = wd(WN_QLO + 1 * QW + jw), hy = wd(WN_QHI + 1 * QW + jw);
-                    const uint32_t lz = wd(WN_QLO + 2 * QW + jw), hz = wd(WN_QHI + 2 * QW + jw);
-                    const float qlx = (float)((lx >> sh) & 0xffu), qhx = (float)((hx >> sh) & 0xffu);
-                    const float qly = (float)((ly >> sh) & 0xffu), qhy = (float)((hy >> sh) & 0xffu);
-                    const float qlz = (float)((lz >> sh) & 0xffu), qhz = (float)((hz >> sh) & 0xffu);
+                    // the entry / exit planes' t of this child's box widened by M:
+                    // q (s / d) + (origin - o) / d -+ M / |d| per axis
+                    const float qnx = (float)((nwx[jw] >> sh) & 0xffu), qfx = (float)((fwx[jw] >> sh) & 0xffu);
+                    const float qny = (float)((nwy[jw] >> sh) & 0xffu), qfy = (float)((fwy[jw] >> sh) & 0xffu);
+                    const float qnz = (float)((nwz[jw] >> sh) & 0xffu), qfz = (float)((fwz[jw] >> sh) & 0xffu);
                     auto box = [&](float M, float& tmin, float& tmax) {
-                        const float mx = nx_lo ? M : -M, my = ny_lo ? M : -M, mz = nz_lo ? M : -M;
-                        const float tnx = __builtin_fmaf(nx_lo ? qlx : qhx, sx, (Dx - mx) * ix);
-                        const float tny = __builtin_fmaf(ny_lo ? qly : qhy, sy, (Dy - my) * iy);
-                        const float tnz = __builtin_fmaf(nz_lo ? qlz : qhz, sz, (Dz - mz) * iz);
-                        const float tfx = __builtin_fmaf(nx_lo ? qhx : qlx, sx, (Dx + mx) * ix);
-                        const float tfy = __builtin_fmaf(ny_lo ? qhy : qly, sy, (Dy + my) * iy);
-                        const float tfz = __builtin_fmaf(nz_lo ? qhz : qlz, sz, (Dz + mz) * iz);
+                        const float tnx = __builtin_fmaf(-M, aix, __builtin_fmaf(qnx, sx, bx));
+                        const float tny = __builtin_fmaf(-M, aiy, __builtin_fmaf(qny, sy, by));
+                        const float tnz = __builtin_fmaf(-M, aiz, __builtin_fmaf(qnz, sz, bz));
+                        const float tfx = __builtin_fmaf(M, aix, __builtin_fmaf(qfx, sx, bx));
+                        const float tfy = __builtin_fmaf(M, aiy, __builtin_fmaf(qfy, sy, by));
+                        const float tfz = __builtin_fmaf(M, aiz, __builtin_fmaf(qfz, sz, bz));
                         tmin = fmaxf(fmaxf(tnx, tny), tnz);
                         tmax = fminf(fminf(tfx, tfy), tfz);
                     };
@@ -725,8 +683,32 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                     }
                     if (ok)
                         key[j] = fminf(fmaxf(tmin, 0.0f), 3.0e38f);
-                    if (W_CASE_B && qlb < QS && ((rbits >> j) & 1u))   // (b): triangles that may lie nearly parallel to d
-                        key[j] = fminf(key[j], wq_case_b(nodes + cur, j, o, d, ix, iy, iz, m, QS, dl, best_s, a, qa, iq));
+                    W_DIAG_ADD(1, 1);
+                    W_DIAG_ADD(2, ok);
+                    // (b): triangles that may lie nearly parallel to d (q < QS), none of whose reports
+                    // precedes kbl (the risk key): the line must cross the octree leaves holding them
+                    // (the child box widened by rho, any t), and the origin must lie within H0 =
+                    // 1.01 (QS + 8u) (L + D) / s2 of a triangle's plane, so within H0 + D sin(theta)
+                    // of the child's slab (D = Dn >= |o - a|)
+                    const float kbl = (rk[j] - rsub) * iqd;
+                    if (W_CASE_B && qlb < QS && rk[j] < INFINITY && !(kbl > best_s)) {
+                        W_DIAG_ADD(4, 1);
+                        const uint32_t e2 = ldg(reinterpret_cast<const uint32_t*>(nodes + cur) + WN_EXT2 + j);
+                        float umin, umax;
+                        box(m + wq_len(e2 & 0xffu), umin, umax);
+                        bool okb = !(umin > __builtin_fmaf(fabsf(umax), SL, umax));
+                        if (okb) {
+                            const float s2 = wq_val((e >> 8) & 0xffu, WQ_UNIT);
+                            const float H0 = 1.01f * (QS + 8.0f * U) * (L + Dn) * fast_rcp(s2) * (1.0f + 0x1p-20f);
+                            const float w = NLH * (H0 + __builtin_fmaf(Dn, sth, m)) * (1.0f + 0x1p-16f) + 384.0f * m;
+                            okb = !(-b < C0 - w || -b > C1 + w);   // N . (o - origin) = -b
+                        }
+                        if (okb) {
+                            W_DIAG_ADD(3, !ok);
+                            W_DIAG_ADD(5, ok && kbl < key[j]);
+                            key[j] = fminf(key[j], fminf(fmaxf(kbl, 0.0f), 3.0e38f));
+                        }
+                    }
                 }
 #if defined(__HIP_DEVICE_COMPILE__)
                 // one child at a time: the scheduler would interleave the children's

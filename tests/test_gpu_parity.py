@@ -945,10 +945,11 @@ def test_camera_matrix_forms_match_oracle(R, cam):
     _check_vs_oracle(g, o, cam, R=R)
 
 
-def test_band_counters_across_self_resetting_launches(R):
-    """Band launches of the default trace path reset their slot's counters themselves (no memset
-    between frames, KParams::self_reset): repeated launches on one stream and on alternating
-    streams each report the frame's shadow-ray count and produce the same strips."""
+def test_band_counters_across_repeated_launches(R):
+    """Band launches of the default trace path each clear their stream slot's counters
+    (render_bands_device's hipMemsetAsync on the slot's stream before the launch): repeated
+    launches on one stream and on alternating streams each report the frame's shadow-ray count
+    and produce the same strips."""
     import torch
     from raytracercpp_amd import scenes
     sc, st = scenes.bumpy70k(width=160, height=96, enable_ssaa=True, ssaa_factor=2)
