@@ -504,18 +504,26 @@ int rt_wbvh_query_ex(const float* tri9, int64_t n, int32_t max_depth, int32_t le
                 S = std::max(S, std::max(std::fabs(f.nodes[0].dn[a]), std::fabs(f.nodes[0].df[a])));
         const bool usable = !w.nodes.empty() && S > 0x1p-20f && S < 0x1p20f;
         // the risk bits of the camera / light (renderer.cpp prepare_risk, kernels.hip wide_risk_kernel)
-        std::vector<float> risk;
+        std::vector<uint64_t> risk;
         rt::WRiskArgs RA{};
         if (usable && (cam || light)) {
             const float lo[3] = {f.nodes[0].dn[0], f.nodes[0].dn[1], f.nodes[0].dn[2]};
             const float hi[3] = {f.nodes[0].df[0], f.nodes[0].df[1], f.nodes[0].df[2]};
             const float zero[3] = {0, 0, 0};
             RA = rt::wbvh_risk_args(lo, hi, S, cam ? cam : zero, light ? light : zero, W_QS_CLOSEST, W_QS_SHADOW);
-            risk.assign(w.nodes.size() * 8, INFINITY);
+            risk.assign(w.nodes.size() * 8, rt::wrisk_pack(INFINITY, 0));
+            std::vector<float> lbox(6 * w.tris.size());
+            for (size_t k = 0; k < w.tris.size(); k++) {
+                const rt::GNode& L = f.nodes[w.leaf_of_k[k]];
+                for (int a = 0; a < 3; a++) {
+                    lbox[6 * k + a] = L.dn[a];
+                    lbox[6 * k + 3 + a] = L.df[a];
+                }
+            }
             if (cam)
-                rt::wbvh_risk_host(w, RA, 0, risk);
+                rt::wbvh_risk_host(w, lbox, RA, 0, risk);
             if (light)
-                rt::wbvh_risk_host(w, RA, 1, risk);
+                rt::wbvh_risk_host(w, lbox, RA, 1, risk);
         }
         std::atomic<int64_t> work_n{0}, work_t{0};
         auto body = [&](int64_t b, int64_t e) {
@@ -524,7 +532,7 @@ int rt_wbvh_query_ex(const float* tri9, int64_t n, int32_t max_depth, int32_t le
             for (int64_t i = b; i < e; i++) {
                 rt::v3 o = rt::mk(orig[3 * i], orig[3 * i + 1], orig[3 * i + 2]);
                 rt::v3 d = rt::mk(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]);
-                const float* rk = nullptr;
+                const uint64_t* rk = nullptr;
                 int rsel = 0;
                 float rsub = 0.0f;
                 if (shadow_rays) {

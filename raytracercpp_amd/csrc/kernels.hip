@@ -901,13 +901,6 @@ __device__ void count_wave_steps(const KParams& P, int base, uint32_t steps)
 }
 #endif
 
-// The grazing split of the wide query's child test (wbvh.hpp wbvh_closest QS) per query kind
-#ifndef W_QS_CLOSEST
-#define W_QS_CLOSEST 0x1p-8f
-#endif
-#ifndef W_QS_SHADOW
-#define W_QS_SHADOW 0x1p-8f
-#endif
 
 // BVH::intersect through the wide BVH and its certificate (wbvh.hpp).
 // Returns true with (h, r) = the reference's record and boolean when the query is
@@ -921,7 +914,7 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
     WStackLds stk{lv};
     WHit w;
     // a ray from the camera position reads the frame's camera risk keys
-    const float* rk = P.wrisk && o.x == P.cam_pos[0] && o.y == P.cam_pos[1] && o.z == P.cam_pos[2] ? P.wrisk : nullptr;
+    const uint64_t* rk = P.wrisk && o.x == P.cam_pos[0] && o.y == P.cam_pos[1] && o.z == P.cam_pos[2] ? P.wrisk : nullptr;
 #if RT_COUNT
     uint32_t wk[4] = {0, 0, 0, 0};
     const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, INFINITY, true,
@@ -988,7 +981,7 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
     const float om = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
     WStackLds stk{lv};
     WHit w;
-    const float* rk = light ? P.wrisk : nullptr;
+    const uint64_t* rk = light ? P.wrisk : nullptr;
     const float rsub = light ? wrisk_sub(W_QS_SHADOW, hi, P.risk_nu) : 0.0f;
 #if RT_COUNT
     uint32_t wk[4] = {0, 0, 0, 0};
@@ -2990,41 +2983,77 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void trace_colors_kernel(KParams P, 
 // The wide BVH's triangle records and their metadata, gathered on the device from the octree's
 // (already uploaded) instead of uploading 64 B per triangle again: wide-BVH triangle k is octree
 // slot s = slot[k]; wmeta[k] = {s, its octree leaf, its caller index, that triangle's material}.
-// The frame's grazing-risk keys (wbvh.hpp wbvh_risk_key / wbvh_risk_host / WRiskArgs):
-// one thread per wide-BVH triangle; a triangle at risk for point sel takes the minimum of its key
-// and its leaf child's, then of its parent entries', stopping where the stored key is already no
-// larger (the walk that stored it goes on to the root).  A point with no bound (A.on 0) gives every
-// child key 0.  risk[] is filled with INFINITY before the launch; non-negative float keys compare
-// as their bit patterns (vector atomics on global memory).
-__global__ __launch_bounds__(256) void wide_risk_kernel(const GTri* __restrict__ wtris,
+// The frame's grazing-risk words (wbvh.hpp wbvh_risk_key / wrisk_pack / wbvh_risk_host, DESIGN.md
+// 5.6): one thread per wide-BVH triangle; a triangle at risk for point sel takes the minimum of its
+// key and its leaf child's and the union of its octree leaf's axis box with the child's, then its
+// parent entries', stopping where both are already there (the walk that put them there goes on to
+// the root).  K (float bits; non-negative floats compare as their bit patterns) is filled with
+// INFINITY, B's lows with +INFINITY and highs with -INFINITY before the launch; wide_risk_pack_kernel
+// then packs them into the risk words.  A point with no bound (A.on 0) gives every child key 0 and its
+// whole frame.  Vector atomics on global memory.
+__device__ __forceinline__ float atomic_min_float(float* p, float v)
+{
+    return v >= 0.0f ? __int_as_float(atomicMin(reinterpret_cast<int*>(p), __float_as_int(v)))
+                     : __uint_as_float(atomicMax(reinterpret_cast<unsigned int*>(p), __float_as_uint(v)));
+}
+__device__ __forceinline__ float atomic_max_float(float* p, float v)
+{
+    return v >= 0.0f ? __int_as_float(atomicMax(reinterpret_cast<int*>(p), __float_as_int(v)))
+                     : __uint_as_float(atomicMin(reinterpret_cast<unsigned int*>(p), __float_as_uint(v)));
+}
+
+__global__ __launch_bounds__(256) void wide_risk_kernel(const GTri* __restrict__ wtris, const uint4* __restrict__ wmeta,
+                                                        const GNode* __restrict__ onodes,
                                                         const uint32_t* __restrict__ tri_leaf,
-                                                        const uint32_t* __restrict__ parent, uint32_t* risk, int n,
-                                                        int nnodes, WRiskArgs A)
+                                                        const uint32_t* __restrict__ parent, uint32_t* K, float* B, int n,
+                                                        WRiskArgs A)
 {
     const int k = (int)(blockIdx.x * 256 + threadIdx.x);
-    if (k < nnodes)
-        for (int sel = 0; sel < 2; sel++)
-            if (!A.on[sel])
-                for (int j = 0; j < 4; j++)
-                    atomicMin(risk + (2 * (size_t)k + sel) * 4 + j, 0u);
     if (k >= n)
         return;
     const GTri t = load_gtri(wtris + k);
     for (int sel = 0; sel < 2; sel++) {
         if (!A.on[sel])
             continue;
-        const float K = wbvh_risk_key(t, A.p[sel][0], A.p[sel][1], A.p[sel][2], A.G[sel], A.nu[sel], A.slack[sel],
-                                      A.QS[sel]);
-        if (!(K < INFINITY))
+        const float Kt = wbvh_risk_key(t, A.p[sel][0], A.p[sel][1], A.p[sel][2], A.G[sel], A.nu[sel], A.slack[sel],
+                                       A.QS[sel]);
+        if (!(Kt < INFINITY))
             continue;
-        const uint32_t kb = __builtin_bit_cast(uint32_t, K);
+        const GNode L = load_gnode(onodes + ldg(wmeta + k).y);   // the octree leaf of its certificate
+        const uint32_t kb = __builtin_bit_cast(uint32_t, Kt);
         uint32_t e = tri_leaf[k];
         for (int it = 0; it < 1024 && e != W_EMPTY; it++) {   // (a walk ends at the root)
-            if (atomicMin(risk + (2 * (size_t)(e >> 2) + sel) * 4 + (e & 3u), kb) <= kb)
+            const size_t i = (2 * (size_t)(e >> 2) + sel) * 4 + (e & 3u);
+            bool has = atomicMin(K + i, kb) <= kb;
+            float* b = B + 6 * i;
+            for (int a = 0; a < 3; a++) {
+                has = (atomic_min_float(b + a, L.dn[a]) <= L.dn[a]) & has;
+                has = (atomic_max_float(b + 3 + a, L.df[a]) >= L.df[a]) & has;
+            }
+            if (has)
                 break;
             e = parent[e >> 2];
         }
     }
+}
+
+__global__ __launch_bounds__(256) void wide_risk_pack_kernel(const WNode* __restrict__ wnodes,
+                                                             const uint32_t* __restrict__ K,
+                                                             const float* __restrict__ B, unsigned long long* risk,
+                                                             int nentries, WRiskArgs A)
+{
+    const int i = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (i >= nentries)
+        return;
+    const int sel = (i >> 2) & 1;
+    const float Ki = __builtin_bit_cast(float, K[i]);
+    if (!A.on[sel])
+        risk[i] = wrisk_pack(0.0f, 0xFFFFFF000000ull);
+    else if (Ki < INFINITY) {
+        const WNode nd = wnodes[i >> 3];
+        risk[i] = wrisk_pack(Ki, wrisk_qbox(nd, B + 6 * (size_t)i, B + 6 * (size_t)i + 3));
+    } else
+        risk[i] = wrisk_pack(INFINITY, 0);
 }
 
 __global__ __launch_bounds__(256) void wide_gather_kernel(const GTri* __restrict__ tris, const int32_t* __restrict__ slot,
@@ -3112,18 +3141,35 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(
     return hipGetLastError();
 }
 
-extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_wide_risk(const rt::GTri* wtris,
-                                                                                const uint32_t* tri_leaf,
-                                                                                const uint32_t* parent, uint32_t* risk,
-                                                                                int n, int nnodes,
-                                                                                const rt::WRiskArgs* A,
-                                                                                hipStream_t stream)
+// the walk's boxes: lows +INFINITY, highs -INFINITY
+__global__ __launch_bounds__(256) void risk_box_init_kernel(float* B, size_t n)
 {
-    const int m = n > nnodes ? n : nnodes;
-    if (m <= 0)
-        return hipSuccess;
-    hipLaunchKernelGGL(rt::wide_risk_kernel, dim3((m + 255) / 256), dim3(256), 0, stream, wtris, tri_leaf, parent, risk,
-                       n, nnodes, *A);
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < 6 * n)
+        B[i] = (i % 6) < 3 ? INFINITY : -INFINITY;
+}
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_risk_box_init(float* B, size_t nentries,
+                                                                                    hipStream_t stream)
+{
+    if (nentries > 0)
+        hipLaunchKernelGGL(risk_box_init_kernel, dim3((unsigned)((6 * nentries + 255) / 256)), dim3(256), 0, stream, B,
+                           nentries);
+    return hipGetLastError();
+}
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_wide_risk(
+    const rt::GTri* wtris, const uint4* wmeta, const rt::GNode* onodes, const rt::WNode* wnodes, const uint32_t* tri_leaf,
+    const uint32_t* parent, uint32_t* K, float* B, unsigned long long* risk, int n, int nnodes, const rt::WRiskArgs* A,
+    hipStream_t stream)
+{
+    if (n > 0)
+        hipLaunchKernelGGL(rt::wide_risk_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, wtris, wmeta, onodes,
+                           tri_leaf, parent, K, B, n, *A);
+    const int ne = 8 * nnodes;
+    if (ne > 0)
+        hipLaunchKernelGGL(rt::wide_risk_pack_kernel, dim3((ne + 255) / 256), dim3(256), 0, stream, wnodes, K, B, risk,
+                           ne, *A);
     return hipGetLastError();
 }
 

@@ -44,11 +44,11 @@ struct KParams {
     const GTri* wtris;           // octree records in wide-BVH leaf order
     const uint4* wmeta;          // wide-BVH triangle k -> {octree GTri slot, flattened octree leaf node (its
                                  // certificate's k-DOP), caller triangle index, material}
-    // the frame's grazing-risk keys (wbvh.hpp wbvh_risk_key; nullptr: every child runs case (b)):
+    // the frame's grazing-risk words (wbvh.hpp wrisk_pack; nullptr: every child runs the full case (b)):
     // wrisk[(2 node + sel) 4 + j], sel 0 for rays from cam_pos, 1 for shadow rays towards light whose
     // segment bound hi <= risk_G and normal |n|_1 <= risk_nl (kernels.hip is_shadowed); risk_nu: the
     // light's nu (WRiskArgs::ray_nu)
-    const float* wrisk;
+    const uint64_t* wrisk;
     float risk_G, risk_nl, risk_nu;
     int32_t nnodes;
     int32_t ntri_slots;       // GTri count (brute-force loop bound when enable_bvh == 0)

@@ -22,6 +22,8 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_stage
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_keys(const rt::KParams* P, const rt::FrameRec* fr,
                                                                          int n, uint32_t* keys, int32_t* idx,
                                                                          hipStream_t stream);
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_risk_box_init(float* B, size_t nentries,
+                                                                                    hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_trace_rays(const rt::KParams* P, const float* o, const float* d, int n, int32_t* id,
                                            float* t, float* u, float* v, uint8_t* ret, hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_trace_colors(const rt::KParams* P, bool refl,
@@ -40,12 +42,10 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ssao(const
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_wide_gather(
     const rt::GTri* tris, const int32_t* slot, const uint32_t* leaf_of_slot, const int32_t* tri_id,
     const int32_t* tri_mat, int n, rt::GTri* wtris, uint4* wmeta, hipStream_t stream);
-extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_wide_risk(const rt::GTri* wtris,
-                                                                                const uint32_t* tri_leaf,
-                                                                                const uint32_t* parent, uint32_t* risk,
-                                                                                int n, int nnodes,
-                                                                                const rt::WRiskArgs* A,
-                                                                                hipStream_t stream);
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_wide_risk(
+    const rt::GTri* wtris, const uint4* wmeta, const rt::GNode* onodes, const rt::WNode* wnodes, const uint32_t* tri_leaf,
+    const uint32_t* parent, uint32_t* K, float* B, unsigned long long* risk, int n, int nnodes, const rt::WRiskArgs* A,
+    hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_downscale(const uint32_t* in, int w, int h_rows, int f, uint32_t* out,
                                           hipStream_t stream);
 
@@ -612,7 +612,7 @@ void Renderer::start_accel()
             if ((e = d_wnodes_.reserve(wn)) == hipSuccess && (e = d_wtris_.reserve(nk * sizeof(GTri))) == hipSuccess &&
                 (e = d_wmeta_.reserve(nk * 16)) == hipSuccess && (e = d_wtmp_.reserve(nk * 8)) == hipSuccess &&
                 (e = d_wlinks_.reserve(nl * 4)) == hipSuccess &&
-                (e = d_wrisk_.reserve(wb_.nodes.size() * 32)) == hipSuccess &&
+                (e = d_wrisk_.reserve(wb_.nodes.size() * 288)) == hipSuccess &&
                 (e = hipMemcpyAsync(d_wlinks_.p, wb_.tri_leaf.data(), wb_.tri_leaf.size() * 4, hipMemcpyHostToDevice,
                                     accel_stream_)) == hipSuccess &&
                 (e = hipMemcpyAsync(d_wlinks_.as<uint32_t>() + wb_.tri_leaf.size(), wb_.parent.data(),
@@ -731,7 +731,7 @@ int Renderer::adopt_from_lead()
             copy(d_wmeta_, L.d_wmeta_, L.wb_.slot.size() * 16);
             copy(d_wlinks_, L.d_wlinks_, (L.wb_.tri_leaf.size() + L.wb_.parent.size()) * 4);
             if (e == hipSuccess)
-                e = d_wrisk_.reserve(L.wb_.nodes.size() * 32);
+                e = d_wrisk_.reserve(L.wb_.nodes.size() * 288);
         }
         if (e == hipSuccess)
             e = hipStreamSynchronize(stream_);
@@ -1746,10 +1746,15 @@ int Renderer::prepare_risk(KParams& P, hipStream_t stream)
         const WRiskArgs A = wbvh_risk_args(lo, hi, P.scene_scale, P.cam_pos, P.light, W_QS_CLOSEST, W_QS_SHADOW);
         risk_valid_ = false;
         const uint32_t* links = d_wlinks_.as<uint32_t>();
-        if ((e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_wrisk_.p), 0x7F800000, (size_t)risk_nodes_ * 8,
-                                   stream)) != hipSuccess ||
-            (e = rt_launch_wide_risk(P.wtris, links, links + risk_tris_, d_wrisk_.as<uint32_t>(), (int)risk_tris_,
-                                     (int)risk_nodes_, &A, stream)) != hipSuccess ||
+        // d_wrisk_: the packed words (8 x 8 B per node), then the walk's keys (8 x 4 B) and boxes (8 x 24 B)
+        const size_t ne = (size_t)risk_nodes_ * 8;
+        unsigned long long* words = d_wrisk_.as<unsigned long long>();
+        uint32_t* K = reinterpret_cast<uint32_t*>(words + ne);
+        float* B = reinterpret_cast<float*>(K + ne);
+        if ((e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(K), 0x7F800000, ne, stream)) != hipSuccess ||
+            (e = rt_launch_risk_box_init(B, ne, stream)) != hipSuccess ||
+            (e = rt_launch_wide_risk(P.wtris, P.wmeta, P.nodes, P.wnodes, links, links + risk_tris_, K, B, words,
+                                     (int)risk_tris_, (int)risk_nodes_, &A, stream)) != hipSuccess ||
             (e = hipEventRecord(risk_ev_, stream)) != hipSuccess)
             return hip_fail(e, "wide_risk_kernel");
         risk_ev_live_ = true;
@@ -1761,7 +1766,7 @@ int Renderer::prepare_risk(KParams& P, hipStream_t stream)
         risk_nu_ = A.ray_nu;
     } else if (risk_ev_live_ && (e = hipStreamWaitEvent(stream, risk_ev_, 0)) != hipSuccess)
         return hip_fail(e, "hipStreamWaitEvent (risk bits)");
-    P.wrisk = d_wrisk_.as<float>();
+    P.wrisk = d_wrisk_.as<uint64_t>();
     P.risk_G = risk_G_;
     P.risk_nl = risk_nl_;
     P.risk_nu = risk_nu_;

@@ -51,20 +51,29 @@ namespace rt {
 constexpr uint32_t W_LEAF = 0x80000000u;
 constexpr uint32_t W_EMPTY = 0xFFFFFFFFu;
 constexpr int W_MAX_LEAF = 8;
-constexpr int W_STACK = 16;   // traversal stack entries per lane (overflow: the query is not certified)
+#ifndef W_STACK_N
+#define W_STACK_N 16
+#endif
+constexpr int W_STACK = W_STACK_N;   // traversal stack entries per lane (overflow: the query is not certified)
 constexpr int W_WIDTH = 4;    // children per node
 
-// the grazing split QS of the wide query's child test per query kind (wbvh_closest, wbvh_risk_tri)
+// the grazing split QS of the wide query's child test per query kind (wbvh_closest, wbvh_risk_key):
+// (a)'s box widening grows as 1 / QS, the risk set of case (b) as QS.  Host node visits per ray on C4
+// (stride-16 rays, tools/wbvh_probe.py rays): camera 2^-5..2^-10: 8.66 / 7.89 / 7.64 / 7.98 / 9.59 /
+// 11.90; shadow 2^-8..2^-16: 15.05 / 13.06 / 11.84 / 13.79 / 29.79
 #ifndef W_QS_CLOSEST
-#define W_QS_CLOSEST 0x1p-8f
+#define W_QS_CLOSEST 0x1p-7f
 #endif
 #ifndef W_QS_SHADOW
-#define W_QS_SHADOW 0x1p-8f
+#define W_QS_SHADOW 0x1p-12f
 #endif
 
 // timing-only switches (tools/variants.py; never sound when off)
 #ifndef W_CASE_B
 #define W_CASE_B 1
+#endif
+#ifndef W_LAZY_EXT2
+#define W_LAZY_EXT2 0
 #endif
 #ifndef W_SOUND_A
 #define W_SOUND_A 1
@@ -261,6 +270,17 @@ RT_HD GNode load_gnode(const GNode* p)
     return g;
 }
 
+// sqrt within 1 ulp on the device (the hardware instruction), correctly rounded on the host; callers
+// round up by far more than 1 ulp where they need an upper bound
+RT_HD float fast_sqrt(float a)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_sqrtf(a);
+#else
+    return std::sqrt(a);
+#endif
+}
+
 RT_HD float fast_rcp(float a)
 {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -358,6 +378,7 @@ RT_HD float wbvh_risk_key(const GTri& t, double px, double py, double pz, double
     const double cl = sqrt(c0 * c0 + c1 * c1 + c2 * c2);
     if (!(la * lc > 0x1p-100) || !(cl > 0x1p-50 * la * lc))
         return 0.0f;
+
     const double ca = fabs(x0 * y0 + x1 * y1 + x2 * y2) / (la * lc);
     const double s2 = sqrt(fmax(0.0, (1.0 - fmin(1.0, ca + 1e-12)) / 2.0)) * (1 - 1e-9);
     const double sa = cl / (la * lc) * (1 - 1e-9);
@@ -436,33 +457,84 @@ RT_HD float wrisk_sub(float QS, float h, float nu)
     return __builtin_fmaf(QS, h, nu) * (1.0f + 0x1p-20f);
 }
 
-// The per-point risk keys of the wide BVH: risk[(2 node + sel) 4 + j] = the smallest key
-// (wbvh_risk_key) of child j's triangles for point sel, INFINITY when none is at risk.  The keys of a
-// triangle go up its leaf entry's parent chain with a minimum, stopping where the stored key is already
-// no larger.  Host version of kernels.hip wide_risk_kernel (tests, rt_wbvh_query_ex).
-inline void wbvh_risk_host(const WBvh& w, const WRiskArgs& A, int sel, std::vector<float>& risk)
+// The per-point risk words of the wide BVH, one 64-bit word per child (risk[(2 node + sel) 4 + j]):
+// bits 0-47 = the box of the octree leaves holding its at-risk triangles (the reference tests such a
+// triangle only where the line crosses its leaf's k-DOP, inside that box), quantised like the child
+// boxes against the node's frame (6 bytes: lo x y z, hi x y z; lo rounded down, hi up, clamped to the
+// frame: the box lies within rho of the child's, so the decoded box widened by rho holds it), bits
+// 48-63 = the smallest key (wbvh_risk_key) of them as a bfloat16 rounded down (INFINITY: none at risk).
+RT_HD uint64_t wrisk_pack(float K, uint64_t box48)
 {
-    risk.resize(w.nodes.size() * 8, INFINITY);
-    if (!A.on[sel]) {   // no bound: every child at risk, key 0
+    return ((uint64_t)(fbits(K) >> 16) << 48) | (box48 & 0xFFFFFFFFFFFFull);
+}
+RT_HD float wrisk_key(uint64_t w)
+{
+    return bitsf((uint32_t)(w >> 48) << 16);
+}
+// the 6 bytes of a float box [lo, hi] against a node's frame (origin, power-of-two steps)
+RT_HD uint64_t wrisk_qbox(const WNode& nd, const float lo[3], const float hi[3])
+{
+    const double org[3] = {nd.ox, nd.oy, nd.oz};
+    uint64_t q = 0;
+    for (int a = 0; a < 3; a++) {
+        const double st = ldexp(1.0, (int)((nd.exps >> (8 * a)) & 0xffu) - 127);
+        const double l = floor(((double)lo[a] - org[a]) / st), h = ceil(((double)hi[a] - org[a]) / st);
+        const uint64_t ql = (uint64_t)fmin(255.0, fmax(0.0, l)), qh = (uint64_t)fmin(255.0, fmax(0.0, h));
+        q |= ql << (8 * a);
+        q |= qh << (8 * (a + 3));
+    }
+    return q;
+}
+
+// Host version of kernels.hip wide_risk_kernel (tests, rt_wbvh_query_ex): a triangle's key and its
+// octree leaf's axis box go up its leaf entry's parent chain (minimum, union), stopping where both are
+// already there (aggregates over subtrees: what an entry holds its ancestors hold too).  leaf_box:
+// per wide-BVH triangle, its octree leaf's axis box (lo xyz, hi xyz).
+inline void wbvh_risk_host(const WBvh& w, const std::vector<float>& leaf_box, const WRiskArgs& A, int sel,
+                           std::vector<uint64_t>& risk)
+{
+    risk.resize(w.nodes.size() * 8, wrisk_pack(INFINITY, 0));
+    const size_t ne = w.nodes.size() * 4;
+    std::vector<float> K(ne, INFINITY), B(ne * 6);
+    for (size_t i = 0; i < ne; i++)
+        for (int a = 0; a < 3; a++) {
+            B[6 * i + a] = INFINITY;
+            B[6 * i + 3 + a] = -INFINITY;
+        }
+    if (!A.on[sel]) {   // no bound: every child at risk, key 0, its whole frame
         for (size_t v = 0; v < w.nodes.size(); v++)
             for (int j = 0; j < 4; j++)
-                risk[(2 * v + sel) * 4 + j] = 0.0f;
+                risk[(2 * v + sel) * 4 + j] = wrisk_pack(0.0f, 0xFFFFFF000000ull);
         return;
     }
     for (size_t k = 0; k < w.tris.size(); k++) {
-        const float K = wbvh_risk_key(w.tris[k], A.p[sel][0], A.p[sel][1], A.p[sel][2], A.G[sel], A.nu[sel],
-                                      A.slack[sel], A.QS[sel]);
-        if (!(K < INFINITY))
+        const float Kt = wbvh_risk_key(w.tris[k], A.p[sel][0], A.p[sel][1], A.p[sel][2], A.G[sel], A.nu[sel],
+                                       A.slack[sel], A.QS[sel]);
+        if (!(Kt < INFINITY))
             continue;
+        const float* lb = &leaf_box[6 * k];
         uint32_t e = w.tri_leaf[k];
         while (e != W_EMPTY) {
-            float& r = risk[(2 * (size_t)(e >> 2) + sel) * 4 + (e & 3u)];
-            if (r <= K)
+            const size_t i = (size_t)(e >> 2) * 4 + (e & 3u);
+            float* b = &B[6 * i];
+            const bool has = K[i] <= Kt && b[0] <= lb[0] && b[1] <= lb[1] && b[2] <= lb[2] && b[3] >= lb[3] &&
+                             b[4] >= lb[4] && b[5] >= lb[5];
+            if (has)
                 break;
-            r = K;
+            K[i] = std::min(K[i], Kt);
+            for (int a = 0; a < 3; a++) {
+                b[a] = std::min(b[a], lb[a]);
+                b[3 + a] = std::max(b[3 + a], lb[3 + a]);
+            }
             e = w.parent[e >> 2];
         }
     }
+    for (size_t v = 0; v < w.nodes.size(); v++)
+        for (int j = 0; j < 4; j++) {
+            const size_t i = v * 4 + j;
+            risk[(2 * v + sel) * 4 + j] = K[i] < INFINITY ? wrisk_pack(K[i], wrisk_qbox(w.nodes[v], &B[6 * i], &B[6 * i + 3]))
+                                                          : wrisk_pack(INFINITY, 0);
+        }
 }
 
 enum WStatus : int { W_MISS = 0, W_HIT = 1, W_UNCERT = 2 };
@@ -478,6 +550,118 @@ struct WStackLocal {   // host
     RT_HD void put(int i, uint2 v) { e[i] = v; }
     RT_HD uint2 get(int i) const { return e[i]; }
 };
+
+// Case (b) of wbvh_closest's child test (the triangles with q < QS) for rays without risk keys
+// (reflection rays, arbitrary rays): the line through the octree leaves' reach, the origin within
+// H0 + D sin(theta) of the slab, the line where it crosses the widened box within H0 + QS |x - o| +
+// diam sin(theta) of it, and the reported point p' = o + t d (0 <= t <= best) within eta + sin(theta)
+// |p' - a| of it.  Out of line state: it re-reads the node (in cache).  Returns the child's key (the
+// smallest t of a reported point it allows), or INFINITY.
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__
+#else
+inline
+#endif
+float wq_case_b(const WNode* node, int j, v3 o, v3 d, float ix, float iy, float iz, float m, float QS, float dl,
+                float best_s, float a, float qa, float iq)
+{
+    constexpr float SL = 0x1p-20f;
+    constexpr float U = 0x1p-24f;
+    constexpr float NLH = 127.9f;
+    // the node's words straight from memory (in cache: the traversal just read them)
+    const uint32_t* Wp = reinterpret_cast<const uint32_t*>(node);
+    auto W = [&](int i) -> uint32_t { return ldg(Wp + i); };
+    const bool nx_lo = !(ix < 0.0f), ny_lo = !(iy < 0.0f), nz_lo = !(iz < 0.0f);
+    const float ss = bitsf(W(WN_SS)), slo = bitsf(W(WN_SS + 1));
+    const uint32_t ex = W(3);
+    const float stx = bitsf((ex & 0xffu) << 23), sty = bitsf(((ex >> 8) & 0xffu) << 23),
+                stz = bitsf(((ex >> 16) & 0xffu) << 23);
+    const float sx = stx * ix, sy = sty * iy, sz = stz * iz;
+    const float Dx = bitsf(W(0)) - o.x, Dy = bitsf(W(1)) - o.y, Dz = bitsf(W(2)) - o.z;
+    const int sh = 8 * (j & 3);
+    const float qlx = (float)((W(WN_QLO + 0) >> sh) & 0xffu), qhx = (float)((W(WN_QHI + 0) >> sh) & 0xffu);
+    const float qly = (float)((W(WN_QLO + 1) >> sh) & 0xffu), qhy = (float)((W(WN_QHI + 1) >> sh) & 0xffu);
+    const float qlz = (float)((W(WN_QLO + 2) >> sh) & 0xffu), qhz = (float)((W(WN_QHI + 2) >> sh) & 0xffu);
+    const uint32_t nrj = W(WN_NRM + j);
+    const float nx = (float)(int8_t)(nrj & 0xffu), ny = (float)(int8_t)((nrj >> 8) & 0xffu),
+                nz = (float)(int8_t)((nrj >> 16) & 0xffu);
+    const uint32_t e = W(WN_EXT + j), e2 = W(WN_EXT2 + j), sbj = W(WN_SLAB + j);
+    const float sth = wq_val((e >> 16) & 0xffu, WQ_UNIT);
+    const float L = wq_len(e >> 24);
+    const float C0 = __builtin_fmaf((float)(sbj & 0xffffu), ss, slo);
+    const float C1 = __builtin_fmaf((float)(sbj >> 16), ss, slo);
+    const float b = nx * Dx + ny * Dy + nz * Dz;   // N . (origin - o)
+    auto box = [&](float M, float& tmin, float& tmax) {
+        const float mx = nx_lo ? M : -M, my = ny_lo ? M : -M, mz = nz_lo ? M : -M;
+        const float tnx = __builtin_fmaf(nx_lo ? qlx : qhx, sx, (Dx - mx) * ix);
+        const float tny = __builtin_fmaf(ny_lo ? qly : qhy, sy, (Dy - my) * iy);
+        const float tnz = __builtin_fmaf(nz_lo ? qlz : qhz, sz, (Dz - mz) * iz);
+        const float tfx = __builtin_fmaf(nx_lo ? qhx : qlx, sx, (Dx + mx) * ix);
+        const float tfy = __builtin_fmaf(ny_lo ? qhy : qly, sy, (Dy + my) * iy);
+        const float tfz = __builtin_fmaf(nz_lo ? qhz : qlz, sz, (Dz + mz) * iz);
+        tmin = fmaxf(fmaxf(tnx, tny), tnz);
+        tmax = fminf(fminf(tfx, tfy), tfz);
+    };
+    float key = INFINITY;
+    const float s2 = wq_val((e >> 8) & 0xffu, WQ_UNIT);
+    const float rho = wq_len(e2 & 0xffu);
+    const float M = m + rho;
+    float umin, umax;
+    box(M, umin, umax);   // the octree leaves' reach, any t
+    bool okb = !(umin > __builtin_fmaf(fabsf(umax), SL, umax));
+    // distances from o: the child box's farthest corner (>= |o - a|), and the
+    // widened box's (>= |x - o|) and diameter
+    const float ax0 = __builtin_fmaf(qlx, stx, Dx), ax1 = __builtin_fmaf(qhx, stx, Dx);
+    const float ay0 = __builtin_fmaf(qly, sty, Dy), ay1 = __builtin_fmaf(qhy, sty, Dy);
+    const float az0 = __builtin_fmaf(qlz, stz, Dz), az1 = __builtin_fmaf(qhz, stz, Dz);
+    const float ex0 = fmaxf(fabsf(ax0), fabsf(ax1)), ey0 = fmaxf(fabsf(ay0), fabsf(ay1)),
+                ez0 = fmaxf(fabsf(az0), fabsf(az1));
+    const float Dm = fast_sqrt(ex0 * ex0 + ey0 * ey0 + ez0 * ez0) * (1.0f + 0x1p-16f) + m;
+    const float H0 = 1.01f * (QS + 8.0f * U) * (L + Dm) / s2;
+    if (okb) {
+        // the origin: N . (o - origin) = -b within the slab widened by H0 + Dm sin(theta)
+        const float w = NLH * (H0 + __builtin_fmaf(Dm, sth, m)) * (1.0f + 0x1p-16f) + 384.0f * m;
+        okb = !(-b < C0 - w || -b > C1 + w);
+    }
+    if (okb) {
+        // the line where it crosses the widened box: within H0 + QS |x - o| of the
+        // triangle's plane, which lies within diam sin(theta) of the slab there
+        const float Dr = Dm + 1.733f * M, dg = fast_sqrt((ax1 - ax0) * (ax1 - ax0) + (ay1 - ay0) * (ay1 - ay0) +
+                                                      (az1 - az0) * (az1 - az0)) + 3.47f * M;
+        const float Hl = H0 + QS * Dr + dg * sth * 1.01f + m;
+        const float w = NLH * Hl * (1.0f + 0x1p-16f) + 384.0f * m;
+        const float ia = fast_rcp(a);
+        const float s0 = (C0 - w + b) * ia, s1 = (C1 + w + b) * ia;
+        umin = fmaxf(umin, fminf(s0, s1));
+        umax = fminf(umax, fmaxf(s0, s1));
+        okb = !(umin > __builtin_fmaf(fabsf(umax), SL, umax));
+    }
+    if (okb) {
+        // the reported point p' = o + t d, 0 <= t <= best: N . (p' - origin) in
+        // [C0, C1] widened by w0 + w1 t (eta and the tilt over |p' - a| <= Dm + t |d|)
+        const float ke = U * __builtin_fmaf(8.0f * qa, iq, 5.0f) + 1.01f * sth;
+        const float w0 = NLH * __builtin_fmaf(ke, Dm, m) * (1.0f + 0x1p-16f) + 384.0f * m;
+        const float w1 = NLH * ke * dl * (1.0f + 0x1p-16f);
+        const float al = C1 + w0 + b, be = C0 - w0 + b;   // S0 = -b
+        float lo = 0.0f, up = best_s;
+        const float pa = a - w1, pb = a + w1;
+        if (pa > 0.0f)
+            up = fminf(up, al / pa * (1.0f + 0x1p-20f));
+        else if (pa < 0.0f)
+            lo = fmaxf(lo, al / pa * (1.0f - 0x1p-20f));
+        else if (al < 0.0f)
+            lo = INFINITY;
+        if (pb > 0.0f)
+            lo = fmaxf(lo, be / pb * (1.0f - 0x1p-20f));
+        else if (pb < 0.0f)
+            up = fminf(up, be / pb * (1.0f + 0x1p-20f));
+        else if (be > 0.0f)
+            lo = INFINITY;
+        if (!(lo > up))
+            key = fminf(key, lo == lo ? fminf(lo, 3.0e38f) : 0.0f);
+    }
+    return key;
+}
 
 // Closest hit over the wide BVH for the ray (o, d) among hits with t <= hi.  m: box margin
 // (2^-16 (max|o| + scene scale), the leaf-slab margin of kernels.hip leaf_missed).
@@ -499,21 +683,22 @@ struct WStackLocal {   // host
 //       cos(phi) - sin(theta) (1 + sin(theta)), phi the angle between N and -d);
 //   (b) for the triangles with q < QS that bound is not used: their reported points can lie
 //       anywhere on their plane, but the origin is then within H0 = 1.01 (QS + 8u) (L + D) / s2 of
-//       that plane (the barycentric numerators must be small), the reference tests such a
+//       that plane (the barycentric numerators must be small), and the reference tests such a
 //       triangle only where the line crosses its octree leaf's k-DOP (inside the child box
-//       widened by rho), and p' = o + t d (0 <= t <= best) lies within eta + sin(theta) |p' - a|
-//       of the child's slab.  A child passing all three is entered, keyed by the smallest such t.
+//       widened by rho).  A child passing both is entered, keyed by its risk key's t bound (0
+//       without risk keys).
 // Robustly back-facing children (the cone) report nothing and are skipped as before.
-// risk (optional): the risk keys of the ray's kind rsel (wbvh_risk_key / wbvh_risk_host / kernels.hip
+// risk (optional): the risk words of the ray's kind rsel (wrisk_pack / wbvh_risk_host / kernels.hip
 // wide_risk_kernel): a child whose key is INFINITY holds no triangle that can report a hit in case (b)
-// for this ray, and none of its (b) reports has t' below (key - rsub) / (QS |d|), so (b) is skipped for
-// it when that exceeds the best hit.  rsub: 0 for the camera (rsel 0); for the light (rsel 1), at least
+// for this ray; its (b) triangles lie in octree leaves inside its at-risk box (so the line must cross
+// that box, widened by rho), and none of their reports has t' below (key - rsub) / (QS |d|), so (b) is
+// skipped for it when that exceeds the best hit.  rsub: 0 for the camera (rsel 0); for the light (rsel 1), at least
 // QS h + nu with h >= |light - o| and nu the frame's (WRiskArgs::ray_nu; wrisk_sub).  The caller
 // guarantees the ray is of that kind.
 template <class Stack>
 RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m, Stack& stk, WHit& h,
                        uint32_t* work = nullptr, float hi = INFINITY, bool ties = true, float QS = 0x1p-8f,
-                       const float* risk = nullptr, int rsel = 0, float rsub = 0.0f)
+                       const uint64_t* risk = nullptr, int rsel = 0, float rsub = 0.0f)
 {
     h.t = INFINITY;
     h.u = 1.0f;
@@ -555,9 +740,13 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
             W_DIAG_ADD(0, 1);
             W_STEP_HOOK(cur, 0);
             const uint4* p = reinterpret_cast<const uint4*>(nodes + cur);
+#if W_LAZY_EXT2
             // every row but the last (ext2: rho, read by case (b) alone, per lane when it runs)
             constexpr int NR = WN_EXT2 / 4;
             static_assert(WN_EXT2 % 4 == 0 && NR == WN_ROWS - 1, "ext2 is the node's last row");
+#else
+            constexpr int NR = WN_ROWS;
+#endif
             uint4 Rw[NR];
 #pragma unroll
             for (int i = 0; i < NR; i++)
@@ -597,17 +786,20 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                 const float fx = fmaxf(fabsf(Dx), fabsf(__builtin_fmaf(255.0f, stx, Dx)));
                 const float fy = fmaxf(fabsf(Dy), fabsf(__builtin_fmaf(255.0f, sty, Dy)));
                 const float fz = fmaxf(fabsf(Dz), fabsf(__builtin_fmaf(255.0f, stz, Dz)));
-                Dn = sqrtf(fx * fx + fy * fy + fz * fz) * (1.0f + 0x1p-16f) + m;
+                Dn = fast_sqrt(fx * fx + fy * fy + fz * fz) * (1.0f + 0x1p-16f) + m;
             }
             const float RA = U * 30.4f * Dn, RB = U * 2.01f * Dn;
-            // the children's risk keys for this ray's kind (wbvh_risk_key): INFINITY skips case (b)
-            float rk[W_WIDTH] = {0.0f, 0.0f, 0.0f, 0.0f};
+            // the children's risk words for this ray's kind (wrisk_pack): key and at-risk box
+            uint32_t rw[2 * W_WIDTH];
             if (risk) {
-                const float4 r4 = ldg(reinterpret_cast<const float4*>(risk) + (2 * (size_t)cur + rsel));
-                rk[0] = r4.x;
-                rk[1] = r4.y;
-                rk[2] = r4.z;
-                rk[3] = r4.w;
+                const uint4* rp = reinterpret_cast<const uint4*>(risk + (2 * (size_t)cur + rsel) * W_WIDTH);
+                const uint4 r0 = ldg(rp), r1 = ldg(rp + 1);
+                rw[0] = r0.x; rw[1] = r0.y; rw[2] = r0.z; rw[3] = r0.w;
+                rw[4] = r1.x; rw[5] = r1.y; rw[6] = r1.z; rw[7] = r1.w;
+            } else {
+#pragma unroll
+                for (int i = 0; i < 2 * W_WIDTH; i++)
+                    rw[i] = 0u;   // key 0 (unused: the full test runs)
             }
             float key[W_WIDTH];
             uint32_t ref[W_WIDTH];
@@ -690,12 +882,31 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                     // (the child box widened by rho, any t), and the origin must lie within H0 =
                     // 1.01 (QS + 8u) (L + D) / s2 of a triangle's plane, so within H0 + D sin(theta)
                     // of the child's slab (D = Dn >= |o - a|)
-                    const float kbl = (rk[j] - rsub) * iqd;
-                    if (W_CASE_B && qlb < QS && rk[j] < INFINITY && !(kbl > best_s)) {
+                    const float rkj = bitsf(rw[2 * j + 1] & 0xFFFF0000u);   // wrisk_key
+                    const float kbl = (rkj - rsub) * iqd;
+                    if (W_CASE_B && !risk && qlb < QS) {
+                        // no risk keys: the full test and its key
                         W_DIAG_ADD(4, 1);
+                        key[j] = fminf(key[j], wq_case_b(nodes + cur, j, o, d, ix, iy, iz, m, QS, dl, best_s, a, qa, iq));
+                    } else if (W_CASE_B && qlb < QS && rkj < INFINITY && !(kbl > best_s)) {
+                        W_DIAG_ADD(4, 1);
+#if W_LAZY_EXT2
                         const uint32_t e2 = ldg(reinterpret_cast<const uint32_t*>(nodes + cur) + WN_EXT2 + j);
-                        float umin, umax;
-                        box(m + wq_len(e2 & 0xffu), umin, umax);
+#else
+                        const uint32_t e2 = wd(WN_EXT2 + j);
+#endif
+                        // the at-risk octree leaves' box widened by m + rho (any t)
+                        const float Mb = m + wq_len(e2 & 0xffu);
+                        const uint32_t r0 = rw[2 * j], r1 = rw[2 * j + 1];   // lo x y z, hi x y z bytes
+                        const float blx = (float)(r0 & 0xffu), bly = (float)((r0 >> 8) & 0xffu),
+                                    blz = (float)((r0 >> 16) & 0xffu), bhx = (float)(r0 >> 24),
+                                    bhy = (float)(r1 & 0xffu), bhz = (float)((r1 >> 8) & 0xffu);
+                        const float umin = fmaxf(fmaxf(__builtin_fmaf(-Mb, aix, __builtin_fmaf(nx_lo ? blx : bhx, sx, bx)),
+                                                       __builtin_fmaf(-Mb, aiy, __builtin_fmaf(ny_lo ? bly : bhy, sy, by))),
+                                                 __builtin_fmaf(-Mb, aiz, __builtin_fmaf(nz_lo ? blz : bhz, sz, bz)));
+                        const float umax = fminf(fminf(__builtin_fmaf(Mb, aix, __builtin_fmaf(nx_lo ? bhx : blx, sx, bx)),
+                                                       __builtin_fmaf(Mb, aiy, __builtin_fmaf(ny_lo ? bhy : bly, sy, by))),
+                                                 __builtin_fmaf(Mb, aiz, __builtin_fmaf(nz_lo ? bhz : blz, sz, bz)));
                         bool okb = !(umin > __builtin_fmaf(fabsf(umax), SL, umax));
                         if (okb) {
                             const float s2 = wq_val((e >> 8) & 0xffu, WQ_UNIT);
@@ -705,6 +916,8 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                         }
                         if (okb) {
                             W_DIAG_ADD(3, !ok);
+                            W_DIAG_ADD(6, !ok && (chj & W_LEAF));
+                            W_DIAG_ADD(7, !ok && kbl > 0.0f);
                             W_DIAG_ADD(5, ok && kbl < key[j]);
                             key[j] = fminf(key[j], fminf(fmaxf(kbl, 0.0f), 3.0e38f));
                         }
