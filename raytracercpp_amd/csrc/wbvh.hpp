@@ -54,7 +54,8 @@ constexpr int W_MAX_LEAF = 8;
 #ifndef W_STACK_N
 #define W_STACK_N 16
 #endif
-constexpr int W_STACK = W_STACK_N;   // traversal stack entries per lane (overflow: the query is not certified)
+constexpr int W_STACK = W_STACK_N;   // traversal stack entries per lane (a child dropped by a full stack
+                                     // whose key is at most the final best hit: the query is not certified)
 constexpr int W_WIDTH = 4;    // children per node
 
 // the grazing split QS of the wide query's child test per query kind (wbvh_closest, wbvh_risk_key):
@@ -726,7 +727,8 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
     const float icp = (1.0f - 0x1p-18f) / (NLH * dl);   // cos(angle(N, -d)) >= -a icp
     const float iqd = (1.0f - 0x1p-20f) / (QS * dl);        // a risk key's t bound: key / (QS |d|)
     float best_s = hi + fabsf(hi) * SL;   // h.t (or hi) plus slack: a child entered at or below it may hold a hit
-    bool tie = false, nanhit = false, infhit = false, overflow = false;
+    bool tie = false, nanhit = false, infhit = false;
+    float dropped = INFINITY;   // the smallest key of the children a full stack could not take
     int sp = 0;
     uint32_t cur = 0;   // root node
     uint32_t nn = 0, nt = 0;
@@ -944,8 +946,23 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                     if (key[j] < INFINITY) {
                         if (sp < W_STACK)
                             stk.put(sp++, make_uint2(ref[j], fbits(key[j])));
-                        else
-                            overflow = true;
+                        else {
+                            // full: the entry with the largest key goes (the new child or one on the
+                            // stack, which it replaces); the query stays certified if the dropped key
+                            // exceeds the final best hit
+                            int im = -1;
+                            float km = key[j];
+                            for (int i = 0; i < W_STACK; i++) {
+                                const float ki = bitsf(stk.get(i).y);
+                                if (ki > km) {
+                                    km = ki;
+                                    im = i;
+                                }
+                            }
+                            if (im >= 0)
+                                stk.put(im, make_uint2(ref[j], fbits(key[j])));
+                            dropped = fminf(dropped, km);
+                        }
                     }
             } else {
                 cur = W_EMPTY;
@@ -997,6 +1014,9 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
         }
         }
     }
+    // a dropped child matters only if it could hold a hit at t <= the final best (a pop would have
+    // skipped it otherwise)
+    const bool overflow = dropped < INFINITY && dropped <= best_s;
     if (work) {
         work[0] += nn;
         work[1] += nt;
