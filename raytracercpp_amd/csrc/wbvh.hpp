@@ -152,6 +152,13 @@ RT_HD float wq_len(uint32_t k)
 {
     return k == 255u ? INFINITY : wq_val(k, WQ_LEN);
 }
+// code k read as if k = 0 stood for the smallest nonzero value (2^-19 x the top value for WQ_UNIT,
+// 2^-16 for WQ_LEN): a larger upper bound, or, for a lower bound used only as a divisor whose tiny
+// values already mean "no bound" (the query's smin, s2), the same decision as 0
+RT_HD float wq_val_nz(uint32_t k, uint32_t base)
+{
+    return __builtin_bit_cast(float, (k << 20) + base);
+}
 
 struct WStats {
     int64_t nodes = 0, leaves = 0, tris = 0, max_leaf = 0, depth = 0;
@@ -790,7 +797,6 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                 const float fz = fmaxf(fabsf(Dz), fabsf(__builtin_fmaf(255.0f, stz, Dz)));
                 Dn = fast_sqrt(fx * fx + fy * fy + fz * fz) * (1.0f + 0x1p-16f) + m;
             }
-            const float RA = U * 30.4f * Dn, RB = U * 2.01f * Dn;
             // the children's risk words for this ray's kind (wrisk_pack): key and at-risk box
             uint32_t rw[2 * W_WIDTH];
             if (risk) {
@@ -819,23 +825,24 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                 // a and of the threshold: < 1e-4 |d|, inside the build's 0.01 |d|): none reports a hit
                 if (chj != W_EMPTY && !(a > (float)(nrj >> 24) * cstep)) {
                     const uint32_t e = wd(WN_EXT + j);
-                    const float smin = wq_val(e & 0xffu, WQ_UNIT);
-                    const float sth = wq_val((e >> 16) & 0xffu, WQ_UNIT);
-                    const float L = wq_len(e >> 24);
+                    const float smin = wq_val_nz(e & 0xffu, WQ_UNIT);
+                    const float sth = wq_val_nz((e >> 16) & 0xffu, WQ_UNIT);
+                    const float L = (e >> 24) == 255u ? INFINITY : wq_val_nz(e >> 24, WQ_LEN);
                     const float qlb = __builtin_fmaf(-sth, 1.0f + sth, -a * icp) - 0x1p-20f;
                     const float qa = fmaxf(qlb, QS);
                     // (a): the box widened by R, the slab by eta + R sin(theta)
                     // R = (A + B D) / (1 - B) with |p' - o| <= D + R folded in: A = u (30.4 D + 14.4 L) /
                     // (q s) + u (4.02 L + 2.01 D), B = 7.21 u / (q s) + 2.01 u; 1 / (1 - B) <= 1 + 2 B for
                     // B <= 1/2 (beyond: no bound)
+                    // A + B D = u (iq (37.61 D + 14.4 L) + 4.02 (D + L)) <= u (D + L) (37.61 iq + 4.02)
                     const float iq = fast_rcp(qa * smin) * (1.0f + 0x1p-18f);
                     const float Bq = __builtin_fmaf(7.21f * U, iq, 2.01f * U);
-                    const float Aq = __builtin_fmaf(__builtin_fmaf(14.4f * U, L, RA), iq, __builtin_fmaf(4.02f * U, L, RB));
 #if W_SOUND_A
                     const float R = !(Bq <= 0.5f) ? INFINITY
-                                                  : __builtin_fmaf(Bq, Dn, Aq) * __builtin_fmaf(2.0f, Bq, 1.0f) * (1.0f + 0x1p-16f) + m;
+                                                  : __builtin_fmaf((Dn + L) * __builtin_fmaf(37.61f * U, iq, 4.02f * U),
+                                                                   __builtin_fmaf(2.0f * (1.0f + 0x1p-16f), Bq, 1.0f + 0x1p-16f), m);
 #else
-                    const float R = m + 0.0f * Bq * Aq;
+                    const float R = m;   // (timing only)
 #endif
                     // the entry / exit planes' t of this child's box widened by M:
                     // q (s / d) + (origin - o) / d -+ M / |d| per axis
@@ -911,7 +918,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                                                  __builtin_fmaf(Mb, aiz, __builtin_fmaf(nz_lo ? bhz : blz, sz, bz)));
                         bool okb = !(umin > __builtin_fmaf(fabsf(umax), SL, umax));
                         if (okb) {
-                            const float s2 = wq_val((e >> 8) & 0xffu, WQ_UNIT);
+                            const float s2 = wq_val_nz((e >> 8) & 0xffu, WQ_UNIT);
                             const float H0 = 1.01f * (QS + 8.0f * U) * (L + Dn) * fast_rcp(s2) * (1.0f + 0x1p-20f);
                             const float w = NLH * (H0 + __builtin_fmaf(Dn, sth, m)) * (1.0f + 0x1p-16f) + 384.0f * m;
                             okb = !(-b < C0 - w || -b > C1 + w);   // N . (o - origin) = -b
