@@ -582,6 +582,13 @@ int rt_wbvh_query_ex(const float* tri9, int64_t n, int32_t max_depth, int32_t le
                 rt::WHit h;
                 int st = rt::wbvh_closest(w.nodes.data(), w.tris.data(), o, d, m, stk, h, wk, INFINITY, true,
                                           shadow_rays ? W_QS_SHADOW : W_QS_CLOSEST, rk, rsel, rsub);
+                if (st == rt::W_DEEP) {   // the kernels' retry with a deeper stack (kernels.hip wide_closest_deep)
+                    rt::WStackArr<rt::W_DEEP_STACK> deep;
+                    st = rt::wbvh_closest(w.nodes.data(), w.tris.data(), o, d, m, deep, h, wk, INFINITY, true,
+                                          shadow_rays ? W_QS_SHADOW : W_QS_CLOSEST, rk, rsel, rsub);
+                    if (st == rt::W_DEEP)
+                        st = rt::W_UNCERT;
+                }
                 if (st == rt::W_HIT) {
                     int32_t slot = w.slot[(size_t)h.k];
                     if (rt::kdop_certifies(f.nodes[w.leaf_of_slot[(size_t)slot]], o, d, h.t)) {

@@ -874,6 +874,7 @@ __device__ __forceinline__ void ph_mark(int k)
 // The lane's wide-BVH traversal stack: entry i at lv[i * BLOCK] (the LDS of the octree
 // level stack, which is not live during the wide-BVH query).
 struct WStackLds {
+    static constexpr int CAP = W_STACK;
     uint2* base;
     __device__ __forceinline__ void put(int i, uint2 v) { base[i * BLOCK] = v; }
     __device__ __forceinline__ uint2 get(int i) const { return base[i * BLOCK]; }
@@ -902,6 +903,18 @@ __device__ void count_wave_steps(const KParams& P, int base, uint32_t steps)
 #endif
 
 
+// A query whose LDS stack overflowed (wbvh_closest returned W_DEEP, ~0.03% of C4's primary rays:
+// grazing rays with many case-(b) children) runs again with a 64-entry stack in private memory, out
+// of line so that its frame stays out of the traversal loop's registers; the exact octree walk is
+// left for what that cannot certify.
+__device__ __noinline__ int wide_closest_deep(const WNode* wnodes, const GTri* wtris, v3 o, v3 d, float m, WHit& w,
+                                              float hi, bool ties, float QS, const uint64_t* rk, int rsel, float rsub)
+{
+    WStackArr<W_DEEP_STACK> stk;
+    const int st = wbvh_closest(wnodes, wtris, o, d, m, stk, w, nullptr, hi, ties, QS, rk, rsel, rsub);
+    return st == W_DEEP ? W_UNCERT : st;
+}
+
 // BVH::intersect through the wide BVH and its certificate (wbvh.hpp).
 // Returns true with (h, r) = the reference's record and boolean when the query is
 // certified; false when it must be traced through the octree.
@@ -917,8 +930,8 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
     const uint64_t* rk = P.wrisk && o.x == P.cam_pos[0] && o.y == P.cam_pos[1] && o.z == P.cam_pos[2] ? P.wrisk : nullptr;
 #if RT_COUNT
     uint32_t wk[4] = {0, 0, 0, 0};
-    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, INFINITY, true,
-                                W_QS_CLOSEST, rk, 0, 0.0f);
+    int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, INFINITY, true,
+                          W_QS_CLOSEST, rk, 0, 0.0f);
     count_wave_steps(P, 22, wk[3]);
     if (P.counters) {
         atomicAdd(&P.counters[10], (unsigned long long)wk[0]);
@@ -928,9 +941,12 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
                 atomicAdd(&P.counters[16 + c], 1ull);   // uncertified, by reason (wbvh_closest)
     }
 #else
-    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, INFINITY,
-                                true, W_QS_CLOSEST, rk, 0, 0.0f);
+    int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, INFINITY,
+                          true, W_QS_CLOSEST, rk, 0, 0.0f);
 #endif
+    if (st == W_DEEP)
+        st = wide_closest_deep(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), w, INFINITY, true, W_QS_CLOSEST,
+                               rk, 0, 0.0f);
     if (st == W_MISS) {
         h.t = -1.0f;
         h.u = 1.0f;
@@ -985,8 +1001,8 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
     const float rsub = light ? wrisk_sub(W_QS_SHADOW, hi, P.risk_nu) : 0.0f;
 #if RT_COUNT
     uint32_t wk[4] = {0, 0, 0, 0};
-    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, hi, false,
-                                W_QS_SHADOW, rk, 1, rsub);
+    int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, hi, false,
+                          W_QS_SHADOW, rk, 1, rsub);
     count_wave_steps(P, 25, wk[3]);
     if (P.counters) {
         atomicAdd(&P.counters[10], (unsigned long long)wk[0]);
@@ -996,9 +1012,12 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
                 atomicAdd(&P.counters[16 + c], 1ull);   // uncertified, by reason (wbvh_closest)
     }
 #else
-    const int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, hi, false,
-                                W_QS_SHADOW, rk, 1, rsub);
+    int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, hi, false,
+                          W_QS_SHADOW, rk, 1, rsub);
 #endif
+    if (st == W_DEEP)
+        st = wide_closest_deep(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), w, hi, false, W_QS_SHADOW, rk,
+                               1, rsub);
     if (st == W_MISS) {
         *sh = false;
         return true;

@@ -545,19 +545,24 @@ inline void wbvh_risk_host(const WBvh& w, const std::vector<float>& leaf_box, co
         }
 }
 
-enum WStatus : int { W_MISS = 0, W_HIT = 1, W_UNCERT = 2 };
+// W_DEEP: not certified only because the stack overflowed (callers may retry with a deeper stack)
+enum WStatus : int { W_MISS = 0, W_HIT = 1, W_UNCERT = 2, W_DEEP = 3 };
+constexpr int W_DEEP_STACK = 64;   // the retry's stack (private memory, kernels.hip wide_closest_deep)
 
 struct WHit {
     float t, u, v;
     int32_t k;   // wide-BVH triangle index (W_HIT)
 };
 
-// A lane's traversal stack: entry (child link, entry t).
-struct WStackLocal {   // host
-    uint2 e[W_STACK];
+// A lane's traversal stack: entry (child link, entry t); CAP entries.
+template <int N>
+struct WStackArr {
+    static constexpr int CAP = N;
+    uint2 e[N];
     RT_HD void put(int i, uint2 v) { e[i] = v; }
     RT_HD uint2 get(int i) const { return e[i]; }
 };
+using WStackLocal = WStackArr<W_STACK>;   // host
 
 // Case (b) of wbvh_closest's child test (the triangles with q < QS) for rays without risk keys
 // (reflection rays, arbitrary rays): the line through the octree leaves' reach, the origin within
@@ -675,7 +680,7 @@ float wq_case_b(const WNode* node, int j, v3 o, v3 d, float ix, float iy, float 
 // (2^-16 (max|o| + scene scale), the leaf-slab margin of kernels.hip leaf_missed).
 // Returns W_MISS (no triangle reports a hit at t <= hi), W_HIT (h = the minimum-t hit, finite
 // and > 0, unique when ties: still to be certified by kdop_certifies on its octree leaf) or
-// W_UNCERT.  Shadow queries (hi = the segment end of kernels.hip is_shadowed, ties false) read
+// W_UNCERT (W_DEEP when only the stack overflowed).  Shadow queries (hi = the segment end of kernels.hip is_shadowed, ties false) read
 // only the record's t.  work (optional, 4 entries): {nodes, triangles} added, [2] = the reasons
 // a query is not certified, [3] = loop iterations added.
 //
@@ -951,7 +956,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
 #pragma unroll
                 for (int j = W_WIDTH - 1; j >= 1; j--)
                     if (key[j] < INFINITY) {
-                        if (sp < W_STACK)
+                        if (sp < Stack::CAP)
                             stk.put(sp++, make_uint2(ref[j], fbits(key[j])));
                         else {
                             // full: the entry with the largest key goes (the new child or one on the
@@ -959,7 +964,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                             // exceeds the final best hit
                             int im = -1;
                             float km = key[j];
-                            for (int i = 0; i < W_STACK; i++) {
+                            for (int i = 0; i < Stack::CAP; i++) {
                                 const float ki = bitsf(stk.get(i).y);
                                 if (ki > km) {
                                     km = ki;
@@ -1033,17 +1038,19 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
         work[2] = (overflow ? 1u : 0u) | (nanhit ? 2u : 0u) | (h.k < 0 && infhit ? 4u : 0u) |
                   (h.k >= 0 && ties && tie ? 8u : 0u) | (h.k >= 0 && !(h.t > 0.0f && h.t < INFINITY) ? 16u : 0u);
     }
-    if (overflow || nanhit)
+    if (nanhit)
         return W_UNCERT;
     if (h.k < 0) {
         if (infhit)
             return W_UNCERT;
+        if (overflow)
+            return W_DEEP;
         h.t = -1.0f;   // HitInfo() (hitInfo.h:8-24): t = -1, u = 1, v = 0
         return W_MISS;
     }
     if ((ties && tie) || !(h.t > 0.0f && h.t < INFINITY))
         return W_UNCERT;
-    return W_HIT;
+    return overflow ? W_DEEP : W_HIT;
 }
 
 }  // namespace rt

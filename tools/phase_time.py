@@ -30,3 +30,9 @@ tot = d.sum()
 print(f"kernel ms {s['kernel_ms']:.3f}  waves {len(d)}  mean cycles per wave {d.sum(1).mean():.0f}")
 for k, n in enumerate(NAMES):
     print(f"  {n:16s} {d[:, k].sum() / tot * 100:6.1f} %   mean per wave {d[:, k].mean():10.0f} cycles")
+w = d.sum(1)
+q = np.quantile(w, [0.5, 0.9, 0.99, 1.0])
+print(f"  cycles per wave: median {q[0]:.0f}  p90 {q[1]:.0f}  p99 {q[2]:.0f}  max {q[3]:.0f}")
+top = d[w >= np.quantile(w, 0.99)]
+print("  slowest 1% of waves, mean cycles per phase: " +
+      "  ".join(f"{n} {top[:, k].mean():.0f}" for k, n in enumerate(NAMES)))

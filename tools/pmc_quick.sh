@@ -1,6 +1,6 @@
 #!/bin/bash
 # Two quick rocprofv3 PMC passes over a short C4 bench (counters only, one run per pass).
-# Usage: bash tools/pmc_quick.sh <outdir> [bench args...]
+# Usage: bash tools/pmc_quick.sh <outdir> [bench args...]   (RT_LIB_PATH selects a variant library)
 set -u
 OUT=$1; shift
 mkdir -p $OUT
