@@ -39,7 +39,8 @@ PEAK_HBM_GBS = 8000.0        # HBM3E spec peak
 GATHER_151MB_GBS = 7650.0    # uniformly random 1,152-B rows of a 151 MB table (Indexed rows: 7.4-7.9 TB/s)
 NODE_BYTES = 56              # one octree k-DOP test reads 14 floats
 TRI_BYTES = 48               # one Moller-Trumbore test reads a, b-a, c-a, n
-WIDE_NODE_BYTES = 96         # one wide-BVH node visit reads the 96-B node (6 x 16-B loads)
+WIDE_NODE_BYTES = 160        # one wide-BVH node visit reads the 128-B node and the ray kind's 32 B of risk words
+                             # (8 + 2 x 16-B loads)
 CERT_BYTES = 72              # one certificate: the octree leaf's 64-B node + two 4-B slot maps
 PIXEL_BYTES = 4              # ARGB32 write per internal pixel
 COUNTS_FILE = os.path.join(ROOT, "profiles", "work_counts.json")

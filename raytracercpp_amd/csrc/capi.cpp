@@ -476,13 +476,13 @@ int rt_wbvh_query(const float* tri9, int64_t n, int32_t max_depth, int32_t leaf_
                   int64_t stats[8], float* ms)
 {
     return rt_wbvh_query_ex(tri9, n, max_depth, leaf_max_obj_count, orig, dir, nrays, nullptr, nullptr, 0, nullptr,
-                            nullptr, status, id, t, u, v, stats, ms);
+                            nullptr, status, id, t, u, v, stats, ms, nullptr);
 }
 
 int rt_wbvh_query_ex(const float* tri9, int64_t n, int32_t max_depth, int32_t leaf_max_obj_count, const float* orig,
                      const float* dir, int64_t nrays, const float* cam, const float* light, int32_t shadow_rays,
                      float* o_out, float* d_out, int32_t* status, int32_t* id, float* t, float* u, float* v,
-                     int64_t stats[8], float* ms)
+                     int64_t stats[8], float* ms, int32_t* ray_nodes)
 {
     if (n < 0 || (n > 0 && !tri9) || nrays < 0 || (nrays > 0 && (!orig || !dir || !status || !id || !t || !u || !v)) ||
         (shadow_rays && !light))
@@ -580,6 +580,7 @@ int rt_wbvh_query_ex(const float* tri9, int64_t n, int32_t max_depth, int32_t le
                 float om = std::max(std::fabs(o.x), std::max(std::fabs(o.y), std::fabs(o.z)));
                 float m = 0x1p-16f * (om + S);
                 rt::WHit h;
+                const uint32_t wk0 = wk[0];
                 int st = rt::wbvh_closest(w.nodes.data(), w.tris.data(), o, d, m, stk, h, wk, INFINITY, true,
                                           shadow_rays ? W_QS_SHADOW : W_QS_CLOSEST, rk, rsel, rsub);
                 if (st == rt::W_DEEP) {   // the kernels' retry with a deeper stack (kernels.hip wide_closest_deep)
@@ -600,6 +601,8 @@ int rt_wbvh_query_ex(const float* tri9, int64_t n, int32_t max_depth, int32_t le
                         st = rt::W_UNCERT;
                 }
                 status[i] = st;
+                if (ray_nodes)
+                    ray_nodes[i] = (int32_t)(wk[0] - wk0);
             }
             work_n += wk[0];
             work_t += wk[1];

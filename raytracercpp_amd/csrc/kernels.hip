@@ -59,7 +59,8 @@ constexpr int BLOCK = 64 * WAVES_PER_BLOCK;
 #define RT_OCC 5
 #endif
 #ifndef RT_OCC_PLAIN
-#define RT_OCC_PLAIN 4   // the plain kernel: 128 VGPRs (measured r02: 0.67 ms vs 0.71 at 5 waves, 0.69 at 3)
+#define RT_OCC_PLAIN 3   // the plain kernel: 168 VGPRs (r04, the sound wide query: 4.31 ms vs 5.4 at 4 waves with
+                         // 103 spills, 5.17 at 2; r02's unsound query: 0.67 ms at 4 vs 0.71 at 5, 0.69 at 3)
 #endif
 // RT_COUNT=1 (diagnostic builds only, tools/count_gpu_work.py): every traversal adds
 // its k-DOP and Moller-Trumbore test counts to P.counters[4..7] (whole-line queries:

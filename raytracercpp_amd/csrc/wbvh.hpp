@@ -73,6 +73,12 @@ constexpr int W_WIDTH = 4;    // children per node
 #ifndef W_CASE_B
 #define W_CASE_B 1
 #endif
+#ifndef W_STEP_CAP
+#define W_STEP_CAP 0
+#endif
+#ifndef W_RISK_FULLB
+#define W_RISK_FULLB 0
+#endif
 #ifndef W_LAZY_EXT2
 #define W_LAZY_EXT2 0
 #endif
@@ -747,6 +753,12 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
     uint32_t steps = 0;   // loop iterations (node or leaf visits)
     while (cur != W_EMPTY) {
         ++steps;
+#if W_STEP_CAP
+        if (steps > W_STEP_CAP) {   // a very long query: the exact octree walk instead
+            nanhit = true;
+            break;
+        }
+#endif
         // ---- inner nodes: test the four child boxes, go to the nearest, push the others ----
         // if-if: every lane takes one step (inner node or leaf) per iteration
         if (!(cur & W_LEAF)) {
@@ -909,6 +921,10 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
 #else
                         const uint32_t e2 = wd(WN_EXT2 + j);
 #endif
+#if W_RISK_FULLB
+                        key[j] = fminf(key[j], fmaxf(kbl, wq_case_b(nodes + cur, j, o, d, ix, iy, iz, m, QS, dl, best_s, a, qa, iq)));
+                        if (false) {
+#endif
                         // the at-risk octree leaves' box widened by m + rho (any t)
                         const float Mb = m + wq_len(e2 & 0xffu);
                         const uint32_t r0 = rw[2 * j], r1 = rw[2 * j + 1];   // lo x y z, hi x y z bytes
@@ -935,6 +951,9 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                             W_DIAG_ADD(5, ok && kbl < key[j]);
                             key[j] = fminf(key[j], fminf(fmaxf(kbl, 0.0f), 3.0e38f));
                         }
+#if W_RISK_FULLB
+                        }
+#endif
                     }
                 }
 #if defined(__HIP_DEVICE_COMPILE__)
