@@ -1684,6 +1684,7 @@ struct BlockQueue {
     unsigned int word;
     int shard, empty;
     int base[4], sh[4];
+    int heavy_done;   // the heavy list is exhausted (any wave may set it)
 };
 __shared__ BlockQueue g_bq;
 
@@ -1693,11 +1694,40 @@ __device__ __forceinline__ void tile_queue_init()
         g_bq.word = 0u;   // generation 0 with no tickets: the first wave refills
         g_bq.shard = (int)(blockIdx.x & (TILE_SHARDS - 1));
         g_bq.empty = 0;
+        g_bq.heavy_done = 0;
     }
     __syncthreads();
 }
 
+__device__ __forceinline__ int tile_queue_next_shards(const KParams& P);
+
+// The next tile: first the heavy list (one global ticket per tile), then the sharded queue with the
+// heavy tiles skipped (each tile exactly once).
 __device__ __forceinline__ int tile_queue_next(const KParams& P)
+{
+    const int lane = threadIdx.x & 63;
+    if (P.heavy_list) {
+        if (!__builtin_amdgcn_readfirstlane(__hip_atomic_load(&g_bq.heavy_done, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_WORKGROUP))) {
+            int t = 0;
+            if (lane == 0)
+                t = atomicAdd(P.heavy_ctr + 1, 1);
+            t = __builtin_amdgcn_readfirstlane(t);
+            if (t < ldg(P.heavy_ctr))
+                return ldg(P.heavy_list + t);
+            if (lane == 0)
+                __hip_atomic_store(&g_bq.heavy_done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        for (;;) {
+            const int tile = tile_queue_next_shards(P);
+            if (tile < 0 || !((ldg(P.heavy_bits + (tile >> 5)) >> (tile & 31)) & 1u))
+                return tile;
+        }
+    }
+    return tile_queue_next_shards(P);
+}
+
+__device__ __forceinline__ int tile_queue_next_shards(const KParams& P)
 {
     const int lane = threadIdx.x & 63;
     for (;;) {
@@ -1846,14 +1876,18 @@ __global__ __launch_bounds__(BLOCK, PLAIN ? RT_OCC_PLAIN : RT_OCC) void ray_trac
         if (PLAIN) PH_MARK(6);
         if (tile < 0)
             break;
+        const uint64_t tile_t0 = __builtin_amdgcn_s_memtime();
         int tx, ty;
         tile_xy(P, tile, tx, ty);
         int px = tx * 8 + (lane & 7);
         int lr = ty * 8 + (lane >> 3);
         int py = lr < P.local_rows ? global_row(P, lr) : P.rh;
         if (PLAIN) PH_MARK(0);
-        if (px >= P.rw || py >= P.rh)
+        if (px >= P.rw || py >= P.rh) {
+            if (P.tile_cost && lane == 0)
+                P.tile_cost[tile] = 0u;
             continue;
+        }
         // ray generation, renderer.cpp:1086-1098
         const v3 rd = camera_dir(P, px, py, cam);
         if (PLAIN) PH_MARK(1);
@@ -1869,6 +1903,11 @@ __global__ __launch_bounds__(BLOCK, PLAIN ? RT_OCC_PLAIN : RT_OCC) void ray_trac
         if (P.shadow) P.shadow[o] = (uint8_t)(po.found && po.shadowed);
         if (!PLAIN && P.zbuf) write_ssao_buffers(P, o, po.found, cam, rd, po.fin);
         if (PLAIN) PH_MARK(5);
+        if (P.tile_cost) {   // the tile's shader cycles (heavy-first order of the next launch)
+            const uint64_t c = __builtin_amdgcn_s_memtime() - tile_t0;
+            if (lane == 0)
+                P.tile_cost[tile] = c > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)c;
+        }
     }
 #if RT_PHASE_TIME
     if (PLAIN) {
@@ -3137,7 +3176,60 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_trace_colo
     return hipGetLastError();
 }
 
+// The heavy list of a launch (KParams::heavy_list) from the previous launch's tile costs of the same
+// layout: the tiles costing at least max(4 x the mean, the largest / 8), at most ntiles / 16 of them,
+// in tile order.  One block; it also clears the bits and resets the ticket.
+__global__ __launch_bounds__(1024) void heavy_prep_kernel(const uint32_t* __restrict__ cost, int ntiles, int32_t* list,
+                                                          uint32_t* bits, int32_t* ctr)
+{
+    __shared__ unsigned long long sum;
+    __shared__ unsigned int mx;
+    __shared__ int cnt;
+    if (threadIdx.x == 0) {
+        sum = 0;
+        mx = 0;
+        cnt = 0;
+    }
+    __syncthreads();
+    unsigned long long s = 0;
+    unsigned int m = 0;
+    for (int i = threadIdx.x; i < ntiles; i += 1024) {
+        s += cost[i];
+        m = max(m, cost[i]);
+    }
+    atomicAdd(&sum, s);
+    atomicMax(&mx, m);
+    for (int i = threadIdx.x; i < (ntiles + 31) / 32; i += 1024)
+        bits[i] = 0u;
+    __syncthreads();
+    const unsigned long long mean = ntiles > 0 ? sum / (unsigned long long)ntiles : 0;
+    const unsigned long long thr = max(4 * mean, (unsigned long long)(mx / 8));
+    const int cap = ntiles / 16;
+    if (mx > 0)
+        for (int i = threadIdx.x; i < ntiles; i += 1024)
+            if (cost[i] >= thr && cost[i] > 0) {
+                const int k = atomicAdd(&cnt, 1);
+                if (k < cap) {
+                    list[k] = i;
+                    atomicOr(bits + (i >> 5), 1u << (i & 31));
+                }
+            }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        ctr[0] = min(cnt, cap);
+        ctr[1] = 0;
+    }
+}
+
 // ---- host-side launch wrappers (called from renderer.cpp) ----
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_heavy_prep(const uint32_t* cost, int ntiles,
+                                                                                 int32_t* list, uint32_t* bits,
+                                                                                 int32_t* ctr, hipStream_t stream)
+{
+    hipLaunchKernelGGL(heavy_prep_kernel, dim3(1), dim3(1024), 0, stream, cost, ntiles, list, bits, ctr);
+    return hipGetLastError();
+}
+
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(const rt::KParams* P, hipStream_t stream)
 {
     int tiles = P->tiles_x * P->tiles_y;

@@ -106,6 +106,14 @@ struct KParams {
     int32_t max_blocks;       // persistent grid size (CUs x resident blocks per CU)
     int32_t plain;            // 1: no texture map, sky, analytic shape, debug shading or SSAO buffers
                               // (ray_trace_kernel's plain specialisation)
+    // heavy tiles first (ray_trace_kernel, kernels.hip heavy_prep_kernel; nullptr: off): tile_cost
+    // receives each tile's shader cycles; the launch's heavy_list[0 .. heavy_ctr[0]) (the previous
+    // launch's slowest tiles of the same layout, flagged in heavy_bits) are dequeued first, by the
+    // ticket heavy_ctr[1]
+    uint32_t* tile_cost;
+    const int32_t* heavy_list;
+    const uint32_t* heavy_bits;
+    int32_t* heavy_ctr;
 
     // outputs, indexed by local_row * rw + px (nullptr = not requested)
     uint32_t* argb;

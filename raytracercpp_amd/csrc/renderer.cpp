@@ -15,6 +15,9 @@
 #include "host_scene.hpp"
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(const rt::KParams* P, hipStream_t stream);
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_heavy_prep(const uint32_t* cost, int ntiles,
+                                                                                 int32_t* list, uint32_t* bits,
+                                                                                 int32_t* ctr, hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_level0(const rt::KParams* P, rt::FrameRec* fr1,
                                                                            unsigned int* nfr1, hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_stage(int stage, const rt::KParams* P,
@@ -100,6 +103,7 @@ Knobs Knobs::from_env()
     k.debug_waves = getenv("RT_DEBUG_WAVES") != nullptr;
     k.exact = on("RT_EXACT", false);
     k.risk = on("RT_WBVH_RISK", true);
+    k.heavy = on("RT_HEAVY_FIRST", true);
     {
         const char* v = getenv("RT_INJECT_FRAME_FAIL");   // tests: the k-th ray_trace fails after its image start
         k.inject_fail = v ? std::atoi(v) : 0;
@@ -1353,6 +1357,8 @@ int Renderer::trace_frame()
         return RT_EHIP;
     if ((rc = prepare_risk(P, stream_)) != RT_OK)
         return rc;
+    if ((rc = prepare_heavy(P, tc_main_, stream_)) != RT_OK)
+        return rc;
     hipEventRecord(ev_[0], stream_);
     if ((rc = launch_frame(P, stream_)) != RT_OK) return rc;
     hipEventRecord(ev_[1], stream_);
@@ -1711,6 +1717,8 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
     if ((e = hipMemsetAsync(S.counters.p, 0, NCOUNTER_WORDS * 8, stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
     if ((rc = prepare_risk(P, stream)) != RT_OK)
         return rc;
+    if ((rc = prepare_heavy(P, S.tc, stream)) != RT_OK)
+        return rc;
     hipEventRecord(ring_[2 * ring_next_], stream);
     if ((rc = launch_frame(P, stream)) != RT_OK) return rc;
     hipEventRecord(ring_[2 * ring_next_ + 1], stream);
@@ -1770,6 +1778,47 @@ int Renderer::prepare_risk(KParams& P, hipStream_t stream)
     P.risk_G = risk_G_;
     P.risk_nl = risk_nl_;
     P.risk_nu = risk_nu_;
+    return RT_OK;
+}
+
+// Heavy tiles first (KParams::tile_cost, kernels.hip heavy_prep_kernel): the launch's tiles that cost
+// the most in the previous launch of the same tile layout on this slot are dequeued first, so that a
+// few very long tiles (grazing silhouette rays) start with the frame instead of ending
+// it.  Only the order changes; every tile is traced once.  Off for the reflection engine and the raster
+// path (their own kernels) and with RT_HEAVY_FIRST=0.
+int Renderer::prepare_heavy(KParams& P, TileCost& T, hipStream_t stream)
+{
+    P.tile_cost = nullptr;
+    P.heavy_list = nullptr;
+    P.heavy_bits = nullptr;
+    P.heavy_ctr = nullptr;
+    if (!knobs_.heavy || P.has_reflection || s_.hybrid_rasterization_tracing)
+        return RT_OK;
+    const int ntiles = P.tiles_x * P.tiles_y;
+    if (ntiles <= 0)
+        return RT_OK;
+    T.cost.device = T.heavy.device = device_;
+    const size_t nb = ((size_t)ntiles + 31) / 32;
+    hipError_t e;
+    if ((e = T.cost.reserve((size_t)ntiles * 4)) != hipSuccess ||
+        (e = T.heavy.reserve((size_t)ntiles * 4 + nb * 4 + 16)) != hipSuccess)
+        return hip_fail(e, "hipMalloc (tile costs)");
+    uint64_t key = 1469598103934665603ull;
+    for (int64_t v : {(int64_t)P.rw, (int64_t)P.rh, (int64_t)P.local_rows, (int64_t)P.tiles_x, (int64_t)P.tiles_y,
+                      (int64_t)P.band_rows, (int64_t)P.rank, (int64_t)P.nranks, (int64_t)T.cost.bytes})
+        key = (key ^ (uint64_t)v) * 1099511628211ull;
+    if (key != T.key && (e = hipMemsetAsync(T.cost.p, 0, (size_t)ntiles * 4, stream)) != hipSuccess)
+        return hip_fail(e, "hipMemsetAsync (tile costs)");
+    T.key = key;
+    int32_t* list = T.heavy.as<int32_t>();
+    uint32_t* bits = reinterpret_cast<uint32_t*>(list + ntiles);
+    int32_t* ctr = reinterpret_cast<int32_t*>(bits + nb);
+    if ((e = rt_launch_heavy_prep(T.cost.as<uint32_t>(), ntiles, list, bits, ctr, stream)) != hipSuccess)
+        return hip_fail(e, "heavy_prep_kernel");
+    P.tile_cost = T.cost.as<uint32_t>();
+    P.heavy_list = list;
+    P.heavy_bits = bits;
+    P.heavy_ctr = ctr;
     return RT_OK;
 }
 

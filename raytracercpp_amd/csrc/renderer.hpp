@@ -54,6 +54,7 @@ struct Knobs {
     bool debug_waves = false; // RT_DEBUG_WAVES: per-wave records of diagnostic builds (rt_debug_read)
     bool exact = false;       // RT_EXACT=1 / rt_set_exact: wbvh and seg off
     bool risk = true;         // RT_WBVH_RISK=0: no per-frame grazing-risk bits (every child runs case (b), 5.6)
+    bool heavy = true;        // RT_HEAVY_FIRST=0: tiles in queue order only (no heavy-first list, 5.6)
     int inject_fail = 0;      // RT_INJECT_FRAME_FAIL=k (tests): the k-th ray_trace fails after its image start
     bool async_accel = true;  // RT_ASYNC_ACCEL=0: the leaf cones / slabs and the wide BVH are built
                               // before the first frame instead of beside it
@@ -296,9 +297,17 @@ private:
     // slot owns an event recorded after its last launch: launches that use buffers shared
     // across launches (reflection engine, raster path) and scene uploads wait on every live
     // slot's event, never on a stored stream handle (the caller may have destroyed it).
+    // heavy tiles first (KParams::tile_cost / heavy_list): the last launch's tile costs of a layout
+    struct TileCost {
+        DevBuf cost, heavy;
+        uint64_t key = 0;
+    };
+    int prepare_heavy(KParams& P, TileCost& T, hipStream_t stream);
+    TileCost tc_main_;   // trace_frame's launches (stream_)
     struct BandSlot {
         hipStream_t stream = nullptr;
         DevBuf counters, tmp;
+        TileCost tc;
         hipEvent_t done = nullptr;   // recorded on 'stream' after the slot's last launch
         bool live = false;           // 'done' has been recorded
         uint64_t used = 0;   // band_uses_ at the slot's last launch (least recently used is recycled)
