@@ -311,6 +311,24 @@ RT_HD float fast_rcp(float a)
 // BoundingVolume::intersect (bvh.h:79-105) with the ray's plane products as
 // OctreeNode::intersect computes them (bvh.h:216-223), branch-free as kernels.hip
 // vol_test: returns pass && t_near <= t.
+// Case (b)'s bound on the origin's distance from a triangle's plane: with q = |cos(n,
+// d)| < QS, s = sin(alpha) (the angle at a), s2 = sin(alpha' / 2), L >= the edges, D >= |o - a| and u =
+// 2^-24, a hit Moller-Trumbore reports (u', v' in [0, 1]; triangle.cpp:25-91) puts the origin within
+//   H0 = 1.01 [QS (2L + D) + u (24.2 L + 48 D) / s + u (30 L + 12 D + 24 D / s) / s2]
+// of the plane: for q s >= 24u the exact line-plane point P0 has barycentrics within 1 + (12.1u + 24u
+// D / |e|) / (q s) of [0, 1] (numerator and Mdet rounding), so |P0 - a| <= 2L + u (24.2 L + 48 D) / (q s),
+// and the distance is q |P0 - o| <= q (|P0 - a| + D); below, Mdet < 30u |ab||ac||d| bounds both
+// barycentric numerators U = -alpha d.n - gamma d.(n x ac), V = -beta d.n + gamma d.(n x ab), and the
+// larger of |d.(n x ab)| / |ab|, |d.(n x ac)| / |ac| is at least s2 |d|.  Device: the hardware
+// reciprocal (1 ulp), inside the 1.01.
+RT_HD float wq_h0(float QS, float L, float D, float s, float s2)
+{
+    constexpr float U = 0x1p-24f;
+    const float is = fast_rcp(s), is2 = fast_rcp(s2);
+    const float a = __builtin_fmaf(QS, 2.0f * L + D, U * __builtin_fmaf(24.2f, L, 48.0f * D) * is);
+    return 1.01f * __builtin_fmaf(U * __builtin_fmaf(30.0f, L, __builtin_fmaf(24.0f, D * is, 12.0f * D)), is2, a);
+}
+
 RT_HD bool kdop_certifies_exact(const GNode& nd, v3 o, v3 d, float t)
 {
     float t_near = -INFINITY, t_far = INFINITY;
@@ -369,8 +387,8 @@ RT_HD float bitsf(uint32_t u) { return __builtin_bit_cast(float, u); }
 // kind X stands for can make the triangle report a hit in case (b) of wbvh_closest (|cos(n, d)| = q <
 // QS); otherwise a key K >= 0 such that every hit it reports in case (b) has
 //   t' >= (K - QS hi - nu) / (QS |d|)      (camera: t' >= K / (QS |d|)).
-// Case (b) puts the ray's origin o within H0 = 1.01 (QS + 8u) (L + |o - a|) / s2 of the triangle's
-// plane (s2 = sin(alpha' / 2) as the build's ext byte 1, L = the longer edge).  And with s = sin(alpha)
+// Case (b) puts the ray's origin o within H0(D = |o - a|) of the triangle's plane (wq_h0; s2 =
+// sin(alpha' / 2) as the build's ext byte 1, L = the longer edge).  And with s = sin(alpha)
 // and u = 2^-24, Moller-Trumbore's float quantities (triangle.cpp:25-91; stored normal n within
 // 2.83u |ab||ac| of the exact one) satisfy |Mdet| <= (q + 6u/s) |n~||d| and |n . OA| >= |n~| (dist(o) -
 // cN |o - a|), cN = (6/s + 1.2)u, so a reported t' >= (dist(o) - cN |o - a|) / ((QS + 6u/s) |d|) (1 - 2.01u).
@@ -402,7 +420,10 @@ RT_HD float wbvh_risk_key(const GTri& t, double px, double py, double pz, double
     const double Da = sqrt(ax * ax + ay * ay + az * az);
     const double dist = fabs(c0 * ax + c1 * ay + c2 * az) / cl;
     const double L = fmax(la, lc) * (1 + 1e-12);
-    const double rhs = (1.01 * (QS + 8.0 * 0x1p-24) * (L + Da + G + slack) / s2 + QS * G + nu) * (1 + 1e-6);
+    const double sa0 = cl / (la * lc);
+    const double Dx = Da + G + slack, u = 0x1p-24;
+    const double H0 = 1.01 * (QS * (2 * L + Dx) + u * (24.2 * L + 48 * Dx) / sa0 + u * (30 * L + 12 * Dx + 24 * Dx / sa0) / s2);
+    const double rhs = (H0 + QS * G + nu) * (1 + 1e-6);
     if (dist > rhs)
         return INFINITY;
     if (!(dist <= rhs))
@@ -636,7 +657,7 @@ float wq_case_b(const WNode* node, int j, v3 o, v3 d, float ix, float iy, float 
     const float ex0 = fmaxf(fabsf(ax0), fabsf(ax1)), ey0 = fmaxf(fabsf(ay0), fabsf(ay1)),
                 ez0 = fmaxf(fabsf(az0), fabsf(az1));
     const float Dm = fast_sqrt(ex0 * ex0 + ey0 * ey0 + ez0 * ez0) * (1.0f + 0x1p-16f) + m;
-    const float H0 = 1.01f * (QS + 8.0f * U) * (L + Dm) / s2;
+    const float H0 = wq_h0(QS, L, Dm, wq_val(e & 0xffu, WQ_UNIT), s2);
     if (okb) {
         // the origin: N . (o - origin) = -b within the slab widened by H0 + Dm sin(theta)
         const float w = NLH * (H0 + __builtin_fmaf(Dm, sth, m)) * (1.0f + 0x1p-16f) + 384.0f * m;
@@ -701,7 +722,7 @@ float wq_case_b(const WNode* node, int j, v3 o, v3 d, float ix, float iy, float 
 //       its slab widened by eta + R sin(theta) hold p' (q is bounded below by the cone: q >=
 //       cos(phi) - sin(theta) (1 + sin(theta)), phi the angle between N and -d);
 //   (b) for the triangles with q < QS that bound is not used: their reported points can lie
-//       anywhere on their plane, but the origin is then within H0 = 1.01 (QS + 8u) (L + D) / s2 of
+//       anywhere on their plane, but the origin is then within H0 (wq_h0) of
 //       that plane (the barycentric numerators must be small), and the reference tests such a
 //       triangle only where the line crosses its octree leaf's k-DOP (inside the child box
 //       widened by rho).  A child passing both is entered, keyed by its risk key's t bound (0
@@ -905,8 +926,8 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                     W_DIAG_ADD(2, ok);
                     // (b): triangles that may lie nearly parallel to d (q < QS), none of whose reports
                     // precedes kbl (the risk key): the line must cross the octree leaves holding them
-                    // (the child box widened by rho, any t), and the origin must lie within H0 =
-                    // 1.01 (QS + 8u) (L + D) / s2 of a triangle's plane, so within H0 + D sin(theta)
+                    // (the child box widened by rho, any t), and the origin must lie within H0
+                    // (wq_h0) of a triangle's plane, so within H0 + D sin(theta)
                     // of the child's slab (D = Dn >= |o - a|)
                     const float rkj = bitsf(rw[2 * j + 1] & 0xFFFF0000u);   // wrisk_key
                     const float kbl = (rkj - rsub) * iqd;
@@ -940,7 +961,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                         bool okb = !(umin > __builtin_fmaf(fabsf(umax), SL, umax));
                         if (okb) {
                             const float s2 = wq_val_nz((e >> 8) & 0xffu, WQ_UNIT);
-                            const float H0 = 1.01f * (QS + 8.0f * U) * (L + Dn) * fast_rcp(s2) * (1.0f + 0x1p-20f);
+                            const float H0 = wq_h0(QS, L, Dn, smin, s2);
                             const float w = NLH * (H0 + __builtin_fmaf(Dn, sth, m)) * (1.0f + 0x1p-16f) + 384.0f * m;
                             okb = !(-b < C0 - w || -b > C1 + w);   // N . (o - origin) = -b
                         }
