@@ -922,7 +922,7 @@ __device__ __noinline__ int wide_closest_deep(const WNode* wnodes, const GTri* w
 // rec (optional): on a certified hit, the record built from the wide BVH's own copies (the
 // triangle from wtris, index and material from wmeta), with no further dependent loads.
 __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit& h, bool& r, uint2* lv,
-                                             Rec* rec = nullptr)
+                                             Rec* rec = nullptr, uint32_t max_steps = 0, bool* longq = nullptr)
 {
     const float om = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
     WStackLds stk{lv};
@@ -943,8 +943,12 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
     }
 #else
     int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, INFINITY,
-                          true, W_QS_CLOSEST, rk, 0, 0.0f);
+                          true, W_QS_CLOSEST, rk, 0, 0.0f, max_steps);
 #endif
+    if (st == W_LONG) {
+        *longq = true;
+        return false;
+    }
     if (st == W_DEEP)
         st = wide_closest_deep(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), w, INFINITY, true, W_QS_CLOSEST,
                                rk, 0, 0.0f);
@@ -2129,8 +2133,11 @@ __device__ __forceinline__ bool refl_gen(const KParams& P, const ReflArgs& A, in
 }
 
 #ifndef RT_OCC_REFL
-#define RT_OCC_REFL 5   // waves per SIMD of the reflection trace / shadow / pass1 kernels (C5: 4 -> 5 about -0.6%)
+#define RT_OCC_REFL 4   // waves per SIMD of the reflection trace / shadow / pass1 kernels (r04, the sound query:
+                        // C5 689 vs 656 Mrays/s at 5 (31 spills), 691 at 3; r03: 4 -> 5 about -0.6%)
 #endif
+__device__ void refl_trace_one(const KParams& P, const ReflArgs& A, int slot, v3 dir, uint2* lv, uint32_t max_steps);
+
 __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_kernel(KParams P, ReflArgs A)
 {
     extern __shared__ uint2 lds_levels[];
@@ -2152,13 +2159,46 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_kernel(KParams 
         }
         return;
     }
+    refl_trace_one(P, A, slot, dir, lv, (uint32_t)A.max_steps);
+}
+
+// The queries refl_trace_kernel deferred (ReflArgs::defer): traced to the end, one lane each, so that
+// their waves hold long queries only.
+__global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_long_kernel(KParams P, ReflArgs A)
+{
+    extern __shared__ uint2 lds_levels[];
+    uint2* lv = lds_levels + threadIdx.x;
+    const int n = (int)ldg(A.defer_count);
+    for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+        const int slot = A.defer[i];
+        unsigned count = 0;
+        v3 dir = mk(0, 0, 0);
+        if (refl_gen(P, A, slot, dir, count))   // (the same direction: path-keyed RNG)
+            refl_trace_one(P, A, slot, dir, lv, 0u);
+    }
+}
+
+// One reflection sample's closest hit into A.hit[slot]; a query past max_steps (> 0) goes to the
+// deferred list instead.
+__device__ void refl_trace_one(const KParams& P, const ReflArgs& A, int slot, v3 dir, uint2* lv, uint32_t max_steps)
+{
     const FrameRec& F = A.fr[A.order[A.c0 + slot / A.stride]];
     TRay R = make_ray(P, ld3(F.ro), dir);
     THit h;
     bool r;
-    if (P.wnodes && P.nnodes > 0 && !R.nan && wide_closest(P, ld3(F.ro), dir, h, r, lv))
+    bool longq = false;
+    if (P.wnodes && P.nnodes > 0 && !R.nan && wide_closest(P, ld3(F.ro), dir, h, r, lv, nullptr, max_steps, &longq))
         ;   // certified by the wide BVH
-    else if (P.seg_scale > 0.0f && P.seg_oct) {
+    else if (longq) {
+        const uint64_t m = __ballot(1);   // the lanes deferring now: one atomic per wave
+        const int leader = __ffsll((unsigned long long)m) - 1;
+        uint32_t base = 0;
+        if ((int)(threadIdx.x & 63) == leader)
+            base = atomicAdd(A.defer_count, (unsigned)__popcll(m));
+        base = __shfl(base, leader);
+        A.defer[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = slot;
+        return;
+    } else if (P.seg_scale > 0.0f && P.seg_oct) {
         R.lo = -seg_margin(P, R);   // nothing behind the origin can be hit (t >= 0)
         r = bvh_closest_seg(P, R, h, lv);
     } else
@@ -3322,7 +3362,7 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_level
     return hipGetLastError();
 }
 
-// stage: 1 gen + trace, 2 pass1, 3 shadow, 4 spawn, 5 resolve, 6 list
+// stage: 1 gen + trace, 2 pass1, 3 shadow, 4 spawn, 5 resolve, 6 list, 7 the deferred long traces
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_stage(int stage, const rt::KParams* P,
                                                                           const rt::ReflArgs* A, hipStream_t stream)
 {
@@ -3334,6 +3374,8 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_stage
     size_t lds = rt::lds_bytes(*P);
     switch (stage) {
     case 1: hipLaunchKernelGGL(rt::refl_trace_kernel, gs, dim3(rt::BLOCK), lds, stream, *P, *A); break;
+    case 7: hipLaunchKernelGGL(rt::refl_trace_long_kernel, dim3(std::min<unsigned>(gs.x, 2048u)), dim3(rt::BLOCK), lds,
+                               stream, *P, *A); break;
     case 2: hipLaunchKernelGGL(rt::refl_pass1_kernel, gf, dim3(rt::BLOCK), 0, stream, *P, *A); break;
     case 3: hipLaunchKernelGGL(rt::refl_shadow_kernel, gs, dim3(rt::BLOCK), lds, stream, *P, *A); break;
     case 4: hipLaunchKernelGGL(rt::refl_spawn_kernel, gs, dim3(rt::BLOCK), 0, stream, *P, *A); break;

@@ -211,6 +211,9 @@ struct ReflArgs {
                              // passes (RT_REFL_FUSE=0), resolve reads the records
     float4* res;             // fused: per sample slot, the colour it returns (xyz) or, in w as int bits,
                              // the index of the child frame whose colour it returns (-1: xyz)
+    int32_t* defer;          // sample slots whose query ran past max_steps in refl_trace_kernel (traced
+    unsigned int* defer_count;   // again by refl_trace_long_kernel, whole waves of long queries); 0: off
+    int32_t max_steps;
 };
 
 // ---- hybrid rasterisation (kernels.hip "Renderer::raster_trace") ----

@@ -104,6 +104,8 @@ Knobs Knobs::from_env()
     k.exact = on("RT_EXACT", false);
     k.risk = on("RT_WBVH_RISK", true);
     k.heavy = on("RT_HEAVY_FIRST", true);
+    if (const char* v = getenv("RT_REFL_DEFER"))   // loop iterations before a reflection query is deferred
+        k.refl_defer = std::max(0, atoi(v));
     {
         const char* v = getenv("RT_INJECT_FRAME_FAIL");   // tests: the k-th ray_trace fails after its image start
         k.inject_fail = v ? std::atoi(v) : 0;
@@ -1143,14 +1145,20 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
         A.c1 = (int)std::min<size_t>((size_t)nframes, (size_t)c0 + chunk);
         A.level = level;
         A.stride = stride;
-        if ((e = hipMemsetAsync(L.cnt.p, 0, 8, stream)) != hipSuccess)
+        // long queries (more than max_steps loop iterations) leave the trace kernel's waves and are
+        // traced again by stage 7 in waves of their own (the shadow list's buffer, free until pass1;
+        // RT_REFL_DEFER=0: off)
+        A.defer = L.list.as<int32_t>();
+        A.defer_count = L.cnt.as<unsigned int>() + 2;
+        A.max_steps = knobs_.refl_defer;
+        if ((e = hipMemsetAsync(L.cnt.p, 0, 12, stream)) != hipSuccess)
             return hip_fail(e, "hipMemsetAsync");
         // fused (default): trace, pass1 (+ shadow list), shadow (+ spawn); RT_REFL_FUSE=0: trace,
         // pass1, list, shadow, spawn
         A.fused = knobs_.refl_fuse;
-        static const int fused_stages[] = {1, 2, 3}, split_stages[] = {1, 2, 6, 3, 4};
+        static const int fused_stages[] = {1, 7, 2, 3}, split_stages[] = {1, 7, 2, 6, 3, 4};
         const int* st = A.fused ? fused_stages : split_stages;
-        const int nst = A.fused ? 3 : 5;
+        const int nst = A.fused ? 4 : 6;
         for (int k = 0; k < nst; k++)
             if ((e = rt_launch_refl_stage(st[k], &P, &A, stream)) != hipSuccess)
                 return hip_fail(e, "reflection stage launch");

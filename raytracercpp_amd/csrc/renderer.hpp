@@ -55,6 +55,8 @@ struct Knobs {
     bool exact = false;       // RT_EXACT=1 / rt_set_exact: wbvh and seg off
     bool risk = true;         // RT_WBVH_RISK=0: no per-frame grazing-risk bits (every child runs case (b), 5.6)
     bool heavy = true;        // RT_HEAVY_FIRST=0: tiles in queue order only (no heavy-first list, 5.6)
+    int refl_defer = 48;      // RT_REFL_DEFER=k: reflection queries past k loop iterations finish in a pass
+                              // of their own (9; 0: never)
     int inject_fail = 0;      // RT_INJECT_FRAME_FAIL=k (tests): the k-th ray_trace fails after its image start
     bool async_accel = true;  // RT_ASYNC_ACCEL=0: the leaf cones / slabs and the wide BVH are built
                               // before the first frame instead of beside it

@@ -76,9 +76,6 @@ constexpr int W_WIDTH = 4;    // children per node
 #ifndef W_STEP_CAP
 #define W_STEP_CAP 0
 #endif
-#ifndef W_RISK_FULLB
-#define W_RISK_FULLB 0
-#endif
 #ifndef W_LAZY_EXT2
 #define W_LAZY_EXT2 0
 #endif
@@ -573,7 +570,8 @@ inline void wbvh_risk_host(const WBvh& w, const std::vector<float>& leaf_box, co
 }
 
 // W_DEEP: not certified only because the stack overflowed (callers may retry with a deeper stack)
-enum WStatus : int { W_MISS = 0, W_HIT = 1, W_UNCERT = 2, W_DEEP = 3 };
+// W_LONG: stopped after max_steps loop iterations (the caller defers the query to a later pass)
+enum WStatus : int { W_MISS = 0, W_HIT = 1, W_UNCERT = 2, W_DEEP = 3, W_LONG = 4 };
 constexpr int W_DEEP_STACK = 64;   // the retry's stack (private memory, kernels.hip wide_closest_deep)
 
 struct WHit {
@@ -590,118 +588,6 @@ struct WStackArr {
     RT_HD uint2 get(int i) const { return e[i]; }
 };
 using WStackLocal = WStackArr<W_STACK>;   // host
-
-// Case (b) of wbvh_closest's child test (the triangles with q < QS) for rays without risk keys
-// (reflection rays, arbitrary rays): the line through the octree leaves' reach, the origin within
-// H0 + D sin(theta) of the slab, the line where it crosses the widened box within H0 + QS |x - o| +
-// diam sin(theta) of it, and the reported point p' = o + t d (0 <= t <= best) within eta + sin(theta)
-// |p' - a| of it.  Out of line state: it re-reads the node (in cache).  Returns the child's key (the
-// smallest t of a reported point it allows), or INFINITY.
-#if defined(__HIP_DEVICE_COMPILE__)
-__device__ __forceinline__
-#else
-inline
-#endif
-float wq_case_b(const WNode* node, int j, v3 o, v3 d, float ix, float iy, float iz, float m, float QS, float dl,
-                float best_s, float a, float qa, float iq)
-{
-    constexpr float SL = 0x1p-20f;
-    constexpr float U = 0x1p-24f;
-    constexpr float NLH = 127.9f;
-    // the node's words straight from memory (in cache: the traversal just read them)
-    const uint32_t* Wp = reinterpret_cast<const uint32_t*>(node);
-    auto W = [&](int i) -> uint32_t { return ldg(Wp + i); };
-    const bool nx_lo = !(ix < 0.0f), ny_lo = !(iy < 0.0f), nz_lo = !(iz < 0.0f);
-    const float ss = bitsf(W(WN_SS)), slo = bitsf(W(WN_SS + 1));
-    const uint32_t ex = W(3);
-    const float stx = bitsf((ex & 0xffu) << 23), sty = bitsf(((ex >> 8) & 0xffu) << 23),
-                stz = bitsf(((ex >> 16) & 0xffu) << 23);
-    const float sx = stx * ix, sy = sty * iy, sz = stz * iz;
-    const float Dx = bitsf(W(0)) - o.x, Dy = bitsf(W(1)) - o.y, Dz = bitsf(W(2)) - o.z;
-    const int sh = 8 * (j & 3);
-    const float qlx = (float)((W(WN_QLO + 0) >> sh) & 0xffu), qhx = (float)((W(WN_QHI + 0) >> sh) & 0xffu);
-    const float qly = (float)((W(WN_QLO + 1) >> sh) & 0xffu), qhy = (float)((W(WN_QHI + 1) >> sh) & 0xffu);
-    const float qlz = (float)((W(WN_QLO + 2) >> sh) & 0xffu), qhz = (float)((W(WN_QHI + 2) >> sh) & 0xffu);
-    const uint32_t nrj = W(WN_NRM + j);
-    const float nx = (float)(int8_t)(nrj & 0xffu), ny = (float)(int8_t)((nrj >> 8) & 0xffu),
-                nz = (float)(int8_t)((nrj >> 16) & 0xffu);
-    const uint32_t e = W(WN_EXT + j), e2 = W(WN_EXT2 + j), sbj = W(WN_SLAB + j);
-    const float sth = wq_val((e >> 16) & 0xffu, WQ_UNIT);
-    const float L = wq_len(e >> 24);
-    const float C0 = __builtin_fmaf((float)(sbj & 0xffffu), ss, slo);
-    const float C1 = __builtin_fmaf((float)(sbj >> 16), ss, slo);
-    const float b = nx * Dx + ny * Dy + nz * Dz;   // N . (origin - o)
-    auto box = [&](float M, float& tmin, float& tmax) {
-        const float mx = nx_lo ? M : -M, my = ny_lo ? M : -M, mz = nz_lo ? M : -M;
-        const float tnx = __builtin_fmaf(nx_lo ? qlx : qhx, sx, (Dx - mx) * ix);
-        const float tny = __builtin_fmaf(ny_lo ? qly : qhy, sy, (Dy - my) * iy);
-        const float tnz = __builtin_fmaf(nz_lo ? qlz : qhz, sz, (Dz - mz) * iz);
-        const float tfx = __builtin_fmaf(nx_lo ? qhx : qlx, sx, (Dx + mx) * ix);
-        const float tfy = __builtin_fmaf(ny_lo ? qhy : qly, sy, (Dy + my) * iy);
-        const float tfz = __builtin_fmaf(nz_lo ? qhz : qlz, sz, (Dz + mz) * iz);
-        tmin = fmaxf(fmaxf(tnx, tny), tnz);
-        tmax = fminf(fminf(tfx, tfy), tfz);
-    };
-    float key = INFINITY;
-    const float s2 = wq_val((e >> 8) & 0xffu, WQ_UNIT);
-    const float rho = wq_len(e2 & 0xffu);
-    const float M = m + rho;
-    float umin, umax;
-    box(M, umin, umax);   // the octree leaves' reach, any t
-    bool okb = !(umin > __builtin_fmaf(fabsf(umax), SL, umax));
-    // distances from o: the child box's farthest corner (>= |o - a|), and the
-    // widened box's (>= |x - o|) and diameter
-    const float ax0 = __builtin_fmaf(qlx, stx, Dx), ax1 = __builtin_fmaf(qhx, stx, Dx);
-    const float ay0 = __builtin_fmaf(qly, sty, Dy), ay1 = __builtin_fmaf(qhy, sty, Dy);
-    const float az0 = __builtin_fmaf(qlz, stz, Dz), az1 = __builtin_fmaf(qhz, stz, Dz);
-    const float ex0 = fmaxf(fabsf(ax0), fabsf(ax1)), ey0 = fmaxf(fabsf(ay0), fabsf(ay1)),
-                ez0 = fmaxf(fabsf(az0), fabsf(az1));
-    const float Dm = fast_sqrt(ex0 * ex0 + ey0 * ey0 + ez0 * ez0) * (1.0f + 0x1p-16f) + m;
-    const float H0 = wq_h0(QS, L, Dm, wq_val(e & 0xffu, WQ_UNIT), s2);
-    if (okb) {
-        // the origin: N . (o - origin) = -b within the slab widened by H0 + Dm sin(theta)
-        const float w = NLH * (H0 + __builtin_fmaf(Dm, sth, m)) * (1.0f + 0x1p-16f) + 384.0f * m;
-        okb = !(-b < C0 - w || -b > C1 + w);
-    }
-    if (okb) {
-        // the line where it crosses the widened box: within H0 + QS |x - o| of the
-        // triangle's plane, which lies within diam sin(theta) of the slab there
-        const float Dr = Dm + 1.733f * M, dg = fast_sqrt((ax1 - ax0) * (ax1 - ax0) + (ay1 - ay0) * (ay1 - ay0) +
-                                                      (az1 - az0) * (az1 - az0)) + 3.47f * M;
-        const float Hl = H0 + QS * Dr + dg * sth * 1.01f + m;
-        const float w = NLH * Hl * (1.0f + 0x1p-16f) + 384.0f * m;
-        const float ia = fast_rcp(a);
-        const float s0 = (C0 - w + b) * ia, s1 = (C1 + w + b) * ia;
-        umin = fmaxf(umin, fminf(s0, s1));
-        umax = fminf(umax, fmaxf(s0, s1));
-        okb = !(umin > __builtin_fmaf(fabsf(umax), SL, umax));
-    }
-    if (okb) {
-        // the reported point p' = o + t d, 0 <= t <= best: N . (p' - origin) in
-        // [C0, C1] widened by w0 + w1 t (eta and the tilt over |p' - a| <= Dm + t |d|)
-        const float ke = U * __builtin_fmaf(8.0f * qa, iq, 5.0f) + 1.01f * sth;
-        const float w0 = NLH * __builtin_fmaf(ke, Dm, m) * (1.0f + 0x1p-16f) + 384.0f * m;
-        const float w1 = NLH * ke * dl * (1.0f + 0x1p-16f);
-        const float al = C1 + w0 + b, be = C0 - w0 + b;   // S0 = -b
-        float lo = 0.0f, up = best_s;
-        const float pa = a - w1, pb = a + w1;
-        if (pa > 0.0f)
-            up = fminf(up, al / pa * (1.0f + 0x1p-20f));
-        else if (pa < 0.0f)
-            lo = fmaxf(lo, al / pa * (1.0f - 0x1p-20f));
-        else if (al < 0.0f)
-            lo = INFINITY;
-        if (pb > 0.0f)
-            lo = fmaxf(lo, be / pb * (1.0f - 0x1p-20f));
-        else if (pb < 0.0f)
-            up = fminf(up, be / pb * (1.0f + 0x1p-20f));
-        else if (be > 0.0f)
-            lo = INFINITY;
-        if (!(lo > up))
-            key = fminf(key, lo == lo ? fminf(lo, 3.0e38f) : 0.0f);
-    }
-    return key;
-}
 
 // Closest hit over the wide BVH for the ray (o, d) among hits with t <= hi.  m: box margin
 // (2^-16 (max|o| + scene scale), the leaf-slab margin of kernels.hip leaf_missed).
@@ -738,7 +624,7 @@ float wq_case_b(const WNode* node, int j, v3 o, v3 d, float ix, float iy, float 
 template <class Stack>
 RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m, Stack& stk, WHit& h,
                        uint32_t* work = nullptr, float hi = INFINITY, bool ties = true, float QS = 0x1p-8f,
-                       const uint64_t* risk = nullptr, int rsel = 0, float rsub = 0.0f)
+                       const uint64_t* risk = nullptr, int rsel = 0, float rsub = 0.0f, uint32_t max_steps = 0)
 {
     h.t = INFINITY;
     h.u = 1.0f;
@@ -774,6 +660,8 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
     uint32_t steps = 0;   // loop iterations (node or leaf visits)
     while (cur != W_EMPTY) {
         ++steps;
+        if (max_steps && steps > max_steps)
+            return W_LONG;
 #if W_STEP_CAP
         if (steps > W_STEP_CAP) {   // a very long query: the exact octree walk instead
             nanhit = true;
@@ -932,19 +820,27 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                     const float rkj = bitsf(rw[2 * j + 1] & 0xFFFF0000u);   // wrisk_key
                     const float kbl = (rkj - rsub) * iqd;
                     if (W_CASE_B && !risk && qlb < QS) {
-                        // no risk keys: the full test and its key
+                        // no risk words (reflection rays, rt_trace_ray):
                         W_DIAG_ADD(4, 1);
-                        key[j] = fminf(key[j], wq_case_b(nodes + cur, j, o, d, ix, iy, iz, m, QS, dl, best_s, a, qa, iq));
+                        // the child box widened by m + rho (any t) and the origin within H0 + D sin(theta) of
+                        // the slab; keyed 0 (no risk key bounds the reports' t)
+                        float umin, umax;
+                        box(m + wq_len(wd(WN_EXT2 + j) & 0xffu), umin, umax);
+                        bool okb = !(umin > __builtin_fmaf(fabsf(umax), SL, umax));
+                        if (okb) {
+                            const float s2 = wq_val_nz((e >> 8) & 0xffu, WQ_UNIT);
+                            const float H0 = wq_h0(QS, L, Dn, smin, s2);
+                            const float w = NLH * (H0 + __builtin_fmaf(Dn, sth, m)) * (1.0f + 0x1p-16f) + 384.0f * m;
+                            okb = !(-b < C0 - w || -b > C1 + w);
+                        }
+                        if (okb)
+                            key[j] = 0.0f;
                     } else if (W_CASE_B && qlb < QS && rkj < INFINITY && !(kbl > best_s)) {
                         W_DIAG_ADD(4, 1);
 #if W_LAZY_EXT2
                         const uint32_t e2 = ldg(reinterpret_cast<const uint32_t*>(nodes + cur) + WN_EXT2 + j);
 #else
                         const uint32_t e2 = wd(WN_EXT2 + j);
-#endif
-#if W_RISK_FULLB
-                        key[j] = fminf(key[j], fmaxf(kbl, wq_case_b(nodes + cur, j, o, d, ix, iy, iz, m, QS, dl, best_s, a, qa, iq)));
-                        if (false) {
 #endif
                         // the at-risk octree leaves' box widened by m + rho (any t)
                         const float Mb = m + wq_len(e2 & 0xffu);
@@ -972,9 +868,6 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                             W_DIAG_ADD(5, ok && kbl < key[j]);
                             key[j] = fminf(key[j], fminf(fmaxf(kbl, 0.0f), 3.0e38f));
                         }
-#if W_RISK_FULLB
-                        }
-#endif
                     }
                 }
 #if defined(__HIP_DEVICE_COMPILE__)
