@@ -20,17 +20,19 @@
 // octree traversal.  With no hit at all, the reference finds none either and returns false
 // with a fresh record.
 //
-// Layout (HBM): WNode 64 B, the four children's boxes quantised to 8 bits per plane
-// against the node's own frame (Ylitie et al.'s compressed wide nodes, 4-wide):
+// Layout (HBM): WNode 128 B (struct WNode below), the four children's boxes quantised to 8 bits
+// per plane against the node's own frame (Ylitie et al.'s compressed wide nodes, 4-wide):
 //   float4 0: origin x, y, z (the node box's low corner) and the three scale exponents
 //             (byte a = biased exponent of the power-of-two step s_a along axis a);
 //   float4 1: q_lo x[4], q_lo y[4], q_lo z[4], q_hi x[4] (one byte per child);
-//   float4 2: q_hi y[4], q_hi z[4], two unused words;
-//   float4 3: the four child links:
+//   float4 2: q_hi y[4], q_hi z[4], the slab scale and offset;
+//   float4 3 / 4: the slab normals and cones / the slab ranges;
+//   float4 5: the four child links:
 //     inner child:  node index (bit 31 clear);
 //     leaf child:   W_LEAF | first << 3 | (count - 1), triangles first .. first + count - 1
 //                   of the wide BVH's own triangle order (count <= 8);
 //     no child:     W_EMPTY.
+//   float4 6 / 7: the conditioning bytes of the sound child test (ext, ext2).
 // Child box = [origin + q_lo s, origin + q_hi s] with q_lo rounded down and q_hi up, so
 // it holds the float box exactly (checked in double by check_wbvh).
 // Triangles: GTri records (octree.hpp) copied in leaf order, plus slot[] = the octree GTri
