@@ -45,7 +45,7 @@ CERT_BYTES = 72              # one certificate: the octree leaf's 64-B node + tw
 PIXEL_BYTES = 4              # ARGB32 write per internal pixel
 COUNTS_FILE = os.path.join(ROOT, "profiles", "work_counts.json")
 # rocprofv3 PMC summary of this kernel on the same command (tools/profile_gpu.sh + profile_summary.py)
-PROFILE_SUMMARY = os.path.join(ROOT, "profiles", "r03g", "summary.json")
+PROFILE_SUMMARY = os.path.join(ROOT, "profiles", "r04", "summary.json")
 C5_CHECK_ROWS = (172, 400, 540, 907)   # output rows whose internal row pairs bench's C5 mode checks
 
 
