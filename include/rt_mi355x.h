@@ -369,11 +369,12 @@ int rt_wbvh_query(const float *tri9, int64_t n, int32_t max_depth, int32_t leaf_
  * required) each ray is given as (hit point p in orig, normal n in dir) and becomes is_shadowed's
  * ray o = p + 1e-4 n, d = normalize(light - p) (renderer.cpp:340-402), reading the light's bits when
  * its segment bound allows, and is answered as a closest-hit query over the whole line.  o_out /
- * d_out (optional, 3 floats per ray) receive the rays queried. */
+ * d_out (optional, 3 floats per ray) receive the rays queried, ray_nodes (optional) each query's
+ * wide-node visits (the retry's included). */
 int rt_wbvh_query_ex(const float *tri9, int64_t n, int32_t max_depth, int32_t leaf_max_obj_count, const float *orig,
                      const float *dir, int64_t nrays, const float *cam, const float *light, int32_t shadow_rays,
                      float *o_out, float *d_out, int32_t *status, int32_t *id, float *t, float *u, float *v,
-                     int64_t stats[8], float *ms);
+                     int64_t stats[8], float *ms, int32_t *ray_nodes);
 
 #ifdef __cplusplus
 }

@@ -136,7 +136,7 @@ SIGNATURES = {
     "rt_wbvh_query": (C.c_int, [_f32p, C.c_int64, C.c_int32, C.c_int32, _f32p, _f32p, C.c_int64, _i32p, _i32p, _f32p,
                                 _f32p, _f32p, _i64p, _f32p]),
     "rt_wbvh_query_ex": (C.c_int, [_f32p, C.c_int64, C.c_int32, C.c_int32, _f32p, _f32p, C.c_int64, _f32p, _f32p,
-                                   C.c_int32, _f32p, _f32p, _i32p, _i32p, _f32p, _f32p, _f32p, _i64p, _f32p]),
+                                   C.c_int32, _f32p, _f32p, _i32p, _i32p, _f32p, _f32p, _f32p, _i64p, _f32p, _i32p]),
 }
 
 _lib = None
@@ -253,7 +253,8 @@ def load_obj(path, xform, mat_offset=0):
         L.rt_obj_close(h)
 
 
-def wbvh_query(tri9, orig, dirs, max_depth=12, leaf=40, cam=None, light=None, shadow_rays=False, rays_out=False):
+def wbvh_query(tri9, orig, dirs, max_depth=12, leaf=40, cam=None, light=None, shadow_rays=False, rays_out=False,
+               ray_nodes=None):
     """rt_wbvh_query(_ex): the wide-BVH certified closest hit on the host (no GPU).  Returns
     (status, id, t, u, v, stats dict, (octree ms, wide-BVH ms)); status 0 certified miss,
     1 certified hit, 2 not certified.  cam / light: the frame's grazing-risk points (rays from cam
@@ -276,7 +277,8 @@ def wbvh_query(tri9, orig, dirs, max_depth=12, leaf=40, cam=None, light=None, sh
                                  None if c is None else ptr(c, _f32p), None if li is None else ptr(li, _f32p),
                                  1 if shadow_rays else 0, ptr(oo, _f32p), ptr(do, _f32p),
                                  ptr(st, _i32p), ptr(ids, _i32p), ptr(t, _f32p), ptr(u, _f32p), ptr(v, _f32p),
-                                 ptr(stats, _i64p), ptr(ms, _f32p)), "rt_wbvh_query")
+                                 ptr(stats, _i64p), ptr(ms, _f32p),
+                                 None if ray_nodes is None else ptr(ray_nodes, _i32p)), "rt_wbvh_query")
     keys = ("nodes", "leaves", "max_leaf", "depth", "node_visits", "tri_tests", "violations", "sah_x1000")
     out = (st, ids, t, u, v, dict(zip(keys, map(int, stats))), (float(ms[0]), float(ms[1])))
     return out + (oo, do) if rays_out else out
