@@ -133,6 +133,7 @@ SIGNATURES = {
     "rt_octree_digest": (C.c_int, [_f32p, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_uint64), _i64p,
                                    _f32p]),
     "rt_debug_read": (C.c_int, [_H, C.POINTER(C.c_uint64), C.c_int64]),
+    "rt_tile_costs": (C.c_int, [_H, C.POINTER(C.c_uint32), C.c_int64, _i32p, _i32p]),
     "rt_wbvh_query": (C.c_int, [_f32p, C.c_int64, C.c_int32, C.c_int32, _f32p, _f32p, C.c_int64, _i32p, _i32p, _f32p,
                                 _f32p, _f32p, _i64p, _f32p]),
     "rt_wbvh_query_ex": (C.c_int, [_f32p, C.c_int64, C.c_int32, C.c_int32, _f32p, _f32p, C.c_int64, _f32p, _f32p,

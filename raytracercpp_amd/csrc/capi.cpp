@@ -289,6 +289,10 @@ int rt_debug_read(rt_renderer* r, uint64_t* out, int64_t n)
 {
     return guarded(R(r), [&] { return out ? R(r)->debug_read(out, n) : RT_EINVAL; });
 }
+int rt_tile_costs(rt_renderer* r, uint32_t* out, int64_t n, int32_t* tiles_x, int32_t* tiles_y)
+{
+    return guarded(R(r), [&] { return tiles_x && tiles_y ? R(r)->tile_costs(out, n, tiles_x, tiles_y) : RT_EINVAL; });
+}
 int rt_local_rows(rt_renderer* r, int32_t band_rows, int32_t rank, int32_t nranks, int32_t* rows_out)
 {
     return guarded(R(r), [&] {

@@ -1788,6 +1788,20 @@ __device__ __forceinline__ int tile_queue_next_shards(const KParams& P)
     }
 }
 
+// The wave's instruction-issue priority among the waves of its SIMD: heavy-list tiles carry a level
+// (heavy_prep_kernel, from the tile's cost in the previous launch) so that the few tiles whose single
+// wave spans most of the launch (grazing silhouette and terminator rays) issue ahead
+// of the cheap tiles sharing their SIMD; every other tile runs at level 0.
+__device__ __forceinline__ void set_wave_prio(int level)
+{
+    switch (level) {
+    case 3: __builtin_amdgcn_s_setprio(3); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    default: __builtin_amdgcn_s_setprio(0); break;
+    }
+}
+
 // ImageUtils::downscale_image_qt_ARGB32 (imageUtils.h:98-147) fused into the tile: the
 // wave holds its 8x8 tile's ARGB values one per lane (lane = 8 * row + column), every
 // lane active; the f x f blocks (f = 1 << P.ds_shift, f | 8, rows f-aligned in the band)
@@ -1876,10 +1890,13 @@ __global__ __launch_bounds__(BLOCK, PLAIN ? RT_OCC_PLAIN : RT_OCC) void ray_trac
         asm volatile("" : "+s"(kpl));   // (the loop's loads depend on it: not hoisted)
         const KParams& P = *reinterpret_cast<const KParams*>((const void*)kpl);
         const v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
-        const int tile = tile_queue_next(P);
+        const int tq = tile_queue_next(P);
         if (PLAIN) PH_MARK(6);
-        if (tile < 0)
+        if (tq < 0)
             break;
+        const int tile = tq & 0x0fffffff;
+        if (P.heavy_list)
+            set_wave_prio(tq >> 28);
         const uint64_t tile_t0 = __builtin_amdgcn_s_memtime();
         int tx, ty;
         tile_xy(P, tile, tx, ty);
@@ -3219,6 +3236,9 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_trace_colo
 // The heavy list of a launch (KParams::heavy_list) from the previous launch's tile costs of the same
 // layout: the tiles costing at least max(4 x the mean, the largest / 8), at most ntiles / 16 of them,
 // in tile order.  One block; it also clears the bits and resets the ticket.
+#ifndef RT_HEAVY_PRIO
+#define RT_HEAVY_PRIO 1   // heavy tiles at raised wave priority (set_wave_prio)
+#endif
 __global__ __launch_bounds__(1024) void heavy_prep_kernel(const uint32_t* __restrict__ cost, int ntiles, int32_t* list,
                                                           uint32_t* bits, int32_t* ctr)
 {
@@ -3250,7 +3270,12 @@ __global__ __launch_bounds__(1024) void heavy_prep_kernel(const uint32_t* __rest
             if (cost[i] >= thr && cost[i] > 0) {
                 const int k = atomicAdd(&cnt, 1);
                 if (k < cap) {
-                    list[k] = i;
+                    // the wave's issue priority while it traces the tile (bits 28-29, ray_trace_kernel)
+                    const int prio = !RT_HEAVY_PRIO || ntiles >= (1 << 28) ? 0
+                                     : cost[i] >= mx / 2               ? 3
+                                     : cost[i] >= mx / 4               ? 2
+                                                                       : 1;
+                    list[k] = i | (prio << 28);
                     atomicOr(bits + (i >> 5), 1u << (i & 31));
                 }
             }

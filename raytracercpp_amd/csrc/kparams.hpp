@@ -109,7 +109,7 @@ struct KParams {
     // heavy tiles first (ray_trace_kernel, kernels.hip heavy_prep_kernel; nullptr: off): tile_cost
     // receives each tile's shader cycles; the launch's heavy_list[0 .. heavy_ctr[0]) (the previous
     // launch's slowest tiles of the same layout, flagged in heavy_bits) are dequeued first, by the
-    // ticket heavy_ctr[1]
+    // ticket heavy_ctr[1]; a list entry is the tile | its wave priority level << 28
     uint32_t* tile_cost;
     const int32_t* heavy_list;
     const uint32_t* heavy_bits;

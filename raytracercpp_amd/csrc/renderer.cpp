@@ -1596,6 +1596,25 @@ int Renderer::debug_read(uint64_t* out, int64_t n)
     return e == hipSuccess ? RT_OK : hip_fail(e, "debug_read");
 }
 
+// The shader cycles (s_memtime) of each tile of trace_frame's last launch, tile = ty * tiles_x + tx
+// (the heavy-first ordering's input; tools/tile_costs.py).  Zero for tiles off the image.
+int Renderer::tile_costs(uint32_t* out, int64_t n, int32_t* tiles_x, int32_t* tiles_y)
+{
+    const TileCost& T = tc_main_;
+    if (!T.cost.p || T.ntiles <= 0)
+        return fail(RT_EINVAL, "tile_costs: no launch with tile costs yet (RT_HEAVY_FIRST=0, reflections or raster?)");
+    *tiles_x = T.tiles_x;
+    *tiles_y = T.tiles_y;
+    if (!out)
+        return RT_OK;
+    if (n < T.ntiles)
+        return fail(RT_EINVAL, "tile_costs: buffer smaller than tiles_x * tiles_y");
+    hipError_t e = hipStreamSynchronize(stream_);
+    if (e == hipSuccess)
+        e = hipMemcpy(out, T.cost.p, (size_t)T.ntiles * 4, hipMemcpyDeviceToHost);
+    return e == hipSuccess ? RT_OK : hip_fail(e, "tile_costs");
+}
+
 int Renderer::get_stats(rt_stats* out) const
 {
     std::memset(out, 0, sizeof(*out));
@@ -1818,6 +1837,9 @@ int Renderer::prepare_heavy(KParams& P, TileCost& T, hipStream_t stream)
     if (key != T.key && (e = hipMemsetAsync(T.cost.p, 0, (size_t)ntiles * 4, stream)) != hipSuccess)
         return hip_fail(e, "hipMemsetAsync (tile costs)");
     T.key = key;
+    T.ntiles = ntiles;
+    T.tiles_x = P.tiles_x;
+    T.tiles_y = P.tiles_y;
     int32_t* list = T.heavy.as<int32_t>();
     uint32_t* bits = reinterpret_cast<uint32_t*>(list + ntiles);
     int32_t* ctr = reinterpret_cast<int32_t*>(bits + nb);

@@ -131,7 +131,8 @@ public:
     // bracketed by HIP events on the launch stream (synchronises on them)
     int kernel_times(float* ms, int n);
     int band_counters(unsigned long long out[2]);
-    int debug_read(uint64_t* out, int64_t n);   // diagnostic builds: the per-wave records of the last frame
+    int debug_read(uint64_t* out, int64_t n);
+    int tile_costs(uint32_t* out, int64_t n, int32_t* tiles_x, int32_t* tiles_y);   // trace_frame's last tile costs   // diagnostic builds: the per-wave records of the last frame
     // single-process multi-device rendering (rt_set_devices, multidev.hpp): render(Renderer&)
     // renders interleaved bands on every device and gathers them here with RCCL
     int set_devices(const int* ids, int n);
@@ -303,6 +304,7 @@ private:
     struct TileCost {
         DevBuf cost, heavy;
         uint64_t key = 0;
+        int ntiles = 0, tiles_x = 0, tiles_y = 0;   // the last launch's layout
     };
     int prepare_heavy(KParams& P, TileCost& T, hipStream_t stream);
     TileCost tc_main_;   // trace_frame's launches (stream_)

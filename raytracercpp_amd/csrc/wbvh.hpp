@@ -63,9 +63,12 @@ constexpr int W_WIDTH = 4;    // children per node
 // the grazing split QS of the wide query's child test per query kind (wbvh_closest, wbvh_risk_key):
 // (a)'s box widening grows as 1 / QS, the risk set of case (b) as QS.  Host node visits per ray on C4
 // (stride-16 rays, tools/wbvh_probe.py rays): camera 2^-5..2^-10: 8.66 / 7.89 / 7.64 / 7.98 / 9.59 /
-// 11.90; shadow 2^-8..2^-16: 15.05 / 13.06 / 11.84 / 13.79 / 29.79
+// 11.90; shadow 2^-8..2^-16: 15.05 / 13.06 / 11.84 / 13.79 / 29.79.  The camera's 2^-8 is not the
+// mean's minimum but the critical path's: the costliest 8x8 tiles (grazing rays near the silhouette,
+// ~280 node visits at 2^-7 against ~115 at 2^-8, tools/tile_costs.py) span the whole C4 launch, whose
+// kernel time drops 2.33 -> 1.84 ms (profiles/r04/qs8.log) for +5% mean visits
 #ifndef W_QS_CLOSEST
-#define W_QS_CLOSEST 0x1p-7f
+#define W_QS_CLOSEST 0x1p-8f
 #endif
 #ifndef W_QS_SHADOW
 #define W_QS_SHADOW 0x1p-12f

@@ -265,6 +265,14 @@ class Renderer:
         self._call("rt_get_ssao_buffers", ptr(z, _f32p), ptr(n4, _f32p), ptr(a, _i32p))
         return z, np.ascontiguousarray(n4[:, :3]), a
 
+    def tile_costs(self):
+        """The last frame's per-tile shader cycles, shape (tiles_y, tiles_x) (rt_tile_costs)."""
+        tx, ty = C.c_int32(0), C.c_int32(0)
+        self._call("rt_tile_costs", None, 0, C.byref(tx), C.byref(ty))
+        out = np.zeros(tx.value * ty.value, np.uint32)
+        self._call("rt_tile_costs", out.ctypes.data_as(C.POINTER(C.c_uint32)), out.size, C.byref(tx), C.byref(ty))
+        return out.reshape(ty.value, tx.value)
+
     def debug_read(self, n):
         """Diagnostic builds: the last frame's per-wave records (rt_debug_read)."""
         out = np.zeros(n, np.uint64)
