@@ -141,6 +141,8 @@ int Renderer::init(std::string& err)
     if (e == hipSuccess)
         e = hipStreamCreateWithFlags(&accel_stream_, hipStreamNonBlocking);
     if (e == hipSuccess)
+        e = hipStreamCreateWithFlags(&fence_stream_, hipStreamNonBlocking);
+    if (e == hipSuccess)
         e = hipDeviceGetAttribute(&num_cus_, hipDeviceAttributeMultiprocessorCount, device_);
     for (int i = 0; i < 4 && e == hipSuccess; i++)
         e = hipEventCreate(&ev_[i]);
@@ -172,8 +174,11 @@ Renderer::~Renderer()
     if (risk_ev_) hipEventDestroy(risk_ev_);
     for (auto& e : ring_)
         if (e) hipEventDestroy(e);
-    for (auto& b : band_slot_)
+    for (auto& b : band_slot_) {
         if (b.done) hipEventDestroy(b.done);
+        if (b.mark) hipEventDestroy(b.mark);
+    }
+    if (fence_stream_) hipStreamDestroy(fence_stream_);
     if (stream_) hipStreamDestroy(stream_);
     if (display_stream_) hipStreamDestroy(display_stream_);
     if (display_host_) hipHostFree(display_host_);
@@ -1688,7 +1693,8 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
         if (band_nslots_ < BAND_SLOTS) {
             si = band_nslots_++;
             band_slot_[si].counters.device = band_slot_[si].tmp.device = device_;
-            if ((e = hipEventCreateWithFlags(&band_slot_[si].done, hipEventDisableTiming)) != hipSuccess)
+            if ((e = hipEventCreateWithFlags(&band_slot_[si].done, hipEventDisableTiming)) != hipSuccess ||
+                (e = hipEventCreateWithFlags(&band_slot_[si].mark, hipEventDisableTiming)) != hipSuccess)
                 return hip_fail(e, "hipEventCreate");
         } else {
             // a ninth stream: the least recently used slot is recycled once its last launch is
@@ -1753,7 +1759,11 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
     if (ring_count_ < EV_RING) ring_count_++;
     if (f > 1 && !fused && (e = rt_launch_downscale(target, P.rw, P.local_rows, f, d_out, stream)) != hipSuccess)
         return hip_fail(e, "downscale launch");
-    if ((e = hipEventRecord(S.done, stream)) != hipSuccess)
+    // 'done' is recorded on the renderer's own fence stream behind the caller's: later waits on it
+    // never touch the caller's stream, which may be destroyed by then (an event recorded on a
+    // destroyed stream made hipEventSynchronize fail with a capture-state error)
+    if ((e = hipEventRecord(S.mark, stream)) != hipSuccess || (e = hipStreamWaitEvent(fence_stream_, S.mark, 0)) != hipSuccess ||
+        (e = hipEventRecord(S.done, fence_stream_)) != hipSuccess)
         return hip_fail(e, "hipEventRecord");
     S.live = true;
     return RT_OK;

@@ -186,6 +186,7 @@ private:
     std::atomic<int> accel_state_{0};   // 0 idle, 1 building, 2 built, 3 failed
     std::string accel_err_;
     hipStream_t accel_stream_ = nullptr;
+    hipStream_t fence_stream_ = nullptr;   // the band slots' 'done' events (render_bands_device)
     float accel_ms_[3] = {};            // cones + slabs, wide BVH, wide-BVH upload (background)
     bool cones_ready_ = false, wide_ready_ = false, lslab_ready_ = false;
     uint64_t accel_ver_ = 0;   // bumped when poll_accel adopts a build
@@ -312,7 +313,8 @@ private:
         hipStream_t stream = nullptr;
         DevBuf counters, tmp;
         TileCost tc;
-        hipEvent_t done = nullptr;   // recorded on 'stream' after the slot's last launch
+        hipEvent_t done = nullptr;   // recorded on fence_stream_ behind the slot's last launch
+        hipEvent_t mark = nullptr;   // recorded on 'stream' after that launch (fence_stream_ waits on it)
         bool live = false;           // 'done' has been recorded
         uint64_t used = 0;   // band_uses_ at the slot's last launch (least recently used is recycled)
     };

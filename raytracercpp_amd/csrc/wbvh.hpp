@@ -84,6 +84,9 @@ constexpr int W_WIDTH = 4;    // children per node
 #ifndef W_LAZY_EXT2
 #define W_LAZY_EXT2 0
 #endif
+#ifndef W_PRIO_ORDER
+#define W_PRIO_ORDER 1   // children visited by their unwidened entry t (wbvh_closest)
+#endif
 #ifndef W_SOUND_A
 #define W_SOUND_A 1
 #endif
@@ -742,12 +745,18 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
             }
             float key[W_WIDTH];
             uint32_t ref[W_WIDTH];
+#if W_PRIO_ORDER
+            float pri[W_WIDTH];   // visiting order (key: the cull bound kept on the stack)
+#endif
 #pragma unroll
             for (int j = 0; j < W_WIDTH; j++) {
                 const int sh = 8 * (j & 3), jw = j >> 2;
                 const uint32_t chj = wd(WN_CHILD + j);
                 ref[j] = chj;
                 key[j] = INFINITY;
+#if W_PRIO_ORDER
+                pri[j] = INFINITY;
+#endif
                 const uint32_t nrj = wd(WN_NRM + j);
                 const float nx = (float)(int8_t)(nrj & 0xffu), ny = (float)(int8_t)((nrj >> 8) & 0xffu),
                             nz = (float)(int8_t)((nrj >> 16) & 0xffu);
@@ -815,6 +824,10 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                     }
                     if (ok)
                         key[j] = fminf(fmaxf(tmin, 0.0f), 3.0e38f);
+#if defined(W_TRACE) && !defined(__HIP_DEVICE_COMPILE__)
+                    printf("node %u child %d leaf %d: qlb %.4g smin %.3g sth %.3g L %.3g Dn %.3g R %.3g tmin %.5g tmax %.5g ok %d best %.5g\n",
+                           cur, j, (int)((chj & W_LEAF) != 0), qlb, smin, sth, L, Dn, R, tmin, tmax, (int)ok, best_s);
+#endif
                     W_DIAG_ADD(1, 1);
                     W_DIAG_ADD(2, ok);
                     // (b): triangles that may lie nearly parallel to d (q < QS), none of whose reports
@@ -874,6 +887,16 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                             key[j] = fminf(key[j], fminf(fmaxf(kbl, 0.0f), 3.0e38f));
                         }
                     }
+#if W_PRIO_ORDER
+                    // visit order: the entry t of the child's unwidened box (not below the key).  A child
+                    // holding ill-conditioned triangles (UV-sphere pole slivers) has a box widened by a
+                    // large R whose entry t precedes the actual hit; ordered by that key the query walked
+                    // such subtrees first, with no best hit to cull them yet (grazing C4 rays: 144 of 156
+                    // entered children before the hit).  The order does not change the answer.
+                    if (key[j] < INFINITY)
+                        pri[j] = fmaxf(key[j], fmaxf(fmaxf(__builtin_fmaf(qnx, sx, bx), __builtin_fmaf(qny, sy, by)),
+                                                     __builtin_fmaf(qnz, sz, bz)));
+#endif
                 }
 #if defined(__HIP_DEVICE_COMPILE__)
                 // one child at a time: the scheduler would interleave the children's
@@ -882,11 +905,20 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
 #endif
             }
             // sort the (key, ref) pairs ascending: misses (INFINITY) go last
+#if W_PRIO_ORDER
+#define W_CSWAP(a, b)                                                              \
+    if (pri[b] < pri[a]) {                                                         \
+        float tp = pri[a]; pri[a] = pri[b]; pri[b] = tp;                           \
+        float tk = key[a]; key[a] = key[b]; key[b] = tk;                           \
+        uint32_t tr = ref[a]; ref[a] = ref[b]; ref[b] = tr;                        \
+    }
+#else
 #define W_CSWAP(a, b)                                                              \
     if (key[b] < key[a]) {                                                         \
         float tk = key[a]; key[a] = key[b]; key[b] = tk;                           \
         uint32_t tr = ref[a]; ref[a] = ref[b]; ref[b] = tr;                        \
     }
+#endif
             W_CSWAP(0, 1) W_CSWAP(2, 3) W_CSWAP(0, 2) W_CSWAP(1, 3) W_CSWAP(1, 2)
 #undef W_CSWAP
             if (key[0] < INFINITY) {
