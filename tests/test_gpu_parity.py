@@ -1024,3 +1024,23 @@ def test_set_devices_distinct_rccl(make_renderer):
     R.set_devices(list(range(min(n, 4))))
     render(R)
     assert np.array_equal(R.get_image(), one)
+
+
+@pytest.mark.gpu
+def test_tile_costs_and_heavy_order_keep_the_frame(R):
+    """rt_tile_costs: after a frame, one cost per 8x8 tile of the render (zero only off the image);
+    the next frames dequeue the costliest tiles first at raised wave priority (heavy_prep_kernel,
+    set_wave_prio) and must produce the same image (only the order changes)."""
+    from raytracercpp_amd import scenes
+    sc, st = scenes.bumpy70k(width=160, height=96)
+    R.load_scene(sc, st)
+    R.ray_trace()
+    first = R.get_image().copy()
+    c = R.tile_costs()
+    rw, rh = st.render_size()
+    assert c.shape == ((rh + 7) // 8, (rw + 7) // 8)
+    assert (c > 0).all()
+    for _ in range(3):
+        R.ray_trace()
+        assert np.array_equal(R.get_image(), first)
+    assert R.tile_costs().shape == c.shape
