@@ -325,6 +325,30 @@ int rt_trace_rays(rt_renderer *r, const float *orig, const float *dir, int64_t n
 int rt_trace_ray(rt_renderer *r, const float *orig, const float *dir, int64_t n, int32_t current_recursion_depth,
                  float *rgba, int32_t *hit_src, float *t, uint8_t *intersection_found, uint8_t *shadowed);
 
+/* The frames' wide-BVH query on the GPU (kernels.hip wide_query_kernel), with its
+ * status, for n rays: the device build (hardware reciprocal / square root, the GPU-computed risk
+ * words of the current camera and light) of what rt_wbvh_query_ex runs on the host, answering
+ * BVH::intersect (bvh.h:212-287) through the resident wide BVH and its certificate.  kind 0: plain
+ * rays (no risk words: reflection rays, rt_trace_ray); 1: camera rays (a ray whose origin equals the
+ * camera position bitwise reads the camera's words, as the frame's primary rays do); 2: each ray is
+ * (hit point p in orig, normal n in dir), traced as is_shadowed's ray o = p + 1e-4 n, d =
+ * normalize(light - p) (renderer.cpp:340-402) with the light's words when the frame's would apply.
+ * o_out / d_out [n][3]: the rays queried.  status: 0 certified miss, 1 certified hit (tri_id / t /
+ * u / v = BVH::intersect's record; it returned true), 2 not certified (a frame takes the exact
+ * octree walk), each as a closest-hit query over the whole line.  shadowed (kind 2): the frame's
+ * own decision through its segment query, 0 lit, 1 shadowed, 2 not decided (octree walk); 2 for the
+ * other kinds.  Waits for the wide BVH's background build (rt_finish_accel); with no wide BVH
+ * (exact mode, RT_WBVH=0, a scene scale outside its margins) every status is 2. */
+int rt_wide_query(rt_renderer *r, const float *orig, const float *dir, int64_t n, int32_t kind, float *o_out,
+                  float *d_out, int32_t *status, int32_t *tri_id, float *t, float *u, float *v, uint8_t *shadowed);
+/* Diagnostics: the current frame's grazing-risk words (8 per wide-BVH node, wbvh.hpp wrisk_pack):
+ * src 0 as the GPU computes them (wide_risk_kernel), src 1 by the host walk (wbvh_risk_host) over
+ * the same resident wide BVH.  *count = the number of words; out (cap words) may be null to query
+ * it.  violations (optional): the words checked against the tree (wbvh.hpp check_risk_words: every
+ * at-risk triangle's key and octree leaf held by each entry above it).  Waits for the wide BVH's
+ * build; RT_ESTATE when there is none. */
+int rt_risk_words(rt_renderer *r, int32_t src, uint64_t *out, int64_t cap, int64_t *count, int64_t *violations);
+
 /* GPU durations (ms) of the ray-trace kernel of the last n rt_render_bands_device
  * calls, from HIP events recorded around each launch on its stream (waits for them). */
 int rt_kernel_times(rt_renderer *r, float *ms, int32_t n);

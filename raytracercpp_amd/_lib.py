@@ -119,6 +119,9 @@ SIGNATURES = {
     "rt_render_bands_device": (C.c_int, [_H, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]),
     "rt_trace_rays": (C.c_int, [_H, _f32p, _f32p, C.c_int64, _i32p, _f32p, _f32p, _f32p, _u8p]),
     "rt_trace_ray": (C.c_int, [_H, _f32p, _f32p, C.c_int64, C.c_int32, _f32p, _i32p, _f32p, _u8p, _u8p]),
+    "rt_wide_query": (C.c_int, [_H, _f32p, _f32p, C.c_int64, C.c_int32, _f32p, _f32p, _i32p, _i32p, _f32p, _f32p, _f32p,
+                                _u8p]),
+    "rt_risk_words": (C.c_int, [_H, C.c_int32, C.POINTER(C.c_uint64), C.c_int64, _i64p, _i64p]),
     "rt_kernel_times": (C.c_int, [_H, _f32p, C.c_int32]),
     "rt_band_counters": (C.c_int, [_H, _i64p, _i64p]),
     "rt_make_transform": (None, [C.c_int32, C.c_float, C.c_float, C.c_float, _f32p]),

@@ -316,6 +316,15 @@ int rt_trace_rays(rt_renderer* r, const float* orig, const float* dir, int64_t n
 {
     return guarded(R(r), [&] { return R(r)->trace_rays(orig, dir, n, tri_id, t, u, v, ret); });
 }
+int rt_wide_query(rt_renderer* r, const float* orig, const float* dir, int64_t n, int32_t kind, float* o_out,
+                  float* d_out, int32_t* status, int32_t* tri_id, float* t, float* u, float* v, uint8_t* shadowed)
+{
+    return guarded(R(r), [&] { return R(r)->wide_query(orig, dir, n, kind, o_out, d_out, status, tri_id, t, u, v, shadowed); });
+}
+int rt_risk_words(rt_renderer* r, int32_t src, uint64_t* out, int64_t cap, int64_t* count, int64_t* violations)
+{
+    return guarded(R(r), [&] { return R(r)->risk_words(src, out, cap, count, violations); });
+}
 int rt_trace_ray(rt_renderer* r, const float* orig, const float* dir, int64_t n, int32_t current_recursion_depth,
                  float* rgba, int32_t* hit_src, float* t, uint8_t* intersection_found, uint8_t* shadowed)
 {
@@ -629,6 +638,13 @@ int rt_wbvh_query_ex(const float* tri9, int64_t n, int32_t max_depth, int32_t le
             stats[4] = work_n.load();
             stats[5] = work_t.load();
             stats[6] = rt::check_wbvh(f, w);
+            // the risk words the queries read (wbvh_risk_host), checked against the tree
+            if (!risk.empty()) {
+                if (cam)
+                    stats[6] += rt::check_risk_words(f, w, RA, 0, risk.data());
+                if (light)
+                    stats[6] += rt::check_risk_words(f, w, RA, 1, risk.data());
+            }
             stats[7] = (int64_t)(w.stats.sah * 1000.0f);
         }
         return RT_OK;

@@ -3063,6 +3063,94 @@ __global__ __launch_bounds__(BLOCK) void trace_rays_kernel(KParams P, const floa
     out_ret[i] = r ? 1 : 0;
 }
 
+// The wide-BVH query of the frames (wbvh.hpp wbvh_closest + kdop_certifies) for a
+// batch of rays, with its status: the device build of what rt_wbvh_query_ex runs on the host (the
+// hardware reciprocal and square root, the GPU-computed risk words of KParams::wrisk), so that the
+// adversarial grazing cases can be checked on the GPU build itself (rt_wide_query).  kind 0: no risk
+// words (reflection rays, rt_trace_ray); 1: rays from the camera read its words when their origin is
+// the camera position, as wide_closest does; 2: (hit point, normal) pairs traced as is_shadowed's ray
+// towards P.light (renderer.cpp:340-402), reading the light's words when the ray qualifies, and, in
+// out_sh, the frame's own decision through wide_shadow (0 lit, 1 shadowed, 2 not decided: the frame
+// takes the octree's segment query).  Every kind is also answered as a closest-hit query over the
+// whole line (status 0 certified miss, 1 certified hit with the record, 2 not certified).
+// (The occupancy bound is the plain kernel's: wide_closest_deep is compiled once for all its callers,
+// within the loosest caller's register budget, and the plain kernel inherits what it uses.)
+__global__ __launch_bounds__(BLOCK, RT_OCC_PLAIN) void wide_query_kernel(KParams P, const float* __restrict__ orig,
+                                                           const float* __restrict__ dir, int n, int kind,
+                                                           float* __restrict__ o_out, float* __restrict__ d_out,
+                                                           int32_t* __restrict__ status, int32_t* __restrict__ out_id,
+                                                           float* __restrict__ out_t, float* __restrict__ out_u,
+                                                           float* __restrict__ out_v, uint8_t* __restrict__ out_sh)
+{
+    extern __shared__ uint2 lds_levels[];
+    uint2* lv = lds_levels + threadIdx.x;
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n)
+        return;
+    v3 o = mk(orig[3 * i], orig[3 * i + 1], orig[3 * i + 2]);
+    v3 d = mk(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]);
+    const uint64_t* rk = nullptr;
+    int rsel = 0;
+    float rsub = 0.0f, QS = W_QS_CLOSEST;
+    uint8_t sh = 2;
+    if (kind == 2) {
+        const v3 p = o, nrm = d, lp = mk(P.light[0], P.light[1], P.light[2]);
+        o = p + nrm * 1.0e-4f;
+        d = normalize(lp - p);
+        QS = W_QS_SHADOW;
+        const TRay R0 = make_ray(P, o, d);
+        const float m = seg_margin(P, R0);
+        const float nl = fabsf(nrm.x) + fabsf(nrm.y) + fabsf(nrm.z);
+        const float hi = (sqrtf(length2(p - lp)) + 1.0e-4f * nl) * (1.0f + 0x1p-10f) + m;
+        const bool light = P.wrisk && hi <= P.risk_G && nl <= P.risk_nl;
+        if (light) {
+            rk = P.wrisk;
+            rsel = 1;
+            rsub = wrisk_sub(W_QS_SHADOW, hi, P.risk_nu);
+        }
+        bool s;
+        if (P.wnodes && P.nnodes > 0 && P.seg_scale > 0.0f && !R0.nan && wide_shadow(P, o, d, hi, p, lp, lv, &s, light))
+            sh = s ? 1 : 0;
+    } else if (kind == 1 && P.wrisk && o.x == P.cam_pos[0] && o.y == P.cam_pos[1] && o.z == P.cam_pos[2]) {
+        rk = P.wrisk;
+    }
+    o_out[3 * i] = o.x;
+    o_out[3 * i + 1] = o.y;
+    o_out[3 * i + 2] = o.z;
+    d_out[3 * i] = d.x;
+    d_out[3 * i + 1] = d.y;
+    d_out[3 * i + 2] = d.z;
+    int st = W_UNCERT;
+    int32_t id = -1;
+    WHit w;
+    w.t = -1.0f;
+    w.u = 1.0f;
+    w.v = 0.0f;
+    if (P.wnodes && P.nnodes > 0 && !ray_is_nan(o, d)) {
+        const float om = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
+        const float m = 0x1p-16f * (om + P.scene_scale);
+        WStackLds stk{lv};
+        st = wbvh_closest(P.wnodes, P.wtris, o, d, m, stk, w, nullptr, INFINITY, true, QS, rk, rsel, rsub);
+        if (st == W_DEEP)
+            st = wide_closest_deep(P.wnodes, P.wtris, o, d, m, w, INFINITY, true, QS, rk, rsel, rsub);
+        if (st == W_HIT) {
+            const uint4 M = ldg(P.wmeta + w.k);
+            if (kdop_certifies(load_gnode(P.nodes + M.y), o, d, w.t))
+                id = (int32_t)M.z;
+            else
+                st = W_UNCERT;
+        }
+        if (st == W_MISS)
+            w.t = -1.0f;
+    }
+    status[i] = st;
+    out_id[i] = id;
+    out_t[i] = st == W_HIT ? w.t : -1.0f;
+    out_u[i] = st == W_HIT ? w.u : 1.0f;
+    out_v[i] = st == W_HIT ? w.v : 0.0f;
+    out_sh[i] = sh;
+}
+
 // Renderer::trace_ray (renderer.cpp:1008-1066) for a batch of arbitrary rays, one lane per
 // ray, each with a fresh HitInfo: the colour trace_ray returns (shading, shadow ray, the
 // compute_reflection recursion when REFL), and the record it leaves.  The host folds
@@ -3211,6 +3299,21 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_trace_rays
     size_t lds = rt::lds_bytes(*P);
     hipLaunchKernelGGL(rt::trace_rays_kernel, dim3((n + rt::BLOCK - 1) / rt::BLOCK), dim3(rt::BLOCK), lds, stream, *P,
                        o, d, n, id, t, u, v, ret);
+    return hipGetLastError();
+}
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_wide_query(const rt::KParams* P, const float* o,
+                                                                                 const float* d, int n, int kind,
+                                                                                 float* o_out, float* d_out,
+                                                                                 int32_t* status, int32_t* id, float* t,
+                                                                                 float* u, float* v, uint8_t* sh,
+                                                                                 hipStream_t stream)
+{
+    if (n <= 0)
+        return hipSuccess;
+    size_t lds = rt::lds_bytes(*P);
+    hipLaunchKernelGGL(rt::wide_query_kernel, dim3((n + rt::BLOCK - 1) / rt::BLOCK), dim3(rt::BLOCK), lds, stream, *P,
+                       o, d, n, kind, o_out, d_out, status, id, t, u, v, sh);
     return hipGetLastError();
 }
 

@@ -29,6 +29,12 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_risk_box_i
                                                                                     hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_trace_rays(const rt::KParams* P, const float* o, const float* d, int n, int32_t* id,
                                            float* t, float* u, float* v, uint8_t* ret, hipStream_t stream);
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_wide_query(const rt::KParams* P, const float* o,
+                                                                                 const float* d, int n, int kind,
+                                                                                 float* o_out, float* d_out,
+                                                                                 int32_t* status, int32_t* id, float* t,
+                                                                                 float* u, float* v, uint8_t* sh,
+                                                                                 hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_trace_colors(const rt::KParams* P, bool refl,
                                                                                    const float* o, const float* d,
                                                                                    int n, float4* rgba, int32_t* src,
@@ -1926,6 +1932,127 @@ int Renderer::trace_rays(const float* orig, const float* dir, int64_t n, int32_t
         return hip_fail(e, "download (rays)");
     if ((e = hipStreamSynchronize(stream_)) != hipSuccess)
         return hip_fail(e, "trace_rays_kernel");
+    return RT_OK;
+}
+
+// The frames' wide-BVH query with its status over n host rays (kernels.hip wide_query_kernel): the
+// device build of rt_wbvh_query_ex, reading the risk words prepare_risk computes on the GPU
+int Renderer::wide_query(const float* orig, const float* dir, int64_t n, int kind, float* o_out, float* d_out,
+                         int32_t* status, int32_t* id, float* t, float* u, float* v, uint8_t* shadow)
+{
+    if (n < 0 || n > (1 << 28) || kind < 0 || kind > 2 ||
+        (n > 0 && (!orig || !dir || !o_out || !d_out || !status || !id || !t || !u || !v || !shadow)))
+        return fail(RT_EINVAL, "wide_query: bad arguments");
+    int rc = ensure_device_scene();
+    if (rc == RT_OK)
+        rc = poll_accel(true);   // the wide BVH the frames use once it is resident
+    if (rc != RT_OK)
+        return rc;
+    if (n == 0)
+        return RT_OK;
+    KParams P;
+    fill_params(P);
+    DevBuf din, dout;
+    din.device = dout.device = device_;
+    const size_t nb = (size_t)n;
+    hipError_t e;
+    // outputs: o, d (12 B each), status, id, t, u, v (4 B each), shadowed (1 B) per ray
+    constexpr size_t OUT_BYTES = 2 * 12 + 5 * 4 + 1;
+    if ((e = din.reserve(nb * 24)) != hipSuccess || (e = dout.reserve(nb * OUT_BYTES)) != hipSuccess)
+        return hip_fail(e, "hipMalloc (rays)");
+    float* d_o = din.as<float>();
+    float* d_d = d_o + 3 * nb;
+    float* d_oo = dout.as<float>();
+    float* d_do = d_oo + 3 * nb;
+    int32_t* d_st = reinterpret_cast<int32_t*>(d_do + 3 * nb);
+    int32_t* d_id = d_st + nb;
+    float* d_t = reinterpret_cast<float*>(d_id + nb);
+    float* d_u = d_t + nb;
+    float* d_v = d_u + nb;
+    uint8_t* d_sh = reinterpret_cast<uint8_t*>(d_v + nb);
+    if ((size_t)(d_sh + nb - dout.as<uint8_t>()) > dout.bytes)
+        return fail(RT_EINVAL, "wide_query: output layout exceeds its buffer");
+    if (wait_slots(stream_) != RT_OK)
+        return RT_EHIP;
+    if ((rc = prepare_risk(P, stream_)) != RT_OK)
+        return rc;
+    if ((e = hipMemcpyAsync(d_o, orig, nb * 12, hipMemcpyHostToDevice, stream_)) != hipSuccess ||
+        (e = hipMemcpyAsync(d_d, dir, nb * 12, hipMemcpyHostToDevice, stream_)) != hipSuccess)
+        return hip_fail(e, "upload (rays)");
+    if ((e = rt_launch_wide_query(&P, d_o, d_d, (int)n, kind, d_oo, d_do, d_st, d_id, d_t, d_u, d_v, d_sh, stream_)) !=
+        hipSuccess)
+        return hip_fail(e, "wide_query_kernel launch");
+    if ((e = hipMemcpyAsync(o_out, d_oo, nb * 12, hipMemcpyDeviceToHost, stream_)) != hipSuccess ||
+        (e = hipMemcpyAsync(d_out, d_do, nb * 12, hipMemcpyDeviceToHost, stream_)) != hipSuccess ||
+        (e = hipMemcpyAsync(status, d_st, nb * 4, hipMemcpyDeviceToHost, stream_)) != hipSuccess ||
+        (e = hipMemcpyAsync(id, d_id, nb * 4, hipMemcpyDeviceToHost, stream_)) != hipSuccess ||
+        (e = hipMemcpyAsync(t, d_t, nb * 4, hipMemcpyDeviceToHost, stream_)) != hipSuccess ||
+        (e = hipMemcpyAsync(u, d_u, nb * 4, hipMemcpyDeviceToHost, stream_)) != hipSuccess ||
+        (e = hipMemcpyAsync(v, d_v, nb * 4, hipMemcpyDeviceToHost, stream_)) != hipSuccess ||
+        (e = hipMemcpyAsync(shadow, d_sh, nb, hipMemcpyDeviceToHost, stream_)) != hipSuccess)
+        return hip_fail(e, "download (rays)");
+    if ((e = hipStreamSynchronize(stream_)) != hipSuccess)
+        return hip_fail(e, "wide_query_kernel");
+    return RT_OK;
+}
+
+// The frame's grazing-risk words for the current camera and light (8 per wide-BVH node, wrisk_pack):
+// src 0 as prepare_risk computes them on the GPU (wide_risk_kernel), src 1 by the host walk
+// wbvh_risk_host over the resident wide BVH with the same WRiskArgs.  *count = the number of words
+// (out may be null to query it).  RT_ESTATE when no wide BVH is resident or the risk words are off.
+int Renderer::risk_words(int src, uint64_t* out, int64_t cap, int64_t* count, int64_t* violations)
+{
+    if (src < 0 || src > 1 || !count)
+        return fail(RT_EINVAL, "risk_words: bad arguments");
+    int rc = ensure_device_scene();
+    if (rc == RT_OK)
+        rc = poll_accel(true);
+    if (rc != RT_OK)
+        return rc;
+    KParams P;
+    fill_params(P);
+    if (!P.wnodes || !knobs_.risk || risk_nodes_ <= 0)
+        return fail(RT_ESTATE, "risk_words: no wide BVH with risk words (exact mode, RT_WBVH=0 or RT_WBVH_RISK=0)");
+    const int64_t ne = risk_nodes_ * 8;
+    *count = ne;
+    if (!out)
+        return RT_OK;
+    if (cap < ne)
+        return fail(RT_EINVAL, "risk_words: output too small");
+    if (src == 0) {
+        if (wait_slots(stream_) != RT_OK)
+            return RT_EHIP;
+        if ((rc = prepare_risk(P, stream_)) != RT_OK)
+            return rc;
+        hipError_t e;
+        if ((e = hipMemcpyAsync(out, P.wrisk, (size_t)ne * 8, hipMemcpyDeviceToHost, stream_)) != hipSuccess ||
+            (e = hipStreamSynchronize(stream_)) != hipSuccess)
+            return hip_fail(e, "download (risk words)");
+    }
+    const float lo[3] = {oct_root_.dn[0], oct_root_.dn[1], oct_root_.dn[2]};
+    const float hi[3] = {oct_root_.df[0], oct_root_.df[1], oct_root_.df[2]};
+    const WRiskArgs A = wbvh_risk_args(lo, hi, P.scene_scale, P.cam_pos, P.light, W_QS_CLOSEST, W_QS_SHADOW);
+    if (violations)
+        *violations = 0;
+    if (src == 0) {
+        if (violations)
+            *violations = check_risk_words(oct_, wb_, A, 0, out) + check_risk_words(oct_, wb_, A, 1, out);
+        return RT_OK;
+    }
+    std::vector<float> lbox(6 * wb_.tris.size());
+    for (size_t k = 0; k < wb_.tris.size(); k++) {
+        const GNode& L = oct_.nodes[wb_.leaf_of_k[k]];
+        for (int a = 0; a < 3; a++) {
+            lbox[6 * k + a] = L.dn[a];
+            lbox[6 * k + 3 + a] = L.df[a];
+        }
+    }
+    std::vector<uint64_t> risk;
+    wbvh_risk_host(wb_, lbox, A, 0, risk);
+    wbvh_risk_host(wb_, lbox, A, 1, risk);
+    std::memcpy(out, risk.data(), (size_t)ne * 8);
+    if (violations)
+        *violations = check_risk_words(oct_, wb_, A, 0, out) + check_risk_words(oct_, wb_, A, 1, out);
     return RT_OK;
 }
 

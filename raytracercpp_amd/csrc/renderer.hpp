@@ -131,8 +131,8 @@ public:
     // bracketed by HIP events on the launch stream (synchronises on them)
     int kernel_times(float* ms, int n);
     int band_counters(unsigned long long out[2]);
-    int debug_read(uint64_t* out, int64_t n);
-    int tile_costs(uint32_t* out, int64_t n, int32_t* tiles_x, int32_t* tiles_y);   // trace_frame's last tile costs   // diagnostic builds: the per-wave records of the last frame
+    int debug_read(uint64_t* out, int64_t n);   // diagnostic builds: the per-wave records of the last frame
+    int tile_costs(uint32_t* out, int64_t n, int32_t* tiles_x, int32_t* tiles_y);   // trace_frame's last tile costs
     // single-process multi-device rendering (rt_set_devices, multidev.hpp): render(Renderer&)
     // renders interleaved bands on every device and gathers them here with RCCL
     int set_devices(const int* ids, int n);
@@ -142,6 +142,11 @@ public:
     // BVH::intersect over n host rays (closest hit, reference semantics)
     int trace_rays(const float* orig, const float* dir, int64_t n, int32_t* id, float* t, float* u, float* v,
                    uint8_t* ret);
+    // the frames' wide-BVH query and its status over n host rays (rt_wide_query)
+    int wide_query(const float* orig, const float* dir, int64_t n, int kind, float* o_out, float* d_out,
+                   int32_t* status, int32_t* id, float* t, float* u, float* v, uint8_t* shadow);
+    // the risk words for the current camera / light: src 0 the GPU's, 1 the host walk's (rt_risk_words)
+    int risk_words(int src, uint64_t* out, int64_t cap, int64_t* count, int64_t* violations);
     // Renderer::trace_ray (shaded) over n host rays at current_recursion_depth 'depth'
     int trace_ray_colors(const float* orig, const float* dir, int64_t n, int depth, float* rgba, int32_t* src,
                          float* t, uint8_t* found, uint8_t* shadow);

@@ -1122,6 +1122,103 @@ void build_wbvh(const FlatOctree& oct, WBvh& out)
     phase("exit");
 }
 
+// The conditioning bytes of child j of node N (WNode::ext / ext2, read as the query's values:
+// wq_val, a code 0 being 0) against wide-BVH triangle k below it, recomputed independently of the
+// build in x87 long double (64-bit significands: the products of float coordinates are exact, each
+// sum rounds at 2^-64 relative) from the record's float edges, i.e. for the triangle (a, a + ab,
+// a + ac) Moller-Trumbore tests (triangle.cpp:25-91):
+//   smin <= sin(alpha), s2 <= sin(alpha' / 2), alpha' = min(alpha, pi - alpha) (alpha: the angle at a);
+//   sth >= sin of the angle between the child's slab normal N and the exact normal ab x ac (1 when
+//        that angle is 90 degrees or more, or the exact normal is 0);
+//   lmax >= |ab|, |ac|;
+//   rho >= how far the axis box of the triangle's octree leaf (its k-DOP's axis slabs) reaches past
+//        the child's decoded box.
+// The slack 2^-60 on the sines is far below every build margin (sin_at_a_lb subtracts 2^-50).
+// Records whose stored normal is 0 never report a hit (Mdet = 0) and need no bound.  Returns the
+// number of violated bounds.
+static int64_t check_conditioning(const FlatOctree& oct, const WBvh& w, const WNode& N, int j, uint32_t k)
+{
+    const GTri& t = w.tris[k];
+    int64_t bad = 0;
+    const uint32_t e = N.ext[j], e2 = N.ext2[j];
+    const long double smin = wq_val(e & 0xffu, WQ_UNIT), s2 = wq_val((e >> 8) & 0xffu, WQ_UNIT);
+    const long double sth = wq_val((e >> 16) & 0xffu, WQ_UNIT);
+    const long double L = (e >> 24) == 255u ? INFINITY : wq_val(e >> 24, WQ_LEN);
+    const long double rho = wq_len(e2 & 0xffu);
+    // rho: the octree leaf's axis box within the decoded child box widened by rho
+    {
+        double lo[3], hi[3];
+        decode(N, j, lo, hi);
+        const GNode& OL = oct.nodes[w.leaf_of_k[k]];
+        for (int a = 0; a < 3; a++)
+            if (!((long double)OL.dn[a] >= (long double)lo[a] - rho && (long double)OL.df[a] <= (long double)hi[a] + rho))
+                bad++;
+    }
+    if (t.n[0] == 0.0f && t.n[1] == 0.0f && t.n[2] == 0.0f)
+        return bad;
+    const long double x0 = t.ab[0], x1 = t.ab[1], x2 = t.ab[2], y0 = t.ac[0], y1 = t.ac[1], y2 = t.ac[2];
+    const long double c0 = x1 * y2 - x2 * y1, c1 = x2 * y0 - x0 * y2, c2 = x0 * y1 - x1 * y0;
+    const long double la = sqrtl(x0 * x0 + x1 * x1 + x2 * x2), lc = sqrtl(y0 * y0 + y1 * y1 + y2 * y2);
+    const long double cl = sqrtl(c0 * c0 + c1 * c1 + c2 * c2);
+    if (!(L >= fmaxl(la, lc)))
+        bad++;
+    if (la > 0 && lc > 0) {
+        const long double sa = cl / (la * lc);
+        if (!(smin <= sa + 0x1p-60L))
+            bad++;
+        const long double ca = fabsl(x0 * y0 + x1 * y1 + x2 * y2) / (la * lc);
+        if (!(s2 <= sqrtl(fmaxl(0.0L, (1.0L - ca) / 2.0L) + 0x1p-60L)))
+            bad++;
+    } else if (smin > 0 || s2 > 0)
+        bad++;
+    const long double N0 = (int8_t)(N.nrm[j] & 0xffu), N1 = (int8_t)((N.nrm[j] >> 8) & 0xffu),
+                      N2 = (int8_t)((N.nrm[j] >> 16) & 0xffu);
+    const long double NL = sqrtl(N0 * N0 + N1 * N1 + N2 * N2);
+    const long double cs = cl > 0 && NL > 0 ? (c0 * N0 + c1 * N1 + c2 * N2) / (cl * NL) : -1.0L;
+    if (cs > 0) {
+        if (!(sth >= sqrtl(fmaxl(0.0L, 1.0L - cs * cs)) - 0x1p-60L))
+            bad++;
+    } else if (!(sth >= 1.0L))
+        bad++;
+    return bad;
+}
+
+int64_t check_risk_words(const FlatOctree& oct, const WBvh& w, const WRiskArgs& A, int sel, const uint64_t* risk)
+{
+    int64_t bad = 0;
+    if (!A.on[sel]) {
+        for (size_t v = 0; v < w.nodes.size(); v++)
+            for (int j = 0; j < W_WIDTH; j++)
+                bad += risk[(2 * v + sel) * W_WIDTH + j] != wrisk_pack(0.0f, 0xFFFFFF000000ull);
+        return bad;
+    }
+    for (size_t k = 0; k < w.tris.size(); k++) {
+        const float Kt = wbvh_risk_key(w.tris[k], A.p[sel][0], A.p[sel][1], A.p[sel][2], A.G[sel], A.nu[sel],
+                                       A.slack[sel], A.QS[sel]);
+        if (!(Kt < INFINITY))
+            continue;
+        const GNode& OL = oct.nodes[w.leaf_of_k[k]];
+        for (uint32_t e = w.tri_leaf[k], hops = 0; e != W_EMPTY && hops < 1024; e = w.parent[e >> 2], hops++) {
+            const WNode& N = w.nodes[e >> 2];
+            const int j = (int)(e & 3u);
+            const uint64_t word = risk[(2 * (size_t)(e >> 2) + sel) * W_WIDTH + j];
+            if (!(wrisk_key(word) <= Kt))
+                bad++;
+            // the at-risk box (in the node's frame) widened by rho holds the triangle's octree leaf
+            const double org[3] = {N.ox, N.oy, N.oz};
+            const double rho = wq_len(N.ext2[j] & 0xffu);
+            for (int a = 0; a < 3; a++) {
+                const double st = std::ldexp(1.0, (int)((N.exps >> (8 * a)) & 0xffu) - 127);
+                const double lo = org[a] + (double)((word >> (8 * a)) & 0xffu) * st;
+                const double hi = org[a] + (double)((word >> (8 * (a + 3))) & 0xffu) * st;
+                if (!((double)OL.dn[a] >= lo - rho && (double)OL.df[a] <= hi + rho))
+                    bad++;
+            }
+        }
+    }
+    return bad;
+}
+
 int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)
 {
     int64_t bad = 0;
@@ -1221,6 +1318,7 @@ int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)
                         if (!(sp >= lo && sp <= hi))
                             bad++;
                     }
+                    bad += check_conditioning(oct, w, N, j, k);
                     const uint32_t code = N.nrm[j] >> 24;
                     const double nn = std::sqrt((double)T.n[0] * T.n[0] + (double)T.n[1] * T.n[1] + (double)T.n[2] * T.n[2]);
                     if (code < 255 && nn > 0) {

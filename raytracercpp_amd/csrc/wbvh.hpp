@@ -577,6 +577,12 @@ inline void wbvh_risk_host(const WBvh& w, const std::vector<float>& leaf_box, co
         }
 }
 
+// Checks a frame's risk words of point sel (host or GPU-computed) against the tree (CPU tests,
+// rt_risk_words): for every triangle with a finite key (wbvh_risk_key), every entry on its leaf's
+// parent chain must hold a key <= it and an at-risk box that, widened by the entry's rho, holds the
+// triangle's octree leaf (what wbvh_closest's case (b) relies on).  Returns the number of violations.
+int64_t check_risk_words(const FlatOctree& oct, const WBvh& w, const WRiskArgs& A, int sel, const uint64_t* risk);
+
 // W_DEEP: not certified only because the stack overflowed (callers may retry with a deeper stack)
 // W_LONG: stopped after max_steps loop iterations (the caller defers the query to a later pass)
 enum WStatus : int { W_MISS = 0, W_HIT = 1, W_UNCERT = 2, W_DEEP = 3, W_LONG = 4 };

@@ -308,6 +308,33 @@ class Renderer:
                    ptr(v, _f32p), ptr(ret, _u8p))
         return ids, t, u, v, ret
 
+    def wide_query(self, orig, dirs, kind=1):
+        """rt_wide_query: the frames' wide-BVH query on the GPU with its status -> dict(o, d, status,
+        id, t, u, v, shadowed); kind 0 plain rays, 1 camera rays, 2 (hit point, normal) pairs as
+        is_shadowed's rays towards the light."""
+        o = f32(orig).reshape(-1, 3)
+        d = f32(dirs).reshape(-1, 3)
+        if d.shape != o.shape:
+            raise ValueError(f"wide_query: {o.shape[0]} origins but {d.shape[0]} directions")
+        n = o.shape[0]
+        out = dict(o=np.zeros((n, 3), np.float32), d=np.zeros((n, 3), np.float32), status=np.zeros(n, np.int32),
+                   id=np.zeros(n, np.int32), t=np.zeros(n, np.float32), u=np.zeros(n, np.float32),
+                   v=np.zeros(n, np.float32), shadowed=np.zeros(n, np.uint8))
+        self._call("rt_wide_query", ptr(o, _f32p), ptr(d, _f32p), n, int(kind), ptr(out["o"], _f32p),
+                   ptr(out["d"], _f32p), ptr(out["status"], _i32p), ptr(out["id"], _i32p), ptr(out["t"], _f32p),
+                   ptr(out["u"], _f32p), ptr(out["v"], _f32p), ptr(out["shadowed"], _u8p))
+        return out
+
+    def risk_words(self, src=0):
+        """rt_risk_words: the current camera / light risk words, src 0 the GPU's, 1 the host walk's
+        -> (words, violations of check_risk_words)."""
+        n, bad = C.c_int64(), C.c_int64()
+        self._call("rt_risk_words", int(src), None, 0, C.byref(n), None)
+        out = np.zeros(n.value, np.uint64)
+        self._call("rt_risk_words", int(src), out.ctypes.data_as(C.POINTER(C.c_uint64)), out.size, C.byref(n),
+                   C.byref(bad))
+        return out, bad.value
+
     def trace_ray(self, orig, dirs, current_recursion_depth=0):
         """Renderer::trace_ray (shaded) for a batch of rays, each with a fresh HitInfo
         -> (rgba [n,4], hit_src, t, intersection_found, shadowed)."""
