@@ -154,6 +154,8 @@ int Renderer::init(std::string& err)
         e = hipEventCreate(&ev_[i]);
     if (e == hipSuccess)
         e = hipEventCreateWithFlags(&risk_ev_, hipEventDisableTiming);
+    if (e == hipSuccess)
+        e = hipEventCreateWithFlags(&risk_mark_, hipEventDisableTiming);
     if (e != hipSuccess) {
         err = std::string("HIP init failed: ") + hipGetErrorString(e);
         return RT_EHIP;
@@ -178,6 +180,7 @@ Renderer::~Renderer()
     for (auto& e : ev_)
         if (e) hipEventDestroy(e);
     if (risk_ev_) hipEventDestroy(risk_ev_);
+    if (risk_mark_) hipEventDestroy(risk_mark_);
     for (auto& e : ring_)
         if (e) hipEventDestroy(e);
     for (auto& b : band_slot_) {
@@ -1806,7 +1809,11 @@ int Renderer::prepare_risk(KParams& P, hipStream_t stream)
             (e = rt_launch_risk_box_init(B, ne, stream)) != hipSuccess ||
             (e = rt_launch_wide_risk(P.wtris, P.wmeta, P.nodes, P.wnodes, links, links + risk_tris_, K, B, words,
                                      (int)risk_tris_, (int)risk_nodes_, &A, stream)) != hipSuccess ||
-            (e = hipEventRecord(risk_ev_, stream)) != hipSuccess)
+            // risk_ev_ is recorded on the renderer's own fence stream behind 'stream' (as a band slot's
+            // 'done'): later launches wait on it after the caller may have destroyed 'stream'
+            (e = hipEventRecord(risk_mark_, stream)) != hipSuccess ||
+            (e = hipStreamWaitEvent(fence_stream_, risk_mark_, 0)) != hipSuccess ||
+            (e = hipEventRecord(risk_ev_, fence_stream_)) != hipSuccess)
             return hip_fail(e, "wide_risk_kernel");
         risk_ev_live_ = true;
         risk_valid_ = true;

@@ -264,7 +264,8 @@ private:
     int64_t risk_nodes_ = 0, risk_tris_ = 0;   // the resident wide BVH's node and triangle counts
     float risk_cam_[3] = {0, 0, 0}, risk_light_[3] = {0, 0, 0};
     float risk_G_ = 0.0f, risk_nl_ = 0.0f, risk_nu_ = 0.0f;
-    hipEvent_t risk_ev_ = nullptr;
+    hipEvent_t risk_ev_ = nullptr;     // recorded on fence_stream_ behind the computation
+    hipEvent_t risk_mark_ = nullptr;   // recorded on the computing stream (fence_stream_ waits on it)
     bool risk_ev_live_ = false;
     // sets P.wrisk (and risk_G / risk_nl) for the frame's camera and light, recomputing the bits on
     // 'stream' when they changed; every launch that reads them waits for their computation

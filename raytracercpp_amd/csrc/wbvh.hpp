@@ -90,6 +90,12 @@ constexpr int W_WIDTH = 4;    // children per node
 #ifndef W_SOUND_A
 #define W_SOUND_A 1
 #endif
+#ifndef W_SMIN_FLOOR
+#define W_SMIN_FLOOR 0.0f   // (diagnostic builds: a floor on the children's smin, to price the slivers' widening)
+#endif
+#ifndef W_R_SCALE
+#define W_R_SCALE 1.0f      // (diagnostic builds: case (a)'s widening R scaled, to price its constants)
+#endif
 
 // host diagnostic counters (tools/variants.py build diag="-DW_DIAG=1"; rt_diag_read)
 #if defined(W_DIAG) && !defined(__HIP_DEVICE_COMPILE__)
@@ -441,6 +447,52 @@ RT_HD float wbvh_risk_key(const GTri& t, double px, double py, double pz, double
     return (double)f > K ? nextafterf(f, 0.0f) : f;
 }
 
+// Case (a)'s reach (r05, DESIGN.md 5.6 "The correlated bound"): how far a point Moller-Trumbore reports
+// (triangle.cpp:25-91) can lie from its triangle T = (a, a + ab, a + ac), and from T's plane.  With u =
+// 2^-24, N = ab x ac, s = |N| / (|ab| |ac|), q = cos(N, -d), L >= |ab|, |ac|, D >= |o - x| for every x of T,
+// the computed m, Mdet, U = m.ac, V = -m.ab, T = n.OA carry errors dm, eM, eu, ev, eT (|n - N| <= 2.83u
+// |ab||ac|, |dm| <= 3.84u |d| |o - a|, |eM| <= 3.01u |n||d|, |eu| <= 3.01u |m||ac|, |ev| <= 3.01u |m||ab|,
+// |eT| <= 4.02u |n| |o - a|).  For P' = a + u' ab + v' ac (in T: u', v' were accepted) and p' = o + t' d,
+// the identities U ab + V ac = m x N and (o - a) x d = M give
+//   Mdet (p' - P') = -(n - N) x M + eM (o - a) + eT d - dm x N - eu ab - ev ac   (+ the final roundings),
+// where |M| = |d| h, h = dist(a, line) <= L + |p' - P'|, and Mdet >= |d||N| G, G = q - 3.01u - 2.84u / s.
+// So the D terms come with 1 / G only and 1 / s meets only L (the former bound had D / (q s)):
+//   E = |p' - P'| <= [8.85u (L + E) / (s G) + 10.87u D / G + 43u^2 D / (s G) + 2.011u (D + E + L)]
+// and, by Binet-Cauchy on Mdet (p' - a).N, the distance of p' from T's plane
+//   eta <= [2.83u (L + E) / (s G) + (3.01 (D + E) + 4.02 D) u kq + 2.011u (D + E)] / (1 - 3.02u / G - 9u^2 / (s G))
+// with kq = (1 + 2.83u / (s G))(1 + 5.85u / (s G)) >= (|n| / |N|)(q / G).  tests/c/wq_lemma.cpp checks both
+// on 10^7 accepted hits (largest |p' - P'| / E 0.33, eta ratio 0.47).  Inputs: lower bounds smin <= s, qa
+// <= q; G >= qa - 5.85u / smin.  wq_reach: E (INFINITY: no bound); wq_eta: eta.  Float evaluation: every
+// constant is rounded up, every step a product or sum of non-negative terms (relative error a few u,
+// inside the final 2^-16).
+struct WReach {
+    float E, isG, iG;   // the reach, >= 1 / (s G), >= 1 / G
+};
+RT_HD WReach wq_reach(float qa, float smin, float L, float D)
+{
+    constexpr float U = 0x1p-24f;
+    WReach r;
+    const float X = __builtin_fmaf(smin, qa, -5.86f * U);   // <= s G (one rounding)
+    r.isG = X > 0.0f ? fast_rcp(X) * (1.0f + 0x1p-18f) : INFINITY;
+    r.iG = smin * r.isG * (1.0f + 0x1p-20f);
+    const float beta = __builtin_fmaf(8.86f * U, r.isG, 2.012f * U);
+    // 1 / (1 - beta) <= 1 + 2 beta for beta <= 1/2
+    const float num = U * __builtin_fmaf(8.86f, L * r.isG, __builtin_fmaf(10.88f, D * r.iG, __builtin_fmaf(43.1f * U, D * r.isG,
+                                                                                                       2.012f * (D + L))));
+    r.E = !(beta <= 0.5f) ? INFINITY : num * __builtin_fmaf(2.0f, beta, 1.0f) * (1.0f + 0x1p-16f);
+    return r;
+}
+RT_HD float wq_eta(const WReach& r, float L, float D)
+{
+    constexpr float U = 0x1p-24f;
+    const float E = r.E;
+    const float kq = __builtin_fmaf(2.84f * U, r.isG, 1.0f) * __builtin_fmaf(5.86f * U, r.isG, 1.0f);
+    const float x = __builtin_fmaf(3.03f * U, r.iG, 9.1f * U * U * r.isG);   // <= 0.17 when E is finite
+    const float n2 = U * __builtin_fmaf(2.85f * (L + E), r.isG,
+                                        __builtin_fmaf(__builtin_fmaf(3.02f, D + E, 4.03f * D), kq, 2.012f * (D + E)));
+    return n2 * __builtin_fmaf(2.0f, x, 1.0f) * (1.0f + 0x1p-16f);
+}
+
 // A frame's two risk points (kernels.hip wide_risk_kernel): sel 0 the camera (rays start at it), sel
 // 1 the light (shadow rays: o = p + 1e-4 n, d = normalize(light - p), renderer.cpp:340-402, for hit
 // points p in the scene box [lo, hi]).  The shadow rays that may use the light's keys are the ones
@@ -615,9 +667,8 @@ using WStackLocal = WStackArr<W_STACK>;   // host
 // below it can REPORT a hit (Moller-Trumbore's rounded t, u, v; triangle.cpp:25-91) that the
 // reference could record at t <= the best hit so far.  With q = |cos(n, d)| of a triangle, s =
 // sin(alpha), u = 2^-24 and D >= |o - a| (the node frame's farthest corner):
-//   (a) every reported point p' lies within R = (A + B D) / (1 - B) of its triangle, A = u (30.4 D +
-//       14.4 L) / (q s) + u (4.02 L + 2.01 D), B = 7.21 u / (q s) + 2.01 u (L: the longest edge),
-//       and within eta = u (5 + 8 / s) (2 D + R) of its plane,
+//   (a) every reported point p' lies within R = wq_reach's E of its triangle (r05: D / q and L / (q s)
+//       terms, L the longest edge) and within eta (wq_eta) of its plane,
 //       which is tilted by theta from the child's slab normal: the child's box widened by R and
 //       its slab widened by eta + R sin(theta) hold p' (q is bounded below by the cone: q >=
 //       cos(phi) - sin(theta) (1 + sin(theta)), phi the angle between N and -d);
@@ -658,7 +709,6 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
     const float aix = fabsf(ix), aiy = fabsf(iy), aiz = fabsf(iz);
 
     constexpr float SL = 0x1p-20f;   // relative slack over the rounding of a slab parameter (<= 3 ulp)
-    constexpr float U = 0x1p-24f;
     constexpr float NLH = 127.9f;    // |N| of a quantised slab normal: 127 +- sqrt(3) / 2 (wbvh.cpp quantise)
     // |d| rounded up (sqrt and dot within 2^-22), times the cone step: threshold = c * cstep
     const float dl = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z) * (1.0f + 0x1p-20f);
@@ -771,22 +821,16 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                 // a and of the threshold: < 1e-4 |d|, inside the build's 0.01 |d|): none reports a hit
                 if (chj != W_EMPTY && !(a > (float)(nrj >> 24) * cstep)) {
                     const uint32_t e = wd(WN_EXT + j);
-                    const float smin = wq_val_nz(e & 0xffu, WQ_UNIT);
+                    const float smin = fmaxf(wq_val_nz(e & 0xffu, WQ_UNIT), W_SMIN_FLOOR);
                     const float sth = wq_val_nz((e >> 16) & 0xffu, WQ_UNIT);
                     const float L = (e >> 24) == 255u ? INFINITY : wq_val_nz(e >> 24, WQ_LEN);
                     const float qlb = __builtin_fmaf(-sth, 1.0f + sth, -a * icp) - 0x1p-20f;
                     const float qa = fmaxf(qlb, QS);
-                    // (a): the box widened by R, the slab by eta + R sin(theta)
-                    // R = (A + B D) / (1 - B) with |p' - o| <= D + R folded in: A = u (30.4 D + 14.4 L) /
-                    // (q s) + u (4.02 L + 2.01 D), B = 7.21 u / (q s) + 2.01 u; 1 / (1 - B) <= 1 + 2 B for
-                    // B <= 1/2 (beyond: no bound)
-                    // A + B D = u (iq (37.61 D + 14.4 L) + 4.02 (D + L)) <= u (D + L) (37.61 iq + 4.02)
-                    const float iq = fast_rcp(qa * smin) * (1.0f + 0x1p-18f);
-                    const float Bq = __builtin_fmaf(7.21f * U, iq, 2.01f * U);
+                    // (a): the box widened by R, the slab by eta + R sin(theta) (wq_reach: the correlated bound of
+                    // Moller-Trumbore's reports, D = Dn)
 #if W_SOUND_A
-                    const float R = !(Bq <= 0.5f) ? INFINITY
-                                                  : __builtin_fmaf((Dn + L) * __builtin_fmaf(37.61f * U, iq, 4.02f * U),
-                                                                   __builtin_fmaf(2.0f * (1.0f + 0x1p-16f), Bq, 1.0f + 0x1p-16f), m);
+                    const WReach wr = wq_reach(qa, smin, L, Dn);
+                    const float R = __builtin_fmaf(W_R_SCALE, wr.E, m);
 #else
                     const float R = m;   // (timing only)
 #endif
@@ -818,7 +862,11 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                     if (ok && R < INFINITY) {
                         // N . (o + t d - origin) in [C0, C1] widened by w: t between
                         // (C0 - w + b) / a and (C1 + w + b) / a
-                        const float eta = U * __builtin_fmaf(8.0f * qa, iq, 5.0f) * __builtin_fmaf(2.0f, Dn, R);
+#if W_SOUND_A
+                        const float eta = wq_eta(wr, L, Dn);
+#else
+                        const float eta = 0.0f;
+#endif
                         const float w = NLH * __builtin_fmaf(R, sth, eta) * (1.0f + 0x1p-16f) + 384.0f * m;
                         // the hardware reciprocal (1 ulp): its error moves the slab's t by a relative
                         // 2^-23, a distance far inside the margin over the scene

@@ -7,6 +7,7 @@
 * C4 ``sphere1m``   : UV sphere nu=1000 nv=500 (1,000,000 tris, texcoords), T(0,0,-3)*Ry30*Rx20*S1.5,
                       1920x1080 with 2x2 SSAA (ssaa_factor 2)
 * C5 ``sphere1m_refl``: C4 + reflection 0.5 / roughness 0.3 / 16 samples + normal & parallax maps
+* ``hair1m``        : 50k curled ribbon strands (1,000,000 tris), C4's transform and frame
 
 All camera placements follow the survey probe: camera at the origin, fov 80,
 light (3,3,2), shadows on, BVH depth 12 / leaf 40.
@@ -245,6 +246,72 @@ def sphere1m(T=None, width=1920, height=1080, ssaa=True, **kw):
                            enable_ssaa=ssaa, ssaa_factor=2, **kw)
 
 
+def hair_triangles(nstrands=50000, nseg=10, width=0.004, root_radius=0.6, seg_len=0.05, curl=0.35, seed=1234):
+    """SURVEY.md 8(d)'s "hair1m" stress scene (BASELINE configs[3]: a ~1M-tri hair / mesh scene):
+    nstrands strands x nseg segments x 2 single-sided ribbon triangles.  Each strand starts on the
+    sphere of radius root_radius (uniform), grows outward along its radial direction tilted at random,
+    and curls: every segment turns its direction by up to `curl` radians about the strand's own random
+    axis.  A segment is a ribbon quad of the given width across (direction x the strand's side
+    vector): tris (p - w, p + w, q + w) and (p - w, q + w, q - w).  Thin, long, crossing ribbons
+    make max-depth octree pile-up leaves (bvh.h:169-193) and many slivers.
+
+    Only +, -, *, /, sqrt and det_sincos on uniforms from numpy's PCG64 (bit-reproducible on every
+    host), float64 then rounded to float32.  Returns tri9 (float32)."""
+    rng = np.random.default_rng(seed)
+    u = rng.random((nstrands, 8))
+    z = 2.0 * u[:, 0] - 1.0
+    s_, c_ = det_sincos(2.0 * np.pi * u[:, 1])
+    r = np.sqrt(np.maximum(0.0, 1.0 - z * z))
+    nrm = np.stack([r * c_, r * s_, z], 1)                        # root normal (unit)
+    # an orthonormal frame around the normal: e1 from a fixed helper axis, e2 = n x e1
+    helper = np.where(np.abs(nrm[:, :1]) < 0.9, np.array([[1.0, 0.0, 0.0]]), np.array([[0.0, 1.0, 0.0]]))
+    e1 = np.cross(helper, nrm)
+    e1 /= np.sqrt((e1 * e1).sum(1, keepdims=True))
+    e2 = np.cross(nrm, e1)
+    ts, tc = det_sincos(2.0 * np.pi * u[:, 2])
+    tilt = 0.6 * u[:, 3]                                          # radial tilt up to ~34 degrees
+    d = nrm + tilt[:, None] * (tc[:, None] * e1 + ts[:, None] * e2)
+    d /= np.sqrt((d * d).sum(1, keepdims=True))
+    axs, axc = det_sincos(2.0 * np.pi * u[:, 4])
+    axis = axc[:, None] * e1 + axs[:, None] * e2                  # the curl axis (across the strand)
+    side = np.cross(d, axis)
+    side /= np.sqrt((side * side).sum(1, keepdims=True))
+    turn = curl * (2.0 * u[:, 5] - 1.0)                           # per-segment turn, signed
+    ks, kc = det_sincos(turn)
+    p = root_radius * nrm
+    tris = np.empty((nstrands, nseg, 2, 9), np.float64)
+    for k in range(nseg):
+        q = p + seg_len * d
+        w = (0.5 * width) * side
+        a0, b0, c0, d0 = p - w, p + w, q + w, q - w
+        tris[:, k, 0] = np.concatenate([a0, b0, c0], 1)
+        tris[:, k, 1] = np.concatenate([a0, c0, d0], 1)
+        # rotate d and side about the curl axis (Rodrigues; axis is orthogonal to neither in general)
+        def rot(v):
+            ax = axis
+            dot = (ax * v).sum(1, keepdims=True)
+            return v * kc[:, None] + np.cross(ax, v) * ks[:, None] + ax * dot * (1.0 - kc[:, None])
+        d = rot(d)
+        d /= np.sqrt((d * d).sum(1, keepdims=True))
+        side = rot(side)
+        side -= d * (side * d).sum(1, keepdims=True)
+        side /= np.sqrt((side * side).sum(1, keepdims=True))
+        p = q
+    return np.ascontiguousarray(tris.reshape(-1, 9).astype(np.float32))
+
+
+def hair1m(T=None, width=1920, height=1080, ssaa=True, **kw):
+    """hair1m (BASELINE configs[3]'s hair / mesh scene): 1,000,000 ribbon triangles,
+    T(0,0,-3)*Ry30*Rx20*S1.5 like C4, 1920x1080 with 2x2 SSAA; not the headline workload (a guard
+    against tuning the grazing-sound query to one smooth sphere)."""
+    T = T or default_transforms()
+    st = base_settings(width, height, enable_ssaa=ssaa, ssaa_factor=2, **kw)
+    tri = transform_triangles(object_transform(T, -3.0, scale=1.5), hair_triangles())
+    thr = specular_threshold((0.5, 0.5, 0.5), 20.0)
+    mats = material(diffuse=(0.55, 0.4, 0.25), specular=(0.5, 0.5, 0.5), ns=20.0, specular_threshold=thr)[None]
+    return _finish(tri, np.zeros(tri.shape[0], np.int32), None, mats, _camera(T, st)), st
+
+
 def procedural_maps(size=1024, seed=1234):
     """Seeded normal + height maps for C5 (values are k/255 like an 8-bit texture read by read_image)."""
     rng = np.random.default_rng(seed)
@@ -321,4 +388,5 @@ CONFIGS = {
     "bumpy70k": bumpy70k,
     "sphere1m": sphere1m,
     "sphere1m_refl": sphere1m_refl,
+    "hair1m": hair1m,
 }

@@ -63,11 +63,12 @@ static L3 closest_on_tri(L3 p, L3 a, L3 b, L3 c)
 int main(int argc, char** argv)
 {
     const long target = argc > 1 ? std::atol(argv[1]) : 10000000L;
+    const double far = argc > 2 ? std::atof(argv[2]) : 300.0;   // origins at 0.1 .. far edge lengths
     const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::atomic<long> accepted{0}, samples{0};
     std::atomic<int> failed{0};
     std::mutex mu;
-    ld worst[3] = {0, 0, 0};
+    ld worst[4] = {0, 0, 0, 0};
     long bins[10] = {};   // acceptances by floor(-log10 Q), Q = q s
     auto work = [&](unsigned tid) {
         std::mt19937_64 rng(0x5EED0000ull + tid);
@@ -78,7 +79,7 @@ int main(int argc, char** argv)
             double x = N(rng), y = N(rng), z = N(rng), l = std::sqrt(x * x + y * y + z * z);
             return l3(x / l, y / l, z / l);
         };
-        ld w[3] = {0, 0, 0};
+        ld w[4] = {0, 0, 0, 0};
         long lb[10] = {};
         while (accepted.load(std::memory_order_relaxed) < target && !failed.load()) {
             samples++;
@@ -120,7 +121,7 @@ int main(int argc, char** argv)
                 continue;
             tdir = tdir * (1 / tl);
             const L3 d0 = tdir * std::sqrt(1 - q * q) + nh * (-q);
-            const L3 o0 = P - d0 * (std::max(la, lc) * logu(0.1, 300.0));
+            const L3 o0 = P - d0 * (std::max(la, lc) * logu(0.1, far));
             const rt::v3 o = rt::mk((float)o0.x, (float)o0.y, (float)o0.z), d = rt::mk((float)d0.x, (float)d0.y, (float)d0.z);
             float t, u, v;
             if (!rt::mt_record(T, o, d, t, u, v) || !std::isfinite(t))
@@ -142,31 +143,44 @@ int main(int argc, char** argv)
             const int bin = Q > 0 ? std::min(9, std::max(0, (int)std::floor(-std::log10((double)Q)))) : 9;
             lb[bin]++;
             const ld H0 = 1.01L * (qq * (2 * L + D) + uu * (24.2L * L + 48 * D) / s + uu * (30 * L + 12 * D + 24 * D / s) / s2);
-            ld r2 = od / H0, r0 = 0, r1 = 0;
+            ld r2 = od / H0, r0 = 0, r1 = 0, r3 = 0;
             bool bad = !(od <= H0);
-            const ld B = 7.21L * uu / Q + 2.01L * uu;
-            if (B <= 0.5L) {
-                const ld Aa = uu * (30.4L * Dv + 14.4L * L) / Q + uu * (4.02L * L + 2.01L * Dv);
-                const ld R = (Aa + B * Dv) / (1 - B);
-                const ld eta = uu * (5 + 8 / s) * (2 * Dv + R);
-                const L3 cp = closest_on_tri(Pp, A, A + AB, A + AC);
-                const ld dist = lenl(Pp - cp);
-                r0 = dist / R;
-                r1 = pl / eta;
-                bad |= !(dist <= R) || !(pl <= eta);
+            // case (a), wbvh.hpp wq_reach (the correlated bound): G >= q - 5.85u / s,
+            // isG >= 1 / (s G), iG >= 1 / G
+            const ld X = s * qq - 5.85L * uu;
+            if (X > 0) {
+                const ld isG = 1 / X, iG = s * isG;
+                const ld beta = 8.85L * uu * isG + 2.011L * uu;
+                if (beta <= 0.5L) {
+                    const ld E = (8.85L * uu * (1 + uu) * L * isG + 10.87L * uu * Dv * iG + 43 * uu * uu * Dv * isG +
+                                  2.011L * uu * (Dv + L)) * (1 + 2 * beta);
+                    const ld kq = (1 + 2.83L * uu * isG) * (1 + 5.85L * uu * isG);
+                    const ld eta = (2.83L * uu * ((1 + uu) * L + E) * isG + (3.01L * (Dv + E) + 4.02L * Dv) * uu * kq +
+                                    2.011L * uu * (Dv + E)) / (1 - 3.02L * uu * iG - 9 * uu * uu * isG);
+                    // P' = a + u' ab + v' ac (MT's accepted barycentrics), |p' - P'| <= E
+                    const L3 Pq = A + AB * (ld)u + AC * (ld)v;
+                    const ld pP = lenl(Pp - Pq);
+                    const L3 cp = closest_on_tri(Pp, A, A + AB, A + AC);
+                    const ld dist = lenl(Pp - cp);
+                    r0 = dist / (E + 2.02L * uu * L);
+                    r3 = pP / E;
+                    r1 = pl / eta;
+                    bad |= !(dist <= E + 2.02L * uu * L) || !(pP <= E) || !(pl <= eta);
+                }
             }
             w[0] = fmaxl(w[0], r0);
             w[1] = fmaxl(w[1], r1);
             w[2] = fmaxl(w[2], r2);
+            w[3] = fmaxl(w[3], r3);
             if (bad && !failed.exchange(1)) {
                 std::lock_guard<std::mutex> g(mu);
                 std::printf("VIOLATION q %.6Lg s %.6Lg s2 %.6Lg D %.6Lg L %.6Lg t %.9g u %.9g v %.9g: dist/R %.6Lg "
-                            "plane/eta %.6Lg origin/H0 %.6Lg\n",
-                            qq, s, s2, D, L, t, u, v, r0, r1, r2);
+                            "plane/eta %.6Lg origin/H0 %.6Lg |p'-P'|/E %.6Lg\n",
+                            qq, s, s2, D, L, t, u, v, r0, r1, r2, r3);
             }
         }
         std::lock_guard<std::mutex> g(mu);
-        for (int i = 0; i < 3; i++)
+        for (int i = 0; i < 4; i++)
             worst[i] = fmaxl(worst[i], w[i]);
         for (int i = 0; i < 10; i++)
             bins[i] += lb[i];
@@ -178,8 +192,8 @@ int main(int argc, char** argv)
         x.join();
     if (failed.load())
         return 1;
-    std::printf("ok %ld %.4Lg %.4Lg %.4Lg samples %ld Q-decades", accepted.load(), worst[0], worst[1], worst[2],
-                samples.load());
+    std::printf("ok %ld %.4Lg %.4Lg %.4Lg %.4Lg samples %ld Q-decades", accepted.load(), worst[0], worst[1], worst[2],
+                worst[3], samples.load());
     for (int i = 0; i < 10; i++)
         std::printf(" %ld", bins[i]);
     std::printf("\n");

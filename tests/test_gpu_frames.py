@@ -1,0 +1,110 @@
+"""Frame-engine invariants on the GPU: the risk words' event survives the caller's
+stream, and the heavy-tiles-first order traces every tile exactly once.  Reference path:
+Renderer::ray_trace (renderer.cpp:1068-1116), whose rows and tiles are independent."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle.bindings import Oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def make_renderer():
+    import os
+    from raytracercpp_amd.renderer import Renderer
+    made = []
+
+    def make(**env):
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update({k: str(v) for k, v in env.items()})
+        try:
+            r = Renderer(0)
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+        made.append(r)
+        return r
+    yield make
+    for r in made:
+        r.close()
+
+
+def test_risk_words_after_the_band_stream_is_destroyed(make_renderer):
+    """The frame's risk words are computed on the first band launch's stream; that stream is then
+    destroyed, and the next launches (same camera and light: they only wait for the words' event)
+    run on new streams.  Every frame equals the one-call render."""
+    import torch
+    from raytracercpp_amd import scenes
+    from raytracercpp_amd.strips import assemble
+    R = make_renderer()
+    sc, st = scenes.bumpy70k(width=160, height=96)
+    R.load_scene(sc, st)
+    R.ray_trace()
+    R.finish_accel()
+    hip = ctypes.CDLL("libamdhip64.so")
+    band, nranks = 8, 2
+    full = None
+    for rep in range(3):
+        if rep == 1:
+            R.set_light_position((2.0, 4.0, 1.0))   # new words, computed on this round's first stream
+        R.ray_trace()
+        R.post_process()
+        full = R.get_image()
+        parts = []
+        for rank in range(nranks):
+            h = ctypes.c_void_p()
+            assert hip.hipStreamCreate(ctypes.byref(h)) == 0
+            b = torch.zeros((R.local_rows(band, rank, nranks), st.image_width), dtype=torch.int32, device="cuda:0")
+            torch.cuda.synchronize()
+            R.render_bands_device(band, rank, nranks, b.data_ptr(), h.value)
+            assert hip.hipStreamSynchronize(h) == 0
+            assert hip.hipStreamDestroy(h) == 0   # the stream the risk words were computed on is gone
+            parts.append(b.cpu().numpy().view(np.uint32))
+        assert np.array_equal(assemble(parts, st.image_height, band), full), rep
+
+
+def _heavy_tiles(cost):
+    """heavy_prep_kernel's rule (kernels.hip): tiles costing >= max(4 x mean, max / 8), at most
+    ntiles / 16 of them."""
+    c = cost.ravel().astype(np.uint64)
+    thr = max(4 * int(c.sum() // c.size), int(c.max()) // 8)
+    return min(int(((c >= thr) & (c > 0)).sum()), c.size // 16)
+
+
+@pytest.mark.parametrize("ssaa", [False, True])
+def test_heavy_first_frames_trace_every_tile_once(make_renderer, ssaa):
+    """Heavy tiles first (Renderer::prepare_heavy): each frame dequeues the previous frame's costliest
+    tiles first.  The light moves between frames, so a tile that was skipped would keep the previous
+    frame's pixels and one traced twice would show no difference only if both traces agree: every
+    frame must equal the oracle's for its own light, and the heavy list must not be empty."""
+    from raytracercpp_amd import scenes
+    R = make_renderer()
+    sc, st = scenes.bumpy70k(width=160, height=96, enable_ssaa=ssaa, ssaa_factor=2)
+    R.load_scene(sc, st)
+    R.ray_trace()
+    R.finish_accel()
+    R.request_aux(hit=True, shadow=True)
+    lights = [(3.0, 3.0, 2.0), (-2.0, 3.5, 1.0), (0.5, -3.0, 2.5), (3.0, 0.5, -1.0)]
+    heavy = []
+    for L in lights:
+        R.set_light_position(L)
+        heavy.append(_heavy_tiles(R.tile_costs()))
+        R.ray_trace()
+        g = R.get_internal(argb=True, hit=True, shadow=True)
+        sc.light = np.asarray(L, np.float32)
+        o = Oracle(sc, st).render_rows()
+        assert np.array_equal(g["hit_id"], o.hit_id), L
+        assert np.array_equal(g["shadow"], o.shadow), L
+        assert np.array_equal(g["argb"], o.argb), L
+        R.post_process()
+        rw, rh = st.render_size()
+        exp = Oracle.downscale(o.argb, rw, rh, 2) if ssaa else o.argb
+        assert np.array_equal(R.get_image().ravel(), exp), L
+    print("heavy tiles per frame:", heavy)
+    assert min(heavy) > 0
