@@ -482,6 +482,26 @@ RT_HD WReach wq_reach(float qa, float smin, float L, float D)
     r.E = !(beta <= 0.5f) ? INFINITY : num * __builtin_fmaf(2.0f, beta, 1.0f) * (1.0f + 0x1p-16f);
     return r;
 }
+// The same error split into a lateral part and a part along d: p' - P' = lat + par, par parallel to d.
+// Only the terms eT d, the d-component of eM (o - a) (o - a = (P' - a) + (p' - P') - t' d) and the final
+// rounding of t' lie along d; so P' + lat, a point of the line, lies within Rlat of T (the line crosses
+// the box widened by Rlat) and p' lies within Rpar of it along the line:
+//   Rlat <= 8.85u (L + E) / (s G) + 3.01u kn (L + E) / G + 3.84u D / G + 23.2u^2 D / (s G) + 2.012u L,
+//   Rpar <= (4.02 D + 3.01 (D + E)) u kn / G + 2.011u (D + E),   kn = 1 + 2.83u / (s G) >= |n| / |N|.
+// The D / q term of the lateral reach is 3.84u D / G against 10.87u D / G for E (tests/c/wq_lemma.cpp:
+// largest lat / Rlat 0.38).
+RT_HD void wq_split(const WReach& r, float L, float D, float& Rlat, float& Rpar)
+{
+    constexpr float U = 0x1p-24f;
+    const float E = r.E;
+    const float kn = __builtin_fmaf(2.84f * U, r.isG, 1.0f);
+    const float LE = (L + E) * (1.0f + 0x1p-22f);
+    Rlat = U * __builtin_fmaf(8.86f * LE, r.isG,
+                              __builtin_fmaf(__builtin_fmaf(3.03f * LE, kn, 3.85f * D), r.iG,
+                                             __builtin_fmaf(23.3f * U * D, r.isG, 2.013f * L))) * (1.0f + 0x1p-16f);
+    Rpar = U * __builtin_fmaf(__builtin_fmaf(4.03f, D, 3.02f * (D + E)) * kn, r.iG, 2.012f * (D + E)) * (1.0f + 0x1p-16f);
+}
+
 RT_HD float wq_eta(const WReach& r, float L, float D)
 {
     constexpr float U = 0x1p-24f;
@@ -713,6 +733,8 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
     // |d| rounded up (sqrt and dot within 2^-22), times the cone step: threshold = c * cstep
     const float dl = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z) * (1.0f + 0x1p-20f);
     const float cstep = dl * W_CONE_STEP;
+    // 1 / |d| rounded up (|d| rounded down, the hardware reciprocal within 1 ulp)
+    const float idl = fast_rcp(sqrtf(d.x * d.x + d.y * d.y + d.z * d.z) * (1.0f - 0x1p-20f)) * (1.0f + 0x1p-18f);
     const float icp = (1.0f - 0x1p-18f) / (NLH * dl);   // cos(angle(N, -d)) >= -a icp
     const float iqd = (1.0f - 0x1p-20f) / (QS * dl);        // a risk key's t bound: key / (QS |d|)
     float best_s = hi + fabsf(hi) * SL;   // h.t (or hi) plus slack: a child entered at or below it may hold a hit
@@ -831,8 +853,14 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
 #if W_SOUND_A
                     const WReach wr = wq_reach(qa, smin, L, Dn);
                     const float R = __builtin_fmaf(W_R_SCALE, wr.E, m);
+                    // the box test: the line crosses the box widened by the lateral reach, and a report lies
+                    // within Rpar of that crossing along the line (wq_split)
+                    float Rlat, Rpar;
+                    wq_split(wr, L, Dn, Rlat, Rpar);
+                    const float Rb = __builtin_fmaf(W_R_SCALE, Rlat, m);
+                    const float dtp = W_R_SCALE * Rpar * idl;
 #else
-                    const float R = m;   // (timing only)
+                    const float R = m, Rb = m, dtp = 0.0f;   // (timing only)
 #endif
                     // the entry / exit planes' t of this child's box widened by M:
                     // q (s / d) + (origin - o) / d -+ M / |d| per axis
@@ -854,7 +882,9 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                     const float C1 = __builtin_fmaf((float)(sbj >> 16), ss, slo);
                     const float b = nx * Dx + ny * Dy + nz * Dz;   // N . (origin - o)
                     float tmin, tmax;
-                    box(R, tmin, tmax);
+                    box(Rb, tmin, tmax);
+                    tmin -= dtp;
+                    tmax += dtp;
                     // enter when max(tmin, 0) <= min(tmax (1 + SL), best_s); a NaN tmin (every
                     // slab NaN) enters too.  The key orders the children; misses get INFINITY.
                     bool ok = fmaxf(tmin, 0.0f) <= fminf(__builtin_fmaf(fabsf(tmax), SL, tmax), best_s);
@@ -879,8 +909,27 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                     if (ok)
                         key[j] = fminf(fmaxf(tmin, 0.0f), 3.0e38f);
 #if defined(W_TRACE) && !defined(__HIP_DEVICE_COMPILE__)
-                    printf("node %u child %d leaf %d: qlb %.4g smin %.3g sth %.3g L %.3g Dn %.3g R %.3g tmin %.5g tmax %.5g ok %d best %.5g\n",
-                           cur, j, (int)((chj & W_LEAF) != 0), qlb, smin, sth, L, Dn, R, tmin, tmax, (int)ok, best_s);
+                    {
+                        // the r03 test (box and slab widened by m only) for comparison: why the child is entered
+                        float t0, t1;
+                        box(m, t0, t1);
+                        bool ok0 = fmaxf(t0, 0.0f) <= fminf(__builtin_fmaf(fabsf(t1), SL, t1), best_s);
+                        bool okbox = ok0;
+                        if (ok0) {
+                            const float ia = fast_rcp(a);
+                            const float s0 = (C0 - 384.0f * m + b) * ia, s1 = (C1 + 384.0f * m + b) * ia;
+                            t0 = fmaxf(t0, fminf(s0, s1));
+                            t1 = fminf(t1, fmaxf(s0, s1));
+                            ok0 = fmaxf(t0, 0.0f) <= fminf(__builtin_fmaf(fabsf(t1), SL, t1), best_s);
+                        }
+                        float b0, b1;
+                        box(Rb, b0, b1);
+                        const bool okRbox = fmaxf(b0 - dtp, 0.0f) <= fminf(b1 + dtp, best_s);
+                        printf("node %u child %d leaf %d: qlb %.4g smin %.3g sth %.3g L %.3g Dn %.3g R %.3g Rlat %.3g Rpar %.3g "
+                               "tmin %.5g tmax %.5g ok %d (tight box %d, tight %d, widened box %d) best %.5g\n",
+                               cur, j, (int)((chj & W_LEAF) != 0), qlb, smin, sth, L, Dn, R, Rlat, Rpar, tmin, tmax, (int)ok,
+                               (int)okbox, (int)ok0, (int)okRbox, best_s);
+                    }
 #endif
                     W_DIAG_ADD(1, 1);
                     W_DIAG_ADD(2, ok);
@@ -933,6 +982,9 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                             const float w = NLH * (H0 + __builtin_fmaf(Dn, sth, m)) * (1.0f + 0x1p-16f) + 384.0f * m;
                             okb = !(-b < C0 - w || -b > C1 + w);   // N . (o - origin) = -b
                         }
+#if defined(W_TRACE) && !defined(__HIP_DEVICE_COMPILE__)
+                        printf("  (b) node %u child %d: okb %d kbl %.5g key %.5g\n", cur, j, (int)okb, kbl, key[j]);
+#endif
                         if (okb) {
                             W_DIAG_ADD(3, !ok);
                             W_DIAG_ADD(6, !ok && (chj & W_LEAF));

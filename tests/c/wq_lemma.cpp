@@ -68,7 +68,7 @@ int main(int argc, char** argv)
     std::atomic<long> accepted{0}, samples{0};
     std::atomic<int> failed{0};
     std::mutex mu;
-    ld worst[4] = {0, 0, 0, 0};
+    ld worst[5] = {0, 0, 0, 0, 0};
     long bins[10] = {};   // acceptances by floor(-log10 Q), Q = q s
     auto work = [&](unsigned tid) {
         std::mt19937_64 rng(0x5EED0000ull + tid);
@@ -79,7 +79,7 @@ int main(int argc, char** argv)
             double x = N(rng), y = N(rng), z = N(rng), l = std::sqrt(x * x + y * y + z * z);
             return l3(x / l, y / l, z / l);
         };
-        ld w[4] = {0, 0, 0, 0};
+        ld w[5] = {0, 0, 0, 0, 0};
         long lb[10] = {};
         while (accepted.load(std::memory_order_relaxed) < target && !failed.load()) {
             samples++;
@@ -143,7 +143,7 @@ int main(int argc, char** argv)
             const int bin = Q > 0 ? std::min(9, std::max(0, (int)std::floor(-std::log10((double)Q)))) : 9;
             lb[bin]++;
             const ld H0 = 1.01L * (qq * (2 * L + D) + uu * (24.2L * L + 48 * D) / s + uu * (30 * L + 12 * D + 24 * D / s) / s2);
-            ld r2 = od / H0, r0 = 0, r1 = 0, r3 = 0;
+            ld r2 = od / H0, r0 = 0, r1 = 0, r3 = 0, r4 = 0;
             bool bad = !(od <= H0);
             // case (a), wbvh.hpp wq_reach (the correlated bound): G >= q - 5.85u / s,
             // isG >= 1 / (s G), iG >= 1 / G
@@ -166,21 +166,34 @@ int main(int argc, char** argv)
                     r3 = pP / E;
                     r1 = pl / eta;
                     bad |= !(dist <= E + 2.02L * uu * L) || !(pP <= E) || !(pl <= eta);
+                    // wq_split: p' - P' = lat + par with par along d, |par| <= Rpar, |lat| <= Rlat, i.e. P' lies
+                    // within Rlat of the line's segment [p' - Rpar d^, p' + Rpar d^]
+                    const ld kn = 1 + 2.83L * uu * isG;
+                    const ld Rlat = 8.85L * uu * ((1 + uu) * L + E) * isG + 3.02L * uu * ((1 + uu) * L + E) * iG * kn +
+                                    3.84L * uu * Dv * iG + 23.2L * uu * uu * Dv * isG + 2.012L * uu * L;
+                    const ld Rpar = (4.02L * D + 3.01L * (Dv + E)) * uu * iG * kn + 2.011L * uu * (Dv + E);
+                    const ld dl = lenl(Dd);
+                    const L3 dh = Dd * (1 / dl);
+                    const ld x = std::max(-Rpar, std::min(Rpar, dotl(Pq - Pp, dh)));
+                    const ld lat = lenl(Pq - (Pp + dh * x));
+                    r4 = lat / Rlat;
+                    bad |= !(lat <= Rlat);
                 }
             }
             w[0] = fmaxl(w[0], r0);
             w[1] = fmaxl(w[1], r1);
             w[2] = fmaxl(w[2], r2);
             w[3] = fmaxl(w[3], r3);
+            w[4] = fmaxl(w[4], r4);
             if (bad && !failed.exchange(1)) {
                 std::lock_guard<std::mutex> g(mu);
                 std::printf("VIOLATION q %.6Lg s %.6Lg s2 %.6Lg D %.6Lg L %.6Lg t %.9g u %.9g v %.9g: dist/R %.6Lg "
-                            "plane/eta %.6Lg origin/H0 %.6Lg |p'-P'|/E %.6Lg\n",
-                            qq, s, s2, D, L, t, u, v, r0, r1, r2, r3);
+                            "plane/eta %.6Lg origin/H0 %.6Lg |p'-P'|/E %.6Lg lat/Rlat %.6Lg\n",
+                            qq, s, s2, D, L, t, u, v, r0, r1, r2, r3, r4);
             }
         }
         std::lock_guard<std::mutex> g(mu);
-        for (int i = 0; i < 4; i++)
+        for (int i = 0; i < 5; i++)
             worst[i] = fmaxl(worst[i], w[i]);
         for (int i = 0; i < 10; i++)
             bins[i] += lb[i];
@@ -192,8 +205,8 @@ int main(int argc, char** argv)
         x.join();
     if (failed.load())
         return 1;
-    std::printf("ok %ld %.4Lg %.4Lg %.4Lg %.4Lg samples %ld Q-decades", accepted.load(), worst[0], worst[1], worst[2],
-                worst[3], samples.load());
+    std::printf("ok %ld %.4Lg %.4Lg %.4Lg %.4Lg %.4Lg samples %ld Q-decades", accepted.load(), worst[0], worst[1],
+                worst[2], worst[3], worst[4], samples.load());
     for (int i = 0; i < 10; i++)
         std::printf(" %ld", bins[i]);
     std::printf("\n");
