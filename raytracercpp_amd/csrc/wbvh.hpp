@@ -61,14 +61,15 @@ constexpr int W_STACK = W_STACK_N;   // traversal stack entries per lane (a chil
 constexpr int W_WIDTH = 4;    // children per node
 
 // the grazing split QS of the wide query's child test per query kind (wbvh_closest, wbvh_risk_key):
-// (a)'s box widening grows as 1 / QS, the risk set of case (b) as QS.  Host node visits per ray on C4
-// (stride-16 rays, tools/wbvh_probe.py rays): camera 2^-5..2^-10: 8.66 / 7.89 / 7.64 / 7.98 / 9.59 /
-// 11.90; shadow 2^-8..2^-16: 15.05 / 13.06 / 11.84 / 13.79 / 29.79.  The camera's 2^-8 is not the
-// mean's minimum but the critical path's: the costliest 8x8 tiles (grazing rays near the silhouette,
-// ~280 node visits at 2^-7 against ~115 at 2^-8, tools/tile_costs.py) span the whole C4 launch, whose
-// kernel time drops 2.33 -> 1.84 ms (profiles/r04/qs8.log) for +5% mean visits
+// (a)'s reach grows as 1 / QS (wq_reach: its D term is 10.87u D / QS), the risk set of case (b) as QS.
+// r05, with the correlated reach (tools/visit_probe.py, host wide-node visits per C4 ray, every 8th
+// tile row): camera 2^-8 / 2^-10 / 2^-12 / 2^-14: 5.71 / 5.15 / 4.83 / 52 (at 2^-14 the pole slivers'
+// s q falls below the bound's 5.86u: no reach); shadow 2^-11 / 2^-12 / 2^-13 / 2^-14: 7.72 / 7.06 /
+// 8.61 / 8.55.  On the GPU (three scenes, so that the choice is not the headline sphere's alone,
+// profiles/r05/qs_scenes.log): camera 2^-10 is ahead of 2^-8 on C4 (+7.8%), hair1m (+5%) and robot
+// (+1%); 2^-12 is ahead on C4 only (hair1m -6%, robot -4%)
 #ifndef W_QS_CLOSEST
-#define W_QS_CLOSEST 0x1p-8f
+#define W_QS_CLOSEST 0x1p-10f
 #endif
 #ifndef W_QS_SHADOW
 #define W_QS_SHADOW 0x1p-12f

@@ -108,3 +108,33 @@ def test_heavy_first_frames_trace_every_tile_once(make_renderer, ssaa):
         assert np.array_equal(R.get_image().ravel(), exp), L
     print("heavy tiles per frame:", heavy)
     assert min(heavy) > 0
+
+
+@pytest.mark.parametrize("camera", ["default", "grazing"])
+def test_hair1m_frame_matches_oracle(make_renderer, camera):
+    """SURVEY.md 8(d)'s hair1m stress scene (1M crossing ribbon triangles, BASELINE configs[3]'s hair /
+    mesh scene) at reduced resolution, first frame on the octree path and the next ones on the wide BVH
+    (its sound query and the camera / light risk words): every internal pixel's hit ID, t, shadow flag
+    and ARGB bit for bit, the SSAA frame too.  'grazing': the camera moved to the hair's silhouette."""
+    from raytracercpp_amd import scenes
+    R = make_renderer()
+    sc, st = scenes.hair1m(width=240, height=136)
+    if camera == "grazing":
+        sc.cam_pos = np.array([0.0, 1.62, -0.2], np.float32)
+        sc.cam_to_world = np.array([1, 0, 0, 0.0, 0, 1, 0, 1.62, 0, 0, 1, -0.2, 0, 0, 0, 1], np.float32)
+    o = Oracle(sc, st).render_rows()
+    R.load_scene(sc, st)
+    R.request_aux(hit=True, shadow=True)
+    for frame in ("octree", "wide BVH"):
+        R.ray_trace()
+        g = R.get_internal(argb=True, hit=True, shadow=True)
+        assert np.array_equal(g["hit_id"], o.hit_id), f"{frame}: {int((g['hit_id'] != o.hit_id).sum())} hit-ID mismatches"
+        assert np.array_equal(g["hit_t"].view(np.uint32), o.hit_t.view(np.uint32)), frame
+        assert np.array_equal(g["shadow"], o.shadow), frame
+        assert np.array_equal(g["argb"], o.argb), frame
+        R.post_process()
+        rw, rh = st.render_size()
+        assert np.array_equal(R.get_image().ravel(), Oracle.downscale(o.argb, rw, rh, 2)), frame
+        R.finish_accel()
+    print(f"hair1m {camera}: {int((o.hit_id >= 0).sum())} of {o.hit_id.size} pixels hit, "
+          f"{o.counters['shadow_rays']} shadow rays")
