@@ -874,11 +874,18 @@ __device__ __forceinline__ void ph_mark(int k)
 
 // The lane's wide-BVH traversal stack: entry i at lv[i * BLOCK] (the LDS of the octree
 // level stack, which is not live during the wide-BVH query).
+// A lane's LDS entries (uint2, entry i at lane + i * BLOCK): the octree walk's level stack (P.levels) or
+// the wide query's stack (W_STACK), then LDS_SAVE_ENTRIES more from lds_save_slot (trace_pixel)
+constexpr int LDS_SAVE_ENTRIES = 3;
+__host__ __device__ __forceinline__ int lds_save_slot(const KParams& P) { return P.levels > W_STACK ? P.levels : W_STACK; }
+
 struct WStackLds {
     static constexpr int CAP = W_STACK;
     uint2* base;
     __device__ __forceinline__ void put(int i, uint2 v) { base[i * BLOCK] = v; }
     __device__ __forceinline__ uint2 get(int i) const { return base[i * BLOCK]; }
+    // entry i of the lane 'delta' lanes away (a lane group's steal, wbvh_closest<.., G>)
+    __device__ __forceinline__ uint2 get_lane(int delta, int i) const { return base[delta + i * BLOCK]; }
 };
 
 #if RT_COUNT
@@ -921,6 +928,7 @@ __device__ __noinline__ int wide_closest_deep(const WNode* wnodes, const GTri* w
 // certified; false when it must be traced through the octree.
 // rec (optional): on a certified hit, the record built from the wide BVH's own copies (the
 // triangle from wtris, index and material from wmeta), with no further dependent loads.
+template <int G = 1>
 __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit& h, bool& r, uint2* lv,
                                              Rec* rec = nullptr, uint32_t max_steps = 0, bool* longq = nullptr)
 {
@@ -931,7 +939,7 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
     const uint64_t* rk = P.wrisk && o.x == P.cam_pos[0] && o.y == P.cam_pos[1] && o.z == P.cam_pos[2] ? P.wrisk : nullptr;
 #if RT_COUNT
     uint32_t wk[4] = {0, 0, 0, 0};
-    int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, INFINITY, true,
+    int st = wbvh_closest<WStackLds, G>(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, INFINITY, true,
                           W_QS_CLOSEST, rk, 0, 0.0f);
     count_wave_steps(P, 22, wk[3]);
     if (P.counters) {
@@ -942,7 +950,7 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
                 atomicAdd(&P.counters[16 + c], 1ull);   // uncertified, by reason (wbvh_closest)
     }
 #else
-    int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, INFINITY,
+    int st = wbvh_closest<WStackLds, G>(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, INFINITY,
                           true, W_QS_CLOSEST, rk, 0, 0.0f, max_steps);
 #endif
     if (st == W_LONG) {
@@ -996,6 +1004,7 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
 // Returns true when decided (shadowed in *sh); false: take the octree segment query.
 // light: the ray is one of the frame's shadow rays towards P.light that may read its risk keys
 // (KParams::wrisk; hi >= |light - o|)
+template <int G = 1>
 __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float hi, v3 p, v3 lp, uint2* lv, bool* sh,
                                             bool light)
 {
@@ -1006,7 +1015,7 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
     const float rsub = light ? wrisk_sub(W_QS_SHADOW, hi, P.risk_nu) : 0.0f;
 #if RT_COUNT
     uint32_t wk[4] = {0, 0, 0, 0};
-    int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, hi, false,
+    int st = wbvh_closest<WStackLds, G>(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, hi, false,
                           W_QS_SHADOW, rk, 1, rsub);
     count_wave_steps(P, 25, wk[3]);
     if (P.counters) {
@@ -1017,7 +1026,7 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
                 atomicAdd(&P.counters[16 + c], 1ull);   // uncertified, by reason (wbvh_closest)
     }
 #else
-    int st = wbvh_closest(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, hi, false,
+    int st = wbvh_closest<WStackLds, G>(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, hi, false,
                           W_QS_SHADOW, rk, 1, rsub);
 #endif
     if (st == W_DEEP)
@@ -1113,7 +1122,7 @@ __device__ __forceinline__ OctQ octree_query(const KParams& P, v3 o, v3 d, float
 }
 
 // renderer.cpp:340-402
-template <bool PLAIN = false>
+template <bool PLAIN = false, int G = 1>
 __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
 {
     if (!P.compute_shadows)
@@ -1139,7 +1148,7 @@ __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
         }
         // (seg_scale > 0: no analytic shapes, so shapes_shadow below has nothing to add)
         bool sh;
-        if (P.wnodes && P.nnodes > 0 && !nan && wide_shadow(P, o, d, hi, p, lp, lv, &sh, light))
+        if (P.wnodes && P.nnodes > 0 && !nan && wide_shadow<G>(P, o, d, hi, p, lp, lv, &sh, light))
             return sh;
         const OctQ q = octree_query<PLAIN>(P, o, d, -m, hi, P.seg_oct != 0, lv);
         h = q.h;
@@ -1216,7 +1225,7 @@ __device__ __forceinline__ void shapes_closest(const KParams& P, v3 o, v3 d, Rec
 // fin is the caller's HitInfo; returns the source (-1 none, >=0 triangle, -2-k shape k).
 // With the wide BVH (P.wnodes), a certified query takes its answer; one it cannot certify
 // is traced through the octree here.
-template <bool PLAIN = false>
+template <bool PLAIN = false, int G = 1>
 __device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv)
 {
     Rec local = rec_fresh();
@@ -1225,7 +1234,7 @@ __device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv)
         THit h;
         bool r = false;
         const bool wide = P.wnodes && P.nnodes > 0 && !ray_is_nan(o, d);
-        if (wide && wide_closest(P, o, d, h, r, lv, &local)) {
+        if (wide && wide_closest<G>(P, o, d, h, r, lv, &local)) {
             // certified: a hit's record is already in local (a miss leaves it fresh)
             if (r && (local.t < fin.t || fin.t == -1)) {
                 fin = local;
@@ -1358,7 +1367,7 @@ __device__ c3 shade_debug(const KParams& P, const Rec& h)
     return fc;
 }
 
-template <bool PLAIN = false>
+template <bool PLAIN = false, int G = 1>
 __device__ Direct shade_direct(const KParams& P, v3 ro, v3 rd, Rec& h, uint2* lv, unsigned& nshadow)
 {
     Direct out;
@@ -1370,7 +1379,7 @@ __device__ Direct shade_direct(const KParams& P, v3 ro, v3 rd, Rec& h, uint2* lv
             nshadow++;
         v3 light = mk(P.light[0], P.light[1], P.light[2]);
         if (PLAIN) PH_MARK(3);
-        out.shadowed = is_shadowed<PLAIN>(P, out.ip, h.normal, light, lv);
+        out.shadowed = is_shadowed<PLAIN, G>(P, out.ip, h.normal, light, lv);
         if (PLAIN) PH_MARK(4);
         out.fc = shade_shadow_emit(P, fc, mat_of(P, h.mat), out.shadowed);
     } else
@@ -1475,7 +1484,7 @@ struct PixelOut {
 
 // Renderer::trace_ray (renderer.cpp:1008-1066) for one primary ray, with the
 // compute_reflection recursion (when REFL) unrolled onto an explicit stack.
-template <bool REFL, bool PLAIN = false>
+template <bool REFL, bool PLAIN = false, int G = 1>
 __device__ PixelOut trace_pixel(const KParams& P, v3 cam, v3 rd0, uint2* lv, uint32_t pixel_key, unsigned& nshadow,
                                 unsigned& nrefl)
 {
@@ -1483,12 +1492,41 @@ __device__ PixelOut trace_pixel(const KParams& P, v3 cam, v3 rd0, uint2* lv, uin
     po.fin = rec_fresh();
     po.found = po.shadowed = false;
     po.alpha = 1.0f;
-    po.src = closest_hit<PLAIN && !REFL>(P, cam, rd0, po.fin, lv);
+    po.src = closest_hit<PLAIN && !REFL, REFL ? 1 : G>(P, cam, rd0, po.fin, lv);
     if (PLAIN) PH_MARK(2);
     if (!REFL) {
+        if (PLAIN && po.fin.t > 0.1f) {
+            // shade_direct<true> with what the pixel needs after its shadow query (the lit colour, the
+            // material, the record's t and the source) waiting in the lane's LDS slots past the traversal
+            // stack: the query's loop takes every register, and values held across it were spilled to
+            // scratch (HBM writes)
+            po.found = true;
+            v3 ip;
+            const c3 fc = shade_lit<true>(P, cam, rd0, po.fin, ip);
+            if (P.compute_shadows)
+                nshadow++;
+            uint2* sv = lv + (size_t)lds_save_slot(P) * BLOCK;
+            sv[0] = make_uint2(fbits(fc.r), fbits(fc.g));
+            sv[BLOCK] = make_uint2(fbits(fc.b), (uint32_t)po.fin.mat);
+            sv[2 * BLOCK] = make_uint2(fbits(po.fin.t), (uint32_t)po.src);
+            asm volatile("" ::: "memory");
+            const v3 light = mk(P.light[0], P.light[1], P.light[2]);
+            if (PLAIN) PH_MARK(3);
+            po.shadowed = is_shadowed<true, G>(P, ip, po.fin.normal, light, lv);
+            if (PLAIN) PH_MARK(4);
+            asm volatile("" ::: "memory");
+            const uint2 s0 = sv[0], s1 = sv[BLOCK], s2 = sv[2 * BLOCK];
+            po.fin.mat = (int)s1.y;
+            po.fin.t = bitsf(s2.x);
+            po.src = (int)s2.y;
+            const float* m = mat_of(P, po.fin.mat);
+            po.color = shade_finish(P, shade_shadow_emit(P, col(bitsf(s0.x), bitsf(s0.y), bitsf(s1.x)), m, po.shadowed), m,
+                                    col(0, 0, 0));
+            return po;
+        }
         if (po.fin.t > 0.1f) {
             po.found = true;
-            Direct D = shade_direct<PLAIN>(P, cam, rd0, po.fin, lv, nshadow);
+            Direct D = shade_direct<PLAIN, G>(P, cam, rd0, po.fin, lv, nshadow);
             po.shadowed = D.shadowed;
             po.color = PLAIN || P.shading_method == RT_SHADING
                            ? shade_finish(P, D.fc, mat_of(P, po.fin.mat), col(0, 0, 0))
@@ -1689,6 +1727,7 @@ struct BlockQueue {
     int shard, empty;
     int base[4], sh[4];
     int heavy_done;   // the heavy list is exhausted (any wave may set it)
+    int split_done;   // the split tiles' parts are exhausted
 };
 __shared__ BlockQueue g_bq;
 
@@ -1699,6 +1738,7 @@ __device__ __forceinline__ void tile_queue_init()
         g_bq.shard = (int)(blockIdx.x & (TILE_SHARDS - 1));
         g_bq.empty = 0;
         g_bq.heavy_done = 0;
+        g_bq.split_done = 0;
     }
     __syncthreads();
 }
@@ -1706,7 +1746,8 @@ __device__ __forceinline__ void tile_queue_init()
 __device__ __forceinline__ int tile_queue_next_shards(const KParams& P);
 
 // The next tile: first the heavy list (one global ticket per tile), then the sharded queue with the
-// heavy tiles skipped (each tile exactly once).
+// heavy tiles skipped (each tile exactly once; the split tiles of heavy_prep_kernel are
+// trace_split_part's).
 __device__ __forceinline__ int tile_queue_next(const KParams& P)
 {
     const int lane = threadIdx.x & 63;
@@ -1807,21 +1848,25 @@ __device__ __forceinline__ void set_wave_prio(int level)
 // lane active; the f x f blocks (f = 1 << P.ds_shift, f | 8, rows f-aligned in the band)
 // are summed per 8-bit channel across lanes, divided by f * f with truncation (the sums
 // are non-negative: a shift) and written by the block's first lane, as downscale_kernel.
+// G > 1 (trace_split_part): pixel i of the wave's rows is held by lanes G i .. G i + G - 1
+// (8 / G rows of the tile; f <= 8 / G).
+template <int G = 1>
 __device__ __forceinline__ void downscale_tile(const KParams& P, int lane, int lr, int px, uint32_t c)
 {
     int r = (int)((c >> 16) & 0xffu), g = (int)((c >> 8) & 0xffu), b = (int)(c & 0xffu);
     const int f = 1 << P.ds_shift;
     for (int m = 1; m < f; m <<= 1) {   // columns, within the lane's row of 8
-        r += __shfl_xor(r, m);
-        g += __shfl_xor(g, m);
-        b += __shfl_xor(b, m);
+        r += __shfl_xor(r, G * m);
+        g += __shfl_xor(g, G * m);
+        b += __shfl_xor(b, G * m);
     }
     for (int m = 8; m < 8 * f; m <<= 1) {   // rows
-        r += __shfl_xor(r, m);
-        g += __shfl_xor(g, m);
-        b += __shfl_xor(b, m);
+        r += __shfl_xor(r, G * m);
+        g += __shfl_xor(g, G * m);
+        b += __shfl_xor(b, G * m);
     }
-    if ((lane & (f - 1)) == 0 && ((lane >> 3) & (f - 1)) == 0) {
+    const int pl = lane / G;   // the lane's pixel: 8 row + column
+    if ((lane & (G - 1)) == 0 && (pl & (f - 1)) == 0 && ((pl >> 3) & (f - 1)) == 0) {
         const int s2 = 2 * P.ds_shift;
         P.ds_out[(size_t)(lr >> P.ds_shift) * (size_t)(P.rw >> P.ds_shift) + (size_t)(px >> P.ds_shift)] =
             qrgb(r >> s2, g >> s2, b >> s2);
@@ -1854,6 +1899,52 @@ __device__ __forceinline__ v3 camera_dir(const KParams& P, int px, int py, v3 ca
     } else
         ws = xform_point(P.cam_to_world, vs);
     return normalize(ws - cam);
+}
+
+// The split tiles (KParams::heavy_group = G, heavy_prep_kernel's second list): a tile whose one wave
+// would outlast the launch's mean wave (grazing silhouette rays walk 100-170 wide nodes)
+// is traced as G parts of 8 / G rows, each part by one wave of ray_trace_kernel with G lanes per pixel
+// (a lane group: wbvh_closest<.., G> walks the pixel's tree on its G lanes together).  The parts are
+// taken first, by the ticket heavy_ctr[2] over the list's G * heavy_ctr[3] parts, so they run on
+// different waves at the same time; each adds its cycles to the tile's cost (heavy_prep_kernel zeroed
+// it).  Plain scenes over the wide BVH only, fused SSAA factors up to 8 / G (the host checks).  Per
+// pixel the results are trace_pixel<false, true>'s: the group's query returns the one-lane answer.
+template <int G>
+__device__ __forceinline__ void trace_split_part(const KParams& P, uint2* lv, int t, int lane, unsigned& nshadow)
+{
+    static_assert(G > 1 && G <= 8 && (G & (G - 1)) == 0, "2, 4 or 8 lanes per pixel");
+    const int cap = P.tiles_x * P.tiles_y / 16;   // (heavy_prep_kernel: the split list at list + cap)
+    const int tq = ldg(P.heavy_list + cap + t / G), part = t % G;
+    const int tile = tq & 0x0fffffff;
+    set_wave_prio(tq >> 28);
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    int tx, ty;
+    tile_xy(P, tile, tx, ty);
+    const int pl = lane / G;   // the lane's pixel among the part's 64 / G
+    const int px = tx * 8 + (pl & 7);
+    const int lr = ty * 8 + part * (8 / G) + (pl >> 3);
+    const int py = lr < P.local_rows ? global_row(P, lr) : P.rh;
+    if (px < P.rw && py < P.rh) {   // (the same for the G lanes of a pixel)
+        const v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+        const v3 rd = camera_dir(P, px, py, cam);
+        unsigned ns = 0, nr = 0;
+        PixelOut po = trace_pixel<false, true, G>(P, cam, rd, lv, 0u, ns, nr);
+        if ((lane & (G - 1)) == 0)
+            nshadow += ns;   // (one count per pixel)
+        const size_t o = (size_t)lr * P.rw + px;
+        const uint32_t c = color_to_argb(po.color);
+        if (P.ds_out) downscale_tile<G>(P, lane, lr, px, c);
+        if ((lane & (G - 1)) == 0) {
+            if (P.argb) P.argb[o] = c;
+            if (P.rgba) P.rgba[o] = make_float4(po.color.r, po.color.g, po.color.b, po.alpha);
+            if (P.hit_id) P.hit_id[o] = po.found ? po.src : -1;
+            if (P.hit_t) P.hit_t[o] = po.fin.t;
+            if (P.shadow) P.shadow[o] = (uint8_t)(po.found && po.shadowed);
+        }
+    }
+    const uint64_t c = __builtin_amdgcn_s_memtime() - t0;
+    if (lane == 0)
+        atomicAdd(P.tile_cost + tile, c > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)c);
 }
 
 // Renderer::ray_trace (renderer.cpp:1068-1116): one lane per pixel, one wave
@@ -1890,6 +1981,20 @@ __global__ __launch_bounds__(BLOCK, PLAIN ? RT_OCC_PLAIN : RT_OCC) void ray_trac
         asm volatile("" : "+s"(kpl));   // (the loop's loads depend on it: not hoisted)
         const KParams& P = *reinterpret_cast<const KParams*>((const void*)kpl);
         const v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+        if (PLAIN && !REFL && P.heavy_group == 4 &&
+            !__builtin_amdgcn_readfirstlane(__hip_atomic_load(&g_bq.split_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) {
+            // the split tiles' parts first (trace_split_part)
+            int t = 0;
+            if (lane == 0)
+                t = atomicAdd(P.heavy_ctr + 2, 1);
+            t = __builtin_amdgcn_readfirstlane(t);
+            if (t < 4 * ldg(P.heavy_ctr + 3)) {
+                trace_split_part<4>(P, lv, t, lane, nshadow);
+                continue;
+            }
+            if (lane == 0)
+                __hip_atomic_store(&g_bq.split_done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
         const int tq = tile_queue_next(P);
         if (PLAIN) PH_MARK(6);
         if (tq < 0)
@@ -3075,6 +3180,7 @@ __global__ __launch_bounds__(BLOCK) void trace_rays_kernel(KParams P, const floa
 // whole line (status 0 certified miss, 1 certified hit with the record, 2 not certified).
 // (The occupancy bound is the plain kernel's: wide_closest_deep is compiled once for all its callers,
 // within the loosest caller's register budget, and the plain kernel inherits what it uses.)
+template <int G>
 __global__ __launch_bounds__(BLOCK, RT_OCC_PLAIN) void wide_query_kernel(KParams P, const float* __restrict__ orig,
                                                            const float* __restrict__ dir, int n, int kind,
                                                            float* __restrict__ o_out, float* __restrict__ d_out,
@@ -3084,7 +3190,9 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_PLAIN) void wide_query_kernel(KParams
 {
     extern __shared__ uint2 lds_levels[];
     uint2* lv = lds_levels + threadIdx.x;
-    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    // G > 1: the G lanes of a lane group trace ray i together (wbvh_closest<.., G>)
+    const int i = (blockIdx.x * BLOCK + threadIdx.x) / G;
+    const bool writer = (threadIdx.x & (G - 1)) == 0;
     if (i >= n)
         return;
     v3 o = mk(orig[3 * i], orig[3 * i + 1], orig[3 * i + 2]);
@@ -3109,17 +3217,19 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_PLAIN) void wide_query_kernel(KParams
             rsub = wrisk_sub(W_QS_SHADOW, hi, P.risk_nu);
         }
         bool s;
-        if (P.wnodes && P.nnodes > 0 && P.seg_scale > 0.0f && !R0.nan && wide_shadow(P, o, d, hi, p, lp, lv, &s, light))
+        if (P.wnodes && P.nnodes > 0 && P.seg_scale > 0.0f && !R0.nan && wide_shadow<G>(P, o, d, hi, p, lp, lv, &s, light))
             sh = s ? 1 : 0;
     } else if (kind == 1 && P.wrisk && o.x == P.cam_pos[0] && o.y == P.cam_pos[1] && o.z == P.cam_pos[2]) {
         rk = P.wrisk;
     }
-    o_out[3 * i] = o.x;
-    o_out[3 * i + 1] = o.y;
-    o_out[3 * i + 2] = o.z;
-    d_out[3 * i] = d.x;
-    d_out[3 * i + 1] = d.y;
-    d_out[3 * i + 2] = d.z;
+    if (writer) {
+        o_out[3 * i] = o.x;
+        o_out[3 * i + 1] = o.y;
+        o_out[3 * i + 2] = o.z;
+        d_out[3 * i] = d.x;
+        d_out[3 * i + 1] = d.y;
+        d_out[3 * i + 2] = d.z;
+    }
     int st = W_UNCERT;
     int32_t id = -1;
     WHit w;
@@ -3130,7 +3240,7 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_PLAIN) void wide_query_kernel(KParams
         const float om = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
         const float m = 0x1p-16f * (om + P.scene_scale);
         WStackLds stk{lv};
-        st = wbvh_closest(P.wnodes, P.wtris, o, d, m, stk, w, nullptr, INFINITY, true, QS, rk, rsel, rsub);
+        st = wbvh_closest<WStackLds, G>(P.wnodes, P.wtris, o, d, m, stk, w, nullptr, INFINITY, true, QS, rk, rsel, rsub);
         if (st == W_DEEP)
             st = wide_closest_deep(P.wnodes, P.wtris, o, d, m, w, INFINITY, true, QS, rk, rsel, rsub);
         if (st == W_HIT) {
@@ -3143,6 +3253,8 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_PLAIN) void wide_query_kernel(KParams
         if (st == W_MISS)
             w.t = -1.0f;
     }
+    if (!writer)
+        return;
     status[i] = st;
     out_id[i] = id;
     out_t[i] = st == W_HIT ? w.t : -1.0f;
@@ -3283,10 +3395,8 @@ __global__ __launch_bounds__(256) void wide_gather_kernel(const GTri* __restrict
 // (the same memory; a lane uses one at a time)
 size_t lds_bytes(const KParams& P)
 {
-    int entries = P.levels > 0 ? P.levels : 1;
-    if (P.wnodes && entries < W_STACK)
-        entries = W_STACK;
-    return (size_t)entries * BLOCK * sizeof(uint2);
+    // the traversal stacks, then the plain pixel's values held across its shadow query (trace_pixel)
+    return (size_t)(lds_save_slot(P) + LDS_SAVE_ENTRIES) * BLOCK * sizeof(uint2);
 }
 
 }  // namespace rt
@@ -3312,8 +3422,17 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_wide_query
     if (n <= 0)
         return hipSuccess;
     size_t lds = rt::lds_bytes(*P);
-    hipLaunchKernelGGL(rt::wide_query_kernel, dim3((n + rt::BLOCK - 1) / rt::BLOCK), dim3(rt::BLOCK), lds, stream, *P,
-                       o, d, n, kind, o_out, d_out, status, id, t, u, v, sh);
+    // RT_WIDE_QUERY_GROUP=2 / 4 / 8 (tests, tools): each ray traced by a lane group (wbvh_closest<.., G>)
+    const char* gv = getenv("RT_WIDE_QUERY_GROUP");
+    const int G = gv && (atoi(gv) == 2 || atoi(gv) == 4 || atoi(gv) == 8) ? atoi(gv) : 1;
+    const dim3 grid((unsigned)(((int64_t)n * G + rt::BLOCK - 1) / rt::BLOCK));
+#define RT_WQ(g) hipLaunchKernelGGL(rt::wide_query_kernel<g>, grid, dim3(rt::BLOCK), lds, stream, *P, o, d, n, kind, \
+                                    o_out, d_out, status, id, t, u, v, sh)
+    if (G == 1) RT_WQ(1);
+    else if (G == 2) RT_WQ(2);
+    else if (G == 4) RT_WQ(4);
+    else RT_WQ(8);
+#undef RT_WQ
     return hipGetLastError();
 }
 
@@ -3337,21 +3456,26 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_trace_colo
 }
 
 // The heavy list of a launch (KParams::heavy_list) from the previous launch's tile costs of the same
-// layout: the tiles costing at least max(4 x the mean, the largest / 8), at most ntiles / 16 of them,
-// in tile order.  One block; it also clears the bits and resets the ticket.
+// layout: the tiles costing at least max(4 x the mean, the largest / 8), at most ntiles / 16 of them.
+// With group G > 1, those that also cost at least split x the launch's mean cycles per wave (the sum
+// over nwaves, the plain kernel's waves: a tile that would outlast the mean wave) go to the split list
+// list[cap .. cap + ctr[3]) of trace_split_part (cap = ntiles / 16), the others to list[0 ..
+// ctr[0]) of ray_trace_kernel.  One block; it also clears the bits and resets the tickets.
 #ifndef RT_HEAVY_PRIO
 #define RT_HEAVY_PRIO 1   // heavy tiles at raised wave priority (set_wave_prio)
 #endif
-__global__ __launch_bounds__(1024) void heavy_prep_kernel(const uint32_t* __restrict__ cost, int ntiles, int32_t* list,
-                                                          uint32_t* bits, int32_t* ctr)
+__global__ __launch_bounds__(1024) void heavy_prep_kernel(uint32_t* __restrict__ cost, int ntiles, int32_t* list,
+                                                          uint32_t* bits, int32_t* ctr, int nwaves, float split,
+                                                          int group)
 {
     __shared__ unsigned long long sum;
     __shared__ unsigned int mx;
-    __shared__ int cnt;
+    __shared__ int cnt, cnt2;
     if (threadIdx.x == 0) {
         sum = 0;
         mx = 0;
         cnt = 0;
+        cnt2 = 0;
     }
     __syncthreads();
     unsigned long long s = 0;
@@ -3367,34 +3491,53 @@ __global__ __launch_bounds__(1024) void heavy_prep_kernel(const uint32_t* __rest
     __syncthreads();
     const unsigned long long mean = ntiles > 0 ? sum / (unsigned long long)ntiles : 0;
     const unsigned long long thr = max(4 * mean, (unsigned long long)(mx / 8));
+    // split: at least split x the mean cycles per wave (never, without a group)
+    const unsigned long long thr2 = group > 1 && nwaves > 0 ? max(thr, (unsigned long long)((double)split * (double)sum / nwaves))
+                                                            : ~0ull;
     const int cap = ntiles / 16;
     if (mx > 0)
         for (int i = threadIdx.x; i < ntiles; i += 1024)
             if (cost[i] >= thr && cost[i] > 0) {
-                const int k = atomicAdd(&cnt, 1);
+                const bool two = cost[i] >= thr2;
+                const int k = atomicAdd(two ? &cnt2 : &cnt, 1);
                 if (k < cap) {
                     // the wave's issue priority while it traces the tile (bits 28-29, ray_trace_kernel)
                     const int prio = !RT_HEAVY_PRIO || ntiles >= (1 << 28) ? 0
                                      : cost[i] >= mx / 2               ? 3
                                      : cost[i] >= mx / 4               ? 2
                                                                        : 1;
-                    list[k] = i | (prio << 28);
+                    list[two ? cap + k : k] = i | (prio << 28);
                     atomicOr(bits + (i >> 5), 1u << (i & 31));
+                    if (two)
+                        cost[i] = 0u;   // (the parts add theirs; ray_trace_kernel stores a tile's own)
                 }
             }
     __syncthreads();
     if (threadIdx.x == 0) {
         ctr[0] = min(cnt, cap);
         ctr[1] = 0;
+        ctr[2] = 0;
+        ctr[3] = min(cnt2, cap);
     }
 }
 
 // ---- host-side launch wrappers (called from renderer.cpp) ----
-extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_heavy_prep(const uint32_t* cost, int ntiles,
-                                                                                 int32_t* list, uint32_t* bits,
-                                                                                 int32_t* ctr, hipStream_t stream)
+// the plain kernel's grid (rt_launch_ray_trace): exactly its residency
+static int plain_blocks(const rt::KParams& P)
 {
-    hipLaunchKernelGGL(heavy_prep_kernel, dim3(1), dim3(1024), 0, stream, cost, ntiles, list, bits, ctr);
+    const int tiles = P.tiles_x * P.tiles_y;
+    const int blocks = (tiles + rt::WAVES_PER_BLOCK - 1) / rt::WAVES_PER_BLOCK;
+    return P.max_blocks > 0 ? std::max(1, std::min(blocks, P.max_blocks / 8 * RT_OCC_PLAIN)) : blocks;
+}
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_heavy_prep(const rt::KParams* P, uint32_t* cost,
+                                                                                 int ntiles, int32_t* list,
+                                                                                 uint32_t* bits, int32_t* ctr,
+                                                                                 float split, int group,
+                                                                                 hipStream_t stream)
+{
+    hipLaunchKernelGGL(heavy_prep_kernel, dim3(1), dim3(1024), 0, stream, cost, ntiles, list, bits, ctr,
+                       plain_blocks(*P) * rt::WAVES_PER_BLOCK, split, group);
     return hipGetLastError();
 }
 
@@ -3408,13 +3551,14 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(
     if (blocks < 1)
         return hipSuccess;
     size_t lds = rt::lds_bytes(*P);
+    const bool plain = !P->has_reflection && P->plain && !P->zbuf && !P->nbuf;
     if (P->has_reflection)
         hipLaunchKernelGGL((rt::ray_trace_kernel<true, false>), dim3(blocks), dim3(rt::BLOCK), lds, stream, *P);
-    else if (P->plain && !P->zbuf && !P->nbuf) {
+    else if (plain) {
         // the plain kernel's grid is exactly its residency (RT_OCC_PLAIN blocks of 4 waves per
         // CU): with two frames in flight, surplus blocks of one frame would be dispatched ahead
         // of the next frame's only to find the queue empty (C4 +1.3%: r02_bench98_*.log)
-        const int pblocks = P->max_blocks > 0 ? std::max(1, std::min(blocks, P->max_blocks / 8 * RT_OCC_PLAIN)) : blocks;
+        const int pblocks = plain_blocks(*P);
         hipLaunchKernelGGL((rt::ray_trace_kernel<false, true>), dim3(pblocks), dim3(rt::BLOCK), lds, stream, *P);
     } else
         hipLaunchKernelGGL((rt::ray_trace_kernel<false, false>), dim3(blocks), dim3(rt::BLOCK), lds, stream, *P);

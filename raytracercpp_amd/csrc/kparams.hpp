@@ -114,6 +114,10 @@ struct KParams {
     const int32_t* heavy_list;
     const uint32_t* heavy_bits;
     int32_t* heavy_ctr;
+    // 0: ray_trace_kernel dequeues the heavy list; G > 1: ray_trace_heavy_kernel<G> traces the listed
+    // tiles before it (each tile as G parts of 8 / G rows, G lanes per pixel, by the ticket heavy_ctr[2];
+    // the parts add their cycles to tile_cost) and ray_trace_kernel skips them
+    int32_t heavy_group;
 
     // outputs, indexed by local_row * rw + px (nullptr = not requested)
     uint32_t* argb;

@@ -15,9 +15,12 @@
 #include "host_scene.hpp"
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(const rt::KParams* P, hipStream_t stream);
-extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_heavy_prep(const uint32_t* cost, int ntiles,
-                                                                                 int32_t* list, uint32_t* bits,
-                                                                                 int32_t* ctr, hipStream_t stream);
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_heavy_prep(const rt::KParams* P, uint32_t* cost,
+                                                                                 int ntiles, int32_t* list,
+                                                                                 uint32_t* bits, int32_t* ctr,
+                                                                                 float split, int group,
+                                                                                 hipStream_t stream);
+
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_level0(const rt::KParams* P, rt::FrameRec* fr1,
                                                                            unsigned int* nfr1, hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_stage(int stage, const rt::KParams* P,
@@ -102,6 +105,7 @@ Knobs Knobs::from_env()
     k.cones = on("RT_CONES", true);
     k.lslab = on("RT_LSLAB", true);
     k.plain = on("RT_PLAIN", true);
+    k.plain_octree = on("RT_PLAIN_OCTREE", true);
     k.fused_ssaa = on("RT_FUSED_SSAA", true);
     k.refl_engine = on("RT_REFL_ENGINE", true);
     k.refl_sort = on("RT_REFL_SORT", true);
@@ -110,6 +114,12 @@ Knobs Knobs::from_env()
     k.exact = on("RT_EXACT", false);
     k.risk = on("RT_WBVH_RISK", true);
     k.heavy = on("RT_HEAVY_FIRST", true);
+    if (const char* v = getenv("RT_HEAVY_GROUP")) {
+        const int g = atoi(v);
+        k.heavy_group = g == 4 ? g : 0;
+    }
+    if (const char* v = getenv("RT_HEAVY_SPLIT"))
+        k.heavy_split = std::max(0.0f, (float)atof(v));
     if (const char* v = getenv("RT_REFL_DEFER"))   // loop iterations before a reflection query is deferred
         k.refl_defer = std::max(0, atoi(v));
     {
@@ -1042,7 +1052,7 @@ void Renderer::fill_params(KParams& P) const
     }
     P.max_blocks = num_cus_ * 8;   // persistent grids: 8 blocks per CU (the plain kernel: its residency)
     // the plain specialisation (RT_PLAIN=0 turns it off); SSAO (zbuf) is checked at launch
-    P.plain = knobs_.plain && P.enable_bvh && P.wnodes && P.shading_method == RT_SHADING && P.nshape == 0 &&
+    P.plain = knobs_.plain && P.enable_bvh && (P.wnodes || knobs_.plain_octree) && P.shading_method == RT_SHADING && P.nshape == 0 &&
               !P.enable_ao_mapping && !P.enable_diffuse_mapping && !P.enable_normal_mapping &&
               !P.enable_displacement_mapping && !P.enable_skysphere && !P.enable_skybox && !P.has_reflection;
     render_size(P.rw, P.rh);
@@ -1842,6 +1852,7 @@ int Renderer::prepare_heavy(KParams& P, TileCost& T, hipStream_t stream)
     P.heavy_list = nullptr;
     P.heavy_bits = nullptr;
     P.heavy_ctr = nullptr;
+    P.heavy_group = 0;
     if (!knobs_.heavy || P.has_reflection || s_.hybrid_rasterization_tracing)
         return RT_OK;
     const int ntiles = P.tiles_x * P.tiles_y;
@@ -1866,12 +1877,19 @@ int Renderer::prepare_heavy(KParams& P, TileCost& T, hipStream_t stream)
     int32_t* list = T.heavy.as<int32_t>();
     uint32_t* bits = reinterpret_cast<uint32_t*>(list + ntiles);
     int32_t* ctr = reinterpret_cast<int32_t*>(bits + nb);
-    if ((e = rt_launch_heavy_prep(T.cost.as<uint32_t>(), ntiles, list, bits, ctr, stream)) != hipSuccess)
+    // tiles are split (kernels.hip trace_split_part) only by the plain kernel over the wide BVH, with a
+    // fused SSAA block within a part's 8 / G rows
+    const int G = knobs_.heavy_group;
+    const bool split = G > 1 && !P.has_reflection && P.plain && !P.zbuf && !P.nbuf && P.wnodes && P.nnodes > 0 &&
+                       (!P.ds_out || (8 >> P.ds_shift) >= G);
+    if ((e = rt_launch_heavy_prep(&P, T.cost.as<uint32_t>(), ntiles, list, bits, ctr, knobs_.heavy_split, split ? G : 0,
+                                  stream)) != hipSuccess)
         return hip_fail(e, "heavy_prep_kernel");
     P.tile_cost = T.cost.as<uint32_t>();
     P.heavy_list = list;
     P.heavy_bits = bits;
     P.heavy_ctr = ctr;
+    P.heavy_group = split ? G : 0;
     return RT_OK;
 }
 

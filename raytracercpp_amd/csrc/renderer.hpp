@@ -46,6 +46,8 @@ struct Knobs {
     bool cones = true;        // RT_CONES=0: no leaf normal cones (5.3; also turns the leaf slabs off)
     bool lslab = true;        // RT_LSLAB=0: no leaf slabs (5.4)
     bool plain = true;        // RT_PLAIN=0: no plain specialisation of ray_trace_kernel (5.6)
+    bool plain_octree = true; // RT_PLAIN_OCTREE=0: frames on the octree path (before the wide BVH is resident,
+                              // exact mode) take the general kernel, not the plain one (5.8)
     bool fused_ssaa = true;   // RT_FUSED_SSAA=0: band launches downscale in a separate pass (7)
     bool refl_engine = true;  // RT_REFL_ENGINE=0: the one-lane-per-pixel recursive kernel (9)
     bool refl_sort = true;    // RT_REFL_SORT=0: reflection frames in spawn order, not Morton order
@@ -55,6 +57,10 @@ struct Knobs {
     bool exact = false;       // RT_EXACT=1 / rt_set_exact: wbvh and seg off
     bool risk = true;         // RT_WBVH_RISK=0: no per-frame grazing-risk bits (every child runs case (b), 5.6)
     bool heavy = true;        // RT_HEAVY_FIRST=0: tiles in queue order only (no heavy-first list, 5.6)
+    int heavy_group = 0;      // RT_HEAVY_GROUP=4: the split tiles traced as 4 parts with 4 lanes per pixel
+                              // (kernels.hip trace_split_part); 0: none split
+    float heavy_split = 0.5f; // RT_HEAVY_SPLIT=c: split the heavy tiles costing >= c x the launch's mean
+                              // cycles per wave (heavy_prep_kernel)
     int refl_defer = 48;      // RT_REFL_DEFER=k: reflection queries past k loop iterations finish in a pass
                               // of their own (9; 0: never)
     int inject_fail = 0;      // RT_INJECT_FRAME_FAIL=k (tests): the k-th ray_trace fails after its image start

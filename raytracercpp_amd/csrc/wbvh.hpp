@@ -676,6 +676,80 @@ struct WStackArr {
 };
 using WStackLocal = WStackArr<W_STACK>;   // host
 
+// A lane group: G adjacent lanes of a wave (lanes g0 .. g0 + G - 1, g0 a multiple of G) trace one ray
+// together (wbvh_closest<Stack, G>, kernels.hip ray_trace_heavy_kernel).  Device only; on the host
+// (G = 1) these are the identity.
+template <int G>
+RT_HD uint32_t wg_lane()
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __lane_id() & (uint32_t)(G - 1);
+#else
+    return 0u;
+#endif
+}
+// the group's lanes where p holds (bit i: group lane i)
+template <int G>
+RT_HD uint32_t wg_bits(bool p)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (uint32_t)(__ballot(p) >> (__lane_id() & ~(uint32_t)(G - 1))) & ((1u << G) - 1u);
+#else
+    return p ? 1u : 0u;
+#endif
+}
+#if defined(__HIP_DEVICE_COMPILE__)
+// a 32-bit value from the lane the DPP quad permutation names (within each group of 4 lanes; all active)
+template <int PERM>
+__device__ __forceinline__ uint32_t wg_quad(uint32_t x)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, PERM, 0xF, 0xF, false);
+}
+#endif
+template <int G>
+RT_HD float wg_min(float x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (G <= 4) {   // DPP quad permutations (lane ^ 1, lane ^ 2), no LDS round trip
+        x = fminf(x, __uint_as_float(wg_quad<0xB1>(__float_as_uint(x))));
+        if (G == 4)
+            x = fminf(x, __uint_as_float(wg_quad<0x4E>(__float_as_uint(x))));
+    } else {
+        for (int m = 1; m < G; m <<= 1)
+            x = fminf(x, __shfl_xor(x, m));
+    }
+#endif
+    return x;
+}
+// x of group lane i (i may differ per lane)
+template <int G, class T>
+RT_HD T wg_read(T x, int i)
+{
+    static_assert(sizeof(T) == 4, "32-bit values");
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (G <= 4) {   // the group's G values by DPP quad broadcasts, then a select
+        uint32_t u;
+        __builtin_memcpy(&u, &x, 4);
+        uint32_t r;
+        if (G == 4) {   // quad lane 0 / 1 / 2 / 3 to every lane of the quad
+            const uint32_t b0 = wg_quad<0x00>(u), b1 = wg_quad<0x55>(u), b2 = wg_quad<0xAA>(u), b3 = wg_quad<0xFF>(u);
+            r = i == 0 ? b0 : i == 1 ? b1 : i == 2 ? b2 : b3;
+        } else {        // pairs: (0, 0, 2, 2) and (1, 1, 3, 3)
+            const uint32_t b0 = wg_quad<0xA0>(u), b1 = wg_quad<0xF5>(u);
+            r = i == 0 ? b0 : b1;
+        }
+        T y;
+        __builtin_memcpy(&y, &r, 4);
+        return y;
+    } else {
+        return __shfl(x, (int)(__lane_id() & ~(uint32_t)(G - 1)) + i);
+    }
+#else
+    (void)i;
+    return x;
+#endif
+}
+
 // Closest hit over the wide BVH for the ray (o, d) among hits with t <= hi.  m: box margin
 // (2^-16 (max|o| + scene scale), the leaf-slab margin of kernels.hip leaf_missed).
 // Returns W_MISS (no triangle reports a hit at t <= hi), W_HIT (h = the minimum-t hit, finite
@@ -707,11 +781,26 @@ using WStackLocal = WStackArr<W_STACK>;   // host
 // skipped for it when that exceeds the best hit.  rsub: 0 for the camera (rsel 0); for the light (rsel 1), at least
 // QS h + nu with h >= |light - o| and nu the frame's (WRiskArgs::ray_nu; wrisk_sub).  The caller
 // guarantees the ray is of that kind.
-template <class Stack>
+//
+// G > 1 (device, Stack = kernels.hip WStackLds, max_steps 0): the G lanes of a lane group (wg_lane)
+// hold the same ray and walk its tree together.  Group lane 0 starts at the root, the others idle; after
+// every step the group shares its best hit bound (best_s, the minimum over the group), and each idle lane
+// takes the bottom entry of a busy lane's stack (the stack is then a ring [bot, sp): pushes and pops at
+// sp, steals at bot; the i-th idle lane in lane order takes from the i-th lane with entries).  Every
+// child pushed is visited by one lane or skipped because its key exceeds the group's best (never below
+// the final best: skipped soundly), so the group's lanes together test every triangle the G = 1 query
+// would need; the answer (minimum over the lanes' records, a tie when two lanes hold it or one lane saw
+// two) is the same on every lane of the group.
+template <class Stack, int G = 1>
 RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m, Stack& stk, WHit& h,
                        uint32_t* work = nullptr, float hi = INFINITY, bool ties = true, float QS = 0x1p-8f,
                        const uint64_t* risk = nullptr, int rsel = 0, float rsub = 0.0f, uint32_t max_steps = 0)
 {
+    static_assert(G == 1 || ((G & (G - 1)) == 0 && G <= 8 && (Stack::CAP & (Stack::CAP - 1)) == 0),
+                  "a lane group: a power of two up to 8 lanes, a ring stack of 2^k entries");
+    static_assert(G == 1 || !W_STEP_CAP, "a lane group leaves the loop together");
+    // the stack index of entry i (a ring in a lane group)
+    auto slot = [](int i) { return G > 1 ? (i & (Stack::CAP - 1)) : i; };
     h.t = INFINITY;
     h.u = 1.0f;
     h.v = 0.0f;
@@ -741,11 +830,11 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
     float best_s = hi + fabsf(hi) * SL;   // h.t (or hi) plus slack: a child entered at or below it may hold a hit
     bool tie = false, nanhit = false, infhit = false;
     float dropped = INFINITY;   // the smallest key of the children a full stack could not take
-    int sp = 0;
-    uint32_t cur = 0;   // root node
+    int sp = 0, bot = 0;        // the stack's entries [bot, sp) (bot > 0: entries taken by the group)
+    uint32_t cur = G > 1 && wg_lane<G>() != 0 ? W_EMPTY : 0u;   // root node
     uint32_t nn = 0, nt = 0;
     uint32_t steps = 0;   // loop iterations (node or leaf visits)
-    while (cur != W_EMPTY) {
+    while (G > 1 ? wg_bits<G>(cur != W_EMPTY) != 0u : cur != W_EMPTY) {
         ++steps;
         if (max_steps && steps > max_steps)
             return W_LONG;
@@ -1033,8 +1122,8 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
 #pragma unroll
                 for (int j = W_WIDTH - 1; j >= 1; j--)
                     if (key[j] < INFINITY) {
-                        if (sp < Stack::CAP)
-                            stk.put(sp++, make_uint2(ref[j], fbits(key[j])));
+                        if (sp - bot < Stack::CAP)
+                            stk.put(slot(sp++), make_uint2(ref[j], fbits(key[j])));
                         else {
                             // full: the entry with the largest key goes (the new child or one on the
                             // stack, which it replaces); the query stays certified if the dropped key
@@ -1055,8 +1144,8 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                     }
             } else {
                 cur = W_EMPTY;
-                while (sp > 0) {
-                    uint2 e = stk.get(--sp);
+                while (sp > bot) {
+                    uint2 e = stk.get(slot(--sp));
                     if (bitsf(e.y) <= best_s) {
                         cur = e.x;
                         break;
@@ -1064,7 +1153,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                 }
             }
         }
-        else {
+        else if (G == 1 || cur != W_EMPTY) {   // (an idle lane of a group: no step)
         // ---- a leaf: its triangles, closest hit kept; equal t from another triangle is a tie ----
         W_STEP_HOOK(cur, 1);
         const uint32_t first = (cur >> 3) & 0x0FFFFFFFu, cnt = (cur & 7u) + 1u;
@@ -1094,14 +1183,54 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
         for (uint32_t k = first; k < kend; k++)
             fold(load_gtri(tris + k), k);
         cur = W_EMPTY;
-        while (sp > 0) {
-            uint2 e = stk.get(--sp);
+        while (sp > bot) {
+            uint2 e = stk.get(slot(--sp));
             if (bitsf(e.y) <= best_s) {
                 cur = e.x;
                 break;
             }
         }
         }
+        if constexpr (G > 1) {
+            // the group's best bound, then the idle lanes take work: the i-th idle lane the bottom
+            // (oldest: the largest subtree) entry of the i-th lane holding entries
+            best_s = wg_min<G>(best_s);
+            const uint32_t idle = wg_bits<G>(cur == W_EMPTY), busy = wg_bits<G>(sp > bot);
+            if (idle && busy) {
+                const uint32_t gl = wg_lane<G>(), below = (1u << gl) - 1u;
+                int src = -1;
+                if (cur == W_EMPTY) {
+                    uint32_t b = busy;
+                    for (int r = __builtin_popcount(idle & below); r > 0 && b; r--)
+                        b &= b - 1u;
+                    src = b ? __builtin_ctz(b) : -1;
+                }
+                const int sbot = wg_read<G>(bot, src >= 0 ? src : (int)gl);
+                if (sp > bot && __builtin_popcount(busy & below) < __builtin_popcount(idle))
+                    bot++;   // (the taker reads the entry below before any later push can reuse its slot)
+                if (src >= 0) {
+                    const uint2 e = stk.get_lane(src - (int)gl, slot(sbot));
+                    if (bitsf(e.y) <= best_s)
+                        cur = e.x;
+                }
+            }
+        }
+    }
+    if constexpr (G > 1) {
+        // the group's answer: the least t over its lanes' records; a tie when two lanes hold it (each
+        // triangle is tested by one lane at most) or the lane holding it saw two
+        const float T = wg_min<G>(h.t);
+        const uint32_t at = wg_bits<G>(h.k >= 0 && h.t == T);
+        const int w = at ? __builtin_ctz(at) : 0;
+        tie = __builtin_popcount(at) > 1 || wg_bits<G>(h.k >= 0 && h.t == T && tie) != 0u;
+        h.t = wg_read<G>(h.t, w);
+        h.u = wg_read<G>(h.u, w);
+        h.v = wg_read<G>(h.v, w);
+        h.k = wg_read<G>(h.k, w);
+        nanhit = wg_bits<G>(nanhit) != 0u;
+        infhit = wg_bits<G>(infhit) != 0u;
+        dropped = wg_min<G>(dropped);
+        best_s = wg_min<G>(best_s);
     }
     // a dropped child matters only if it could hold a hit at t <= the final best (a pop would have
     // skipped it otherwise)

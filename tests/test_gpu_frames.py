@@ -69,22 +69,27 @@ def test_risk_words_after_the_band_stream_is_destroyed(make_renderer):
         assert np.array_equal(assemble(parts, st.image_height, band), full), rep
 
 
-def _heavy_tiles(cost):
+def _heavy_tiles(cost, nwaves=None, split=0.5):
     """heavy_prep_kernel's rule (kernels.hip): tiles costing >= max(4 x mean, max / 8), at most
-    ntiles / 16 of them."""
+    ntiles / 16 of them; with nwaves (the plain kernel's waves), the number of those split into parts
+    (cost >= split x the sum / nwaves)."""
     c = cost.ravel().astype(np.uint64)
     thr = max(4 * int(c.sum() // c.size), int(c.max()) // 8)
-    return min(int(((c >= thr) & (c > 0)).sum()), c.size // 16)
+    heavy = (c >= thr) & (c > 0)
+    if nwaves is None:
+        return min(int(heavy.sum()), c.size // 16)
+    return min(int((heavy & (c >= max(thr, int(split * float(c.sum()) / nwaves)))).sum()), c.size // 16)
 
 
-@pytest.mark.parametrize("ssaa", [False, True])
-def test_heavy_first_frames_trace_every_tile_once(make_renderer, ssaa):
-    """Heavy tiles first (Renderer::prepare_heavy): each frame dequeues the previous frame's costliest
-    tiles first.  The light moves between frames, so a tile that was skipped would keep the previous
-    frame's pixels and one traced twice would show no difference only if both traces agree: every
-    frame must equal the oracle's for its own light, and the heavy list must not be empty."""
+@pytest.mark.parametrize("ssaa,group", [(False, 4), (True, 4), (False, 2), (False, 8), (True, 0)])
+def test_heavy_first_frames_trace_every_tile_once(make_renderer, ssaa, group):
+    """Heavy tiles first (Renderer::prepare_heavy): each frame takes the previous frame's costliest
+    tiles first, by ray_trace_heavy_kernel with 'group' lanes per pixel (RT_HEAVY_GROUP; 0: dequeued by
+    ray_trace_kernel itself).  The light moves between frames, so a tile that was skipped would keep the
+    previous frame's pixels and one traced twice would show no difference only if both traces agree:
+    every frame must equal the oracle's for its own light, and the heavy list must not be empty."""
     from raytracercpp_amd import scenes
-    R = make_renderer()
+    R = make_renderer(RT_HEAVY_GROUP=group)
     sc, st = scenes.bumpy70k(width=160, height=96, enable_ssaa=ssaa, ssaa_factor=2)
     R.load_scene(sc, st)
     R.ray_trace()
@@ -94,7 +99,9 @@ def test_heavy_first_frames_trace_every_tile_once(make_renderer, ssaa):
     heavy = []
     for L in lights:
         R.set_light_position(L)
-        heavy.append(_heavy_tiles(R.tile_costs()))
+        c = R.tile_costs()
+        # (the plain kernel's grid at this size: one wave per tile)
+        heavy.append((_heavy_tiles(c), _heavy_tiles(c, nwaves=c.size) if group > 1 else 0))
         R.ray_trace()
         g = R.get_internal(argb=True, hit=True, shadow=True)
         sc.light = np.asarray(L, np.float32)
@@ -106,8 +113,54 @@ def test_heavy_first_frames_trace_every_tile_once(make_renderer, ssaa):
         rw, rh = st.render_size()
         exp = Oracle.downscale(o.argb, rw, rh, 2) if ssaa else o.argb
         assert np.array_equal(R.get_image().ravel(), exp), L
-    print("heavy tiles per frame:", heavy)
-    assert min(heavy) > 0
+        assert R.stats()["shadow_rays"] == o.counters["shadow_rays"], L   # each pixel's shadow ray counted once
+    print("heavy tiles (all, split) per frame:", heavy)
+    assert min(h[0] for h in heavy) > 0
+    if group > 1:
+        assert min(h[1] for h in heavy) > 0   # tiles were split into parts
+
+
+@pytest.mark.parametrize("group", [4, 2])
+def test_c4_heavy_parts_match_oracle(make_renderer, group):
+    """The benchmark workload (C4) with its heavy tiles traced by ray_trace_heavy_kernel (G lanes per
+    pixel walking one pixel's wide-BVH query together, wbvh_closest<.., G>): the octree frame, then two
+    wide-BVH frames (heavy lists from the octree frame's and the wide frame's tile costs), every internal
+    pixel bit for bit; then the band path with the SSAA box filter fused into both kernels' tiles."""
+    import torch
+    from raytracercpp_amd import scenes
+    from raytracercpp_amd.strips import assemble
+    R = make_renderer(RT_HEAVY_GROUP=group)
+    sc, st = scenes.sphere1m()
+    o = Oracle(sc, st).render_rows()
+    R.load_scene(sc, st)
+    R.request_aux(hit=True, shadow=True)
+    rw, rh = st.render_size()
+    exp = Oracle.downscale(o.argb, rw, rh, 2)
+    heavy = []
+    for frame in range(3):
+        if frame:
+            heavy.append(_heavy_tiles(R.tile_costs()))
+        R.ray_trace()
+        g = R.get_internal(argb=True, hit=True, shadow=True)
+        assert np.array_equal(g["hit_id"], o.hit_id), f"frame {frame}: {int((g['hit_id'] != o.hit_id).sum())} hit-ID mismatches"
+        assert np.array_equal(g["hit_t"].view(np.uint32), o.hit_t.view(np.uint32)), frame
+        assert np.array_equal(g["shadow"], o.shadow), frame
+        assert np.array_equal(g["argb"], o.argb), frame
+        assert R.stats()["shadow_rays"] == o.counters["shadow_rays"], frame
+        if frame == 0:
+            R.finish_accel()
+    assert min(heavy) > 0, heavy
+    band, nranks = 8, 2   # output rows per band (16 internal rows)
+    for rep in range(3):   # the first launch per slot has no tile costs yet: no heavy list
+        parts = []
+        for rank in range(nranks):
+            b = torch.zeros((R.local_rows(band, rank, nranks), st.image_width), dtype=torch.int32, device="cuda:0")
+            torch.cuda.synchronize()
+            R.render_bands_device(band, rank, nranks, b.data_ptr(), 0)
+            torch.cuda.synchronize()
+            parts.append(b.cpu().numpy().view(np.uint32))
+        assert np.array_equal(assemble(parts, st.image_height, band).ravel(), exp), rep
+    print(f"C4 heavy tiles per frame (G = {group}):", heavy)
 
 
 @pytest.mark.parametrize("camera", ["default", "grazing"])

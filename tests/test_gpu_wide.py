@@ -288,3 +288,40 @@ def test_camera_plane_frames_match_oracle(R, h):
     assert np.array_equal(g["shadow"], o.shadow)
     assert np.array_equal(g["argb"], o.argb)
     assert float(np.abs(g["rgba"] - o.rgba).max()) <= 1e-4
+
+
+def _group_case(name):
+    """(tri, o, d, kind, cam, light) of one grazing case above."""
+    if name == "plane":
+        tri, o, d = tw.grazing_plane_case(seed=99, sin_lo=1e-7, sin_hi=1e-3)
+        return tri, o, d, 0, None, None
+    if name == "sphere":
+        tri, o, d = tw.grazing_sphere_case()
+        return tri, o, d, 0, None, None
+    if name == "camera_plane":
+        tri, o, d, cam = tw._plane_frame(23, 1e-7)
+        return tri, o, d, 1, cam, cam + np.float32(7.0)
+    if name == "light_plane":
+        tri, p, nrm, L = _light_plane(0.0)
+        return tri, p, nrm, 2, np.array([0.0, 30.0, 0.0], np.float32), L
+    raise KeyError(name)
+
+
+@pytest.mark.parametrize("G", [2, 4, 8])
+@pytest.mark.parametrize("name", ["plane", "sphere", "camera_plane", "light_plane"])
+def test_device_lane_groups_match_one_lane(R, monkeypatch, name, G):
+    """wbvh_closest<.., G> (G lanes walking one ray's tree together: work taken from each other's stacks,
+    the best hit shared, kernels.hip ray_trace_heavy_kernel) returns the one-lane query's answers bit for
+    bit -- status, triangle, t, u, v and the shadow decision -- on the grazing cases above, and 0 of its
+    certified answers differ from the oracle."""
+    tri, o, d, kind, cam, light = _group_case(name)
+    monkeypatch.delenv("RT_WIDE_QUERY_GROUP", raising=False)
+    cert1, bad1, g1 = _device_differences(R, tri, o, d, kind, cam=cam, light=light)
+    monkeypatch.setenv("RT_WIDE_QUERY_GROUP", str(G))
+    certG, badG, gG = _device_differences(R, tri, o, d, kind, cam=cam, light=light)
+    for k in ("status", "id", "shadowed"):
+        assert np.array_equal(gG[k], g1[k]), (k, int((gG[k] != g1[k]).sum()))
+    for k in ("t", "u", "v"):
+        assert np.array_equal(bits(gG[k]), bits(g1[k])), k
+    print(f"{name}, {G} lanes per ray: {certG:.4f} certified, {badG} differ (one lane: {cert1:.4f}, {bad1})")
+    assert badG == 0
