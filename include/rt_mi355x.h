@@ -130,10 +130,11 @@ int rt_set_settings(rt_renderer *r, const rt_settings *s);
 
 /* Exact mode (no reference counterpart).  on != 0: every BVH query walks
  * the octree over the whole ray line as BVH::intersect does (bvh.h:212-287), so every
- * result is the reference's by construction, rays grazing a triangle within rounding
- * included.  Off (default): closest hits come from the certified wide BVH, exact except
- * for rays whose line is nearly coplanar with a triangle's plane (DESIGN.md 5.6 bounds
- * that set).  Also RT_EXACT=1 at rt_create. */
+ * result is the reference's by construction.  Off (default): closest hits come from the
+ * wide BVH, whose child test is sound for every ray (grazing rays included, r04-r05), and
+ * each answer is certified on the reference's own octree leaf; the few queries it cannot
+ * certify (ties, NaN hits, overflowed stacks) walk the octree in place.  Both give the
+ * same images; exact mode is slower.  Also RT_EXACT=1 at rt_create. */
 int rt_set_exact(rt_renderer *r, int on);
 
 /* Acceleration structures beside the octree (no reference counterpart): after a

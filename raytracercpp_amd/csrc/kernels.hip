@@ -915,12 +915,20 @@ __device__ void count_wave_steps(const KParams& P, int base, uint32_t steps)
 // grazing rays with many case-(b) children) runs again with a 64-entry stack in private memory, out
 // of line so that its frame stays out of the traversal loop's registers; the exact octree walk is
 // left for what that cannot certify.
-__device__ __noinline__ int wide_closest_deep(const WNode* wnodes, const GTri* wtris, v3 o, v3 d, float m, WHit& w,
-                                              float hi, bool ties, float QS, const uint64_t* rk, int rsel, float rsub)
+// The record comes back by value (WDeep, in registers): a WHit passed by reference would live in
+// scratch in every caller, and each query's record went through it (r05: the plain kernel's HBM writes).
+struct WDeep {
+    int st;
+    WHit w;
+};
+__device__ __noinline__ WDeep wide_closest_deep(const WNode* wnodes, const GTri* wtris, v3 o, v3 d, float m, float hi,
+                                                bool ties, float QS, const uint64_t* rk, int rsel, float rsub)
 {
     WStackArr<W_DEEP_STACK> stk;
-    const int st = wbvh_closest(wnodes, wtris, o, d, m, stk, w, nullptr, hi, ties, QS, rk, rsel, rsub);
-    return st == W_DEEP ? W_UNCERT : st;
+    WDeep r;
+    const int st = wbvh_closest(wnodes, wtris, o, d, m, stk, r.w, nullptr, hi, ties, QS, rk, rsel, rsub);
+    r.st = st == W_DEEP ? W_UNCERT : st;
+    return r;
 }
 
 // BVH::intersect through the wide BVH and its certificate (wbvh.hpp).
@@ -957,9 +965,12 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
         *longq = true;
         return false;
     }
-    if (st == W_DEEP)
-        st = wide_closest_deep(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), w, INFINITY, true, W_QS_CLOSEST,
-                               rk, 0, 0.0f);
+    if (st == W_DEEP) {
+        const WDeep r = wide_closest_deep(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), INFINITY, true,
+                                          W_QS_CLOSEST, rk, 0, 0.0f);
+        st = r.st;
+        w = r.w;
+    }
     if (st == W_MISS) {
         h.t = -1.0f;
         h.u = 1.0f;
@@ -1029,9 +1040,12 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
     int st = wbvh_closest<WStackLds, G>(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, hi, false,
                           W_QS_SHADOW, rk, 1, rsub);
 #endif
-    if (st == W_DEEP)
-        st = wide_closest_deep(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), w, hi, false, W_QS_SHADOW, rk,
-                               1, rsub);
+    if (st == W_DEEP) {
+        const WDeep r = wide_closest_deep(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), hi, false, W_QS_SHADOW,
+                                          rk, 1, rsub);
+        st = r.st;
+        w = r.w;
+    }
     if (st == W_MISS) {
         *sh = false;
         return true;
@@ -3241,8 +3255,11 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_PLAIN) void wide_query_kernel(KParams
         const float m = 0x1p-16f * (om + P.scene_scale);
         WStackLds stk{lv};
         st = wbvh_closest<WStackLds, G>(P.wnodes, P.wtris, o, d, m, stk, w, nullptr, INFINITY, true, QS, rk, rsel, rsub);
-        if (st == W_DEEP)
-            st = wide_closest_deep(P.wnodes, P.wtris, o, d, m, w, INFINITY, true, QS, rk, rsel, rsub);
+        if (st == W_DEEP) {
+            const WDeep r = wide_closest_deep(P.wnodes, P.wtris, o, d, m, INFINITY, true, QS, rk, rsel, rsub);
+            st = r.st;
+            w = r.w;
+        }
         if (st == W_HIT) {
             const uint4 M = ldg(P.wmeta + w.k);
             if (kdop_certifies(load_gnode(P.nodes + M.y), o, d, w.t))

@@ -53,6 +53,9 @@ namespace rt {
 constexpr uint32_t W_LEAF = 0x80000000u;
 constexpr uint32_t W_EMPTY = 0xFFFFFFFFu;
 constexpr int W_MAX_LEAF = 8;
+#ifndef W_GROUP_ILP
+#define W_GROUP_ILP 0   // lane groups: the four children's tests interleaved by the scheduler (wbvh_closest)
+#endif
 #ifndef W_STACK_N
 #define W_STACK_N 16
 #endif
@@ -1096,8 +1099,10 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                 }
 #if defined(__HIP_DEVICE_COMPILE__)
                 // one child at a time: the scheduler would interleave the children's
-                // temporaries (VALU latency is hidden by the other waves anyway)
-                __builtin_amdgcn_sched_barrier(0);
+                // temporaries (VALU latency is hidden by the other waves anyway); a lane group
+                // (the few long queries of split tiles, W_GROUP_ILP) may interleave them
+                if (G == 1 || !W_GROUP_ILP)
+                    __builtin_amdgcn_sched_barrier(0);
 #endif
             }
             // sort the (key, ref) pairs ascending: misses (INFINITY) go last
