@@ -539,6 +539,7 @@ int rt_wbvh_query_ex(const float* tri9, int64_t n, int32_t max_depth, int32_t le
                 rt::wbvh_risk_host(w, lbox, RA, 1, risk);
         }
         std::atomic<int64_t> work_n{0}, work_t{0};
+        const bool probe_hi = std::getenv("RT_WQ_PROBE_HI") != nullptr;
         auto body = [&](int64_t b, int64_t e) {
             rt::WStackLocal stk;
             uint32_t wk[4] = {0, 0, 0, 0};
@@ -602,6 +603,15 @@ int rt_wbvh_query_ex(const float* tri9, int64_t n, int32_t max_depth, int32_t le
                                           shadow_rays ? W_QS_SHADOW : W_QS_CLOSEST, rk, rsel, rsub);
                     if (st == rt::W_DEEP)
                         st = rt::W_UNCERT;
+                }
+                if (st == rt::W_HIT && probe_hi) {
+                    // (diagnostic, RT_WQ_PROBE_HI=1: the same query again with its answer known up front,
+                    // hi = t*: the visits a perfect visiting order would leave; ray_nodes reports those)
+                    rt::WStackArr<rt::W_DEEP_STACK> deep;
+                    rt::WHit h2;
+                    wk[0] = wk0;
+                    rt::wbvh_closest(w.nodes.data(), w.tris.data(), o, d, m, deep, h2, wk, h.t, true,
+                                     shadow_rays ? W_QS_SHADOW : W_QS_CLOSEST, rk, rsel, rsub);
                 }
                 if (st == rt::W_HIT) {
                     int32_t slot = w.slot[(size_t)h.k];

@@ -2126,8 +2126,12 @@ __device__ __forceinline__ void make_frame(const KParams& P, FrameRec& F, v3 ip,
 
 // Level 0: the primary ray of every pixel, shaded (with its shadow query); a
 // reflective hit becomes a level-1 frame, any other pixel is finished here.
-__global__ __launch_bounds__(BLOCK, RT_OCC) void refl_level0_kernel(KParams P, FrameRec* fr1, unsigned int* nfr1)
+__global__ __launch_bounds__(BLOCK, RT_OCC) void refl_level0_kernel(KParams P_arg, FrameRec* fr1, unsigned int* nfr1)
 {
+    // the parameters where the kernel received them (not a copy: passing the by-value argument to a
+    // call made every lane copy it to scratch, r05: C5's shadow pass wrote ~90 GB per launch)
+    const KParams& P = kernel_params();
+    (void)P_arg;
     extern __shared__ uint2 lds_levels[];
     uint2* lv = lds_levels + threadIdx.x;
     int lane = threadIdx.x & 63;
@@ -2274,8 +2278,12 @@ __device__ __forceinline__ bool refl_gen(const KParams& P, const ReflArgs& A, in
 #endif
 __device__ void refl_trace_one(const KParams& P, const ReflArgs& A, int slot, v3 dir, uint2* lv, uint32_t max_steps);
 
-__global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_kernel(KParams P, ReflArgs A)
+__global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_kernel(KParams P_arg, ReflArgs A)
 {
+    // the parameters where the kernel received them (not a copy: passing the by-value argument to a
+    // call made every lane copy it to scratch, r05: C5's shadow pass wrote ~90 GB per launch)
+    const KParams& P = kernel_params();
+    (void)P_arg;
     extern __shared__ uint2 lds_levels[];
     uint2* lv = lds_levels + threadIdx.x;
     int slot = blockIdx.x * BLOCK + threadIdx.x;
@@ -2300,8 +2308,12 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_kernel(KParams 
 
 // The queries refl_trace_kernel deferred (ReflArgs::defer): traced to the end, one lane each, so that
 // their waves hold long queries only.
-__global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_long_kernel(KParams P, ReflArgs A)
+__global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_long_kernel(KParams P_arg, ReflArgs A)
 {
+    // the parameters where the kernel received them (not a copy: passing the by-value argument to a
+    // call made every lane copy it to scratch, r05: C5's shadow pass wrote ~90 GB per launch)
+    const KParams& P = kernel_params();
+    (void)P_arg;
     extern __shared__ uint2 lds_levels[];
     uint2* lv = lds_levels + threadIdx.x;
     const int n = (int)ldg(A.defer_count);
@@ -2362,8 +2374,12 @@ __device__ __forceinline__ void list_append(const ReflArgs& A, int slot)
 }
 
 // pass1: per frame, the samples' trace_ray up to the shadow query, in sample order
-__global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_pass1_kernel(KParams P, ReflArgs A)
+__global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_pass1_kernel(KParams P_arg, ReflArgs A)
 {
+    // the parameters where the kernel received them (not a copy: passing the by-value argument to a
+    // call made every lane copy it to scratch, r05: C5's shadow pass wrote ~90 GB per launch)
+    const KParams& P = kernel_params();
+    (void)P_arg;
     int p = A.c0 + blockIdx.x * BLOCK + threadIdx.x;
     unsigned nshadow = 0;
     if (p < A.c1) {
@@ -2443,8 +2459,12 @@ __global__ __launch_bounds__(BLOCK) void refl_list_kernel(KParams P, ReflArgs A)
 __device__ __forceinline__ int spawn_sample(const KParams& P, const ReflArgs& A, int slot, SampleRec& S, bool sh);
 
 // shadow: is_shadowed (renderer.cpp:340-402) for every shaded sample (via the list)
-__global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_shadow_kernel(KParams P, ReflArgs A)
+__global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_shadow_kernel(KParams P_arg, ReflArgs A)
 {
+    // the parameters where the kernel received them (not a copy: passing the by-value argument to a
+    // call made every lane copy it to scratch, r05: C5's shadow pass wrote ~90 GB per launch)
+    const KParams& P = kernel_params();
+    (void)P_arg;
     extern __shared__ uint2 lds_levels[];
     uint2* lv = lds_levels + threadIdx.x;
     unsigned t = blockIdx.x * BLOCK + threadIdx.x;
@@ -2485,8 +2505,12 @@ __device__ __forceinline__ int spawn_sample(const KParams& P, const ReflArgs& A,
 }
 
 // spawn: reflective hits become frames of the next level (A.fused == 0; else the shadow pass)
-__global__ __launch_bounds__(BLOCK) void refl_spawn_kernel(KParams P, ReflArgs A)
+__global__ __launch_bounds__(BLOCK) void refl_spawn_kernel(KParams P_arg, ReflArgs A)
 {
+    // the parameters where the kernel received them (not a copy: passing the by-value argument to a
+    // call made every lane copy it to scratch, r05: C5's shadow pass wrote ~90 GB per launch)
+    const KParams& P = kernel_params();
+    (void)P_arg;
     int slot = blockIdx.x * BLOCK + threadIdx.x;
     int nslot = (A.c1 - A.c0) * A.stride;
     if (slot >= nslot)
@@ -2499,8 +2523,12 @@ __global__ __launch_bounds__(BLOCK) void refl_spawn_kernel(KParams P, ReflArgs A
 }
 
 // resolve: compute_reflection's sum in sample order, then the frame's hit colour
-__global__ __launch_bounds__(BLOCK) void refl_resolve_kernel(KParams P, ReflArgs A)
+__global__ __launch_bounds__(BLOCK) void refl_resolve_kernel(KParams P_arg, ReflArgs A)
 {
+    // the parameters where the kernel received them (not a copy: passing the by-value argument to a
+    // call made every lane copy it to scratch, r05: C5's shadow pass wrote ~90 GB per launch)
+    const KParams& P = kernel_params();
+    (void)P_arg;
     int p = A.c0 + blockIdx.x * BLOCK + threadIdx.x;
     if (p >= A.c1)
         return;
@@ -2816,9 +2844,13 @@ __global__ __launch_bounds__(BLOCK) void raster_fill_big_kernel(KParams P, Raste
 // per pixel: the winning piece's shading (trace_triangle / debug shadings), reflective
 // hits become level-1 frames of the reflection engine.  P.tri_uv is the piece_uv table
 // and Rec::tri a piece index here (trace_triangle's temporary triangle).
-__global__ __launch_bounds__(BLOCK, RT_OCC) void raster_shade_kernel(KParams P, RasterArgs A,
+__global__ __launch_bounds__(BLOCK, RT_OCC) void raster_shade_kernel(KParams P_arg, RasterArgs A,
                                                                      FrameRec* fr1, unsigned int* nfr1)
 {
+    // the parameters where the kernel received them (not a copy: passing the by-value argument to a
+    // call made every lane copy it to scratch, r05: C5's shadow pass wrote ~90 GB per launch)
+    const KParams& P = kernel_params();
+    (void)P_arg;
     extern __shared__ uint2 lds_levels[];
     uint2* lv = lds_levels + threadIdx.x;
     int lane = threadIdx.x & 63;
@@ -3146,12 +3178,16 @@ __global__ __launch_bounds__(256) void downscale_kernel(const uint32_t* __restri
 // BVH::intersect (bvh.cpp:68-71) for a batch of arbitrary rays: the closest-hit
 // query the reference's trace_ray / is_shadowed issue, exposed for callers and
 // for ray-level parity tests.  Brute-force loop when enable_bvh is off.
-__global__ __launch_bounds__(BLOCK) void trace_rays_kernel(KParams P, const float* __restrict__ orig,
+__global__ __launch_bounds__(BLOCK) void trace_rays_kernel(KParams P_arg, const float* __restrict__ orig,
                                                            const float* __restrict__ dir, int n,
                                                            int32_t* __restrict__ out_id, float* __restrict__ out_t,
                                                            float* __restrict__ out_u, float* __restrict__ out_v,
                                                            uint8_t* __restrict__ out_ret)
 {
+    // the parameters where the kernel received them (not a copy: passing the by-value argument to a
+    // call made every lane copy it to scratch, r05: C5's shadow pass wrote ~90 GB per launch)
+    const KParams& P = kernel_params();
+    (void)P_arg;
     extern __shared__ uint2 lds_levels[];
     uint2* lv = lds_levels + threadIdx.x;
     int i = blockIdx.x * BLOCK + threadIdx.x;
@@ -3195,13 +3231,17 @@ __global__ __launch_bounds__(BLOCK) void trace_rays_kernel(KParams P, const floa
 // (The occupancy bound is the plain kernel's: wide_closest_deep is compiled once for all its callers,
 // within the loosest caller's register budget, and the plain kernel inherits what it uses.)
 template <int G>
-__global__ __launch_bounds__(BLOCK, RT_OCC_PLAIN) void wide_query_kernel(KParams P, const float* __restrict__ orig,
+__global__ __launch_bounds__(BLOCK, RT_OCC_PLAIN) void wide_query_kernel(KParams P_arg, const float* __restrict__ orig,
                                                            const float* __restrict__ dir, int n, int kind,
                                                            float* __restrict__ o_out, float* __restrict__ d_out,
                                                            int32_t* __restrict__ status, int32_t* __restrict__ out_id,
                                                            float* __restrict__ out_t, float* __restrict__ out_u,
                                                            float* __restrict__ out_v, uint8_t* __restrict__ out_sh)
 {
+    // the parameters where the kernel received them (not a copy: passing the by-value argument to a
+    // call made every lane copy it to scratch, r05: C5's shadow pass wrote ~90 GB per launch)
+    const KParams& P = kernel_params();
+    (void)P_arg;
     extern __shared__ uint2 lds_levels[];
     uint2* lv = lds_levels + threadIdx.x;
     // G > 1: the G lanes of a lane group trace ray i together (wbvh_closest<.., G>)
@@ -3286,7 +3326,7 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_PLAIN) void wide_query_kernel(KParams
 // current_recursion_depth into P.max_recursion_depth (only their difference is read).  Ray
 // i's rough-reflection stream is keyed as pixel i of a frame.
 template <bool REFL>
-__global__ __launch_bounds__(BLOCK, RT_OCC) void trace_colors_kernel(KParams P, const float* __restrict__ orig,
+__global__ __launch_bounds__(BLOCK, RT_OCC) void trace_colors_kernel(KParams P_arg, const float* __restrict__ orig,
                                                                      const float* __restrict__ dir, int n,
                                                                      float4* __restrict__ out_rgba,
                                                                      int32_t* __restrict__ out_src,
@@ -3294,6 +3334,10 @@ __global__ __launch_bounds__(BLOCK, RT_OCC) void trace_colors_kernel(KParams P, 
                                                                      uint8_t* __restrict__ out_found,
                                                                      uint8_t* __restrict__ out_shadow)
 {
+    // the parameters where the kernel received them (not a copy: passing the by-value argument to a
+    // call made every lane copy it to scratch, r05: C5's shadow pass wrote ~90 GB per launch)
+    const KParams& P = kernel_params();
+    (void)P_arg;
     extern __shared__ uint2 lds_levels[];
     uint2* lv = lds_levels + threadIdx.x;
     const int i = blockIdx.x * BLOCK + threadIdx.x;
