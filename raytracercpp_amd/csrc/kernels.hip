@@ -1136,7 +1136,7 @@ __device__ __forceinline__ OctQ octree_query(const KParams& P, v3 o, v3 d, float
 }
 
 // renderer.cpp:340-402
-template <bool PLAIN = false, int G = 1>
+template <bool PLAIN = false, int G = 1, bool CALL = PLAIN>
 __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
 {
     if (!P.compute_shadows)
@@ -1164,7 +1164,7 @@ __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
         bool sh;
         if (P.wnodes && P.nnodes > 0 && !nan && wide_shadow<G>(P, o, d, hi, p, lp, lv, &sh, light))
             return sh;
-        const OctQ q = octree_query<PLAIN>(P, o, d, -m, hi, P.seg_oct != 0, lv);
+        const OctQ q = octree_query<CALL>(P, o, d, -m, hi, P.seg_oct != 0, lv);
         h = q.h;
         r = q.r;
         if (r) {
@@ -1178,7 +1178,7 @@ __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
     }
     if (PLAIN || P.enable_bvh) {
         // whole-line query (segment queries off)
-        const OctQ oq = octree_query<PLAIN>(P, o, d, 0.0f, 0.0f, false, lv);
+        const OctQ oq = octree_query<CALL>(P, o, d, 0.0f, 0.0f, false, lv);
         h = oq.h;
         r = oq.r;
         if (r) {
@@ -2276,7 +2276,8 @@ __device__ __forceinline__ bool refl_gen(const KParams& P, const ReflArgs& A, in
 #define RT_OCC_REFL 4   // waves per SIMD of the reflection trace / shadow / pass1 kernels (r04, the sound query:
                         // C5 689 vs 656 Mrays/s at 5 (31 spills), 691 at 3; r03: 4 -> 5 about -0.6%)
 #endif
-__device__ void refl_trace_one(const KParams& P, const ReflArgs& A, int slot, v3 dir, uint2* lv, uint32_t max_steps);
+__device__ __forceinline__ void refl_trace_one(const KParams& P, const ReflArgs& A, int slot, v3 dir, uint2* lv,
+                                               uint32_t max_steps);
 
 __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_kernel(KParams P_arg, ReflArgs A)
 {
@@ -2328,14 +2329,17 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_long_kernel(KPa
 
 // One reflection sample's closest hit into A.hit[slot]; a query past max_steps (> 0) goes to the
 // deferred list instead.
-__device__ void refl_trace_one(const KParams& P, const ReflArgs& A, int slot, v3 dir, uint2* lv, uint32_t max_steps)
+// In line, with the octree fallback behind the out-of-line octree_query_call (results by value): a
+// ray record or hit record whose address reached a call lived in scratch for every sample (r05).
+__device__ __forceinline__ void refl_trace_one(const KParams& P, const ReflArgs& A, int slot, v3 dir, uint2* lv,
+                                               uint32_t max_steps)
 {
     const FrameRec& F = A.fr[A.order[A.c0 + slot / A.stride]];
-    TRay R = make_ray(P, ld3(F.ro), dir);
+    const v3 ro = ld3(F.ro);
     THit h;
     bool r;
     bool longq = false;
-    if (P.wnodes && P.nnodes > 0 && !R.nan && wide_closest(P, ld3(F.ro), dir, h, r, lv, nullptr, max_steps, &longq))
+    if (P.wnodes && P.nnodes > 0 && !ray_is_nan(ro, dir) && wide_closest(P, ro, dir, h, r, lv, nullptr, max_steps, &longq))
         ;   // certified by the wide BVH
     else if (longq) {
         const uint64_t m = __ballot(1);   // the lanes deferring now: one atomic per wave
@@ -2346,11 +2350,14 @@ __device__ void refl_trace_one(const KParams& P, const ReflArgs& A, int slot, v3
         base = __shfl(base, leader);
         A.defer[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = slot;
         return;
-    } else if (P.seg_scale > 0.0f && P.seg_oct) {
-        R.lo = -seg_margin(P, R);   // nothing behind the origin can be hit (t >= 0)
-        r = bvh_closest_seg(P, R, h, lv);
-    } else
-        r = bvh_closest(P, R, h, lv);
+    } else {
+        const bool seg = P.seg_scale > 0.0f && P.seg_oct;
+        // (seg: nothing behind the origin can be hit, t >= 0)
+        const float lo = seg ? -seg_margin(P, make_ray(P, ro, dir)) : 0.0f;
+        const OctQ q = octree_query<true>(P, ro, dir, lo, INFINITY, seg, lv);
+        h = q.h;
+        r = q.r;
+    }
     RawHit H;
     H.t = h.t;
     H.u = h.u;
@@ -2459,6 +2466,9 @@ __global__ __launch_bounds__(BLOCK) void refl_list_kernel(KParams P, ReflArgs A)
 __device__ __forceinline__ int spawn_sample(const KParams& P, const ReflArgs& A, int slot, SampleRec& S, bool sh);
 
 // shadow: is_shadowed (renderer.cpp:340-402) for every shaded sample (via the list)
+#ifndef RT_REFL_SHADOW_CALL
+#define RT_REFL_SHADOW_CALL 1   // the shadow pass's octree fallback out of line (octree_query_call)
+#endif
 __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_shadow_kernel(KParams P_arg, ReflArgs A)
 {
     // the parameters where the kernel received them (not a copy: passing the by-value argument to a
@@ -2473,7 +2483,7 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_shadow_kernel(KParams
     const int slot = A.list[t];
     SampleRec& S = A.sm[slot];
     v3 light = mk(P.light[0], P.light[1], P.light[2]);
-    const bool sh = is_shadowed(P, ld3(S.ip), ld3(S.nrm), light, lv);
+    const bool sh = is_shadowed<false, 1, RT_REFL_SHADOW_CALL != 0>(P, ld3(S.ip), ld3(S.nrm), light, lv);
     S.sh = sh ? 1 : 0;
     if (A.fused) {
         // the colour this sample returns (resolve, below): its child frame's, or its own finished shade

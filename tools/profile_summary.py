@@ -67,7 +67,8 @@ for f in sorted(glob.glob(f"{src}/pmc_*/**/run_counter_collection.csv", recursiv
         for k, v in agg[main].items():
             out["pmc_ray_trace_kernel"][k] = sum(v.values()) / len(v)
     name = f.split(os.sep)[-3] if "pmc_" in f.split(os.sep)[-3] else os.path.basename(os.path.dirname(f))
-    shutil.copy(f, os.path.join(dst, f"{name}_counters.csv"))
+    if os.path.getsize(f) < (1 << 20):   # (a C5 run's passes hold ~10k dispatches: kept in gpurun_out only)
+        shutil.copy(f, os.path.join(dst, f"{name}_counters.csv"))
 out.update(derive(out["pmc_ray_trace_kernel"]))
 for kname, p in per.items():
     out["pmc_per_kernel"][kname] = dict(counters=p, **derive(p))
