@@ -281,8 +281,9 @@ int rt_get_stats(rt_renderer *r, rt_stats *out);
  * shader cycles per phase {tile setup, ray generation, primary query, shading, shadow query,
  * framebuffer, dequeue} of the plain kernel.  RT_EINVAL when no record buffer exists. */
 int rt_debug_read(rt_renderer *r, uint64_t *out, int64_t n);
-/* Diagnostics (no reference counterpart): the shader cycles of each 8x8 tile of the last rt_render /
- * rt_ray_trace launch (tile = ty * tiles_x + tx; the heavy-first ordering's input).
+/* Diagnostics (no reference counterpart): the shader cycles of each 8x8 tile of the last launch --
+ * rt_render / rt_ray_trace, or rt_render_bands_device (its launch-local tiles) -- (tile = ty * tiles_x
+ * + tx; the heavy-first ordering's input; a split tile, the sum of its parts' cycles).
  * out == NULL: only the layout.  RT_EINVAL before a launch that records them (reflections, raster,
  * RT_HEAVY_FIRST=0). */
 int rt_tile_costs(rt_renderer *r, uint32_t *out, int64_t n, int32_t *tiles_x, int32_t *tiles_y);

@@ -62,6 +62,9 @@ constexpr int BLOCK = 64 * WAVES_PER_BLOCK;
 #define RT_OCC_PLAIN 3   // the plain kernel: 168 VGPRs (r04, the sound wide query: 4.31 ms vs 5.4 at 4 waves with
                          // 103 spills, 5.17 at 2; r02's unsound query: 0.67 ms at 4 vs 0.71 at 5, 0.69 at 3)
 #endif
+#ifndef RT_OCC_OCT
+#define RT_OCC_OCT 5     // ray_trace_kernel<false, true, true>: the octree walk alone (first frames, exact mode)
+#endif
 // RT_COUNT=1 (diagnostic builds only, tools/count_gpu_work.py): every traversal adds
 // its k-DOP and Moller-Trumbore test counts to P.counters[4..7] (whole-line queries:
 // 4 / 5, segment queries: 6 / 7), the work the kernel actually did
@@ -1136,7 +1139,8 @@ __device__ __forceinline__ OctQ octree_query(const KParams& P, v3 o, v3 d, float
 }
 
 // renderer.cpp:340-402
-template <bool PLAIN = false, int G = 1, bool CALL = PLAIN>
+// OCT: the octree walk only (ray_trace_kernel's octree specialisation: no wide-BVH code)
+template <bool PLAIN = false, int G = 1, bool CALL = PLAIN, bool OCT = false>
 __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
 {
     if (!P.compute_shadows)
@@ -1162,7 +1166,7 @@ __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
         }
         // (seg_scale > 0: no analytic shapes, so shapes_shadow below has nothing to add)
         bool sh;
-        if (P.wnodes && P.nnodes > 0 && !nan && wide_shadow<G>(P, o, d, hi, p, lp, lv, &sh, light))
+        if (!OCT && P.wnodes && P.nnodes > 0 && !nan && wide_shadow<G>(P, o, d, hi, p, lp, lv, &sh, light))
             return sh;
         const OctQ q = octree_query<CALL>(P, o, d, -m, hi, P.seg_oct != 0, lv);
         h = q.h;
@@ -1239,7 +1243,7 @@ __device__ __forceinline__ void shapes_closest(const KParams& P, v3 o, v3 d, Rec
 // fin is the caller's HitInfo; returns the source (-1 none, >=0 triangle, -2-k shape k).
 // With the wide BVH (P.wnodes), a certified query takes its answer; one it cannot certify
 // is traced through the octree here.
-template <bool PLAIN = false, int G = 1>
+template <bool PLAIN = false, int G = 1, bool OCT = false>
 __device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv)
 {
     Rec local = rec_fresh();
@@ -1247,7 +1251,7 @@ __device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv)
     if (PLAIN || P.enable_bvh) {
         THit h;
         bool r = false;
-        const bool wide = P.wnodes && P.nnodes > 0 && !ray_is_nan(o, d);
+        const bool wide = !OCT && P.wnodes && P.nnodes > 0 && !ray_is_nan(o, d);
         if (wide && wide_closest<G>(P, o, d, h, r, lv, &local)) {
             // certified: a hit's record is already in local (a miss leaves it fresh)
             if (r && (local.t < fin.t || fin.t == -1)) {
@@ -1255,7 +1259,7 @@ __device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv)
                 src = local.tri;
             }
         } else {
-            const OctQ q = octree_query<PLAIN>(P, o, d, 0.0f, 0.0f, false, lv);
+            const OctQ q = octree_query<PLAIN && !OCT>(P, o, d, 0.0f, 0.0f, false, lv);
             bvh_record(P, q.h, q.r, local, fin, src);
         }
     } else {
@@ -1381,7 +1385,7 @@ __device__ c3 shade_debug(const KParams& P, const Rec& h)
     return fc;
 }
 
-template <bool PLAIN = false, int G = 1>
+template <bool PLAIN = false, int G = 1, bool OCT = false>
 __device__ Direct shade_direct(const KParams& P, v3 ro, v3 rd, Rec& h, uint2* lv, unsigned& nshadow)
 {
     Direct out;
@@ -1393,7 +1397,7 @@ __device__ Direct shade_direct(const KParams& P, v3 ro, v3 rd, Rec& h, uint2* lv
             nshadow++;
         v3 light = mk(P.light[0], P.light[1], P.light[2]);
         if (PLAIN) PH_MARK(3);
-        out.shadowed = is_shadowed<PLAIN, G>(P, out.ip, h.normal, light, lv);
+        out.shadowed = is_shadowed<PLAIN, G, PLAIN && !OCT, OCT>(P, out.ip, h.normal, light, lv);
         if (PLAIN) PH_MARK(4);
         out.fc = shade_shadow_emit(P, fc, mat_of(P, h.mat), out.shadowed);
     } else
@@ -1498,7 +1502,7 @@ struct PixelOut {
 
 // Renderer::trace_ray (renderer.cpp:1008-1066) for one primary ray, with the
 // compute_reflection recursion (when REFL) unrolled onto an explicit stack.
-template <bool REFL, bool PLAIN = false, int G = 1>
+template <bool REFL, bool PLAIN = false, int G = 1, bool OCT = false>
 __device__ PixelOut trace_pixel(const KParams& P, v3 cam, v3 rd0, uint2* lv, uint32_t pixel_key, unsigned& nshadow,
                                 unsigned& nrefl)
 {
@@ -1506,7 +1510,7 @@ __device__ PixelOut trace_pixel(const KParams& P, v3 cam, v3 rd0, uint2* lv, uin
     po.fin = rec_fresh();
     po.found = po.shadowed = false;
     po.alpha = 1.0f;
-    po.src = closest_hit<PLAIN && !REFL, REFL ? 1 : G>(P, cam, rd0, po.fin, lv);
+    po.src = closest_hit<PLAIN && !REFL, REFL ? 1 : G, OCT>(P, cam, rd0, po.fin, lv);
     if (PLAIN) PH_MARK(2);
     if (!REFL) {
         if (PLAIN && po.fin.t > 0.1f) {
@@ -1526,7 +1530,7 @@ __device__ PixelOut trace_pixel(const KParams& P, v3 cam, v3 rd0, uint2* lv, uin
             asm volatile("" ::: "memory");
             const v3 light = mk(P.light[0], P.light[1], P.light[2]);
             if (PLAIN) PH_MARK(3);
-            po.shadowed = is_shadowed<true, G>(P, ip, po.fin.normal, light, lv);
+            po.shadowed = is_shadowed<true, G, !OCT, OCT>(P, ip, po.fin.normal, light, lv);
             if (PLAIN) PH_MARK(4);
             asm volatile("" ::: "memory");
             const uint2 s0 = sv[0], s1 = sv[BLOCK], s2 = sv[2 * BLOCK];
@@ -1540,7 +1544,7 @@ __device__ PixelOut trace_pixel(const KParams& P, v3 cam, v3 rd0, uint2* lv, uin
         }
         if (po.fin.t > 0.1f) {
             po.found = true;
-            Direct D = shade_direct<PLAIN, G>(P, cam, rd0, po.fin, lv, nshadow);
+            Direct D = shade_direct<PLAIN, G, OCT>(P, cam, rd0, po.fin, lv, nshadow);
             po.shadowed = D.shadowed;
             po.color = PLAIN || P.shading_method == RT_SHADING
                            ? shade_finish(P, D.fc, mat_of(P, po.fin.mat), col(0, 0, 0))
@@ -1968,8 +1972,10 @@ __device__ __forceinline__ void trace_split_part(const KParams& P, uint2* lv, in
 // still trace; dynamic pulling keeps every CU busy until the queue drains.
 // PLAIN: no texture map, sky, analytic shape, debug shading or SSAO buffer (host-checked,
 // KParams::plain): those code paths are compiled out.
-template <bool REFL, bool PLAIN = false>
-__global__ __launch_bounds__(BLOCK, PLAIN ? RT_OCC_PLAIN : RT_OCC) void ray_trace_kernel(KParams P_arg)
+// OCT (with PLAIN): frames before the wide BVH is resident -- the octree walk in line, no
+// wide-BVH code, at its own occupancy
+template <bool REFL, bool PLAIN = false, bool OCT = false>
+__global__ __launch_bounds__(BLOCK, OCT ? RT_OCC_OCT : PLAIN ? RT_OCC_PLAIN : RT_OCC) void ray_trace_kernel(KParams P_arg)
 {
     // The kernel reads its parameters where the kernel received them, through a pointer
     // the compiler cannot hoist out of the tile loop: each field is loaded (scalar cache) where
@@ -1995,7 +2001,7 @@ __global__ __launch_bounds__(BLOCK, PLAIN ? RT_OCC_PLAIN : RT_OCC) void ray_trac
         asm volatile("" : "+s"(kpl));   // (the loop's loads depend on it: not hoisted)
         const KParams& P = *reinterpret_cast<const KParams*>((const void*)kpl);
         const v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
-        if (PLAIN && !REFL && P.heavy_group == 4 &&
+        if (PLAIN && !REFL && !OCT && P.heavy_group == 4 &&
             !__builtin_amdgcn_readfirstlane(__hip_atomic_load(&g_bq.split_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) {
             // the split tiles' parts first (trace_split_part)
             int t = 0;
@@ -2033,7 +2039,7 @@ __global__ __launch_bounds__(BLOCK, PLAIN ? RT_OCC_PLAIN : RT_OCC) void ray_trac
         if (PLAIN) PH_MARK(1);
 
         uint32_t rng = REFL ? pixel_seed((uint32_t)(py * P.rw + px), P.rng_seed) : 0u;
-        PixelOut po = trace_pixel<REFL, PLAIN>(P, cam, rd, lv, rng, nshadow, nrefl);
+        PixelOut po = trace_pixel<REFL, PLAIN, 1, OCT>(P, cam, rd, lv, rng, nshadow, nrefl);
         size_t o = (size_t)lr * P.rw + px;
         if (P.argb) P.argb[o] = color_to_argb(po.color);
         if (!REFL && P.ds_out) downscale_tile(P, lane, lr, px, color_to_argb(po.color));
@@ -3629,6 +3635,10 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(
         // the plain kernel's grid is exactly its residency (RT_OCC_PLAIN blocks of 4 waves per
         // CU): with two frames in flight, surplus blocks of one frame would be dispatched ahead
         // of the next frame's only to find the queue empty (C4 +1.3%: r02_bench98_*.log)
+        if (!P->wnodes) {   // the octree specialisation (its residency differs: the generic grid)
+            hipLaunchKernelGGL((rt::ray_trace_kernel<false, true, true>), dim3(blocks), dim3(rt::BLOCK), lds, stream, *P);
+            return hipGetLastError();
+        }
         const int pblocks = plain_blocks(*P);
         hipLaunchKernelGGL((rt::ray_trace_kernel<false, true>), dim3(pblocks), dim3(rt::BLOCK), lds, stream, *P);
     } else

@@ -1624,7 +1624,7 @@ int Renderer::debug_read(uint64_t* out, int64_t n)
 // (the heavy-first ordering's input; tools/tile_costs.py).  Zero for tiles off the image.
 int Renderer::tile_costs(uint32_t* out, int64_t n, int32_t* tiles_x, int32_t* tiles_y)
 {
-    const TileCost& T = tc_main_;
+    const TileCost& T = last_tc_ ? *last_tc_ : tc_main_;   // the last launch's (a band launch's slot, or trace_frame's)
     if (!T.cost.p || T.ntiles <= 0)
         return fail(RT_EINVAL, "tile_costs: no launch with tile costs yet (RT_HEAVY_FIRST=0, reflections or raster?)");
     *tiles_x = T.tiles_x;
@@ -1634,6 +1634,8 @@ int Renderer::tile_costs(uint32_t* out, int64_t n, int32_t* tiles_x, int32_t* ti
     if (n < T.ntiles)
         return fail(RT_EINVAL, "tile_costs: buffer smaller than tiles_x * tiles_y");
     hipError_t e = hipStreamSynchronize(stream_);
+    if (e == hipSuccess && sync_slots() != RT_OK)
+        return RT_EHIP;
     if (e == hipSuccess)
         e = hipMemcpy(out, T.cost.p, (size_t)T.ntiles * 4, hipMemcpyDeviceToHost);
     return e == hipSuccess ? RT_OK : hip_fail(e, "tile_costs");
@@ -1886,6 +1888,7 @@ int Renderer::prepare_heavy(KParams& P, TileCost& T, hipStream_t stream)
                                   stream)) != hipSuccess)
         return hip_fail(e, "heavy_prep_kernel");
     P.tile_cost = T.cost.as<uint32_t>();
+    last_tc_ = &T;
     P.heavy_list = list;
     P.heavy_bits = bits;
     P.heavy_ctr = ctr;

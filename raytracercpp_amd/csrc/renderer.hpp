@@ -320,6 +320,7 @@ private:
         int ntiles = 0, tiles_x = 0, tiles_y = 0;   // the last launch's layout
     };
     int prepare_heavy(KParams& P, TileCost& T, hipStream_t stream);
+    const TileCost* last_tc_ = nullptr;   // the last launch's (rt_tile_costs)
     TileCost tc_main_;   // trace_frame's launches (stream_)
     struct BandSlot {
         hipStream_t stream = nullptr;

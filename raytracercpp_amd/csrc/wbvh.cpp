@@ -841,6 +841,15 @@ void build_two_level(const FlatOctree& oct, std::vector<Prim, DefaultInitAlloc<P
                      std::vector<Prim, DefaultInitAlloc<Prim>>& tmp, std::vector<BNode, DefaultInitAlloc<BNode>>& bn,
                      Pool& pool)
 {
+    const bool prof = std::getenv("RT_BUILD_PROFILE") != nullptr;
+    auto tick = std::chrono::steady_clock::now();
+    auto phase = [&](const char* what) {
+        if (!prof)
+            return;
+        auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[wbvh]   two-level %-8s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(now - tick).count());
+        tick = now;
+    };
     std::vector<uint32_t> leaves;
     for (size_t i = 0; i < oct.nodes.size(); i++)
         if ((oct.nodes[i].b & LEAF_BIT) && (oct.nodes[i].b & ~LEAF_BIT) > 0)
@@ -873,6 +882,7 @@ void build_two_level(const FlatOctree& oct, std::vector<Prim, DefaultInitAlloc<P
         T.maxleaf = 1;
         T.run(nl);
     }
+    phase("top");
     // the top tree's nodes: those reachable from the root
     std::vector<int32_t> order;   // top nodes, preorder
     std::vector<int32_t> st{0};
@@ -937,6 +947,7 @@ void build_two_level(const FlatOctree& oct, std::vector<Prim, DefaultInitAlloc<P
         Bt.build_serial(k, b, e, vb.box(), vc.box(), alloc, sah);
         bn[(size_t)k].box = N0.box;
     });
+    phase("bottom");
     // top inner nodes: triangle ranges and normal sums, children first
     for (size_t q = order.size(); q-- > 0;) {
         BNode& N = bn[(size_t)order[q]];
