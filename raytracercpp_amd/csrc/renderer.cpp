@@ -106,6 +106,7 @@ Knobs Knobs::from_env()
     k.lslab = on("RT_LSLAB", true);
     k.plain = on("RT_PLAIN", true);
     k.plain_octree = on("RT_PLAIN_OCTREE", true);
+    k.quick_wbvh = on("RT_WBVH_QUICK_FIRST", true);
     k.fused_ssaa = on("RT_FUSED_SSAA", true);
     k.refl_engine = on("RT_REFL_ENGINE", true);
     k.refl_sort = on("RT_REFL_SORT", true);
@@ -174,7 +175,7 @@ int Renderer::init(std::string& err)
                      &d_image_, &d_rgba_,  &d_hit_id_, &d_hit_t_,   &d_shadow_, &d_counters_,
                      &d_tri9_,  &d_rcount_, &d_roff_,  &d_pieces_,  &d_piece_uv_, &d_zkey_, &d_big_, &d_scan_tmp_,
                      &d_zbuf_,  &d_nbuf_,   &d_ao_,     &d_cones_, &d_lslab_, &d_lsin_, &d_wnodes_, &d_wtris_, &d_wmeta_, &d_wtmp_,
-                     &d_wlinks_, &d_wrisk_, &d_dbg_};
+                     &d_wlinks_, &d_wrisk_, &d_dbg_, &d_wnodes2_, &d_wtris2_, &d_wmeta2_, &d_wtmp2_, &d_wlinks2_};
     for (DevBuf* b : all) b->device = device_;
     for (auto& b : d_tex_) b.device = device_;
     for (auto& b : d_sky_) b.device = device_;
@@ -605,6 +606,46 @@ static void leaf_cones(const FlatOctree& o, std::vector<float>& out, std::vector
 // The leaf cones / slabs and the wide BVH of the current octree, on accel_thread_ (DESIGN.md
 // 5.8).  Reads oct_ and the uploaded triangle tables; writes only cones_, lslab_, lsin_, wb_, their
 // device buffers and accel_ms_, none of which a frame reads before poll_accel adopts them.
+hipError_t Renderer::upload_wide(const WBvh& w, DevBuf& nodes, DevBuf& tris, DevBuf& meta, DevBuf& tmp, DevBuf& links,
+                                 hipStream_t stream)
+{
+    // the nodes, and the permutation from which the device gathers the wide BVH's triangle records
+    // and, per triangle, everything a certified hit needs in one 16-B load: the octree slot (the
+    // record's triangle), the leaf of its certificate, the caller's triangle index and its material
+    // (kernels.hip wide_gather_kernel)
+    hipError_t e;
+    const size_t nk = w.slot.size(), wn = w.nodes.size() * sizeof(WNode);
+    const size_t nl = w.tri_leaf.size() + w.parent.size();
+    if ((e = nodes.reserve(wn)) != hipSuccess || (e = tris.reserve(nk * sizeof(GTri))) != hipSuccess ||
+        (e = meta.reserve(nk * 16)) != hipSuccess || (e = tmp.reserve(nk * 8)) != hipSuccess ||
+        (e = links.reserve(nl * 4)) != hipSuccess)
+        return e;
+    hipSetDevice(device_);
+    int32_t* d_slot = tmp.as<int32_t>();
+    uint32_t* d_leaf = reinterpret_cast<uint32_t*>(d_slot + nk);
+    if ((e = hipMemcpyAsync(links.p, w.tri_leaf.data(), w.tri_leaf.size() * 4, hipMemcpyHostToDevice, stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(links.as<uint32_t>() + w.tri_leaf.size(), w.parent.data(), w.parent.size() * 4,
+                            hipMemcpyHostToDevice, stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(nodes.p, w.nodes.data(), wn, hipMemcpyHostToDevice, stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(d_slot, w.slot.data(), nk * 4, hipMemcpyHostToDevice, stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(d_leaf, w.leaf_of_slot.data(), nk * 4, hipMemcpyHostToDevice, stream)) != hipSuccess)
+        return e;
+    return rt_launch_wide_gather(d_tris_.as<GTri>(), d_slot, d_leaf, d_tri_id_.as<int32_t>(), d_tri_mat_.as<int32_t>(),
+                                 (int)nk, tris.as<GTri>(), meta.as<uint4>(), stream);
+}
+
+// The risk words' buffer for the resident tree (8 x 8 B words, 8 x 4 B keys and 8 x 24 B boxes per
+// node); growing it replaces the buffer, so launches in flight that read it are waited for first.
+int Renderer::reserve_risk(size_t nodes)
+{
+    if (d_wrisk_.bytes >= nodes * 288)
+        return RT_OK;
+    if (d_wrisk_.p && (sync_slots() != RT_OK || hipStreamSynchronize(stream_) != hipSuccess))
+        return RT_EHIP;
+    hipError_t e = d_wrisk_.reserve(nodes * 288);
+    return e == hipSuccess ? RT_OK : hip_fail(e, "hipMalloc (risk words)");
+}
+
 void Renderer::start_accel()
 {
     accel_state_.store(1);
@@ -626,41 +667,14 @@ void Renderer::start_accel()
         accel_ms_[0] = ms_since(t0);
         auto t1 = clk::now();
         if (knobs_.wbvh && !knobs_.exact)
-            build_wbvh(oct_, wb_);
+            build_wbvh(oct_, wb_next_);
         else
-            wb_ = WBvh();
+            wb_next_ = WBvh();
         accel_ms_[1] = ms_since(t1);
         auto t2 = clk::now();
         hipSetDevice(device_);
-        if (e == hipSuccess && !wb_.nodes.empty()) {
-            // the nodes, and the permutation from which the device gathers the wide BVH's triangle
-            // records and, per triangle, everything a certified hit needs in one 16-B load: the
-            // octree slot (the record's triangle), the leaf of its certificate, the caller's
-            // triangle index and its material (kernels.hip wide_gather_kernel)
-            const size_t nk = wb_.slot.size(), wn = wb_.nodes.size() * sizeof(WNode);
-            const size_t nl = wb_.tri_leaf.size() + wb_.parent.size();
-            if ((e = d_wnodes_.reserve(wn)) == hipSuccess && (e = d_wtris_.reserve(nk * sizeof(GTri))) == hipSuccess &&
-                (e = d_wmeta_.reserve(nk * 16)) == hipSuccess && (e = d_wtmp_.reserve(nk * 8)) == hipSuccess &&
-                (e = d_wlinks_.reserve(nl * 4)) == hipSuccess &&
-                (e = d_wrisk_.reserve(wb_.nodes.size() * 288)) == hipSuccess &&
-                (e = hipMemcpyAsync(d_wlinks_.p, wb_.tri_leaf.data(), wb_.tri_leaf.size() * 4, hipMemcpyHostToDevice,
-                                    accel_stream_)) == hipSuccess &&
-                (e = hipMemcpyAsync(d_wlinks_.as<uint32_t>() + wb_.tri_leaf.size(), wb_.parent.data(),
-                                    wb_.parent.size() * 4, hipMemcpyHostToDevice, accel_stream_)) == hipSuccess) {
-                hipSetDevice(device_);
-                int32_t* d_slot = d_wtmp_.as<int32_t>();
-                uint32_t* d_leaf = reinterpret_cast<uint32_t*>(d_slot + nk);
-                if ((e = hipMemcpyAsync(d_wnodes_.p, wb_.nodes.data(), wn, hipMemcpyHostToDevice, accel_stream_)) ==
-                        hipSuccess &&
-                    (e = hipMemcpyAsync(d_slot, wb_.slot.data(), nk * 4, hipMemcpyHostToDevice, accel_stream_)) ==
-                        hipSuccess &&
-                    (e = hipMemcpyAsync(d_leaf, wb_.leaf_of_slot.data(), nk * 4, hipMemcpyHostToDevice, accel_stream_)) ==
-                        hipSuccess)
-                    e = rt_launch_wide_gather(d_tris_.as<GTri>(), d_slot, d_leaf, d_tri_id_.as<int32_t>(),
-                                              d_tri_mat_.as<int32_t>(), (int)nk, d_wtris_.as<GTri>(), d_wmeta_.as<uint4>(),
-                                              accel_stream_);
-            }
-        }
+        if (e == hipSuccess && !wb_next_.nodes.empty())
+            e = upload_wide(wb_next_, d_wnodes2_, d_wtris2_, d_wmeta2_, d_wtmp2_, d_wlinks2_, accel_stream_);
         if (e == hipSuccess)
             e = hipStreamSynchronize(accel_stream_);
         accel_ms_[2] = ms_since(t2);
@@ -685,8 +699,21 @@ int Renderer::poll_accel(bool wait)
     }
     accel_state_.store(0);
     cones_ready_ = !cones_.empty();
-    wide_ready_ = !wb_.nodes.empty();
     lslab_ready_ = !lslab_.empty();
+    if (!wb_next_.nodes.empty() || !knobs_.wbvh || knobs_.exact) {
+        // the background's tree replaces the resident one (the quick tree, if any): launches in flight
+        // keep reading the old buffers, which the next geometry change rewrites only after waiting for them
+        std::swap(wb_, wb_next_);
+        wb_next_ = WBvh();
+        d_wnodes_.swap(d_wnodes2_);
+        d_wtris_.swap(d_wtris2_);
+        d_wmeta_.swap(d_wmeta2_);
+        d_wtmp_.swap(d_wtmp2_);
+        d_wlinks_.swap(d_wlinks2_);
+    }
+    wide_ready_ = !wb_.nodes.empty();
+    if (wide_ready_ && reserve_risk(wb_.nodes.size()) != RT_OK)
+        return RT_EHIP;
     risk_valid_ = false;
     risk_nodes_ = (int64_t)wb_.nodes.size();
     risk_tris_ = (int64_t)wb_.tri_leaf.size();
@@ -849,6 +876,18 @@ int Renderer::ensure_device_scene()
             e = hipMemcpyAsync(d_tri_mat_.p, tri_mat_.data(), tri_mat_.size() * 4, hipMemcpyHostToDevice, stream_);
         if (e == hipSuccess && !tri_uv_.empty())
             e = hipMemcpyAsync(d_tri_uv_.p, tri_uv_.data(), tri_uv_.size() * 4, hipMemcpyHostToDevice, stream_);
+        // the quick wide BVH (the octree's own hierarchy, O(n): wbvh.hpp build_wbvh_quick) while the octree
+        // uploads, resident for the next frames until the SAH tree replaces it
+        const bool quick = e == hipSuccess && s_.enable_bvh && knobs_.quick_wbvh && knobs_.wbvh && !knobs_.exact &&
+                           oct_nn_ > 0;
+        wb_ = WBvh();
+        if (quick) {
+            auto tq = clk::now();
+            build_wbvh_quick(oct_, wb_);
+            build_split_ms_[2] = ms_since(tq);
+            if (!wb_.nodes.empty())
+                e = upload_wide(wb_, d_wnodes_, d_wtris_, d_wmeta_, d_wtmp_, d_wlinks_, stream_);
+        }
         if (e == hipSuccess)
             e = hipStreamSynchronize(stream_);
         if (e != hipSuccess)
@@ -857,7 +896,18 @@ int Renderer::ensure_device_scene()
         geom_dirty_ = false;
         tri9_dirty_ = true;
         build_ms_ = ms_since(t0);
-        build_split_ms_[1] = build_split_ms_[2] = 0.0f;
+        build_split_ms_[1] = 0.0f;
+        if (!wb_.nodes.empty()) {
+            wide_ready_ = true;
+            int rc = reserve_risk(wb_.nodes.size());
+            if (rc != RT_OK)
+                return rc;
+            risk_valid_ = false;
+            risk_nodes_ = (int64_t)wb_.nodes.size();
+            risk_tris_ = (int64_t)wb_.tri_leaf.size();
+            ++accel_ver_;
+        } else
+            build_split_ms_[2] = 0.0f;
         // the leaf cones / slabs and the wide BVH: beside the next frames (RT_ASYNC_ACCEL=0: now)
         if (s_.enable_bvh) {
             start_accel();

@@ -29,6 +29,13 @@ struct DevBuf {
     hipError_t reserve(size_t n);   // grows (never shrinks); contents undefined after growth
     void release();
     template <class T> T* as() const { return static_cast<T*>(p); }
+    // exchanges the allocations (a copy would free one buffer twice)
+    void swap(DevBuf& o)
+    {
+        std::swap(p, o.p);
+        std::swap(bytes, o.bytes);
+        std::swap(device, o.device);
+    }
 };
 
 struct HostTex {
@@ -46,6 +53,8 @@ struct Knobs {
     bool cones = true;        // RT_CONES=0: no leaf normal cones (5.3; also turns the leaf slabs off)
     bool lslab = true;        // RT_LSLAB=0: no leaf slabs (5.4)
     bool plain = true;        // RT_PLAIN=0: no plain specialisation of ray_trace_kernel (5.6)
+    bool quick_wbvh = true;   // RT_WBVH_QUICK_FIRST=0: no quick wide BVH after a geometry change (the frames
+                              // before the SAH tree is resident walk the octree; 5.9)
     bool plain_octree = true; // RT_PLAIN_OCTREE=0: frames on the octree path (before the wide BVH is resident,
                               // exact mode) take the general kernel, not the plain one (5.8)
     bool fused_ssaa = true;   // RT_FUSED_SSAA=0: band launches downscale in a separate pass (7)
@@ -263,6 +272,15 @@ private:
     WBvh wb_;
     DevBuf d_wnodes_, d_wtris_, d_wmeta_;
     DevBuf d_wtmp_;   // the wide BVH's slot map and the octree's slot -> leaf map, for wide_gather_kernel
+    // the background build's tree and buffers (start_accel), swapped in at adoption (poll_accel): the
+    // resident tree may be the quick one (wbvh.hpp build_wbvh_quick) that frames in flight still read
+    WBvh wb_next_;
+    DevBuf d_wnodes2_, d_wtris2_, d_wmeta2_, d_wtmp2_, d_wlinks2_;
+    // a wide BVH's upload into the given buffers on 'stream' (the gather of its triangle records and
+    // metadata from the resident octree tables on the device)
+    hipError_t upload_wide(const WBvh& w, DevBuf& nodes, DevBuf& tris, DevBuf& meta, DevBuf& tmp, DevBuf& links,
+                           hipStream_t stream);
+    int reserve_risk(size_t nodes);
     // the grazing-risk keys (KParams::wrisk): the walk's links (WBvh::tri_leaf then parent), the keys,
     // and the camera / light / structure they were computed for; risk_ev_ follows their launch
     DevBuf d_wlinks_, d_wrisk_;

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <thread>
 
 #include <emmintrin.h>   // SSE2 (x86-64 baseline): the builder's box min / max four lanes at a time
@@ -965,6 +966,11 @@ void build_two_level(const FlatOctree& oct, std::vector<Prim, DefaultInitAlloc<P
 
 void build_wbvh(const FlatOctree& oct, WBvh& out)
 {
+    if (const char* q = std::getenv("RT_WBVH_QUICK"))
+        if (q[0] == '1') {   // (tests, probes: the quick tree in place of the SAH tree)
+            build_wbvh_quick(oct, out);
+            return;
+        }
     const bool prof = std::getenv("RT_BUILD_PROFILE") != nullptr;
     auto tick = std::chrono::steady_clock::now();
     auto phase = [&](const char* what) {
@@ -1133,6 +1139,474 @@ void build_wbvh(const FlatOctree& oct, WBvh& out)
     phase("exit");
 }
 
+// ---- The quick wide BVH (r05): the octree itself as the tree -----------------------------------
+// For the frames right after a geometry change: every octree inner node becomes a
+// wide node (one with up to four children; with five to eight, the extra ones under one or two group
+// nodes), an octree leaf of up to 8 triangles a leaf child, a larger one a small 4-ary tree over its
+// triangles in runs of 8.  The triangles take the octree's depth-first leaf order, so every subtree is a
+// range.  Everything is O(n): a leaf-level child's slab range, cones and conditioning come from its
+// triangles exactly; an upper child's from its children, conservatively -- the slab from its box's
+// corners, the cone half-angles by the triangle inequality (angle(n, N) <= angle(n, N_c) +
+// angle(N_c, N)), min / max for the rest.  Its float box holds its octree node's axis box, so rho = 0
+// above the octree leaves (as in the two-level SAH tree).  check_wbvh verifies all of it like the SAH
+// tree's.
+namespace {
+
+struct QChild {
+    Box box;
+    uint32_t link = W_EMPTY;   // W_LEAF | first << 3 | (count - 1), or a node index
+    double ns[3] = {0, 0, 0};  // sum of the stored normals (the slab normal's direction)
+    int nq[3] = {1, 0, 0};     // the quantised slab normal (quantise's rule)
+    double slo = INFINITY, shi = -INFINITY;   // range of nq . v over the triangles' vertices (absolute)
+    double tc = 0, ts = 0;     // half-angles between nq and the stored normals / the exact normals below
+    bool nocone = false, nosth = false;
+    double smin = 1.0, s2 = 1.0, lmax = 0.0;
+    int32_t leaf = -1;         // a run of an octree leaf's triangles: that leaf (rho against its axis box)
+};
+
+inline void q_normal(QChild& c)
+{
+    const double len = std::sqrt(c.ns[0] * c.ns[0] + c.ns[1] * c.ns[1] + c.ns[2] * c.ns[2]);
+    for (int a = 0; a < 3; a++)
+        c.nq[a] = len > 0 ? (int)std::lround(127.0 * c.ns[a] / len) : (a == 0 ? 1 : 0);
+    if (c.nq[0] == 0 && c.nq[1] == 0 && c.nq[2] == 0)
+        c.nq[0] = 1;
+}
+
+inline double q_len(const int* q) { return std::sqrt((double)q[0] * q[0] + (double)q[1] * q[1] + (double)q[2] * q[2]); }
+
+// angle between two quantised normals, rounded up (acos near 1 turns the cosine's rounding, ~1e-16,
+// into ~1.5e-8 of angle: 1e-7 of slack)
+inline double q_angle(const int* a, const int* b)
+{
+    const double c = ((double)a[0] * b[0] + (double)a[1] * b[1] + (double)a[2] * b[2]) / (q_len(a) * q_len(b));
+    return std::acos(std::max(-1.0, std::min(1.0, c))) + 1e-7;
+}
+
+// a run of triangles [first, first + cnt) of the wide order: everything from the triangles themselves
+void q_from_tris(QChild& c, const GTri* t, int32_t first, int32_t cnt)
+{
+    c.box = empty_box();
+    for (int a = 0; a < 3; a++)
+        c.ns[a] = 0;
+    for (int32_t i = first; i < first + cnt; i++) {
+        grow(c.box, tri_box(t[i]));
+        for (int a = 0; a < 3; a++)
+            c.ns[a] += (double)t[i].n[a];
+    }
+    q_normal(c);
+    const double n0 = c.nq[0], n1 = c.nq[1], n2 = c.nq[2], NL = q_len(c.nq);
+    double cmin = 1.0, smn = 1.0;   // stored normals (cone), exact normals (sth)
+    for (int32_t i = first; i < first + cnt; i++) {
+        const GTri& T = t[i];
+        const double a0 = T.a[0], a1 = T.a[1], a2 = T.a[2];
+        const double s0 = n0 * a0 + n1 * a1 + n2 * a2;
+        const double s1 = n0 * (a0 + (double)T.ab[0]) + n1 * (a1 + (double)T.ab[1]) + n2 * (a2 + (double)T.ab[2]);
+        const double sv = n0 * (a0 + (double)T.ac[0]) + n1 * (a1 + (double)T.ac[1]) + n2 * (a2 + (double)T.ac[2]);
+        c.slo = std::min(c.slo, std::min(s0, std::min(s1, sv)));
+        c.shi = std::max(c.shi, std::max(s0, std::max(s1, sv)));
+        const double m0 = T.n[0], m1 = T.n[1], m2 = T.n[2];
+        const double mlen = std::sqrt(m0 * m0 + m1 * m1 + m2 * m2);
+        if (mlen == 0)
+            continue;   // Mdet = 0: never a hit (no cone, no conditioning bound needed)
+        if (!(mlen > 1e-30 && mlen < 1e27))
+            c.nocone = true;
+        else
+            cmin = std::min(cmin, (m0 * n0 + m1 * n1 + m2 * n2) / (mlen * NL));
+        const double x0 = T.ab[0], x1 = T.ab[1], x2 = T.ab[2], y0 = T.ac[0], y1 = T.ac[1], y2 = T.ac[2];
+        const double c0 = x1 * y2 - x2 * y1, c1 = x2 * y0 - x0 * y2, c2 = x0 * y1 - x1 * y0;
+        const double la = std::sqrt(x0 * x0 + x1 * x1 + x2 * x2), lc = std::sqrt(y0 * y0 + y1 * y1 + y2 * y2);
+        const double cl = std::sqrt(c0 * c0 + c1 * c1 + c2 * c2);
+        c.lmax = std::max(c.lmax, std::max(la, lc) * (1 + 1e-12));
+        c.smin = std::min(c.smin, sin_at_a_lb(T));
+        if (!(la * lc > 0x1p-100) || !(cl > 0x1p-50 * la * lc)) {
+            c.s2 = 0.0;
+            c.nosth = true;
+            continue;
+        }
+        const double ca = std::fabs(x0 * y0 + x1 * y1 + x2 * y2) / (la * lc);
+        c.s2 = std::min(c.s2, std::sqrt(std::max(0.0, (1.0 - std::min(1.0, ca + 1e-12)) / 2.0)) * (1 - 1e-9));
+        smn = std::min(smn, (c0 * n0 + c1 * n1 + c2 * n2) / (cl * NL) - 1e-12);
+    }
+    c.tc = std::acos(std::max(-1.0, std::min(1.0, cmin))) + 1e-7;
+    c.ts = std::acos(std::max(-1.0, std::min(1.0, smn))) + 1e-7;
+}
+
+// an upper child from its children (and the octree node's axis box, which it holds)
+void q_combine(QChild& p, const QChild* ch, int nc, const Box* extra)
+{
+    p.box = empty_box();
+    if (extra)
+        p.box = *extra;
+    for (int a = 0; a < 3; a++)
+        p.ns[a] = 0;
+    p.nocone = p.nosth = false;
+    p.smin = p.s2 = 1.0;
+    p.lmax = 0.0;
+    for (int i = 0; i < nc; i++) {
+        grow(p.box, ch[i].box);
+        for (int a = 0; a < 3; a++)
+            p.ns[a] += ch[i].ns[a];
+        p.nocone |= ch[i].nocone;
+        p.nosth |= ch[i].nosth;
+        p.smin = std::min(p.smin, ch[i].smin);
+        p.s2 = std::min(p.s2, ch[i].s2);
+        p.lmax = std::max(p.lmax, ch[i].lmax);
+    }
+    q_normal(p);
+    p.tc = p.ts = 0;
+    for (int i = 0; i < nc; i++) {
+        const double d = q_angle(p.nq, ch[i].nq);
+        p.tc = std::max(p.tc, d + ch[i].tc);
+        p.ts = std::max(p.ts, d + ch[i].ts);
+    }
+    // the slab: the range of nq . v over the box's corners (the box holds every vertex below)
+    p.slo = INFINITY;
+    p.shi = -INFINITY;
+    for (int k = 0; k < 8; k++) {
+        const double v0 = (k & 1) ? p.box.hi[0] : p.box.lo[0], v1 = (k & 2) ? p.box.hi[1] : p.box.lo[1],
+                     v2 = (k & 4) ? p.box.hi[2] : p.box.lo[2];
+        const double sv = p.nq[0] * v0 + p.nq[1] * v1 + p.nq[2] * v2;
+        p.slo = std::min(p.slo, sv);
+        p.shi = std::max(p.shi, sv);
+    }
+    p.leaf = -1;
+}
+
+// the node's boxes (quantise's rule), then per child the slab (absolute range shifted to the node's
+// origin, widened by the rounding of that shift), the cone code, the conditioning bytes and rho
+WNode q_node(const QChild* ch, int nc, const FlatOctree& oct)
+{
+    WNode w;
+    std::memset(&w, 0, sizeof(w));
+    Box nb = empty_box();
+    for (int j = 0; j < nc; j++)
+        grow(nb, ch[j].box);
+    const float org[3] = {nb.lo[0], nb.lo[1], nb.lo[2]};
+    w.ox = org[0];
+    w.oy = org[1];
+    w.oz = org[2];
+    for (int a = 0; a < 3; a++) {
+        const double ext = (double)nb.hi[a] - (double)org[a];
+        int k = -100;
+        if (ext > 0) {
+            int e;
+            std::frexp(ext / 255.0, &e);
+            k = std::max(-100, std::min(127, e - 1));
+            while (k < 127 && std::ldexp(255.0, k) < ext)
+                k++;
+        }
+        w.exps |= (uint32_t)(127 + k) << (8 * a);
+        const double st = std::ldexp(1.0, k);
+        for (int j = 0; j < nc; j++) {
+            const double lo = std::floor(((double)ch[j].box.lo[a] - org[a]) / st);
+            const double hi = std::ceil(((double)ch[j].box.hi[a] - org[a]) / st);
+            w.qlo[a][j] = (uint8_t)std::max(0.0, std::min(255.0, lo));
+            w.qhi[a][j] = (uint8_t)std::max(0.0, std::min(255.0, hi));
+        }
+    }
+    for (int j = 0; j < W_WIDTH; j++)
+        w.child[j] = j < nc ? ch[j].link : W_EMPTY;
+    double lo[W_WIDTH], hi[W_WIDTH], lo_all = INFINITY, hi_all = -INFINITY;
+    for (int j = 0; j < nc; j++) {
+        const double sh = (double)ch[j].nq[0] * org[0] + (double)ch[j].nq[1] * org[1] + (double)ch[j].nq[2] * org[2];
+        // |rounding| of the absolute sums and of the shift: a few ulps of the largest magnitude
+        const double slack = 0x1p-48 * (std::fabs(ch[j].slo) + std::fabs(ch[j].shi) + std::fabs(sh) +
+                                        128.0 * (std::fabs((double)org[0]) + std::fabs((double)org[1]) + std::fabs((double)org[2])));
+        lo[j] = ch[j].slo - sh - slack;
+        hi[j] = ch[j].shi - sh + slack;
+        lo_all = std::min(lo_all, lo[j]);
+        hi_all = std::max(hi_all, hi[j]);
+    }
+    const float slo = down(lo_all);
+    const double ext = hi_all - (double)slo;
+    int k = -100;
+    if (ext > 0) {
+        int e;
+        std::frexp(ext / 65535.0, &e);
+        k = std::max(-100, std::min(127, e - 1));
+        while (k < 127 && std::ldexp(65535.0, k) < ext)
+            k++;
+    }
+    const double st = std::ldexp(1.0, k);
+    w.s = (float)st;
+    w.slo = slo;
+    for (int j = 0; j < nc; j++) {
+        const QChild& c = ch[j];
+        // the cone code (cone_code's rule) from the half-angle
+        int code = 255;
+        const double NL = q_len(c.nq);
+        const double psi = std::acos(W_CONE_EPS) - c.tc - 1e-9;
+        if (!c.nocone && psi > 0) {
+            const double cd = std::ceil((std::cos(psi) * NL + 0.01) / ((double)W_CONE_STEP * (1 - 1e-9)));
+            code = cd <= 254 ? (int)cd : 255;
+        }
+        w.nrm[j] = (uint32_t)(uint8_t)(int8_t)c.nq[0] | ((uint32_t)(uint8_t)(int8_t)c.nq[1] << 8) |
+                   ((uint32_t)(uint8_t)(int8_t)c.nq[2] << 16) | ((uint32_t)code << 24);
+        double q0 = std::floor((lo[j] - (double)slo) / st), q1 = std::ceil((hi[j] - (double)slo) / st);
+        q0 = std::max(0.0, std::min(65535.0, q0));
+        q1 = std::max(0.0, std::min(65535.0, q1));
+        w.slab[j] = (uint32_t)q0 | ((uint32_t)q1 << 16);
+        const double sth = c.nosth || c.ts >= M_PI / 2 ? 1.0 : std::min(1.0, std::sin(c.ts) + 1e-12);
+        w.ext[j] = wq_code_lb(c.smin) | (wq_code_lb(c.s2) << 8) | (wq_code_ub(sth, WQ_UNIT) << 16) |
+                   (wq_code_ub(c.lmax, WQ_LEN) << 24);
+        double rho = 0.0;
+        if (c.leaf >= 0) {
+            double dlo[3], dhi[3];
+            decode(w, j, dlo, dhi);
+            const GNode& L = oct.nodes[(size_t)c.leaf];
+            for (int a = 0; a < 3; a++)
+                rho = std::max(rho, std::max(dlo[a] - (double)L.dn[a], (double)L.df[a] - dhi[a]));
+        }
+        w.ext2[j] = wq_code_ub(rho, WQ_LEN);
+    }
+    return w;
+}
+
+}  // namespace
+
+void build_wbvh_quick(const FlatOctree& oct, WBvh& out)
+{
+    const bool prof = std::getenv("RT_BUILD_PROFILE") != nullptr;
+    auto tick = std::chrono::steady_clock::now();
+    auto phase = [&](const char* what) {
+        if (!prof)
+            return;
+        auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[wbvh quick] %-10s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(now - tick).count());
+        tick = now;
+    };
+    out = WBvh();
+    const int64_t n = (int64_t)oct.tris.size();
+    Pool& pool = build_pool();
+    out.leaf_of_slot.assign((size_t)n, 0u);
+    parallel_for(pool, (int64_t)oct.nodes.size(), 4096, [&](int64_t i) {
+        const GNode& g = oct.nodes[(size_t)i];
+        if (g.b & LEAF_BIT)
+            for (uint32_t s = g.a; s < g.a + (g.b & ~LEAF_BIT); s++)
+                out.leaf_of_slot[s] = (uint32_t)i;
+    });
+    if (n == 0 || n >= ((int64_t)1 << 28))
+        return;
+    // wide nodes, planned depth first (the root is node 0; a node's children have higher indices)
+    struct Plan {
+        int nc = 0;
+        int kind[W_WIDTH];      // 0: a run of triangles (first, cnt); 1: a wide node
+        int32_t a[W_WIDTH], b[W_WIDTH];   // run: first, count; node: index, -
+        int32_t leaf[W_WIDTH];  // run: the octree leaf it belongs to (rho), or -1 when the run is the whole leaf
+        int32_t oct = -1;       // the octree node whose axis box the node's parent entry holds (-1: none)
+        int32_t runleaf = -1;   // a node over runs of octree leaf L's triangles: L (its entry's rho against L)
+        int32_t depth = 0;
+    };
+    std::vector<Plan> plans;
+    plans.reserve((size_t)(n / 4 + 16));
+    std::vector<int32_t> order;   // wide order -> slot
+    order.reserve((size_t)n);
+    int32_t maxd = 0;
+    // a 4-ary tree over the runs [first, first + cnt) in runs of 8 of octree leaf L
+    std::function<int32_t(int32_t, int32_t, int32_t, int32_t)> runs = [&](int32_t first, int32_t cnt, int32_t L, int32_t depth) {
+        const int32_t me = (int32_t)plans.size();
+        plans.emplace_back();
+        plans[(size_t)me].depth = depth;
+        plans[(size_t)me].runleaf = L;
+        maxd = std::max(maxd, depth);
+        const int32_t nr = (cnt + W_MAX_LEAF - 1) / W_MAX_LEAF;   // runs
+        // split the runs over up to four children as evenly as possible
+        const int parts = (int)std::min<int32_t>(W_WIDTH, nr);
+        int32_t r0 = 0;
+        for (int p = 0; p < parts; p++) {
+            const int32_t r1 = (int32_t)((int64_t)nr * (p + 1) / parts);
+            const int32_t f = first + r0 * W_MAX_LEAF, c = std::min(cnt, r1 * W_MAX_LEAF) - r0 * W_MAX_LEAF;
+            Plan& P = plans[(size_t)me];
+            const int j = P.nc++;
+            if (r1 - r0 == 1) {
+                P.kind[j] = 0;
+                P.a[j] = f;
+                P.b[j] = c;
+                P.leaf[j] = L;
+            } else {
+                const int32_t child = runs(f, c, L, depth + 1);
+                Plan& Q = plans[(size_t)me];
+                Q.kind[j] = 1;
+                Q.a[j] = child;
+                Q.b[j] = 0;
+                Q.leaf[j] = -1;
+            }
+            r0 = r1;
+        }
+        return me;
+    };
+    // the entry for octree node u: fills (kind, a, b, leaf) of child slot j of plan p
+    std::function<void(int32_t, int32_t, int, int32_t)> entry;
+    std::function<int32_t(int32_t, int32_t)> inner = [&](int32_t u, int32_t depth) {
+        // a wide node for octree inner node u (children c0 .. c0 + cn - 1, up to 8)
+        const GNode& g = oct.nodes[(size_t)u];
+        const int32_t c0 = (int32_t)g.a, cn = (int32_t)g.b;
+        const int32_t me = (int32_t)plans.size();
+        plans.emplace_back();
+        plans[(size_t)me].depth = depth;
+        maxd = std::max(maxd, depth);
+        // direct children and groups: 1-4 direct; 5-7: 3 direct + 1 group; 8: 2 direct + 2 groups of 3
+        int direct = cn <= W_WIDTH ? cn : (cn <= 7 ? 3 : 2);
+        for (int i = 0; i < direct; i++)
+            entry(c0 + i, me, plans[(size_t)me].nc++, depth);
+        int32_t rest = cn - direct, at = c0 + direct;
+        const int groups = rest == 0 ? 0 : (cn <= 7 ? 1 : 2);
+        for (int gi = 0; gi < groups; gi++) {
+            const int32_t gs = gi == groups - 1 ? rest : (rest + 1) / 2;
+            const int32_t gnode = (int32_t)plans.size();
+            plans.emplace_back();
+            plans[(size_t)gnode].depth = depth + 1;
+            maxd = std::max(maxd, depth + 1);
+            for (int32_t i = 0; i < gs; i++)
+                entry(at + i, gnode, plans[(size_t)gnode].nc++, depth + 1);
+            Plan& P = plans[(size_t)me];
+            const int j = P.nc++;
+            P.kind[j] = 1;
+            P.a[j] = gnode;
+            P.b[j] = 0;
+            P.leaf[j] = -1;
+            at += gs;
+            rest -= gs;
+        }
+        return me;
+    };
+    entry = [&](int32_t u, int32_t p, int j, int32_t depth) {
+        const GNode& g = oct.nodes[(size_t)u];
+        if (g.b & LEAF_BIT) {
+            const int32_t cnt = (int32_t)(g.b & ~LEAF_BIT), first = (int32_t)order.size();
+            for (int32_t s = 0; s < cnt; s++)
+                order.push_back((int32_t)g.a + s);
+            if (cnt <= W_MAX_LEAF) {
+                Plan& P = plans[(size_t)p];
+                P.kind[j] = 0;
+                P.a[j] = first;
+                P.b[j] = cnt;
+                P.leaf[j] = u;
+            } else {
+                const int32_t child = runs(first, cnt, u, depth + 1);
+                Plan& P = plans[(size_t)p];
+                P.kind[j] = 1;
+                P.a[j] = child;
+                P.b[j] = 0;
+                P.leaf[j] = -1;
+                plans[(size_t)child].oct = u;   // (the runs' node holds the leaf's axis box: rho = 0 above it)
+            }
+        } else {
+            const int32_t child = inner(u, depth + 1);
+            Plan& P = plans[(size_t)p];
+            P.kind[j] = 1;
+            P.a[j] = child;
+            P.b[j] = 0;
+            P.leaf[j] = -1;
+            plans[(size_t)child].oct = u;
+        }
+    };
+    if (oct.nodes[0].b & LEAF_BIT) {
+        // a single leaf: one node over its runs (with one run, a node with one leaf child)
+        const GNode& g = oct.nodes[0];
+        const int32_t cnt = (int32_t)(g.b & ~LEAF_BIT);
+        for (int32_t s = 0; s < cnt; s++)
+            order.push_back((int32_t)g.a + s);
+        runs(0, cnt, 0, 0);
+        plans[0].oct = 0;
+    } else {
+        inner(0, 0);
+        plans[0].oct = 0;
+    }
+    phase("plan");
+    if ((int64_t)order.size() != n)
+        return;   // (cannot happen: every slot is in one leaf)
+    out.tris.resize((size_t)n);
+    out.slot.resize((size_t)n);
+    out.leaf_of_k.resize((size_t)n);
+    parallel_for(pool, n, 8192, [&](int64_t k) {
+        const int32_t s = order[(size_t)k];
+        out.tris[(size_t)k] = oct.tris[(size_t)s];
+        out.slot[(size_t)k] = s;
+        out.leaf_of_k[(size_t)k] = out.leaf_of_slot[(size_t)s];
+    });
+    phase("order");
+    // geometry, deepest nodes first (each level in parallel): a node's children are complete when it runs
+    const size_t np = plans.size();
+    out.nodes.resize(np);
+    std::vector<QChild> agg(np);   // each node as its parent's child
+    std::vector<std::vector<int32_t>> by_depth((size_t)maxd + 1);
+    for (size_t w = 0; w < np; w++)
+        by_depth[(size_t)plans[w].depth].push_back((int32_t)w);
+    for (int32_t d = maxd; d >= 0; d--) {
+        const std::vector<int32_t>& lv = by_depth[(size_t)d];
+        parallel_for(pool, (int64_t)lv.size(), 64, [&](int64_t q) {
+            const int32_t w = lv[(size_t)q];
+            const Plan& P = plans[(size_t)w];
+            QChild ch[W_WIDTH];
+            for (int j = 0; j < P.nc; j++) {
+                if (P.kind[j] == 0) {
+                    q_from_tris(ch[j], out.tris.data(), P.a[j], P.b[j]);
+                    ch[j].link = W_LEAF | ((uint32_t)P.a[j] << 3) | (uint32_t)(P.b[j] - 1);
+                    ch[j].leaf = P.leaf[j];
+                } else {
+                    ch[j] = agg[(size_t)P.a[j]];
+                    ch[j].link = (uint32_t)P.a[j];
+                }
+            }
+            out.nodes[(size_t)w] = q_node(ch, P.nc, oct);
+            // the node's entry in its parent holds the axis boxes of the octree leaves below (rho = 0
+            // there): its octree node's, and those of its leaf-run children (their record boxes can sit
+            // an ulp inside the leaf's k-DOP, which the original vertices set)
+            Box ax = empty_box();
+            auto axis = [&](int32_t u) {
+                const GNode& g = oct.nodes[(size_t)u];
+                Box b;
+                for (int a = 0; a < 3; a++) {
+                    b.lo[a] = g.dn[a];
+                    b.hi[a] = g.df[a];
+                }
+                grow(ax, b);
+            };
+            if (P.oct >= 0)
+                axis(P.oct);
+            for (int j = 0; j < P.nc; j++)
+                if (P.kind[j] == 0 && P.leaf[j] >= 0)
+                    axis(P.leaf[j]);
+            q_combine(agg[(size_t)w], ch, P.nc, &ax);
+            agg[(size_t)w].leaf = P.runleaf;   // (0 reach for the top one: it holds the leaf's axis box)
+        });
+    }
+    phase("geometry");
+    // the risk walk's links
+    out.tri_leaf.assign((size_t)n, W_EMPTY);
+    out.parent.assign(np, W_EMPTY);
+    parallel_for(pool, (int64_t)np, 256, [&](int64_t w) {
+        const WNode& WN = out.nodes[(size_t)w];
+        for (int j = 0; j < W_WIDTH; j++) {
+            const uint32_t c = WN.child[j];
+            const uint32_t e = (uint32_t)w << 2 | (uint32_t)j;
+            if (c == W_EMPTY)
+                continue;
+            if (c & W_LEAF) {
+                const uint32_t first = (c >> 3) & 0x0FFFFFFFu, cnt = (c & 7u) + 1u;
+                for (uint32_t k = first; k < first + cnt; k++)
+                    out.tri_leaf[k] = e;
+            } else
+                out.parent[c] = e;
+        }
+    });
+    int64_t leaves = 0, maxleaf = 0;
+    for (const Plan& P : plans)
+        for (int j = 0; j < P.nc; j++)
+            if (P.kind[j] == 0) {
+                leaves++;
+                maxleaf = std::max<int64_t>(maxleaf, P.b[j]);
+            }
+    out.stats.nodes = (int64_t)np;
+    out.stats.leaves = leaves;
+    out.stats.max_leaf = maxleaf;
+    out.stats.depth = maxd + 1;
+    out.stats.tris = n;
+    phase("links");
+}
+
 // The conditioning bytes of child j of node N (WNode::ext / ext2, read as the query's values:
 // wq_val, a code 0 being 0) against wide-BVH triangle k below it, recomputed independently of the
 // build in x87 long double (64-bit significands: the products of float coordinates are exact, each
@@ -1147,6 +1621,16 @@ void build_wbvh(const FlatOctree& oct, WBvh& out)
 // The slack 2^-60 on the sines is far below every build margin (sin_at_a_lb subtracts 2^-50).
 // Records whose stored normal is 0 never report a hit (Mdet = 0) and need no bound.  Returns the
 // number of violated bounds.
+// (RT_CHECK_VERBOSE=1: each violation's source line on stderr, the first 40)
+static void w_viol_note(int line)
+{
+    static const bool on = std::getenv("RT_CHECK_VERBOSE") != nullptr;
+    static std::atomic<int> shown{0};
+    if (on && shown.fetch_add(1) < 40)
+        fprintf(stderr, "[check_wbvh] violation at wbvh.cpp:%d\n", line);
+}
+#define W_VIOL() (bad++, w_viol_note(__LINE__))
+
 static int64_t check_conditioning(const FlatOctree& oct, const WBvh& w, const WNode& N, int j, uint32_t k)
 {
     const GTri& t = w.tris[k];
@@ -1162,8 +1646,12 @@ static int64_t check_conditioning(const FlatOctree& oct, const WBvh& w, const WN
         decode(N, j, lo, hi);
         const GNode& OL = oct.nodes[w.leaf_of_k[k]];
         for (int a = 0; a < 3; a++)
-            if (!((long double)OL.dn[a] >= (long double)lo[a] - rho && (long double)OL.df[a] <= (long double)hi[a] + rho))
-                bad++;
+            if (!((long double)OL.dn[a] >= (long double)lo[a] - rho && (long double)OL.df[a] <= (long double)hi[a] + rho)) {
+                W_VIOL();
+                if (std::getenv("RT_CHECK_VERBOSE"))
+                    fprintf(stderr, "  rho: node %ld child %d (link %08x) tri %u leaf %u axis %d: leaf [%.9g, %.9g] box [%.9g, %.9g] rho %.3Lg\n",
+                            (long)(&N - w.nodes.data()), j, N.child[j], k, w.leaf_of_k[k], a, OL.dn[a], OL.df[a], lo[a], hi[a], rho);
+            }
     }
     if (t.n[0] == 0.0f && t.n[1] == 0.0f && t.n[2] == 0.0f)
         return bad;
@@ -1172,25 +1660,25 @@ static int64_t check_conditioning(const FlatOctree& oct, const WBvh& w, const WN
     const long double la = sqrtl(x0 * x0 + x1 * x1 + x2 * x2), lc = sqrtl(y0 * y0 + y1 * y1 + y2 * y2);
     const long double cl = sqrtl(c0 * c0 + c1 * c1 + c2 * c2);
     if (!(L >= fmaxl(la, lc)))
-        bad++;
+        W_VIOL();
     if (la > 0 && lc > 0) {
         const long double sa = cl / (la * lc);
         if (!(smin <= sa + 0x1p-60L))
-            bad++;
+            W_VIOL();
         const long double ca = fabsl(x0 * y0 + x1 * y1 + x2 * y2) / (la * lc);
         if (!(s2 <= sqrtl(fmaxl(0.0L, (1.0L - ca) / 2.0L) + 0x1p-60L)))
-            bad++;
+            W_VIOL();
     } else if (smin > 0 || s2 > 0)
-        bad++;
+        W_VIOL();
     const long double N0 = (int8_t)(N.nrm[j] & 0xffu), N1 = (int8_t)((N.nrm[j] >> 8) & 0xffu),
                       N2 = (int8_t)((N.nrm[j] >> 16) & 0xffu);
     const long double NL = sqrtl(N0 * N0 + N1 * N1 + N2 * N2);
     const long double cs = cl > 0 && NL > 0 ? (c0 * N0 + c1 * N1 + c2 * N2) / (cl * NL) : -1.0L;
     if (cs > 0) {
         if (!(sth >= sqrtl(fmaxl(0.0L, 1.0L - cs * cs)) - 0x1p-60L))
-            bad++;
+            W_VIOL();
     } else if (!(sth >= 1.0L))
-        bad++;
+        W_VIOL();
     return bad;
 }
 
@@ -1214,7 +1702,7 @@ int64_t check_risk_words(const FlatOctree& oct, const WBvh& w, const WRiskArgs& 
             const int j = (int)(e & 3u);
             const uint64_t word = risk[(2 * (size_t)(e >> 2) + sel) * W_WIDTH + j];
             if (!(wrisk_key(word) <= Kt))
-                bad++;
+                W_VIOL();
             // the at-risk box (in the node's frame) widened by rho holds the triangle's octree leaf
             const double org[3] = {N.ox, N.oy, N.oz};
             const double rho = wq_len(N.ext2[j] & 0xffu);
@@ -1223,7 +1711,7 @@ int64_t check_risk_words(const FlatOctree& oct, const WBvh& w, const WRiskArgs& 
                 const double lo = org[a] + (double)((word >> (8 * a)) & 0xffu) * st;
                 const double hi = org[a] + (double)((word >> (8 * (a + 3))) & 0xffu) * st;
                 if (!((double)OL.dn[a] >= lo - rho && (double)OL.df[a] <= hi + rho))
-                    bad++;
+                    W_VIOL();
             }
         }
     }
@@ -1238,22 +1726,22 @@ int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)
         return 1;
     for (size_t k = 0; k < n; k++)
         if (w.slot[k] >= 0 && (size_t)w.slot[k] < n && w.leaf_of_k[k] != w.leaf_of_slot[(size_t)w.slot[k]])
-            bad++;
+            W_VIOL();
     if (n == 0)
         return w.nodes.empty() ? 0 : 1;
     std::vector<uint8_t> seen(n, 0), used(w.tris.size(), 0);
     for (size_t i = 0; i < n; i++) {
         int32_t s = w.slot[i];
         if (s < 0 || (size_t)s >= n || seen[(size_t)s]++)
-            bad++;
+            W_VIOL();
         else if (std::memcmp(&w.tris[i], &oct.tris[(size_t)s], sizeof(GTri)))
-            bad++;
+            W_VIOL();
     }
     for (size_t s = 0; s < n; s++) {
         uint32_t L = w.leaf_of_slot[s];
         if (L >= oct.nodes.size() || !(oct.nodes[L].b & LEAF_BIT) || s < oct.nodes[L].a ||
             s >= oct.nodes[L].a + (oct.nodes[L].b & ~LEAF_BIT))
-            bad++;
+            W_VIOL();
     }
     // the risk walk's links: each triangle's leaf entry names it, each node's parent entry names it,
     // and every walk reaches the root
@@ -1262,18 +1750,18 @@ int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)
     for (size_t k = 0; k < n; k++) {
         const uint32_t e = w.tri_leaf[k];
         if (e == W_EMPTY || (e >> 2) >= w.nodes.size()) {
-            bad++;
+            W_VIOL();
             continue;
         }
         const uint32_t c = w.nodes[e >> 2].child[e & 3u];
         const uint32_t first = (c >> 3) & 0x0FFFFFFFu, cnt = (c & 7u) + 1u;
         if (c == W_EMPTY || !(c & W_LEAF) || k < first || k >= first + cnt)
-            bad++;
+            W_VIOL();
     }
     for (size_t v = 1; v < w.nodes.size(); v++) {
         const uint32_t e = w.parent[v];
         if (e == W_EMPTY || (e >> 2) >= w.nodes.size() || w.nodes[e >> 2].child[e & 3u] != (uint32_t)v)
-            bad++;
+            W_VIOL();
     }
     // every child box holds its subtree: node boxes and triangle vertices (a, a + ab, a + ac);
     // every slab and cone on the path holds each triangle below (checked at the leaves)
@@ -1305,14 +1793,14 @@ int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)
         if (it.ref & W_LEAF) {
             uint32_t first = (it.ref >> 3) & 0x0FFFFFFFu, cnt = (it.ref & 7u) + 1u;
             if ((size_t)first + cnt > n) {
-                bad++;
+                W_VIOL();
                 continue;
             }
             for (uint32_t k = first; k < first + cnt; k++) {
                 if (used[k]++)
-                    bad++;
+                    W_VIOL();
                 if (!inside(tri_box(w.tris[k]), it.box))
-                    bad++;
+                    W_VIOL();
                 const GTri& T = w.tris[k];
                 for (int q = 0; q < it.np; q++) {
                     const WNode& N = w.nodes[it.path[q] >> 3];
@@ -1327,7 +1815,7 @@ int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)
                         for (int a = 0; a < 3; a++)
                             sp += nv[a] * ((double)T.a[a] + (v == 1 ? (double)T.ab[a] : v == 2 ? (double)T.ac[a] : 0.0) - org[a]);
                         if (!(sp >= lo && sp <= hi))
-                            bad++;
+                            W_VIOL();
                     }
                     bad += check_conditioning(oct, w, N, j, k);
                     const uint32_t code = N.nrm[j] >> 24;
@@ -1341,14 +1829,14 @@ int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)
                         const double ang = std::acos(std::max(-1.0, std::min(1.0, c)));
                         if (!(nn > 1e-30 && nn < 1e27) || !(kap > -1.0) ||
                             !(std::acos(std::min(1.0, kap)) + ang < std::acos(W_CONE_EPS)))
-                            bad++;
+                            W_VIOL();
                     }
                 }
             }
             continue;
         }
         if (it.ref >= w.nodes.size() || ++visited > w.nodes.size()) {
-            bad++;
+            W_VIOL();
             continue;
         }
         const WNode& N = w.nodes[it.ref];
@@ -1367,7 +1855,7 @@ int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)
                 ch.box.hi[a] = std::min(cb.hi[a], it.box.hi[a]);
             }
             if (ch.np >= MAXP) {
-                bad++;
+                W_VIOL();
                 continue;
             }
             ch.path[ch.np++] = (it.ref << 3) | (uint32_t)j;
@@ -1376,7 +1864,7 @@ int64_t check_wbvh(const FlatOctree& oct, const WBvh& w)
     }
     for (size_t k = 0; k < n; k++)
         if (!used[k])
-            bad++;
+            W_VIOL();
     return bad;
 }
 

@@ -235,6 +235,10 @@ inline float sin_at_a_f(const GTri& t)
 // (RT_BUILD_THREADS threads, as the octree build).  Boxes are the records' vertices a,
 // a + ab, a + ac rounded outward to float.
 void build_wbvh(const FlatOctree& oct, WBvh& out);
+// The quick tree (r05, wbvh.cpp): the octree's own hierarchy as the wide BVH, O(n) to build, for the
+// frames right after a geometry change while the SAH tree builds; RT_WBVH_QUICK=1 makes
+// build_wbvh build it instead.
+void build_wbvh_quick(const FlatOctree& oct, WBvh& out);
 
 // Structural check (CPU tests): every octree slot exactly once, each child box holds its
 // subtree's boxes / its triangles' vertices, leaf sizes within W_MAX_LEAF, leaf_of_slot
