@@ -883,7 +883,7 @@ int Renderer::ensure_device_scene()
         wb_ = WBvh();
         if (quick) {
             auto tq = clk::now();
-            build_wbvh_quick(oct_, wb_);
+            build_wbvh_quick(oct_, wb_, false);   // (records gathered on the device)
             build_split_ms_[2] = ms_since(tq);
             if (!wb_.nodes.empty())
                 e = upload_wide(wb_, d_wnodes_, d_wtris_, d_wmeta_, d_wtmp_, d_wlinks_, stream_);
@@ -2107,6 +2107,8 @@ int Renderer::risk_words(int src, uint64_t* out, int64_t cap, int64_t* count, in
             (e = hipStreamSynchronize(stream_)) != hipSuccess)
             return hip_fail(e, "download (risk words)");
     }
+    if (wb_.tris.size() != wb_.slot.size())
+        wbvh_fill_tris(oct_, wb_);   // (the quick tree keeps no host copy of the records)
     const float lo[3] = {oct_root_.dn[0], oct_root_.dn[1], oct_root_.dn[2]};
     const float hi[3] = {oct_root_.df[0], oct_root_.df[1], oct_root_.df[2]};
     const WRiskArgs A = wbvh_risk_args(lo, hi, P.scene_scale, P.cam_pos, P.light, W_QS_CLOSEST, W_QS_SHADOW);

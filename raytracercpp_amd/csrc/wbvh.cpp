@@ -964,6 +964,13 @@ void build_two_level(const FlatOctree& oct, std::vector<Prim, DefaultInitAlloc<P
 
 }  // namespace
 
+void wbvh_fill_tris(const FlatOctree& oct, WBvh& w)
+{
+    const int64_t n = (int64_t)w.slot.size();
+    w.tris.resize((size_t)n);
+    parallel_for(build_pool(), n, 8192, [&](int64_t k) { w.tris[(size_t)k] = oct.tris[(size_t)w.slot[(size_t)k]]; });
+}
+
 void build_wbvh(const FlatOctree& oct, WBvh& out)
 {
     if (const char* q = std::getenv("RT_WBVH_QUICK"))
@@ -1183,22 +1190,24 @@ inline double q_angle(const int* a, const int* b)
     return std::acos(std::max(-1.0, std::min(1.0, c))) + 1e-7;
 }
 
-// a run of triangles [first, first + cnt) of the wide order: everything from the triangles themselves
-void q_from_tris(QChild& c, const GTri* t, int32_t first, int32_t cnt)
+// a run of triangles [first, first + cnt) of the wide order (record i: t[map[i]]): everything from the
+// triangles themselves
+void q_from_tris(QChild& c, const GTri* t, const int32_t* map, int32_t first, int32_t cnt)
 {
     c.box = empty_box();
     for (int a = 0; a < 3; a++)
         c.ns[a] = 0;
     for (int32_t i = first; i < first + cnt; i++) {
-        grow(c.box, tri_box(t[i]));
+        const GTri& T = t[map[i]];
+        grow(c.box, tri_box(T));
         for (int a = 0; a < 3; a++)
-            c.ns[a] += (double)t[i].n[a];
+            c.ns[a] += (double)T.n[a];
     }
     q_normal(c);
     const double n0 = c.nq[0], n1 = c.nq[1], n2 = c.nq[2], NL = q_len(c.nq);
     double cmin = 1.0, smn = 1.0;   // stored normals (cone), exact normals (sth)
     for (int32_t i = first; i < first + cnt; i++) {
-        const GTri& T = t[i];
+        const GTri& T = t[map[i]];
         const double a0 = T.a[0], a1 = T.a[1], a2 = T.a[2];
         const double s0 = n0 * a0 + n1 * a1 + n2 * a2;
         const double s1 = n0 * (a0 + (double)T.ab[0]) + n1 * (a1 + (double)T.ab[1]) + n2 * (a2 + (double)T.ab[2]);
@@ -1365,7 +1374,7 @@ WNode q_node(const QChild* ch, int nc, const FlatOctree& oct)
 
 }  // namespace
 
-void build_wbvh_quick(const FlatOctree& oct, WBvh& out)
+void build_wbvh_quick(const FlatOctree& oct, WBvh& out, bool tris)
 {
     const bool prof = std::getenv("RT_BUILD_PROFILE") != nullptr;
     auto tick = std::chrono::steady_clock::now();
@@ -1517,15 +1526,15 @@ void build_wbvh_quick(const FlatOctree& oct, WBvh& out)
     phase("plan");
     if ((int64_t)order.size() != n)
         return;   // (cannot happen: every slot is in one leaf)
-    out.tris.resize((size_t)n);
     out.slot.resize((size_t)n);
     out.leaf_of_k.resize((size_t)n);
     parallel_for(pool, n, 8192, [&](int64_t k) {
         const int32_t s = order[(size_t)k];
-        out.tris[(size_t)k] = oct.tris[(size_t)s];
         out.slot[(size_t)k] = s;
         out.leaf_of_k[(size_t)k] = out.leaf_of_slot[(size_t)s];
     });
+    if (tris)
+        wbvh_fill_tris(oct, out);
     phase("order");
     // geometry, deepest nodes first (each level in parallel): a node's children are complete when it runs
     const size_t np = plans.size();
@@ -1542,7 +1551,7 @@ void build_wbvh_quick(const FlatOctree& oct, WBvh& out)
             QChild ch[W_WIDTH];
             for (int j = 0; j < P.nc; j++) {
                 if (P.kind[j] == 0) {
-                    q_from_tris(ch[j], out.tris.data(), P.a[j], P.b[j]);
+                    q_from_tris(ch[j], oct.tris.data(), out.slot.data(), P.a[j], P.b[j]);
                     ch[j].link = W_LEAF | ((uint32_t)P.a[j] << 3) | (uint32_t)(P.b[j] - 1);
                     ch[j].leaf = P.leaf[j];
                 } else {

@@ -238,7 +238,10 @@ void build_wbvh(const FlatOctree& oct, WBvh& out);
 // The quick tree (r05, wbvh.cpp): the octree's own hierarchy as the wide BVH, O(n) to build, for the
 // frames right after a geometry change while the SAH tree builds; RT_WBVH_QUICK=1 makes
 // build_wbvh build it instead.
-void build_wbvh_quick(const FlatOctree& oct, WBvh& out);
+// tris = false: WBvh::tris left empty (the renderer gathers the records on the device; wbvh_fill_tris
+// makes the host copy when a host check needs it).
+void build_wbvh_quick(const FlatOctree& oct, WBvh& out, bool tris = true);
+void wbvh_fill_tris(const FlatOctree& oct, WBvh& w);
 
 // Structural check (CPU tests): every octree slot exactly once, each child box holds its
 // subtree's boxes / its triangles' vertices, leaf sizes within W_MAX_LEAF, leaf_of_slot

@@ -1,5 +1,7 @@
-"""Frame-engine invariants on the GPU (ADVICE r04): the risk words' event survives the caller's
-stream, and the heavy-tiles-first order traces every tile exactly once.  Reference path:
+"""Frame-engine invariants on the GPU (ADVICE r04, r05): the risk words' event survives the caller's
+stream; the heavy-tiles-first order and the split tiles (4 parts, lane groups) trace every tile exactly
+once, C4 included; hair1m frames; the reflection engine's long-query deferral on and off; camera and
+light moves after the SAH tree is resident.  Every frame is compared with the oracle.  Reference path:
 Renderer::ray_trace (renderer.cpp:1068-1116), whose rows and tiles are independent."""
 import ctypes
 
@@ -191,3 +193,58 @@ def test_hair1m_frame_matches_oracle(make_renderer, camera):
         R.finish_accel()
     print(f"hair1m {camera}: {int((o.hit_id >= 0).sum())} of {o.hit_id.size} pixels hit, "
           f"{o.counters['shadow_rays']} shadow rays")
+
+
+@pytest.mark.parametrize("defer", ["48", "0", "6"])
+def test_reflection_deferral_matches_oracle(make_renderer, defer):
+    """The reflection engine's long-query deferral (RT_REFL_DEFER=k: queries past k loop iterations of
+    refl_trace_kernel finish in refl_trace_long_kernel; 0: never deferred) changes only where a query
+    runs: C5's features at a reduced size, first on the quick wide BVH (the frame right after the scene
+    load), then on the SAH tree, equal the oracle bit for bit."""
+    from raytracercpp_amd import scenes
+    sc, st = scenes.sphere1m_refl(width=64, height=36, samples=4)
+    st = st.copy(max_recursion_depth=3)
+    o = Oracle(sc, st).render_rows()
+    R = make_renderer(RT_REFL_DEFER=defer)
+    R.load_scene(sc, st)
+    R.request_aux(hit=True, shadow=True)
+    for frame in ("quick tree", "SAH tree"):
+        R.ray_trace()
+        g = R.get_internal(argb=True, hit=True, shadow=True)
+        assert np.array_equal(g["hit_id"], o.hit_id), frame
+        assert np.array_equal(g["shadow"], o.shadow), frame
+        assert np.array_equal(g["argb"], o.argb), f"{frame}: {int((g['argb'] != o.argb).sum())} ARGB mismatches"
+        assert R.stats()["reflection_rays"] == o.counters["reflection_rays"], frame
+        R.finish_accel()
+
+
+def test_camera_and_light_moves_after_finish_accel(make_renderer):
+    """After the SAH tree is resident (rt_finish_accel), the camera and the light move between frames
+    (new camera / light risk words each time, Renderer::prepare_risk): every frame equals the oracle's
+    for its own camera and light."""
+    from raytracercpp_amd import _lib, scenes
+    from raytracercpp_amd.scene import SceneData
+    sc, st = scenes.bumpy70k(width=160, height=96)
+    R = make_renderer()
+    R.load_scene(sc, st)
+    R.ray_trace()
+    R.finish_accel()
+    R.request_aux(hit=True, shadow=True)
+    moves = [(None, (2.0, 4.0, 1.0)), (_lib.make_transform("ry", 12), None), (_lib.make_transform("rx", -8), (-3.0, 2.0, 2.0)),
+             (_lib.compose(_lib.make_transform("translation", 0.3, -0.2, 0.4), _lib.make_transform("rz", 5)), None)]
+    light = np.asarray(sc.light, np.float32)
+    for k, (cam, L) in enumerate(moves):
+        if cam is not None:
+            R.set_camera_transform(cam)
+        if L is not None:
+            R.set_light_position(L)
+            light = np.asarray(L, np.float32)
+        R.ray_trace()
+        g = R.get_internal(argb=True, hit=True, shadow=True)
+        sc2 = SceneData(**vars(sc))
+        sc2.cam_pos, sc2.proj_inv, sc2.cam_to_world = R.get_camera_matrices()
+        sc2.light = light
+        o = Oracle(sc2, st).render_rows()
+        assert np.array_equal(g["hit_id"], o.hit_id), k
+        assert np.array_equal(g["shadow"], o.shadow), k
+        assert np.array_equal(g["argb"], o.argb), k
