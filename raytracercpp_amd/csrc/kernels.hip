@@ -1866,25 +1866,25 @@ __device__ __forceinline__ void set_wave_prio(int level)
 // lane active; the f x f blocks (f = 1 << P.ds_shift, f | 8, rows f-aligned in the band)
 // are summed per 8-bit channel across lanes, divided by f * f with truncation (the sums
 // are non-negative: a shift) and written by the block's first lane, as downscale_kernel.
-// G > 1 (trace_split_part): pixel i of the wave's rows is held by lanes G i .. G i + G - 1
-// (8 / G rows of the tile; f <= 8 / G).
-template <int G = 1>
+// G > 1 (trace_split_part): pixel i of the wave's C-wide block is held by lanes G i .. G i + G - 1
+// (f <= the block's columns and rows, checked on the host).
+template <int G = 1, int C = 8>
 __device__ __forceinline__ void downscale_tile(const KParams& P, int lane, int lr, int px, uint32_t c)
 {
     int r = (int)((c >> 16) & 0xffu), g = (int)((c >> 8) & 0xffu), b = (int)(c & 0xffu);
     const int f = 1 << P.ds_shift;
-    for (int m = 1; m < f; m <<= 1) {   // columns, within the lane's row of 8
+    for (int m = 1; m < f; m <<= 1) {   // columns, within the lane's row of C
         r += __shfl_xor(r, G * m);
         g += __shfl_xor(g, G * m);
         b += __shfl_xor(b, G * m);
     }
-    for (int m = 8; m < 8 * f; m <<= 1) {   // rows
+    for (int m = C; m < C * f; m <<= 1) {   // rows
         r += __shfl_xor(r, G * m);
         g += __shfl_xor(g, G * m);
         b += __shfl_xor(b, G * m);
     }
-    const int pl = lane / G;   // the lane's pixel: 8 row + column
-    if ((lane & (G - 1)) == 0 && (pl & (f - 1)) == 0 && ((pl >> 3) & (f - 1)) == 0) {
+    const int pl = lane / G;   // the lane's pixel: C row + column
+    if ((lane & (G - 1)) == 0 && ((pl % C) & (f - 1)) == 0 && ((pl / C) & (f - 1)) == 0) {
         const int s2 = 2 * P.ds_shift;
         P.ds_out[(size_t)(lr >> P.ds_shift) * (size_t)(P.rw >> P.ds_shift) + (size_t)(px >> P.ds_shift)] =
             qrgb(r >> s2, g >> s2, b >> s2);
@@ -1938,9 +1938,11 @@ __device__ __forceinline__ void trace_split_part(const KParams& P, uint2* lv, in
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     int tx, ty;
     tile_xy(P, tile, tx, ty);
-    const int pl = lane / G;   // the lane's pixel among the part's 64 / G
-    const int px = tx * 8 + (pl & 7);
-    const int lr = ty * 8 + part * (8 / G) + (pl >> 3);
+    // part p: columns (p % (8 / C)) C .. + C, rows (p / (8 / C)) R .. + R of the tile (C x R = 64 / G pixels)
+    constexpr int C = G == 8 ? 4 : 8, R = 64 / G / C;
+    const int pl = lane / G;   // the lane's pixel among the part's, row-major C wide
+    const int px = tx * 8 + (part % (8 / C)) * C + pl % C;
+    const int lr = ty * 8 + (part / (8 / C)) * R + pl / C;
     const int py = lr < P.local_rows ? global_row(P, lr) : P.rh;
     if (px < P.rw && py < P.rh) {   // (the same for the G lanes of a pixel)
         const v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
@@ -1951,7 +1953,7 @@ __device__ __forceinline__ void trace_split_part(const KParams& P, uint2* lv, in
             nshadow += ns;   // (one count per pixel)
         const size_t o = (size_t)lr * P.rw + px;
         const uint32_t c = color_to_argb(po.color);
-        if (P.ds_out) downscale_tile<G>(P, lane, lr, px, c);
+        if (P.ds_out) downscale_tile<G, C>(P, lane, lr, px, c);
         if ((lane & (G - 1)) == 0) {
             if (P.argb) P.argb[o] = c;
             if (P.rgba) P.rgba[o] = make_float4(po.color.r, po.color.g, po.color.b, po.alpha);
@@ -2001,15 +2003,15 @@ __global__ __launch_bounds__(BLOCK, OCT ? RT_OCC_OCT : PLAIN ? RT_OCC_PLAIN : RT
         asm volatile("" : "+s"(kpl));   // (the loop's loads depend on it: not hoisted)
         const KParams& P = *reinterpret_cast<const KParams*>((const void*)kpl);
         const v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
-        if (PLAIN && !REFL && !OCT && P.heavy_group == 4 &&
+        if (PLAIN && !REFL && !OCT && P.heavy_group == SPLIT_G &&
             !__builtin_amdgcn_readfirstlane(__hip_atomic_load(&g_bq.split_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) {
             // the split tiles' parts first (trace_split_part)
             int t = 0;
             if (lane == 0)
                 t = atomicAdd(P.heavy_ctr + 2, 1);
             t = __builtin_amdgcn_readfirstlane(t);
-            if (t < 4 * ldg(P.heavy_ctr + 3)) {
-                trace_split_part<4>(P, lv, t, lane, nshadow);
+            if (t < SPLIT_G * ldg(P.heavy_ctr + 3)) {
+                trace_split_part<SPLIT_G>(P, lv, t, lane, nshadow);
                 continue;
             }
             if (lane == 0)

@@ -9,6 +9,16 @@
 
 namespace rt {
 
+// The split tiles' lane-group size G (kernels.hip trace_split_part; one instantiation in the plain
+// kernel): a part is SPLIT_COLS x SPLIT_ROWS = 64 / G pixels of its 8 x 8 tile
+#ifndef RT_SPLIT_G
+#define RT_SPLIT_G 4
+#endif
+constexpr int SPLIT_G = RT_SPLIT_G;
+constexpr int SPLIT_COLS = SPLIT_G == 8 ? 4 : 8;
+constexpr int SPLIT_ROWS = 64 / SPLIT_G / SPLIT_COLS;
+static_assert(SPLIT_G == 2 || SPLIT_G == 4 || SPLIT_G == 8, "2, 4 or 8 lanes per pixel");
+
 constexpr int TEX_SLOTS = 6;   // ao, diffuse, normal, displacement, roughness, skysphere (renderer.h:77-84)
 constexpr int MAT_STRIDE = 16; // see include/rt_mi355x.h
 constexpr int MAX_SHAPES = 64;
@@ -114,9 +124,9 @@ struct KParams {
     const int32_t* heavy_list;
     const uint32_t* heavy_bits;
     int32_t* heavy_ctr;
-    // 0: ray_trace_kernel dequeues the heavy list; G > 1: ray_trace_heavy_kernel<G> traces the listed
-    // tiles before it (each tile as G parts of 8 / G rows, G lanes per pixel, by the ticket heavy_ctr[2];
-    // the parts add their cycles to tile_cost) and ray_trace_kernel skips them
+    // 0: no split tiles; RT_SPLIT_G: heavy_prep_kernel's split tiles are traced first, each as G parts of
+    // 64 / G pixels with G lanes per pixel (kernels.hip trace_split_part, by the ticket heavy_ctr[2]; the
+    // parts add their cycles to tile_cost)
     int32_t heavy_group;
 
     // outputs, indexed by local_row * rw + px (nullptr = not requested)

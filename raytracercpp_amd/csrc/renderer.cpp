@@ -117,7 +117,7 @@ Knobs Knobs::from_env()
     k.heavy = on("RT_HEAVY_FIRST", true);
     if (const char* v = getenv("RT_HEAVY_GROUP")) {
         const int g = atoi(v);
-        k.heavy_group = g == 4 ? g : 0;
+        k.heavy_group = g > 1 ? SPLIT_G : 0;   // (the split's group size is the build's, kparams.hpp RT_SPLIT_G)
     }
     if (const char* v = getenv("RT_HEAVY_SPLIT"))
         k.heavy_split = std::max(0.0f, (float)atof(v));
@@ -881,10 +881,8 @@ int Renderer::ensure_device_scene()
         const bool quick = e == hipSuccess && s_.enable_bvh && knobs_.quick_wbvh && knobs_.wbvh && !knobs_.exact &&
                            oct_nn_ > 0;
         wb_ = WBvh();
-        if (quick) {
-            auto tq = clk::now();
+        if (quick) {   // (its time counts in build_ms, the blocking part; build_split_ms[2] is the SAH tree's)
             build_wbvh_quick(oct_, wb_, false);   // (records gathered on the device)
-            build_split_ms_[2] = ms_since(tq);
             if (!wb_.nodes.empty())
                 e = upload_wide(wb_, d_wnodes_, d_wtris_, d_wmeta_, d_wtmp_, d_wlinks_, stream_);
         }
@@ -906,8 +904,8 @@ int Renderer::ensure_device_scene()
             risk_nodes_ = (int64_t)wb_.nodes.size();
             risk_tris_ = (int64_t)wb_.tri_leaf.size();
             ++accel_ver_;
-        } else
-            build_split_ms_[2] = 0.0f;
+        }
+        build_split_ms_[2] = 0.0f;
         // the leaf cones / slabs and the wide BVH: beside the next frames (RT_ASYNC_ACCEL=0: now)
         if (s_.enable_bvh) {
             start_accel();
@@ -1933,7 +1931,7 @@ int Renderer::prepare_heavy(KParams& P, TileCost& T, hipStream_t stream)
     // fused SSAA block within a part's 8 / G rows
     const int G = knobs_.heavy_group;
     const bool split = G > 1 && !P.has_reflection && P.plain && !P.zbuf && !P.nbuf && P.wnodes && P.nnodes > 0 &&
-                       (!P.ds_out || (8 >> P.ds_shift) >= G);
+                       (!P.ds_out || ((1 << P.ds_shift) <= SPLIT_ROWS && (1 << P.ds_shift) <= SPLIT_COLS));
     if ((e = rt_launch_heavy_prep(&P, T.cost.as<uint32_t>(), ntiles, list, bits, ctr, knobs_.heavy_split, split ? G : 0,
                                   stream)) != hipSuccess)
         return hip_fail(e, "heavy_prep_kernel");

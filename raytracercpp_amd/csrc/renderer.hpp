@@ -66,8 +66,8 @@ struct Knobs {
     bool exact = false;       // RT_EXACT=1 / rt_set_exact: wbvh and seg off
     bool risk = true;         // RT_WBVH_RISK=0: no per-frame grazing-risk bits (every child runs case (b), 5.6)
     bool heavy = true;        // RT_HEAVY_FIRST=0: tiles in queue order only (no heavy-first list, 5.6)
-    int heavy_group = 4;      // RT_HEAVY_GROUP=4: the split tiles traced as 4 parts with 4 lanes per pixel
-                              // (kernels.hip trace_split_part); 0: none split
+    int heavy_group = SPLIT_G; // RT_HEAVY_GROUP=0: no split tiles (else: the build's RT_SPLIT_G parts of a tile,
+                              // each with that many lanes per pixel, kernels.hip trace_split_part)
     float heavy_split = 0.5f; // RT_HEAVY_SPLIT=c: split the heavy tiles costing >= c x the launch's mean
                               // cycles per wave (heavy_prep_kernel)
     int refl_defer = 48;      // RT_REFL_DEFER=k: reflection queries past k loop iterations finish in a pass

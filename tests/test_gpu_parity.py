@@ -893,9 +893,10 @@ def test_set_devices_first_frame_after_geometry_change(make_renderer):
 
 
 def test_async_accel_frames(make_renderer):
-    """The product default: the first frame after a geometry change runs while the
-    leaf cones / slabs and the wide BVH are still building (exact octree path), later frames on
-    them; every frame equals the oracle, also when the geometry changes again mid-build."""
+    """The product default: the first frame after a geometry change runs on the
+    quick wide BVH (the octree's own hierarchy) while the leaf cones / slabs and the SAH tree are still
+    building, later frames on them; every frame equals the oracle, also when the geometry changes again
+    mid-build."""
     from raytracercpp_amd import scenes
     R = make_renderer(RT_ASYNC_ACCEL="1")
     sc, st = scenes.sphere1m(width=160, height=90)
@@ -912,7 +913,7 @@ def test_async_accel_frames(make_renderer):
             g = R.get_internal(argb=True, rgba=True, hit=True, shadow=True)
         _check_vs_oracle(g, o, f"async step {step}", R=R)
         if step == 0:
-            assert R.stats()["build_split_ms"][2] == 0.0   # the wide BVH was not adopted yet
+            assert R.stats()["build_split_ms"][2] == 0.0   # the SAH tree was not adopted yet
         if step == 1:
             R.finish_accel()
     R.finish_accel()
