@@ -137,12 +137,14 @@ int rt_set_settings(rt_renderer *r, const rt_settings *s);
  * same images; exact mode is slower.  Also RT_EXACT=1 at rt_create. */
 int rt_set_exact(rt_renderer *r, int on);
 
-/* Acceleration structures beside the octree (no reference counterpart; DESIGN.md 5.8): after a
+/* Acceleration structures beside the octree (no reference counterpart; DESIGN.md 5.8, 5.9): after a
  * geometry change the octree (the reference's BVH, renderer.cpp:214-224) is built and uploaded
- * before the next frame, and the leaf cones / slabs and the wide BVH are built on a background
- * thread; frames that start before they are resident take the exact octree traversal (the same
- * images).  rt_finish_accel waits for that build (RT_ASYNC_ACCEL=0 at rt_create: every geometry
- * change waits for it). */
+ * before the next frame, together with a quick wide BVH (the octree's own hierarchy, O(n)); the
+ * leaf cones / slabs and the SAH wide BVH are built on a background thread and replace it when
+ * resident.  Frames certify their answers on either tree (the same images; without a wide BVH, as
+ * in exact mode, they take the octree traversal).  rt_finish_accel waits for the background build
+ * (RT_ASYNC_ACCEL=0 at rt_create: every geometry change waits for it; RT_WBVH_QUICK_FIRST=0: no
+ * quick tree). */
 int rt_finish_accel(rt_renderer *r);
 
 /* Single-process multi-device rendering (no reference counterpart: the reference renders on
