@@ -2284,6 +2284,7 @@ __device__ __forceinline__ bool refl_gen(const KParams& P, const ReflArgs& A, in
 #define RT_OCC_REFL 4   // waves per SIMD of the reflection trace / shadow / pass1 kernels (r04, the sound query:
                         // C5 689 vs 656 Mrays/s at 5 (31 spills), 691 at 3; r03: 4 -> 5 about -0.6%)
 #endif
+template <int G = 1>
 __device__ __forceinline__ void refl_trace_one(const KParams& P, const ReflArgs& A, int slot, v3 dir, uint2* lv,
                                                uint32_t max_steps);
 
@@ -2315,10 +2316,16 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_kernel(KParams 
     refl_trace_one(P, A, slot, dir, lv, (uint32_t)A.max_steps);
 }
 
-// The queries refl_trace_kernel deferred (ReflArgs::defer): traced to the end, one lane each, so that
-// their waves hold long queries only.
+#ifndef RT_REFL_LONG_G
+#define RT_REFL_LONG_G 4   // lanes per deferred reflection query (refl_trace_long_kernel)
+#endif
+// The queries refl_trace_kernel deferred (ReflArgs::defer): traced to the end in waves of long
+// queries only, each by a lane group of RT_REFL_LONG_G lanes (wbvh_closest<.., G>: one stack shared
+// by steals, so that the few longest queries do not hold the wave alone).
 __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_long_kernel(KParams P_arg, ReflArgs A)
 {
+    constexpr int G = RT_REFL_LONG_G;
+    static_assert(G == 1 || G == 2 || G == 4 || G == 8, "lane groups of 1, 2, 4 or 8");
     // the parameters where the kernel received them (not a copy: passing the by-value argument to a
     // call made every lane copy it to scratch, r05: C5's shadow pass wrote ~90 GB per launch)
     const KParams& P = kernel_params();
@@ -2326,12 +2333,13 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_long_kernel(KPa
     extern __shared__ uint2 lds_levels[];
     uint2* lv = lds_levels + threadIdx.x;
     const int n = (int)ldg(A.defer_count);
-    for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+    // query i is held by lanes G i .. G i + G - 1 of the grid (whole groups inside one wave)
+    for (int i = (int)((blockIdx.x * BLOCK + threadIdx.x) / G); i < n; i += (int)(gridDim.x * BLOCK / G)) {
         const int slot = A.defer[i];
         unsigned count = 0;
         v3 dir = mk(0, 0, 0);
-        if (refl_gen(P, A, slot, dir, count))   // (the same direction: path-keyed RNG)
-            refl_trace_one(P, A, slot, dir, lv, 0u);
+        if (refl_gen(P, A, slot, dir, count))   // (the same direction: path-keyed RNG; every lane of the group)
+            refl_trace_one<G>(P, A, slot, dir, lv, 0u);
     }
 }
 
@@ -2339,6 +2347,9 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_long_kernel(KPa
 // deferred list instead.
 // In line, with the octree fallback behind the out-of-line octree_query_call (results by value): a
 // ray record or hit record whose address reached a call lived in scratch for every sample (r05).
+// G > 1 (refl_trace_long_kernel): the G lanes of a group hold the same slot and run the query
+// together; the group's first lane writes the result.
+template <int G>
 __device__ __forceinline__ void refl_trace_one(const KParams& P, const ReflArgs& A, int slot, v3 dir, uint2* lv,
                                                uint32_t max_steps)
 {
@@ -2347,7 +2358,7 @@ __device__ __forceinline__ void refl_trace_one(const KParams& P, const ReflArgs&
     THit h;
     bool r;
     bool longq = false;
-    if (P.wnodes && P.nnodes > 0 && !ray_is_nan(ro, dir) && wide_closest(P, ro, dir, h, r, lv, nullptr, max_steps, &longq))
+    if (P.wnodes && P.nnodes > 0 && !ray_is_nan(ro, dir) && wide_closest<G>(P, ro, dir, h, r, lv, nullptr, max_steps, &longq))
         ;   // certified by the wide BVH
     else if (longq) {
         const uint64_t m = __ballot(1);   // the lanes deferring now: one atomic per wave
@@ -2373,7 +2384,8 @@ __device__ __forceinline__ void refl_trace_one(const KParams& P, const ReflArgs&
     H.k = h.k;
     st3(H.d, dir);
     H.r = (r ? 1 : 0) | (A.fused ? 2 : 0);
-    A.hit[slot] = H;
+    if (G == 1 || (threadIdx.x & (G - 1)) == 0)
+        A.hit[slot] = H;
 }
 
 // append slot to the shadow list from (possibly divergent) lanes: one atomic per wave

@@ -70,7 +70,7 @@ struct Knobs {
                               // each with that many lanes per pixel, kernels.hip trace_split_part)
     float heavy_split = 0.5f; // RT_HEAVY_SPLIT=c: split the heavy tiles costing >= c x the launch's mean
                               // cycles per wave (heavy_prep_kernel)
-    int refl_defer = 48;      // RT_REFL_DEFER=k: reflection queries past k loop iterations finish in a pass
+    int refl_defer = 32;      // RT_REFL_DEFER=k: reflection queries past k loop iterations finish in a pass
                               // of their own (9; 0: never)
     int inject_fail = 0;      // RT_INJECT_FRAME_FAIL=k (tests): the k-th ray_trace fails after its image start
     bool async_accel = true;  // RT_ASYNC_ACCEL=0: the leaf cones / slabs and the wide BVH are built

@@ -78,6 +78,12 @@ constexpr int W_WIDTH = 4;    // children per node
 #define W_QS_SHADOW 0x1p-12f
 #endif
 
+// case (b)'s D (wbvh_closest): the farthest corner of the child's box (sound either way; 0: the node's
+// frame for every ray, 1: per child for rays without risk words, 2: per child for every ray)
+#ifndef W_B_CHILD_D
+#define W_B_CHILD_D 2
+#endif
+
 // timing-only switches (tools/variants.py; never sound when off)
 #ifndef W_CASE_B
 #define W_CASE_B 1
@@ -1040,6 +1046,19 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                     // of the child's slab (D = Dn >= |o - a|)
                     const float rkj = bitsf(rw[2 * j + 1] & 0xFFFF0000u);   // wrisk_key
                     const float kbl = (rkj - rsub) * iqd;
+                    // D for case (b): o to the farthest corner of child j's box (it holds the child's
+                    // vertices; Dn's frame can be several times larger, and near the origin (b) is priced
+                    // by D sin(theta))
+                    auto dchild = [&]() -> float {
+#if W_B_CHILD_D
+                        const float fx = fmaxf(fabsf(__builtin_fmaf(qnx, stx, Dx)), fabsf(__builtin_fmaf(qfx, stx, Dx)));
+                        const float fy = fmaxf(fabsf(__builtin_fmaf(qny, sty, Dy)), fabsf(__builtin_fmaf(qfy, sty, Dy)));
+                        const float fz = fmaxf(fabsf(__builtin_fmaf(qnz, stz, Dz)), fabsf(__builtin_fmaf(qfz, stz, Dz)));
+                        return fast_sqrt(fx * fx + fy * fy + fz * fz) * (1.0f + 0x1p-16f) + m;
+#else
+                        return Dn;
+#endif
+                    };
                     if (W_CASE_B && !risk && qlb < QS) {
                         // no risk words (reflection rays, rt_trace_ray):
                         W_DIAG_ADD(4, 1);
@@ -1050,9 +1069,14 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                         bool okb = !(umin > __builtin_fmaf(fabsf(umax), SL, umax));
                         if (okb) {
                             const float s2 = wq_val_nz((e >> 8) & 0xffu, WQ_UNIT);
-                            const float H0 = wq_h0(QS, L, Dn, smin, s2);
-                            const float w = NLH * (H0 + __builtin_fmaf(Dn, sth, m)) * (1.0f + 0x1p-16f) + 384.0f * m;
+                            const float Dc = dchild();
+                            const float H0 = wq_h0(QS, L, Dc, smin, s2);
+                            const float w = NLH * (H0 + __builtin_fmaf(Dc, sth, m)) * (1.0f + 0x1p-16f) + 384.0f * m;
                             okb = !(-b < C0 - w || -b > C1 + w);
+#if defined(W_TRACE) && !defined(__HIP_DEVICE_COMPILE__)
+                            printf("  (b0) node %u child %d: umin %.4g umax %.4g -b %.4g slab [%.4g, %.4g] w %.4g H0 %.3g Dc %.3g sth %.3g okb %d\n",
+                                   cur, j, umin, umax, -b, C0, C1, w, H0, Dc, sth, (int)okb);
+#endif
                         }
                         if (okb)
                             key[j] = 0.0f;
@@ -1078,8 +1102,9 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                         bool okb = !(umin > __builtin_fmaf(fabsf(umax), SL, umax));
                         if (okb) {
                             const float s2 = wq_val_nz((e >> 8) & 0xffu, WQ_UNIT);
-                            const float H0 = wq_h0(QS, L, Dn, smin, s2);
-                            const float w = NLH * (H0 + __builtin_fmaf(Dn, sth, m)) * (1.0f + 0x1p-16f) + 384.0f * m;
+                            const float Dc = W_B_CHILD_D >= 2 ? dchild() : Dn;
+                            const float H0 = wq_h0(QS, L, Dc, smin, s2);
+                            const float w = NLH * (H0 + __builtin_fmaf(Dc, sth, m)) * (1.0f + 0x1p-16f) + 384.0f * m;
                             okb = !(-b < C0 - w || -b > C1 + w);   // N . (o - origin) = -b
                         }
 #if defined(W_TRACE) && !defined(__HIP_DEVICE_COMPILE__)
