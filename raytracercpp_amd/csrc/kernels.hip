@@ -2280,6 +2280,9 @@ __device__ __forceinline__ bool refl_gen(const KParams& P, const ReflArgs& A, in
     return true;
 }
 
+#ifndef RT_REFL_G
+#define RT_REFL_G 1   // lanes per reflection sample in refl_trace_kernel
+#endif
 #ifndef RT_OCC_REFL
 #define RT_OCC_REFL 4   // waves per SIMD of the reflection trace / shadow / pass1 kernels (r04, the sound query:
                         // C5 689 vs 656 Mrays/s at 5 (31 spills), 691 at 3; r03: 4 -> 5 about -0.6%)
@@ -2296,14 +2299,16 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_kernel(KParams 
     (void)P_arg;
     extern __shared__ uint2 lds_levels[];
     uint2* lv = lds_levels + threadIdx.x;
-    int slot = blockIdx.x * BLOCK + threadIdx.x;
+    constexpr int G = RT_REFL_G;   // lanes per sample (the launch has G threads per slot)
+    const bool lead = G == 1 || (threadIdx.x & (G - 1)) == 0;
+    int slot = (int)((blockIdx.x * BLOCK + threadIdx.x) / G);
     int nslot = (A.c1 - A.c0) * A.stride;
     unsigned count = 0;
     v3 dir = mk(0, 0, 0);
     bool ray = slot < nslot && refl_gen(P, A, slot, dir, count);
-    wave_count_add(&P.counters[1], count);
+    wave_count_add(&P.counters[1], lead ? count : 0u);
     if (!ray) {
-        if (A.fused && slot < nslot) {   // no ray (pass1 skips it: bit 1 clear)
+        if (A.fused && slot < nslot && lead) {   // no ray (pass1 skips it: bit 1 clear)
             RawHit H;
             H.t = H.u = H.v = 0.0f;
             H.k = -1;
@@ -2313,7 +2318,7 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_kernel(KParams 
         }
         return;
     }
-    refl_trace_one(P, A, slot, dir, lv, (uint32_t)A.max_steps);
+    refl_trace_one<G>(P, A, slot, dir, lv, (uint32_t)A.max_steps);
 }
 
 #ifndef RT_REFL_LONG_G
@@ -2361,13 +2366,16 @@ __device__ __forceinline__ void refl_trace_one(const KParams& P, const ReflArgs&
     if (P.wnodes && P.nnodes > 0 && !ray_is_nan(ro, dir) && wide_closest<G>(P, ro, dir, h, r, lv, nullptr, max_steps, &longq))
         ;   // certified by the wide BVH
     else if (longq) {
-        const uint64_t m = __ballot(1);   // the lanes deferring now: one atomic per wave
+        // the groups deferring now (their first lanes): one atomic per wave
+        const bool lead = G == 1 || (threadIdx.x & (G - 1)) == 0;
+        const uint64_t m = __ballot(lead);
         const int leader = __ffsll((unsigned long long)m) - 1;
         uint32_t base = 0;
         if ((int)(threadIdx.x & 63) == leader)
             base = atomicAdd(A.defer_count, (unsigned)__popcll(m));
         base = __shfl(base, leader);
-        A.defer[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = slot;
+        if (lead)
+            A.defer[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = slot;
         return;
     } else {
         const bool seg = P.seg_scale > 0.0f && P.seg_oct;
@@ -3740,7 +3748,7 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_stage
     dim3 gs((nslot + rt::BLOCK - 1) / rt::BLOCK), gf((nframes + rt::BLOCK - 1) / rt::BLOCK);
     size_t lds = rt::lds_bytes(*P);
     switch (stage) {
-    case 1: hipLaunchKernelGGL(rt::refl_trace_kernel, gs, dim3(rt::BLOCK), lds, stream, *P, *A); break;
+    case 1: hipLaunchKernelGGL(rt::refl_trace_kernel, dim3(gs.x * RT_REFL_G), dim3(rt::BLOCK), lds, stream, *P, *A); break;
     case 7: hipLaunchKernelGGL(rt::refl_trace_long_kernel, dim3(std::min<unsigned>(gs.x, 2048u)), dim3(rt::BLOCK), lds,
                                stream, *P, *A); break;
     case 2: hipLaunchKernelGGL(rt::refl_pass1_kernel, gf, dim3(rt::BLOCK), 0, stream, *P, *A); break;
