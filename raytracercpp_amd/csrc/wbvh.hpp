@@ -83,6 +83,9 @@ constexpr int W_WIDTH = 4;    // children per node
 #ifndef W_B_CHILD_D
 #define W_B_CHILD_D 2
 #endif
+#ifndef W_A_CHILD_D
+#define W_A_CHILD_D 0   // case (a)'s D per child as well (sound either way)
+#endif
 
 // timing-only switches (tools/variants.py; never sound when off)
 #ifndef W_CASE_B
@@ -954,15 +957,32 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                     const float L = (e >> 24) == 255u ? INFINITY : wq_val_nz(e >> 24, WQ_LEN);
                     const float qlb = __builtin_fmaf(-sth, 1.0f + sth, -a * icp) - 0x1p-20f;
                     const float qa = fmaxf(qlb, QS);
+                    const float qnx = (float)((nwx[jw] >> sh) & 0xffu), qfx = (float)((fwx[jw] >> sh) & 0xffu);
+                    const float qny = (float)((nwy[jw] >> sh) & 0xffu), qfy = (float)((fwy[jw] >> sh) & 0xffu);
+                    const float qnz = (float)((nwz[jw] >> sh) & 0xffu), qfz = (float)((fwz[jw] >> sh) & 0xffu);
+                    // D for case (b) (and (a), W_A_CHILD_D): o to the farthest corner of child j's box (it holds the child's
+                    // vertices; Dn's frame can be several times larger, and near the origin (b) is priced
+                    // by D sin(theta))
+                    auto dchild = [&]() -> float {
+#if W_B_CHILD_D
+                        const float fx = fmaxf(fabsf(__builtin_fmaf(qnx, stx, Dx)), fabsf(__builtin_fmaf(qfx, stx, Dx)));
+                        const float fy = fmaxf(fabsf(__builtin_fmaf(qny, sty, Dy)), fabsf(__builtin_fmaf(qfy, sty, Dy)));
+                        const float fz = fmaxf(fabsf(__builtin_fmaf(qnz, stz, Dz)), fabsf(__builtin_fmaf(qfz, stz, Dz)));
+                        return fast_sqrt(fx * fx + fy * fy + fz * fz) * (1.0f + 0x1p-16f) + m;
+#else
+                        return Dn;
+#endif
+                    };
                     // (a): the box widened by R, the slab by eta + R sin(theta) (wq_reach: the correlated bound of
                     // Moller-Trumbore's reports, D = Dn)
 #if W_SOUND_A
-                    const WReach wr = wq_reach(qa, smin, L, Dn);
+                    const float Da = W_A_CHILD_D ? dchild() : Dn;
+                    const WReach wr = wq_reach(qa, smin, L, Da);
                     const float R = __builtin_fmaf(W_R_SCALE, wr.E, m);
                     // the box test: the line crosses the box widened by the lateral reach, and a report lies
                     // within Rpar of that crossing along the line (wq_split)
                     float Rlat, Rpar;
-                    wq_split(wr, L, Dn, Rlat, Rpar);
+                    wq_split(wr, L, Da, Rlat, Rpar);
                     const float Rb = __builtin_fmaf(W_R_SCALE, Rlat, m);
                     const float dtp = W_R_SCALE * Rpar * idl;
 #else
@@ -970,9 +990,6 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
 #endif
                     // the entry / exit planes' t of this child's box widened by M:
                     // q (s / d) + (origin - o) / d -+ M / |d| per axis
-                    const float qnx = (float)((nwx[jw] >> sh) & 0xffu), qfx = (float)((fwx[jw] >> sh) & 0xffu);
-                    const float qny = (float)((nwy[jw] >> sh) & 0xffu), qfy = (float)((fwy[jw] >> sh) & 0xffu);
-                    const float qnz = (float)((nwz[jw] >> sh) & 0xffu), qfz = (float)((fwz[jw] >> sh) & 0xffu);
                     auto box = [&](float M, float& tmin, float& tmax) {
                         const float tnx = __builtin_fmaf(-M, aix, __builtin_fmaf(qnx, sx, bx));
                         const float tny = __builtin_fmaf(-M, aiy, __builtin_fmaf(qny, sy, by));
@@ -999,7 +1016,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                         // N . (o + t d - origin) in [C0, C1] widened by w: t between
                         // (C0 - w + b) / a and (C1 + w + b) / a
 #if W_SOUND_A
-                        const float eta = wq_eta(wr, L, Dn);
+                        const float eta = wq_eta(wr, L, Da);
 #else
                         const float eta = 0.0f;
 #endif
@@ -1046,19 +1063,6 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                     // of the child's slab (D = Dn >= |o - a|)
                     const float rkj = bitsf(rw[2 * j + 1] & 0xFFFF0000u);   // wrisk_key
                     const float kbl = (rkj - rsub) * iqd;
-                    // D for case (b): o to the farthest corner of child j's box (it holds the child's
-                    // vertices; Dn's frame can be several times larger, and near the origin (b) is priced
-                    // by D sin(theta))
-                    auto dchild = [&]() -> float {
-#if W_B_CHILD_D
-                        const float fx = fmaxf(fabsf(__builtin_fmaf(qnx, stx, Dx)), fabsf(__builtin_fmaf(qfx, stx, Dx)));
-                        const float fy = fmaxf(fabsf(__builtin_fmaf(qny, sty, Dy)), fabsf(__builtin_fmaf(qfy, sty, Dy)));
-                        const float fz = fmaxf(fabsf(__builtin_fmaf(qnz, stz, Dz)), fabsf(__builtin_fmaf(qfz, stz, Dz)));
-                        return fast_sqrt(fx * fx + fy * fy + fz * fz) * (1.0f + 0x1p-16f) + m;
-#else
-                        return Dn;
-#endif
-                    };
                     if (W_CASE_B && !risk && qlb < QS) {
                         // no risk words (reflection rays, rt_trace_ray):
                         W_DIAG_ADD(4, 1);
