@@ -2321,6 +2321,9 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_kernel(KParams 
     refl_trace_one<G>(P, A, slot, dir, lv, (uint32_t)A.max_steps);
 }
 
+#ifndef RT_REFL_LONG_QUEUE
+#define RT_REFL_LONG_QUEUE 0   // refl_trace_long_kernel: waves take batches from a ticket (0: grid stride)
+#endif
 #ifndef RT_REFL_LONG_G
 #define RT_REFL_LONG_G 4   // lanes per deferred reflection query (refl_trace_long_kernel)
 #endif
@@ -2338,8 +2341,25 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_long_kernel(KPa
     extern __shared__ uint2 lds_levels[];
     uint2* lv = lds_levels + threadIdx.x;
     const int n = (int)ldg(A.defer_count);
+#if RT_REFL_LONG_QUEUE
+    // a wave takes the next 64 / G queries from a ticket (defer_count[1], zeroed with the count) when it
+    // is done with its last ones: the waves' batches differ in length, a fixed grid stride left the
+    // kernel to its slowest wave's sum of batches
+    const int lane = (int)(threadIdx.x & 63);
+    for (;;) {
+        int base = 0;
+        if (lane == 0)
+            base = (int)atomicAdd(A.defer_count + 1, (unsigned)(64 / G));
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (base >= n)
+            break;
+        const int i = base + lane / G;   // query i: lanes G i .. G i + G - 1 of the batch
+        if (i >= n)
+            continue;
+#else
     // query i is held by lanes G i .. G i + G - 1 of the grid (whole groups inside one wave)
     for (int i = (int)((blockIdx.x * BLOCK + threadIdx.x) / G); i < n; i += (int)(gridDim.x * BLOCK / G)) {
+#endif
         const int slot = A.defer[i];
         unsigned count = 0;
         v3 dir = mk(0, 0, 0);

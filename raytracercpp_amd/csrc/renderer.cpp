@@ -1223,7 +1223,7 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
         A.defer = L.list.as<int32_t>();
         A.defer_count = L.cnt.as<unsigned int>() + 2;
         A.max_steps = knobs_.refl_defer;
-        if ((e = hipMemsetAsync(L.cnt.p, 0, 12, stream)) != hipSuccess)
+        if ((e = hipMemsetAsync(L.cnt.p, 0, 16, stream)) != hipSuccess)   // (+ the long kernel's ticket)
             return hip_fail(e, "hipMemsetAsync");
         // fused (default): trace, pass1 (+ shadow list), shadow (+ spawn); RT_REFL_FUSE=0: trace,
         // pass1, list, shadow, spawn
