@@ -2322,7 +2322,7 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_kernel(KParams 
 }
 
 #ifndef RT_REFL_LONG_QUEUE
-#define RT_REFL_LONG_QUEUE 0   // refl_trace_long_kernel: waves take batches from a ticket (0: grid stride)
+#define RT_REFL_LONG_QUEUE 1   // refl_trace_long_kernel: waves take batches from a ticket (0: grid stride)
 #endif
 #ifndef RT_REFL_LONG_G
 #define RT_REFL_LONG_G 4   // lanes per deferred reflection query (refl_trace_long_kernel)
