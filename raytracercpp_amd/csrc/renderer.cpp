@@ -130,7 +130,7 @@ Knobs Knobs::from_env()
     k.async_accel = on("RT_ASYNC_ACCEL", true);
     if (const char* ce = getenv("RT_REFL_CHUNK_LOG2")) {
         const int v = atoi(ce);
-        if (v >= 10 && v <= 25)   // small values (tests): many chunks per level
+        if (v >= 10 && v <= 27)   // small values (tests): many chunks per level
             k.refl_chunk_log2 = v;
     }
     return k;
@@ -1150,8 +1150,9 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
     ReflLevel& L = refl_[level];
     ReflLevel& C = refl_[level + 1];
     hipError_t e;
-    // about 2^RT_REFL_CHUNK_LOG2 sample slots per chunk (default 2^25: C5 0.765 / 0.714 / 0.695 /
-    // 0.679 s at 2^21 / 2^23 / 2^24 / 2^25): one host round trip per chunk, ~204 B of records per
+    // about 2^RT_REFL_CHUNK_LOG2 sample slots per chunk (default 2^27: C5 1,757 / 1,841 / 1,902 / 1,927
+    // Mrays/s at 2^24 / 2^25 / 2^26 / 2^27, r05; r02: 0.765 / 0.714 / 0.695 / 0.679 s at 2^21 / 2^23 /
+    // 2^24 / 2^25): one host round trip per chunk, ~204 B of records per
     // slot (72-B SampleRec, 32-B RawHit, 16-B result, list entry, child frame and its colour).
     // A level may take at most a quarter of the memory still free (what it already holds
     // counts as free), so that the deeper levels, each bounded the same way, fit behind it;

@@ -61,7 +61,7 @@ struct Knobs {
     bool refl_engine = true;  // RT_REFL_ENGINE=0: the one-lane-per-pixel recursive kernel (9)
     bool refl_sort = true;    // RT_REFL_SORT=0: reflection frames in spawn order, not Morton order
     bool refl_fuse = true;    // RT_REFL_FUSE=0: the engine's separate list / spawn passes
-    int refl_chunk_log2 = 25; // RT_REFL_CHUNK_LOG2 (10..25): sample slots per engine chunk
+    int refl_chunk_log2 = 27; // RT_REFL_CHUNK_LOG2 (10..27): sample slots per engine chunk
     bool debug_waves = false; // RT_DEBUG_WAVES: per-wave records of diagnostic builds (rt_debug_read)
     bool exact = false;       // RT_EXACT=1 / rt_set_exact: wbvh and seg off
     bool risk = true;         // RT_WBVH_RISK=0: no per-frame grazing-risk bits (every child runs case (b), 5.6)
