@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true", help="skip max_abs_dpixel (the oracle frame)")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=3,
                     help="frames in flight: consecutive steps alternate over this many streams (DESIGN.md 7)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU ranks over gloo, synthetic pattern strips: the launch / gather / check plumbing only")
