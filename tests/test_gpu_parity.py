@@ -772,7 +772,7 @@ def test_band_slots_recycle_and_shared_buffers(R):
 
 def test_rccl_frame_pipeline_world1():
     """bench.py's N>1 path on one GPU: an RCCL process group (world size 1, torchrun) on a
-    high-priority stream, two frames in flight with asynchronous all-gathers
+    high-priority stream, three frames in flight (the bench's default) with asynchronous all-gathers
     (strips.FramePipeline, gather forced on): every gathered frame equals the rendered strips
     (tools/nccl_check.py).  Runs in its own process: the rendezvous and RCCL state stay out of
     this one."""

@@ -21,8 +21,9 @@ r = Renderer(0)
 r.load_scene(sc, st)
 band = 8
 n = r.local_rows(band, 0, 1)
-streams = [torch.cuda.current_stream(dev), torch.cuda.Stream(dev)]
-outs = [torch.zeros((n, st.image_width), dtype=torch.int32, device=dev) for _ in range(2)]
+q = 3   # frames in flight: bench.py's default (--inflight)
+streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(q - 1)]
+outs = [torch.zeros((n, st.image_width), dtype=torch.int32, device=dev) for _ in range(q)]
 torch.cuda.synchronize()
 pipe = FramePipeline(lambda o, s: r.render_bands_device(band, 0, 1, o.data_ptr(), s.cuda_stream), outs, 1, streams, dist)
 pipe.world = 2   # force the gather path with one rank: parts[i] holds 2 slots, gather fills slot 0
@@ -32,7 +33,7 @@ for k in range(12):
     pipe.step()
 pipe.drain()
 ref = outs[0].clone()
-for i in range(2):
+for i in range(q):
     ok &= bool(torch.equal(pipe.parts[i][0], outs[i])) and bool(torch.equal(outs[i], ref))
 print("nccl pipeline ok" if ok else "nccl pipeline MISMATCH", flush=True)
 dist.destroy_process_group()
