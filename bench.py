@@ -44,9 +44,13 @@ WIDE_NODE_BYTES = 160        # one wide-BVH node visit reads the 128-B node and 
 CERT_BYTES = 72              # one certificate: the octree leaf's 64-B node + two 4-B slot maps
 PIXEL_BYTES = 4              # ARGB32 write per internal pixel
 COUNTS_FILE = os.path.join(ROOT, "profiles", "work_counts.json")
-# rocprofv3 PMC summary of this kernel on the same command (tools/profile_gpu.sh + profile_summary.py)
-PROFILE_SUMMARY = os.path.join(ROOT, "profiles", "r04", "summary.json")
-C5_CHECK_ROWS = (172, 400, 540, 907)   # output rows whose internal row pairs bench's C5 mode checks
+# configs whose oracle frame takes minutes on the host (hair1m: ~100 s on 8 threads): bench checks
+# every CHECK_STRIDE-th output row (its f internal rows) instead of the whole frame
+SAMPLED_CHECK = ("hair1m",)
+CHECK_STRIDE = 8
+# rocprofv3 PMC summary of the benched kernel (tools/profile_gpu.sh + profile_summary.py, copied from the
+# round's profile directory): kept outside the per-round directories so that it ships to the GPU box
+PROFILE_SUMMARY = os.path.join(ROOT, "profiles", "c4_summary.json")
 
 
 def parse():
@@ -61,6 +65,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--inflight", type=int, default=3,
                     help="frames in flight: consecutive steps alternate over this many streams (DESIGN.md 7)")
+    ap.add_argument("--no-balance", dest="balance", action="store_false",
+                    help="N > 1: keep the interleaved bands (default: cost-balanced band lists after the warm-up)")
+    ap.add_argument("--no-legs", action="store_true", help="N = 1: skip the sync and moving-camera legs")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU ranks over gloo, synthetic pattern strips: the launch / gather / check plumbing only")
     return ap.parse_args()
@@ -114,7 +121,7 @@ def main():
     import torch.distributed as dist
     from raytracercpp_amd import scenes
     from raytracercpp_amd.renderer import Renderer
-    from raytracercpp_amd.strips import FramePipeline, assemble_torch
+    from raytracercpp_amd.strips import FramePipeline, assign_bands, gather_index, num_bands
 
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -134,37 +141,71 @@ def main():
     W, H = st.image_width, st.image_height
     rw, rh = st.render_size()
     band = args.band_rows
-    nloc = r.local_rows(band, rank, world)
+    nb = num_bands(H, band)
+    c5 = args.config == "sphere1m_refl"
     # Frames in flight: step i renders on stream i % q into its own output
     # buffer, and its all-gather is enqueued asynchronously behind it, so the next frame's
     # kernel fills the CUs that this frame's tail leaves idle and the gather overlaps it.
     # Before a slot is reused its previous gather has finished reading the buffer (wait).
     q = max(1, args.inflight)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(q - 1)]
-    outs = [torch.empty((nloc, W), dtype=torch.int32, device=dev) for _ in range(q)]
-    pipe = FramePipeline(lambda o, s: r.render_bands_device(band, rank, world, o.data_ptr(), s.cuda_stream),
-                         outs, world, streams, dist)
-    step, drain = pipe.step, pipe.drain
 
+    def make_pipe(lists):
+        """The strips pipeline of this rank: the interleaved bands (lists None) or a band list per
+        rank; rank 0 re-assembles every gathered frame on the slot's stream inside the step."""
+        nloc = len(lists[0]) * band if lists is not None else r.local_rows(band, rank, world)
+        outs = [torch.empty((nloc, W), dtype=torch.int32, device=dev) for _ in range(q)]
+        if lists is None:
+            render = lambda o, s_: r.render_bands_device(band, rank, world, o.data_ptr(), s_.cuda_stream)  # noqa: E731
+        else:
+            mine = lists[rank]
+            render = lambda o, s_: r.render_band_list_device(band, mine, o.data_ptr(), s_.cuda_stream)  # noqa: E731
+        frames, asm = None, None
+        if world > 1 and rank == 0:
+            idx = torch.as_tensor(gather_index(H, band, world, nloc, lists), device=dev)
+            frames = [torch.empty((H, W), dtype=torch.int32, device=dev) for _ in range(q)]
+            asm = lambda i, flat: torch.index_select(flat, 0, idx, out=frames[i])  # noqa: E731
+        pipe = FramePipeline(render, outs, world, streams, dist, assemble=asm)
+        return pipe, (frames if frames is not None else outs)
+
+    pipe, frames = make_pipe(None)
     t_build0 = time.perf_counter()
-    step()   # first call: builds + uploads the octree; the wide BVH and leaf cones build beside it
-    drain()
+    pipe.step()   # first call: builds + uploads the octree; the wide BVH and leaf cones build beside it
+    pipe.drain()
     t_first = time.perf_counter() - t_build0
     r.finish_accel()   # the timed frames run on the wide BVH (DESIGN.md 5.8)
     t_accel = time.perf_counter() - t_build0
     build = r.stats()
     shadow_local, refl_local = r.band_counters()
     for _ in range(args.warmup):
-        step()
-    drain()
+        pipe.step()
+    pipe.drain()
+    balance = None
+    if world > 1 and args.balance and not c5:
+        # cost-balanced strips (strips.assign_bands): the warm-up frames' band costs of every rank,
+        # summed (each band was rendered by one rank), give every rank the same balanced lists
+        costs = r.band_costs(nb, streams[(args.warmup - 1) % q].cuda_stream if args.warmup else 0)
+        ct = torch.as_tensor(costs, device=dev)
+        dist.all_reduce(ct)
+        costs = ct.cpu().numpy()
+        lists = assign_bands(costs, world)
+        loads = [float(costs[lst].sum()) for lst in lists]
+        balance = {"interleaved_max_over_mean": round(max(float(costs[b::world].sum()) for b in range(world)) /
+                                                      (sum(loads) / world), 4),
+                   "balanced_max_over_mean": round(max(loads) / (sum(loads) / world), 4),
+                   "bands_per_rank": [len(x) for x in lists]}
+        pipe, frames = make_pipe(lists)
+        for _ in range(args.warmup):   # (each stream's heavy lists learn the new layout)
+            pipe.step()
+        pipe.drain()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     last = 0
     for _ in range(args.steps):
-        last = step()
-    drain()
+        last = pipe.step()
+    pipe.drain()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -183,8 +224,7 @@ def main():
     shadow_total = int(per_rank[:, 1].sum())
     k_max, k_min = float(per_rank[:, 2].max()), float(per_rank[:, 2].min())
     refl_total = int(per_rank[:, 3].sum())
-    c5 = args.config == "sphere1m_refl"
-    frame = assemble_torch(pipe.parts[last], H, band) if rank == 0 else None
+    frame = frames[last] if rank == 0 else None
 
     if rank == 0:
         primary = rw * rh
@@ -194,6 +234,12 @@ def main():
         img = frame.cpu().numpy().view(np.uint32)
         metric = ("Mrays/sec (primary+shadow+reflection) at 1920x1080, 1M-tri scene + rough reflections (C5)" if c5
                   else "Mrays/sec (primary+shadow) at 1920x1080, 1M-tri scene; max |dpixel|")
+        workloads = {"sphere1m_refl": "C5 sphere1m_refl: C4 + reflection 0.5 / roughness 0.3, 16 samples, depth 5, "
+                                      "normal + parallax maps",
+                     "sphere1m": "C4 sphere1m: 1,000,000 tris, 1920x1080, ssaa_factor 2 (3840x2160 rays), "
+                                 "primary + shadow, octree 12/40",
+                     "hair1m": "hair1m: 50k ribbon strands (1,000,000 tris), 1920x1080, ssaa_factor 2, "
+                               "primary + shadow, octree 12/40 (BASELINE configs[3]'s hair scene)"}
         res = {
             "metric": metric,
             "value": round(value, 3),
@@ -206,14 +252,12 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (deterministic 1M-tri UV sphere, SURVEY.md 8(d) C4)",
-            "config": {"workload": ("C5 sphere1m_refl: C4 + reflection 0.5 / roughness 0.3, 16 samples, depth 5, "
-                                    "normal + parallax maps" if c5 else
-                                    "C4 sphere1m: 1,000,000 tris, 1920x1080, ssaa_factor 2 (3840x2160 rays), "
-                                    "primary + shadow, octree 12/40"), "image": [W, H], "render": [rw, rh],
+            "data": f"synthetic (deterministic {args.config} scene, SURVEY.md 8(d))",
+            "config": {"workload": workloads.get(args.config, args.config), "image": [W, H], "render": [rw, rh],
                        "rays_per_frame": rays, "primary_rays": primary, "shadow_rays": shadow_total,
                        "reflection_rays": refl_total, "band_rows": band, "parallelism": f"image strips x{world}",
-                       "frames_in_flight": q, "world_size": world},
+                       "frames_in_flight": q, "world_size": world,
+                       "bands": "cost-balanced lists" if balance else "interleaved b % N"},
             "kernel_ms": round(k_max, 4),
             "kernel_ms_per_rank": {"max": round(k_max, 4), "min": round(k_min, 4)},
             "first_call_s": round(t_first, 3),
@@ -222,27 +266,98 @@ def main():
                          **{k: round(v, 1) for k, v in zip(("octree", "cones_slabs_background", "wide_bvh_background",
                                                              "octree_upload"), build["build_split_ms"])}},
         }
-        rl = roofline(args.config, world, k_max, ms_per_step, primary)
+        if balance:
+            res["balance"] = balance
+        legs = {}
+        if world == 1 and not c5 and not args.no_legs:
+            legs["sync"], sync_img = sync_leg(r, args, rays)
+            legs["moving_camera"], mv_img, mv_scene = moving_camera_leg(r, args, pipe, frames, sc, primary)
+        rl = roofline(args.config, world, (legs.get("sync") or {}).get("kernel_ms"), k_max, ms_per_step, primary)
         if rl:
             res["roofline"] = rl
+        res.update(legs)
         if not args.no_check or (world == 1 and not args.no_cpu_baseline):
             base, dpx, check = cpu_leg(sc, st, img, args.cpu_threads, c5, check=not args.no_check,
-                                       baseline=world == 1 and not args.no_cpu_baseline)
+                                       baseline=world == 1 and not args.no_cpu_baseline, name=args.config,
+                                       extra={"sync": (sc, sync_img), "moving_camera": (mv_scene, mv_img)} if legs else None)
             if base:
                 res["cpu_baseline"] = base
             if dpx is not None:
-                res["max_abs_dpixel"] = dpx
+                res["max_abs_dpixel"] = dpx.pop("main")
                 res["dpixel_check"] = check
+                for k, v in dpx.items():
+                    res[k]["max_abs_dpixel"] = v
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
 
 
-def roofline(config, world, kernel_ms, ms_per_step, primary):
+def sync_leg(r, args, rays):
+    """The reference's synchronous call surface (utils/mainUtils.cpp:6-21, QT/mainWindowThreads.cpp:39-65):
+    rt_ray_trace + rt_post_process + rt_get_image to host, one frame at a time.  Its kernel time (HIP
+    events around the one launch, rt_stats.kernel_ms) is the non-overlapped per-launch duration that
+    the roofline prices."""
+    for _ in range(args.warmup):
+        r.ray_trace()
+        r.post_process()
+        r.get_image()
+    kms = []
+    t0 = time.perf_counter()
+    img = None
+    for _ in range(args.steps):
+        r.ray_trace()
+        kms.append(r.stats()["kernel_ms"])
+        r.post_process()
+        img = r.get_image()
+    el = time.perf_counter() - t0
+    return ({"value": round(rays * args.steps / el / 1e6, 3), "unit": "Mrays/s", "ms_per_step": round(1e3 * el / args.steps, 4),
+             "kernel_ms": round(float(np.mean(kms)), 4), "frames_in_flight": 1,
+             "what": "rt_ray_trace + rt_post_process + rt_get_image to host, one frame at a time"}, img.ravel())
+
+
+def moving_camera_leg(r, args, pipe, frames, sc, primary):
+    """set_camera_transform before every step (a small yaw sweep, renderer.cpp:235-241's camera
+    transform): the per-camera work -- the camera's risk words (wide_risk_kernel + pack) and the heavy
+    list from the previous, slightly different view -- runs inside the timed loop; frames in flight as
+    the headline.  Returns the leg, the last frame and that frame's scene (camera) for the check."""
+    import dataclasses
+    import torch
+    from raytracercpp_amd import _lib
+    angles = [0.25 * (k % 8) for k in range(args.steps + args.warmup)]
+
+    def step(k):
+        r.set_camera_transform(_lib.make_transform("ry", angles[k]))
+        return pipe.step()
+    for k in range(args.warmup):
+        step(k)
+    pipe.drain()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    last = 0
+    for k in range(args.warmup, args.warmup + args.steps):
+        last = step(k)
+    pipe.drain()
+    el = time.perf_counter() - t0
+    shadow, _ = r.band_counters()   # (the last frame's; the sweep changes it little)
+    img = frames[last].cpu().numpy().view(np.uint32).ravel()
+    sc2 = dataclasses.replace(sc)
+    sc2.cam_pos, sc2.proj_inv, sc2.cam_to_world = r.get_camera_matrices()
+    r.set_camera_matrices(sc.cam_pos, sc.proj_inv, sc.cam_to_world)
+    rays = primary + shadow
+    return ({"value": round(rays * args.steps / el / 1e6, 3), "unit": "Mrays/s", "ms_per_step": round(1e3 * el / args.steps, 4),
+             "frames_in_flight": len(pipe.outs), "camera": "set_camera_transform(ry(0.25 * (k % 8) deg)) every step",
+             "rays_per_frame_last": rays}, img, sc2)
+
+
+def roofline(config, world, sync_kernel_ms, overlapped_kernel_ms, ms_per_step, primary):
     """The roofline object, recomputable from the files it names: unit counts of
     the RT_COUNT build (profiles/work_counts.json "gpu_executed") times bytes per unit, per
-    launch (this rank's share of the frame), over the launch's HIP-event duration."""
+    launch (this rank's share of the frame), over the launch's HIP-event duration with no other
+    frame in flight (the sync leg's rt_ray_trace launch; at N > 1, where there is no sync leg, the
+    step interval).  The frames-in-flight launches overlap each other, so their duration
+    (overlapped_kernel_ms) is reported beside it, not priced."""
+    kernel_ms = sync_kernel_ms if sync_kernel_ms else ms_per_step
     if not os.path.exists(COUNTS_FILE):
         return None
     with open(COUNTS_FILE) as f:
@@ -263,9 +378,10 @@ def roofline(config, world, kernel_ms, ms_per_step, primary):
     out = {"bound": "l1_l2_gather", "achieved": round(achieved, 1), "peak": PEAK_L2_GBS, "unit": "GB/s",
            "frac": round(achieved / PEAK_L2_GBS, 4), "traffic": None,
            "basis": "bytes the launch's traversal reads (units x bytes_per_unit, RT_COUNT build counts for the "
-                    "whole frame, x 1/world) / kernel_ms (HIP events on the launch stream); peak = L2 aggregate",
+                    "whole frame, x 1/world) / kernel_ms: " + ("the sync leg's launch (HIP events on its stream, one "
+                    "frame in flight)" if sync_kernel_ms else "the step interval") + "; peak = L2 aggregate",
            "units_per_frame": units, "bytes_per_unit": per, "bytes_per_launch": int(launch_bytes),
-           "kernel_ms": round(kernel_ms, 4),
+           "kernel_ms": round(kernel_ms, 4), "overlapped_launch_ms": round(overlapped_kernel_ms, 4),
            "counts_source": "profiles/work_counts.json [%s].gpu_executed" % config,
            "gather_ceiling": {"peak": GATHER_151MB_GBS, "unit": "GB/s", "frac": round(achieved / GATHER_151MB_GBS, 4),
                               "what": "uniformly random 1,152-B rows of a 151 MB table (MI355X_MICROARCH.md, "
@@ -278,9 +394,11 @@ def roofline(config, world, kernel_ms, ms_per_step, primary):
         if traffic:
             out["traffic"] = int(traffic)
             hbm = traffic / (kernel_ms * 1e-3) / 1e9
+            with open(PROFILE_SUMMARY) as f:
+                src = json.load(f).get("source", "")
             out["hbm"] = {"bytes_per_launch": int(traffic), "achieved": round(hbm, 1), "peak": PEAK_HBM_GBS,
                           "frac": round(hbm / PEAK_HBM_GBS, 4),
-                          "source": os.path.relpath(PROFILE_SUMMARY, ROOT) + " (2 x FETCH_SIZE + WRITE_SIZE)"}
+                          "source": os.path.relpath(PROFILE_SUMMARY, ROOT) + " (2 x FETCH_SIZE + WRITE_SIZE) " + src}
     if "child_tests_primary" in counts:
         # SURVEY.md 8(d)'s model priced on the REFERENCE's traversal (oracle count mode): the work
         # the reference's octree walk would read, per second of this kernel -- a rate of retiring
@@ -344,7 +462,7 @@ def cpu_info(threads):
             "cgroup_cpu_quota": cgroup_cpus(), "threads": threads}
 
 
-def cpu_leg(sc, st, gpu_img, threads, c5, check=True, baseline=True):
+def cpu_leg(sc, st, gpu_img, threads, c5, check=True, baseline=True, name="sphere1m", extra=None):
     """The CPU leg (rank 0, outside the timed region): the only place bench.py uses oracle/.
     * check: max |dpixel| of the GPU frame against the oracle's C restatement -- the full C4
       frame, or for C5 the row pairs of C5_CHECK_ROWS (oracle.render_row_set, downscaled);
@@ -353,7 +471,8 @@ def cpu_leg(sc, st, gpu_img, threads, c5, check=True, baseline=True):
       row loop, renderer.cpp:1082) on a bounded row sample, one warm-up pass then the median of
       5; the port's rate (oracle.c) beside it, or as the baseline when the
       reference library was not built."""
-    from oracle.bindings import Oracle, RefHarness
+    from oracle.bindings import Oracle, RefHarness, RefHarnessShipped
+    from raytracercpp_amd.scenes import C5_CHECK_ROWS   # the 16 output rows of test_c5_full_config_matches_oracle
     if not threads:
         threads = all_cores()
     env_threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
@@ -362,23 +481,37 @@ def cpu_leg(sc, st, gpu_img, threads, c5, check=True, baseline=True):
     dpx, check_desc, port = None, None, None
     o = Oracle(sc, st)
     if check or baseline:
-        if c5:
-            rows = [2 * r + k for r in C5_CHECK_ROWS for k in (0, 1)]
-            res = o.render_row_set(rows, nthreads=threads)
-            ref = Oracle.downscale(res.argb, rw, len(rows), 2).reshape(len(C5_CHECK_ROWS), W)
-            gpu = np.asarray(gpu_img).reshape(-1, W)[list(C5_CHECK_ROWS)]
-            check_desc = f"output rows {list(C5_CHECK_ROWS)} (internal rows {rows}) vs oracle.c, SSAA applied"
-            port_rays = res.counters["primary_rays"] + res.counters["shadow_rays"] + res.counters["reflection_rays"]
+        out_rows = (list(C5_CHECK_ROWS) if c5 else
+                    list(range(CHECK_STRIDE // 2, st.image_height, CHECK_STRIDE)) if name in SAMPLED_CHECK else None)
+        f = st.ssaa_factor if st.enable_ssaa else 1
+        rows = None if out_rows is None else [f * r + k for r in out_rows for k in range(f)]
+
+        def oracle_frame(orc):
+            """(the oracle's output rows to compare: the whole frame or the sampled rows, its run)"""
+            if rows is None:
+                rr = orc.render_rows(nthreads=threads)
+                return (Oracle.downscale(rr.argb, rw, rh, f) if f > 1 else rr.argb), rr
+            rr = orc.render_row_set(rows, nthreads=threads)
+            return (Oracle.downscale(rr.argb, rw, len(rows), f) if f > 1 else rr.argb).reshape(len(out_rows), W), rr
+
+        def gpu_rows(img):
+            return np.asarray(img) if out_rows is None else np.asarray(img).reshape(-1, W)[out_rows]
+        ref, res = oracle_frame(o)
+        if out_rows is not None:
+            check_desc = (f"output rows {out_rows} (internal rows {rows})" if c5 else
+                          f"every {CHECK_STRIDE}th output row ({len(out_rows)} rows from {out_rows[0]}, their "
+                          f"{len(rows)} internal rows)") + " vs oracle.c, SSAA applied"
         else:
-            res = o.render_rows(nthreads=threads)
-            ref = Oracle.downscale(res.argb, rw, rh, st.ssaa_factor) if st.enable_ssaa else res.argb
-            gpu = gpu_img
             check_desc = "whole frame vs oracle.c (the C restatement), SSAA applied"
-            port_rays = res.counters["primary_rays"] + res.counters["shadow_rays"]
+        port_rays = res.counters["primary_rays"] + res.counters["shadow_rays"] + res.counters["reflection_rays"]
         if check:
-            dpx = max_abs_dpixel(gpu, ref)
+            dpx = {"main": max_abs_dpixel(gpu_rows(gpu_img), ref)}
+            for k, (sck, imgk) in (extra or {}).items():
+                # the legs' last frames: the same scene (sync) against the same oracle frame, or the
+                # moved camera's own oracle frame
+                dpx[k] = max_abs_dpixel(gpu_rows(imgk), ref if sck is sc else oracle_frame(Oracle(sck, st))[0])
         port = {"value": round(port_rays / res.seconds / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-                "sample": ("the C5 check rows" if c5 else f"full C4 frame ({rw}x{rh} primary + "
+                "sample": ("the check rows" if out_rows is not None else f"full frame ({rw}x{rh} primary + "
                            f"{res.counters['shadow_rays']} shadow rays)") + f" in {res.seconds:.2f} s, oracle.c OpenMP x{threads}"}
     if not baseline:
         return None, dpx, check_desc
@@ -387,12 +520,12 @@ def cpu_leg(sc, st, gpu_img, threads, c5, check=True, baseline=True):
         return port, dpx, check_desc
     stride = 128 if c5 else 2
 
-    def ref_rate(nthr):
-        RefHarness.set_threads(nthr)
+    def ref_rate(nthr, H=RefHarness):
+        H.set_threads(nthr)
         passes = []
         rr = None
         for i in range(6):   # one warm-up pass, then 5 timed
-            rr = RefHarness.render_row_sample(sc, st, stride // 2, rh // stride, stride)
+            rr = H.render_row_sample(sc, st, stride // 2, rh // stride, stride)
             if i:
                 passes.append(rr.seconds)
         sec = float(np.median(passes))
@@ -413,6 +546,15 @@ def cpu_leg(sc, st, gpu_img, threads, c5, check=True, baseline=True):
                       f" rays, octree build excluded), reference TUs + OpenMP x{threads}; median of 5 passes "
                       f"after one warm-up ({', '.join(f'{p:.3f}' for p in passes)} s)",
             "port_value": port["value"] if port else None}
+    base["flags"] = "g++ -O3 -ffp-contract=off -fopenmp (oracle/Makefile REF_CXXFLAGS: the parity build)"
+    if RefHarnessShipped.available():
+        # the same TUs at the reference's shipped optimisation flags (tp2/CMakeLists.txt:105-117, made
+        # portable): the baseline a user of the reference would time
+        srate, spasses, _ = ref_rate(threads, RefHarnessShipped)
+        base["shipped_flags"] = {"value": round(srate, 3), "unit": "Mrays/s", "cores": threads,
+                                 "flags": "g++ -O3 -march=x86-64-v3 -mfma -fopenmp, default FP contraction "
+                                          "(oracle/Makefile ref_v3)",
+                                 "passes_s": [round(p, 3) for p in spasses]}
     if alt:
         base["omp_num_threads_env"] = alt
     base.update(cpu_info(threads))
@@ -420,13 +562,15 @@ def cpu_leg(sc, st, gpu_img, threads, c5, check=True, baseline=True):
 
 
 def dry_run(args, world):
-    """--dry-run: gloo ranks, each 'renders' its bands as a pattern keyed by the global row
-    (strips.rank_rows), frames in flight through strips.FramePipeline, the same all-gather and
-    re-assembly as the GPU path; rank 0 checks the frame against the pattern computed whole."""
+    """--dry-run: gloo ranks, each 'renders' its bands as a pattern keyed by the global row, frames in
+    flight through strips.FramePipeline, the same flat all-gather and in-step re-assembly on rank 0 as
+    the GPU path; after the warm-up, the cost-balanced band lists from synthetic band costs (a costly
+    cluster of bands, as the sphere's silhouette), summed over the ranks with the same all-reduce; rank
+    0 checks the last frame against the pattern computed whole."""
     import torch
     import torch.distributed as dist
     from raytracercpp_amd import scenes
-    from raytracercpp_amd.strips import FramePipeline, assemble, local_rows, rank_rows
+    from raytracercpp_amd.strips import FramePipeline, assign_bands, gather_index, list_rows, num_bands, rank_rows
     rank = int(os.environ.get("RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo")
@@ -434,16 +578,38 @@ def dry_run(args, world):
     _, st = scenes.CONFIGS[args.config]()
     W, H = st.image_width, st.image_height
     band = args.band_rows
-    nloc = local_rows(H, band, world)
-    rows = rank_rows(H, band, rank, world)
-    outs = [torch.zeros((nloc, W), dtype=torch.int32) for _ in range(max(1, args.inflight))]
+    nb = num_bands(H, band)
+    q = max(1, args.inflight)
 
-    def render(o, _stream):
-        o.copy_(torch.from_numpy(pattern_strip(rows, W)))
-    pipe = FramePipeline(render, outs, world, None, dist if world > 1 else None)
+    def make_pipe(lists):
+        nloc = len(lists[0]) * band if lists is not None else len(rank_rows(H, band, rank, world))
+        rows = list_rows(lists[rank], H, band, nloc // band) if lists is not None else rank_rows(H, band, rank, world)
+        outs = [torch.zeros((nloc, W), dtype=torch.int32) for _ in range(q)]
+        frames = [torch.zeros((H, W), dtype=torch.int32) for _ in range(q)]
+        idx = torch.as_tensor(gather_index(H, band, world, nloc, lists))
+
+        def render(o, _stream):
+            o.copy_(torch.from_numpy(pattern_strip(rows, W)))
+        if world == 1:
+            return FramePipeline(render, outs, 1), [o[:H] for o in outs], rows
+        asm = (lambda i, flat: torch.index_select(flat, 0, idx, out=frames[i])) if rank == 0 else None
+        return FramePipeline(render, outs, world, None, dist, assemble=asm), frames, rows
+    pipe, frames, rows = make_pipe(None)
     for _ in range(args.warmup):
         pipe.step()
     pipe.drain()
+    balanced = False
+    if world > 1 and args.balance:
+        mine = np.zeros(nb)
+        b = np.unique(rows[rows >= 0] // band)
+        mine[b] = 1.0 + 40.0 * ((b > 0.45 * nb) & (b < 0.55 * nb))
+        ct = torch.as_tensor(mine)
+        dist.all_reduce(ct)
+        pipe, frames, rows = make_pipe(assign_bands(ct.numpy(), world))
+        balanced = True
+        for _ in range(args.warmup):
+            pipe.step()
+        pipe.drain()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -455,8 +621,7 @@ def dry_run(args, world):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if rank == 0:
-        parts = [p.numpy() for p in pipe.parts[last]]
-        frame = assemble(parts, H, band)
+        frame = frames[last].numpy()
         expect = pattern_strip(np.arange(H), W)
         ms = 1e3 * elapsed / max(1, args.steps)
         print(json.dumps({"metric": "dry run: strip layout + gloo all-gather + re-assembly (no rendering)",
@@ -464,7 +629,8 @@ def dry_run(args, world):
                           "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
                           "scaling": "strong", "vs_baseline": None, "dtype": "u32", "data": "synthetic pattern strips",
                           "config": {"workload": "dry run", "image": [W, H], "band_rows": band,
-                                     "parallelism": f"image strips x{world}", "world_size": world},
+                                     "parallelism": f"image strips x{world}", "world_size": world,
+                                     "bands": "cost-balanced lists" if balanced else "interleaved b % N"},
                           "dry_run": True, "max_abs_dpixel": max_abs_dpixel(frame, expect)}), flush=True)
     if world > 1:
         dist.barrier()

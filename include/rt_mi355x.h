@@ -108,6 +108,9 @@ typedef struct rt_stats {
                                   rt_finish_accel; 0 until adopted); the octree's upload */
     int64_t host_builds;       /* host octree builds since rt_create, over every device of rt_set_devices (its
                                   helpers copy the lead's build: one per geometry change, renderer.cpp:214-224) */
+    int32_t wide_tree;         /* the wide BVH serving frames: 0 none (octree walk), 1 the quick tree built with the
+                                  octree, 2 the SAH tree adopted after the background build, -1 that build failed
+                                  (rt_finish_accel returned the error) and the quick tree keeps serving */
 } rt_stats;
 
 typedef struct rt_renderer rt_renderer;
@@ -278,18 +281,6 @@ int rt_get_internal(rt_renderer *r, uint32_t *argb, float *rgba, int32_t *hit_id
 
 int rt_get_stats(rt_renderer *r, rt_stats *out);
 
-/* Diagnostic builds (-DRT_PHASE_TIME=1, with RT_DEBUG_WAVES set in the environment when the
- * renderer is created): the last ray_trace's per-wave records of 8 words, n = 8 x waves values --
- * shader cycles per phase {tile setup, ray generation, primary query, shading, shadow query,
- * framebuffer, dequeue} of the plain kernel.  RT_EINVAL when no record buffer exists. */
-int rt_debug_read(rt_renderer *r, uint64_t *out, int64_t n);
-/* Diagnostics (no reference counterpart): the shader cycles of each 8x8 tile of the last launch --
- * rt_render / rt_ray_trace, or rt_render_bands_device (its launch-local tiles) -- (tile = ty * tiles_x
- * + tx; the heavy-first ordering's input; a split tile, the sum of its parts' cycles).
- * out == NULL: only the layout.  RT_EINVAL before a launch that records them (reflections, raster,
- * RT_HEAVY_FIRST=0). */
-int rt_tile_costs(rt_renderer *r, uint32_t *out, int64_t n, int32_t *tiles_x, int32_t *tiles_y);
-
 /* Image-strip rendering for multi-GPU (one process per GPU): renders the bands of
  * band_rows OUTPUT rows with band % nranks == rank into the device buffer d_out
  * (image_width x local_rows(...) ARGB32, final resolution, SSAA applied) on the
@@ -308,6 +299,19 @@ int rt_tile_costs(rt_renderer *r, uint32_t *out, int64_t n, int32_t *tiles_x, in
 int rt_local_rows(rt_renderer *r, int32_t band_rows, int32_t rank, int32_t nranks, int32_t *rows_out);
 int rt_render_bands_device(rt_renderer *r, int32_t band_rows, int32_t rank, int32_t nranks, uint32_t *d_out,
                            void *hip_stream);
+/* Cost-balanced strips: renders the listed OUTPUT bands (bands[i] in [0, ceil(image_height /
+ * band_rows)), each at most once) into d_out, local band i = rows [i * band_rows, (i + 1) *
+ * band_rows) of an image_width x (nbands * band_rows) ARGB32 buffer; otherwise as
+ * rt_render_bands_device (which renders the list rank, rank + nranks, ...), same stream contract.
+ * A list that differs from the stream's previous one waits for that stream's last launch. */
+int rt_render_band_list_device(rt_renderer *r, int32_t band_rows, const int32_t *bands, int32_t nbands,
+                               uint32_t *d_out, void *hip_stream);
+/* The cost of each OUTPUT band in the last band launch on hip_stream (NULL = the handle's stream):
+ * the shader cycles of its 8x8 tiles (a tile is charged to the band of its first row), written to
+ * costs[global band] for the bands that launch rendered; the others are left as they are, so that
+ * ranks can sum their vectors.  Waits for that launch.  nbands >= ceil(image_height / band_rows).
+ * RT_EINVAL before a band launch that records tile costs (reflections, raster, RT_HEAVY_FIRST=0). */
+int rt_band_costs(rt_renderer *r, void *hip_stream, double *costs, int32_t nbands);
 
 /* BVH::intersect (bvh.cpp:68-71; OctreeNode::intersect, bvh.h:212-287) for n arbitrary
  * rays (origins / directions [n][3]): the closest-hit query trace_ray and is_shadowed
@@ -328,30 +332,6 @@ int rt_trace_rays(rt_renderer *r, const float *orig, const float *dir, int64_t n
  * reflection ray counts. */
 int rt_trace_ray(rt_renderer *r, const float *orig, const float *dir, int64_t n, int32_t current_recursion_depth,
                  float *rgba, int32_t *hit_src, float *t, uint8_t *intersection_found, uint8_t *shadowed);
-
-/* The frames' wide-BVH query on the GPU (kernels.hip wide_query_kernel), with its
- * status, for n rays: the device build (hardware reciprocal / square root, the GPU-computed risk
- * words of the current camera and light) of what rt_wbvh_query_ex runs on the host, answering
- * BVH::intersect (bvh.h:212-287) through the resident wide BVH and its certificate.  kind 0: plain
- * rays (no risk words: reflection rays, rt_trace_ray); 1: camera rays (a ray whose origin equals the
- * camera position bitwise reads the camera's words, as the frame's primary rays do); 2: each ray is
- * (hit point p in orig, normal n in dir), traced as is_shadowed's ray o = p + 1e-4 n, d =
- * normalize(light - p) (renderer.cpp:340-402) with the light's words when the frame's would apply.
- * o_out / d_out [n][3]: the rays queried.  status: 0 certified miss, 1 certified hit (tri_id / t /
- * u / v = BVH::intersect's record; it returned true), 2 not certified (a frame takes the exact
- * octree walk), each as a closest-hit query over the whole line.  shadowed (kind 2): the frame's
- * own decision through its segment query, 0 lit, 1 shadowed, 2 not decided (octree walk); 2 for the
- * other kinds.  Waits for the wide BVH's background build (rt_finish_accel); with no wide BVH
- * (exact mode, RT_WBVH=0, a scene scale outside its margins) every status is 2. */
-int rt_wide_query(rt_renderer *r, const float *orig, const float *dir, int64_t n, int32_t kind, float *o_out,
-                  float *d_out, int32_t *status, int32_t *tri_id, float *t, float *u, float *v, uint8_t *shadowed);
-/* Diagnostics: the current frame's grazing-risk words (8 per wide-BVH node, wbvh.hpp wrisk_pack):
- * src 0 as the GPU computes them (wide_risk_kernel), src 1 by the host walk (wbvh_risk_host) over
- * the same resident wide BVH.  *count = the number of words; out (cap words) may be null to query
- * it.  violations (optional): the words checked against the tree (wbvh.hpp check_risk_words: every
- * at-risk triangle's key and octree leaf held by each entry above it).  Waits for the wide BVH's
- * build; RT_ESTATE when there is none. */
-int rt_risk_words(rt_renderer *r, int32_t src, uint64_t *out, int64_t cap, int64_t *count, int64_t *violations);
 
 /* GPU durations (ms) of the ray-trace kernel of the last n rt_render_bands_device
  * calls, from HIP events recorded around each launch on its stream (waits for them). */
@@ -377,37 +357,8 @@ int rt_obj_counts(const rt_obj *o, int64_t *ntri, int32_t *nmat, int32_t *has_uv
 int rt_obj_fetch(const rt_obj *o, float *tri9, int32_t *mat, float *uv6, float *mats16);
 void rt_obj_close(rt_obj *o);
 
-/* ---- Host octree build (BVH::BVH, tp2/projets/bvh.cpp:19-66; bvh.h:141-210), no GPU ----
- * Builds and flattens the octree over tri9 and returns a 64-bit FNV-1a digest of the
- * flattened nodes, triangle records and slot -> triangle map, and stats[7] =
- * {inner, leaves, empty_leaves, max_leaf, max_depth, nodes, flattened levels}.
- * builder 0: the parallel level-by-level build the renderer uses; 1: the reference's
- * one-insert-at-a-time algorithm restated.  *ms (optional) gets the build time. */
-int rt_octree_digest(const float *tri9, int64_t n, int32_t max_depth, int32_t leaf_max_obj_count, int32_t builder,
-                     uint64_t *digest, int64_t stats[7], float *ms);
-
-/* ---- Wide-BVH certified closest hit, on the host, no GPU ----
- * Builds the octree over tri9 and the 4-wide SAH BVH over its triangle records, then runs,
- * for each ray, the traversal and certificate the primary-ray kernel runs (wbvh.hpp).
- * status[i]: 0 = certified no hit (BVH::intersect returns false, record untouched),
- * 1 = certified hit (id / t / u / v = BVH::intersect's record, bvh.h:212-287, returns true),
- * 2 = not certified (the kernel re-traces it through the octree).  stats[8] = {wide nodes,
- * leaves, max leaf, depth, node visits, triangle tests, structural violations (check_wbvh),
- * SAH cost x 1000}; ms[2] (optional) = {octree build, wide-BVH build} milliseconds. */
-int rt_wbvh_query(const float *tri9, int64_t n, int32_t max_depth, int32_t leaf_max_obj_count, const float *orig,
-                  const float *dir, int64_t nrays, int32_t *status, int32_t *id, float *t, float *u, float *v,
-                  int64_t stats[8], float *ms);
-/* The same with the frame's grazing-risk bits of a camera and / or a light point:
- * rays whose origin equals cam (bitwise) read the camera's bits; with shadow_rays = 1 (light
- * required) each ray is given as (hit point p in orig, normal n in dir) and becomes is_shadowed's
- * ray o = p + 1e-4 n, d = normalize(light - p) (renderer.cpp:340-402), reading the light's bits when
- * its segment bound allows, and is answered as a closest-hit query over the whole line.  o_out /
- * d_out (optional, 3 floats per ray) receive the rays queried, ray_nodes (optional) each query's
- * wide-node visits (the retry's included). */
-int rt_wbvh_query_ex(const float *tri9, int64_t n, int32_t max_depth, int32_t leaf_max_obj_count, const float *orig,
-                     const float *dir, int64_t nrays, const float *cam, const float *light, int32_t shadow_rays,
-                     float *o_out, float *d_out, int32_t *status, int32_t *id, float *t, float *u, float *v,
-                     int64_t stats[8], float *ms, int32_t *ray_nodes);
+/* Diagnostics (tile costs, per-wave records, the wide query and its risk words on the GPU, the host
+ * octree digest and wide-BVH query) are declared in rt_mi355x_diag.h; the same library exports them. */
 
 #ifdef __cplusplus
 }

@@ -329,17 +329,18 @@ class RefHarness:
     """oracle/_ref/libref_harness.so (reference TUs).  Raises if not built."""
 
     _lib = None
+    SO = REF_SO
 
     @classmethod
     def available(cls):
-        return os.path.exists(REF_SO)
+        return os.path.exists(cls.SO)
 
     @classmethod
     def lib(cls):
         if cls._lib is None:
-            if not os.path.exists(REF_SO):
-                raise RuntimeError(f"{REF_SO} missing: run `make -C oracle ref` where /root/reference exists")
-            L = C.CDLL(REF_SO)
+            if not os.path.exists(cls.SO):
+                raise RuntimeError(f"{cls.SO} missing: run `make -C oracle ref` where /root/reference exists")
+            L = C.CDLL(cls.SO)
             L.ref_camera_matrices.argtypes = [C.c_float, C.c_float, C.c_float, C.c_float, _f32p, _f32p]
             L.ref_make_transform.argtypes = [C.c_int, C.c_float, C.c_float, C.c_float, _f32p]
             L.ref_compose.argtypes = [_f32p, _f32p, _f32p]
@@ -531,3 +532,13 @@ class RefHarness:
         if rc != 0:
             raise ValueError("size not divisible by factor")
         return out
+
+
+class RefHarnessShipped(RefHarness):
+    """oracle/_ref/libref_harness_v3.so: the same reference TUs and harness built with the reference's
+    shipped optimisation flags as far as they are portable (tp2/CMakeLists.txt:105-117: -O3 with
+    -march=native -mfma; here -march=x86-64-v3 -mfma, GCC's default contraction): a CPU-baseline timing
+    only, never a parity checker (contracted FMAs change a few pixels)."""
+
+    _lib = None
+    SO = os.path.join(os.path.dirname(REF_SO), "libref_harness_v3.so")

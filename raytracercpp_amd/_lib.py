@@ -56,6 +56,7 @@ class RtStats(C.Structure):
         ("render_width", C.c_int32), ("render_height", C.c_int32), ("seg_scale", C.c_float),
         ("work", C.c_int64 * 4), ("work_wide", C.c_int64 * 4), ("uncertified", C.c_int64 * 6),
         ("wave_steps", C.c_int64 * 6), ("build_split_ms", C.c_float * 4), ("host_builds", C.c_int64),
+        ("wide_tree", C.c_int32),
     ]
 
     def as_dict(self):
@@ -117,6 +118,8 @@ SIGNATURES = {
     "rt_get_stats": (C.c_int, [_H, C.POINTER(RtStats)]),
     "rt_local_rows": (C.c_int, [_H, C.c_int32, C.c_int32, C.c_int32, _i32p]),
     "rt_render_bands_device": (C.c_int, [_H, C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]),
+    "rt_render_band_list_device": (C.c_int, [_H, C.c_int32, _i32p, C.c_int32, C.c_void_p, C.c_void_p]),
+    "rt_band_costs": (C.c_int, [_H, C.c_void_p, C.POINTER(C.c_double), C.c_int32]),
     "rt_trace_rays": (C.c_int, [_H, _f32p, _f32p, C.c_int64, _i32p, _f32p, _f32p, _f32p, _u8p]),
     "rt_trace_ray": (C.c_int, [_H, _f32p, _f32p, C.c_int64, C.c_int32, _f32p, _i32p, _f32p, _u8p, _u8p]),
     "rt_wide_query": (C.c_int, [_H, _f32p, _f32p, C.c_int64, C.c_int32, _f32p, _f32p, _i32p, _i32p, _f32p, _f32p, _f32p,

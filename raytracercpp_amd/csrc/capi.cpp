@@ -7,7 +7,7 @@
 #include <new>
 #include <string>
 
-#include "../../include/rt_mi355x.h"
+#include "../../include/rt_mi355x_diag.h"   // (includes rt_mi355x.h)
 #include "host_scene.hpp"
 #include "octree.hpp"
 #include "wbvh.hpp"
@@ -309,6 +309,18 @@ int rt_render_bands_device(rt_renderer* r, int32_t band_rows, int32_t rank, int3
     return guarded(R(r), [&] {
         return R(r)->render_bands_device(band_rows, rank, nranks, d_out, reinterpret_cast<hipStream_t>(hip_stream));
     });
+}
+
+int rt_render_band_list_device(rt_renderer* r, int32_t band_rows, const int32_t* bands, int32_t nbands, uint32_t* d_out,
+                               void* hip_stream)
+{
+    return guarded(R(r), [&] {
+        return R(r)->render_band_list_device(band_rows, bands, nbands, d_out, reinterpret_cast<hipStream_t>(hip_stream));
+    });
+}
+int rt_band_costs(rt_renderer* r, void* hip_stream, double* costs, int32_t nbands)
+{
+    return guarded(R(r), [&] { return R(r)->band_costs(reinterpret_cast<hipStream_t>(hip_stream), costs, nbands); });
 }
 
 int rt_trace_rays(rt_renderer* r, const float* orig, const float* dir, int64_t n, int32_t* tri_id, float* t,

@@ -1703,13 +1703,14 @@ __device__ __forceinline__ void tile_xy(const KParams& P, int tile, int& tx, int
     ty = q;
 }
 
-// Global internal row of a launch-local row (interleaved bands across ranks).
+// Global internal row of a launch-local row (interleaved bands across ranks, or a band list).
 __device__ __forceinline__ int global_row(const KParams& P, int lr)
 {
     if (P.nranks == 1)
         return lr;   // (band * 1 + 0) * band_rows + lr - band * band_rows
     int band = lr / P.band_rows;
-    return (band * P.nranks + P.rank) * P.band_rows + (lr - band * P.band_rows);
+    const int g = P.band_map ? ldg(P.band_map + band) : band * P.nranks + P.rank;
+    return g * P.band_rows + (lr - band * P.band_rows);
 }
 
 // The persistent tile queue, sharded: shard s owns the tile rows [s Y / 8, (s + 1) Y / 8)
@@ -1746,6 +1747,11 @@ struct BlockQueue {
     int base[4], sh[4];
     int heavy_done;   // the heavy list is exhausted (any wave may set it)
     int split_done;   // the split tiles' parts are exhausted
+    // the block's share of the launch's tile-cost sum and max (KParams::tile_stats; the last wave of
+    // the block to finish adds it to the launch's)
+    unsigned long long cost_sum;
+    unsigned int cost_max;
+    int waves_done;
 };
 __shared__ BlockQueue g_bq;
 
@@ -1757,8 +1763,33 @@ __device__ __forceinline__ void tile_queue_init()
         g_bq.empty = 0;
         g_bq.heavy_done = 0;
         g_bq.split_done = 0;
+        g_bq.cost_sum = 0;
+        g_bq.cost_max = 0;
+        g_bq.waves_done = 0;
     }
     __syncthreads();
+}
+
+// A tile's (or a split part's: its cost x G stands for the tile's in the max) cost into the block's sums.
+__device__ __forceinline__ void tile_stats_add(uint32_t c, uint32_t cmax)
+{
+    __hip_atomic_fetch_add(&g_bq.cost_sum, (unsigned long long)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_max(&g_bq.cost_max, cmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// At a wave's exit: the last wave of the block adds the block's sums to the launch's (2 global atomics
+// per block instead of one per tile; heavy_prep_kernel reads them for the next launch).
+__device__ __forceinline__ void tile_stats_flush(const KParams& P, int lane)
+{
+    if (!P.tile_stats || lane != 0)
+        return;
+    const int k = __hip_atomic_fetch_add(&g_bq.waves_done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (k != (int)(blockDim.x >> 6) - 1)
+        return;
+    const unsigned long long s = __hip_atomic_load(&g_bq.cost_sum, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const unsigned int m = __hip_atomic_load(&g_bq.cost_max, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (s) atomicAdd(P.tile_stats, s);
+    if (m) atomicMax(P.tile_stats + 1, (unsigned long long)m);
 }
 
 __device__ __forceinline__ int tile_queue_next_shards(const KParams& P);
@@ -1776,7 +1807,7 @@ __device__ __forceinline__ int tile_queue_next(const KParams& P)
             if (lane == 0)
                 t = atomicAdd(P.heavy_ctr + 1, 1);
             t = __builtin_amdgcn_readfirstlane(t);
-            if (t < ldg(P.heavy_ctr))
+            if (t < min(ldg(P.heavy_ctr), P.tiles_x * P.tiles_y / 16))   // (heavy_prep_kernel counts past its cap)
                 return ldg(P.heavy_list + t);
             if (lane == 0)
                 __hip_atomic_store(&g_bq.heavy_done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1868,8 +1899,8 @@ __device__ __forceinline__ void set_wave_prio(int level)
 // are non-negative: a shift) and written by the block's first lane, as downscale_kernel.
 // G > 1 (trace_split_part): pixel i of the wave's C-wide block is held by lanes G i .. G i + G - 1
 // (f <= the block's columns and rows, checked on the host).
-template <int G = 1, int C = 8>
-__device__ __forceinline__ void downscale_tile(const KParams& P, int lane, int lr, int px, uint32_t c)
+template <int G = 1, int C0 = 8>
+__device__ __forceinline__ void downscale_tile(const KParams& P, int lane, int lr, int px, uint32_t c, int C = C0)
 {
     int r = (int)((c >> 16) & 0xffu), g = (int)((c >> 8) & 0xffu), b = (int)(c & 0xffu);
     const int f = 1 << P.ds_shift;
@@ -1932,19 +1963,22 @@ __device__ __forceinline__ void trace_split_part(const KParams& P, uint2* lv, in
 {
     static_assert(G > 1 && G <= 8 && (G & (G - 1)) == 0, "2, 4 or 8 lanes per pixel");
     const int cap = P.tiles_x * P.tiles_y / 16;   // (heavy_prep_kernel: the split list at list + cap)
-    const int tq = ldg(P.heavy_list + cap + t / G), part = t % G;
+    const int np = P.split_parts;                 // parts per tile: G (every lane busy) or 2G (half the lanes)
+    const int tq = ldg(P.heavy_list + cap + t / np), part = t % np;
     const int tile = tq & 0x0fffffff;
     set_wave_prio(tq >> 28);
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     int tx, ty;
     tile_xy(P, tile, tx, ty);
-    // part p: columns (p % (8 / C)) C .. + C, rows (p / (8 / C)) R .. + R of the tile (C x R = 64 / G pixels)
-    constexpr int C = G == 8 ? 4 : 8, R = 64 / G / C;
+    // part p: columns (p % (8 / C)) C .. + C, rows (p / (8 / C)) R .. + R of the tile (C x R = 64 / np
+    // pixels: C = 8 and R = 64 / np / 8 down to 16 pixels, then 4 x 2 and 2 x 2 blocks)
+    const int npix = 64 / np;
+    const int C = npix >= 16 ? 8 : npix / 2, R = npix / C;
     const int pl = lane / G;   // the lane's pixel among the part's, row-major C wide
     const int px = tx * 8 + (part % (8 / C)) * C + pl % C;
     const int lr = ty * 8 + (part / (8 / C)) * R + pl / C;
     const int py = lr < P.local_rows ? global_row(P, lr) : P.rh;
-    if (px < P.rw && py < P.rh) {   // (the same for the G lanes of a pixel)
+    if (pl < npix && px < P.rw && py < P.rh) {   // (the same for the G lanes of a pixel)
         const v3 cam = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
         const v3 rd = camera_dir(P, px, py, cam);
         unsigned ns = 0, nr = 0;
@@ -1953,7 +1987,7 @@ __device__ __forceinline__ void trace_split_part(const KParams& P, uint2* lv, in
             nshadow += ns;   // (one count per pixel)
         const size_t o = (size_t)lr * P.rw + px;
         const uint32_t c = color_to_argb(po.color);
-        if (P.ds_out) downscale_tile<G, C>(P, lane, lr, px, c);
+        if (P.ds_out) downscale_tile<G>(P, lane, lr, px, c, C);
         if ((lane & (G - 1)) == 0) {
             if (P.argb) P.argb[o] = c;
             if (P.rgba) P.rgba[o] = make_float4(po.color.r, po.color.g, po.color.b, po.alpha);
@@ -1963,8 +1997,11 @@ __device__ __forceinline__ void trace_split_part(const KParams& P, uint2* lv, in
         }
     }
     const uint64_t c = __builtin_amdgcn_s_memtime() - t0;
-    if (lane == 0)
-        atomicAdd(P.tile_cost + tile, c > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)c);
+    if (lane == 0) {
+        const uint32_t c32 = c > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)c;
+        atomicAdd(P.tile_cost + tile, c32);
+        tile_stats_add(c32, c32 > 0xFFFFFFFFu / G ? 0xFFFFFFFFu : c32 * G);
+    }
 }
 
 // Renderer::ray_trace (renderer.cpp:1068-1116): one lane per pixel, one wave
@@ -2010,7 +2047,7 @@ __global__ __launch_bounds__(BLOCK, OCT ? RT_OCC_OCT : PLAIN ? RT_OCC_PLAIN : RT
             if (lane == 0)
                 t = atomicAdd(P.heavy_ctr + 2, 1);
             t = __builtin_amdgcn_readfirstlane(t);
-            if (t < SPLIT_G * ldg(P.heavy_ctr + 3)) {
+            if (t < P.split_parts * min(ldg(P.heavy_ctr + 3), P.tiles_x * P.tiles_y / 16)) {
                 trace_split_part<SPLIT_G>(P, lv, t, lane, nshadow);
                 continue;
             }
@@ -2053,10 +2090,14 @@ __global__ __launch_bounds__(BLOCK, OCT ? RT_OCC_OCT : PLAIN ? RT_OCC_PLAIN : RT
         if (PLAIN) PH_MARK(5);
         if (P.tile_cost) {   // the tile's shader cycles (heavy-first order of the next launch)
             const uint64_t c = __builtin_amdgcn_s_memtime() - tile_t0;
-            if (lane == 0)
-                P.tile_cost[tile] = c > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)c;
+            if (lane == 0) {
+                const uint32_t c32 = c > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)c;
+                P.tile_cost[tile] = c32;
+                tile_stats_add(c32, c32);
+            }
         }
     }
+    tile_stats_flush(P, lane);
 #if RT_PHASE_TIME
     if (PLAIN) {
         PH_MARK(0);   // the final (empty) dequeues
@@ -2820,6 +2861,10 @@ __device__ __forceinline__ float edge_fn(float px, float py, v3 a, v3 b)
 __device__ __forceinline__ int local_row(const KParams& P, int py)
 {
     int band = py / P.band_rows;
+    if (P.band_inv) {
+        const int lb = ldg(P.band_inv + band);
+        return lb < 0 ? -1 : lb * P.band_rows + (py - band * P.band_rows);
+    }
     if (band % P.nranks != P.rank)
         return -1;
     return (band / P.nranks) * P.band_rows + (py - band * P.band_rows);
@@ -3512,10 +3557,12 @@ __global__ __launch_bounds__(256) void wide_gather_kernel(const GTri* __restrict
 
 // dynamic LDS of the traversal kernels: the octree level stack, or the wide-BVH stack
 // (the same memory; a lane uses one at a time)
-size_t lds_bytes(const KParams& P)
+// plain_pixel: the launch runs trace_pixel<false, true> (the plain ray_trace_kernel instances and their
+// split parts), whose pixel values wait in LDS_SAVE_ENTRIES more slots across the shadow query; the
+// other kernels do not take them (32 -> 38 KB per block cost the 5-wave kernels a block)
+size_t lds_bytes(const KParams& P, bool plain_pixel = false)
 {
-    // the traversal stacks, then the plain pixel's values held across its shadow query (trace_pixel)
-    return (size_t)(lds_save_slot(P) + LDS_SAVE_ENTRIES) * BLOCK * sizeof(uint2);
+    return (size_t)(lds_save_slot(P) + (plain_pixel ? LDS_SAVE_ENTRIES : 0)) * BLOCK * sizeof(uint2);
 }
 
 }  // namespace rt
@@ -3578,66 +3625,57 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_trace_colo
 // layout: the tiles costing at least max(4 x the mean, the largest / 8), at most ntiles / 16 of them.
 // With group G > 1, those that also cost at least split x the launch's mean cycles per wave (the sum
 // over nwaves, the plain kernel's waves: a tile that would outlast the mean wave) go to the split list
-// list[cap .. cap + ctr[3]) of trace_split_part (cap = ntiles / 16), the others to list[0 ..
-// ctr[0]) of ray_trace_kernel.  One block; it also clears the bits and resets the tickets.
+// list[cap .. cap + ctr[3]) of trace_split_part (cap = ntiles / 16), the others to list[0 .. ctr[0])
+// of ray_trace_kernel (the consumers clamp the counts to cap).  One lane per tile over the whole grid:
+// the sum and the largest cost come from the previous launch itself (KParams::tile_stats, stats_prev),
+// the list slots from one atomic per wave and list, each wave writes its 64 tiles' two bit words, and
+// block 0 clears the sums the coming launch accumulates (stats_next).  ctr[] (in the launch's counter
+// words) was zeroed with them.  r05 ran this as one 1,024-thread block: 83-91 us per launch at C4.
 #ifndef RT_HEAVY_PRIO
 #define RT_HEAVY_PRIO 1   // heavy tiles at raised wave priority (set_wave_prio)
 #endif
-__global__ __launch_bounds__(1024) void heavy_prep_kernel(uint32_t* __restrict__ cost, int ntiles, int32_t* list,
-                                                          uint32_t* bits, int32_t* ctr, int nwaves, float split,
-                                                          int group)
+__global__ __launch_bounds__(256) void heavy_prep_kernel(uint32_t* __restrict__ cost, int ntiles, int32_t* list,
+                                                         uint32_t* bits, int32_t* ctr,
+                                                         const unsigned long long* stats_prev,
+                                                         unsigned long long* stats_next, int nwaves, float split,
+                                                         int group)
 {
-    __shared__ unsigned long long sum;
-    __shared__ unsigned int mx;
-    __shared__ int cnt, cnt2;
-    if (threadIdx.x == 0) {
-        sum = 0;
-        mx = 0;
-        cnt = 0;
-        cnt2 = 0;
-    }
-    __syncthreads();
-    unsigned long long s = 0;
-    unsigned int m = 0;
-    for (int i = threadIdx.x; i < ntiles; i += 1024) {
-        s += cost[i];
-        m = max(m, cost[i]);
-    }
-    atomicAdd(&sum, s);
-    atomicMax(&mx, m);
-    for (int i = threadIdx.x; i < (ntiles + 31) / 32; i += 1024)
-        bits[i] = 0u;
-    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x < 2)
+        stats_next[threadIdx.x] = 0ull;
+    const unsigned long long sum = stats_prev[0];
+    const unsigned int mx = (unsigned int)min(stats_prev[1], 0xFFFFFFFFull);
     const unsigned long long mean = ntiles > 0 ? sum / (unsigned long long)ntiles : 0;
     const unsigned long long thr = max(4 * mean, (unsigned long long)(mx / 8));
     // split: at least split x the mean cycles per wave (never, without a group)
     const unsigned long long thr2 = group > 1 && nwaves > 0 ? max(thr, (unsigned long long)((double)split * (double)sum / nwaves))
                                                             : ~0ull;
     const int cap = ntiles / 16;
-    if (mx > 0)
-        for (int i = threadIdx.x; i < ntiles; i += 1024)
-            if (cost[i] >= thr && cost[i] > 0) {
-                const bool two = cost[i] >= thr2;
-                const int k = atomicAdd(two ? &cnt2 : &cnt, 1);
-                if (k < cap) {
-                    // the wave's issue priority while it traces the tile (bits 28-29, ray_trace_kernel)
-                    const int prio = !RT_HEAVY_PRIO || ntiles >= (1 << 28) ? 0
-                                     : cost[i] >= mx / 2               ? 3
-                                     : cost[i] >= mx / 4               ? 2
-                                                                       : 1;
-                    list[two ? cap + k : k] = i | (prio << 28);
-                    atomicOr(bits + (i >> 5), 1u << (i & 31));
-                    if (two)
-                        cost[i] = 0u;   // (the parts add theirs; ray_trace_kernel stores a tile's own)
-                }
-            }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        ctr[0] = min(cnt, cap);
-        ctr[1] = 0;
-        ctr[2] = 0;
-        ctr[3] = min(cnt2, cap);
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int lane = (int)(threadIdx.x & 63);
+    const uint32_t c = i < ntiles ? cost[i] : 0u;
+    const bool heavy = mx > 0 && c >= thr && c > 0;
+    const bool two = heavy && c >= thr2;
+    const uint64_t b1 = __ballot(heavy && !two), b2 = __ballot(two);
+    int base1 = 0, base2 = 0;
+    if (lane == 0) {
+        if (b1) base1 = atomicAdd(ctr, __popcll(b1));
+        if (b2) base2 = atomicAdd(ctr + 3, __popcll(b2));
     }
+    base1 = __builtin_amdgcn_readfirstlane(base1);
+    base2 = __builtin_amdgcn_readfirstlane(base2);
+    const uint64_t below = (1ull << lane) - 1ull;   // (lane < 64)
+    const int k = two ? base2 + __popcll(b2 & below) : base1 + __popcll(b1 & below);
+    const bool listed = heavy && k < cap;
+    if (listed) {
+        // the wave's issue priority while it traces the tile (bits 28-29, ray_trace_kernel)
+        const int prio = !RT_HEAVY_PRIO || ntiles >= (1 << 28) ? 0 : c >= mx / 2 ? 3 : c >= mx / 4 ? 2 : 1;
+        list[two ? cap + k : k] = i | (prio << 28);
+        if (two)
+            cost[i] = 0u;   // (the parts add theirs; ray_trace_kernel stores a tile's own)
+    }
+    const uint64_t bl = __ballot(listed);
+    if ((lane & 31) == 0 && i < ntiles)
+        bits[i >> 5] = (uint32_t)(bl >> lane);
 }
 
 // ---- host-side launch wrappers (called from renderer.cpp) ----
@@ -3652,11 +3690,15 @@ static int plain_blocks(const rt::KParams& P)
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_heavy_prep(const rt::KParams* P, uint32_t* cost,
                                                                                  int ntiles, int32_t* list,
                                                                                  uint32_t* bits, int32_t* ctr,
+                                                                                 const unsigned long long* stats_prev,
+                                                                                 unsigned long long* stats_next,
                                                                                  float split, int group,
                                                                                  hipStream_t stream)
 {
-    hipLaunchKernelGGL(heavy_prep_kernel, dim3(1), dim3(1024), 0, stream, cost, ntiles, list, bits, ctr,
-                       plain_blocks(*P) * rt::WAVES_PER_BLOCK, split, group);
+    if (ntiles <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(heavy_prep_kernel, dim3((ntiles + 255) / 256), dim3(256), 0, stream, cost, ntiles, list, bits,
+                       ctr, stats_prev, stats_next, plain_blocks(*P) * rt::WAVES_PER_BLOCK, split, group);
     return hipGetLastError();
 }
 
@@ -3669,8 +3711,8 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(
         blocks = P->max_blocks;
     if (blocks < 1)
         return hipSuccess;
-    size_t lds = rt::lds_bytes(*P);
     const bool plain = !P->has_reflection && P->plain && !P->zbuf && !P->nbuf;
+    size_t lds = rt::lds_bytes(*P, plain);
     if (P->has_reflection)
         hipLaunchKernelGGL((rt::ray_trace_kernel<true, false>), dim3(blocks), dim3(rt::BLOCK), lds, stream, *P);
     else if (plain) {

@@ -110,7 +110,11 @@ struct KParams {
     // image: render size (internal, after the SSAA factor) and this launch's rows
     int32_t rw, rh;
     int32_t band_rows;        // internal rows per band
-    int32_t nranks, rank;     // bands b with b % nranks == rank are rendered
+    int32_t nranks, rank;     // bands b with b % nranks == rank are rendered (band_map == nullptr)
+    // a band list (rt_render_band_list_device, cost-balanced strips): local band i is the global band
+    // band_map[i]; band_inv[b] = the local band of global band b, or -1 (nullptr: the interleaved layout)
+    const int32_t* band_map;
+    const int32_t* band_inv;
     int32_t local_rows;       // rows in this launch's (padded) local buffers
     int32_t tiles_x, tiles_y; // 8x8 tiles over (rw, local_rows)
     int32_t max_blocks;       // persistent grid size (CUs x resident blocks per CU)
@@ -121,6 +125,7 @@ struct KParams {
     // launch's slowest tiles of the same layout, flagged in heavy_bits) are dequeued first, by the
     // ticket heavy_ctr[1]; a list entry is the tile | its wave priority level << 28
     uint32_t* tile_cost;
+    unsigned long long* tile_stats;   // this launch's sum and max of the tile costs (the next heavy_prep's input)
     const int32_t* heavy_list;
     const uint32_t* heavy_bits;
     int32_t* heavy_ctr;
@@ -128,6 +133,7 @@ struct KParams {
     // 64 / G pixels with G lanes per pixel (kernels.hip trace_split_part, by the ticket heavy_ctr[2]; the
     // parts add their cycles to tile_cost)
     int32_t heavy_group;
+    int32_t split_parts;      // parts per split tile: G (64 / G pixels each, every lane busy) or 2 G (half)
 
     // outputs, indexed by local_row * rw + px (nullptr = not requested)
     uint32_t* argb;

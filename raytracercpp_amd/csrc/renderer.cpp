@@ -18,6 +18,8 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_heavy_prep(const rt::KParams* P, uint32_t* cost,
                                                                                  int ntiles, int32_t* list,
                                                                                  uint32_t* bits, int32_t* ctr,
+                                                                                 const unsigned long long* stats_prev,
+                                                                                 unsigned long long* stats_next,
                                                                                  float split, int group,
                                                                                  hipStream_t stream);
 
@@ -121,6 +123,10 @@ Knobs Knobs::from_env()
     }
     if (const char* v = getenv("RT_HEAVY_SPLIT"))
         k.heavy_split = std::max(0.0f, (float)atof(v));
+    if (const char* v = getenv("RT_HEAVY_SPLIT_EXP"))
+        k.heavy_split_exp = std::max(0.0f, (float)atof(v));
+    if (const char* v = getenv("RT_SPLIT_PARTS"))
+        k.split_parts = atoi(v) == 2 * SPLIT_G ? 2 * SPLIT_G : SPLIT_G;
     if (const char* v = getenv("RT_REFL_DEFER"))   // loop iterations before a reflection query is deferred
         k.refl_defer = std::max(0, atoi(v));
     {
@@ -694,7 +700,11 @@ int Renderer::poll_accel(bool wait)
     accel_thread_.join();
     hipSetDevice(device_);
     if (accel_state_.load() == 3) {
+        // the SAH tree was not built or uploaded: the resident tree (the quick one, if any) keeps serving
+        // frames for this geometry, and rt_stats.wide_tree says so until the next geometry change
         accel_state_.store(0);
+        wb_next_ = WBvh();
+        wide_tree_ = wide_ready_ ? -1 : 0;
         return fail(RT_EHIP, accel_err_);
     }
     accel_state_.store(0);
@@ -712,6 +722,7 @@ int Renderer::poll_accel(bool wait)
         d_wlinks_.swap(d_wlinks2_);
     }
     wide_ready_ = !wb_.nodes.empty();
+    wide_tree_ = wide_ready_ ? 2 : 0;
     if (wide_ready_ && reserve_risk(wb_.nodes.size()) != RT_OK)
         return RT_EHIP;
     risk_valid_ = false;
@@ -895,8 +906,10 @@ int Renderer::ensure_device_scene()
         tri9_dirty_ = true;
         build_ms_ = ms_since(t0);
         build_split_ms_[1] = 0.0f;
+        wide_tree_ = 0;
         if (!wb_.nodes.empty()) {
             wide_ready_ = true;
+            wide_tree_ = 1;
             int rc = reserve_risk(wb_.nodes.size());
             if (rc != RT_OK)
                 return rc;
@@ -1690,6 +1703,44 @@ int Renderer::tile_costs(uint32_t* out, int64_t n, int32_t* tiles_x, int32_t* ti
     return e == hipSuccess ? RT_OK : hip_fail(e, "tile_costs");
 }
 
+// Per global output band, the cycles of its tiles in the slot's last launch (a tile is charged to the
+// band of its first internal row; the heavy-first order's tile costs, a split tile the sum of its parts).
+int Renderer::band_costs(hipStream_t stream, double* costs, int nbands)
+{
+    if (!stream)
+        stream = stream_;
+    const int H = s_.image_height;
+    const BandSlot* S = nullptr;
+    for (int i = 0; i < band_nslots_; i++)
+        if (band_slot_[i].stream == stream) S = &band_slot_[i];
+    if (!S || !S->live || !S->tc.cost.p || S->tc.ntiles <= 0 || S->tc.band_rows <= 0)
+        return fail(RT_EINVAL, "band_costs: no band launch with tile costs on this stream");
+    const TileCost& T = S->tc;
+    if (!costs || nbands < (H + T.band_rows - 1) / T.band_rows)
+        return fail(RT_EINVAL, "band_costs: buffer smaller than the image's bands");
+    hipError_t e = hipEventSynchronize(S->done);
+    std::vector<uint32_t> c((size_t)T.ntiles);
+    if (e == hipSuccess)
+        e = hipMemcpy(c.data(), T.cost.p, c.size() * 4, hipMemcpyDeviceToHost);
+    if (e != hipSuccess)
+        return hip_fail(e, "band_costs");
+    const int rows_per_band = T.band_rows * T.ssaa;   // internal rows
+    std::vector<double> local(T.bands.size(), 0.0);
+    for (int ty = 0; ty < T.tiles_y; ty++) {
+        const int lb = (8 * ty) / rows_per_band;
+        if (lb >= (int)local.size())
+            continue;
+        double s = 0.0;
+        for (int tx = 0; tx < T.tiles_x; tx++)
+            s += c[(size_t)ty * T.tiles_x + tx];
+        local[lb] += s;
+    }
+    for (size_t i = 0; i < local.size(); i++)
+        if (T.bands[i] < nbands)
+            costs[T.bands[i]] = local[i];
+    return RT_OK;
+}
+
 int Renderer::get_stats(rt_stats* out) const
 {
     std::memset(out, 0, sizeof(*out));
@@ -1717,6 +1768,7 @@ int Renderer::get_stats(rt_stats* out) const
     for (int i = 0; i < 6; i++) out->uncertified[i] = last_uncert_[i];
     for (int i = 0; i < 6; i++) out->wave_steps[i] = last_wave_[i];
     for (int i = 0; i < 4; i++) out->build_split_ms[i] = build_split_ms_[i];
+    out->wide_tree = wide_tree_;
     return RT_OK;
 }
 
@@ -1731,7 +1783,29 @@ int Renderer::local_rows(int band_rows, int rank, int nranks) const
 
 int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t* d_out, hipStream_t stream)
 {
-    int lrows = local_rows(band_rows, rank, nranks);
+    return render_bands_impl(band_rows, rank, nranks, nullptr, 0, d_out, stream);
+}
+
+int Renderer::render_band_list_device(int band_rows, const int32_t* bands, int nbands, uint32_t* d_out,
+                                      hipStream_t stream)
+{
+    if (band_rows <= 0 || nbands <= 0 || !bands)
+        return fail(RT_EINVAL, "render_band_list_device: empty band list");
+    const int nb = (s_.image_height + band_rows - 1) / band_rows;
+    std::vector<char> seen(nb, 0);
+    for (int i = 0; i < nbands; i++) {
+        if (bands[i] < 0 || bands[i] >= nb || seen[bands[i]])
+            return fail(RT_EINVAL, "render_band_list_device: band out of range or listed twice");
+        seen[bands[i]] = 1;
+    }
+    return render_bands_impl(band_rows, 0, 2, bands, nbands, d_out, stream);
+}
+
+// One launch of interleaved bands (bands == nullptr: band b % nranks == rank) or of a band list.
+int Renderer::render_bands_impl(int band_rows, int rank, int nranks, const int32_t* bands, int nbands,
+                                uint32_t* d_out, hipStream_t stream)
+{
+    int lrows = bands ? nbands * band_rows : local_rows(band_rows, rank, nranks);
     if (lrows < 0 || !d_out)
         return fail(RT_EINVAL, "render_bands_device: bad band layout");
     if (s_.enable_ssao)   // its samples and 7x7 blur read across bands
@@ -1791,6 +1865,31 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
     P.nranks = nranks;
     P.rank = rank;
     P.local_rows = lrows * f;
+    uint64_t layout_key = 0;
+    if (bands) {
+        // the list and its inverse in the slot's device buffer; a new list waits for the slot's last
+        // launch (which may still read the old one) and is copied synchronously: lists change rarely
+        const int nb = (s_.image_height + band_rows - 1) / band_rows;
+        std::vector<int32_t> host(bands, bands + nbands);
+        host.resize((size_t)nbands + nb, -1);
+        for (int i = 0; i < nbands; i++)
+            host[(size_t)nbands + bands[i]] = i;
+        if (host != S.map_host || nb != S.map_nb) {
+            if (S.live && (e = hipEventSynchronize(S.done)) != hipSuccess)
+                return hip_fail(e, "render_band_list_device: waiting for the slot's last launch");
+            S.map.device = device_;
+            if ((e = S.map.reserve(host.size() * 4)) != hipSuccess ||
+                (e = hipMemcpy(S.map.p, host.data(), host.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
+                return hip_fail(e, "band list upload");
+            S.map_host.swap(host);
+            S.map_nb = nb;
+        }
+        P.band_map = S.map.as<int32_t>();
+        P.band_inv = P.band_map + nbands;
+        layout_key = 1469598103934665603ull;
+        for (int32_t b : S.map_host)
+            layout_key = (layout_key ^ (uint64_t)(uint32_t)b) * 1099511628211ull;
+    }
     P.tiles_x = (P.rw + 7) / 8;
     P.tiles_y = (P.local_rows + 7) / 8;
     if ((e = S.counters.reserve(NCOUNTER_WORDS * 8)) != hipSuccess) return hip_fail(e, "hipMalloc (counters)");
@@ -1820,8 +1919,13 @@ int Renderer::render_bands_device(int band_rows, int rank, int nranks, uint32_t*
     if ((e = hipMemsetAsync(S.counters.p, 0, NCOUNTER_WORDS * 8, stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
     if ((rc = prepare_risk(P, stream)) != RT_OK)
         return rc;
-    if ((rc = prepare_heavy(P, S.tc, stream)) != RT_OK)
+    if ((rc = prepare_heavy(P, S.tc, stream, layout_key)) != RT_OK)
         return rc;
+    S.tc.band_rows = band_rows;
+    S.tc.ssaa = f;
+    S.tc.bands.resize(lrows / band_rows);
+    for (int i = 0; i < (int)S.tc.bands.size(); i++)
+        S.tc.bands[i] = bands ? bands[i] : i * nranks + rank;
     hipEventRecord(ring_[2 * ring_next_], stream);
     if ((rc = launch_frame(P, stream)) != RT_OK) return rc;
     hipEventRecord(ring_[2 * ring_next_ + 1], stream);
@@ -1897,7 +2001,7 @@ int Renderer::prepare_risk(KParams& P, hipStream_t stream)
 // few very long tiles (grazing silhouette rays) start with the frame instead of ending
 // it.  Only the order changes; every tile is traced once.  Off for the reflection engine and the raster
 // path (their own kernels) and with RT_HEAVY_FIRST=0.
-int Renderer::prepare_heavy(KParams& P, TileCost& T, hipStream_t stream)
+int Renderer::prepare_heavy(KParams& P, TileCost& T, hipStream_t stream, uint64_t layout_key)
 {
     P.tile_cost = nullptr;
     P.heavy_list = nullptr;
@@ -1912,36 +2016,55 @@ int Renderer::prepare_heavy(KParams& P, TileCost& T, hipStream_t stream)
     T.cost.device = T.heavy.device = device_;
     const size_t nb = ((size_t)ntiles + 31) / 32;
     hipError_t e;
+    // T.heavy: the list (ntiles), the bits (nb words), then two {sum, max} pairs of the launches' tile
+    // costs (KParams::tile_stats, alternating: a launch accumulates one, the next heavy_prep reads it)
+    const size_t stats_off = ((size_t)ntiles * 4 + nb * 4 + 7) / 8 * 8;
     if ((e = T.cost.reserve((size_t)ntiles * 4)) != hipSuccess ||
-        (e = T.heavy.reserve((size_t)ntiles * 4 + nb * 4 + 16)) != hipSuccess)
+        (e = T.heavy.reserve(stats_off + 4 * 8)) != hipSuccess)
         return hip_fail(e, "hipMalloc (tile costs)");
+    unsigned long long* stats = reinterpret_cast<unsigned long long*>(static_cast<char*>(T.heavy.p) + stats_off);
     uint64_t key = 1469598103934665603ull;
     for (int64_t v : {(int64_t)P.rw, (int64_t)P.rh, (int64_t)P.local_rows, (int64_t)P.tiles_x, (int64_t)P.tiles_y,
-                      (int64_t)P.band_rows, (int64_t)P.rank, (int64_t)P.nranks, (int64_t)T.cost.bytes})
+                      (int64_t)P.band_rows, (int64_t)P.rank, (int64_t)P.nranks, (int64_t)T.cost.bytes,
+                      (int64_t)layout_key})
         key = (key ^ (uint64_t)v) * 1099511628211ull;
-    if (key != T.key && (e = hipMemsetAsync(T.cost.p, 0, (size_t)ntiles * 4, stream)) != hipSuccess)
+    if (key != T.key && ((e = hipMemsetAsync(T.cost.p, 0, (size_t)ntiles * 4, stream)) != hipSuccess ||
+                         (e = hipMemsetAsync(stats, 0, 4 * 8, stream)) != hipSuccess))
         return hip_fail(e, "hipMemsetAsync (tile costs)");
     T.key = key;
+    T.parity ^= 1u;
     T.ntiles = ntiles;
     T.tiles_x = P.tiles_x;
     T.tiles_y = P.tiles_y;
     int32_t* list = T.heavy.as<int32_t>();
     uint32_t* bits = reinterpret_cast<uint32_t*>(list + ntiles);
-    int32_t* ctr = reinterpret_cast<int32_t*>(bits + nb);
+    // the list counts and tickets: launch counter words 28-29, zeroed with the others before this call
+    int32_t* ctr = reinterpret_cast<int32_t*>(P.counters + 28);
     // tiles are split (kernels.hip trace_split_part) only by the plain kernel over the wide BVH, with a
     // fused SSAA block within a part's 8 / G rows
     const int G = knobs_.heavy_group;
     const bool split = G > 1 && !P.has_reflection && P.plain && !P.zbuf && !P.nbuf && P.wnodes && P.nnodes > 0 &&
                        (!P.ds_out || ((1 << P.ds_shift) <= SPLIT_ROWS && (1 << P.ds_shift) <= SPLIT_COLS));
-    if ((e = rt_launch_heavy_prep(&P, T.cost.as<uint32_t>(), ntiles, list, bits, ctr, knobs_.heavy_split, split ? G : 0,
-                                  stream)) != hipSuccess)
+    unsigned long long* stats_next = stats + 2 * T.parity;
+    // The split bar (x the launch's mean cycles per wave): a band launch of 1 / N of the frame has ~N times
+    // cheaper mean waves on the same grid, and splitting at the full frame's bar there splits tiles that
+    // would not outlast the launch (their parts cost ~1.8x their cycles): the bar grows as the launch's
+    // share shrinks, by sqrt(N) (strips N = 8 at three in flight: 0.318 -> 0.227-0.260 ms per step at
+    // bars 1 / 1.5 / 2 against 0.5, profiles/r06/strips_split_sweep.log)
+    const double share = (double)ntiles / (double)((int64_t)((P.rw + 7) / 8) * ((P.rh + 7) / 8));
+    const float split_bar = knobs_.heavy_split * (float)std::pow(std::min(1.0, std::max(share, 1e-6)),
+                                                                  -(double)knobs_.heavy_split_exp);
+    if ((e = rt_launch_heavy_prep(&P, T.cost.as<uint32_t>(), ntiles, list, bits, ctr, stats + 2 * (T.parity ^ 1u),
+                                  stats_next, split_bar, split ? G : 0, stream)) != hipSuccess)
         return hip_fail(e, "heavy_prep_kernel");
     P.tile_cost = T.cost.as<uint32_t>();
+    P.tile_stats = stats_next;
     last_tc_ = &T;
     P.heavy_list = list;
     P.heavy_bits = bits;
     P.heavy_ctr = ctr;
     P.heavy_group = split ? G : 0;
+    P.split_parts = knobs_.split_parts > 0 ? knobs_.split_parts : G;
     return RT_OK;
 }
 

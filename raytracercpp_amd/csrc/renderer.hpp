@@ -68,6 +68,8 @@ struct Knobs {
     bool heavy = true;        // RT_HEAVY_FIRST=0: tiles in queue order only (no heavy-first list, 5.6)
     int heavy_group = SPLIT_G; // RT_HEAVY_GROUP=0: no split tiles (else: the build's RT_SPLIT_G parts of a tile,
                               // each with that many lanes per pixel, kernels.hip trace_split_part)
+    int split_parts = 0;      // RT_SPLIT_PARTS=n (G or 2 G): parts per split tile (0: G)
+    float heavy_split_exp = 0.5f;  // RT_HEAVY_SPLIT_EXP=e: the bar below grows as (frame tiles / launch tiles)^e
     float heavy_split = 0.5f; // RT_HEAVY_SPLIT=c: split the heavy tiles costing >= c x the launch's mean
                               // cycles per wave (heavy_prep_kernel)
     int refl_defer = 32;      // RT_REFL_DEFER=k: reflection queries past k loop iterations finish in a pass
@@ -142,6 +144,12 @@ public:
     // ---- multi-GPU strips ----
     int local_rows(int band_rows, int rank, int nranks) const;
     int render_bands_device(int band_rows, int rank, int nranks, uint32_t* d_out, hipStream_t stream);
+    // the listed OUTPUT bands into consecutive local bands of d_out (cost-balanced strips, strips.py
+    // assign_bands); render_bands_device is the list rank, rank + nranks, ...
+    int render_band_list_device(int band_rows, const int32_t* bands, int nbands, uint32_t* d_out, hipStream_t stream);
+    // per global output band, the shader cycles of its tiles in the last band launch on 'stream' (the
+    // bands that launch did not render are left as they are)
+    int band_costs(hipStream_t stream, double* costs, int nbands);
     // durations (ms) of the last n ray_trace_kernel launches of render_bands_device,
     // bracketed by HIP events on the launch stream (synchronises on them)
     int kernel_times(float* ms, int n);
@@ -209,6 +217,7 @@ private:
     hipStream_t fence_stream_ = nullptr;   // the band slots' 'done' events (render_bands_device)
     float accel_ms_[3] = {};            // cones + slabs, wide BVH, wide-BVH upload (background)
     bool cones_ready_ = false, wide_ready_ = false, lslab_ready_ = false;
+    int wide_tree_ = 0;   // rt_stats.wide_tree: 0 none, 1 the quick tree, 2 the SAH tree, -1 its build failed
     uint64_t accel_ver_ = 0;   // bumped when poll_accel adopts a build
     void start_accel();
     int poll_accel(bool wait);
@@ -336,8 +345,15 @@ private:
         DevBuf cost, heavy;
         uint64_t key = 0;
         int ntiles = 0, tiles_x = 0, tiles_y = 0;   // the last launch's layout
+        uint32_t parity = 0;   // which of the two tile-cost sums the last launch accumulated
+        // its bands (band_costs): output rows per band, the SSAA factor, and the global band of each
+        // local band
+        int band_rows = 0, ssaa = 1;
+        std::vector<int32_t> bands;
     };
-    int prepare_heavy(KParams& P, TileCost& T, hipStream_t stream);
+    int prepare_heavy(KParams& P, TileCost& T, hipStream_t stream, uint64_t layout_key = 0);
+    int render_bands_impl(int band_rows, int rank, int nranks, const int32_t* bands, int nbands, uint32_t* d_out,
+                          hipStream_t stream);
     const TileCost* last_tc_ = nullptr;   // the last launch's (rt_tile_costs)
     TileCost tc_main_;   // trace_frame's launches (stream_)
     struct BandSlot {
@@ -347,6 +363,9 @@ private:
         hipEvent_t done = nullptr;   // recorded on fence_stream_ behind the slot's last launch
         hipEvent_t mark = nullptr;   // recorded on 'stream' after that launch (fence_stream_ waits on it)
         bool live = false;           // 'done' has been recorded
+        DevBuf map;                  // the band list of the slot's last list launch: map, then inverse
+        std::vector<int32_t> map_host;
+        int map_nb = 0;              // global bands of that list's image
         uint64_t used = 0;   // band_uses_ at the slot's last launch (least recently used is recycled)
     };
     static constexpr int BAND_SLOTS = 8;

@@ -696,7 +696,7 @@ struct WStackArr {
 using WStackLocal = WStackArr<W_STACK>;   // host
 
 // A lane group: G adjacent lanes of a wave (lanes g0 .. g0 + G - 1, g0 a multiple of G) trace one ray
-// together (wbvh_closest<Stack, G>, kernels.hip ray_trace_heavy_kernel).  Device only; on the host
+// together (wbvh_closest<Stack, G>, kernels.hip trace_split_part and refl_trace_long_kernel).  Device only; on the host
 // (G = 1) these are the identity.
 template <int G>
 RT_HD uint32_t wg_lane()

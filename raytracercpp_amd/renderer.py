@@ -294,6 +294,20 @@ class Renderer:
         self._call("rt_render_bands_device", int(band_rows), int(rank), int(nranks), C.c_void_p(d_out_ptr),
                    C.c_void_p(stream_ptr))
 
+    def render_band_list_device(self, band_rows, bands, d_out_ptr: int, stream_ptr: int = 0):
+        """rt_render_band_list_device: the listed output bands into consecutive local bands of d_out
+        (cost-balanced strips, strips.assign_bands)."""
+        b = np.ascontiguousarray(bands, np.int32)
+        self._call("rt_render_band_list_device", int(band_rows), ptr(b, _i32p), int(b.size), C.c_void_p(d_out_ptr),
+                   C.c_void_p(stream_ptr))
+
+    def band_costs(self, nbands: int, stream_ptr: int = 0, out=None) -> np.ndarray:
+        """rt_band_costs: the cost (tile shader cycles) of each output band of the last band launch on the
+        stream; the bands it did not render stay as in ``out`` (zeros by default)."""
+        c = np.zeros(nbands, np.float64) if out is None else np.ascontiguousarray(out, np.float64)
+        self._call("rt_band_costs", C.c_void_p(stream_ptr), c.ctypes.data_as(C.POINTER(C.c_double)), int(nbands))
+        return c
+
     def trace_rays(self, orig, dirs):
         """BVH::intersect for a batch of rays -> (tri_id, t, u, v, ret)."""
         o = f32(orig).reshape(-1, 3)

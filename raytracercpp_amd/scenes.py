@@ -381,6 +381,23 @@ def robot1080(T=None, width=1920, height=1080, loader=None, **kw):
     return obj_scene(data_path(os.path.join("Robot", "robot.obj")), -4.0, width, height, T=T, loader=loader, **kw)
 
 
+def c5_check_rows(seed=2026):
+    """The 16 C5 output rows (1920x1080) whose internal row pairs the full-configuration parity test
+    and bench.py's C5 check compare with the oracle: the four r03 rows (172, 400, 540, 907), and
+    12 drawn from a seeded generator, 4 in each band where the costliest rays sit -- the sphere's
+    top silhouette (output rows 166-182), the tilted pole seen from the camera (400-536, the C4
+    frame's costliest tiles, ty 100-133 of 8 internal rows) and the bottom silhouette (896-914)."""
+    rng = np.random.default_rng(seed)
+    rows = {172, 400, 540, 907}
+    for lo, hi in ((166, 183), (400, 537), (896, 915)):
+        band = [r for r in range(lo, hi) if r not in rows]
+        rows.update(int(r) for r in rng.choice(band, 4, replace=False))
+    return tuple(sorted(rows))
+
+
+C5_CHECK_ROWS = c5_check_rows()
+
+
 CONFIGS = {
     "sphere256": sphere256,
     "cube1080": cube1080,

@@ -132,3 +132,34 @@ def test_gloo_frame_pipeline(nslots):
         p.join(timeout=300)
         assert p.exitcode == 0
     assert all(ok for _, ok in res), res
+
+
+@pytest.mark.parametrize("nranks", [1, 2, 3, 8])
+def test_assign_bands_balanced_and_deterministic(nranks):
+    """strips.assign_bands: every band exactly once, equal band counts (ceil or one fewer, so the
+    all-gather keeps one buffer size), the same lists from the same vector, and the predicted loads
+    within the costliest band of each other (longest processing time first); assemble with the
+    lists re-builds the frame from per-rank buffers."""
+    from raytracercpp_amd.strips import assemble, assign_bands, list_rows
+    rng = np.random.default_rng(nranks)
+    H, band = 1080, 8
+    nb = (H + band - 1) // band
+    costs = rng.exponential(size=nb) * (rng.random(nb) < 0.3) + 1e-3
+    costs[60:67] *= 50.0   # a cluster of costly bands (the sphere's silhouette / pole rows)
+    lists = assign_bands(costs, nranks)
+    assert all(np.array_equal(a, b) for a, b in zip(lists, assign_bands(costs.copy(), nranks)))
+    flat = np.concatenate(lists)
+    assert sorted(flat.tolist()) == list(range(nb))
+    per = (nb + nranks - 1) // nranks
+    assert all(len(lst) in (per, per - 1) for lst in lists) and len(lists[0]) == per
+    loads = np.array([costs[lst].sum() for lst in lists])
+    assert loads.max() - loads.min() <= costs.max() + 1e-9
+    W = 5
+    frame = (np.arange(H)[:, None] * 7 + np.arange(W)[None]).astype(np.int32)
+    parts = []
+    for lst in lists:
+        g = list_rows(lst, H, band, per)
+        p = np.zeros((per * band, W), np.int32)
+        p[g >= 0] = frame[g[g >= 0]]
+        parts.append(p)
+    assert np.array_equal(assemble(parts, H, band, lists), frame)

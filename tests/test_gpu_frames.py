@@ -122,16 +122,18 @@ def test_heavy_first_frames_trace_every_tile_once(make_renderer, ssaa, group):
         assert min(h[1] for h in heavy) > 0   # tiles were split into parts
 
 
-@pytest.mark.parametrize("group", [4])
-def test_c4_heavy_parts_match_oracle(make_renderer, group):
-    """The benchmark workload (C4) with its heavy tiles traced by ray_trace_heavy_kernel (G lanes per
-    pixel walking one pixel's wide-BVH query together, wbvh_closest<.., G>): the octree frame, then two
-    wide-BVH frames (heavy lists from the octree frame's and the wide frame's tile costs), every internal
-    pixel bit for bit; then the band path with the SSAA box filter fused into both kernels' tiles."""
+@pytest.mark.parametrize("group,quick", [(4, 1), (4, 0)])
+def test_c4_heavy_parts_match_oracle(make_renderer, group, quick):
+    """The benchmark workload (C4) with its heavy tiles split into parts (trace_split_part: G lanes per
+    pixel walking one pixel's wide-BVH query together, wbvh_closest<.., G>).  Frame 0 runs right after
+    the scene load: on the quick wide BVH (quick = 1, the default), or with
+    RT_WBVH_QUICK_FIRST=0 on the octree-only plain kernel ray_trace_kernel<false, true, true>.  Then two
+    frames on the SAH tree (heavy lists from the previous frames' tile costs), every internal pixel bit
+    for bit; then the band path with the SSAA box filter fused into the tiles and the split parts."""
     import torch
     from raytracercpp_amd import scenes
     from raytracercpp_amd.strips import assemble
-    R = make_renderer(RT_HEAVY_GROUP=group)
+    R = make_renderer(RT_HEAVY_GROUP=group, RT_WBVH_QUICK_FIRST=quick)
     sc, st = scenes.sphere1m()
     o = Oracle(sc, st).render_rows()
     R.load_scene(sc, st)
@@ -150,7 +152,9 @@ def test_c4_heavy_parts_match_oracle(make_renderer, group):
         assert np.array_equal(g["argb"], o.argb), frame
         assert R.stats()["shadow_rays"] == o.counters["shadow_rays"], frame
         if frame == 0:
+            assert R.stats()["wide_tree"] in ((1, 2) if quick else (0, 2))   # (the SAH tree may be adopted already)
             R.finish_accel()
+            assert R.stats()["wide_tree"] == 2   # the SAH tree adopted
     assert min(heavy) > 0, heavy
     band, nranks = 8, 2   # output rows per band (16 internal rows)
     for rep in range(3):   # the first launch per slot has no tile costs yet: no heavy list

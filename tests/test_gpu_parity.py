@@ -260,6 +260,57 @@ def test_band_streams_fused_ssaa(make_renderer, f, fused):
         assert np.array_equal(assemble(parts, st.image_height, band), full), (nranks, band)
 
 
+@pytest.mark.parametrize("f", [2, 3])
+def test_band_lists_cost_balanced(make_renderer, f):
+    """Cost-balanced strips (rt_render_band_list_device + rt_band_costs, strips.assign_bands): each
+    "rank" renders the interleaved layout, the band costs of its launches are summed into one vector,
+    then every rank renders its balanced list on its own stream, a few frames in flight (heavy lists
+    and split tiles learnt per list); the re-assembled frame equals the full render (f = 2 fused SSAA,
+    f = 3 the separate pass), the costs cover every band, and bad lists are refused."""
+    import torch
+    from raytracercpp_amd import scenes
+    from raytracercpp_amd._lib import RtError
+    from raytracercpp_amd.strips import assemble, assign_bands, num_bands
+    R = make_renderer()
+    sc, st = scenes.bumpy70k(width=320, height=184, enable_ssaa=True, ssaa_factor=f)
+    R.load_scene(sc, st)
+    R.ray_trace()
+    R.finish_accel()
+    R.ray_trace()
+    R.post_process()
+    full = R.get_image()
+    band, nranks = 8, 3
+    nb = num_bands(st.image_height, band)
+    streams = [torch.cuda.Stream() for _ in range(nranks)]
+    costs = np.zeros(nb)
+    for rank in range(nranks):
+        b = torch.zeros((R.local_rows(band, rank, nranks), st.image_width), dtype=torch.int32, device="cuda:0")
+        torch.cuda.synchronize()
+        for _ in range(2):
+            R.render_bands_device(band, rank, nranks, b.data_ptr(), streams[rank].cuda_stream)
+        costs = R.band_costs(nb, streams[rank].cuda_stream, costs)
+    assert (costs > 0).all(), costs
+    lists = assign_bands(costs, nranks)
+    assert sorted(np.concatenate(lists).tolist()) == list(range(nb))
+    per = len(lists[0])
+    bufs = [torch.zeros((per * band, st.image_width), dtype=torch.int32, device="cuda:0") for _ in range(nranks)]
+    torch.cuda.synchronize()
+    for rep in range(3):
+        for rank in range(nranks):
+            R.render_band_list_device(band, lists[rank], bufs[rank].data_ptr(), streams[rank].cuda_stream)
+        torch.cuda.synchronize()
+        parts = [x.cpu().numpy().view(np.uint32) for x in bufs]
+        assert np.array_equal(assemble(parts, st.image_height, band, lists), full), rep
+    # the list launches' own costs cover exactly their bands
+    c2 = np.zeros(nb)
+    for rank in range(nranks):
+        c2 = R.band_costs(nb, streams[rank].cuda_stream, c2)
+    assert (c2 > 0).all()
+    for bad in ([0, 0], [nb], [-1]):
+        with pytest.raises(RtError):
+            R.render_band_list_device(band, bad, bufs[0].data_ptr(), streams[0].cuda_stream)
+
+
 def test_render_api_and_errors(R):
     from raytracercpp_amd import scenes
     from raytracercpp_amd._lib import RtError
@@ -344,14 +395,15 @@ def test_reflection_engine_matches_oracle_c5_small(make_renderer):
 
 
 # C5 at its own configuration: 1920x1080, SSAA 2, 16 rough samples, depth 5,
-# normal + parallax maps.  Output rows whose internal row pairs are checked: the top and bottom
-# silhouettes of the sphere (internal rows ~337 and ~1823), the centre, and one in between.
-C5_OUTPUT_ROWS = (172, 400, 540, 907)
+# normal + parallax maps.  Output rows whose internal row pairs are checked (scenes.c5_check_rows,
+# the same rows as bench.py's C5 check): the r03 rows plus 12 seeded ones in the top silhouette,
+# pole and bottom silhouette bands (internal rows ~337 .. 1823).
+from raytracercpp_amd.scenes import C5_CHECK_ROWS as C5_OUTPUT_ROWS  # noqa: E402
 
 
 def test_c5_full_config_matches_oracle(R):
-    """The whole C5 frame on the GPU (frame engine, 2^25-slot chunks, multi-level Morton sorts,
-    ~2.2G reflection rays) against the oracle on 8 internal rows: hit ID, hit t bits, shadow
+    """The whole C5 frame on the GPU (frame engine, 2^27-slot chunks, multi-level Morton sorts,
+    ~2.2G reflection rays) against the oracle on 32 internal rows (16 output rows): hit ID, hit t bits, shadow
     flags and ARGB exact, float RGBA within 1e-4, the SSAA output rows exact, and the shadow /
     reflection ray counts of each row pair (a one-output-row band launch, rt_band_counters)."""
     import torch

@@ -50,7 +50,9 @@ def _oracle_for(sc):
 
 def _device_differences(R, tri, o, d, kind, cam=None, light=None):
     """Runs the rays through the device query; returns (certified fraction, differing certified
-    answers, the device's output).  The oracle answers the rays the device built."""
+    answers, the device's output).  The oracle answers the rays the device built.  Every input is
+    finite: a NaN ray is a miss on both sides and would inflate the certified fraction."""
+    assert np.isfinite(o).all() and np.isfinite(d).all(), "non-finite ray inputs"
     sc, st = _scene(tri, cam, light)
     R.load_scene(sc, st)
     g = R.wide_query(o, d, kind)
@@ -175,10 +177,14 @@ def test_device_light_sphere_terminator(R):
     T = tri.reshape(-1, 3, 3).astype(np.float64)
     L = np.array([5.0, 0.5, 1.0], np.float32)
     nn = np.cross(T[:, 1] - T[:, 0], T[:, 2] - T[:, 0])
-    nn /= np.maximum(np.linalg.norm(nn, axis=1, keepdims=True), 1e-30)
+    area = np.linalg.norm(nn, axis=1)
+    nn /= np.maximum(area, 1e-30)[:, None]
     toL = L - T.mean(1)
     toL /= np.linalg.norm(toL, axis=1, keepdims=True)
-    k = np.argsort(np.abs((nn * toL).sum(1)))[:20000]
+    # the terminator: the triangles most nearly edge-on to the light (zero-area pole triangles have no
+    # normal and are left out, or their zero directions would sort first)
+    key = np.where(area > 1e-12, np.abs((nn * toL).sum(1)), np.inf)
+    k = np.argsort(key)[:20000]
     uv = rng.uniform(0, 1, (len(k), 2))
     uv[uv.sum(1) > 1] = 1 - uv[uv.sum(1) > 1]
     p = (T[k, 0] + (T[k, 1] - T[k, 0]) * uv[:, :1] + (T[k, 2] - T[k, 0]) * uv[:, 1:]).astype(np.float32)
@@ -311,7 +317,7 @@ def _group_case(name):
 @pytest.mark.parametrize("name", ["plane", "sphere", "camera_plane", "light_plane"])
 def test_device_lane_groups_match_one_lane(R, monkeypatch, name, G):
     """wbvh_closest<.., G> (G lanes walking one ray's tree together: work taken from each other's stacks,
-    the best hit shared, kernels.hip ray_trace_heavy_kernel) returns the one-lane query's answers bit for
+    the best hit shared, kernels.hip trace_split_part) returns the one-lane query's answers bit for
     bit -- status, triangle, t, u, v and the shadow decision -- on the grazing cases above, and 0 of its
     certified answers differ from the oracle."""
     tri, o, d, kind, cam, light = _group_case(name)

@@ -1,5 +1,5 @@
 """Host-side checks that need no GPU: the C-ABI library loads and exports exactly the
-symbols include/rt_mi355x.h declares (no compute calls), settings defaults mirror
+symbols include/rt_mi355x.h and rt_mi355x_diag.h declare (no compute calls), settings defaults mirror
 RenderSettings, host math / OBJ loading against the committed fixtures, and the
 strip layout used for multi-GPU rendering."""
 import ctypes
@@ -15,12 +15,23 @@ from raytracercpp_amd.scene import RenderSettings
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "rt_mi355x.h")
+DIAG_HEADER = os.path.join(ROOT, "include", "rt_mi355x_diag.h")   # the diagnostic entry points
 
 
-def declared_functions():
-    text = open(HEADER).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", text))
+def declared_functions(headers=(HEADER, DIAG_HEADER)):
+    out = set()
+    for h in headers:
+        text = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        out |= set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", text))
+    return out
+
+
+def test_diagnostics_apart_from_the_renderer_surface():
+    """rt_mi355x.h holds the Renderer surface; the diagnostics live in rt_mi355x_diag.h only."""
+    main, diag = declared_functions((HEADER,)), declared_functions((DIAG_HEADER,))
+    assert {"rt_tile_costs", "rt_debug_read", "rt_wide_query", "rt_risk_words", "rt_wbvh_query", "rt_wbvh_query_ex",
+            "rt_octree_digest"} == diag
+    assert not (main & diag)
 
 
 def test_library_exports_every_declared_symbol():

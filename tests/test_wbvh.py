@@ -222,7 +222,11 @@ def grazing_sphere_case(seed=3, n_rays=20000):
     tri = sc.tri
     T = tri.reshape(-1, 3, 3).astype(np.float64)
     c = T.reshape(-1, 3).mean(0)
-    k = rng.integers(0, len(T), n_rays)
+    # tangent planes of triangles with an area only: the UV sphere's zero-area pole triangles have
+    # no normal (their rays would be NaN and check nothing)
+    area = np.linalg.norm(np.cross(T[:, 1] - T[:, 0], T[:, 2] - T[:, 0]), axis=1)
+    ok = np.flatnonzero(area > 1e-12)
+    k = ok[rng.integers(0, len(ok), n_rays)]
     p = T[k].mean(1)
     n = np.cross(T[k, 1] - T[k, 0], T[k, 2] - T[k, 0])
     n /= np.linalg.norm(n, axis=1, keepdims=True)
@@ -232,7 +236,9 @@ def grazing_sphere_case(seed=3, n_rays=20000):
     d = t1 + n * (eps * rng.choice([-1, 1], n_rays))[:, None]
     d /= np.linalg.norm(d, axis=1, keepdims=True)
     o = p - d * rng.uniform(0.5, 4.0, n_rays)[:, None] + n * (eps * rng.uniform(0, 1, n_rays))[:, None]
-    return tri, o.astype(np.float32), d.astype(np.float32)
+    o, d = o.astype(np.float32), d.astype(np.float32)
+    assert np.isfinite(o).all() and np.isfinite(d).all()
+    return tri, o, d
 
 
 def test_grazing_sphere_certified_answers_match_oracle():

@@ -1,6 +1,7 @@
-"""RCCL path of bench.py on one GPU (world size 1, torchrun): high-priority process group, two
-frames in flight with async all-gathers (strips.FramePipeline with the gather forced on);
-every gathered frame must equal the rendered strips.  Usage (GPU box):
+"""RCCL path of bench.py on one GPU (world size 1, torchrun): high-priority process group, three
+frames in flight with async all-gathers into one flat buffer (strips.FramePipeline with the gather
+forced on) and the re-assembly on the slot's stream; every gathered and re-assembled frame must equal
+the rendered strips.  Usage (GPU box):
   python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 \\
       --master-port 29511 tools/nccl_check.py"""
 import os, sys
@@ -9,7 +10,7 @@ import torch
 import torch.distributed as dist
 from raytracercpp_amd import scenes
 from raytracercpp_amd.renderer import Renderer
-from raytracercpp_amd.strips import FramePipeline
+from raytracercpp_amd.strips import FramePipeline, gather_index
 
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
@@ -25,9 +26,11 @@ q = 3   # frames in flight: bench.py's default (--inflight)
 streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(q - 1)]
 outs = [torch.zeros((n, st.image_width), dtype=torch.int32, device=dev) for _ in range(q)]
 torch.cuda.synchronize()
-pipe = FramePipeline(lambda o, s: r.render_bands_device(band, 0, 1, o.data_ptr(), s.cuda_stream), outs, 1, streams, dist)
-pipe.world = 2   # force the gather path with one rank: parts[i] holds 2 slots, gather fills slot 0
-pipe.parts = [[torch.empty_like(o)] for o in outs]
+# the gather forced on with one rank, and rank 0's in-step re-assembly (bench.py) through gather_index
+idx = torch.as_tensor(gather_index(st.image_height, band, 1, n), device=dev)
+frames = [torch.zeros((st.image_height, st.image_width), dtype=torch.int32, device=dev) for _ in range(q)]
+pipe = FramePipeline(lambda o, s: r.render_bands_device(band, 0, 1, o.data_ptr(), s.cuda_stream), outs, 1, streams, dist,
+                     assemble=lambda i, flat: torch.index_select(flat, 0, idx, out=frames[i]), gather=True)
 ok = True
 for k in range(12):
     pipe.step()
@@ -35,6 +38,7 @@ pipe.drain()
 ref = outs[0].clone()
 for i in range(q):
     ok &= bool(torch.equal(pipe.parts[i][0], outs[i])) and bool(torch.equal(outs[i], ref))
+    ok &= bool(torch.equal(frames[i], ref[:st.image_height]))
 print("nccl pipeline ok" if ok else "nccl pipeline MISMATCH", flush=True)
 dist.destroy_process_group()
 sys.exit(0 if ok else 1)

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--all-ranks", action="store_true", help="time every rank of each N (default: rank 0 and N-1)")
     ap.add_argument("--inflight", type=int, nargs="+", default=[1],
                     help="frames in flight: consecutive steps alternate over this many streams")
+    ap.add_argument("--balance", action="store_true",
+                    help="cost-balanced band lists (strips.assign_bands over the interleaved layout's band costs)")
     args = ap.parse_args()
     import torch
     from raytracercpp_amd import scenes
@@ -44,16 +46,37 @@ def main():
     rw, rh = st.render_size()
     band = args.band_rows
     res = []
+    from raytracercpp_amd.strips import assign_bands, num_bands
+    nb = num_bands(st.image_height, band)
+    lists = {}
+    if args.balance:
+        # every rank's band costs under the interleaved layout (each rank's share alone on the GPU, as
+        # on its own GPU), summed into one vector, then the balanced lists
+        for n in args.ranks:
+            costs = np.zeros(nb)
+            for rank in range(n):
+                nloc = r.local_rows(band, rank, n)
+                o = torch.empty((nloc, W), dtype=torch.int32, device="cuda")
+                for _ in range(args.warmup + 2):
+                    r.render_bands_device(band, rank, n, o.data_ptr(), 0)
+                costs = r.band_costs(nb, 0, costs)
+            lists[n] = assign_bands(costs, n)
+            loads = [float(costs[lst].sum()) for lst in lists[n]]
+            print(json.dumps({"N": n, "balanced_loads_rel": [round(x / max(loads), 3) for x in loads]}), flush=True)
     for q in args.inflight:
         streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(q - 1)]
         for n in args.ranks:
             ranks = range(n) if args.all_ranks else sorted({0, n - 1})
             for rank in ranks:
-                nloc = r.local_rows(band, rank, n)
+                lst = lists[n][rank] if n in lists else None
+                nloc = (len(lists[n][0]) * band) if lst is not None else r.local_rows(band, rank, n)
                 outs = [torch.empty((nloc, W), dtype=torch.int32, device="cuda") for _ in range(q)]
 
                 def step(i):
-                    r.render_bands_device(band, rank, n, outs[i % q].data_ptr(), streams[i % q].cuda_stream)
+                    if lst is not None:
+                        r.render_band_list_device(band, lst, outs[i % q].data_ptr(), streams[i % q].cuda_stream)
+                    else:
+                        r.render_bands_device(band, rank, n, outs[i % q].data_ptr(), streams[i % q].cuda_stream)
 
                 for i in range(args.warmup):
                     step(i)
@@ -66,7 +89,7 @@ def main():
                 dt = (time.perf_counter() - t0) / args.steps
                 k = float(np.mean(r.kernel_times(args.steps)))
                 shadow, _ = r.band_counters()
-                rec = {"inflight": q, "N": n, "rank": rank, "step_ms": round(dt * 1e3, 4), "kernel_ms": round(k, 4),
+                rec = {"inflight": q, "N": n, "rank": rank, "balanced": lst is not None, "step_ms": round(dt * 1e3, 4), "kernel_ms": round(k, 4),
                        "overhead_ms": round(dt * 1e3 - k, 4), "host_ms": round(th * 1e3, 4), "local_rows": nloc,
                        "shadow_rays": shadow}
                 res.append(rec)
