@@ -49,7 +49,7 @@ print(d['config'].get('workload','')[:24], 'value', d['value'], 'ms/step', d['ms
 trace() {   # trace <name> <secs> <bench args...>
     local name=$1 secs=$2; shift 2
     timeout -k 10 "$secs" rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$name" -o run -- \
-        python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-check "$@"
+        python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-check --no-legs "$@"
 }
 
 run_step() {

@@ -11,11 +11,11 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
-    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-check $EXTRA > $OUT/trace.log 2>&1 || exit 1
+    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-check --no-legs $EXTRA > $OUT/trace.log 2>&1 || exit 1
 pass() {   # pass <name> <counters...>
     local name=$1; shift
     timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d $OUT/pmc_$name -o run -- \
-        python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-check $EXTRA > $OUT/pmc_$name.log 2>&1
+        python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-check --no-legs $EXTRA > $OUT/pmc_$name.log 2>&1
 }
 pass fetch FETCH_SIZE || exit 2
 pass write WRITE_SIZE || exit 3
