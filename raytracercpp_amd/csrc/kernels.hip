@@ -3629,19 +3629,30 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_trace_colo
 // of ray_trace_kernel (the consumers clamp the counts to cap).  One lane per tile over the whole grid:
 // the sum and the largest cost come from the previous launch itself (KParams::tile_stats, stats_prev),
 // the list slots from one atomic per wave and list, each wave writes its 64 tiles' two bit words, and
-// block 0 clears the sums the coming launch accumulates (stats_next).  ctr[] (in the launch's counter
-// words) was zeroed with them.  r05 ran this as one 1,024-thread block: 83-91 us per launch at C4.
+// block 0 clears the launch's counter words, the sums the coming launch accumulates (stats_next) and the
+// counts of the slot's next heavy_prep (ctr_next; ctr was cleared by the previous one).  r05 ran this
+// as one 1,024-thread block: 83-91 us per launch at C4.
 #ifndef RT_HEAVY_PRIO
 #define RT_HEAVY_PRIO 1   // heavy tiles at raised wave priority (set_wave_prio)
 #endif
-__global__ __launch_bounds__(256) void heavy_prep_kernel(uint32_t* __restrict__ cost, int ntiles, int32_t* list,
-                                                         uint32_t* bits, int32_t* ctr,
-                                                         const unsigned long long* stats_prev,
-                                                         unsigned long long* stats_next, int nwaves, float split,
-                                                         int group)
+__global__ __launch_bounds__(64) void heavy_prep_kernel(uint32_t* __restrict__ cost, int ntiles, int32_t* list,
+                                                        uint32_t* bits, int32_t* ctr, int32_t* ctr_next,
+                                                        const unsigned long long* stats_prev,
+                                                        unsigned long long* stats_next,
+                                                        unsigned long long* counters, int ncounters, int nwaves,
+                                                        float split, int group)
 {
-    if (blockIdx.x == 0 && threadIdx.x < 2)
-        stats_next[threadIdx.x] = 0ull;
+    if (blockIdx.x == 0) {
+        // for the coming launch: its counter words (the memset the launch would need otherwise: one
+        // dispatch fewer per frame, each waiting for a free wave slot among the frames in flight), and
+        // for the slot's next heavy_prep its list counts and tickets (this launch's are ctr)
+        for (int i = (int)threadIdx.x; i < ncounters; i += (int)blockDim.x)
+            counters[i] = 0ull;
+        if (threadIdx.x < 4)
+            ctr_next[threadIdx.x] = 0;
+        if (threadIdx.x < 2)
+            stats_next[threadIdx.x] = 0ull;
+    }
     const unsigned long long sum = stats_prev[0];
     const unsigned int mx = (unsigned int)min(stats_prev[1], 0xFFFFFFFFull);
     const unsigned long long mean = ntiles > 0 ? sum / (unsigned long long)ntiles : 0;
@@ -3690,6 +3701,7 @@ static int plain_blocks(const rt::KParams& P)
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_heavy_prep(const rt::KParams* P, uint32_t* cost,
                                                                                  int ntiles, int32_t* list,
                                                                                  uint32_t* bits, int32_t* ctr,
+                                                                                 int32_t* ctr_next,
                                                                                  const unsigned long long* stats_prev,
                                                                                  unsigned long long* stats_next,
                                                                                  float split, int group,
@@ -3697,8 +3709,10 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_heavy_prep
 {
     if (ntiles <= 0)
         return hipSuccess;
-    hipLaunchKernelGGL(heavy_prep_kernel, dim3((ntiles + 255) / 256), dim3(256), 0, stream, cost, ntiles, list, bits,
-                       ctr, stats_prev, stats_next, plain_blocks(*P) * rt::WAVES_PER_BLOCK, split, group);
+    // one-wave blocks: each finds a slot beside the persistent grids of the frames in flight
+    hipLaunchKernelGGL(heavy_prep_kernel, dim3((ntiles + 63) / 64), dim3(64), 0, stream, cost, ntiles, list, bits,
+                       ctr, ctr_next, stats_prev, stats_next, P->counters, rt::NCOUNTER_WORDS,
+                       plain_blocks(*P) * rt::WAVES_PER_BLOCK, split, group);
     return hipGetLastError();
 }
 

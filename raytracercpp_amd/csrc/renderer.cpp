@@ -18,6 +18,7 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ray_trace(
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_heavy_prep(const rt::KParams* P, uint32_t* cost,
                                                                                  int ntiles, int32_t* list,
                                                                                  uint32_t* bits, int32_t* ctr,
+                                                                                 int32_t* ctr_next,
                                                                                  const unsigned long long* stats_prev,
                                                                                  unsigned long long* stats_next,
                                                                                  float split, int group,
@@ -125,6 +126,8 @@ Knobs Knobs::from_env()
         k.heavy_split = std::max(0.0f, (float)atof(v));
     if (const char* v = getenv("RT_HEAVY_SPLIT_EXP"))
         k.heavy_split_exp = std::max(0.0f, (float)atof(v));
+    if (const char* v = getenv("RT_HEAVY_SPLIT_EXP_OVERLAP"))
+        k.heavy_split_exp_overlap = std::max(0.0f, (float)atof(v));
     if (const char* v = getenv("RT_SPLIT_PARTS"))
         k.split_parts = atoi(v) == 2 * SPLIT_G ? 2 * SPLIT_G : SPLIT_G;
     if (const char* v = getenv("RT_REFL_DEFER"))   // loop iterations before a reflection query is deferred
@@ -1440,7 +1443,6 @@ int Renderer::trace_frame()
     P.hit_t = want_hit_ ? d_hit_t_.as<float>() : nullptr;
     P.shadow = want_shadow_ ? d_shadow_.as<uint8_t>() : nullptr;
     P.counters = d_counters_.as<unsigned long long>();
-    if ((e = hipMemsetAsync(d_counters_.p, 0, NCOUNTER_WORDS * 8, stream_)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
     if (knobs_.debug_waves) {   // diagnostic builds: per-wave records (rt_debug_read)
         if ((e = d_dbg_.reserve((size_t)DBG_WAVES * DBG_WORDS * 8)) != hipSuccess ||
             (e = hipMemsetAsync(d_dbg_.p, 0, (size_t)DBG_WAVES * DBG_WORDS * 8, stream_)) != hipSuccess)
@@ -1451,8 +1453,11 @@ int Renderer::trace_frame()
         return RT_EHIP;
     if ((rc = prepare_risk(P, stream_)) != RT_OK)
         return rc;
-    if ((rc = prepare_heavy(P, tc_main_, stream_)) != RT_OK)
+    bool zeroed = false;   // heavy_prep_kernel clears the counter words itself
+    if ((rc = prepare_heavy(P, tc_main_, stream_, 0, &zeroed)) != RT_OK)
         return rc;
+    if (!zeroed && (e = hipMemsetAsync(d_counters_.p, 0, NCOUNTER_WORDS * 8, stream_)) != hipSuccess)
+        return hip_fail(e, "hipMemsetAsync");
     hipEventRecord(ev_[0], stream_);
     if ((rc = launch_frame(P, stream_)) != RT_OK) return rc;
     hipEventRecord(ev_[1], stream_);
@@ -1916,11 +1921,16 @@ int Renderer::render_bands_impl(int band_rows, int rank, int nranks, const int32
         for (auto& ev : ring_)
             if ((e = hipEventCreate(&ev)) != hipSuccess) return hip_fail(e, "hipEventCreate");
     }
-    if ((e = hipMemsetAsync(S.counters.p, 0, NCOUNTER_WORDS * 8, stream)) != hipSuccess) return hip_fail(e, "hipMemsetAsync");
     if ((rc = prepare_risk(P, stream)) != RT_OK)
         return rc;
-    if ((rc = prepare_heavy(P, S.tc, stream, layout_key)) != RT_OK)
+    bool zeroed = false;   // heavy_prep_kernel clears the counter words itself (one dispatch fewer)
+    bool overlapped = false;   // another band launch still in flight (frames in flight)
+    for (int i = 0; i < band_nslots_ && !overlapped; i++)
+        overlapped = i != si && band_slot_[i].live && hipEventQuery(band_slot_[i].done) == hipErrorNotReady;
+    if ((rc = prepare_heavy(P, S.tc, stream, layout_key, &zeroed, overlapped)) != RT_OK)
         return rc;
+    if (!zeroed && (e = hipMemsetAsync(S.counters.p, 0, NCOUNTER_WORDS * 8, stream)) != hipSuccess)
+        return hip_fail(e, "hipMemsetAsync");
     S.tc.band_rows = band_rows;
     S.tc.ssaa = f;
     S.tc.bands.resize(lrows / band_rows);
@@ -2001,8 +2011,11 @@ int Renderer::prepare_risk(KParams& P, hipStream_t stream)
 // few very long tiles (grazing silhouette rays) start with the frame instead of ending
 // it.  Only the order changes; every tile is traced once.  Off for the reflection engine and the raster
 // path (their own kernels) and with RT_HEAVY_FIRST=0.
-int Renderer::prepare_heavy(KParams& P, TileCost& T, hipStream_t stream, uint64_t layout_key)
+int Renderer::prepare_heavy(KParams& P, TileCost& T, hipStream_t stream, uint64_t layout_key, bool* zeroed,
+                            bool overlapped)
 {
+    if (zeroed)
+        *zeroed = false;
     P.tile_cost = nullptr;
     P.heavy_list = nullptr;
     P.heavy_bits = nullptr;
@@ -2018,18 +2031,20 @@ int Renderer::prepare_heavy(KParams& P, TileCost& T, hipStream_t stream, uint64_
     hipError_t e;
     // T.heavy: the list (ntiles), the bits (nb words), then two {sum, max} pairs of the launches' tile
     // costs (KParams::tile_stats, alternating: a launch accumulates one, the next heavy_prep reads it)
+    // ... and two sets of the list counts and tickets (int32 x 4 each, alternating the same way)
     const size_t stats_off = ((size_t)ntiles * 4 + nb * 4 + 7) / 8 * 8;
     if ((e = T.cost.reserve((size_t)ntiles * 4)) != hipSuccess ||
-        (e = T.heavy.reserve(stats_off + 4 * 8)) != hipSuccess)
+        (e = T.heavy.reserve(stats_off + 4 * 8 + 2 * 16)) != hipSuccess)
         return hip_fail(e, "hipMalloc (tile costs)");
     unsigned long long* stats = reinterpret_cast<unsigned long long*>(static_cast<char*>(T.heavy.p) + stats_off);
+    int32_t* ctrs = reinterpret_cast<int32_t*>(stats + 4);
     uint64_t key = 1469598103934665603ull;
     for (int64_t v : {(int64_t)P.rw, (int64_t)P.rh, (int64_t)P.local_rows, (int64_t)P.tiles_x, (int64_t)P.tiles_y,
                       (int64_t)P.band_rows, (int64_t)P.rank, (int64_t)P.nranks, (int64_t)T.cost.bytes,
                       (int64_t)layout_key})
         key = (key ^ (uint64_t)v) * 1099511628211ull;
     if (key != T.key && ((e = hipMemsetAsync(T.cost.p, 0, (size_t)ntiles * 4, stream)) != hipSuccess ||
-                         (e = hipMemsetAsync(stats, 0, 4 * 8, stream)) != hipSuccess))
+                         (e = hipMemsetAsync(stats, 0, 4 * 8 + 2 * 16, stream)) != hipSuccess))
         return hip_fail(e, "hipMemsetAsync (tile costs)");
     T.key = key;
     T.parity ^= 1u;
@@ -2038,8 +2053,8 @@ int Renderer::prepare_heavy(KParams& P, TileCost& T, hipStream_t stream, uint64_
     T.tiles_y = P.tiles_y;
     int32_t* list = T.heavy.as<int32_t>();
     uint32_t* bits = reinterpret_cast<uint32_t*>(list + ntiles);
-    // the list counts and tickets: launch counter words 28-29, zeroed with the others before this call
-    int32_t* ctr = reinterpret_cast<int32_t*>(P.counters + 28);
+    // the list counts and tickets of this launch (cleared by the slot's previous heavy_prep, or above)
+    int32_t* ctr = ctrs + 4 * T.parity;
     // tiles are split (kernels.hip trace_split_part) only by the plain kernel over the wide BVH, with a
     // fused SSAA block within a part's 8 / G rows
     const int G = knobs_.heavy_group;
@@ -2049,13 +2064,15 @@ int Renderer::prepare_heavy(KParams& P, TileCost& T, hipStream_t stream, uint64_
     // The split bar (x the launch's mean cycles per wave): a band launch of 1 / N of the frame has ~N times
     // cheaper mean waves on the same grid, and splitting at the full frame's bar there splits tiles that
     // would not outlast the launch (their parts cost ~1.8x their cycles): the bar grows as the launch's
-    // share shrinks, by sqrt(N) (strips N = 8 at three in flight: 0.318 -> 0.227-0.260 ms per step at
-    // bars 1 / 1.5 / 2 against 0.5, profiles/r06/strips_split_sweep.log)
+    // share shrinks, by N^0.5 alone and N^0.7 while other band launches are in flight, whose work hides
+    // this one's tail (strips N = 8: 0.318 -> 0.227-0.260 ms per step at three in flight with bars
+    // 1 / 1.5 / 2 against 0.5, one in flight best at 1-1.5; profiles/r06/strips_split_sweep.log)
     const double share = (double)ntiles / (double)((int64_t)((P.rw + 7) / 8) * ((P.rh + 7) / 8));
-    const float split_bar = knobs_.heavy_split * (float)std::pow(std::min(1.0, std::max(share, 1e-6)),
-                                                                  -(double)knobs_.heavy_split_exp);
-    if ((e = rt_launch_heavy_prep(&P, T.cost.as<uint32_t>(), ntiles, list, bits, ctr, stats + 2 * (T.parity ^ 1u),
-                                  stats_next, split_bar, split ? G : 0, stream)) != hipSuccess)
+    const float split_bar = knobs_.heavy_split *
+                            (float)std::pow(std::min(1.0, std::max(share, 1e-6)),
+                                            -(double)(overlapped ? knobs_.heavy_split_exp_overlap : knobs_.heavy_split_exp));
+    if ((e = rt_launch_heavy_prep(&P, T.cost.as<uint32_t>(), ntiles, list, bits, ctr, ctrs + 4 * (T.parity ^ 1u),
+                                  stats + 2 * (T.parity ^ 1u), stats_next, split_bar, split ? G : 0, stream)) != hipSuccess)
         return hip_fail(e, "heavy_prep_kernel");
     P.tile_cost = T.cost.as<uint32_t>();
     P.tile_stats = stats_next;
@@ -2065,6 +2082,8 @@ int Renderer::prepare_heavy(KParams& P, TileCost& T, hipStream_t stream, uint64_
     P.heavy_ctr = ctr;
     P.heavy_group = split ? G : 0;
     P.split_parts = knobs_.split_parts > 0 ? knobs_.split_parts : G;
+    if (zeroed)
+        *zeroed = true;   // (heavy_prep_kernel cleared P.counters)
     return RT_OK;
 }
 

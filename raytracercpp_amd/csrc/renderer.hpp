@@ -70,6 +70,8 @@ struct Knobs {
                               // each with that many lanes per pixel, kernels.hip trace_split_part)
     int split_parts = 0;      // RT_SPLIT_PARTS=n (G or 2 G): parts per split tile (0: G)
     float heavy_split_exp = 0.5f;  // RT_HEAVY_SPLIT_EXP=e: the bar below grows as (frame tiles / launch tiles)^e
+    float heavy_split_exp_overlap = 0.7f;  // RT_HEAVY_SPLIT_EXP_OVERLAP: the same while other band launches are
+                                           // in flight (the launch's tail overlaps them: fewer splits pay)
     float heavy_split = 0.5f; // RT_HEAVY_SPLIT=c: split the heavy tiles costing >= c x the launch's mean
                               // cycles per wave (heavy_prep_kernel)
     int refl_defer = 32;      // RT_REFL_DEFER=k: reflection queries past k loop iterations finish in a pass
@@ -351,7 +353,8 @@ private:
         int band_rows = 0, ssaa = 1;
         std::vector<int32_t> bands;
     };
-    int prepare_heavy(KParams& P, TileCost& T, hipStream_t stream, uint64_t layout_key = 0);
+    int prepare_heavy(KParams& P, TileCost& T, hipStream_t stream, uint64_t layout_key = 0, bool* zeroed = nullptr,
+                      bool overlapped = false);
     int render_bands_impl(int band_rows, int rank, int nranks, const int32_t* bands, int nbands, uint32_t* d_out,
                           hipStream_t stream);
     const TileCost* last_tc_ = nullptr;   // the last launch's (rt_tile_costs)

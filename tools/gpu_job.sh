@@ -24,6 +24,7 @@
 #   bandcosts      tools/band_tile_costs.py: one rank's band launch (N:rank in BAND_LAYOUTS), tile costs + time
 #   trace_c4       rocprofv3 kernel trace of bench.py (three frames in flight)
 #   trace_c4_1     rocprofv3 kernel trace of bench.py --inflight 1 (per-kernel durations not overlapped)
+#   trace_strips8  rocprofv3 kernel trace of the strips probe at N = 8 (ranks 0 and 7, one and three in flight)
 #   pmc_c4         PMC passes of bench.py (tools/profile_gpu.sh)
 #   trace_c5 / pmc_c5 / trace_hair / pmc_hair   the same for C5 / hair1m
 #   count_c4 / count_c5 / count_hair   RT_COUNT=1 work counts (needs _variants/librt_count.so)
@@ -68,8 +69,11 @@ run_step() {
     nccl) python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 \
               --master-port 29517 tools/nccl_check.py ;;
     tilecosts) python tools/tile_costs.py gpu sphere1m 5 "$OUT/tile_costs.npy" ;;
+    tilecosts_hair) python tools/tile_costs.py gpu hair1m 5 "$OUT/tile_costs_hair.npy" ;;
     bandcosts) BAND_LAYOUTS=${BAND_LAYOUTS:-1:0,8:0,8:3,8:5} python tools/band_tile_costs.py sphere1m ;;
     trace_c4) trace trace_c4 300 ;;
+    trace_strips8) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_strips8" -o run -- \
+                       python3 tools/strip_scaling.py --ranks 8 --steps 40 --inflight 1 3 ;;
     trace_c4_1) trace trace_c4_1 300 --inflight 1 ;;
     trace_c5) trace trace_c5 600 --config sphere1m_refl --steps 4 --warmup 1 ;;
     trace_hair) trace trace_hair 300 --config hair1m ;;
