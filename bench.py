@@ -298,22 +298,23 @@ def sync_leg(r, args, rays):
     rt_ray_trace + rt_post_process + rt_get_image to host, one frame at a time.  Its kernel time (HIP
     events around the one launch, rt_stats.kernel_ms) is the non-overlapped per-launch duration that
     the roofline prices."""
+    img = None   # the caller's image buffer, kept across frames (as a display keeps its QImage)
     for _ in range(args.warmup):
         r.ray_trace()
         r.post_process()
-        r.get_image()
+        img = r.get_image(img)
     kms = []
     t0 = time.perf_counter()
-    img = None
     for _ in range(args.steps):
         r.ray_trace()
         kms.append(r.stats()["kernel_ms"])
         r.post_process()
-        img = r.get_image()
+        img = r.get_image(img)
     el = time.perf_counter() - t0
     return ({"value": round(rays * args.steps / el / 1e6, 3), "unit": "Mrays/s", "ms_per_step": round(1e3 * el / args.steps, 4),
              "kernel_ms": round(float(np.mean(kms)), 4), "frames_in_flight": 1,
-             "what": "rt_ray_trace + rt_post_process + rt_get_image to host, one frame at a time"}, img.ravel())
+             "what": "rt_ray_trace + rt_post_process + rt_get_image into the caller's host buffer, one frame at a "
+                     "time"}, img.ravel().copy())
 
 
 def moving_camera_leg(r, args, pipe, frames, sc, primary):

@@ -209,6 +209,8 @@ Renderer::~Renderer()
     }
     if (fence_stream_) hipStreamDestroy(fence_stream_);
     if (stream_) hipStreamDestroy(stream_);
+    for (hipEvent_t ev : display_ev_)
+        if (ev) hipEventDestroy(ev);
     if (display_stream_) hipStreamDestroy(display_stream_);
     if (display_host_) hipHostFree(display_host_);
     for (void* q : display_old_)
@@ -1606,16 +1608,35 @@ int Renderer::get_image(uint32_t* argb, int32_t* w, int32_t* h)
         }
     }
     const DevBuf& src = img_is_internal_ ? d_internal_ : d_image_;
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(display_host_, src.p, n * 4, hipMemcpyDeviceToHost, display_stream_);
-    if (e == hipSuccess)
-        e = hipStreamSynchronize(display_stream_);
+    // in chunks: the DMA of chunk i + 1 runs while the host copies chunk i out of the pinned staging
+    // buffer (8.3 MB at 1080p: the two serialised took ~0.7 ms)
+    constexpr int NCH = 8;
+    const size_t bytes = n * 4, step = ((bytes + NCH - 1) / NCH + 4095) / 4096 * 4096;
+    if (e == hipSuccess && !display_ev_[0])
+        for (int i = 0; i < NCH && e == hipSuccess; i++)
+            e = hipEventCreateWithFlags(&display_ev_[i], hipEventDisableTiming);
+    int nch = 0;
+    for (size_t off = 0; e == hipSuccess && off < bytes; off += step, nch++) {
+        const size_t len = std::min(step, bytes - off);
+        e = hipMemcpyAsync(static_cast<char*>(display_host_) + off, static_cast<const char*>(src.p) + off, len,
+                           hipMemcpyDeviceToHost, display_stream_);
+        if (e == hipSuccess)
+            e = hipEventRecord(display_ev_[nch], display_stream_);
+    }
+    for (int i = 0; e == hipSuccess && i < nch; i++) {
+        e = hipEventSynchronize(display_ev_[i]);
+        if (e == hipSuccess) {
+            const size_t off = (size_t)i * step;
+            std::memcpy(reinterpret_cast<char*>(argb) + off, static_cast<const char*>(display_host_) + off,
+                        std::min(step, bytes - off));
+        }
+    }
     if (e != hipSuccess) {
+        hipStreamSynchronize(display_stream_);
         // (not err_: the owning thread may be writing it)
         display_err_ = std::string("get_image: ") + hipGetErrorString(e);
         return RT_EHIP;
     }
-    std::memcpy(argb, display_host_, n * 4);
     return RT_OK;
 }
 

@@ -319,6 +319,7 @@ private:
     // non-blocking stream through a pinned staging buffer.
     std::recursive_mutex image_mu_;
     hipStream_t display_stream_ = nullptr;
+    hipEvent_t display_ev_[8] = {};   // get_image's chunks (renderer.cpp get_image)
     void* display_host_ = nullptr;
     size_t display_bytes_ = 0;
     std::vector<void*> display_old_;   // outgrown staging buffers (freed with the renderer)

@@ -215,15 +215,18 @@ class Renderer:
     def post_process(self):
         self._call("rt_post_process")
 
-    def get_image(self) -> np.ndarray:
+    def get_image(self, out=None) -> np.ndarray:
         """Renderer::get_image: the current ARGB32 image as (h, w) uint32 (row 0 = bottom).
         Safe from a display thread while another thread renders (progressive readback): the
-        size query and the copy run under the image lock."""
+        size query and the copy run under the image lock.  ``out``: a (h, w) uint32 array to
+        fill (a display that keeps its image buffer, as a QImage); a new one when it does not
+        match the image's size."""
         w, h = C.c_int32(), C.c_int32()
         self.lock_image()
         try:
             self._call("rt_get_image", ptr(None, _u32p), C.byref(w), C.byref(h))
-            out = np.zeros((h.value, w.value), np.uint32)
+            if out is None or out.shape != (h.value, w.value) or out.dtype != np.uint32 or not out.flags.c_contiguous:
+                out = np.empty((h.value, w.value), np.uint32)
             self._call("rt_get_image", ptr(out, _u32p), C.byref(w), C.byref(h))
         finally:
             self.unlock_image()
