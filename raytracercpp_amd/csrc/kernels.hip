@@ -881,15 +881,32 @@ __device__ __forceinline__ void ph_mark(int k)
 // the wide query's stack (W_STACK), then LDS_SAVE_ENTRIES more from lds_save_slot (trace_pixel)
 constexpr int LDS_SAVE_ENTRIES = 3;
 __host__ __device__ __forceinline__ int lds_save_slot(const KParams& P) { return P.levels > W_STACK ? P.levels : W_STACK; }
+// The plain kernel (3 blocks of 4 waves per CU by its 168 VGPRs) may take up to 160 KB / 3 / 256 lanes = 26
+// LDS entries per lane: its one-lane queries get a deeper stack than W_STACK, so that fewer of them overflow
+// into the 64-entry scratch stack of wide_closest_deep (hair1m: 0.5% of its queries at 16 entries, the
+// longest ones); its lane groups keep the W_STACK ring.  The octree-only plain kernel has no wide stack.
+#ifndef RT_W_STACK_PLAIN
+#define RT_W_STACK_PLAIN 22
+#endif
+constexpr int W_STACK_PLAIN = RT_W_STACK_PLAIN;
+static_assert(W_STACK_PLAIN >= W_STACK && W_STACK_PLAIN + LDS_SAVE_ENTRIES <= 26, "the plain kernel's LDS entries");
+template <bool OCT>
+__host__ __device__ __forceinline__ int lds_save_slot_plain(const KParams& P)
+{
+    const int w = OCT ? 0 : W_STACK_PLAIN;
+    return P.levels > w ? P.levels : w;
+}
 
-struct WStackLds {
-    static constexpr int CAP = W_STACK;
+template <int N = W_STACK>
+struct WStackLdsN {
+    static constexpr int CAP = N;
     uint2* base;
     __device__ __forceinline__ void put(int i, uint2 v) { base[i * BLOCK] = v; }
     __device__ __forceinline__ uint2 get(int i) const { return base[i * BLOCK]; }
     // entry i of the lane 'delta' lanes away (a lane group's steal, wbvh_closest<.., G>)
     __device__ __forceinline__ uint2 get_lane(int delta, int i) const { return base[delta + i * BLOCK]; }
 };
+using WStackLds = WStackLdsN<W_STACK>;
 
 #if RT_COUNT
 // counters[base]: the wave's longest lane's loop iterations, [base + 1]: every lane's, [base + 2]:
@@ -939,18 +956,19 @@ __device__ __noinline__ WDeep wide_closest_deep(const WNode* wnodes, const GTri*
 // certified; false when it must be traced through the octree.
 // rec (optional): on a certified hit, the record built from the wide BVH's own copies (the
 // triangle from wtris, index and material from wmeta), with no further dependent loads.
-template <int G = 1>
+template <int G = 1, int CAP = W_STACK>
 __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit& h, bool& r, uint2* lv,
                                              Rec* rec = nullptr, uint32_t max_steps = 0, bool* longq = nullptr)
 {
+    using Stk = WStackLdsN<G == 1 ? CAP : W_STACK>;   // (a lane group's ring: W_STACK entries)
     const float om = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
-    WStackLds stk{lv};
+    Stk stk{lv};
     WHit w;
     // a ray from the camera position reads the frame's camera risk keys
     const uint64_t* rk = P.wrisk && o.x == P.cam_pos[0] && o.y == P.cam_pos[1] && o.z == P.cam_pos[2] ? P.wrisk : nullptr;
 #if RT_COUNT
     uint32_t wk[4] = {0, 0, 0, 0};
-    int st = wbvh_closest<WStackLds, G>(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, INFINITY, true,
+    int st = wbvh_closest<Stk, G>(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, INFINITY, true,
                           W_QS_CLOSEST, rk, 0, 0.0f);
     count_wave_steps(P, 22, wk[3]);
     if (P.counters) {
@@ -961,7 +979,7 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
                 atomicAdd(&P.counters[16 + c], 1ull);   // uncertified, by reason (wbvh_closest)
     }
 #else
-    int st = wbvh_closest<WStackLds, G>(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, INFINITY,
+    int st = wbvh_closest<Stk, G>(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, INFINITY,
                           true, W_QS_CLOSEST, rk, 0, 0.0f, max_steps);
 #endif
     if (st == W_LONG) {
@@ -1018,18 +1036,19 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
 // Returns true when decided (shadowed in *sh); false: take the octree segment query.
 // light: the ray is one of the frame's shadow rays towards P.light that may read its risk keys
 // (KParams::wrisk; hi >= |light - o|)
-template <int G = 1>
+template <int G = 1, int CAP = W_STACK>
 __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float hi, v3 p, v3 lp, uint2* lv, bool* sh,
                                             bool light)
 {
+    using Stk = WStackLdsN<G == 1 ? CAP : W_STACK>;
     const float om = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
-    WStackLds stk{lv};
+    Stk stk{lv};
     WHit w;
     const uint64_t* rk = light ? P.wrisk : nullptr;
     const float rsub = light ? wrisk_sub(W_QS_SHADOW, hi, P.risk_nu) : 0.0f;
 #if RT_COUNT
     uint32_t wk[4] = {0, 0, 0, 0};
-    int st = wbvh_closest<WStackLds, G>(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, hi, false,
+    int st = wbvh_closest<Stk, G>(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, hi, false,
                           W_QS_SHADOW, rk, 1, rsub);
     count_wave_steps(P, 25, wk[3]);
     if (P.counters) {
@@ -1040,7 +1059,7 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
                 atomicAdd(&P.counters[16 + c], 1ull);   // uncertified, by reason (wbvh_closest)
     }
 #else
-    int st = wbvh_closest<WStackLds, G>(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, hi, false,
+    int st = wbvh_closest<Stk, G>(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, hi, false,
                           W_QS_SHADOW, rk, 1, rsub);
 #endif
     if (st == W_DEEP) {
@@ -1166,7 +1185,8 @@ __device__ bool is_shadowed(const KParams& P, v3 p, v3 n, v3 lp, uint2* lv)
         }
         // (seg_scale > 0: no analytic shapes, so shapes_shadow below has nothing to add)
         bool sh;
-        if (!OCT && P.wnodes && P.nnodes > 0 && !nan && wide_shadow<G>(P, o, d, hi, p, lp, lv, &sh, light))
+        if (!OCT && P.wnodes && P.nnodes > 0 && !nan &&
+            wide_shadow<G, PLAIN ? W_STACK_PLAIN : W_STACK>(P, o, d, hi, p, lp, lv, &sh, light))
             return sh;
         const OctQ q = octree_query<CALL>(P, o, d, -m, hi, P.seg_oct != 0, lv);
         h = q.h;
@@ -1252,7 +1272,7 @@ __device__ int closest_hit(const KParams& P, v3 o, v3 d, Rec& fin, uint2* lv)
         THit h;
         bool r = false;
         const bool wide = !OCT && P.wnodes && P.nnodes > 0 && !ray_is_nan(o, d);
-        if (wide && wide_closest<G>(P, o, d, h, r, lv, &local)) {
+        if (wide && wide_closest<G, PLAIN ? W_STACK_PLAIN : W_STACK>(P, o, d, h, r, lv, &local)) {
             // certified: a hit's record is already in local (a miss leaves it fresh)
             if (r && (local.t < fin.t || fin.t == -1)) {
                 fin = local;
@@ -1523,7 +1543,7 @@ __device__ PixelOut trace_pixel(const KParams& P, v3 cam, v3 rd0, uint2* lv, uin
             const c3 fc = shade_lit<true>(P, cam, rd0, po.fin, ip);
             if (P.compute_shadows)
                 nshadow++;
-            uint2* sv = lv + (size_t)lds_save_slot(P) * BLOCK;
+            uint2* sv = lv + (size_t)lds_save_slot_plain<OCT>(P) * BLOCK;
             sv[0] = make_uint2(fbits(fc.r), fbits(fc.g));
             sv[BLOCK] = make_uint2(fbits(fc.b), (uint32_t)po.fin.mat);
             sv[2 * BLOCK] = make_uint2(fbits(po.fin.t), (uint32_t)po.src);
@@ -3562,7 +3582,10 @@ __global__ __launch_bounds__(256) void wide_gather_kernel(const GTri* __restrict
 // other kernels do not take them (32 -> 38 KB per block cost the 5-wave kernels a block)
 size_t lds_bytes(const KParams& P, bool plain_pixel = false)
 {
-    return (size_t)(lds_save_slot(P) + (plain_pixel ? LDS_SAVE_ENTRIES : 0)) * BLOCK * sizeof(uint2);
+    if (plain_pixel)   // (the plain kernel over the wide BVH, or its octree-only instance without one)
+        return (size_t)((P.wnodes ? lds_save_slot_plain<false>(P) : lds_save_slot_plain<true>(P)) + LDS_SAVE_ENTRIES) *
+               BLOCK * sizeof(uint2);
+    return (size_t)lds_save_slot(P) * BLOCK * sizeof(uint2);
 }
 
 }  // namespace rt
