@@ -2382,6 +2382,139 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_kernel(KParams 
     refl_trace_one<G>(P, A, slot, dir, lv, (uint32_t)A.max_steps);
 }
 
+// Lane refill for the reflection queries (ReflArgs::feed; Aila and Laine's persistent threads with
+// dynamic ray fetch).  Most reflection queries end in a few steps and a few run long: with one query
+// per lane, a wave ran to its longest lane (up to the deferral threshold) with ~15% of its lanes busy
+// (RT_COUNT SIMD efficiency, profiles/r05/c5/work_counts_c5.log).  Here the waves are persistent: a
+// lane whose query ended waits until threshold lanes of its wave wait, then each of them writes its
+// result and takes the next sample slot (one atomic per wave), so that the wave keeps working on fresh
+// queries while its long ones run on.  Per query the wide query is wbvh_closest's (the same state, reset
+// per query, the same steps) and the record the certificate's; the queries it cannot certify (a stack
+// overflow, a tie, a NaN ray) go to the defer list, which refl_trace_long_kernel runs as before (deep
+// retry, octree walk).  The result per slot is refl_trace_one's, bit for bit.
+constexpr int W_STACK_REFL_FEED = 20;   // (160 KB / 4 blocks / 256 lanes / 8 B)
+static_assert(W_STACK_REFL_FEED >= W_STACK, "the feed's stack");
+
+struct ReflFeed {
+    static constexpr bool on = true;
+    bool busy = false;      // the lane holds a query (slot) not yet finished
+    bool drained = false;   // (wave-uniform) every slot has been handed out
+    int threshold;
+    int slot = -1;
+    unsigned count = 0;  // reflection rays of the lane's slots (refl_gen)
+    const KParams* P;
+    const ReflArgs* A;
+    int nslot;
+
+    // defer the lanes' slots (divergent lanes: one atomic per wave)
+    __device__ __forceinline__ void defer() const
+    {
+        const uint64_t mk = __ballot(1);
+        const int leader = __ffsll((unsigned long long)mk) - 1;
+        uint32_t base = 0;
+        if ((int)(threadIdx.x & 63) == leader)
+            base = atomicAdd(A->defer_count, (unsigned)__popcll(mk));
+        base = __shfl(base, leader);
+        A->defer[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u))] = slot;
+    }
+
+    __device__ __forceinline__ void finish(int st, WHit& w, v3 o, v3 d)
+    {
+        busy = false;
+        RawHit H;
+        H.k = -1;
+        H.t = -1.0f;
+        H.u = 1.0f;
+        H.v = 0.0f;
+        bool r = false, ok = st == W_MISS;
+        if (st == W_HIT) {
+            // the certificate (wide_closest): the octree leaf holding the triangle passes the reference's
+            // k-DOP test at t* (bvh.h:79-105)
+            const uint4 M = ldg(P->wmeta + w.k);
+            if (kdop_certifies(load_gnode(P->nodes + M.y), o, d, w.t)) {
+                H.t = w.t;
+                H.u = w.u;
+                H.v = w.v;
+                H.k = (int32_t)M.x;
+                r = ok = true;
+            }
+        }
+        if (!ok) {
+            defer();
+            return;
+        }
+        st3(H.d, d);
+        H.r = (r ? 1 : 0) | (A->fused ? 2 : 0);
+        A->hit[slot] = H;
+    }
+
+    // wave-uniform: the waiting lanes (want) take the next slots; true for a lane given a ray
+    __device__ __forceinline__ bool fetch(bool want, v3& o, v3& d, float& m)
+    {
+        const uint64_t wb = __ballot(want);
+        if (!wb)
+            return false;
+        const int leader = __ffsll((unsigned long long)wb) - 1;
+        int base = 0;
+        if ((int)(threadIdx.x & 63) == leader)
+            base = (int)atomicAdd(A->feed_ticket, (unsigned)__popcll(wb));
+        base = __shfl(base, leader);
+        drained = base + __popcll(wb) >= nslot;
+        if (!want)
+            return false;
+        slot = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(wb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wb, 0u));
+        if (slot >= nslot)
+            return false;
+        v3 dir = mk(0, 0, 0);
+        unsigned c = 0;   // (refl_gen sets it for a frame's first sample: the frame's reflection rays)
+        const bool gen = refl_gen(*P, *A, slot, dir, c);
+        count += c;
+        if (!gen) {
+            if (A->fused) {   // no ray (pass1 skips it: bit 1 clear)
+                RawHit H;
+                H.t = H.u = H.v = 0.0f;
+                H.k = -1;
+                st3(H.d, dir);
+                H.r = 0;
+                A->hit[slot] = H;
+            }
+            return false;
+        }
+        const FrameRec& F = A->fr[A->order[A->c0 + slot / A->stride]];
+        o = ld3(F.ro);
+        d = dir;
+        if (ray_is_nan(o, d) || !(P->wnodes && P->nnodes > 0)) {   // (refl_trace_one's octree path)
+            defer();
+            return false;
+        }
+        const float om = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
+        m = 0x1p-16f * (om + P->scene_scale);
+        busy = true;
+        return true;
+    }
+};
+
+__global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_feed_kernel(KParams P_arg, ReflArgs A)
+{
+    const KParams& P = kernel_params();
+    (void)P_arg;
+    extern __shared__ uint2 lds_levels[];
+    uint2* lv = lds_levels + threadIdx.x;
+    ReflFeed feed;
+    feed.threshold = A.feed;
+    feed.P = &P;
+    feed.A = &A;
+    feed.nslot = (A.c1 - A.c0) * A.stride;
+    // its one-lane queries take the reflection kernels' LDS budget (4 blocks per CU: 40 KB, 20 entries per
+    // lane): fewer overflow into the defer list
+    WStackLdsN<W_STACK_REFL_FEED> stk{lv};
+    WHit w;
+    wbvh_closest<WStackLdsN<W_STACK_REFL_FEED>, 1, ReflFeed>(P.wnodes, P.wtris, mk(0, 0, 0), mk(1, 0, 0), 0.0f, stk, w,
+                                                             nullptr, INFINITY, true, W_QS_CLOSEST, nullptr, 0, 0.0f, 0u,
+                                                             &feed);
+    wave_count_add(&P.counters[1], feed.count);
+}
+
 #ifndef RT_REFL_LONG_QUEUE
 #define RT_REFL_LONG_QUEUE 1   // refl_trace_long_kernel: waves take batches from a ticket (0: grid stride)
 #endif
@@ -3847,7 +3980,15 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_stage
     dim3 gs((nslot + rt::BLOCK - 1) / rt::BLOCK), gf((nframes + rt::BLOCK - 1) / rt::BLOCK);
     size_t lds = rt::lds_bytes(*P);
     switch (stage) {
-    case 1: hipLaunchKernelGGL(rt::refl_trace_kernel, dim3(gs.x * RT_REFL_G), dim3(rt::BLOCK), lds, stream, *P, *A); break;
+    case 1:
+        if (A->feed > 0)   // persistent waves (lane refill): the reflection kernels' residency
+            hipLaunchKernelGGL(rt::refl_trace_feed_kernel,
+                               dim3(std::max(1u, std::min<unsigned>(gs.x, (unsigned)(P->max_blocks / 8 * RT_OCC_REFL)))),
+                               dim3(rt::BLOCK), (size_t)std::max(P->levels, rt::W_STACK_REFL_FEED) * rt::BLOCK * sizeof(uint2),
+                               stream, *P, *A);
+        else
+            hipLaunchKernelGGL(rt::refl_trace_kernel, dim3(gs.x * RT_REFL_G), dim3(rt::BLOCK), lds, stream, *P, *A);
+        break;
     case 7: hipLaunchKernelGGL(rt::refl_trace_long_kernel, dim3(std::min<unsigned>(gs.x, 2048u)), dim3(rt::BLOCK), lds,
                                stream, *P, *A); break;
     case 2: hipLaunchKernelGGL(rt::refl_pass1_kernel, gf, dim3(rt::BLOCK), 0, stream, *P, *A); break;

@@ -234,6 +234,11 @@ struct ReflArgs {
     int32_t* defer;          // sample slots whose query ran past max_steps in refl_trace_kernel (traced
     unsigned int* defer_count;   // again by refl_trace_long_kernel, whole waves of long queries); 0: off
     int32_t max_steps;
+    // > 0: refl_trace_feed_kernel instead of refl_trace_kernel (persistent waves, lane refill when this
+    // many lanes wait; the queries the wide BVH does not certify go to the defer list); feed_ticket: its
+    // next slot
+    int32_t feed;
+    unsigned int* feed_ticket;
 };
 
 // ---- hybrid rasterisation (kernels.hip "Renderer::raster_trace") ----

@@ -132,6 +132,8 @@ Knobs Knobs::from_env()
         k.split_parts = atoi(v) == 2 * SPLIT_G ? 2 * SPLIT_G : SPLIT_G;
     if (const char* v = getenv("RT_REFL_DEFER"))   // loop iterations before a reflection query is deferred
         k.refl_defer = std::max(0, atoi(v));
+    if (const char* v = getenv("RT_REFL_FEED"))    // lane refill of the reflection queries at this many waiting lanes
+        k.refl_feed = std::min(64, std::max(0, atoi(v)));
     {
         const char* v = getenv("RT_INJECT_FRAME_FAIL");   // tests: the k-th ray_trace fails after its image start
         k.inject_fail = v ? std::atoi(v) : 0;
@@ -1242,7 +1244,10 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
         A.defer = L.list.as<int32_t>();
         A.defer_count = L.cnt.as<unsigned int>() + 2;
         A.max_steps = knobs_.refl_defer;
-        if ((e = hipMemsetAsync(L.cnt.p, 0, 16, stream)) != hipSuccess)   // (+ the long kernel's ticket)
+        // lane refill (kernels.hip refl_trace_feed_kernel; RT_REFL_FEED=k: refill at k waiting lanes, 0: off)
+        A.feed = knobs_.refl_feed;
+        A.feed_ticket = L.cnt.as<unsigned int>() + 4;
+        if ((e = hipMemsetAsync(L.cnt.p, 0, 32, stream)) != hipSuccess)   // (+ the long kernel's and the feed's tickets)
             return hip_fail(e, "hipMemsetAsync");
         // fused (default): trace, pass1 (+ shadow list), shadow (+ spawn); RT_REFL_FUSE=0: trace,
         // pass1, list, shadow, spawn

@@ -75,6 +75,9 @@ struct Knobs {
     float heavy_split = 0.5f; // RT_HEAVY_SPLIT=c: split the heavy tiles costing >= c x the launch's mean
                               // cycles per wave (heavy_prep_kernel)
     int refl_defer = 32;      // RT_REFL_DEFER=k: reflection queries past k loop iterations finish in a pass
+    int refl_feed = 24;       // RT_REFL_FEED=k: the reflection queries by refl_trace_feed_kernel (lane refill at k
+                              // waiting lanes of a wave; C5 16 / 24 / 32 / 48: 1,128 / 1,101 / 1,103 / 1,155 ms per
+                              // frame, 1,195 without); 0: refl_trace_kernel with its deferral
                               // of their own (9; 0: never)
     int inject_fail = 0;      // RT_INJECT_FRAME_FAIL=k (tests): the k-th ray_trace fails after its image start
     bool async_accel = true;  // RT_ASYNC_ACCEL=0: the leaf cones / slabs and the wide BVH are built

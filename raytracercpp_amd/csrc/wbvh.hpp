@@ -810,14 +810,32 @@ RT_HD T wg_read(T x, int i)
 // the final best: skipped soundly), so the group's lanes together test every triangle the G = 1 query
 // would need; the answer (minimum over the lanes' records, a tie when two lanes hold it or one lane saw
 // two) is the same on every lane of the group.
-template <class Stack, int G = 1>
+// No lane refill (the default): one query per call.
+struct WNoFeed {
+    static constexpr bool on = false;
+    bool busy = false;
+    bool drained = true;   // (wave-uniform) the feed has no query left to hand out
+    int threshold = 64;
+    template <class H> RT_HD void finish(int, H&, v3, v3) {}
+    RT_HD bool fetch(bool, v3&, v3&, float&) { return false; }
+};
+
+template <class Stack, int G = 1, class Feed = WNoFeed>
 RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m, Stack& stk, WHit& h,
                        uint32_t* work = nullptr, float hi = INFINITY, bool ties = true, float QS = 0x1p-8f,
-                       const uint64_t* risk = nullptr, int rsel = 0, float rsub = 0.0f, uint32_t max_steps = 0)
+                       const uint64_t* risk = nullptr, int rsel = 0, float rsub = 0.0f, uint32_t max_steps = 0,
+                       Feed* feed = nullptr)
 {
     static_assert(G == 1 || ((G & (G - 1)) == 0 && G <= 8 && (Stack::CAP & (Stack::CAP - 1)) == 0),
                   "a lane group: a power of two up to 8 lanes, a ring stack of 2^k entries");
     static_assert(G == 1 || !W_STEP_CAP, "a lane group leaves the loop together");
+    // Feed::on (device, one lane per query): lane refill.  The wave stays in the loop; a lane whose query
+    // ended waits, and when at least feed->threshold lanes (or every lane) wait, each hands its query's
+    // status and record to feed->finish and takes the next ray from feed->fetch (o, d, m; hi, ties, QS
+    // and the risk words are the same for every query of the feed).  The per-query work is the one-query
+    // call's: the same state, reset per query, the same steps.  Returns W_MISS once the feed is drained.
+    constexpr bool FEED = Feed::on;
+    static_assert(!FEED || (G == 1 && !W_STEP_CAP), "lane refill: one lane per query");
     // the stack index of entry i (a ring in a lane group)
     auto slot = [](int i) { return G > 1 ? (i & (Stack::CAP - 1)) : i; };
     h.t = INFINITY;
@@ -829,31 +847,87 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
     // slab's t range then exceeds 2^70 m / |d| on the far side, far beyond the scene's, so
     // it constrains only as much as the true one does (the margin covers the origin's side).
     const float DMIN = 0x1p-100f;
-    const float ix = 1.0f / (fabsf(d.x) < DMIN ? copysignf(DMIN, d.x) : d.x);
-    const float iy = 1.0f / (fabsf(d.y) < DMIN ? copysignf(DMIN, d.y) : d.y);
-    const float iz = 1.0f / (fabsf(d.z) < DMIN ? copysignf(DMIN, d.z) : d.z);
-    // per axis, the byte row of the entry (near) planes: q_lo where the direction is positive,
-    // q_hi where it is negative; the near plane is widened by -M sign(d), the far one by +M sign(d)
-    const bool nx_lo = !(ix < 0.0f), ny_lo = !(iy < 0.0f), nz_lo = !(iz < 0.0f);
-    const float aix = fabsf(ix), aiy = fabsf(iy), aiz = fabsf(iz);
-
     constexpr float SL = 0x1p-20f;   // relative slack over the rounding of a slab parameter (<= 3 ulp)
     constexpr float NLH = 127.9f;    // |N| of a quantised slab normal: 127 +- sqrt(3) / 2 (wbvh.cpp quantise)
-    // |d| rounded up (sqrt and dot within 2^-22), times the cone step: threshold = c * cstep
-    const float dl = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z) * (1.0f + 0x1p-20f);
-    const float cstep = dl * W_CONE_STEP;
-    // 1 / |d| rounded up (|d| rounded down, the hardware reciprocal within 1 ulp)
-    const float idl = fast_rcp(sqrtf(d.x * d.x + d.y * d.y + d.z * d.z) * (1.0f - 0x1p-20f)) * (1.0f + 0x1p-18f);
-    const float icp = (1.0f - 0x1p-18f) / (NLH * dl);   // cos(angle(N, -d)) >= -a icp
-    const float iqd = (1.0f - 0x1p-20f) / (QS * dl);        // a risk key's t bound: key / (QS |d|)
+    float ix, iy, iz, aix, aiy, aiz, dl, cstep, idl, icp, iqd;
+    bool nx_lo, ny_lo, nz_lo;
+    auto setup = [&]() {
+        ix = 1.0f / (fabsf(d.x) < DMIN ? copysignf(DMIN, d.x) : d.x);
+        iy = 1.0f / (fabsf(d.y) < DMIN ? copysignf(DMIN, d.y) : d.y);
+        iz = 1.0f / (fabsf(d.z) < DMIN ? copysignf(DMIN, d.z) : d.z);
+        // per axis, the byte row of the entry (near) planes: q_lo where the direction is positive,
+        // q_hi where it is negative; the near plane is widened by -M sign(d), the far one by +M sign(d)
+        nx_lo = !(ix < 0.0f);
+        ny_lo = !(iy < 0.0f);
+        nz_lo = !(iz < 0.0f);
+        aix = fabsf(ix);
+        aiy = fabsf(iy);
+        aiz = fabsf(iz);
+        // |d| rounded up (sqrt and dot within 2^-22), times the cone step: threshold = c * cstep
+        dl = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z) * (1.0f + 0x1p-20f);
+        cstep = dl * W_CONE_STEP;
+        // 1 / |d| rounded up (|d| rounded down, the hardware reciprocal within 1 ulp)
+        idl = fast_rcp(sqrtf(d.x * d.x + d.y * d.y + d.z * d.z) * (1.0f - 0x1p-20f)) * (1.0f + 0x1p-18f);
+        icp = (1.0f - 0x1p-18f) / (NLH * dl);   // cos(angle(N, -d)) >= -a icp
+        iqd = (1.0f - 0x1p-20f) / (QS * dl);    // a risk key's t bound: key / (QS |d|)
+    };
+    setup();
     float best_s = hi + fabsf(hi) * SL;   // h.t (or hi) plus slack: a child entered at or below it may hold a hit
     bool tie = false, nanhit = false, infhit = false;
     float dropped = INFINITY;   // the smallest key of the children a full stack could not take
     int sp = 0, bot = 0;        // the stack's entries [bot, sp) (bot > 0: entries taken by the group)
-    uint32_t cur = G > 1 && wg_lane<G>() != 0 ? W_EMPTY : 0u;   // root node
+    uint32_t cur = FEED || (G > 1 && wg_lane<G>() != 0) ? W_EMPTY : 0u;   // root node (FEED: no query yet)
     uint32_t nn = 0, nt = 0;
     uint32_t steps = 0;   // loop iterations (node or leaf visits)
-    while (G > 1 ? wg_bits<G>(cur != W_EMPTY) != 0u : cur != W_EMPTY) {
+    // the status of the lane's query once its loop is over (G = 1; the tail below for every G)
+    auto status = [&]() -> int {
+        const bool ovf = dropped < INFINITY && dropped <= best_s;
+        if (nanhit)
+            return W_UNCERT;
+        if (h.k < 0) {
+            if (infhit)
+                return W_UNCERT;
+            if (ovf)
+                return W_DEEP;
+            h.t = -1.0f;   // HitInfo() (hitInfo.h:8-24): t = -1, u = 1, v = 0
+            return W_MISS;
+        }
+        if ((ties && tie) || !(h.t > 0.0f && h.t < INFINITY))
+            return W_UNCERT;
+        return ovf ? W_DEEP : W_HIT;
+    };
+    // FEED: at the loop's head, with the wave together; false once the feed is drained and no lane runs
+    auto refill = [&]() -> bool {
+        if constexpr (FEED) {
+#if defined(__HIP_DEVICE_COMPILE__)
+            const bool idle_lane = cur == W_EMPTY;
+            const uint64_t idle = __ballot(idle_lane);
+            if (idle != 0ull && (idle == __ballot(1) || __popcll(idle) >= feed->threshold)) {
+                if (idle_lane && feed->busy)
+                    feed->finish(status(), h, o, d);
+                if (feed->fetch(idle_lane, o, d, m)) {   // (wave-uniform call; true for the lanes given a ray)
+                    setup();
+                    h.t = INFINITY;
+                    h.u = 1.0f;
+                    h.v = 0.0f;
+                    h.k = -1;
+                    best_s = hi + fabsf(hi) * SL;
+                    tie = nanhit = infhit = false;
+                    dropped = INFINITY;
+                    sp = bot = 0;
+                    cur = 0u;
+                }
+                return __ballot(cur != W_EMPTY) != 0ull || !feed->drained;
+            }
+#endif
+        }
+        return true;
+    };
+    while (FEED ? refill() : (G > 1 ? wg_bits<G>(cur != W_EMPTY) != 0u : cur != W_EMPTY)) {
+        if constexpr (FEED) {
+            if (cur == W_EMPTY)
+                continue;   // (waits for the refill)
+        }
         ++steps;
         if (max_steps && steps > max_steps)
             return W_LONG;
@@ -1285,6 +1359,8 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
         work[2] = (overflow ? 1u : 0u) | (nanhit ? 2u : 0u) | (h.k < 0 && infhit ? 4u : 0u) |
                   (h.k >= 0 && ties && tie ? 8u : 0u) | (h.k >= 0 && !(h.t > 0.0f && h.t < INFINITY) ? 16u : 0u);
     }
+    if constexpr (FEED)
+        return W_MISS;   // (every query went to feed->finish)
     if (nanhit)
         return W_UNCERT;
     if (h.k < 0) {
