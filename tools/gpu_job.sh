@@ -60,6 +60,8 @@ run_step() {
     smoke) python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
     bench) python bench.py $BA ;;
     bench_fast) python bench.py --no-cpu-baseline $BA ;;
+    bench_q2) python bench.py --no-cpu-baseline --no-legs --inflight 2 $BA ;;
+    bench_q4) python bench.py --no-cpu-baseline --no-legs --inflight 4 $BA ;;
     bench_c5) python bench.py --config sphere1m_refl --steps 6 --warmup 2 --no-cpu-baseline $BA ;;
     bench_hair) python bench.py --config hair1m --steps 20 --warmup 3 --no-cpu-baseline $BA ;;
     strips1) python tools/strip_scaling.py --ranks 1 2 4 8 --steps 40 --all-ranks --inflight 1 ;;
