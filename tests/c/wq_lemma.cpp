@@ -13,8 +13,10 @@
 //       u (30 L + 12 D + 24 D / s) / s2] of the plane (wq_h0 with QS = q, the strongest form).
 // Random triangles (slivers with sines down to 1e-7 and obtuse ones, scales 2^-6 .. 2^6, offsets up to
 // 8x the scale), rays aimed at points in and around them with q log-uniform in [1e-10, 1] (so Q = q s
-// covers 1e-9 .. 1 and below), origins at 0.1 .. 300 edge lengths.  Prints "ok <acceptances> <max
-// ratio dist/R> <max plane/eta> <max origin/H0>" or the first violation.
+// covers 1e-9 .. 1 and below), origins at 0.1 .. 300 edge lengths.  The same hits are also checked
+// against the float functions the kernels evaluate (wq_reach, wq_split, wq_eta, wq_h0 on float bounds of
+// the exact quantities).  Prints "ok <acceptances> <max ratio dist/R> <max plane/eta> <max origin/H0> ...
+// float-bounds <|p'-P'|/E> <lat/Rlat> <plane/eta> <origin/H0>" or the first violation.
 #include <atomic>
 #include <cmath>
 #include <cstdint>
@@ -68,7 +70,7 @@ int main(int argc, char** argv)
     std::atomic<long> accepted{0}, samples{0};
     std::atomic<int> failed{0};
     std::mutex mu;
-    ld worst[5] = {0, 0, 0, 0, 0};
+    ld worst[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     long bins[10] = {};   // acceptances by floor(-log10 Q), Q = q s
     auto work = [&](unsigned tid) {
         std::mt19937_64 rng(0x5EED0000ull + tid);
@@ -79,7 +81,7 @@ int main(int argc, char** argv)
             double x = N(rng), y = N(rng), z = N(rng), l = std::sqrt(x * x + y * y + z * z);
             return l3(x / l, y / l, z / l);
         };
-        ld w[5] = {0, 0, 0, 0, 0};
+        ld w[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
         long lb[10] = {};
         while (accepted.load(std::memory_order_relaxed) < target && !failed.load()) {
             samples++;
@@ -180,6 +182,35 @@ int main(int argc, char** argv)
                     bad |= !(lat <= Rlat);
                 }
             }
+            // the SHIPPED float bounds (wbvh.hpp wq_reach / wq_split / wq_eta / wq_h0, as the query evaluates
+            // them) on float bounds of the exact quantities (q, s, s2 rounded down; L, D rounded up): a typo
+            // or a rounding slip in the constants the kernels run would show here, not only in an oracle frame
+            {
+                auto dn = [](ld x) { float f = (float)x; return (ld)f > x ? std::nextafterf(f, 0.0f) : f; };
+                auto up = [](ld x) { float f = (float)x; return (ld)f < x ? std::nextafterf(f, INFINITY) : f; };
+                const float qf = dn(qq), sf = dn(s), s2f = dn(s2), Lf = up(L), Df = up(D), Dvf = up(Dv);
+                const rt::WReach wr = rt::wq_reach(qf, sf, Lf, Dvf);
+                if (wr.E < INFINITY) {
+                    const L3 Pq = A + AB * (ld)u + AC * (ld)v;
+                    const L3 cp = closest_on_tri(Pp, A, A + AB, A + AC);
+                    const ld dist = lenl(Pp - cp), pP = lenl(Pp - Pq);
+                    float Rlat, Rpar;
+                    rt::wq_split(wr, Lf, Dvf, Rlat, Rpar);
+                    const float eta = rt::wq_eta(wr, Lf, Dvf);
+                    const ld dl = lenl(Dd);
+                    const L3 dh = Dd * (1 / dl);
+                    const ld x = std::max(-(ld)Rpar, std::min((ld)Rpar, dotl(Pq - Pp, dh)));
+                    const ld lat = lenl(Pq - (Pp + dh * x));
+                    w[5] = fmaxl(w[5], pP / wr.E);
+                    w[6] = fmaxl(w[6], lat / Rlat);
+                    w[7] = fmaxl(w[7], pl / eta);
+                    bad |= !(pP <= wr.E) || !(dist <= wr.E + 2.02L * uu * L) || !(lat <= Rlat) || !(pl <= eta);
+                }
+                // case (b) with QS = q rounded up (the strongest form the kernels can evaluate)
+                const float h0 = rt::wq_h0(up(qq), Lf, Df, sf, s2f);
+                w[8] = fmaxl(w[8], od / h0);
+                bad |= !(od <= h0);
+            }
             w[0] = fmaxl(w[0], r0);
             w[1] = fmaxl(w[1], r1);
             w[2] = fmaxl(w[2], r2);
@@ -193,7 +224,7 @@ int main(int argc, char** argv)
             }
         }
         std::lock_guard<std::mutex> g(mu);
-        for (int i = 0; i < 5; i++)
+        for (int i = 0; i < 9; i++)
             worst[i] = fmaxl(worst[i], w[i]);
         for (int i = 0; i < 10; i++)
             bins[i] += lb[i];
@@ -209,6 +240,6 @@ int main(int argc, char** argv)
                 worst[2], worst[3], worst[4], samples.load());
     for (int i = 0; i < 10; i++)
         std::printf(" %ld", bins[i]);
-    std::printf("\n");
+    std::printf(" float-bounds %.4Lg %.4Lg %.4Lg %.4Lg\n", worst[5], worst[6], worst[7], worst[8]);
     return 0;
 }

@@ -5,7 +5,8 @@ checked directly on Moller-Trumbore's float arithmetic (mt_record = triangle.cpp
 accepted hits of random triangles (slivers and obtuse ones included) and rays with |cos(n, d)| from
 1e-10 to 1, the reported point lies within R of its triangle and within eta of its plane (case (a)),
 and the origin within H0 of the plane (case (b)), with the exact constants of wbvh.hpp, evaluated in
-long double by tests/c/wq_lemma.cpp.
+long double by tests/c/wq_lemma.cpp, and with the float functions the kernels run (wq_reach, wq_split,
+wq_eta, wq_h0 on float bounds of the exact quantities).
 2. The metadata the proof reads: the checkers report a tree's conditioning bytes and a frame's risk
 words that are not sound (tests/c/wbvh_mutation.cpp).  CPU only."""
 import os
@@ -25,8 +26,12 @@ def test_reported_points_within_the_query_bounds(tmp_path):
     f = out.stdout.split()
     assert int(f[1]) >= 10_000_000
     # every Q = q sin(alpha) decade from 1 to 1e-9 and below holds acceptances
-    decades = [int(x) for x in f[f.index("Q-decades") + 1:]]
+    decades = [int(x) for x in f[f.index("Q-decades") + 1:f.index("float-bounds")]]
     assert len(decades) == 10 and min(decades) > 1000, decades
+    # the float functions the kernels evaluate hold on the same hits (ratios <= 1; the exit status
+    # already fails on a violation)
+    ratios = [float(x) for x in f[f.index("float-bounds") + 1:]]
+    assert len(ratios) == 4 and max(ratios) <= 1.0 and min(ratios) > 0.0, ratios
     print(out.stdout)
 
 
