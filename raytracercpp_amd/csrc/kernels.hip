@@ -2519,7 +2519,8 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_feed_kernel(KPa
 #define RT_REFL_LONG_QUEUE 1   // refl_trace_long_kernel: waves take batches from a ticket (0: grid stride)
 #endif
 #ifndef RT_REFL_LONG_G
-#define RT_REFL_LONG_G 4   // lanes per deferred reflection query (refl_trace_long_kernel)
+#define RT_REFL_LONG_G 8   // lanes per deferred reflection query (refl_trace_long_kernel; r06: with lane refill only
+                           // the overflowed / uncertified queries come here, the longest: C5 1,105 -> 1,078 ms at 8)
 #endif
 // The queries refl_trace_kernel deferred (ReflArgs::defer): traced to the end in waves of long
 // queries only, each by a lane group of RT_REFL_LONG_G lanes (wbvh_closest<.., G>: one stack shared
