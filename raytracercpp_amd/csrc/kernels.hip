@@ -2448,8 +2448,9 @@ struct ReflFeed {
         A->hit[slot] = H;
     }
 
-    // wave-uniform: the waiting lanes (want) take the next slots; true for a lane given a ray
-    __device__ __forceinline__ bool fetch(bool want, v3& o, v3& d, float& m)
+    // wave-uniform: the waiting lanes (want) take the next slots; true for a lane given a ray (hi, risk and
+    // rsub stay the call's: INFINITY, none, 0)
+    __device__ __forceinline__ bool fetch(bool want, v3& o, v3& d, float& m, float&, const uint64_t*&, float&)
     {
         const uint64_t wb = __ballot(want);
         if (!wb)
@@ -2708,6 +2709,23 @@ __global__ __launch_bounds__(BLOCK) void refl_list_kernel(KParams P, ReflArgs A)
 
 __device__ __forceinline__ int spawn_sample(const KParams& P, const ReflArgs& A, int slot, SampleRec& S, bool sh);
 
+// a sample's shadow decided: its record, and (fused) the child frame it spawns and the colour it returns
+__device__ __forceinline__ void refl_shadow_done(const KParams& P, const ReflArgs& A, int slot, bool sh)
+{
+    SampleRec& S = A.sm[slot];
+    S.sh = sh ? 1 : 0;
+    if (A.fused) {
+        // the colour this sample returns (resolve, below): its child frame's, or its own finished shade
+        const int child = spawn_sample(P, A, slot, S, sh);
+        c3 c = col(0.0f, 0.0f, 0.0f);
+        if (child < 0) {
+            const float* m = mat_of(P, S.mat);
+            c = shade_finish(P, shade_shadow_emit(P, ldc(S.fc), m, sh), m, col(0, 0, 0));
+        }
+        A.res[slot] = make_float4(c.r, c.g, c.b, __int_as_float(child));
+    }
+}
+
 // shadow: is_shadowed (renderer.cpp:340-402) for every shaded sample (via the list)
 #ifndef RT_REFL_SHADOW_CALL
 #define RT_REFL_SHADOW_CALL 1   // the shadow pass's octree fallback out of line (octree_query_call)
@@ -2726,18 +2744,123 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_shadow_kernel(KParams
     const int slot = A.list[t];
     SampleRec& S = A.sm[slot];
     v3 light = mk(P.light[0], P.light[1], P.light[2]);
-    const bool sh = is_shadowed<false, 1, RT_REFL_SHADOW_CALL != 0>(P, ld3(S.ip), ld3(S.nrm), light, lv);
-    S.sh = sh ? 1 : 0;
-    if (A.fused) {
-        // the colour this sample returns (resolve, below): its child frame's, or its own finished shade
-        const int child = spawn_sample(P, A, slot, S, sh);
-        c3 c = col(0.0f, 0.0f, 0.0f);
-        if (child < 0) {
-            const float* m = mat_of(P, S.mat);
-            c = shade_finish(P, shade_shadow_emit(P, ldc(S.fc), m, sh), m, col(0, 0, 0));
-        }
-        A.res[slot] = make_float4(c.r, c.g, c.b, __int_as_float(child));
+    refl_shadow_done(P, A, slot, is_shadowed<false, 1, RT_REFL_SHADOW_CALL != 0>(P, ld3(S.ip), ld3(S.nrm), light, lv));
+}
+
+// Lane refill for the shadow pass (ReflArgs::shadow_feed; the reflection queries' ReflFeed, above): most
+// shadow segments end in a few steps and a few run long (lane utilisation ~0.2 with one segment per
+// lane).  Per list entry the query is is_shadowed's wide part (wide_shadow: the segment [0, hi], no ties,
+// the light's risk words when they hold for the ray) and the decision its; the entries it does not decide
+// (a stack overflow, an uncertified hit, a NaN ray, no segment query) go to the deferred list, which
+// refl_shadow_kernel runs as before (deep retry, octree segment query).  Each entry's result is
+// refl_shadow_kernel's, bit for bit.
+struct ShadowFeed {
+    static constexpr bool on = true;
+    bool busy = false;
+    bool drained = false;
+    int threshold;
+    int slot = -1;
+    const KParams* P;
+    const ReflArgs* A;
+    int nlist;
+    v3 light;
+
+    __device__ __forceinline__ void defer() const
+    {
+        const uint64_t mk = __ballot(1);
+        const int leader = __ffsll((unsigned long long)mk) - 1;
+        uint32_t base = 0;
+        if ((int)(threadIdx.x & 63) == leader)
+            base = atomicAdd(A->sdefer_count, (unsigned)__popcll(mk));
+        base = __shfl(base, leader);
+        A->sdefer[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u))] = slot;
     }
+
+    __device__ __forceinline__ void finish(int st, WHit& w, v3 o, v3 d)
+    {
+        busy = false;
+        bool sh = false;
+        if (st == W_HIT) {
+            // wide_shadow: a certified minimum hit t* <= hi is the reference's record t
+            if (!kdop_certifies(load_gnode(P->nodes + ldg(P->wmeta + w.k).y), o, d, w.t)) {
+                defer();
+                return;
+            }
+            const v3 p = ld3(A->sm[slot].ip);
+            const v3 q = o + d * w.t;
+            sh = length2(p - q) < length2(p - light);
+        } else if (st != W_MISS) {   // (a miss: lit)
+            defer();
+            return;
+        }
+        refl_shadow_done(*P, *A, slot, sh);
+    }
+
+    __device__ __forceinline__ bool fetch(bool want, v3& o, v3& d, float& m, float& hi, const uint64_t*& risk, float& rsub)
+    {
+        const uint64_t wb = __ballot(want);
+        if (!wb)
+            return false;
+        const int leader = __ffsll((unsigned long long)wb) - 1;
+        int base = 0;
+        if ((int)(threadIdx.x & 63) == leader)
+            base = (int)atomicAdd(A->shadow_ticket, (unsigned)__popcll(wb));
+        base = __shfl(base, leader);
+        drained = base + __popcll(wb) >= nlist;
+        if (!want)
+            return false;
+        const int t = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(wb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wb, 0u));
+        if (t >= nlist)
+            return false;
+        slot = A->list[t];
+        if (!P->compute_shadows) {   // (is_shadowed: lit)
+            refl_shadow_done(*P, *A, slot, false);
+            return false;
+        }
+        const SampleRec& S = A->sm[slot];
+        const v3 p = ld3(S.ip), n = ld3(S.nrm);
+        o = p + n * 1.0e-4f;
+        d = normalize(light - p);
+        if (!(P->enable_bvh && P->seg_scale > 0.0f && P->wnodes && P->nnodes > 0)) {
+            defer();
+            return false;
+        }
+        // is_shadowed's segment end and risk words, the same expressions
+        const TRay R0 = make_ray(*P, o, d);
+        const float ms = seg_margin(*P, R0);
+        const float nl = fabsf(n.x) + fabsf(n.y) + fabsf(n.z);
+        hi = (sqrtf(length2(p - light)) + 1.0e-4f * nl) * (1.0f + 0x1p-10f) + ms;
+        if (R0.nan) {
+            defer();
+            return false;
+        }
+        const bool lr = P->wrisk && hi <= P->risk_G && nl <= P->risk_nl;
+        risk = lr ? P->wrisk : nullptr;
+        rsub = lr ? wrisk_sub(W_QS_SHADOW, hi, P->risk_nu) : 0.0f;
+        const float om = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
+        m = 0x1p-16f * (om + P->scene_scale);
+        busy = true;
+        return true;
+    }
+};
+
+__global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_shadow_feed_kernel(KParams P_arg, ReflArgs A)
+{
+    const KParams& P = kernel_params();
+    (void)P_arg;
+    extern __shared__ uint2 lds_levels[];
+    uint2* lv = lds_levels + threadIdx.x;
+    ShadowFeed feed;
+    feed.threshold = A.shadow_feed;
+    feed.P = &P;
+    feed.A = &A;
+    feed.nlist = (int)*A.list_count;
+    feed.light = mk(P.light[0], P.light[1], P.light[2]);
+    WStackLdsN<W_STACK_REFL_FEED> stk{lv};
+    WHit w;
+    wbvh_closest<WStackLdsN<W_STACK_REFL_FEED>, 1, ShadowFeed>(P.wnodes, P.wtris, mk(0, 0, 0), mk(1, 0, 0), 0.0f, stk, w,
+                                                               nullptr, INFINITY, false, W_QS_SHADOW, nullptr, 1, 0.0f, 0u,
+                                                               &feed);
 }
 
 // a shaded sample with a reflective material becomes a frame of the next level (its
@@ -3993,7 +4116,20 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_stage
     case 7: hipLaunchKernelGGL(rt::refl_trace_long_kernel, dim3(std::min<unsigned>(gs.x, 2048u)), dim3(rt::BLOCK), lds,
                                stream, *P, *A); break;
     case 2: hipLaunchKernelGGL(rt::refl_pass1_kernel, gf, dim3(rt::BLOCK), 0, stream, *P, *A); break;
-    case 3: hipLaunchKernelGGL(rt::refl_shadow_kernel, gs, dim3(rt::BLOCK), lds, stream, *P, *A); break;
+    case 3:
+        if (A->shadow_feed > 0 && A->fused && !RT_COUNT) {
+            // persistent waves (lane refill), then the entries they deferred by the one-query kernel
+            hipLaunchKernelGGL(rt::refl_shadow_feed_kernel,
+                               dim3(std::max(1u, std::min<unsigned>(gs.x, (unsigned)(P->max_blocks / 8 * RT_OCC_REFL)))),
+                               dim3(rt::BLOCK), (size_t)std::max(P->levels, rt::W_STACK_REFL_FEED) * rt::BLOCK * sizeof(uint2),
+                               stream, *P, *A);
+            rt::ReflArgs D = *A;
+            D.list = A->sdefer;
+            D.list_count = A->sdefer_count;
+            hipLaunchKernelGGL(rt::refl_shadow_kernel, gs, dim3(rt::BLOCK), lds, stream, *P, D);
+        } else
+            hipLaunchKernelGGL(rt::refl_shadow_kernel, gs, dim3(rt::BLOCK), lds, stream, *P, *A);
+        break;
     case 4: hipLaunchKernelGGL(rt::refl_spawn_kernel, gs, dim3(rt::BLOCK), 0, stream, *P, *A); break;
     case 6: hipLaunchKernelGGL(rt::refl_list_kernel, gs, dim3(rt::BLOCK), 0, stream, *P, *A); break;
     default: hipLaunchKernelGGL(rt::refl_resolve_kernel, gf, dim3(rt::BLOCK), 0, stream, *P, *A); break;

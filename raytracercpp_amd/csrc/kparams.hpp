@@ -239,6 +239,12 @@ struct ReflArgs {
     // next slot
     int32_t feed;
     unsigned int* feed_ticket;
+    // > 0 (fused only): the shadow pass by refl_shadow_feed_kernel (lane refill at this many waiting lanes;
+    // shadow_ticket its next list entry), then refl_shadow_kernel over the entries it deferred (sdefer)
+    int32_t shadow_feed;
+    unsigned int* shadow_ticket;
+    int32_t* sdefer;
+    unsigned int* sdefer_count;
 };
 
 // ---- hybrid rasterisation (kernels.hip "Renderer::raster_trace") ----

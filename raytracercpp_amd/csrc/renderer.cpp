@@ -134,6 +134,8 @@ Knobs Knobs::from_env()
         k.refl_defer = std::max(0, atoi(v));
     if (const char* v = getenv("RT_REFL_FEED"))    // lane refill of the reflection queries at this many waiting lanes
         k.refl_feed = std::min(64, std::max(0, atoi(v)));
+    if (const char* v = getenv("RT_REFL_SHADOW_FEED"))
+        k.refl_shadow_feed = std::min(64, std::max(0, atoi(v)));
     {
         const char* v = getenv("RT_INJECT_FRAME_FAIL");   // tests: the k-th ray_trace fails after its image start
         k.inject_fail = v ? std::atoi(v) : 0;
@@ -1143,7 +1145,7 @@ int Renderer::launch_trace(const KParams& P, hipStream_t stream)
     }
     for (auto& L : refl_)
         L.fr.device = L.ret.device = L.sm.device = L.hit.device = L.cnt.device = L.list.device = L.sort.device =
-            L.sort_tmp.device = L.res.device = device_;
+            L.sort_tmp.device = L.res.device = L.sdefer.device = device_;
     size_t npx = (size_t)P.rw * P.local_rows;
     ReflLevel& L1 = refl_[1];
     if ((e = L1.fr.reserve(npx * sizeof(FrameRec))) != hipSuccess || (e = L1.cnt.reserve(64)) != hipSuccess)
@@ -1177,12 +1179,13 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
     // A level may take at most a quarter of the memory still free (what it already holds
     // counts as free), so that the deeper levels, each bounded the same way, fit behind it;
     // an allocation that fails anyway halves the chunk and retries.
-    constexpr size_t SLOT_BYTES = sizeof(SampleRec) + sizeof(RawHit) + 4 + 16 + sizeof(FrameRec) + 12;
+    constexpr size_t SLOT_BYTES = sizeof(SampleRec) + sizeof(RawHit) + 4 + 4 + 16 + sizeof(FrameRec) + 12;
     size_t chunk = (size_t)std::max(1024, (1 << knobs_.refl_chunk_log2) / stride);
     {
         size_t freeb = 0, totalb = 0;
         if (hipMemGetInfo(&freeb, &totalb) == hipSuccess) {
-            const size_t held = L.sm.bytes + L.hit.bytes + L.list.bytes + L.res.bytes + C.fr.bytes + C.ret.bytes;
+            const size_t held =
+                L.sm.bytes + L.hit.bytes + L.list.bytes + L.sdefer.bytes + L.res.bytes + C.fr.bytes + C.ret.bytes;
             const size_t cap = (freeb + held) / 4 / (SLOT_BYTES * (size_t)stride);
             chunk = std::max<size_t>(1024, std::min(chunk, cap));
         }
@@ -1193,7 +1196,8 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
         const size_t slots = std::min((size_t)nframes, chunk) * stride;
         if ((e = L.sm.reserve(slots * sizeof(SampleRec))) == hipSuccess &&
             (e = L.hit.reserve(slots * sizeof(RawHit))) == hipSuccess && (e = L.list.reserve(slots * 4)) == hipSuccess &&
-            (e = L.res.reserve(slots * 16)) == hipSuccess && (e = C.fr.reserve(slots * sizeof(FrameRec))) == hipSuccess &&
+            (e = L.sdefer.reserve(slots * 4)) == hipSuccess && (e = L.res.reserve(slots * 16)) == hipSuccess &&
+            (e = C.fr.reserve(slots * sizeof(FrameRec))) == hipSuccess &&
             (e = C.ret.reserve(slots * 12)) == hipSuccess)
             break;
         if (e != hipErrorOutOfMemory || chunk <= 1024)
@@ -1247,7 +1251,12 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
         // lane refill (kernels.hip refl_trace_feed_kernel; RT_REFL_FEED=k: refill at k waiting lanes, 0: off)
         A.feed = knobs_.refl_feed;
         A.feed_ticket = L.cnt.as<unsigned int>() + 4;
-        if ((e = hipMemsetAsync(L.cnt.p, 0, 32, stream)) != hipSuccess)   // (+ the long kernel's and the feed's tickets)
+        // the shadow pass's lane refill (refl_shadow_feed_kernel; RT_REFL_SHADOW_FEED=k, 0: off)
+        A.shadow_feed = knobs_.refl_shadow_feed;
+        A.shadow_ticket = L.cnt.as<unsigned int>() + 5;
+        A.sdefer = L.sdefer.as<int32_t>();
+        A.sdefer_count = L.cnt.as<unsigned int>() + 6;
+        if ((e = hipMemsetAsync(L.cnt.p, 0, 32, stream)) != hipSuccess)   // (+ the long kernel's and the feeds' counters)
             return hip_fail(e, "hipMemsetAsync");
         // fused (default): trace, pass1 (+ shadow list), shadow (+ spawn); RT_REFL_FUSE=0: trace,
         // pass1, list, shadow, spawn
@@ -1336,7 +1345,7 @@ int Renderer::launch_raster(const KParams& P, hipStream_t stream)
     PS.tri_uv = A.piece_uv;
     for (auto& L : refl_)
         L.fr.device = L.ret.device = L.sm.device = L.hit.device = L.cnt.device = L.list.device = L.sort.device =
-            L.sort_tmp.device = L.res.device = device_;
+            L.sort_tmp.device = L.res.device = L.sdefer.device = device_;
     ReflLevel& L1 = refl_[1];
     const bool frames = P.has_reflection;
     if (frames) {

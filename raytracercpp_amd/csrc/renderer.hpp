@@ -74,11 +74,14 @@ struct Knobs {
                                            // in flight (the launch's tail overlaps them: fewer splits pay)
     float heavy_split = 0.5f; // RT_HEAVY_SPLIT=c: split the heavy tiles costing >= c x the launch's mean
                               // cycles per wave (heavy_prep_kernel)
-    int refl_defer = 32;      // RT_REFL_DEFER=k: reflection queries past k loop iterations finish in a pass
+    int refl_defer = 32;      // RT_REFL_DEFER=k (refl_feed = 0): reflection queries past k loop iterations
+                              // finish in a pass of their own
     int refl_feed = 24;       // RT_REFL_FEED=k: the reflection queries by refl_trace_feed_kernel (lane refill at k
                               // waiting lanes of a wave; C5 16 / 24 / 32 / 48: 1,128 / 1,101 / 1,103 / 1,155 ms per
-                              // frame, 1,195 without); 0: refl_trace_kernel with its deferral
-                              // of their own (9; 0: never)
+                              // frame, 1,195 without); 0: refl_trace_kernel with its deferral (RT_REFL_DEFER)
+    int refl_shadow_feed = 0; // RT_REFL_SHADOW_FEED=k: the engine's shadow pass by refl_shadow_feed_kernel (lane
+                              // refill at k waiting lanes; fused engine only; C5 16 / 24 / 32 / 48: 1,154 / 1,118 /
+                              // 1,094 / 1,078 ms per frame, 1,079 without); 0: refl_shadow_kernel per entry
     int inject_fail = 0;      // RT_INJECT_FRAME_FAIL=k (tests): the k-th ray_trace fails after its image start
     bool async_accel = true;  // RT_ASYNC_ACCEL=0: the leaf cones / slabs and the wide BVH are built
                               // before the first frame instead of beside it
@@ -336,7 +339,7 @@ private:
 
     // reflection engine buffers, per level (frames, results, chunk samples / hits, child counter)
     struct ReflLevel {
-        DevBuf fr, ret, sm, hit, cnt, list, sort, sort_tmp, res;
+        DevBuf fr, ret, sm, hit, cnt, list, sort, sort_tmp, res, sdefer;
     };
     static constexpr int REFL_LEVELS = 18;   // max_recursion_depth <= 15: frames at levels 1..16, +1 child slot
     ReflLevel refl_[REFL_LEVELS];

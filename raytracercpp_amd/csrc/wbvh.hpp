@@ -817,7 +817,7 @@ struct WNoFeed {
     bool drained = true;   // (wave-uniform) the feed has no query left to hand out
     int threshold = 64;
     template <class H> RT_HD void finish(int, H&, v3, v3) {}
-    RT_HD bool fetch(bool, v3&, v3&, float&) { return false; }
+    RT_HD bool fetch(bool, v3&, v3&, float&, float&, const uint64_t*&, float&) { return false; }
 };
 
 template <class Stack, int G = 1, class Feed = WNoFeed>
@@ -831,8 +831,9 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
     static_assert(G == 1 || !W_STEP_CAP, "a lane group leaves the loop together");
     // Feed::on (device, one lane per query): lane refill.  The wave stays in the loop; a lane whose query
     // ended waits, and when at least feed->threshold lanes (or every lane) wait, each hands its query's
-    // status and record to feed->finish and takes the next ray from feed->fetch (o, d, m; hi, ties, QS
-    // and the risk words are the same for every query of the feed).  The per-query work is the one-query
+    // status and record to feed->finish and takes the next ray from feed->fetch (o, d, m, hi and the risk
+    // words and rsub, which it may leave as they are; ties, QS and rsel are the same for every query of the
+    // feed).  The per-query work is the one-query
     // call's: the same state, reset per query, the same steps.  Returns W_MISS once the feed is drained.
     constexpr bool FEED = Feed::on;
     static_assert(!FEED || (G == 1 && !W_STEP_CAP), "lane refill: one lane per query");
@@ -897,6 +898,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
         return ovf ? W_DEEP : W_HIT;
     };
     // FEED: at the loop's head, with the wave together; false once the feed is drained and no lane runs
+    (void)status;
     auto refill = [&]() -> bool {
         if constexpr (FEED) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -905,7 +907,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
             if (idle != 0ull && (idle == __ballot(1) || __popcll(idle) >= feed->threshold)) {
                 if (idle_lane && feed->busy)
                     feed->finish(status(), h, o, d);
-                if (feed->fetch(idle_lane, o, d, m)) {   // (wave-uniform call; true for the lanes given a ray)
+                if (feed->fetch(idle_lane, o, d, m, hi, risk, rsub)) {   // (wave-uniform call; true for the lanes given a ray)
                     setup();
                     h.t = INFINITY;
                     h.u = 1.0f;

@@ -199,19 +199,21 @@ def test_hair1m_frame_matches_oracle(make_renderer, camera):
           f"{o.counters['shadow_rays']} shadow rays")
 
 
-@pytest.mark.parametrize("defer,feed", [("48", "0"), ("0", "0"), ("6", "0"), ("32", "16"), ("32", "1"), ("32", "64")])
-def test_reflection_deferral_matches_oracle(make_renderer, defer, feed):
+@pytest.mark.parametrize("defer,feed,sfeed", [("48", "0", "0"), ("0", "0", "0"), ("6", "0", "24"), ("32", "16", "1"),
+                                               ("32", "1", "64"), ("32", "64", "16"), ("32", "24", "0")])
+def test_reflection_deferral_matches_oracle(make_renderer, defer, feed, sfeed):
     """The reflection engine's long-query deferral (RT_REFL_DEFER=k: queries past k loop iterations of
     refl_trace_kernel finish in refl_trace_long_kernel; 0: never deferred) and its lane refill
     (RT_REFL_FEED=k: refl_trace_feed_kernel's persistent waves take new queries when k lanes wait, the
-    uncertified ones deferred) change only where a query runs: C5's features at a reduced size, first on
+    uncertified ones deferred; RT_REFL_SHADOW_FEED=k: the same for the shadow pass,
+    refl_shadow_feed_kernel) change only where a query runs: C5's features at a reduced size, first on
     the quick wide BVH (the frame right after the scene load), then on the SAH tree, equal
     the oracle bit for bit."""
     from raytracercpp_amd import scenes
     sc, st = scenes.sphere1m_refl(width=64, height=36, samples=4)
     st = st.copy(max_recursion_depth=3)
     o = Oracle(sc, st).render_rows()
-    R = make_renderer(RT_REFL_DEFER=defer, RT_REFL_FEED=feed)
+    R = make_renderer(RT_REFL_DEFER=defer, RT_REFL_FEED=feed, RT_REFL_SHADOW_FEED=sfeed)
     R.load_scene(sc, st)
     R.request_aux(hit=True, shadow=True)
     for frame in ("quick tree", "SAH tree"):

@@ -29,6 +29,7 @@
 #   trace_c5 / pmc_c5 / trace_hair / pmc_hair   the same for C5 / hair1m
 #   count_c4 / count_c5 / count_hair   RT_COUNT=1 work counts (needs _variants/librt_count.so)
 #   py:<file>      python <file> (a probe under tools/)
+#   pt:<expr>      pytest -m gpu -k <expr> (a subset of the GPU suite)
 set -u
 OUT=gpurun_out/${1:?outdir}
 shift
@@ -86,6 +87,7 @@ run_step() {
     count_c5) RT_LIB_PATH=_variants/librt_count.so python tools/count_gpu_work.py sphere1m_refl seg ;;
     count_hair) RT_LIB_PATH=_variants/librt_count.so python tools/count_gpu_work.py hair1m seg ;;
     py:*) python ${step#py:} ;;
+    pt:*) python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -k "${step#pt:}" ;;
     *) echo "unknown step $step"; return 2 ;;
     esac
 }
