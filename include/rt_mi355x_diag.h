@@ -74,11 +74,31 @@ int rt_wbvh_query(const float *tri9, int64_t n, int32_t max_depth, int32_t leaf_
  * ray o = p + 1e-4 n, d = normalize(light - p) (renderer.cpp:340-402), reading the light's bits when
  * its segment bound allows, and is answered as a closest-hit query over the whole line.  o_out /
  * d_out (optional, 3 floats per ray) receive the rays queried, ray_nodes (optional) each query's
- * wide-node visits (the retry's included). */
+ * wide-node visits (the retry's included).  ocone_dim > 0: the origin cones at that
+ * resolution for the rays that read no risk words (the reflection queries' skip of case (b));
+ * oc_stats[5] (optional) = {cells computed, cells with no triangle at risk, cells without a bound,
+ * rays that skipped case (b), grid build ms}. */
 int rt_wbvh_query_ex(const float *tri9, int64_t n, int32_t max_depth, int32_t leaf_max_obj_count, const float *orig,
                      const float *dir, int64_t nrays, const float *cam, const float *light, int32_t shadow_rays,
                      float *o_out, float *d_out, int32_t *status, int32_t *id, float *t, float *u, float *v,
-                     int64_t stats[8], float *ms, int32_t *ray_nodes);
+                     int64_t stats[8], float *ms, int32_t *ray_nodes, int32_t ocone_dim, int64_t oc_stats[5]);
+
+/* The origin cones' soundness by brute force (CPU tests): builds the octree, the wide
+ * BVH and the origin-cone grid (ocone_dim cells along the longest axis) over tri9; for each ray whose
+ * origin cone lets it skip case (b) (skip[i] = 1, optional), runs Moller-Trumbore (triangle.cpp:25-91)
+ * on every triangle nearly parallel to it (|cos(N, d)| < the query's split, or degenerate): a reported
+ * hit is a violation.  out[6] = {violations, rays skipping, grazing triangle tests, cells computed,
+ * cells with no triangle at risk, cells without a bound}. */
+int rt_ocone_check(const float *tri9, int64_t n, int32_t max_depth, int32_t leaf_max_obj_count, int32_t ocone_dim,
+                   const float *orig, const float *dir, int64_t nrays, int32_t *skip, int64_t out[6],
+                   const uint32_t *cells, const int32_t *dims, const float *lo_ih, uint32_t *cells_out);
+/* cells / dims / lo_ih (optional, all or none): check that grid instead of building one (a renderer's,
+ * rt_ocone_read; out[3] then counts its cells); cells_out (optional): the built grid's words, 2 per cell
+ * (its frame: ocone_dim along the longest axis, as the renderer builds it).
+ * The renderer's resident origin-cone grid (built on the device at the last geometry change when a
+ * material reflects): dims[3], lo_ih[4] = {lo x, y, z, 1 / cell size}; out (optional) receives its
+ * words, 2 per cell (n >= 2 dims[0] dims[1] dims[2]). */
+int rt_ocone_read(rt_renderer *r, uint32_t *out, int64_t n, int32_t dims[3], float lo_ih[4]);
 
 #ifdef __cplusplus
 }

@@ -143,7 +143,11 @@ SIGNATURES = {
     "rt_wbvh_query": (C.c_int, [_f32p, C.c_int64, C.c_int32, C.c_int32, _f32p, _f32p, C.c_int64, _i32p, _i32p, _f32p,
                                 _f32p, _f32p, _i64p, _f32p]),
     "rt_wbvh_query_ex": (C.c_int, [_f32p, C.c_int64, C.c_int32, C.c_int32, _f32p, _f32p, C.c_int64, _f32p, _f32p,
-                                   C.c_int32, _f32p, _f32p, _i32p, _i32p, _f32p, _f32p, _f32p, _i64p, _f32p, _i32p]),
+                                   C.c_int32, _f32p, _f32p, _i32p, _i32p, _f32p, _f32p, _f32p, _i64p, _f32p, _i32p,
+                                   C.c_int32, _i64p]),
+    "rt_ocone_check": (C.c_int, [_f32p, C.c_int64, C.c_int32, C.c_int32, C.c_int32, _f32p, _f32p, C.c_int64, _i32p,
+                                 _i64p, C.POINTER(C.c_uint32), _i32p, _f32p, C.POINTER(C.c_uint32)]),
+    "rt_ocone_read": (C.c_int, [_H, C.POINTER(C.c_uint32), C.c_int64, _i32p, _f32p]),
 }
 
 _lib = None
@@ -261,7 +265,7 @@ def load_obj(path, xform, mat_offset=0):
 
 
 def wbvh_query(tri9, orig, dirs, max_depth=12, leaf=40, cam=None, light=None, shadow_rays=False, rays_out=False,
-               ray_nodes=None):
+               ray_nodes=None, ocone_dim=0, oc_stats=None):
     """rt_wbvh_query(_ex): the wide-BVH certified closest hit on the host (no GPU).  Returns
     (status, id, t, u, v, stats dict, (octree ms, wide-BVH ms)); status 0 certified miss,
     1 certified hit, 2 not certified.  cam / light: the frame's grazing-risk points (rays from cam
@@ -285,10 +289,40 @@ def wbvh_query(tri9, orig, dirs, max_depth=12, leaf=40, cam=None, light=None, sh
                                  1 if shadow_rays else 0, ptr(oo, _f32p), ptr(do, _f32p),
                                  ptr(st, _i32p), ptr(ids, _i32p), ptr(t, _f32p), ptr(u, _f32p), ptr(v, _f32p),
                                  ptr(stats, _i64p), ptr(ms, _f32p),
-                                 None if ray_nodes is None else ptr(ray_nodes, _i32p)), "rt_wbvh_query")
+                                 None if ray_nodes is None else ptr(ray_nodes, _i32p), int(ocone_dim),
+                                 None if oc_stats is None else ptr(oc_stats, _i64p)), "rt_wbvh_query")
     keys = ("nodes", "leaves", "max_leaf", "depth", "node_visits", "tri_tests", "violations", "sah_x1000")
     out = (st, ids, t, u, v, dict(zip(keys, map(int, stats))), (float(ms[0]), float(ms[1])))
     return out + (oo, do) if rays_out else out
+
+
+def ocone_check(tri9, orig, dirs, max_depth=12, leaf=40, ocone_dim=64, grid=None, want_cells=False):
+    """rt_ocone_check: (skip flags, dict[, cells]) -- the origin cones' brute-force soundness check (no
+    GPU).  grid: (cells uint32 [n, 2], dims, lo_ih) to check instead of building one (Renderer.ocone_read);
+    want_cells: also return the built grid's words."""
+    tri9 = f32(tri9).reshape(-1, 9)
+    o = f32(orig).reshape(-1, 3)
+    d = f32(dirs).reshape(-1, 3)
+    skip = np.zeros(o.shape[0], np.int32)
+    out = np.zeros(6, np.int64)
+    _u32p = C.POINTER(C.c_uint32)
+    cells = dims = lo_ih = None
+    if grid is not None:
+        cells = np.ascontiguousarray(grid[0], np.uint32)
+        dims = np.ascontiguousarray(grid[1], np.int32)
+        lo_ih = f32(grid[2])
+    built = None
+    if want_cells:
+        # the grid's size: the renderer's frame (ocone_dim + 2 cells at most per axis)
+        built = np.zeros(((ocone_dim + 2) ** 3, 2), np.uint32)
+    check(lib().rt_ocone_check(ptr(tri9, _f32p), tri9.shape[0], max_depth, leaf, ocone_dim, ptr(o, _f32p),
+                               ptr(d, _f32p), o.shape[0], ptr(skip, _i32p), ptr(out, _i64p),
+                               None if cells is None else ptr(cells, _u32p), None if dims is None else ptr(dims, _i32p),
+                               None if lo_ih is None else ptr(lo_ih, _f32p), None if built is None else ptr(built, _u32p)),
+          "rt_ocone_check")
+    keys = ("violations", "skipping", "grazing_tests", "cells", "empty_cells", "noskip_cells")
+    res = (skip, dict(zip(keys, map(int, out))))
+    return res + (built,) if want_cells else res
 
 
 def octree_digest(tri9, max_depth=12, leaf=40, builder=0):

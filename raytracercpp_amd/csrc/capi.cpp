@@ -10,6 +10,7 @@
 #include "../../include/rt_mi355x_diag.h"   // (includes rt_mi355x.h)
 #include "host_scene.hpp"
 #include "octree.hpp"
+#include "ocone.hpp"
 #include "wbvh.hpp"
 #include "renderer.hpp"
 
@@ -293,6 +294,10 @@ int rt_tile_costs(rt_renderer* r, uint32_t* out, int64_t n, int32_t* tiles_x, in
 {
     return guarded(R(r), [&] { return tiles_x && tiles_y ? R(r)->tile_costs(out, n, tiles_x, tiles_y) : RT_EINVAL; });
 }
+int rt_ocone_read(rt_renderer* r, uint32_t* out, int64_t n, int32_t dims[3], float lo_ih[4])
+{
+    return guarded(R(r), [&] { return dims && lo_ih ? R(r)->origin_cones(out, n, dims, lo_ih) : RT_EINVAL; });
+}
 int rt_local_rows(rt_renderer* r, int32_t band_rows, int32_t rank, int32_t nranks, int32_t* rows_out)
 {
     return guarded(R(r), [&] {
@@ -444,6 +449,117 @@ int rt_obj_fetch(const rt_obj* o, float* tri9, int32_t* mat, float* uv6, float* 
 
 void rt_obj_close(rt_obj* o) { delete o; }
 
+// The origin cones' soundness by brute force (CPU tests): for each ray (o, d) that ocone_skip lets
+// skip case (b), every triangle with q = |cos(N, d)| < W_QS_CLOSEST (N = ab x ac exact) is run through
+// Moller-Trumbore (mt_record, the reference's expressions): a reported hit is a violation.
+int rt_ocone_check(const float* tri9, int64_t n, int32_t max_depth, int32_t leaf_max_obj_count, int32_t ocone_dim,
+                   const float* orig, const float* dir, int64_t nrays, int32_t* skip, int64_t out[6],
+                   const uint32_t* cells, const int32_t* dims, const float* lo_ih, uint32_t* cells_out)
+{
+    if (n <= 0 || !tri9 || nrays < 0 || (nrays > 0 && (!orig || !dir)) || ocone_dim <= 0 || !out)
+        return bad("rt_ocone_check: bad arguments");
+    try {
+        rt::FlatOctree f;
+        rt::WBvh w;
+        rt::build_flat_octree(tri9, n, max_depth, leaf_max_obj_count, f);
+        rt::build_wbvh(f, w);
+        float S = 0.0f;
+        if (!f.nodes.empty())
+            for (int a = 0; a < 3; a++)
+                S = std::max(S, std::max(std::fabs(f.nodes[0].dn[a]), std::fabs(f.nodes[0].df[a])));
+        rt::OConeGrid g;
+        if (cells && dims && lo_ih) {   // a given grid (a renderer's, rt_ocone_read)
+            for (int a = 0; a < 3; a++) {
+                g.dim[a] = dims[a];
+                g.lo[a] = lo_ih[a];
+            }
+            g.ih = lo_ih[3];
+            const size_t nc = (size_t)dims[0] * dims[1] * dims[2];
+            g.cells.resize(nc);
+            std::memcpy(g.cells.data(), cells, nc * sizeof(uint2));
+            g.computed = (int64_t)nc;
+            rt::origin_cones_count(g);
+        } else {
+            rt::build_origin_cones(w, S, W_QS_CLOSEST, 0.0102 + 0x1p-16 * S, ocone_dim, 80.0 * 3.14159265358979 / 180.0, 0, g);
+            if (cells_out && !g.cells.empty())
+                std::memcpy(cells_out, g.cells.data(), g.cells.size() * sizeof(uint2));
+        }
+        rt::OConeView v{};
+        if (!g.cells.empty()) {
+            v.cells = g.cells.data();
+            for (int a = 0; a < 3; a++) {
+                v.lo[a] = g.lo[a];
+                v.dim[a] = g.dim[a];
+            }
+            v.ih = g.ih;
+        }
+        // per triangle: q's numerator scale |N| (exact normal of the float edges)
+        std::vector<double> Nn(w.tris.size() * 4);
+        for (size_t k = 0; k < w.tris.size(); k++) {
+            const rt::GTri& t = w.tris[k];
+            const double x0 = t.ab[0], x1 = t.ab[1], x2 = t.ab[2], y0 = t.ac[0], y1 = t.ac[1], y2 = t.ac[2];
+            Nn[4 * k] = x1 * y2 - x2 * y1;
+            Nn[4 * k + 1] = x2 * y0 - x0 * y2;
+            Nn[4 * k + 2] = x0 * y1 - x1 * y0;
+            Nn[4 * k + 3] = std::sqrt(Nn[4 * k] * Nn[4 * k] + Nn[4 * k + 1] * Nn[4 * k + 1] + Nn[4 * k + 2] * Nn[4 * k + 2]);
+        }
+        std::atomic<int64_t> nskip{0}, nviol{0}, ngraze{0};
+        auto body = [&](int64_t b, int64_t e) {
+            for (int64_t i = b; i < e; i++) {
+                const rt::v3 o = rt::mk(orig[3 * i], orig[3 * i + 1], orig[3 * i + 2]);
+                const rt::v3 d = rt::mk(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]);
+                const bool sk = rt::ocone_skip(v, o, d);
+                if (skip)
+                    skip[i] = sk ? 1 : 0;
+                if (!sk)
+                    continue;
+                ++nskip;
+                const double dl = std::sqrt((double)d.x * d.x + (double)d.y * d.y + (double)d.z * d.z);
+                for (size_t k = 0; k < w.tris.size(); k++) {
+                    const double* N = &Nn[4 * k];
+                    const double q = std::fabs(N[0] * d.x + N[1] * d.y + N[2] * d.z) / (N[3] * dl);
+                    if (!(q < W_QS_CLOSEST))
+                        continue;   // (a)'s, or degenerate / NaN: tested below too
+                    ++ngraze;
+                    float tt, uu, vv;
+                    if (rt::mt_record(w.tris[k], o, d, tt, uu, vv))
+                        ++nviol;
+                }
+                // degenerate records (q undefined) are case (b)'s as well
+                for (size_t k = 0; k < w.tris.size(); k++) {
+                    const double* N = &Nn[4 * k];
+                    const double q = std::fabs(N[0] * d.x + N[1] * d.y + N[2] * d.z) / (N[3] * dl);
+                    if (q == q)
+                        continue;
+                    float tt, uu, vv;
+                    if (rt::mt_record(w.tris[k], o, d, tt, uu, vv))
+                        ++nviol;
+                }
+            }
+        };
+        unsigned hc = std::max(1u, std::min(std::thread::hardware_concurrency(), 16u));
+        std::vector<std::thread> th;
+        int64_t chunk = (nrays + hc - 1) / hc;
+        for (unsigned k = 0; k < hc; k++) {
+            int64_t b = (int64_t)k * chunk, e = std::min(nrays, b + chunk);
+            if (b < e)
+                th.emplace_back(body, b, e);
+        }
+        for (auto& x : th)
+            x.join();
+        out[0] = nviol.load();
+        out[1] = nskip.load();
+        out[2] = ngraze.load();
+        out[3] = g.computed;
+        out[4] = g.empty;
+        out[5] = g.noskip;
+        return RT_OK;
+    } catch (const std::bad_alloc&) {
+        g_err = "rt_ocone_check: out of host memory";
+        return RT_ENOMEM;
+    }
+}
+
 int rt_octree_digest(const float* tri9, int64_t n, int32_t max_depth, int32_t leaf_max_obj_count, int32_t builder,
                      uint64_t* digest, int64_t stats[7], float* ms)
 {
@@ -501,13 +617,13 @@ int rt_wbvh_query(const float* tri9, int64_t n, int32_t max_depth, int32_t leaf_
                   int64_t stats[8], float* ms)
 {
     return rt_wbvh_query_ex(tri9, n, max_depth, leaf_max_obj_count, orig, dir, nrays, nullptr, nullptr, 0, nullptr,
-                            nullptr, status, id, t, u, v, stats, ms, nullptr);
+                            nullptr, status, id, t, u, v, stats, ms, nullptr, 0, nullptr);
 }
 
 int rt_wbvh_query_ex(const float* tri9, int64_t n, int32_t max_depth, int32_t leaf_max_obj_count, const float* orig,
                      const float* dir, int64_t nrays, const float* cam, const float* light, int32_t shadow_rays,
                      float* o_out, float* d_out, int32_t* status, int32_t* id, float* t, float* u, float* v,
-                     int64_t stats[8], float* ms, int32_t* ray_nodes)
+                     int64_t stats[8], float* ms, int32_t* ray_nodes, int32_t ocone_dim, int64_t oc_stats[5])
 {
     if (n < 0 || (n > 0 && !tri9) || nrays < 0 || (nrays > 0 && (!orig || !dir || !status || !id || !t || !u || !v)) ||
         (shadow_rays && !light))
@@ -550,7 +666,22 @@ int rt_wbvh_query_ex(const float* tri9, int64_t n, int32_t max_depth, int32_t le
             if (light)
                 rt::wbvh_risk_host(w, lbox, RA, 1, risk);
         }
-        std::atomic<int64_t> work_n{0}, work_t{0};
+        // the origin cones (ocone.hpp) for the rays neither from the camera nor shadow rays (renderer.cpp
+        // start_accel's build)
+        rt::OConeGrid ocg;
+        rt::OConeView ocv{};
+        if (usable && ocone_dim > 0) {
+            rt::build_origin_cones(w, S, W_QS_CLOSEST, 0.0102 + 0x1p-16 * S, ocone_dim, 80.0 * 3.14159265358979 / 180.0, 0, ocg);
+            if (!ocg.cells.empty()) {
+                ocv.cells = ocg.cells.data();
+                for (int a = 0; a < 3; a++) {
+                    ocv.lo[a] = ocg.lo[a];
+                    ocv.dim[a] = ocg.dim[a];
+                }
+                ocv.ih = ocg.ih;
+            }
+        }
+        std::atomic<int64_t> work_n{0}, work_t{0}, n_nob{0};
         const bool probe_hi = std::getenv("RT_WQ_PROBE_HI") != nullptr;
         auto body = [&](int64_t b, int64_t e) {
             rt::WStackLocal stk;
@@ -607,8 +738,12 @@ int rt_wbvh_query_ex(const float* tri9, int64_t n, int32_t max_depth, int32_t le
                 float m = 0x1p-16f * (om + S);
                 rt::WHit h;
                 const uint32_t wk0 = wk[0];
+                const bool nob = !shadow_rays && !rk && rt::ocone_skip(ocv, o, d);
+                if (nob)
+                    ++n_nob;
                 int st = rt::wbvh_closest(w.nodes.data(), w.tris.data(), o, d, m, stk, h, wk, INFINITY, true,
-                                          shadow_rays ? W_QS_SHADOW : W_QS_CLOSEST, rk, rsel, rsub);
+                                          shadow_rays ? W_QS_SHADOW : W_QS_CLOSEST, rk, rsel, rsub, 0u,
+                                          (rt::WNoFeed*)nullptr, nob);
                 if (st == rt::W_DEEP) {   // the kernels' retry with a deeper stack (kernels.hip wide_closest_deep)
                     rt::WStackArr<rt::W_DEEP_STACK> deep;
                     st = rt::wbvh_closest(w.nodes.data(), w.tris.data(), o, d, m, deep, h, wk, INFINITY, true,
@@ -668,6 +803,13 @@ int rt_wbvh_query_ex(const float* tri9, int64_t n, int32_t max_depth, int32_t le
                     stats[6] += rt::check_risk_words(f, w, RA, 1, risk.data());
             }
             stats[7] = (int64_t)(w.stats.sah * 1000.0f);
+        }
+        if (oc_stats) {
+            oc_stats[0] = ocg.computed;
+            oc_stats[1] = ocg.empty;
+            oc_stats[2] = ocg.noskip;
+            oc_stats[3] = n_nob.load();
+            oc_stats[4] = (int64_t)ocg.ms;
         }
         return RT_OK;
     } catch (const std::bad_alloc&) {

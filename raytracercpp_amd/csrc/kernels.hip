@@ -2449,8 +2449,8 @@ struct ReflFeed {
     }
 
     // wave-uniform: the waiting lanes (want) take the next slots; true for a lane given a ray (hi, risk and
-    // rsub stay the call's: INFINITY, none, 0)
-    __device__ __forceinline__ bool fetch(bool want, v3& o, v3& d, float& m, float&, const uint64_t*&, float&)
+    // rsub stay the call's: INFINITY, none, 0; nob: the origin cones, ocone.hpp)
+    __device__ __forceinline__ bool fetch(bool want, v3& o, v3& d, float& m, float&, const uint64_t*&, float&, bool& nob)
     {
         const uint64_t wb = __ballot(want);
         if (!wb)
@@ -2490,6 +2490,7 @@ struct ReflFeed {
         }
         const float om = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
         m = 0x1p-16f * (om + P->scene_scale);
+        nob = ocone_skip(P->ocone, o, d);
         busy = true;
         return true;
     }
@@ -2510,10 +2511,21 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_feed_kernel(KPa
     // lane): fewer overflow into the defer list
     WStackLdsN<W_STACK_REFL_FEED> stk{lv};
     WHit w;
+#if RT_COUNT
+    uint32_t wk[4] = {0, 0, 0, 0};   // (the lane's queries' node visits and triangle tests)
+#else
+    uint32_t* wk = nullptr;
+#endif
     wbvh_closest<WStackLdsN<W_STACK_REFL_FEED>, 1, ReflFeed>(P.wnodes, P.wtris, mk(0, 0, 0), mk(1, 0, 0), 0.0f, stk, w,
-                                                             nullptr, INFINITY, true, W_QS_CLOSEST, nullptr, 0, 0.0f, 0u,
+                                                             wk, INFINITY, true, W_QS_CLOSEST, nullptr, 0, 0.0f, 0u,
                                                              &feed);
     wave_count_add(&P.counters[1], feed.count);
+#if RT_COUNT
+    if (P.counters) {
+        atomicAdd(&P.counters[10], (unsigned long long)wk[0]);
+        atomicAdd(&P.counters[11], (unsigned long long)wk[1]);
+    }
+#endif
 }
 
 #ifndef RT_REFL_LONG_QUEUE
@@ -2796,7 +2808,8 @@ struct ShadowFeed {
         refl_shadow_done(*P, *A, slot, sh);
     }
 
-    __device__ __forceinline__ bool fetch(bool want, v3& o, v3& d, float& m, float& hi, const uint64_t*& risk, float& rsub)
+    __device__ __forceinline__ bool fetch(bool want, v3& o, v3& d, float& m, float& hi, const uint64_t*& risk, float& rsub,
+                                          bool&)
     {
         const uint64_t wb = __ballot(want);
         if (!wb)
@@ -4064,6 +4077,60 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_wide_gathe
         return hipSuccess;
     hipLaunchKernelGGL(rt::wide_gather_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, tris, slot, leaf_of_slot,
                        tri_id, tri_mat, n, wtris, wmeta);
+    return hipGetLastError();
+}
+
+// ---- origin cones (ocone.hpp): each listed cell's word, one lane per cell; the rest OC_NOSKIP ----
+namespace rt {
+__global__ void ocone_fill_kernel(uint2* cells, size_t n)
+{
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n)
+        cells[i] = make_uint2(0u, OC_NOSKIP << 16);
+}
+
+struct OConeArgs {
+    float lo[3];
+    int32_t dim[3];
+    double h, r, slack, QS, cos_cap;
+};
+
+__global__ __launch_bounds__(256) void ocone_kernel(const OConeEnt* E, const GTri* tris, const uint32_t* todo, int n,
+                                                    OConeArgs A, uint2* cells)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t id = todo[i];
+    double c[3];
+    ocone_center(A.lo, A.dim, A.h, id, c);
+    cells[id] = ocone_cell<OC_STACK>(E, tris, c, A.r, A.slack, A.QS, A.cos_cap);
+}
+}  // namespace rt
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ocone(const rt::OConeEnt* E, const rt::GTri* tris,
+                                                                     const uint32_t* todo, int n, const float lo[3],
+                                                                     const int32_t dim[3], double h, double r, double slack,
+                                                                     double QS, double cos_cap, uint2* cells,
+                                                                     size_t ncells, hipStream_t stream)
+{
+    if (ncells == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(rt::ocone_fill_kernel, dim3((unsigned)((ncells + 255) / 256)), dim3(256), 0, stream, cells, ncells);
+    if (n > 0) {
+        rt::OConeArgs A;
+        for (int a = 0; a < 3; a++) {
+            A.lo[a] = lo[a];
+            A.dim[a] = dim[a];
+        }
+        A.h = h;
+        A.r = r;
+        A.slack = slack;
+        A.QS = QS;
+        A.cos_cap = cos_cap;
+        hipLaunchKernelGGL(rt::ocone_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, E, tris, todo, n, A,
+                           cells);
+    }
     return hipGetLastError();
 }
 

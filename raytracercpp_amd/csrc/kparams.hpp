@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "octree.hpp"
+#include "ocone.hpp"
 #include "wbvh.hpp"
 
 namespace rt {
@@ -60,6 +61,9 @@ struct KParams {
     // light's nu (WRiskArgs::ray_nu)
     const uint64_t* wrisk;
     float risk_G, risk_nl, risk_nu;
+    // the origin cones (ocone.hpp; cells nullptr: none resident): the rays without risk words whose
+    // ocone_skip holds skip case (b) (the reflection queries, ReflFeed)
+    OConeView ocone;
     int32_t nnodes;
     int32_t ntri_slots;       // GTri count (brute-force loop bound when enable_bvh == 0)
     int32_t levels;           // flattened tree depth + 1 (LDS level-stack entries per lane)

@@ -54,6 +54,11 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_raster_sha
                                                                             rt::FrameRec* fr1, unsigned int* nfr1,
                                                                             hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ssao(const rt::SsaoArgs* A, hipStream_t stream);
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ocone(const rt::OConeEnt* E, const rt::GTri* tris,
+                                                                     const uint32_t* todo, int n, const float lo[3],
+                                                                     const int32_t dim[3], double h, double r, double slack,
+                                                                     double QS, double cos_cap, uint2* cells,
+                                                                     size_t ncells, hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_wide_gather(
     const rt::GTri* tris, const int32_t* slot, const uint32_t* leaf_of_slot, const int32_t* tri_id,
     const int32_t* tri_mat, int n, rt::GTri* wtris, uint4* wmeta, hipStream_t stream);
@@ -134,6 +139,10 @@ Knobs Knobs::from_env()
         k.refl_defer = std::max(0, atoi(v));
     if (const char* v = getenv("RT_REFL_FEED"))    // lane refill of the reflection queries at this many waiting lanes
         k.refl_feed = std::min(64, std::max(0, atoi(v)));
+    if (const char* v = getenv("RT_OCONE"))
+        k.ocone = atoi(v) != 0;
+    if (const char* v = getenv("RT_OCONE_DIM"))
+        k.ocone_dim = std::min(1024, std::max(1, atoi(v)));
     if (const char* v = getenv("RT_REFL_SHADOW_FEED"))
         k.refl_shadow_feed = std::min(64, std::max(0, atoi(v)));
     {
@@ -188,7 +197,8 @@ int Renderer::init(std::string& err)
                      &d_image_, &d_rgba_,  &d_hit_id_, &d_hit_t_,   &d_shadow_, &d_counters_,
                      &d_tri9_,  &d_rcount_, &d_roff_,  &d_pieces_,  &d_piece_uv_, &d_zkey_, &d_big_, &d_scan_tmp_,
                      &d_zbuf_,  &d_nbuf_,   &d_ao_,     &d_cones_, &d_lslab_, &d_lsin_, &d_wnodes_, &d_wtris_, &d_wmeta_, &d_wtmp_,
-                     &d_wlinks_, &d_wrisk_, &d_dbg_, &d_wnodes2_, &d_wtris2_, &d_wmeta2_, &d_wtmp2_, &d_wlinks2_};
+                     &d_wlinks_, &d_wrisk_, &d_dbg_, &d_wnodes2_, &d_wtris2_, &d_wmeta2_, &d_wtmp2_, &d_wlinks2_,
+                     &d_ocone_, &d_ocone2_, &d_oc_ent_, &d_oc_todo_};
     for (DevBuf* b : all) b->device = device_;
     for (auto& b : d_tex_) b.device = device_;
     for (auto& b : d_sky_) b.device = device_;
@@ -665,7 +675,17 @@ void Renderer::start_accel()
 {
     accel_state_.store(1);
     accel_err_.clear();
-    accel_thread_ = std::thread([this] {
+    // the origin cones serve the reflection queries: built when a material reflects (read here, on the
+    // caller's thread; a material made reflective later finds none, and its queries run case (b))
+    bool reflective = false;
+    for (size_t i = 12; i < mats_.size(); i += MAT_STRIDE)
+        reflective |= mats_[i] > 0.0f;
+    const bool want_oc = reflective && knobs_.ocone && knobs_.wbvh && !knobs_.exact;
+    float S = 0.0f;
+    if (oct_nn_ > 0)
+        for (int c = 0; c < 3; c++)
+            S = std::max(S, std::max(std::fabs(oct_root_.dn[c]), std::fabs(oct_root_.df[c])));
+    accel_thread_ = std::thread([this, want_oc, S] {
         using clk = std::chrono::steady_clock;
         auto ms_since = [](clk::time_point t) { return std::chrono::duration<float, std::milli>(clk::now() - t).count(); };
         hipError_t e = hipSetDevice(device_);
@@ -685,11 +705,38 @@ void Renderer::start_accel()
             build_wbvh(oct_, wb_next_);
         else
             wb_next_ = WBvh();
+        // origin cones: reflection origins lie 0.01 |n| off their hit points (make_frame), so the cells
+        // within 0.0102 of a triangle; the host plans, the device searches (ocone_kernel, after the wide
+        // BVH's records are gathered on the same stream)
+        ocg_next_ = OConeGrid();
+        OConeJob job;
+        if (want_oc && !wb_next_.nodes.empty())
+            origin_cones_plan(wb_next_, S, W_QS_CLOSEST, 0.0102 + 0x1p-16 * S, knobs_.ocone_dim,
+                              80.0 * 3.14159265358979 / 180.0, ocg_next_, job);
         accel_ms_[1] = ms_since(t1);
         auto t2 = clk::now();
         hipSetDevice(device_);
         if (e == hipSuccess && !wb_next_.nodes.empty())
             e = upload_wide(wb_next_, d_wnodes2_, d_wtris2_, d_wmeta2_, d_wtmp2_, d_wlinks2_, accel_stream_);
+        if (e == hipSuccess && !job.todo.empty()) {
+            // (a failure here only leaves the reflection queries without the cones)
+            const size_t ncell = (size_t)ocg_next_.dim[0] * ocg_next_.dim[1] * ocg_next_.dim[2];
+            hipError_t eo;
+            if ((eo = d_ocone2_.reserve(ncell * sizeof(uint2))) == hipSuccess &&
+                (eo = d_oc_ent_.reserve(job.ent.size() * sizeof(OConeEnt))) == hipSuccess &&
+                (eo = d_oc_todo_.reserve(job.todo.size() * 4)) == hipSuccess &&
+                (eo = hipMemcpyAsync(d_oc_ent_.p, job.ent.data(), job.ent.size() * sizeof(OConeEnt), hipMemcpyHostToDevice,
+                                     accel_stream_)) == hipSuccess &&
+                (eo = hipMemcpyAsync(d_oc_todo_.p, job.todo.data(), job.todo.size() * 4, hipMemcpyHostToDevice,
+                                     accel_stream_)) == hipSuccess)
+                eo = rt_launch_ocone(d_oc_ent_.as<OConeEnt>(), d_wtris2_.as<GTri>(), d_oc_todo_.as<uint32_t>(),
+                                     (int)job.todo.size(), ocg_next_.lo, ocg_next_.dim, job.h, job.r, job.slack, job.QS,
+                                     job.cos_cap, d_ocone2_.as<uint2>(), ncell, accel_stream_);
+            if (eo != hipSuccess) {
+                ocg_next_ = OConeGrid();
+                (void)hipGetLastError();
+            }
+        }
         if (e == hipSuccess)
             e = hipStreamSynchronize(accel_stream_);
         accel_ms_[2] = ms_since(t2);
@@ -730,6 +777,11 @@ int Renderer::poll_accel(bool wait)
         d_wtmp_.swap(d_wtmp2_);
         d_wlinks_.swap(d_wlinks2_);
     }
+    // (the cones describe the geometry, not the tree: the resident ones go with the old geometry)
+    std::swap(ocg_, ocg_next_);
+    ocg_next_ = OConeGrid();
+    d_ocone_.swap(d_ocone2_);
+    ocone_ready_ = ocg_.computed > 0;
     wide_ready_ = !wb_.nodes.empty();
     wide_tree_ = wide_ready_ ? 2 : 0;
     if (wide_ready_ && reserve_risk(wb_.nodes.size()) != RT_OK)
@@ -768,7 +820,7 @@ int Renderer::adopt_from_lead()
     };
     if (geom_dirty_) {
         poll_accel(true);
-        cones_ready_ = wide_ready_ = lslab_ready_ = false;
+        cones_ready_ = wide_ready_ = lslab_ready_ = ocone_ready_ = false;
         auto t0 = std::chrono::steady_clock::now();
         oct_ = FlatOctree();   // (never built here)
         oct_nn_ = L.oct_nn_;
@@ -840,7 +892,7 @@ int Renderer::ensure_device_scene()
     } else if (geom_dirty_) {
         // a build of the previous geometry reads oct_: let it finish (its result is dropped)
         poll_accel(true);
-        cones_ready_ = wide_ready_ = lslab_ready_ = false;
+        cones_ready_ = wide_ready_ = lslab_ready_ = ocone_ready_ = false;
         using clk = std::chrono::steady_clock;
         auto ms_since = [](clk::time_point t) { return std::chrono::duration<float, std::milli>(clk::now() - t).count(); };
         auto t0 = clk::now();
@@ -1039,6 +1091,14 @@ void Renderer::fill_params(KParams& P) const
         P.wnodes = d_wnodes_.as<WNode>();
         P.wtris = d_wtris_.as<GTri>();
         P.wmeta = d_wmeta_.as<uint4>();
+        if (ocone_ready_ && knobs_.ocone) {
+            P.ocone.cells = d_ocone_.as<uint2>();
+            for (int a = 0; a < 3; a++) {
+                P.ocone.lo[a] = ocg_.lo[a];
+                P.ocone.dim[a] = ocg_.dim[a];
+            }
+            P.ocone.ih = ocg_.ih;
+        }
     }
     P.nnodes = (int32_t)oct_nn_;
     P.ntri_slots = (int32_t)oct_nt_;
@@ -1741,6 +1801,25 @@ int Renderer::tile_costs(uint32_t* out, int64_t n, int32_t* tiles_x, int32_t* ti
     if (e == hipSuccess)
         e = hipMemcpy(out, T.cost.p, (size_t)T.ntiles * 4, hipMemcpyDeviceToHost);
     return e == hipSuccess ? RT_OK : hip_fail(e, "tile_costs");
+}
+
+int Renderer::origin_cones(uint32_t* out, int64_t n, int32_t dims[3], float lo_ih[4])
+{
+    if (!ocone_ready_)
+        return fail(RT_EINVAL, "origin_cones: none resident (no reflective material at the last geometry change, "
+                               "RT_OCONE=0, or the SAH tree not adopted yet)");
+    const int64_t ncell = (int64_t)ocg_.dim[0] * ocg_.dim[1] * ocg_.dim[2];
+    for (int a = 0; a < 3; a++) {
+        dims[a] = ocg_.dim[a];
+        lo_ih[a] = ocg_.lo[a];
+    }
+    lo_ih[3] = ocg_.ih;
+    if (!out)
+        return RT_OK;
+    if (n < 2 * ncell)
+        return fail(RT_EINVAL, "origin_cones: buffer smaller than 2 words per cell");
+    hipError_t e = hipMemcpy(out, d_ocone_.p, (size_t)ncell * sizeof(uint2), hipMemcpyDeviceToHost);
+    return e == hipSuccess ? RT_OK : hip_fail(e, "origin_cones");
 }
 
 // Per global output band, the cycles of its tiles in the slot's last launch (a tile is charged to the

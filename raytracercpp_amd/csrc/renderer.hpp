@@ -16,6 +16,7 @@
 
 #include "../../include/rt_mi355x.h"
 #include "kparams.hpp"
+#include "ocone.hpp"
 #include "octree.hpp"
 #include "wbvh.hpp"
 
@@ -79,6 +80,8 @@ struct Knobs {
     int refl_feed = 24;       // RT_REFL_FEED=k: the reflection queries by refl_trace_feed_kernel (lane refill at k
                               // waiting lanes of a wave; C5 16 / 24 / 32 / 48: 1,128 / 1,101 / 1,103 / 1,155 ms per
                               // frame, 1,195 without); 0: refl_trace_kernel with its deferral (RT_REFL_DEFER)
+    bool ocone = true;        // RT_OCONE=0: no origin cones (reflection queries always run case (b), ocone.hpp)
+    int ocone_dim = 128;      // RT_OCONE_DIM=n: the origin-cone grid's cells along the scene's longest axis
     int refl_shadow_feed = 0; // RT_REFL_SHADOW_FEED=k: the engine's shadow pass by refl_shadow_feed_kernel (lane
                               // refill at k waiting lanes; fused engine only; C5 16 / 24 / 32 / 48: 1,154 / 1,118 /
                               // 1,094 / 1,078 ms per frame, 1,079 without); 0: refl_shadow_kernel per entry
@@ -164,6 +167,8 @@ public:
     int band_counters(unsigned long long out[2]);
     int debug_read(uint64_t* out, int64_t n);   // diagnostic builds: the per-wave records of the last frame
     int tile_costs(uint32_t* out, int64_t n, int32_t* tiles_x, int32_t* tiles_y);   // trace_frame's last tile costs
+    // the resident origin-cone grid (ocone.hpp; rt_ocone_read): its frame, and its words when out holds them
+    int origin_cones(uint32_t* out, int64_t n, int32_t dims[3], float lo_ih[4]);
     // single-process multi-device rendering (rt_set_devices, multidev.hpp): render(Renderer&)
     // renders interleaved bands on every device and gathers them here with RCCL
     int set_devices(const int* ids, int n);
@@ -293,6 +298,10 @@ private:
     // resident tree may be the quick one (wbvh.hpp build_wbvh_quick) that frames in flight still read
     WBvh wb_next_;
     DevBuf d_wnodes2_, d_wtris2_, d_wmeta2_, d_wtmp2_, d_wlinks2_;
+    // the origin cones (ocone.hpp) of the resident SAH tree's triangles and the background build's
+    OConeGrid ocg_, ocg_next_;
+    DevBuf d_ocone_, d_ocone2_, d_oc_ent_, d_oc_todo_;
+    bool ocone_ready_ = false;
     // a wide BVH's upload into the given buffers on 'stream' (the gather of its triangle records and
     // metadata from the resident octree tables on the device)
     hipError_t upload_wide(const WBvh& w, DevBuf& nodes, DevBuf& tris, DevBuf& meta, DevBuf& tmp, DevBuf& links,

@@ -793,6 +793,8 @@ RT_HD T wg_read(T x, int i)
 //       widened by rho).  A child passing both is entered, keyed by its risk key's t bound (0
 //       without risk keys).
 // Robustly back-facing children (the cone) report nothing and are skipped as before.
+// nob (rays without risk words): no triangle with q < QS can report a hit for this ray (ocone.hpp
+// ocone_skip, the origin cones), so case (b) is skipped.
 // risk (optional): the risk words of the ray's kind rsel (wrisk_pack / wbvh_risk_host / kernels.hip
 // wide_risk_kernel): a child whose key is INFINITY holds no triangle that can report a hit in case (b)
 // for this ray; its (b) triangles lie in octree leaves inside its at-risk box (so the line must cross
@@ -817,23 +819,23 @@ struct WNoFeed {
     bool drained = true;   // (wave-uniform) the feed has no query left to hand out
     int threshold = 64;
     template <class H> RT_HD void finish(int, H&, v3, v3) {}
-    RT_HD bool fetch(bool, v3&, v3&, float&, float&, const uint64_t*&, float&) { return false; }
+    RT_HD bool fetch(bool, v3&, v3&, float&, float&, const uint64_t*&, float&, bool&) { return false; }
 };
 
 template <class Stack, int G = 1, class Feed = WNoFeed>
 RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m, Stack& stk, WHit& h,
                        uint32_t* work = nullptr, float hi = INFINITY, bool ties = true, float QS = 0x1p-8f,
                        const uint64_t* risk = nullptr, int rsel = 0, float rsub = 0.0f, uint32_t max_steps = 0,
-                       Feed* feed = nullptr)
+                       Feed* feed = nullptr, bool nob = false)
 {
     static_assert(G == 1 || ((G & (G - 1)) == 0 && G <= 8 && (Stack::CAP & (Stack::CAP - 1)) == 0),
                   "a lane group: a power of two up to 8 lanes, a ring stack of 2^k entries");
     static_assert(G == 1 || !W_STEP_CAP, "a lane group leaves the loop together");
     // Feed::on (device, one lane per query): lane refill.  The wave stays in the loop; a lane whose query
     // ended waits, and when at least feed->threshold lanes (or every lane) wait, each hands its query's
-    // status and record to feed->finish and takes the next ray from feed->fetch (o, d, m, hi and the risk
-    // words and rsub, which it may leave as they are; ties, QS and rsel are the same for every query of the
-    // feed).  The per-query work is the one-query
+    // status and record to feed->finish and takes the next ray from feed->fetch (o, d, m, hi, the risk
+    // words, rsub and nob, which it may leave as they are; ties, QS and rsel are the same for every query of
+    // the feed).  The per-query work is the one-query
     // call's: the same state, reset per query, the same steps.  Returns W_MISS once the feed is drained.
     constexpr bool FEED = Feed::on;
     static_assert(!FEED || (G == 1 && !W_STEP_CAP), "lane refill: one lane per query");
@@ -907,7 +909,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
             if (idle != 0ull && (idle == __ballot(1) || __popcll(idle) >= feed->threshold)) {
                 if (idle_lane && feed->busy)
                     feed->finish(status(), h, o, d);
-                if (feed->fetch(idle_lane, o, d, m, hi, risk, rsub)) {   // (wave-uniform call; true for the lanes given a ray)
+                if (feed->fetch(idle_lane, o, d, m, hi, risk, rsub, nob)) {   // (wave-uniform call; true for the lanes given a ray)
                     setup();
                     h.t = INFINITY;
                     h.u = 1.0f;
@@ -1139,13 +1141,18 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                     // of the child's slab (D = Dn >= |o - a|)
                     const float rkj = bitsf(rw[2 * j + 1] & 0xFFFF0000u);   // wrisk_key
                     const float kbl = (rkj - rsub) * iqd;
-                    if (W_CASE_B && !risk && qlb < QS) {
+                    if (W_CASE_B && !risk && !nob && qlb < QS) {
                         // no risk words (reflection rays, rt_trace_ray):
                         W_DIAG_ADD(4, 1);
                         // the child box widened by m + rho (any t) and the origin within H0 + D sin(theta) of
                         // the slab; keyed 0 (no risk key bounds the reports' t)
                         float umin, umax;
-                        box(m + wq_len(wd(WN_EXT2 + j) & 0xffu), umin, umax);
+#if W_LAZY_EXT2
+                        const uint32_t e2 = ldg(reinterpret_cast<const uint32_t*>(nodes + cur) + WN_EXT2 + j);
+#else
+                        const uint32_t e2 = wd(WN_EXT2 + j);
+#endif
+                        box(m + wq_len(e2 & 0xffu), umin, umax);
                         bool okb = !(umin > __builtin_fmaf(fabsf(umax), SL, umax));
                         if (okb) {
                             const float s2 = wq_val_nz((e >> 8) & 0xffu, WQ_UNIT);
@@ -1160,7 +1167,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                         }
                         if (okb)
                             key[j] = 0.0f;
-                    } else if (W_CASE_B && qlb < QS && rkj < INFINITY && !(kbl > best_s)) {
+                    } else if (W_CASE_B && risk && qlb < QS && rkj < INFINITY && !(kbl > best_s)) {
                         W_DIAG_ADD(4, 1);
 #if W_LAZY_EXT2
                         const uint32_t e2 = ldg(reinterpret_cast<const uint32_t*>(nodes + cur) + WN_EXT2 + j);

@@ -276,6 +276,18 @@ class Renderer:
         self._call("rt_tile_costs", out.ctypes.data_as(C.POINTER(C.c_uint32)), out.size, C.byref(tx), C.byref(ty))
         return out.reshape(ty.value, tx.value)
 
+    def ocone_read(self):
+        """The resident origin-cone grid (rt_ocone_read): (cells uint32 [n, 2], dims int32 [3], lo_ih float32 [4])."""
+        dims = np.zeros(3, np.int32)
+        lo_ih = np.zeros(4, np.float32)
+        i32 = C.POINTER(C.c_int32)
+        f32p = C.POINTER(C.c_float)
+        self._call("rt_ocone_read", None, 0, dims.ctypes.data_as(i32), lo_ih.ctypes.data_as(f32p))
+        cells = np.zeros((int(np.prod(dims.astype(np.int64))), 2), np.uint32)
+        self._call("rt_ocone_read", cells.ctypes.data_as(C.POINTER(C.c_uint32)), cells.size, dims.ctypes.data_as(i32),
+                   lo_ih.ctypes.data_as(f32p))
+        return cells, dims, lo_ih
+
     def debug_read(self, n):
         """Diagnostic builds: the last frame's per-wave records (rt_debug_read)."""
         out = np.zeros(n, np.uint64)

@@ -256,3 +256,45 @@ def test_camera_and_light_moves_after_finish_accel(make_renderer):
         assert np.array_equal(g["hit_id"], o.hit_id), k
         assert np.array_equal(g["shadow"], o.shadow), k
         assert np.array_equal(g["argb"], o.argb), k
+
+
+def test_origin_cones_device_grid(make_renderer):
+    """The origin cones (ocone.hpp) the renderer builds on the device once the SAH tree is
+    adopted (ocone_kernel): every cell's word equals the host builder's (ocone_cell on the CPU) up to one
+    step of the rounded-up half-angle, and the device grid passes the brute-force soundness check
+    (rt_ocone_check: no triangle nearly parallel to a ray that skips case (b) reports a hit) on
+    reflection-like, grazing and random rays; a scene without a reflective material gets no grid."""
+    from raytracercpp_amd import _lib, scenes
+    from test_ocone import _rays
+    sc, st = scenes.uv_sphere_scene(200, 100, 1.5, 0.0, 160, 96)
+    sc.materials[0, 12] = 0.5
+    R = make_renderer(RT_OCONE_DIM=64)
+    R.load_scene(sc, st)
+    R.ray_trace()
+    R.finish_accel()
+    cells, dims, lo_ih = R.ocone_read()
+    tri9 = np.asarray(sc.tri, np.float32).reshape(-1, 9)
+    o, d = _rays(tri9, 2000, seed=9)
+    skip, stats, host = _lib.ocone_check(tri9, o, d, st.bvh_max_depth, st.bvh_leaf_object_count, ocone_dim=64,
+                                         want_cells=True)
+    host = host[: len(cells)]
+    assert stats["violations"] == 0, stats
+    code_d, code_h = cells[:, 1] >> 16, host[:, 1] >> 16
+    same = np.all(cells == host, axis=1)
+    special = (code_d >= 0x7FFE) | (code_h >= 0x7FFE)
+    assert np.array_equal(code_d[special], code_h[special])
+    assert np.array_equal(cells[:, 0], host[:, 0]) and np.array_equal(cells[:, 1] & 0xFFFF, host[:, 1] & 0xFFFF)
+    assert np.abs(code_d.astype(np.int64) - code_h.astype(np.int64)).max() <= 1
+    skip_d, sd = _lib.ocone_check(tri9, o, d, st.bvh_max_depth, st.bvh_leaf_object_count, ocone_dim=64,
+                                  grid=(cells, dims, lo_ih))
+    assert sd["violations"] == 0 and sd["skipping"] > 0, sd
+    print(f"device grid {dims.tolist()}: {int(same.sum())} of {len(cells)} words equal the host's; "
+          f"rays skipping (b) {sd['skipping']} of {len(o)}")
+    # no reflective material: no grid
+    sc.materials[0, 12] = 0.0
+    R2 = make_renderer(RT_OCONE_DIM=64)
+    R2.load_scene(sc, st)
+    R2.ray_trace()
+    R2.finish_accel()
+    with pytest.raises(_lib.RtError):
+        R2.ocone_read()

@@ -49,7 +49,7 @@ print(d['config'].get('workload','')[:24], 'value', d['value'], 'ms/step', d['ms
 }
 
 trace() {   # trace <name> <secs> <bench args...>
-    local name=$1 secs=$2; shift 2
+    local name=$1${TAG:+_$TAG} secs=$2; shift 2
     timeout -k 10 "$secs" rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/$name" -o run -- \
         python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-check --no-legs "$@"
 }
@@ -109,7 +109,7 @@ for spec in "$@"; do
     log="$OUT/$(echo "$step${tag:+@$tag}" | tr '/:' '__').log"
     start=$(date +%s)
     ( [ -n "$envv" ] && export $envv; run_step_limit=$(limit "$step"); \
-      timeout -k 10 "$run_step_limit" bash -c "$(declare -f run_step trace); OUT=$OUT BA='$BA'; run_step '$step'" ) > "$log" 2>&1
+      timeout -k 10 "$run_step_limit" bash -c "$(declare -f run_step trace); OUT=$OUT BA='$BA' TAG='$tag'; run_step '$step'" ) > "$log" 2>&1
     rc=$?
     echo "$step${tag:+@$tag} rc=$rc $(( $(date +%s) - start ))s" | tee -a "$OUT/steps.log"
     case "$step" in
