@@ -1046,10 +1046,14 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
     WHit w;
     const uint64_t* rk = light ? P.wrisk : nullptr;
     const float rsub = light ? wrisk_sub(W_QS_SHADOW, hi, P.risk_nu) : 0.0f;
+    // the origin cones (a lit point's shadow ray leaves its surface: the triangles whose planes pass near
+    // the origin face away from it; ocone.hpp, built for W_QS_CLOSEST >= W_QS_SHADOW, so for a superset)
+    static_assert(W_QS_SHADOW <= W_QS_CLOSEST, "the origin cones hold the at-risk triangles for the larger split");
+    const bool nob = ocone_skip(P.ocone, o, d);
 #if RT_COUNT
     uint32_t wk[4] = {0, 0, 0, 0};
     int st = wbvh_closest<Stk, G>(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, hi, false,
-                          W_QS_SHADOW, rk, 1, rsub);
+                          W_QS_SHADOW, rk, 1, rsub, 0u, (WNoFeed*)nullptr, nob);
     count_wave_steps(P, 25, wk[3]);
     if (P.counters) {
         atomicAdd(&P.counters[10], (unsigned long long)wk[0]);
@@ -1060,7 +1064,7 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
     }
 #else
     int st = wbvh_closest<Stk, G>(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, hi, false,
-                          W_QS_SHADOW, rk, 1, rsub);
+                          W_QS_SHADOW, rk, 1, rsub, 0u, (WNoFeed*)nullptr, nob);
 #endif
     if (st == W_DEEP) {
         const WDeep r = wide_closest_deep(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), hi, false, W_QS_SHADOW,

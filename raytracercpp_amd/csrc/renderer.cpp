@@ -674,13 +674,11 @@ int Renderer::reserve_risk(size_t nodes)
 void Renderer::start_accel()
 {
     accel_state_.store(1);
+    oc_done_.store(false);
+    tree_pending_ = true;
     accel_err_.clear();
-    // the origin cones serve the reflection queries: built when a material reflects (read here, on the
-    // caller's thread; a material made reflective later finds none, and its queries run case (b))
-    bool reflective = false;
-    for (size_t i = 12; i < mats_.size(); i += MAT_STRIDE)
-        reflective |= mats_[i] > 0.0f;
-    const bool want_oc = reflective && knobs_.ocone && knobs_.wbvh && !knobs_.exact;
+    // the origin cones serve the shadow and reflection queries (ocone.hpp)
+    const bool want_oc = knobs_.ocone && knobs_.wbvh && !knobs_.exact;
     float S = 0.0f;
     if (oct_nn_ > 0)
         for (int c = 0; c < 3; c++)
@@ -705,22 +703,38 @@ void Renderer::start_accel()
             build_wbvh(oct_, wb_next_);
         else
             wb_next_ = WBvh();
-        // origin cones: reflection origins lie 0.01 |n| off their hit points (make_frame), so the cells
-        // within 0.0102 of a triangle; the host plans, the device searches (ocone_kernel, after the wide
-        // BVH's records are gathered on the same stream)
-        ocg_next_ = OConeGrid();
-        OConeJob job;
-        if (want_oc && !wb_next_.nodes.empty())
-            origin_cones_plan(wb_next_, S, W_QS_CLOSEST, 0.0102 + 0x1p-16 * S, knobs_.ocone_dim,
-                              80.0 * 3.14159265358979 / 180.0, ocg_next_, job);
         accel_ms_[1] = ms_since(t1);
         auto t2 = clk::now();
         hipSetDevice(device_);
         if (e == hipSuccess && !wb_next_.nodes.empty())
             e = upload_wide(wb_next_, d_wnodes2_, d_wtris2_, d_wmeta2_, d_wtmp2_, d_wlinks2_, accel_stream_);
-        if (e == hipSuccess && !job.todo.empty()) {
-            // (a failure here only leaves the reflection queries without the cones)
-            const size_t ncell = (size_t)ocg_next_.dim[0] * ocg_next_.dim[1] * ocg_next_.dim[2];
+        if (e == hipSuccess)
+            e = hipStreamSynchronize(accel_stream_);
+        accel_ms_[2] = ms_since(t2);
+        if (e != hipSuccess)
+            accel_err_ = std::string("acceleration structures (upload): ") + hipGetErrorString(e);
+        // the origin cones after the tree, which frames may adopt meanwhile (poll_accel): their search
+        // reads the tree's nodes and records, copied here, and its device records (resident or not, they
+        // live until the next geometry change, which joins this thread first).  Reflection origins lie
+        // 0.01 |n| off their hit points (make_frame), shadow origins 1e-4 |n|: the cells within 0.0102 of a
+        // triangle.  The host plans, the device searches (ocone_kernel).
+        OConeGrid g;
+        WBvh w;
+        const GTri* wtris = d_wtris2_.as<GTri>();
+        if (e == hipSuccess && want_oc && !wb_next_.nodes.empty()) {
+            w.nodes = wb_next_.nodes;
+            w.tris = wb_next_.tris;
+        }
+        accel_state_.store(e == hipSuccess ? 2 : 3);
+        auto t3 = clk::now();
+        OConeJob job;
+        if (!w.nodes.empty())
+            origin_cones_plan(w, S, W_QS_CLOSEST, 0.0102 + 0x1p-16 * S, knobs_.ocone_dim, 80.0 * 3.14159265358979 / 180.0,
+                              g, job);
+        w = WBvh();
+        if (!job.todo.empty()) {
+            // (a failure here only leaves the queries without the cones)
+            const size_t ncell = (size_t)g.dim[0] * g.dim[1] * g.dim[2];
             hipError_t eo;
             if ((eo = d_ocone2_.reserve(ncell * sizeof(uint2))) == hipSuccess &&
                 (eo = d_oc_ent_.reserve(job.ent.size() * sizeof(OConeEnt))) == hipSuccess &&
@@ -728,70 +742,78 @@ void Renderer::start_accel()
                 (eo = hipMemcpyAsync(d_oc_ent_.p, job.ent.data(), job.ent.size() * sizeof(OConeEnt), hipMemcpyHostToDevice,
                                      accel_stream_)) == hipSuccess &&
                 (eo = hipMemcpyAsync(d_oc_todo_.p, job.todo.data(), job.todo.size() * 4, hipMemcpyHostToDevice,
-                                     accel_stream_)) == hipSuccess)
-                eo = rt_launch_ocone(d_oc_ent_.as<OConeEnt>(), d_wtris2_.as<GTri>(), d_oc_todo_.as<uint32_t>(),
-                                     (int)job.todo.size(), ocg_next_.lo, ocg_next_.dim, job.h, job.r, job.slack, job.QS,
-                                     job.cos_cap, d_ocone2_.as<uint2>(), ncell, accel_stream_);
+                                     accel_stream_)) == hipSuccess &&
+                (eo = rt_launch_ocone(d_oc_ent_.as<OConeEnt>(), wtris, d_oc_todo_.as<uint32_t>(), (int)job.todo.size(),
+                                      g.lo, g.dim, job.h, job.r, job.slack, job.QS, job.cos_cap, d_ocone2_.as<uint2>(),
+                                      ncell, accel_stream_)) == hipSuccess)
+                eo = hipStreamSynchronize(accel_stream_);
             if (eo != hipSuccess) {
-                ocg_next_ = OConeGrid();
+                g = OConeGrid();
                 (void)hipGetLastError();
             }
         }
-        if (e == hipSuccess)
-            e = hipStreamSynchronize(accel_stream_);
-        accel_ms_[2] = ms_since(t2);
-        if (e != hipSuccess)
-            accel_err_ = std::string("acceleration structures (upload): ") + hipGetErrorString(e);
-        accel_state_.store(e == hipSuccess ? 2 : 3);
+        ocg_next_ = g;
+        oc_ms_ = ms_since(t3);
+        oc_done_.store(true);
     });
 }
 
-// Adopts a finished background build (wait: blocks until it is); its structures are resident.
+// Adopts a finished background build (wait: blocks until it is, the origin cones included): the SAH
+// tree as soon as it is resident, the origin cones when the thread is done.
 int Renderer::poll_accel(bool wait)
 {
     if (!accel_thread_.joinable())
         return RT_OK;
     if (!wait && accel_state_.load() == 1)
         return RT_OK;
-    accel_thread_.join();
-    hipSetDevice(device_);
-    if (accel_state_.load() == 3) {
-        // the SAH tree was not built or uploaded: the resident tree (the quick one, if any) keeps serving
-        // frames for this geometry, and rt_stats.wide_tree says so until the next geometry change
+    if (wait || accel_state_.load() == 3 || oc_done_.load()) {
+        accel_thread_.join();
+        hipSetDevice(device_);
+    }
+    if (tree_pending_) {
+        tree_pending_ = false;
+        if (accel_state_.load() == 3) {
+            // the SAH tree was not built or uploaded: the resident tree (the quick one, if any) keeps serving
+            // frames for this geometry, and rt_stats.wide_tree says so until the next geometry change
+            if (accel_thread_.joinable())
+                accel_thread_.join();
+            accel_state_.store(0);
+            wb_next_ = WBvh();
+            wide_tree_ = wide_ready_ ? -1 : 0;
+            return fail(RT_EHIP, accel_err_);
+        }
+        cones_ready_ = !cones_.empty();
+        lslab_ready_ = !lslab_.empty();
+        if (!wb_next_.nodes.empty() || !knobs_.wbvh || knobs_.exact) {
+            // the background's tree replaces the resident one (the quick tree, if any): launches in flight
+            // keep reading the old buffers, which the next geometry change rewrites only after waiting for them
+            std::swap(wb_, wb_next_);
+            wb_next_ = WBvh();
+            d_wnodes_.swap(d_wnodes2_);
+            d_wtris_.swap(d_wtris2_);
+            d_wmeta_.swap(d_wmeta2_);
+            d_wtmp_.swap(d_wtmp2_);
+            d_wlinks_.swap(d_wlinks2_);
+        }
+        wide_ready_ = !wb_.nodes.empty();
+        wide_tree_ = wide_ready_ ? 2 : 0;
+        if (wide_ready_ && reserve_risk(wb_.nodes.size()) != RT_OK)
+            return RT_EHIP;
+        risk_valid_ = false;
+        risk_nodes_ = (int64_t)wb_.nodes.size();
+        risk_tris_ = (int64_t)wb_.tri_leaf.size();
+        ++accel_ver_;
+        build_split_ms_[1] = accel_ms_[0];
+        build_split_ms_[2] = accel_ms_[1] + accel_ms_[2];
+    }
+    if (!accel_thread_.joinable()) {   // (joined: the origin cones are done)
         accel_state_.store(0);
-        wb_next_ = WBvh();
-        wide_tree_ = wide_ready_ ? -1 : 0;
-        return fail(RT_EHIP, accel_err_);
+        // (the cones describe the geometry, not the tree)
+        std::swap(ocg_, ocg_next_);
+        ocg_next_ = OConeGrid();
+        d_ocone_.swap(d_ocone2_);
+        ocone_ready_ = ocg_.computed > 0;
     }
-    accel_state_.store(0);
-    cones_ready_ = !cones_.empty();
-    lslab_ready_ = !lslab_.empty();
-    if (!wb_next_.nodes.empty() || !knobs_.wbvh || knobs_.exact) {
-        // the background's tree replaces the resident one (the quick tree, if any): launches in flight
-        // keep reading the old buffers, which the next geometry change rewrites only after waiting for them
-        std::swap(wb_, wb_next_);
-        wb_next_ = WBvh();
-        d_wnodes_.swap(d_wnodes2_);
-        d_wtris_.swap(d_wtris2_);
-        d_wmeta_.swap(d_wmeta2_);
-        d_wtmp_.swap(d_wtmp2_);
-        d_wlinks_.swap(d_wlinks2_);
-    }
-    // (the cones describe the geometry, not the tree: the resident ones go with the old geometry)
-    std::swap(ocg_, ocg_next_);
-    ocg_next_ = OConeGrid();
-    d_ocone_.swap(d_ocone2_);
-    ocone_ready_ = ocg_.computed > 0;
-    wide_ready_ = !wb_.nodes.empty();
-    wide_tree_ = wide_ready_ ? 2 : 0;
-    if (wide_ready_ && reserve_risk(wb_.nodes.size()) != RT_OK)
-        return RT_EHIP;
-    risk_valid_ = false;
-    risk_nodes_ = (int64_t)wb_.nodes.size();
-    risk_tris_ = (int64_t)wb_.tri_leaf.size();
-    ++accel_ver_;
-    build_split_ms_[1] = accel_ms_[0];
-    build_split_ms_[2] = accel_ms_[1] + accel_ms_[2];
     return RT_OK;
 }
 

@@ -224,7 +224,10 @@ private:
     // the octree is uploaded, adopted by the first frame that starts after they are resident;
     // until then frames take the exact octree path (same results).
     std::thread accel_thread_;
-    std::atomic<int> accel_state_{0};   // 0 idle, 1 building, 2 built, 3 failed
+    std::atomic<int> accel_state_{0};   // 0 idle, 1 building, 2 the tree built (the origin cones may follow), 3 failed
+    std::atomic<bool> oc_done_{false};  // the background thread has finished (the origin cones included)
+    bool tree_pending_ = false;         // the background's tree not adopted yet
+    float oc_ms_ = 0.0f;                // the origin cones' build (background, after the tree)
     std::string accel_err_;
     hipStream_t accel_stream_ = nullptr;
     hipStream_t fence_stream_ = nullptr;   // the band slots' 'done' events (render_bands_device)

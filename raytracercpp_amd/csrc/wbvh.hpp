@@ -793,8 +793,8 @@ RT_HD T wg_read(T x, int i)
 //       widened by rho).  A child passing both is entered, keyed by its risk key's t bound (0
 //       without risk keys).
 // Robustly back-facing children (the cone) report nothing and are skipped as before.
-// nob (rays without risk words): no triangle with q < QS can report a hit for this ray (ocone.hpp
-// ocone_skip, the origin cones), so case (b) is skipped.
+// nob: no triangle with q < QS can report a hit for this ray (ocone.hpp ocone_skip, the origin cones),
+// so case (b) is skipped (with or without risk words).
 // risk (optional): the risk words of the ray's kind rsel (wrisk_pack / wbvh_risk_host / kernels.hip
 // wide_risk_kernel): a child whose key is INFINITY holds no triangle that can report a hit in case (b)
 // for this ray; its (b) triangles lie in octree leaves inside its at-risk box (so the line must cross
@@ -1167,7 +1167,7 @@ RT_HD int wbvh_closest(const WNode* nodes, const GTri* tris, v3 o, v3 d, float m
                         }
                         if (okb)
                             key[j] = 0.0f;
-                    } else if (W_CASE_B && risk && qlb < QS && rkj < INFINITY && !(kbl > best_s)) {
+                    } else if (W_CASE_B && risk && !nob && qlb < QS && rkj < INFINITY && !(kbl > best_s)) {
                         W_DIAG_ADD(4, 1);
 #if W_LAZY_EXT2
                         const uint32_t e2 = ldg(reinterpret_cast<const uint32_t*>(nodes + cur) + WN_EXT2 + j);

@@ -263,7 +263,7 @@ def test_origin_cones_device_grid(make_renderer):
     adopted (ocone_kernel): every cell's word equals the host builder's (ocone_cell on the CPU) up to one
     step of the rounded-up half-angle, and the device grid passes the brute-force soundness check
     (rt_ocone_check: no triangle nearly parallel to a ray that skips case (b) reports a hit) on
-    reflection-like, grazing and random rays; a scene without a reflective material gets no grid."""
+    reflection-like, grazing and random rays; RT_OCONE=0 builds none."""
     from raytracercpp_amd import _lib, scenes
     from test_ocone import _rays
     sc, st = scenes.uv_sphere_scene(200, 100, 1.5, 0.0, 160, 96)
@@ -290,9 +290,8 @@ def test_origin_cones_device_grid(make_renderer):
     assert sd["violations"] == 0 and sd["skipping"] > 0, sd
     print(f"device grid {dims.tolist()}: {int(same.sum())} of {len(cells)} words equal the host's; "
           f"rays skipping (b) {sd['skipping']} of {len(o)}")
-    # no reflective material: no grid
-    sc.materials[0, 12] = 0.0
-    R2 = make_renderer(RT_OCONE_DIM=64)
+    # RT_OCONE=0: no grid
+    R2 = make_renderer(RT_OCONE=0)
     R2.load_scene(sc, st)
     R2.ray_trace()
     R2.finish_accel()
