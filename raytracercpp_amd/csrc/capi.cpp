@@ -647,6 +647,8 @@ int rt_wbvh_query_ex(const float* tri9, int64_t n, int32_t max_depth, int32_t le
         // the risk bits of the camera / light (renderer.cpp prepare_risk, kernels.hip wide_risk_kernel)
         std::vector<uint64_t> risk;
         rt::WRiskArgs RA{};
+        float cap[2] = {-1.0f, -1.0f};   // (no cap: never skips)
+        float cap_dir[2][3] = {};
         if (usable && (cam || light)) {
             const float lo[3] = {f.nodes[0].dn[0], f.nodes[0].dn[1], f.nodes[0].dn[2]};
             const float hi[3] = {f.nodes[0].df[0], f.nodes[0].df[1], f.nodes[0].df[2]};
@@ -665,6 +667,28 @@ int rt_wbvh_query_ex(const float* tri9, int64_t n, int32_t max_depth, int32_t le
                 rt::wbvh_risk_host(w, lbox, RA, 0, risk);
             if (light)
                 rt::wbvh_risk_host(w, lbox, RA, 1, risk);
+            // the risk caps (renderer.cpp prepare_risk, kernels.hip wide_risk_kernel): towards the scene's centre
+            if (std::getenv("RT_RISK_CAP") == nullptr || std::atoi(std::getenv("RT_RISK_CAP")) != 0)
+                for (int sel = 0; sel < 2; sel++) {
+                    if (!RA.on[sel] || (sel == 0 ? !cam : !light))
+                        continue;
+                    const float* X = sel == 0 ? cam : light;
+                    double v[3], l = 0;
+                    for (int a = 0; a < 3; a++) {
+                        v[a] = 0.5 * ((double)lo[a] + (double)hi[a]) - (double)X[a];
+                        l += v[a] * v[a];
+                    }
+                    l = std::sqrt(l);
+                    for (int a = 0; a < 3; a++)
+                        cap_dir[sel][a] = l > 0 && l < INFINITY ? (float)(v[a] / l) : (a == 0 ? 1.0f : 0.0f);
+                    const double c[3] = {cap_dir[sel][0], cap_dir[sel][1], cap_dir[sel][2]};
+                    float sm = INFINITY;
+                    for (const rt::GTri& t : w.tris)
+                        if (rt::wbvh_risk_key(t, RA.p[sel][0], RA.p[sel][1], RA.p[sel][2], RA.G[sel], RA.nu[sel],
+                                              RA.slack[sel], RA.QS[sel]) < INFINITY)
+                            sm = std::min(sm, rt::risk_cap_tri(t, c));
+                    cap[sel] = sm;
+                }
         }
         // the origin cones (ocone.hpp) for the rays neither from the camera nor shadow rays (renderer.cpp
         // start_accel's build)
@@ -738,7 +762,11 @@ int rt_wbvh_query_ex(const float* tri9, int64_t n, int32_t max_depth, int32_t le
                 float m = 0x1p-16f * (om + S);
                 rt::WHit h;
                 const uint32_t wk0 = wk[0];
-                const bool nob = !shadow_rays && !rk && rt::ocone_skip(ocv, o, d);
+                bool nob = !shadow_rays && !rk && rt::ocone_skip(ocv, o, d);
+                if (rk && !shadow_rays && cap[0] >= 0.0f)   // a camera ray: the camera's risk cap
+                    nob = rt::risk_cap_skip(cap[0], cap_dir[0], d, W_QS_CLOSEST);
+                if (rk && shadow_rays && cap[1] >= 0.0f)    // a shadow ray with the light's words: the light's cap
+                    nob = rt::risk_cap_skip(cap[1], cap_dir[1], d, W_QS_SHADOW);
                 if (nob)
                     ++n_nob;
                 int st = rt::wbvh_closest(w.nodes.data(), w.tris.data(), o, d, m, stk, h, wk, INFINITY, true,

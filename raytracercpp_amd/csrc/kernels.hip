@@ -966,10 +966,12 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
     WHit w;
     // a ray from the camera position reads the frame's camera risk keys
     const uint64_t* rk = P.wrisk && o.x == P.cam_pos[0] && o.y == P.cam_pos[1] && o.z == P.cam_pos[2] ? P.wrisk : nullptr;
+    // the camera's risk cap: a ray into the silhouette's interior meets no at-risk triangle in case (b)
+    const bool nob = rk && P.risk_cap && risk_cap_skip(P.risk_cap[0], P.cap_dir[0], d, W_QS_CLOSEST);
 #if RT_COUNT
     uint32_t wk[4] = {0, 0, 0, 0};
     int st = wbvh_closest<Stk, G>(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, INFINITY, true,
-                          W_QS_CLOSEST, rk, 0, 0.0f);
+                          W_QS_CLOSEST, rk, 0, 0.0f, 0u, (WNoFeed*)nullptr, nob);
     count_wave_steps(P, 22, wk[3]);
     if (P.counters) {
         atomicAdd(&P.counters[10], (unsigned long long)wk[0]);
@@ -980,7 +982,7 @@ __device__ __forceinline__ bool wide_closest(const KParams& P, v3 o, v3 d, THit&
     }
 #else
     int st = wbvh_closest<Stk, G>(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, nullptr, INFINITY,
-                          true, W_QS_CLOSEST, rk, 0, 0.0f, max_steps);
+                          true, W_QS_CLOSEST, rk, 0, 0.0f, max_steps, (WNoFeed*)nullptr, nob);
 #endif
     if (st == W_LONG) {
         *longq = true;
@@ -1049,7 +1051,7 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
     // the origin cones (a lit point's shadow ray leaves its surface: the triangles whose planes pass near
     // the origin face away from it; ocone.hpp, built for W_QS_CLOSEST >= W_QS_SHADOW, so for a superset)
     static_assert(W_QS_SHADOW <= W_QS_CLOSEST, "the origin cones hold the at-risk triangles for the larger split");
-    const bool nob = ocone_skip(P.ocone, o, d);
+    const bool nob = ocone_skip(P.ocone, o, d) || (light && P.risk_cap && risk_cap_skip(P.risk_cap[1], P.cap_dir[1], d, W_QS_SHADOW));
 #if RT_COUNT
     uint32_t wk[4] = {0, 0, 0, 0};
     int st = wbvh_closest<Stk, G>(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, hi, false,
@@ -3776,11 +3778,14 @@ __device__ __forceinline__ float atomic_max_float(float* p, float v)
                      : __uint_as_float(atomicMin(reinterpret_cast<unsigned int*>(p), __float_as_uint(v)));
 }
 
+struct RiskCapDirs {
+    float c[2][3];
+};
 __global__ __launch_bounds__(256) void wide_risk_kernel(const GTri* __restrict__ wtris, const uint4* __restrict__ wmeta,
                                                         const GNode* __restrict__ onodes,
                                                         const uint32_t* __restrict__ tri_leaf,
                                                         const uint32_t* __restrict__ parent, uint32_t* K, float* B, int n,
-                                                        WRiskArgs A)
+                                                        WRiskArgs A, uint32_t* cap, RiskCapDirs cd)
 {
     const int k = (int)(blockIdx.x * 256 + threadIdx.x);
     if (k >= n)
@@ -3793,6 +3798,10 @@ __global__ __launch_bounds__(256) void wide_risk_kernel(const GTri* __restrict__
                                        A.QS[sel]);
         if (!(Kt < INFINITY))
             continue;
+        if (cap) {   // the point's risk cap: the least |cos(N, c)| over its at-risk triangles
+            const double c[3] = {cd.c[sel][0], cd.c[sel][1], cd.c[sel][2]};
+            atomicMin(cap + sel, __builtin_bit_cast(uint32_t, risk_cap_tri(t, c)));
+        }
         const GNode L = load_gnode(onodes + ldg(wmeta + k).y);   // the octree leaf of its certificate
         const uint32_t kb = __builtin_bit_cast(uint32_t, Kt);
         uint32_t e = tri_leaf[k];
@@ -4061,11 +4070,14 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_risk_box_i
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_wide_risk(
     const rt::GTri* wtris, const uint4* wmeta, const rt::GNode* onodes, const rt::WNode* wnodes, const uint32_t* tri_leaf,
     const uint32_t* parent, uint32_t* K, float* B, unsigned long long* risk, int n, int nnodes, const rt::WRiskArgs* A,
-    hipStream_t stream)
+    uint32_t* cap, const float* cap_dir, hipStream_t stream)
 {
+    rt::RiskCapDirs cd;
+    for (int i = 0; i < 6; i++)
+        cd.c[i / 3][i % 3] = cap_dir ? cap_dir[i] : 0.0f;
     if (n > 0)
         hipLaunchKernelGGL(rt::wide_risk_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, wtris, wmeta, onodes,
-                           tri_leaf, parent, K, B, n, *A);
+                           tri_leaf, parent, K, B, n, *A, cap, cd);
     const int ne = 8 * nnodes;
     if (ne > 0)
         hipLaunchKernelGGL(rt::wide_risk_pack_kernel, dim3((ne + 255) / 256), dim3(256), 0, stream, wnodes, K, B, risk,

@@ -61,6 +61,10 @@ struct KParams {
     // light's nu (WRiskArgs::ray_nu)
     const uint64_t* wrisk;
     float risk_G, risk_nl, risk_nu;
+    // the risk caps (wbvh.hpp risk_cap_skip; with wrisk): risk_cap[sel] >= |cos(N, cap_dir[sel])| of every
+    // triangle at risk for the camera (sel 0) / the light (sel 1), computed with the words
+    const float* risk_cap;
+    float cap_dir[2][3];
     // the origin cones (ocone.hpp; cells nullptr: none resident): the rays without risk words whose
     // ocone_skip holds skip case (b) (the reflection queries, ReflFeed)
     OConeView ocone;

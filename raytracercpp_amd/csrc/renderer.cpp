@@ -65,7 +65,7 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_wide_gathe
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_wide_risk(
     const rt::GTri* wtris, const uint4* wmeta, const rt::GNode* onodes, const rt::WNode* wnodes, const uint32_t* tri_leaf,
     const uint32_t* parent, uint32_t* K, float* B, unsigned long long* risk, int n, int nnodes, const rt::WRiskArgs* A,
-    hipStream_t stream);
+    uint32_t* cap, const float* cap_dir, hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_downscale(const uint32_t* in, int w, int h_rows, int f, uint32_t* out,
                                           hipStream_t stream);
 
@@ -139,6 +139,8 @@ Knobs Knobs::from_env()
         k.refl_defer = std::max(0, atoi(v));
     if (const char* v = getenv("RT_REFL_FEED"))    // lane refill of the reflection queries at this many waiting lanes
         k.refl_feed = std::min(64, std::max(0, atoi(v)));
+    if (const char* v = getenv("RT_RISK_CAP"))
+        k.risk_cap = atoi(v) != 0;
     if (const char* v = getenv("RT_OCONE"))
         k.ocone = atoi(v) != 0;
     if (const char* v = getenv("RT_OCONE_DIM"))
@@ -663,11 +665,11 @@ hipError_t Renderer::upload_wide(const WBvh& w, DevBuf& nodes, DevBuf& tris, Dev
 // node); growing it replaces the buffer, so launches in flight that read it are waited for first.
 int Renderer::reserve_risk(size_t nodes)
 {
-    if (d_wrisk_.bytes >= nodes * 288)
+    if (d_wrisk_.bytes >= nodes * 288 + 64)
         return RT_OK;
     if (d_wrisk_.p && (sync_slots() != RT_OK || hipStreamSynchronize(stream_) != hipSuccess))
         return RT_EHIP;
-    hipError_t e = d_wrisk_.reserve(nodes * 288);
+    hipError_t e = d_wrisk_.reserve(nodes * 288 + 64);   // (+ the risk caps)
     return e == hipSuccess ? RT_OK : hip_fail(e, "hipMalloc (risk words)");
 }
 
@@ -882,7 +884,7 @@ int Renderer::adopt_from_lead()
             copy(d_wmeta_, L.d_wmeta_, L.wb_.slot.size() * 16);
             copy(d_wlinks_, L.d_wlinks_, (L.wb_.tri_leaf.size() + L.wb_.parent.size()) * 4);
             if (e == hipSuccess)
-                e = d_wrisk_.reserve(L.wb_.nodes.size() * 288);
+                e = d_wrisk_.reserve(L.wb_.nodes.size() * 288 + 64);
         }
         if (e == hipSuccess)
             e = hipStreamSynchronize(stream_);
@@ -2099,8 +2101,23 @@ int Renderer::prepare_risk(KParams& P, hipStream_t stream)
     P.risk_G = 0.0f;
     P.risk_nl = 0.0f;
     P.risk_nu = 0.0f;
+    P.risk_cap = nullptr;
     if (!P.wnodes || !knobs_.risk || risk_nodes_ <= 0 || !d_wrisk_.p || !d_wlinks_.p)
         return RT_OK;
+    // the risk caps' directions: from the camera / the light towards the scene's centre (any direction is
+    // sound; this one makes a convex object's silhouette interior skip case (b), wbvh.hpp risk_cap_skip)
+    float cap_dir[2][3];
+    for (int sel = 0; sel < 2; sel++) {
+        const float* X = sel == 0 ? P.cam_pos : P.light;
+        double v[3], l = 0;
+        for (int a = 0; a < 3; a++) {
+            v[a] = 0.5 * ((double)oct_root_.dn[a] + (double)oct_root_.df[a]) - (double)X[a];
+            l += v[a] * v[a];
+        }
+        l = std::sqrt(l);
+        for (int a = 0; a < 3; a++)
+            cap_dir[sel][a] = l > 0 && l < INFINITY ? (float)(v[a] / l) : (a == 0 ? 1.0f : 0.0f);
+    }
     hipError_t e;
     if (!risk_valid_ || std::memcmp(risk_cam_, P.cam_pos, sizeof risk_cam_) ||
         std::memcmp(risk_light_, P.light, sizeof risk_light_)) {
@@ -2116,10 +2133,13 @@ int Renderer::prepare_risk(KParams& P, hipStream_t stream)
         unsigned long long* words = d_wrisk_.as<unsigned long long>();
         uint32_t* K = reinterpret_cast<uint32_t*>(words + ne);
         float* B = reinterpret_cast<float*>(K + ne);
+        uint32_t* cap = reinterpret_cast<uint32_t*>(B + 6 * ne);   // (the 2 caps, past the boxes)
+        std::memcpy(risk_cap_dir_, cap_dir, sizeof risk_cap_dir_);
         if ((e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(K), 0x7F800000, ne, stream)) != hipSuccess ||
+            (e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(cap), 0x7F800000, 2, stream)) != hipSuccess ||
             (e = rt_launch_risk_box_init(B, ne, stream)) != hipSuccess ||
             (e = rt_launch_wide_risk(P.wtris, P.wmeta, P.nodes, P.wnodes, links, links + risk_tris_, K, B, words,
-                                     (int)risk_tris_, (int)risk_nodes_, &A, stream)) != hipSuccess ||
+                                     (int)risk_tris_, (int)risk_nodes_, &A, cap, &risk_cap_dir_[0][0], stream)) != hipSuccess ||
             // risk_ev_ is recorded on the renderer's own fence stream behind 'stream' (as a band slot's
             // 'done'): later launches wait on it after the caller may have destroyed 'stream'
             (e = hipEventRecord(risk_mark_, stream)) != hipSuccess ||
@@ -2139,6 +2159,10 @@ int Renderer::prepare_risk(KParams& P, hipStream_t stream)
     P.risk_G = risk_G_;
     P.risk_nl = risk_nl_;
     P.risk_nu = risk_nu_;
+    if (knobs_.risk_cap) {
+        P.risk_cap = reinterpret_cast<const float*>(d_wrisk_.as<uint8_t>() + (size_t)risk_nodes_ * 288);
+        std::memcpy(P.cap_dir, risk_cap_dir_, sizeof P.cap_dir);
+    }
     return RT_OK;
 }
 

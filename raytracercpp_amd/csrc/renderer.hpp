@@ -80,6 +80,8 @@ struct Knobs {
     int refl_feed = 24;       // RT_REFL_FEED=k: the reflection queries by refl_trace_feed_kernel (lane refill at k
                               // waiting lanes of a wave; C5 16 / 24 / 32 / 48: 1,128 / 1,101 / 1,103 / 1,155 ms per
                               // frame, 1,195 without); 0: refl_trace_kernel with its deferral (RT_REFL_DEFER)
+    bool risk_cap = true;     // RT_RISK_CAP=0: no risk caps (camera / shadow rays into a silhouette's interior skip
+                              // case (b), wbvh.hpp risk_cap_skip)
     bool ocone = true;        // RT_OCONE=0: no origin cones (reflection queries always run case (b), ocone.hpp)
     int ocone_dim = 128;      // RT_OCONE_DIM=n: the origin-cone grid's cells along the scene's longest axis
     int refl_shadow_feed = 0; // RT_REFL_SHADOW_FEED=k: the engine's shadow pass by refl_shadow_feed_kernel (lane
@@ -305,6 +307,7 @@ private:
     OConeGrid ocg_, ocg_next_;
     DevBuf d_ocone_, d_ocone2_, d_oc_ent_, d_oc_todo_;
     bool ocone_ready_ = false;
+    float risk_cap_dir_[2][3] = {};   // the risk caps' directions of the resident words (camera, light)
     // a wide BVH's upload into the given buffers on 'stream' (the gather of its triangle records and
     // metadata from the resident octree tables on the device)
     hipError_t upload_wide(const WBvh& w, DevBuf& nodes, DevBuf& tris, DevBuf& meta, DevBuf& tmp, DevBuf& links,

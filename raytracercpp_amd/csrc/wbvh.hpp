@@ -583,6 +583,39 @@ inline WRiskArgs wbvh_risk_args(const float lo[3], const float hi[3], float S, c
     return A;
 }
 
+// The risk cap of a frame's point X (camera or light): s <= |cos(N, c)| for the exact normal N of every
+// triangle at risk for X's rays (wbvh_risk_key < INFINITY), c a unit direction (from X towards the scene).
+// A ray of X's kind at angle g to the line of c has, for each of them, |cos(N, d)| >= s cos g - sqrt(1 -
+// s^2) sin g (N = a c + b e with |a| >= s, e normal to c): when that is >= QS (plus a margin over the float
+// evaluation) none of them is in case (b) for the ray, and the others cannot report there (their key is
+// INFINITY), so the query skips case (b).  For a convex object seen from X the at-risk triangles are its
+// silhouette, whose normals are all at 90 degrees + the silhouette's angle from the direction to its
+// centre: every ray into the silhouette's interior skips.
+RT_HD bool risk_cap_skip(float s, const float c[3], v3 d, float QS)
+{
+    const float dl = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);
+    const float cg = fabsf(c[0] * d.x + c[1] * d.y + c[2] * d.z) / dl;
+    const float x = c[1] * d.z - c[2] * d.y, y = c[2] * d.x - c[0] * d.z, z = c[0] * d.y - c[1] * d.x;
+    const float sg = sqrtf(x * x + y * y + z * z) / dl;
+    return s * cg - sqrtf(fmaxf(0.0f, 1.0f - s * s)) * sg >= QS + 0x1p-14f;
+}
+// A triangle's lower bound on |cos(N, c)| (risk_cap_skip), in double from the record's float edges; 0 for
+// a degenerate record (no normal: it counts as at risk for every ray)
+RT_HD float risk_cap_tri(const GTri& t, const double c[3])
+{
+    const double x0 = t.ab[0], x1 = t.ab[1], x2 = t.ab[2], y0 = t.ac[0], y1 = t.ac[1], y2 = t.ac[2];
+    const double c0 = x1 * y2 - x2 * y1, c1 = x2 * y0 - x0 * y2, c2 = x0 * y1 - x1 * y0;
+    const double la = sqrt(x0 * x0 + x1 * x1 + x2 * x2), lc = sqrt(y0 * y0 + y1 * y1 + y2 * y2);
+    const double cl = sqrt(c0 * c0 + c1 * c1 + c2 * c2);
+    if (!(la * lc > 0x1p-100) || !(cl > 0x1p-50 * la * lc) || !(cl < INFINITY))
+        return 0.0f;
+    const double v = fabs(c0 * c[0] + c1 * c[1] + c2 * c[2]) / cl - 1e-9;
+    if (!(v > 0.0))
+        return 0.0f;
+    const float f = (float)v;
+    return (double)f > v ? nextafterf(f, 0.0f) : f;
+}
+
 // rsub of wbvh_closest for a shadow ray with |light - o| <= h (rounded up)
 RT_HD float wrisk_sub(float QS, float h, float nu)
 {
