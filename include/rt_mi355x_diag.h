@@ -99,6 +99,12 @@ int rt_ocone_check(const float *tri9, int64_t n, int32_t max_depth, int32_t leaf
  * material reflects): dims[3], lo_ih[4] = {lo x, y, z, 1 / cell size}; out (optional) receives its
  * words, 2 per cell (n >= 2 dims[0] dims[1] dims[2]). */
 int rt_ocone_read(rt_renderer *r, uint32_t *out, int64_t n, int32_t dims[3], float lo_ih[4]);
+/* The camera's risk cap by brute force (CPU tests): rays from cam with directions dir; for
+ * each that the cap (as the renderer computes it per frame, or cap_override >= 0) lets skip case (b) (skip[i]
+ * = 1, optional), Moller-Trumbore runs on every triangle nearly parallel to it or degenerate: a reported hit
+ * is a violation.  out[4] = {violations, rays skipping, grazing triangle tests, the cap x 1e9 (-1: none)}. */
+int rt_risk_cap_check(const float *tri9, int64_t n, int32_t max_depth, int32_t leaf_max_obj_count, const float *cam,
+                      const float *dir, int64_t nrays, float cap_override, int32_t *skip, int64_t out[4]);
 
 #ifdef __cplusplus
 }

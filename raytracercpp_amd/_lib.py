@@ -148,6 +148,8 @@ SIGNATURES = {
     "rt_ocone_check": (C.c_int, [_f32p, C.c_int64, C.c_int32, C.c_int32, C.c_int32, _f32p, _f32p, C.c_int64, _i32p,
                                  _i64p, C.POINTER(C.c_uint32), _i32p, _f32p, C.POINTER(C.c_uint32)]),
     "rt_ocone_read": (C.c_int, [_H, C.POINTER(C.c_uint32), C.c_int64, _i32p, _f32p]),
+    "rt_risk_cap_check": (C.c_int, [_f32p, C.c_int64, C.c_int32, C.c_int32, _f32p, _f32p, C.c_int64, C.c_float, _i32p,
+                                    _i64p]),
 }
 
 _lib = None
@@ -323,6 +325,19 @@ def ocone_check(tri9, orig, dirs, max_depth=12, leaf=40, ocone_dim=64, grid=None
     keys = ("violations", "skipping", "grazing_tests", "cells", "empty_cells", "noskip_cells")
     res = (skip, dict(zip(keys, map(int, out))))
     return res + (built,) if want_cells else res
+
+
+def risk_cap_check(tri9, cam, dirs, max_depth=12, leaf=40, cap_override=-1.0):
+    """rt_risk_cap_check: (skip flags, dict) -- the camera risk cap's brute-force soundness check (no GPU)."""
+    tri9 = f32(tri9).reshape(-1, 9)
+    c = f32(cam).reshape(3)
+    d = f32(dirs).reshape(-1, 3)
+    skip = np.zeros(d.shape[0], np.int32)
+    out = np.zeros(4, np.int64)
+    check(lib().rt_risk_cap_check(ptr(tri9, _f32p), tri9.shape[0], max_depth, leaf, ptr(c, _f32p), ptr(d, _f32p),
+                                  d.shape[0], float(cap_override), ptr(skip, _i32p), ptr(out, _i64p)), "rt_risk_cap_check")
+    return skip, {"violations": int(out[0]), "skipping": int(out[1]), "grazing_tests": int(out[2]),
+                  "cap": float(out[3]) * 1e-9 if out[3] >= 0 else None}
 
 
 def octree_digest(tri9, max_depth=12, leaf=40, builder=0):

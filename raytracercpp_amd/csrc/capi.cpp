@@ -449,6 +449,117 @@ int rt_obj_fetch(const rt_obj* o, float* tri9, int32_t* mat, float* uv6, float* 
 
 void rt_obj_close(rt_obj* o) { delete o; }
 
+// For a ray that skips case (b): how many triangles nearly parallel to it (|cos(N, d)| < W_QS_CLOSEST, N
+// = ab x ac exact, per-triangle N and |N| in Nn) or degenerate (no finite q) Moller-Trumbore reports a hit
+// from (mt_record, the reference's expressions); grazing counts the first kind tested
+static int64_t grazing_reports(const std::vector<rt::GTri>& tris, const std::vector<double>& Nn, rt::v3 o, rt::v3 d,
+                               int64_t& grazing)
+{
+    int64_t viol = 0;
+    const double dl = std::sqrt((double)d.x * d.x + (double)d.y * d.y + (double)d.z * d.z);
+    for (size_t k = 0; k < tris.size(); k++) {
+        const double* N = &Nn[4 * k];
+        const double q = std::fabs(N[0] * d.x + N[1] * d.y + N[2] * d.z) / (N[3] * dl);
+        if (q == q && !(q < W_QS_CLOSEST))
+            continue;   // (a)'s
+        grazing += q == q;
+        float tt, uu, vv;
+        if (rt::mt_record(tris[k], o, d, tt, uu, vv))
+            ++viol;
+    }
+    return viol;
+}
+
+static std::vector<double> exact_normals(const std::vector<rt::GTri>& tris)
+{
+    std::vector<double> Nn(tris.size() * 4);
+    for (size_t k = 0; k < tris.size(); k++) {
+        const rt::GTri& t = tris[k];
+        const double x0 = t.ab[0], x1 = t.ab[1], x2 = t.ab[2], y0 = t.ac[0], y1 = t.ac[1], y2 = t.ac[2];
+        Nn[4 * k] = x1 * y2 - x2 * y1;
+        Nn[4 * k + 1] = x2 * y0 - x0 * y2;
+        Nn[4 * k + 2] = x0 * y1 - x1 * y0;
+        Nn[4 * k + 3] = std::sqrt(Nn[4 * k] * Nn[4 * k] + Nn[4 * k + 1] * Nn[4 * k + 1] + Nn[4 * k + 2] * Nn[4 * k + 2]);
+    }
+    return Nn;
+}
+
+// The camera's risk cap by brute force (CPU tests): rays from cam; for each that risk_cap_skip lets skip case
+// (b) (the cap as renderer.cpp prepare_risk computes it, or cap_override >= 0), every triangle nearly parallel
+// to it goes through Moller-Trumbore.  out[4] = {violations, rays skipping, grazing tests, the cap x 1e9}.
+int rt_risk_cap_check(const float* tri9, int64_t n, int32_t max_depth, int32_t leaf_max_obj_count, const float* cam,
+                      const float* dir, int64_t nrays, float cap_override, int32_t* skip, int64_t out[4])
+{
+    if (n <= 0 || !tri9 || !cam || nrays < 0 || (nrays > 0 && !dir) || !out)
+        return bad("rt_risk_cap_check: bad arguments");
+    try {
+        rt::FlatOctree f;
+        rt::WBvh w;
+        rt::build_flat_octree(tri9, n, max_depth, leaf_max_obj_count, f);
+        rt::build_wbvh(f, w);
+        if (f.nodes.empty())
+            return bad("rt_risk_cap_check: no octree");
+        float S = 0.0f;
+        for (int a = 0; a < 3; a++)
+            S = std::max(S, std::max(std::fabs(f.nodes[0].dn[a]), std::fabs(f.nodes[0].df[a])));
+        const float lo[3] = {f.nodes[0].dn[0], f.nodes[0].dn[1], f.nodes[0].dn[2]};
+        const float hi[3] = {f.nodes[0].df[0], f.nodes[0].df[1], f.nodes[0].df[2]};
+        const float zero[3] = {0, 0, 0};
+        const rt::WRiskArgs RA = rt::wbvh_risk_args(lo, hi, S, cam, zero, W_QS_CLOSEST, W_QS_SHADOW);
+        float cdir[3];
+        double v[3], l = 0;
+        for (int a = 0; a < 3; a++) {
+            v[a] = 0.5 * ((double)lo[a] + (double)hi[a]) - (double)cam[a];
+            l += v[a] * v[a];
+        }
+        l = std::sqrt(l);
+        for (int a = 0; a < 3; a++)
+            cdir[a] = l > 0 && l < INFINITY ? (float)(v[a] / l) : (a == 0 ? 1.0f : 0.0f);
+        const double c[3] = {cdir[0], cdir[1], cdir[2]};
+        float cap = INFINITY;
+        for (const rt::GTri& t : w.tris)
+            if (rt::wbvh_risk_key(t, RA.p[0][0], RA.p[0][1], RA.p[0][2], RA.G[0], RA.nu[0], RA.slack[0], RA.QS[0]) < INFINITY)
+                cap = std::min(cap, rt::risk_cap_tri(t, c));
+        if (cap_override >= 0.0f)
+            cap = cap_override;
+        const std::vector<double> Nn = exact_normals(w.tris);
+        std::atomic<int64_t> nskip{0}, nviol{0}, ngraze{0};
+        const rt::v3 o = rt::mk(cam[0], cam[1], cam[2]);
+        auto body = [&](int64_t b, int64_t e) {
+            for (int64_t i = b; i < e; i++) {
+                const rt::v3 d = rt::mk(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]);
+                const bool sk = RA.on[0] && rt::risk_cap_skip(cap, cdir, d, W_QS_CLOSEST);
+                if (skip)
+                    skip[i] = sk ? 1 : 0;
+                if (!sk)
+                    continue;
+                ++nskip;
+                int64_t g = 0;
+                nviol += grazing_reports(w.tris, Nn, o, d, g);
+                ngraze += g;
+            }
+        };
+        unsigned hc = std::max(1u, std::min(std::thread::hardware_concurrency(), 16u));
+        std::vector<std::thread> th;
+        int64_t chunk = (nrays + hc - 1) / hc;
+        for (unsigned k = 0; k < hc; k++) {
+            int64_t b = (int64_t)k * chunk, e = std::min(nrays, b + chunk);
+            if (b < e)
+                th.emplace_back(body, b, e);
+        }
+        for (auto& x : th)
+            x.join();
+        out[0] = nviol.load();
+        out[1] = nskip.load();
+        out[2] = ngraze.load();
+        out[3] = (int64_t)(cap < INFINITY ? (double)cap * 1e9 : -1);
+        return RT_OK;
+    } catch (const std::bad_alloc&) {
+        g_err = "rt_risk_cap_check: out of host memory";
+        return RT_ENOMEM;
+    }
+}
+
 // The origin cones' soundness by brute force (CPU tests): for each ray (o, d) that ocone_skip lets
 // skip case (b), every triangle with q = |cos(N, d)| < W_QS_CLOSEST (N = ab x ac exact) is run through
 // Moller-Trumbore (mt_record, the reference's expressions): a reported hit is a violation.
@@ -493,16 +604,7 @@ int rt_ocone_check(const float* tri9, int64_t n, int32_t max_depth, int32_t leaf
             }
             v.ih = g.ih;
         }
-        // per triangle: q's numerator scale |N| (exact normal of the float edges)
-        std::vector<double> Nn(w.tris.size() * 4);
-        for (size_t k = 0; k < w.tris.size(); k++) {
-            const rt::GTri& t = w.tris[k];
-            const double x0 = t.ab[0], x1 = t.ab[1], x2 = t.ab[2], y0 = t.ac[0], y1 = t.ac[1], y2 = t.ac[2];
-            Nn[4 * k] = x1 * y2 - x2 * y1;
-            Nn[4 * k + 1] = x2 * y0 - x0 * y2;
-            Nn[4 * k + 2] = x0 * y1 - x1 * y0;
-            Nn[4 * k + 3] = std::sqrt(Nn[4 * k] * Nn[4 * k] + Nn[4 * k + 1] * Nn[4 * k + 1] + Nn[4 * k + 2] * Nn[4 * k + 2]);
-        }
+        const std::vector<double> Nn = exact_normals(w.tris);
         std::atomic<int64_t> nskip{0}, nviol{0}, ngraze{0};
         auto body = [&](int64_t b, int64_t e) {
             for (int64_t i = b; i < e; i++) {
@@ -514,27 +616,9 @@ int rt_ocone_check(const float* tri9, int64_t n, int32_t max_depth, int32_t leaf
                 if (!sk)
                     continue;
                 ++nskip;
-                const double dl = std::sqrt((double)d.x * d.x + (double)d.y * d.y + (double)d.z * d.z);
-                for (size_t k = 0; k < w.tris.size(); k++) {
-                    const double* N = &Nn[4 * k];
-                    const double q = std::fabs(N[0] * d.x + N[1] * d.y + N[2] * d.z) / (N[3] * dl);
-                    if (!(q < W_QS_CLOSEST))
-                        continue;   // (a)'s, or degenerate / NaN: tested below too
-                    ++ngraze;
-                    float tt, uu, vv;
-                    if (rt::mt_record(w.tris[k], o, d, tt, uu, vv))
-                        ++nviol;
-                }
-                // degenerate records (q undefined) are case (b)'s as well
-                for (size_t k = 0; k < w.tris.size(); k++) {
-                    const double* N = &Nn[4 * k];
-                    const double q = std::fabs(N[0] * d.x + N[1] * d.y + N[2] * d.z) / (N[3] * dl);
-                    if (q == q)
-                        continue;
-                    float tt, uu, vv;
-                    if (rt::mt_record(w.tris[k], o, d, tt, uu, vv))
-                        ++nviol;
-                }
+                int64_t g = 0;
+                nviol += grazing_reports(w.tris, Nn, o, d, g);
+                ngraze += g;
             }
         };
         unsigned hc = std::max(1u, std::min(std::thread::hardware_concurrency(), 16u));

@@ -30,7 +30,7 @@ def test_diagnostics_apart_from_the_renderer_surface():
     """rt_mi355x.h holds the Renderer surface; the diagnostics live in rt_mi355x_diag.h only."""
     main, diag = declared_functions((HEADER,)), declared_functions((DIAG_HEADER,))
     assert {"rt_tile_costs", "rt_debug_read", "rt_wide_query", "rt_risk_words", "rt_wbvh_query", "rt_wbvh_query_ex",
-            "rt_octree_digest", "rt_ocone_check", "rt_ocone_read"} == diag
+            "rt_octree_digest", "rt_ocone_check", "rt_ocone_read", "rt_risk_cap_check"} == diag
     assert not (main & diag)
 
 

@@ -138,3 +138,48 @@ def test_origin_cones_same_answers_fewer_visits():
     assert oc[3] > len(o) // 2, oc            # most skip case (b)
     assert n1.sum() < 0.7 * n0.sum(), (n0.mean(), n1.mean())
     print(f"visits per ray {n0.mean():.2f} -> {n1.mean():.2f}; rays skipping (b) {oc[3]} of {len(o)}; cells {oc[0]}")
+
+
+def _camera_rays(tri9, n, seed):
+    """A camera off the scene's box; rays towards random points of random triangles, towards points of the
+    triangles most nearly edge-on to the camera (the silhouette), and in random directions."""
+    rng = np.random.default_rng(seed)
+    T = tri9.reshape(-1, 3, 3).astype(np.float64)
+    lo, hi = T.reshape(-1, 3).min(0), T.reshape(-1, 3).max(0)
+    cam = (lo + hi) / 2 + np.array([0.3, 0.45, 1.0]) * 1.6 * (hi - lo).max()
+    nrm = np.cross(T[:, 1] - T[:, 0], T[:, 2] - T[:, 0])
+    ln = np.linalg.norm(nrm, axis=1)
+    ok = np.flatnonzero(ln > 1e-12)
+    ctr = T.mean(1)
+    w = ctr - cam
+    edge = np.abs((nrm * w).sum(1)) / (ln * np.linalg.norm(w, axis=1) + 1e-30)
+    sil = ok[np.argsort(edge[ok])[: max(50, len(ok) // 50)]]
+    pick = np.concatenate([rng.choice(ok, n), rng.choice(sil, n)])
+    p = (T[pick] * rng.dirichlet([1, 1, 1], len(pick))[:, :, None]).sum(1)
+    d = np.concatenate([p - cam, rng.normal(size=(n // 2, 3))])
+    return cam.astype(np.float32), d.astype(np.float32)
+
+
+@pytest.mark.parametrize("name", ["sphere", "bumpy", "sphere_floor", "cube", "soup_clean"])
+def test_risk_cap_sound_by_brute_force(name):
+    """The camera's risk cap (wbvh.hpp risk_cap_skip): for every camera ray it lets skip case (b), no triangle
+    nearly parallel to the ray (or degenerate) reports a hit in Moller-Trumbore; on the smooth sphere most rays
+    at the object skip."""
+    tri9 = MESHES[name]()
+    cam, d = _camera_rays(tri9, 1500, seed=len(name) + 1)
+    skip, st = _lib.risk_cap_check(tri9, cam, d)
+    assert st["violations"] == 0, st
+    if name == "sphere":
+        assert skip[:1500].mean() > 0.5 and st["grazing_tests"] > 0, (skip[:1500].mean(), st)
+    print(name, st, "skip fraction", skip.mean())
+
+
+def test_risk_cap_check_catches_a_wrong_cap():
+    """The checker has teeth: a cap of 1 (every at-risk normal claimed parallel to the centre's direction)
+    lets the silhouette's grazing rays skip, and Moller-Trumbore reports hits from the nearly parallel
+    triangles they graze."""
+    tri9 = MESHES["sphere"]()
+    cam, d = _camera_rays(tri9, 1500, seed=3)
+    _, good = _lib.risk_cap_check(tri9, cam, d)
+    _, bad = _lib.risk_cap_check(tri9, cam, d, cap_override=1.0)
+    assert good["violations"] == 0 and bad["violations"] > 0, (good, bad)
