@@ -610,7 +610,7 @@ int rt_ocone_check(const float* tri9, int64_t n, int32_t max_depth, int32_t leaf
             for (int64_t i = b; i < e; i++) {
                 const rt::v3 o = rt::mk(orig[3 * i], orig[3 * i + 1], orig[3 * i + 2]);
                 const rt::v3 d = rt::mk(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]);
-                const bool sk = rt::ocone_skip(v, o, d);
+                const bool sk = rt::ocone_skip(v, o, d, W_QS_CLOSEST);
                 if (skip)
                     skip[i] = sk ? 1 : 0;
                 if (!sk)
@@ -846,7 +846,7 @@ int rt_wbvh_query_ex(const float* tri9, int64_t n, int32_t max_depth, int32_t le
                 float m = 0x1p-16f * (om + S);
                 rt::WHit h;
                 const uint32_t wk0 = wk[0];
-                bool nob = !shadow_rays && !rk && rt::ocone_skip(ocv, o, d);
+                bool nob = !shadow_rays && !rk && rt::ocone_skip(ocv, o, d, W_QS_CLOSEST);
                 if (rk && !shadow_rays && cap[0] >= 0.0f)   // a camera ray: the camera's risk cap
                     nob = rt::risk_cap_skip(cap[0], cap_dir[0], d, W_QS_CLOSEST);
                 if (rk && shadow_rays && cap[1] >= 0.0f)    // a shadow ray with the light's words: the light's cap

@@ -1051,7 +1051,7 @@ __device__ __forceinline__ bool wide_shadow(const KParams& P, v3 o, v3 d, float 
     // the origin cones (a lit point's shadow ray leaves its surface: the triangles whose planes pass near
     // the origin face away from it; ocone.hpp, built for W_QS_CLOSEST >= W_QS_SHADOW, so for a superset)
     static_assert(W_QS_SHADOW <= W_QS_CLOSEST, "the origin cones hold the at-risk triangles for the larger split");
-    const bool nob = ocone_skip(P.ocone, o, d) || (light && P.risk_cap && risk_cap_skip(P.risk_cap[1], P.cap_dir[1], d, W_QS_SHADOW));
+    const bool nob = ocone_skip(P.ocone, o, d, W_QS_SHADOW) || (light && P.risk_cap && risk_cap_skip(P.risk_cap[1], P.cap_dir[1], d, W_QS_SHADOW));
 #if RT_COUNT
     uint32_t wk[4] = {0, 0, 0, 0};
     int st = wbvh_closest<Stk, G>(P.wnodes, P.wtris, o, d, 0x1p-16f * (om + P.scene_scale), stk, w, wk, hi, false,
@@ -2496,7 +2496,7 @@ struct ReflFeed {
         }
         const float om = fmaxf(fabsf(o.x), fmaxf(fabsf(o.y), fabsf(o.z)));
         m = 0x1p-16f * (om + P->scene_scale);
-        nob = ocone_skip(P->ocone, o, d);
+        nob = ocone_skip(P->ocone, o, d, W_QS_CLOSEST);
         busy = true;
         return true;
     }

@@ -70,7 +70,7 @@ Cone merge(const Cone& p, const Cone& q)
 struct Agg {
     double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     Cone plane;    // exact normals N = ab x ac of the non-degenerate triangles (the lemma's planes)
-    Cone stored;   // stored normals n~ (Moller-Trumbore's Mdet), the non-zero ones
+    Cone stored;   // stored normals n~ (Moller-Trumbore's Mdet), the non-zero ones, and the exact ones
     double lmax = 0, smin = INFINITY, s2min = INFINITY;   // the lemma's L, s, s2 (0: degenerate below)
     bool any = false;   // a triangle with a non-zero stored normal (one that can report at all)
 };
@@ -115,6 +115,7 @@ void add_tri(Agg& g, const GTri& t)
     cp.a[2] = c2 / cl;
     cp.th = 1e-15;
     g.plane = merge(g.plane, cp);
+    g.stored = merge(g.stored, cp);   // (the cell cones bound both normals: ocone_cell's front route reads N)
 }
 
 void add_agg(Agg& g, const Agg& c)

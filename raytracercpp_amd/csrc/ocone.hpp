@@ -15,9 +15,14 @@
 // fewer node visits (a reflection ray leaving the surface faces the back of the triangles near its
 // origin, which are the ones whose planes pass near it).
 //
+// The cone holds the exact unit normals N = ab x ac of the at-risk triangles too, which gives a second
+// route: a ray with angle(A, -d) + beta <= acos(QS + EPS) has |cos(N, d)| >= QS for every at-risk triangle,
+// so none of them is in case (b) (a ray entering the surface its origin is above: a reflection sample that
+// turns back into a bumpy surface).  A degenerate at-risk record (no N) closes that route (OC_NOFRONT).
+//
 // Cell word (uint2): x = A.x | A.y << 16, y = A.z | code << 16 (A as signed 16-bit integers, the axis
-// A / |A|); code = beta in units of (pi/2) / OC_BMAX rounded up, OC_NOSKIP (no bound: case (b) runs),
-// OC_EMPTY (no triangle at risk: every ray may skip).
+// A / |A|); code = beta in units of (pi/2) / OC_BMAX rounded up (| OC_NOFRONT), OC_NOSKIP (no bound: case
+// (b) runs), OC_EMPTY (no triangle at risk: every ray may skip).
 #pragma once
 
 #include <stdint.h>
@@ -28,7 +33,7 @@
 
 namespace rt {
 
-constexpr uint32_t OC_BMAX = 0x7FFDu, OC_EMPTY = 0x7FFEu, OC_NOSKIP = 0x7FFFu;
+constexpr uint32_t OC_BMAX = 0x7FFDu, OC_EMPTY = 0x7FFEu, OC_NOSKIP = 0x7FFFu, OC_NOFRONT = 0x8000u;
 constexpr float OC_EPS = 0x1p-12f;   // the test's margin in cos(angle(n~, -d)) (rounding: < 1e-5)
 // the grid search's shortcut (ocone_cell): entries of half-angle <= 2 degrees reaching <= 1 degree past the cone
 constexpr double OC_SIN_TAU = 0.034899496702500969, OC_COS_TAU2 = 0.99984769515639127, OC_SIN_TAU2 = 0.017452406437283512;
@@ -43,7 +48,7 @@ struct OConeView {
 };
 
 // True: the ray (o, d) may skip case (b) (no triangle of it can report a hit, see above).
-RT_HD bool ocone_skip(const OConeView& g, v3 o, v3 d)
+RT_HD bool ocone_skip(const OConeView& g, v3 o, v3 d, float QS)
 {
     if (!g.cells)
         return false;
@@ -52,7 +57,7 @@ RT_HD bool ocone_skip(const OConeView& g, v3 o, v3 d)
         return false;
     const int ix = (int)fx, iy = (int)fy, iz = (int)fz;
     const uint2 w = g.cells[((size_t)iz * (size_t)g.dim[1] + (size_t)iy) * (size_t)g.dim[0] + (size_t)ix];
-    const uint32_t code = w.y >> 16;
+    const uint32_t word = w.y >> 16, code = word & 0x7FFFu;
     if (code == OC_NOSKIP)
         return false;
     if (code == OC_EMPTY)
@@ -64,8 +69,9 @@ RT_HD bool ocone_skip(const OConeView& g, v3 o, v3 d)
     const float c = -(ax * d.x + ay * d.y + az * d.z) * inv;   // cos(angle(A, -d))
     const float cx = ay * d.z - az * d.y, cy = az * d.x - ax * d.z, cz = ax * d.y - ay * d.x;
     const float s = sqrtf(cx * cx + cy * cy + cz * cz) * inv;   // sin(angle(A, -d))
-    // cos(angle(A, -d) - beta) <= -EPS: every at-risk stored normal is past pi/2 + asin(EPS) from -d
-    return c * cb + s * sb <= -OC_EPS;
+    // cos(angle(A, -d) - beta) <= -EPS: every at-risk stored normal is past pi/2 + asin(EPS) from -d; or
+    // cos(angle(A, -d) + beta) >= QS + EPS: every at-risk exact normal within acos(QS + EPS) of -d
+    return c * cb + s * sb <= -OC_EPS || (!(word & OC_NOFRONT) && c * cb - s * sb >= QS + OC_EPS);
 }
 
 // One child entry (node v, slot j) of the wide BVH for the grid's search (ocone.cpp oc_entries): what
@@ -204,7 +210,7 @@ RT_HD uint2 ocone_cell(const OConeEnt* E, const GTri* tris, const double c[3], d
     for (int i = 0; i < 3; i++)
         Aq[i] /= ql;
     // 2. the half-angle: cb = cos of the largest angle found (any: a triangle at risk found)
-    bool any = false;
+    bool any = false, nofront = false;
     double cb = 2.0, sb = 0.0;
     // cos of the largest angle from Aq an entry's stored normals may make (-2: no bound)
     auto cub = [&](const OConeEnt& g) {
@@ -226,12 +232,15 @@ RT_HD uint2 ocone_cell(const OConeEnt* E, const GTri* tris, const double c[3], d
     while (sp > 0) {
         const OConeEnt& g = E[stk[--sp]];
         const double kg = cub(g);
-        if (any && kg >= fmin(cb, cabs))
-            continue;   // every stored normal below within the cone so far
+        if (any && kg >= fmin(cb, cabs)) {
+            nofront |= g.smin == 0;   // (a degenerate record below, at risk or not: the front route closes)
+            continue;                 // every normal below within the cone so far
+        }
         if (!oc_may_risk(g, c, r, slack, QS))
             continue;
         if (any && !(g.link & W_LEAF) && g.sc > 0 && g.ss <= OC_SIN_TAU && kg >= clim) {
             cabs = fmin(cabs, kg);
+            nofront |= g.smin == 0;
             continue;
         }
         if (g.link & W_LEAF) {
@@ -243,13 +252,32 @@ RT_HD uint2 ocone_cell(const OConeEnt* E, const GTri* tris, const double c[3], d
                     continue;   // Mdet = 0: never a hit
                 if (!(nn < INFINITY))
                     return pack(q, OC_NOSKIP);
-                const double u[3] = {t.n[0] / nn, t.n[1] / nn, t.n[2] / nn};
-                const double cu = Aq[0] * u[0] + Aq[1] * u[1] + Aq[2] * u[2];
-                if (any && !(cu < cb))
+                // the stored normal and (non-degenerate records) the exact one: the farther from the axis
+                double u[3] = {t.n[0] / nn, t.n[1] / nn, t.n[2] / nn};
+                double cu = Aq[0] * u[0] + Aq[1] * u[1] + Aq[2] * u[2];
+                bool degen = false;
+                {
+                    const double x0 = t.ab[0], x1 = t.ab[1], x2 = t.ab[2], y0 = t.ac[0], y1 = t.ac[1], y2 = t.ac[2];
+                    const double n0 = x1 * y2 - x2 * y1, n1 = x2 * y0 - x0 * y2, n2 = x0 * y1 - x1 * y0;
+                    const double la = sqrt(x0 * x0 + x1 * x1 + x2 * x2), lc = sqrt(y0 * y0 + y1 * y1 + y2 * y2);
+                    const double cl = sqrt(n0 * n0 + n1 * n1 + n2 * n2);
+                    degen = !(la * lc > 0x1p-100) || !(cl > 0x1p-50 * la * lc) || !(cl < INFINITY);
+                    if (!degen) {
+                        const double cN = (Aq[0] * n0 + Aq[1] * n1 + Aq[2] * n2) / cl;
+                        if (cN < cu) {
+                            cu = cN;
+                            u[0] = n0 / cl;
+                            u[1] = n1 / cl;
+                            u[2] = n2 / cl;
+                        }
+                    }
+                }
+                if (any && !(cu < cb) && !degen)
                     continue;   // within the half-angle found: at risk or not, it changes nothing
                 if (!(wbvh_risk_key(t, c[0], c[1], c[2], r, r, slack, QS) < INFINITY))
                     continue;   // no origin of the cell lies near its plane
-                {
+                nofront |= degen;
+                if (!any || cu < cb) {
                     const double x = Aq[1] * u[2] - Aq[2] * u[1], y = Aq[2] * u[0] - Aq[0] * u[2], z = Aq[0] * u[1] - Aq[1] * u[0];
                     cb = cu;
                     sb = sqrt(x * x + y * y + z * z);
@@ -290,7 +318,7 @@ RT_HD uint2 ocone_cell(const OConeEnt* E, const GTri* tris, const double c[3], d
     const double code = ceil((beta * (1 + 1e-9) + 1e-9) / 1.5707963267948966 * OC_BMAX);
     if (!(code <= OC_BMAX))
         return pack(q, OC_NOSKIP);
-    return pack(q, (uint32_t)code);
+    return pack(q, (uint32_t)code | (nofront ? OC_NOFRONT : 0u));
 }
 
 struct OConeGrid {

@@ -58,7 +58,8 @@ MESHES = {
 
 def _rays(tri9, n, seed):
     """Reflection-like rays (hit point + 0.01 n, outgoing hemisphere), rays from points of a triangle's
-    plane grazing it or its neighbours, and random rays through the scene box."""
+    plane grazing it or its neighbours, random rays through the scene box, and rays from the reflection-like
+    origins back into the surface."""
     rng = np.random.default_rng(seed)
     T = tri9.reshape(-1, 3, 3).astype(np.float64)
     nrm = np.cross(T[:, 1] - T[:, 0], T[:, 2] - T[:, 0])
@@ -85,8 +86,10 @@ def _rays(tri9, n, seed):
     lo, hi = tri9.reshape(-1, 3).min(0), tri9.reshape(-1, 3).max(0)
     o3 = rng.uniform(lo - 0.05, hi + 0.05, (n, 3))
     d3 = rng.normal(size=(n, 3))
-    o = np.concatenate([o1, o2, o3]).astype(np.float32)
-    d = np.concatenate([d1, d2, d3]).astype(np.float32)
+    # 4. into the surface from above it (a rough sample turning back: the front route)
+    d4 = -d1 + nn * rng.uniform(-0.3, 0.3, (n, 1))
+    o = np.concatenate([o1, o2, o3, o1]).astype(np.float32)
+    d = np.concatenate([d1, d2, d3, d4]).astype(np.float32)
     keep = np.isfinite(o).all(1) & np.isfinite(d).all(1) & (np.abs(d).sum(1) > 0)
     return o[keep], d[keep]
 
