@@ -2293,13 +2293,30 @@ __global__ __launch_bounds__(BLOCK) void refl_keys_kernel(KParams P, const Frame
     idx[f] = f;
 }
 
+// The chunk's sample slots (ReflArgs::sample_major): slot = i * nfr + (p - c0), nfr = c1 - c0, the i-th
+// samples of consecutive frames side by side, so that the per-frame passes (pass1, resolve: one lane per
+// frame, its samples in order) read their records coalesced; 0: slot = (p - c0) * stride + i, a frame's
+// samples side by side
+__device__ __forceinline__ int slot_pos(const ReflArgs& A, int slot)
+{
+    return A.sample_major ? A.c0 + slot % (A.c1 - A.c0) : A.c0 + slot / A.stride;
+}
+__device__ __forceinline__ int slot_sample(const ReflArgs& A, int slot)
+{
+    return A.sample_major ? slot / (A.c1 - A.c0) : slot % A.stride;
+}
+__device__ __forceinline__ int slot_of(const ReflArgs& A, int p, int i)
+{
+    return A.sample_major ? i * (A.c1 - A.c0) + (p - A.c0) : (p - A.c0) * A.stride + i;
+}
+
 // gen: one thread per sample slot of the chunk
 // gen + trace: each sample slot's direction (path-keyed RNG: no draw depends on another
 // sample, renderer.cpp:296-315) written to its record, then the sample's closest-hit query.
 // One kernel, so that the record writes overlap the traversals.
 __device__ __forceinline__ bool refl_gen(const KParams& P, const ReflArgs& A, int slot, v3& dir, unsigned& count)
 {
-    int f = A.order[A.c0 + slot / A.stride], i = slot % A.stride;
+    int f = A.order[slot_pos(A, slot)], i = slot_sample(A, slot);
     const FrameRec& F = A.fr[f];
     SampleRec& S = A.sm[slot];
     // fused: a sample's direction and ray flag go to its 32-B RawHit (written by the trace
@@ -2487,7 +2504,7 @@ struct ReflFeed {
             }
             return false;
         }
-        const FrameRec& F = A->fr[A->order[A->c0 + slot / A->stride]];
+        const FrameRec& F = A->fr[A->order[slot_pos(*A, slot)]];
         o = ld3(F.ro);
         d = dir;
         if (ray_is_nan(o, d) || !(P->wnodes && P->nnodes > 0)) {   // (refl_trace_one's octree path)
@@ -2592,7 +2609,7 @@ template <int G>
 __device__ __forceinline__ void refl_trace_one(const KParams& P, const ReflArgs& A, int slot, v3 dir, uint2* lv,
                                                uint32_t max_steps)
 {
-    const FrameRec& F = A.fr[A.order[A.c0 + slot / A.stride]];
+    const FrameRec& F = A.fr[A.order[slot_pos(A, slot)]];
     const v3 ro = ld3(F.ro);
     THit h;
     bool r;
@@ -2656,7 +2673,7 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_pass1_kernel(KParams 
         v3 ro = ld3(F.ro);
         Rec rhi = rec_fresh();   // reflection_hit_info, renderer.cpp:286
         for (int i = 0; i < F.nsamp; i++) {
-            int slot = (p - A.c0) * A.stride + i;
+            int slot = slot_of(A, p, i);
             SampleRec& S = A.sm[slot];
             const RawHit H = A.hit[slot];
             if (A.fused ? !(H.r & 2) : !S.ray)
@@ -2889,7 +2906,7 @@ __device__ __forceinline__ int spawn_sample(const KParams& P, const ReflArgs& A,
     const float* m = mat_of(P, S.mat);
     if (!(m[12] > 0.0f))
         return -1;
-    int f = A.order[A.c0 + slot / A.stride], i = slot % A.stride;
+    int f = A.order[slot_pos(A, slot)], i = slot_sample(A, slot);
     const FrameRec& F = A.fr[f];
     unsigned idx = atomicAdd(A.child_count, 1u);
     c3 dfc = shade_shadow_emit(P, ldc(S.fc), m, sh);
@@ -2931,7 +2948,7 @@ __global__ __launch_bounds__(BLOCK) void refl_resolve_kernel(KParams P_arg, Refl
     const FrameRec& F = A.fr[f];
     c3 total = col(0.0f, 0.0f, 0.0f);
     for (int i = 0; i < F.nsamp; i++) {
-        const int slot = (p - A.c0) * A.stride + i;
+        const int slot = slot_of(A, p, i);
         c3 ret;
         if (A.fused) {   // 16 B per sample instead of its 72-B record
             const float4 r = A.res[slot];

@@ -80,6 +80,8 @@ struct Knobs {
     int refl_feed = 24;       // RT_REFL_FEED=k: the reflection queries by refl_trace_feed_kernel (lane refill at k
                               // waiting lanes of a wave; C5 16 / 24 / 32 / 48: 1,128 / 1,101 / 1,103 / 1,155 ms per
                               // frame, 1,195 without); 0: refl_trace_kernel with its deferral (RT_REFL_DEFER)
+    bool refl_sample_major = true;  // RT_REFL_SAMPLE_MAJOR=0: the engine's slots frame-major (a frame's samples
+                              // side by side) instead of sample-major (kernels.hip slot_of)
     bool risk_cap = true;     // RT_RISK_CAP=0: no risk caps (camera / shadow rays into a silhouette's interior skip
                               // case (b), wbvh.hpp risk_cap_skip)
     bool ocone = true;        // RT_OCONE=0: no origin cones (reflection queries always run case (b), ocone.hpp)
