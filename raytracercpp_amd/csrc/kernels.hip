@@ -2489,6 +2489,10 @@ struct ReflFeed {
         slot = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(wb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wb, 0u));
         if (slot >= nslot)
             return false;
+        // the tickets in frame order (a frame's samples on adjacent lanes: one origin, coherent first
+        // steps), whatever the slots' order
+        if (A->sample_major && A->feed_frame_order)
+            slot = slot_of(*A, A->c0 + slot / A->stride, slot % A->stride);
         v3 dir = mk(0, 0, 0);
         unsigned c = 0;   // (refl_gen sets it for a frame's first sample: the frame's reflection rays)
         const bool gen = refl_gen(*P, *A, slot, dir, c);

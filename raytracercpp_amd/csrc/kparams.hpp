@@ -235,6 +235,7 @@ struct ReflArgs {
     int32_t level;           // samples trace at depth = level
     int32_t stride;          // max(N, 1)
     int32_t sample_major;    // the slots' order (kernels.hip slot_of): 1 sample-major, 0 frame-major
+    int32_t feed_frame_order;   // (sample-major) the feed hands out a frame's samples together
     int32_t fused;           // 1: pass1 builds the shadow list and the shadow pass spawns (no list /
                              // spawn kernels), and every sample's result is in res; 0: the separate
                              // passes (RT_REFL_FUSE=0), resolve reads the records

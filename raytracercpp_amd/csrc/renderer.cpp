@@ -139,6 +139,8 @@ Knobs Knobs::from_env()
         k.refl_defer = std::max(0, atoi(v));
     if (const char* v = getenv("RT_REFL_FEED"))    // lane refill of the reflection queries at this many waiting lanes
         k.refl_feed = std::min(64, std::max(0, atoi(v)));
+    if (const char* v = getenv("RT_REFL_FEED_FRAME_ORDER"))
+        k.refl_feed_frame_order = atoi(v) != 0;
     if (const char* v = getenv("RT_REFL_SAMPLE_MAJOR"))
         k.refl_sample_major = atoi(v) != 0;
     if (const char* v = getenv("RT_RISK_CAP"))
@@ -1329,6 +1331,7 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
         A.level = level;
         A.stride = stride;
         A.sample_major = knobs_.refl_sample_major ? 1 : 0;
+        A.feed_frame_order = knobs_.refl_feed_frame_order ? 1 : 0;
         // long queries (more than max_steps loop iterations) leave the trace kernel's waves and are
         // traced again by stage 7 in waves of their own (the shadow list's buffer, free until pass1;
         // RT_REFL_DEFER=0: off)

@@ -82,6 +82,8 @@ struct Knobs {
                               // frame, 1,195 without); 0: refl_trace_kernel with its deferral (RT_REFL_DEFER)
     bool refl_sample_major = true;  // RT_REFL_SAMPLE_MAJOR=0: the engine's slots frame-major (a frame's samples
                               // side by side) instead of sample-major (kernels.hip slot_of)
+    bool refl_feed_frame_order = false; // RT_REFL_FEED_FRAME_ORDER=1: the feed hands out a frame's samples together
+                              // over the sample-major slots (C5 977 vs 965 ms per frame: not faster)
     bool risk_cap = true;     // RT_RISK_CAP=0: no risk caps (camera / shadow rays into a silhouette's interior skip
                               // case (b), wbvh.hpp risk_cap_skip)
     bool ocone = true;        // RT_OCONE=0: no origin cones (reflection queries always run case (b), ocone.hpp)
