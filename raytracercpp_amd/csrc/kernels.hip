@@ -2297,6 +2297,13 @@ __global__ __launch_bounds__(BLOCK) void refl_keys_kernel(KParams P, const Frame
 // samples of consecutive frames side by side, so that the per-frame passes (pass1, resolve: one lane per
 // frame, its samples in order) read their records coalesced; 0: slot = (p - c0) * stride + i, a frame's
 // samples side by side
+// the frame at sorted position p: the level's sorted copy (ReflArgs::frs, refl_sort_frames_kernel) when
+// there is one, else through the order
+__device__ __forceinline__ const FrameRec& refl_frame(const ReflArgs& A, int p)
+{
+    return A.frs ? A.frs[p] : A.fr[A.order[p]];
+}
+
 __device__ __forceinline__ int slot_pos(const ReflArgs& A, int slot)
 {
     return A.sample_major ? A.c0 + slot % (A.c1 - A.c0) : A.c0 + slot / A.stride;
@@ -2316,8 +2323,8 @@ __device__ __forceinline__ int slot_of(const ReflArgs& A, int p, int i)
 // One kernel, so that the record writes overlap the traversals.
 __device__ __forceinline__ bool refl_gen(const KParams& P, const ReflArgs& A, int slot, v3& dir, unsigned& count)
 {
-    int f = A.order[slot_pos(A, slot)], i = slot_sample(A, slot);
-    const FrameRec& F = A.fr[f];
+    const int i = slot_sample(A, slot);
+    const FrameRec& F = refl_frame(A, slot_pos(A, slot));
     SampleRec& S = A.sm[slot];
     // fused: a sample's direction and ray flag go to its 32-B RawHit (written by the trace
     // kernel, coalesced) and nothing to the 72-B record, which only shaded samples fill
@@ -2508,7 +2515,7 @@ struct ReflFeed {
             }
             return false;
         }
-        const FrameRec& F = A->fr[A->order[slot_pos(*A, slot)]];
+        const FrameRec& F = refl_frame(*A, slot_pos(*A, slot));
         o = ld3(F.ro);
         d = dir;
         if (ray_is_nan(o, d) || !(P->wnodes && P->nnodes > 0)) {   // (refl_trace_one's octree path)
@@ -2613,7 +2620,7 @@ template <int G>
 __device__ __forceinline__ void refl_trace_one(const KParams& P, const ReflArgs& A, int slot, v3 dir, uint2* lv,
                                                uint32_t max_steps)
 {
-    const FrameRec& F = A.fr[A.order[slot_pos(A, slot)]];
+    const FrameRec& F = refl_frame(A, slot_pos(A, slot));
     const v3 ro = ld3(F.ro);
     THit h;
     bool r;
@@ -2673,7 +2680,7 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_pass1_kernel(KParams 
     int p = A.c0 + blockIdx.x * BLOCK + threadIdx.x;
     unsigned nshadow = 0;
     if (p < A.c1) {
-        const FrameRec& F = A.fr[A.order[p]];
+        const FrameRec& F = refl_frame(A, p);
         v3 ro = ld3(F.ro);
         Rec rhi = rec_fresh();   // reflection_hit_info, renderer.cpp:286
         for (int i = 0; i < F.nsamp; i++) {
@@ -2910,8 +2917,8 @@ __device__ __forceinline__ int spawn_sample(const KParams& P, const ReflArgs& A,
     const float* m = mat_of(P, S.mat);
     if (!(m[12] > 0.0f))
         return -1;
-    int f = A.order[slot_pos(A, slot)], i = slot_sample(A, slot);
-    const FrameRec& F = A.fr[f];
+    const int i = slot_sample(A, slot);
+    const FrameRec& F = refl_frame(A, slot_pos(A, slot));
     unsigned idx = atomicAdd(A.child_count, 1u);
     c3 dfc = shade_shadow_emit(P, ldc(S.fc), m, sh);
     make_frame(P, A.child_fr[idx], ld3(S.ip), ld3(S.nrm), A.fused ? ld3(A.hit[slot].d) : ld3(S.d), dfc, S.crough, S.mat,
@@ -2949,7 +2956,7 @@ __global__ __launch_bounds__(BLOCK) void refl_resolve_kernel(KParams P_arg, Refl
     if (p >= A.c1)
         return;
     const int f = A.order[p];
-    const FrameRec& F = A.fr[f];
+    const FrameRec& F = refl_frame(A, p);
     c3 total = col(0.0f, 0.0f, 0.0f);
     for (int i = 0; i < F.nsamp; i++) {
         const int slot = slot_of(A, p, i);
@@ -4238,6 +4245,26 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_stage
     case 6: hipLaunchKernelGGL(rt::refl_list_kernel, gs, dim3(rt::BLOCK), 0, stream, *P, *A); break;
     default: hipLaunchKernelGGL(rt::refl_resolve_kernel, gf, dim3(rt::BLOCK), 0, stream, *P, *A); break;
     }
+    return hipGetLastError();
+}
+
+namespace rt {
+// the level's frames copied in their sorted order (ReflArgs::frs): the passes that walk the sorted
+// positions read adjacent records
+__global__ __launch_bounds__(256) void refl_sort_frames_kernel(const FrameRec* __restrict__ fr, const int32_t* __restrict__ order,
+                                                               int n, FrameRec* __restrict__ frs)
+{
+    const int p = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (p < n)
+        frs[p] = fr[order[p]];
+}
+}  // namespace rt
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_sort_frames(const rt::FrameRec* fr, const int32_t* order,
+                                                                                int n, rt::FrameRec* frs, hipStream_t stream)
+{
+    if (n > 0)
+        hipLaunchKernelGGL(rt::refl_sort_frames_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, fr, order, n, frs);
     return hipGetLastError();
 }
 

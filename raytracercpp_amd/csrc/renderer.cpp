@@ -59,6 +59,8 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ocone(cons
                                                                      const int32_t dim[3], double h, double r, double slack,
                                                                      double QS, double cos_cap, uint2* cells,
                                                                      size_t ncells, hipStream_t stream);
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_sort_frames(const rt::FrameRec* fr, const int32_t* order,
+                                                                                int n, rt::FrameRec* frs, hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_wide_gather(
     const rt::GTri* tris, const int32_t* slot, const uint32_t* leaf_of_slot, const int32_t* tri_id,
     const int32_t* tri_mat, int n, rt::GTri* wtris, uint4* wmeta, hipStream_t stream);
@@ -143,6 +145,8 @@ Knobs Knobs::from_env()
         k.refl_feed_frame_order = atoi(v) != 0;
     if (const char* v = getenv("RT_REFL_SAMPLE_MAJOR"))
         k.refl_sample_major = atoi(v) != 0;
+    if (const char* v = getenv("RT_REFL_SORTED_FRAMES"))
+        k.refl_sorted_frames = atoi(v) != 0;
     if (const char* v = getenv("RT_RISK_CAP"))
         k.risk_cap = atoi(v) != 0;
     if (const char* v = getenv("RT_OCONE"))
@@ -1233,7 +1237,7 @@ int Renderer::launch_trace(const KParams& P, hipStream_t stream)
     }
     for (auto& L : refl_)
         L.fr.device = L.ret.device = L.sm.device = L.hit.device = L.cnt.device = L.list.device = L.sort.device =
-            L.sort_tmp.device = L.res.device = L.sdefer.device = device_;
+            L.sort_tmp.device = L.res.device = L.sdefer.device = L.frs.device = device_;
     size_t npx = (size_t)P.rw * P.local_rows;
     ReflLevel& L1 = refl_[1];
     if ((e = L1.fr.reserve(npx * sizeof(FrameRec))) != hipSuccess || (e = L1.cnt.reserve(64)) != hipSuccess)
@@ -1273,7 +1277,7 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
         size_t freeb = 0, totalb = 0;
         if (hipMemGetInfo(&freeb, &totalb) == hipSuccess) {
             const size_t held =
-                L.sm.bytes + L.hit.bytes + L.list.bytes + L.sdefer.bytes + L.res.bytes + C.fr.bytes + C.ret.bytes;
+                L.sm.bytes + L.hit.bytes + L.list.bytes + L.sdefer.bytes + L.res.bytes + L.frs.bytes + C.fr.bytes + C.ret.bytes;
             const size_t cap = (freeb + held) / 4 / (SLOT_BYTES * (size_t)stride);
             chunk = std::max<size_t>(1024, std::min(chunk, cap));
         }
@@ -1313,9 +1317,18 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
             return hip_fail(e, "frame sort");
         order = idx_out;
     }
+    // the frames in sorted order, copied once per level (the passes below walk the sorted positions)
+    const FrameRec* frs = nullptr;
+    if (knobs_.refl_sorted_frames) {
+        if ((e = L.frs.reserve((size_t)nframes * sizeof(FrameRec))) != hipSuccess ||
+            (e = rt_launch_refl_sort_frames(L.fr.as<FrameRec>(), order, nframes, L.frs.as<FrameRec>(), stream)) != hipSuccess)
+            return hip_fail(e, "refl_sort_frames_kernel");
+        frs = L.frs.as<FrameRec>();
+    }
     for (int c0 = 0; c0 < nframes; c0 += (int)chunk) {
         ReflArgs A;
         A.order = order;
+        A.frs = frs;
         A.fr = L.fr.as<FrameRec>();
         A.sm = L.sm.as<SampleRec>();
         A.hit = L.hit.as<RawHit>();
@@ -1435,7 +1448,7 @@ int Renderer::launch_raster(const KParams& P, hipStream_t stream)
     PS.tri_uv = A.piece_uv;
     for (auto& L : refl_)
         L.fr.device = L.ret.device = L.sm.device = L.hit.device = L.cnt.device = L.list.device = L.sort.device =
-            L.sort_tmp.device = L.res.device = L.sdefer.device = device_;
+            L.sort_tmp.device = L.res.device = L.sdefer.device = L.frs.device = device_;
     ReflLevel& L1 = refl_[1];
     const bool frames = P.has_reflection;
     if (frames) {

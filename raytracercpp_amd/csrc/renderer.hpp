@@ -84,6 +84,8 @@ struct Knobs {
                               // side by side) instead of sample-major (kernels.hip slot_of)
     bool refl_feed_frame_order = false; // RT_REFL_FEED_FRAME_ORDER=1: the feed hands out a frame's samples together
                               // over the sample-major slots (C5 977 vs 965 ms per frame: not faster)
+    bool refl_sorted_frames = true;  // RT_REFL_SORTED_FRAMES=0: the engine reads frames through the sort order
+                              // instead of a sorted copy (kernels.hip refl_sort_frames_kernel)
     bool risk_cap = true;     // RT_RISK_CAP=0: no risk caps (camera / shadow rays into a silhouette's interior skip
                               // case (b), wbvh.hpp risk_cap_skip)
     bool ocone = true;        // RT_OCONE=0: no origin cones (reflection queries always run case (b), ocone.hpp)
@@ -358,7 +360,7 @@ private:
 
     // reflection engine buffers, per level (frames, results, chunk samples / hits, child counter)
     struct ReflLevel {
-        DevBuf fr, ret, sm, hit, cnt, list, sort, sort_tmp, res, sdefer;
+        DevBuf fr, ret, sm, hit, cnt, list, sort, sort_tmp, res, sdefer, frs;
     };
     static constexpr int REFL_LEVELS = 18;   // max_recursion_depth <= 15: frames at levels 1..16, +1 child slot
     ReflLevel refl_[REFL_LEVELS];
