@@ -226,6 +226,32 @@ def test_reflection_deferral_matches_oracle(make_renderer, defer, feed, sfeed):
         R.finish_accel()
 
 
+@pytest.mark.parametrize("major,sorted_frames,frame_order", [("1", "1", "0"), ("1", "0", "0"), ("0", "1", "0"),
+                                                              ("0", "0", "0"), ("1", "1", "1")])
+def test_reflection_engine_layouts_match_oracle(make_renderer, major, sorted_frames, frame_order):
+    """The reflection engine's storage layouts change only where its records live: sample-major or
+    frame-major slots (RT_REFL_SAMPLE_MAJOR, kernels.hip slot_of), the frames read from their sorted
+    copy or through the sort order (RT_REFL_SORTED_FRAMES, refl_sort_frames_kernel), the feed's tickets
+    in slot or frame order (RT_REFL_FEED_FRAME_ORDER).  C5's features at a reduced size, on the quick
+    tree and then the SAH tree, equal the oracle bit for bit in every combination."""
+    from raytracercpp_amd import scenes
+    sc, st = scenes.sphere1m_refl(width=64, height=36, samples=4)
+    st = st.copy(max_recursion_depth=3)
+    o = Oracle(sc, st).render_rows()
+    R = make_renderer(RT_REFL_SAMPLE_MAJOR=major, RT_REFL_SORTED_FRAMES=sorted_frames,
+                      RT_REFL_FEED_FRAME_ORDER=frame_order)
+    R.load_scene(sc, st)
+    R.request_aux(hit=True, shadow=True)
+    for frame in ("quick tree", "SAH tree"):
+        R.ray_trace()
+        g = R.get_internal(argb=True, hit=True, shadow=True)
+        assert np.array_equal(g["hit_id"], o.hit_id), frame
+        assert np.array_equal(g["shadow"], o.shadow), frame
+        assert np.array_equal(g["argb"], o.argb), f"{frame}: {int((g['argb'] != o.argb).sum())} ARGB mismatches"
+        assert R.stats()["reflection_rays"] == o.counters["reflection_rays"], frame
+        R.finish_accel()
+
+
 def test_camera_and_light_moves_after_finish_accel(make_renderer):
     """After the SAH tree is resident (rt_finish_accel), the camera and the light move between frames
     (new camera / light risk words each time, Renderer::prepare_risk): every frame equals the oracle's
