@@ -2293,6 +2293,26 @@ __global__ __launch_bounds__(BLOCK) void refl_keys_kernel(KParams P, const Frame
     idx[f] = f;
 }
 
+// keys of the shadow list (ReflArgs::list, RT_REFL_SHADOW_SORT): the 30-bit Morton code of each entry's hit
+// point in the scene box, so that the shadow pass takes its segments in spatial order (adjacent lanes
+// start from nearby points toward the one light)
+__global__ __launch_bounds__(BLOCK) void refl_shadow_keys_kernel(KParams P, const SampleRec* sm, const int32_t* list, int n,
+                                                                 uint32_t* keys)
+{
+    int t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= n)
+        return;
+    const SampleRec& S = sm[list[t]];
+    uint32_t q[3];
+    for (int a = 0; a < 3; a++) {
+        float lo = P.nodes[0].dn[a], hi = P.nodes[0].df[a];
+        float u = (S.ip[a] - lo) / (hi - lo);
+        u = u == u ? fminf(fmaxf(u, 0.0f), 1.0f) : 0.0f;
+        q[a] = (uint32_t)(u * 1023.0f);
+    }
+    keys[t] = spread10(q[0]) | (spread10(q[1]) << 1) | (spread10(q[2]) << 2);
+}
+
 // The chunk's sample slots (ReflArgs::sample_major): slot = i * nfr + (p - c0), nfr = c1 - c0, the i-th
 // samples of consecutive frames side by side, so that the per-frame passes (pass1, resolve: one lane per
 // frame, its samples in order) read their records coalesced; 0: slot = (p - c0) * stride + i, a frame's
@@ -4265,6 +4285,16 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_sort_
 {
     if (n > 0)
         hipLaunchKernelGGL(rt::refl_sort_frames_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, fr, order, n, frs);
+    return hipGetLastError();
+}
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_shadow_keys(const rt::KParams* P, const rt::SampleRec* sm,
+                                                                                 const int32_t* list, int n, uint32_t* keys,
+                                                                                 hipStream_t stream)
+{
+    if (n > 0)
+        hipLaunchKernelGGL(rt::refl_shadow_keys_kernel, dim3((n + rt::BLOCK - 1) / rt::BLOCK), dim3(rt::BLOCK), 0, stream, *P,
+                           sm, list, n, keys);
     return hipGetLastError();
 }
 

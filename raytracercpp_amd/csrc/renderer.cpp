@@ -59,6 +59,9 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ocone(cons
                                                                      const int32_t dim[3], double h, double r, double slack,
                                                                      double QS, double cos_cap, uint2* cells,
                                                                      size_t ncells, hipStream_t stream);
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_shadow_keys(const rt::KParams* P, const rt::SampleRec* sm,
+                                                                                 const int32_t* list, int n, uint32_t* keys,
+                                                                                 hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_sort_frames(const rt::FrameRec* fr, const int32_t* order,
                                                                                 int n, rt::FrameRec* frs, hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_wide_gather(
@@ -145,6 +148,8 @@ Knobs Knobs::from_env()
         k.refl_feed_frame_order = atoi(v) != 0;
     if (const char* v = getenv("RT_REFL_SAMPLE_MAJOR"))
         k.refl_sample_major = atoi(v) != 0;
+    if (const char* v = getenv("RT_REFL_SHADOW_SORT"))
+        k.refl_shadow_sort = atoi(v) != 0;
     if (const char* v = getenv("RT_REFL_SORTED_FRAMES"))
         k.refl_sorted_frames = atoi(v) != 0;
     if (const char* v = getenv("RT_RISK_CAP"))
@@ -1237,7 +1242,7 @@ int Renderer::launch_trace(const KParams& P, hipStream_t stream)
     }
     for (auto& L : refl_)
         L.fr.device = L.ret.device = L.sm.device = L.hit.device = L.cnt.device = L.list.device = L.sort.device =
-            L.sort_tmp.device = L.res.device = L.sdefer.device = L.frs.device = device_;
+            L.sort_tmp.device = L.res.device = L.sdefer.device = L.frs.device = L.slist.device = device_;
     size_t npx = (size_t)P.rw * P.local_rows;
     ReflLevel& L1 = refl_[1];
     if ((e = L1.fr.reserve(npx * sizeof(FrameRec))) != hipSuccess || (e = L1.cnt.reserve(64)) != hipSuccess)
@@ -1271,13 +1276,14 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
     // A level may take at most a quarter of the memory still free (what it already holds
     // counts as free), so that the deeper levels, each bounded the same way, fit behind it;
     // an allocation that fails anyway halves the chunk and retries.
-    constexpr size_t SLOT_BYTES = sizeof(SampleRec) + sizeof(RawHit) + 4 + 4 + 16 + sizeof(FrameRec) + 12;
+    constexpr size_t SLOT_BYTES = sizeof(SampleRec) + sizeof(RawHit) + 4 + 4 + 16 + sizeof(FrameRec) + 12 + 12;
     size_t chunk = (size_t)std::max(1024, (1 << knobs_.refl_chunk_log2) / stride);
     {
         size_t freeb = 0, totalb = 0;
         if (hipMemGetInfo(&freeb, &totalb) == hipSuccess) {
             const size_t held =
-                L.sm.bytes + L.hit.bytes + L.list.bytes + L.sdefer.bytes + L.res.bytes + L.frs.bytes + C.fr.bytes + C.ret.bytes;
+                L.sm.bytes + L.hit.bytes + L.list.bytes + L.sdefer.bytes + L.res.bytes + L.frs.bytes + L.slist.bytes + C.fr.bytes +
+                C.ret.bytes;
             const size_t cap = (freeb + held) / 4 / (SLOT_BYTES * (size_t)stride);
             chunk = std::max<size_t>(1024, std::min(chunk, cap));
         }
@@ -1290,7 +1296,8 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
             (e = L.hit.reserve(slots * sizeof(RawHit))) == hipSuccess && (e = L.list.reserve(slots * 4)) == hipSuccess &&
             (e = L.sdefer.reserve(slots * 4)) == hipSuccess && (e = L.res.reserve(slots * 16)) == hipSuccess &&
             (e = C.fr.reserve(slots * sizeof(FrameRec))) == hipSuccess &&
-            (e = C.ret.reserve(slots * 12)) == hipSuccess)
+            (e = C.ret.reserve(slots * 12)) == hipSuccess &&
+            (!knobs_.refl_shadow_sort || (e = L.slist.reserve(slots * 12)) == hipSuccess))
             break;
         if (e != hipErrorOutOfMemory || chunk <= 1024)
             return hip_fail(e, "hipMalloc (reflection level)");
@@ -1367,9 +1374,32 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
         static const int fused_stages[] = {1, 7, 2, 3}, split_stages[] = {1, 7, 2, 6, 3, 4};
         const int* st = A.fused ? fused_stages : split_stages;
         const int nst = A.fused ? 4 : 6;
-        for (int k = 0; k < nst; k++)
+        for (int k = 0; k < nst; k++) {
+            if (st[k] == 3 && A.fused && knobs_.refl_shadow_sort && P.compute_shadows) {
+                // the shadow list sorted by hit point (Morton order): the shadow pass's adjacent lanes start
+                // from nearby points (its entries' results do not depend on their order)
+                unsigned n = 0;
+                if ((e = hipMemcpyAsync(&n, A.list_count, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+                    (e = hipStreamSynchronize(stream)) != hipSuccess)
+                    return hip_fail(e, "shadow list count");
+                if (n > 1) {
+                    uint32_t* kin = L.slist.as<uint32_t>();
+                    uint32_t* kout = kin + n;
+                    int32_t* vout = reinterpret_cast<int32_t*>(kout + n);
+                    size_t tb = 0;
+                    if ((e = rt_launch_refl_shadow_keys(&P, A.sm, A.list, (int)n, kin, stream)) != hipSuccess ||
+                        (e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kin, kout, A.list, vout, (int)n, 0, 30,
+                                                                stream)) != hipSuccess ||
+                        (e = L.sort_tmp.reserve(tb)) != hipSuccess ||
+                        (e = hipcub::DeviceRadixSort::SortPairs(L.sort_tmp.p, tb, kin, kout, A.list, vout, (int)n, 0, 30,
+                                                                stream)) != hipSuccess)
+                        return hip_fail(e, "shadow list sort");
+                    A.list = vout;
+                }
+            }
             if ((e = rt_launch_refl_stage(st[k], &P, &A, stream)) != hipSuccess)
                 return hip_fail(e, "reflection stage launch");
+        }
         unsigned nchild = 0;
         if ((e = hipMemcpyAsync(&nchild, L.cnt.p, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
             (e = hipStreamSynchronize(stream)) != hipSuccess)
@@ -1448,7 +1478,7 @@ int Renderer::launch_raster(const KParams& P, hipStream_t stream)
     PS.tri_uv = A.piece_uv;
     for (auto& L : refl_)
         L.fr.device = L.ret.device = L.sm.device = L.hit.device = L.cnt.device = L.list.device = L.sort.device =
-            L.sort_tmp.device = L.res.device = L.sdefer.device = L.frs.device = device_;
+            L.sort_tmp.device = L.res.device = L.sdefer.device = L.frs.device = L.slist.device = device_;
     ReflLevel& L1 = refl_[1];
     const bool frames = P.has_reflection;
     if (frames) {

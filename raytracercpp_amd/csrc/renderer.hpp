@@ -84,6 +84,8 @@ struct Knobs {
                               // side by side) instead of sample-major (kernels.hip slot_of)
     bool refl_feed_frame_order = false; // RT_REFL_FEED_FRAME_ORDER=1: the feed hands out a frame's samples together
                               // over the sample-major slots (C5 977 vs 965 ms per frame: not faster)
+    bool refl_shadow_sort = true;  // RT_REFL_SHADOW_SORT=0: the engine's shadow pass takes its list in the order
+                              // pass1 appended it, not sorted by hit point (kernels.hip refl_shadow_keys_kernel)
     bool refl_sorted_frames = true;  // RT_REFL_SORTED_FRAMES=0: the engine reads frames through the sort order
                               // instead of a sorted copy (kernels.hip refl_sort_frames_kernel)
     bool risk_cap = true;     // RT_RISK_CAP=0: no risk caps (camera / shadow rays into a silhouette's interior skip
@@ -360,7 +362,7 @@ private:
 
     // reflection engine buffers, per level (frames, results, chunk samples / hits, child counter)
     struct ReflLevel {
-        DevBuf fr, ret, sm, hit, cnt, list, sort, sort_tmp, res, sdefer, frs;
+        DevBuf fr, ret, sm, hit, cnt, list, sort, sort_tmp, res, sdefer, frs, slist;
     };
     static constexpr int REFL_LEVELS = 18;   // max_recursion_depth <= 15: frames at levels 1..16, +1 child slot
     ReflLevel refl_[REFL_LEVELS];
