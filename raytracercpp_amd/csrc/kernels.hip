@@ -2337,6 +2337,58 @@ __device__ __forceinline__ int slot_of(const ReflArgs& A, int p, int i)
     return A.sample_major ? i * (A.c1 - A.c0) + (p - A.c0) : (p - A.c0) * A.stride + i;
 }
 
+// the i-th sample's direction of a frame (renderer.cpp:296-315: path-keyed RNG, no draw depends on another
+// sample)
+__device__ __forceinline__ v3 refl_dir(const FrameRec& F, int i)
+{
+    if (F.rough > 0) {
+        uint32_t rng = sample_state(F.key, (uint32_t)i);
+        float rx = rng_bilateral(rng);
+        float ry = rng_bilateral(rng);
+        float rz = rng_bilateral(rng);
+        v3 rdir = normalize(mk(rx, ry, rz));
+        if (dot(rdir, ld3(F.n)) < 0)
+            rdir = -rdir;
+        return F.rough * rdir + (1 - F.rough) * ld3(F.perfect);
+    }
+    return ld3(F.perfect);
+}
+
+// keys of the feed's tickets (ReflArgs::perm, RT_REFL_DIR_SORT): each slot's direction binned by its
+// cube-map face and a 2 x 2 cell of the face (the slots without a ray last); a stable sort by these keys
+// keeps the slots' order (the frames' Morton order) inside each bin, so that a wave's lanes take rays of
+// nearby origins and similar directions
+__global__ __launch_bounds__(BLOCK) void refl_dir_keys_kernel(KParams P, ReflArgs A, uint32_t* keys, int32_t* vals)
+{
+    const int slot = (int)(blockIdx.x * BLOCK + threadIdx.x);
+    const int nslot = (A.c1 - A.c0) * A.stride;
+    if (slot >= nslot)
+        return;
+    const int i = slot_sample(A, slot);
+    const FrameRec& F = refl_frame(A, slot_pos(A, slot));
+    uint32_t key = 127u;
+    if (i < F.nsamp && A.level <= P.max_recursion_depth) {
+        const v3 d = refl_dir(F, i);
+        const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+        int face;
+        float u, v, m;
+        if (ax >= ay && ax >= az) {
+            face = d.x < 0 ? 1 : 0;
+            u = d.y, v = d.z, m = ax;
+        } else if (ay >= az) {
+            face = d.y < 0 ? 3 : 2;
+            u = d.x, v = d.z, m = ay;
+        } else {
+            face = d.z < 0 ? 5 : 4;
+            u = d.x, v = d.y, m = az;
+        }
+        const uint32_t cu = m > 0 && u > 0 ? 1u : 0u, cv = m > 0 && v > 0 ? 1u : 0u;
+        key = d.x == d.x && d.y == d.y && d.z == d.z ? (uint32_t)face << 2 | cu << 1 | cv : 126u;
+    }
+    keys[slot] = key;
+    vals[slot] = slot;
+}
+
 // gen: one thread per sample slot of the chunk
 // gen + trace: each sample slot's direction (path-keyed RNG: no draw depends on another
 // sample, renderer.cpp:296-315) written to its record, then the sample's closest-hit query.
@@ -2357,17 +2409,7 @@ __device__ __forceinline__ bool refl_gen(const KParams& P, const ReflArgs& A, in
         }
         return false;
     }
-    if (F.rough > 0) {
-        uint32_t rng = sample_state(F.key, (uint32_t)i);
-        float rx = rng_bilateral(rng);
-        float ry = rng_bilateral(rng);
-        float rz = rng_bilateral(rng);
-        v3 rdir = normalize(mk(rx, ry, rz));
-        if (dot(rdir, ld3(F.n)) < 0)
-            rdir = -rdir;
-        dir = F.rough * rdir + (1 - F.rough) * ld3(F.perfect);
-    } else
-        dir = ld3(F.perfect);
+    dir = refl_dir(F, i);
     if (!A.fused)
         st3(S.d, dir);
     if (i == 0)
@@ -2518,7 +2560,9 @@ struct ReflFeed {
             return false;
         // the tickets in frame order (a frame's samples on adjacent lanes: one origin, coherent first
         // steps), whatever the slots' order
-        if (A->sample_major && A->feed_frame_order)
+        if (A->perm)
+            slot = A->perm[slot];
+        else if (A->sample_major && A->feed_frame_order)
             slot = slot_of(*A, A->c0 + slot / A->stride, slot % A->stride);
         v3 dir = mk(0, 0, 0);
         unsigned c = 0;   // (refl_gen sets it for a frame's first sample: the frame's reflection rays)
@@ -4295,6 +4339,16 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_shado
     if (n > 0)
         hipLaunchKernelGGL(rt::refl_shadow_keys_kernel, dim3((n + rt::BLOCK - 1) / rt::BLOCK), dim3(rt::BLOCK), 0, stream, *P,
                            sm, list, n, keys);
+    return hipGetLastError();
+}
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_dir_keys(const rt::KParams* P, const rt::ReflArgs* A,
+                                                                              uint32_t* keys, int32_t* vals, hipStream_t stream)
+{
+    const int n = (A->c1 - A->c0) * A->stride;
+    if (n > 0)
+        hipLaunchKernelGGL(rt::refl_dir_keys_kernel, dim3((n + rt::BLOCK - 1) / rt::BLOCK), dim3(rt::BLOCK), 0, stream, *P,
+                           *A, keys, vals);
     return hipGetLastError();
 }
 

@@ -230,6 +230,7 @@ struct ReflArgs {
     unsigned int* child_count;
     const int32_t* order;    // frame at sorted position p is order[p] (spatially sorted)
     const FrameRec* frs;     // (optional) the frames copied in sorted order: frs[p] = fr[order[p]]
+    const int32_t* perm;     // (optional) the feed's ticket t takes slot perm[t] (slots grouped by direction)
     int32_t* list;           // compacted sample slots with a shadow query
     unsigned int* list_count;
     int32_t c0, c1;          // sorted positions [c0, c1) of this level

@@ -59,6 +59,8 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ocone(cons
                                                                      const int32_t dim[3], double h, double r, double slack,
                                                                      double QS, double cos_cap, uint2* cells,
                                                                      size_t ncells, hipStream_t stream);
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_dir_keys(const rt::KParams* P, const rt::ReflArgs* A,
+                                                                              uint32_t* keys, int32_t* vals, hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_shadow_keys(const rt::KParams* P, const rt::SampleRec* sm,
                                                                                  const int32_t* list, int n, uint32_t* keys,
                                                                                  hipStream_t stream);
@@ -148,6 +150,8 @@ Knobs Knobs::from_env()
         k.refl_feed_frame_order = atoi(v) != 0;
     if (const char* v = getenv("RT_REFL_SAMPLE_MAJOR"))
         k.refl_sample_major = atoi(v) != 0;
+    if (const char* v = getenv("RT_REFL_DIR_SORT"))
+        k.refl_dir_sort = atoi(v) != 0;
     if (const char* v = getenv("RT_REFL_SHADOW_SORT"))
         k.refl_shadow_sort = atoi(v) != 0;
     if (const char* v = getenv("RT_REFL_SORTED_FRAMES"))
@@ -1276,7 +1280,7 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
     // A level may take at most a quarter of the memory still free (what it already holds
     // counts as free), so that the deeper levels, each bounded the same way, fit behind it;
     // an allocation that fails anyway halves the chunk and retries.
-    constexpr size_t SLOT_BYTES = sizeof(SampleRec) + sizeof(RawHit) + 4 + 4 + 16 + sizeof(FrameRec) + 12 + 12;
+    constexpr size_t SLOT_BYTES = sizeof(SampleRec) + sizeof(RawHit) + 4 + 4 + 16 + sizeof(FrameRec) + 12 + 16;
     size_t chunk = (size_t)std::max(1024, (1 << knobs_.refl_chunk_log2) / stride);
     {
         size_t freeb = 0, totalb = 0;
@@ -1297,7 +1301,7 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
             (e = L.sdefer.reserve(slots * 4)) == hipSuccess && (e = L.res.reserve(slots * 16)) == hipSuccess &&
             (e = C.fr.reserve(slots * sizeof(FrameRec))) == hipSuccess &&
             (e = C.ret.reserve(slots * 12)) == hipSuccess &&
-            (!knobs_.refl_shadow_sort || (e = L.slist.reserve(slots * 12)) == hipSuccess))
+            (!(knobs_.refl_shadow_sort || knobs_.refl_dir_sort) || (e = L.slist.reserve(slots * 16)) == hipSuccess))
             break;
         if (e != hipErrorOutOfMemory || chunk <= 1024)
             return hip_fail(e, "hipMalloc (reflection level)");
@@ -1336,6 +1340,7 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
         ReflArgs A;
         A.order = order;
         A.frs = frs;
+        A.perm = nullptr;
         A.fr = L.fr.as<FrameRec>();
         A.sm = L.sm.as<SampleRec>();
         A.hit = L.hit.as<RawHit>();
@@ -1374,6 +1379,23 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
         static const int fused_stages[] = {1, 7, 2, 3}, split_stages[] = {1, 7, 2, 6, 3, 4};
         const int* st = A.fused ? fused_stages : split_stages;
         const int nst = A.fused ? 4 : 6;
+        if (knobs_.refl_dir_sort && A.fused && A.feed > 0) {
+            // the feed's tickets over the slots grouped by direction bin (a stable sort: the frames' order
+            // inside each bin); the buffer is free again once the feed is done (the shadow sort reuses it)
+            const int n = (A.c1 - A.c0) * A.stride;
+            uint32_t* kin = L.slist.as<uint32_t>();
+            uint32_t* kout = kin + n;
+            int32_t* vin = reinterpret_cast<int32_t*>(kout + n);
+            int32_t* vout = vin + n;
+            size_t tb = 0;
+            if ((e = rt_launch_refl_dir_keys(&P, &A, kin, vin, stream)) != hipSuccess ||
+                (e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kin, kout, vin, vout, n, 0, 7, stream)) != hipSuccess ||
+                (e = L.sort_tmp.reserve(tb)) != hipSuccess ||
+                (e = hipcub::DeviceRadixSort::SortPairs(L.sort_tmp.p, tb, kin, kout, vin, vout, n, 0, 7, stream)) !=
+                    hipSuccess)
+                return hip_fail(e, "feed direction sort");
+            A.perm = vout;
+        }
         for (int k = 0; k < nst; k++) {
             if (st[k] == 3 && A.fused && knobs_.refl_shadow_sort && P.compute_shadows) {
                 // the shadow list sorted by hit point (Morton order): the shadow pass's adjacent lanes start
