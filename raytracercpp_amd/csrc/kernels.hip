@@ -2389,6 +2389,15 @@ __global__ __launch_bounds__(BLOCK) void refl_dir_keys_kernel(KParams P, ReflArg
     vals[slot] = slot;
 }
 
+// keys of the deferred queries (ReflArgs::defer, RT_REFL_DEFER_SORT): each slot's frame position, so that
+// refl_trace_long_kernel takes them in the frames' Morton order (nearby origins in a wave)
+__global__ __launch_bounds__(BLOCK) void refl_defer_keys_kernel(ReflArgs A, int n, uint32_t* keys)
+{
+    int t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t < n)
+        keys[t] = (uint32_t)(slot_pos(A, A.defer[t]) - A.c0);
+}
+
 // gen: one thread per sample slot of the chunk
 // gen + trace: each sample slot's direction (path-keyed RNG: no draw depends on another
 // sample, renderer.cpp:296-315) written to its record, then the sample's closest-hit query.
@@ -4349,6 +4358,15 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_dir_k
     if (n > 0)
         hipLaunchKernelGGL(rt::refl_dir_keys_kernel, dim3((n + rt::BLOCK - 1) / rt::BLOCK), dim3(rt::BLOCK), 0, stream, *P,
                            *A, keys, vals);
+    return hipGetLastError();
+}
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_defer_keys(const rt::ReflArgs* A, int n, uint32_t* keys,
+                                                                                hipStream_t stream)
+{
+    if (n > 0)
+        hipLaunchKernelGGL(rt::refl_defer_keys_kernel, dim3((n + rt::BLOCK - 1) / rt::BLOCK), dim3(rt::BLOCK), 0, stream, *A, n,
+                           keys);
     return hipGetLastError();
 }
 

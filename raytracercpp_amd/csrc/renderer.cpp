@@ -59,6 +59,8 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_ocone(cons
                                                                      const int32_t dim[3], double h, double r, double slack,
                                                                      double QS, double cos_cap, uint2* cells,
                                                                      size_t ncells, hipStream_t stream);
+extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_defer_keys(const rt::ReflArgs* A, int n, uint32_t* keys,
+                                                                                hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_dir_keys(const rt::KParams* P, const rt::ReflArgs* A,
                                                                               uint32_t* keys, int32_t* vals, hipStream_t stream);
 extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_shadow_keys(const rt::KParams* P, const rt::SampleRec* sm,
@@ -152,6 +154,8 @@ Knobs Knobs::from_env()
         k.refl_sample_major = atoi(v) != 0;
     if (const char* v = getenv("RT_REFL_DIR_SORT"))
         k.refl_dir_sort = atoi(v) != 0;
+    if (const char* v = getenv("RT_REFL_DEFER_SORT"))
+        k.refl_defer_sort = atoi(v) != 0;
     if (const char* v = getenv("RT_REFL_SHADOW_SORT"))
         k.refl_shadow_sort = atoi(v) != 0;
     if (const char* v = getenv("RT_REFL_SORTED_FRAMES"))
@@ -1301,7 +1305,7 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
             (e = L.sdefer.reserve(slots * 4)) == hipSuccess && (e = L.res.reserve(slots * 16)) == hipSuccess &&
             (e = C.fr.reserve(slots * sizeof(FrameRec))) == hipSuccess &&
             (e = C.ret.reserve(slots * 12)) == hipSuccess &&
-            (!(knobs_.refl_shadow_sort || knobs_.refl_dir_sort) || (e = L.slist.reserve(slots * 16)) == hipSuccess))
+            (!(knobs_.refl_shadow_sort || knobs_.refl_dir_sort || knobs_.refl_defer_sort) || (e = L.slist.reserve(slots * 16)) == hipSuccess))
             break;
         if (e != hipErrorOutOfMemory || chunk <= 1024)
             return hip_fail(e, "hipMalloc (reflection level)");
@@ -1397,6 +1401,31 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
             A.perm = vout;
         }
         for (int k = 0; k < nst; k++) {
+            if (st[k] == 7 && knobs_.refl_defer_sort) {
+                // the deferred queries in their frames' (Morton) order: a wave's lane groups start from nearby
+                // origins (each query's result does not depend on its place in the list)
+                unsigned n = 0;
+                if ((e = hipMemcpyAsync(&n, A.defer_count, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+                    (e = hipStreamSynchronize(stream)) != hipSuccess)
+                    return hip_fail(e, "deferred query count");
+                if (n > 1) {
+                    int bits = 1;
+                    while (bits < 31 && (1u << bits) < (unsigned)(A.c1 - A.c0))
+                        bits++;
+                    uint32_t* kin = L.slist.as<uint32_t>();
+                    uint32_t* kout = kin + n;
+                    int32_t* vout = reinterpret_cast<int32_t*>(kout + n);
+                    size_t tb = 0;
+                    if ((e = rt_launch_refl_defer_keys(&A, (int)n, kin, stream)) != hipSuccess ||
+                        (e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kin, kout, A.defer, vout, (int)n, 0, bits,
+                                                                stream)) != hipSuccess ||
+                        (e = L.sort_tmp.reserve(tb)) != hipSuccess ||
+                        (e = hipcub::DeviceRadixSort::SortPairs(L.sort_tmp.p, tb, kin, kout, A.defer, vout, (int)n, 0, bits,
+                                                                stream)) != hipSuccess)
+                        return hip_fail(e, "deferred query sort");
+                    A.defer = vout;
+                }
+            }
             if (st[k] == 3 && A.fused && knobs_.refl_shadow_sort && P.compute_shadows) {
                 // the shadow list sorted by hit point (Morton order): the shadow pass's adjacent lanes start
                 // from nearby points (its entries' results do not depend on their order)

@@ -86,6 +86,8 @@ struct Knobs {
                               // over the sample-major slots (C5 977 vs 965 ms per frame: not faster)
     bool refl_dir_sort = false;  // RT_REFL_DIR_SORT=1: the feed takes its slots grouped by direction bin
                               // (kernels.hip refl_dir_keys_kernel, ReflArgs::perm)
+    bool refl_defer_sort = false;  // RT_REFL_DEFER_SORT=1: the long kernel takes the deferred queries in their
+                              // frames' order (refl_defer_keys_kernel; measured slower)
     bool refl_shadow_sort = true;  // RT_REFL_SHADOW_SORT=0: the engine's shadow pass takes its list in the order
                               // pass1 appended it, not sorted by hit point (kernels.hip refl_shadow_keys_kernel)
     bool refl_sorted_frames = true;  // RT_REFL_SORTED_FRAMES=0: the engine reads frames through the sort order
