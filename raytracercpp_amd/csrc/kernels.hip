@@ -2493,7 +2493,16 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_kernel(KParams 
 // per query, the same steps) and the record the certificate's; the queries it cannot certify (a stack
 // overflow, a tie, a NaN ray) go to the defer list, which refl_trace_long_kernel runs as before (deep
 // retry, octree walk).  The result per slot is refl_trace_one's, bit for bit.
-constexpr int W_STACK_REFL_FEED = 20;   // (160 KB / 4 blocks / 256 lanes / 8 B)
+#ifndef RT_OCC_FEED
+#define RT_OCC_FEED 3   // waves per SIMD of refl_trace_feed_kernel (its persistent grid; r06, C5 ms per frame:
+                        // 3 waves with a 26-entry stack 903-904, 4 / 20 entries 913-915, 2 / 32 912, 3 / 20 921-923,
+                        // 5 / 16 1,077: the deeper stack defers fewer queries, more waves thrash the L1)
+#endif
+#ifndef RT_STACK_REFL_FEED
+#define RT_STACK_REFL_FEED 26   // (160 KB / 3 blocks / 256 lanes / 8 B)
+#endif
+static_assert(RT_OCC_FEED * RT_STACK_REFL_FEED * 256 * 8 <= 160 * 1024, "the feed's stacks fit the CU's LDS");
+constexpr int W_STACK_REFL_FEED = RT_STACK_REFL_FEED;
 static_assert(W_STACK_REFL_FEED >= W_STACK, "the feed's stack");
 
 struct ReflFeed {
@@ -2603,7 +2612,7 @@ struct ReflFeed {
     }
 };
 
-__global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_feed_kernel(KParams P_arg, ReflArgs A)
+__global__ __launch_bounds__(BLOCK, RT_OCC_FEED) void refl_trace_feed_kernel(KParams P_arg, ReflArgs A)
 {
     const KParams& P = kernel_params();
     (void)P_arg;
@@ -2614,7 +2623,7 @@ __global__ __launch_bounds__(BLOCK, RT_OCC_REFL) void refl_trace_feed_kernel(KPa
     feed.P = &P;
     feed.A = &A;
     feed.nslot = (A.c1 - A.c0) * A.stride;
-    // its one-lane queries take the reflection kernels' LDS budget (4 blocks per CU: 40 KB, 20 entries per
+    // its one-lane queries take the CU's LDS at RT_OCC_FEED blocks (3 blocks per CU: 52 KB, 26 entries per
     // lane): fewer overflow into the defer list
     WStackLdsN<W_STACK_REFL_FEED> stk{lv};
     WHit w;
@@ -4291,7 +4300,7 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t rt_launch_refl_stage
     case 1:
         if (A->feed > 0)   // persistent waves (lane refill): the reflection kernels' residency
             hipLaunchKernelGGL(rt::refl_trace_feed_kernel,
-                               dim3(std::max(1u, std::min<unsigned>(gs.x, (unsigned)(P->max_blocks / 8 * RT_OCC_REFL)))),
+                               dim3(std::max(1u, std::min<unsigned>(gs.x, (unsigned)(P->max_blocks / 8 * RT_OCC_FEED)))),
                                dim3(rt::BLOCK), (size_t)std::max(P->levels, rt::W_STACK_REFL_FEED) * rt::BLOCK * sizeof(uint2),
                                stream, *P, *A);
         else
