@@ -2511,6 +2511,7 @@ struct ReflFeed {
     bool drained = false;   // (wave-uniform) every slot has been handed out
     int threshold;
     int slot = -1;
+    int part = 0;        // (feed_parts, wave-uniform) eighths of the slots this wave has found exhausted
     unsigned count = 0;  // reflection rays of the lane's slots (refl_gen)
     const KParams* P;
     const ReflArgs* A;
@@ -2566,16 +2567,49 @@ struct ReflFeed {
         if (!wb)
             return false;
         const int leader = __ffsll((unsigned long long)wb) - 1;
-        int base = 0;
-        if ((int)(threadIdx.x & 63) == leader)
-            base = (int)atomicAdd(A->feed_ticket, (unsigned)__popcll(wb));
-        base = __shfl(base, leader);
-        drained = base + __popcll(wb) >= nslot;
-        if (!want)
-            return false;
-        slot = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(wb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wb, 0u));
-        if (slot >= nslot)
-            return false;
+        const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(wb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wb, 0u));
+        if (A->feed_parts) {
+            // the slots in eighths, one ticket each: a wave starts on its XCD's eighth (workgroups go to the
+            // 8 XCDs round robin), so that each XCD's L2 holds the nodes of one part of the frames' Morton
+            // order, and moves on to the next eighths when its own is exhausted
+            const int xcd = (int)(blockIdx.x & 7);
+            int base = 0, lim = 0;
+            for (;;) {
+                if (part >= 8) {
+                    drained = true;
+                    return false;
+                }
+                const int x = (xcd + part) & 7;
+                const int lo = (int)((long long)nslot * x / 8), hi = (int)((long long)nslot * (x + 1) / 8);
+                int b = 0;
+                if ((int)(threadIdx.x & 63) == leader)
+                    b = (int)atomicAdd(A->feed_parts + x, (unsigned)__popcll(wb));
+                b = __shfl(b, leader);
+                if (lo + b < hi) {
+                    base = lo + b;
+                    lim = hi;
+                    break;
+                }
+                part++;
+            }
+            drained = false;
+            if (!want)
+                return false;
+            slot = base + rank;
+            if (slot >= lim)
+                return false;
+        } else {
+            int base = 0;
+            if ((int)(threadIdx.x & 63) == leader)
+                base = (int)atomicAdd(A->feed_ticket, (unsigned)__popcll(wb));
+            base = __shfl(base, leader);
+            drained = base + __popcll(wb) >= nslot;
+            if (!want)
+                return false;
+            slot = base + rank;
+            if (slot >= nslot)
+                return false;
+        }
         // the tickets in frame order (a frame's samples on adjacent lanes: one origin, coherent first
         // steps), whatever the slots' order
         if (A->perm)

@@ -231,6 +231,8 @@ struct ReflArgs {
     const int32_t* order;    // frame at sorted position p is order[p] (spatially sorted)
     const FrameRec* frs;     // (optional) the frames copied in sorted order: frs[p] = fr[order[p]]
     const int32_t* perm;     // (optional) the feed's ticket t takes slot perm[t] (slots grouped by direction)
+    unsigned int* feed_parts;   // (optional) 8 tickets, one per eighth of the slots: a wave takes its XCD's
+                                // eighth first, then the next ones (RT_REFL_FEED_XCD)
     int32_t* list;           // compacted sample slots with a shadow query
     unsigned int* list_count;
     int32_t c0, c1;          // sorted positions [c0, c1) of this level

@@ -154,6 +154,8 @@ Knobs Knobs::from_env()
         k.refl_sample_major = atoi(v) != 0;
     if (const char* v = getenv("RT_REFL_DIR_SORT"))
         k.refl_dir_sort = atoi(v) != 0;
+    if (const char* v = getenv("RT_REFL_FEED_XCD"))
+        k.refl_feed_xcd = atoi(v) != 0;
     if (const char* v = getenv("RT_REFL_DEFER_SORT"))
         k.refl_defer_sort = atoi(v) != 0;
     if (const char* v = getenv("RT_REFL_SHADOW_SORT"))
@@ -1345,6 +1347,7 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
         A.order = order;
         A.frs = frs;
         A.perm = nullptr;
+        A.feed_parts = knobs_.refl_feed_xcd ? L.cnt.as<unsigned int>() + 8 : nullptr;
         A.fr = L.fr.as<FrameRec>();
         A.sm = L.sm.as<SampleRec>();
         A.hit = L.hit.as<RawHit>();
@@ -1375,7 +1378,7 @@ int Renderer::refl_level(const KParams& P, int level, int nframes, hipStream_t s
         A.shadow_ticket = L.cnt.as<unsigned int>() + 5;
         A.sdefer = L.sdefer.as<int32_t>();
         A.sdefer_count = L.cnt.as<unsigned int>() + 6;
-        if ((e = hipMemsetAsync(L.cnt.p, 0, 32, stream)) != hipSuccess)   // (+ the long kernel's and the feeds' counters)
+        if ((e = hipMemsetAsync(L.cnt.p, 0, 64, stream)) != hipSuccess)   // (+ the long kernel's and the feeds' counters)
             return hip_fail(e, "hipMemsetAsync");
         // fused (default): trace, pass1 (+ shadow list), shadow (+ spawn); RT_REFL_FUSE=0: trace,
         // pass1, list, shadow, spawn

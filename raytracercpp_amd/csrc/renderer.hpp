@@ -86,6 +86,8 @@ struct Knobs {
                               // over the sample-major slots (C5 977 vs 965 ms per frame: not faster)
     bool refl_dir_sort = false;  // RT_REFL_DIR_SORT=1: the feed takes its slots grouped by direction bin
                               // (kernels.hip refl_dir_keys_kernel, ReflArgs::perm)
+    bool refl_feed_xcd = true;  // RT_REFL_FEED_XCD=0: one ticket over all the feed's slots instead of eighths, a wave
+                              // starting on its XCD's (kernels.hip ReflFeed::fetch, ReflArgs::feed_parts)
     bool refl_defer_sort = false;  // RT_REFL_DEFER_SORT=1: the long kernel takes the deferred queries in their
                               // frames' order (refl_defer_keys_kernel; measured slower)
     bool refl_shadow_sort = true;  // RT_REFL_SHADOW_SORT=0: the engine's shadow pass takes its list in the order

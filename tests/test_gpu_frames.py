@@ -228,7 +228,7 @@ def test_reflection_deferral_matches_oracle(make_renderer, defer, feed, sfeed):
 
 @pytest.mark.parametrize("major,sorted_frames,frame_order,shadow_sort", [
     ("1", "1", "0", "1"), ("1", "0", "0", "1"), ("0", "1", "0", "1"), ("0", "0", "0", "0"), ("1", "1", "1", "1"),
-    ("1", "1", "0", "0"), ("1", "1", "0", "1+dir"), ("0", "0", "0", "0+dir"), ("1", "1", "0", "1+defer")])
+    ("1", "1", "0", "0"), ("1", "1", "0", "1+dir"), ("0", "0", "0", "0+dir"), ("1", "1", "0", "1+defer"), ("1", "1", "0", "1-xcd"), ("0", "1", "1", "1-xcd")])
 def test_reflection_engine_layouts_match_oracle(make_renderer, major, sorted_frames, frame_order, shadow_sort):
     """The reflection engine's storage layouts change only where its records live: sample-major or
     frame-major slots (RT_REFL_SAMPLE_MAJOR, kernels.hip slot_of), the frames read from their sorted
@@ -236,7 +236,8 @@ def test_reflection_engine_layouts_match_oracle(make_renderer, major, sorted_fra
     in slot or frame order (RT_REFL_FEED_FRAME_ORDER), the shadow list sorted by hit point or in append
     order (RT_REFL_SHADOW_SORT, refl_shadow_keys_kernel), the feed's tickets over the slots grouped by
     direction bin (RT_REFL_DIR_SORT, refl_dir_keys_kernel; "+dir"), the deferred queries in their frames'
-    order or in the order deferred (RT_REFL_DEFER_SORT, refl_defer_keys_kernel; "+defer").  C5's features at a reduced size, on the quick
+    order or in the order deferred (RT_REFL_DEFER_SORT, refl_defer_keys_kernel; "+defer"), the feed's
+    tickets in eighths per XCD or one ticket (RT_REFL_FEED_XCD; "-xcd": one ticket).  C5's features at a reduced size, on the quick
     tree and then the SAH tree, equal the oracle bit for bit in every combination."""
     from raytracercpp_amd import scenes
     sc, st = scenes.sphere1m_refl(width=64, height=36, samples=4)
@@ -245,7 +246,8 @@ def test_reflection_engine_layouts_match_oracle(make_renderer, major, sorted_fra
     R = make_renderer(RT_REFL_SAMPLE_MAJOR=major, RT_REFL_SORTED_FRAMES=sorted_frames,
                       RT_REFL_FEED_FRAME_ORDER=frame_order, RT_REFL_SHADOW_SORT=shadow_sort[0],
                       RT_REFL_DIR_SORT=int(shadow_sort.endswith("+dir")),
-                      RT_REFL_DEFER_SORT=int(shadow_sort.endswith("+defer")))
+                      RT_REFL_DEFER_SORT=int(shadow_sort.endswith("+defer")),
+                      RT_REFL_FEED_XCD=int(not shadow_sort.endswith("-xcd")))
     R.load_scene(sc, st)
     R.request_aux(hit=True, shadow=True)
     for frame in ("quick tree", "SAH tree"):
